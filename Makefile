@@ -1,0 +1,58 @@
+# Build recipe for the MI355X `path` integrator (no cmake needed).
+#   make            -> host scene library, GPU library (gfx950), CLI, oracle
+#   make device     -> my-mitsuba_amd/libmtsg.so only (hipcc --offload-arch=gfx950)
+# Outputs are in-tree .so files (git-ignored, shipped to the GPU box by gpurun).
+
+HIPCC   ?= /opt/rocm/bin/hipcc
+CXX     ?= g++
+PKG     := my-mitsuba_amd
+ARCH    ?= gfx950
+JOBS    ?= 8
+
+HOST_SRC := $(wildcard $(PKG)/host/*.cpp)
+HOST_HDR := $(wildcard $(PKG)/host/*.h) $(PKG)/host/ior_table.inc include/mtsg.h include/mtsh.h
+DEV_SRC  := $(PKG)/csrc/mtsg.hip
+DEV_HDR  := $(wildcard $(PKG)/csrc/*.h) include/mtsg.h
+
+HOST_LIB := $(PKG)/libmtsg_host.so
+DEV_LIB  := $(PKG)/libmtsg.so
+PATH_LIB := $(PKG)/libmtsg_path.so
+CLI      := $(PKG)/mtsg-render
+
+ORACLE      := oracle/liboracle.so
+ORACLE_FAST := oracle/liboracle_fast.so
+
+.PHONY: all host device oracle clean
+all: host device oracle $(PATH_LIB) $(CLI)
+host: $(HOST_LIB)
+device: $(DEV_LIB)
+oracle: $(ORACLE) $(ORACLE_FAST)
+
+$(HOST_LIB): $(HOST_SRC) $(HOST_HDR)
+	$(CXX) -std=c++17 -O2 -g -fPIC -shared -Wall -o $@ $(HOST_SRC) -lpthread
+
+# gfx950 only: no dual CUDA/HIP paths, no hipify output.
+$(DEV_LIB): $(DEV_SRC) $(DEV_HDR)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall \
+	    -munsafe-fp-atomics -Wno-unused-value -Wno-unused-result -o $@ $(DEV_SRC)
+
+# Host-side `path` integrator plugin mirror: tiles the film over GPUs
+$(PATH_LIB): $(PKG)/host/path_integrator.cc $(HOST_LIB) $(DEV_LIB) include/mtsg.h include/mtsh.h
+	$(CXX) -std=c++17 -O2 -fPIC -shared -Wall -o $@ $(PKG)/host/path_integrator.cc \
+	    -L$(PKG) -lmtsg_host -lmtsg -Wl,-rpath,'$$ORIGIN' -lpthread
+
+$(CLI): $(PKG)/host/mtsg_render_main.cc $(PATH_LIB)
+	$(CXX) -std=c++17 -O2 -Wall -o $@ $(PKG)/host/mtsg_render_main.cc \
+	    -L$(PKG) -lmtsg_path -lmtsg_host -lmtsg -Wl,-rpath,'$$ORIGIN' -lpthread
+
+# Oracle (TEST INFRASTRUCTURE): precise build for parity ...
+$(ORACLE): oracle/oracle.cpp oracle/oracle.h include/mtsg.h
+	$(CXX) -std=c++17 -O2 -fPIC -shared -ffp-contract=off -o $@ oracle/oracle.cpp -lpthread
+# ... and the reference's own compiler flags (build/config-linux-gcc.py:7)
+# for the timed CPU baseline.
+$(ORACLE_FAST): oracle/oracle.cpp oracle/oracle.h include/mtsg.h
+	$(CXX) -std=c++17 -O3 -msse2 -march=nocona -funsafe-math-optimizations -fPIC -shared \
+	    -o $@ oracle/oracle.cpp -lpthread
+
+clean:
+	rm -f $(HOST_LIB) $(DEV_LIB) $(PATH_LIB) $(CLI) $(ORACLE) $(ORACLE_FAST)

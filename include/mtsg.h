@@ -1,0 +1,286 @@
+/*
+ * mtsg.h -- C-ABI of the MI355X (gfx950) wavefront `path` integrator.
+ *
+ * This is the drop-in boundary.  The reference exposes the
+ * `path` plugin as a C++ `SamplingIntegrator` created through
+ * `extern "C" CreateInstance` (reference: include/mitsuba/core/cobject.h:99-107,
+ * src/libcore/plugin.cpp:62-121); its work happens in
+ *   SamplingIntegrator::render      src/librender/integrator.cpp:99-133
+ *   SamplingIntegrator::renderBlock src/librender/integrator.cpp:144-197
+ *   MIPathTracer::Li                src/integrators/path/path.cpp:119-294
+ * A Mitsuba-side `path` plugin whose render() calls this library replaces all
+ * three.  Everything here is plain C: fixed-width scalars,
+ * plain pointers and sizes, integer error codes, no exceptions across the ABI.
+ *
+ * Ownership: the caller owns every host buffer.  mtsg_scene_create copies the
+ * scene description to device memory (HBM); the description may be freed
+ * after the call returns.
+ *
+ * Threading: one host thread per GPU.  A scene handle is bound to the device
+ * it was created on.  mtsg_cancel() may be called from any thread.
+ */
+#ifndef MTSG_H
+#define MTSG_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTSG_ABI_VERSION 1
+
+/* ---- error codes (mtsg_last_error() gives the message) ------------------ */
+enum {
+    MTSG_OK             = 0,
+    MTSG_ERR_INVALID    = -1,  /* malformed descriptor / parameters        */
+    MTSG_ERR_DEVICE     = -2,  /* HIP runtime error                        */
+    MTSG_ERR_OOM        = -3,  /* device allocation failed                 */
+    MTSG_ERR_CANCELLED  = -4,  /* mtsg_cancel() was called (render() == false) */
+    MTSG_ERR_NODEVICE   = -5   /* no gfx950 device / bad device index      */
+};
+
+/* ---- scene description: flat arrays, all world space -------------------- */
+
+/* 8-byte kd-tree node, bit-identical to Mitsuba's KDNode
+ * (include/mitsuba/render/gkdtree.h:452-600):
+ *   inner: combined = axis | (relOffsetToLeftChild << 2), data = float split bits
+ *   leaf : combined = 0x80000000 | primStart,              data = primEnd
+ * Children are adjacent (right = left + 1).  Indirection nodes are not used. */
+typedef struct mtsg_kdnode {
+    uint32_t combined;
+    uint32_t data;
+} mtsg_kdnode;
+
+/* 48-byte Wald projection triangle, field order of Mitsuba's TriAccel
+ * (include/mitsuba/render/triaccel.h:37-51).  k == 0xFFFFFFFF marks an
+ * analytic shape (rectangle) whose index is in prim_index; k == 3 marks a
+ * degenerate triangle that never intersects. */
+typedef struct mtsg_triaccel {
+    uint32_t k;
+    float n_u, n_v, n_d;
+    float a_u, a_v, b_nu, b_nv;
+    float c_nu, c_nv;
+    uint32_t shape_index;
+    uint32_t prim_index;   /* global triangle index, or rectangle index */
+} mtsg_triaccel;
+
+#define MTSG_TRIACCEL_SHAPE 0xFFFFFFFFu
+
+/* Analytic `rectangle` (src/shapes/rectangle.cpp:78-170). */
+typedef struct mtsg_rect {
+    float to_object[12];   /* world->object affine, row-major 3x4          */
+    float to_world[12];    /* object->world affine, row-major 3x4          */
+    float frame_s[3], frame_t[3], frame_n[3];  /* m_frame                  */
+    float dpdu[3], dpdv[3];
+    float inv_area;
+    uint32_t shape_index;
+} mtsg_rect;
+
+enum { MTSG_SHAPE_MESH = 0, MTSG_SHAPE_RECT = 1 };
+
+typedef struct mtsg_shape {
+    int32_t type;          /* MTSG_SHAPE_*                                 */
+    int32_t bsdf;          /* index into bsdfs                             */
+    int32_t emitter;       /* index into emitters, -1 if none              */
+    int32_t face_normals;  /* 1: no vertex normals (TriMesh faceNormals)   */
+    uint32_t tri_begin;    /* mesh: first global triangle                  */
+    uint32_t tri_count;
+    uint32_t rect;         /* rectangle index                              */
+    uint32_t pad;
+} mtsg_shape;
+
+enum {
+    MTSG_BSDF_DIFFUSE        = 1,   /* src/bsdfs/diffuse.cpp        */
+    MTSG_BSDF_ROUGHCONDUCTOR = 2,   /* src/bsdfs/roughconductor.cpp */
+    MTSG_BSDF_DIELECTRIC     = 3    /* src/bsdfs/dielectric.cpp     */
+};
+enum { MTSG_MF_BECKMANN = 0, MTSG_MF_GGX = 1 };
+
+typedef struct mtsg_bsdf {
+    int32_t type;
+    int32_t distribution;    /* MTSG_MF_*                                   */
+    int32_t sample_visible;
+    int32_t smooth;          /* BSDF::ESmooth set -> NEE (path.cpp:174)     */
+    int32_t ref_n_zero;      /* ETransmission|EBackSide -> refN = 0 (records.inl:160-164) */
+    int32_t pad[3];
+    float reflectance[3];    /* diffuse                                     */
+    float eta[3], k[3];      /* roughconductor, already divided by extEta   */
+    float spec_refl[3];      /* roughconductor / dielectric                 */
+    float spec_trans[3];     /* dielectric                                  */
+    float alpha_u, alpha_v;  /* already clamped to >= 1e-4                  */
+    float ior_eta, ior_inv_eta; /* dielectric intIOR/extIOR and inverse     */
+} mtsg_bsdf;
+
+enum { MTSG_EMITTER_AREA = 1 };
+
+typedef struct mtsg_emitter {
+    int32_t type;
+    int32_t shape;           /* emitting shape index                         */
+    uint32_t cdf_offset;     /* mesh: area CDF (tri_count+1 floats) in emitter_tri_cdf */
+    float pdf_discrete;      /* samplingWeight * normalization (scene.h:849-851) */
+    float radiance[3];
+    float inv_area;          /* m_invSurfaceArea of the shape                */
+} mtsg_emitter;
+
+enum { MTSG_FILTER_BOX = 0, MTSG_FILTER_GAUSSIAN = 1 };
+
+/* Perspective sensor + film, precomputed host side
+ * (src/sensors/perspective.cpp:126-176, src/librender/sensor.cpp:241-262). */
+typedef struct mtsg_camera {
+    float sample_to_camera[16];   /* row-major 4x4                          */
+    float camera_to_world[12];    /* row-major 3x4 affine                   */
+    float dx[3], dy[3];           /* near-plane differentials (m_dx, m_dy)  */
+    float near_clip, far_clip;
+    float inv_res_x, inv_res_y;   /* 1 / film size                          */
+    int32_t film_w, film_h;       /* full film size                         */
+    int32_t crop_x, crop_y, crop_w, crop_h;
+    /* reconstruction filter (src/libcore/rfilter.cpp:37-57)               */
+    int32_t filter_type;
+    float filter_radius;
+    float filter_scale;           /* MTS_FILTER_RESOLUTION / radius         */
+    int32_t border;               /* ceil(radius - 0.5)                     */
+    float filter_values[32];      /* MTS_FILTER_RESOLUTION + 1 entries      */
+    int32_t has_alpha;            /* film stores a real alpha channel       */
+    int32_t pad[3];
+} mtsg_camera;
+
+typedef struct mtsg_scene_desc {
+    uint32_t abi_version;         /* = MTSG_ABI_VERSION                     */
+    uint32_t n_vertices;
+    const float *vtx_pos;         /* 3 * n_vertices                         */
+    const float *vtx_nrm;         /* 3 * n_vertices                         */
+    uint32_t n_triangles;
+    const uint32_t *tri_idx;      /* 3 * n_triangles (into vtx_*)           */
+    const float *tri_dpdu;        /* 3 * n_triangles: UV tangent or p1-p0   */
+    uint32_t n_rects;
+    const mtsg_rect *rects;
+    uint32_t n_shapes;
+    const mtsg_shape *shapes;
+    uint32_t n_bsdfs;
+    const mtsg_bsdf *bsdfs;
+    uint32_t n_emitters;
+    const mtsg_emitter *emitters;
+    const float *emitter_cdf;     /* n_emitters + 1 (pmf.h DiscreteDistribution) */
+    uint32_t n_emitter_tri_cdf;
+    const float *emitter_tri_cdf; /* concatenated per-emitter triangle CDFs */
+    /* kd-tree */
+    uint32_t n_nodes;
+    const mtsg_kdnode *nodes;
+    uint32_t n_indices;
+    const uint32_t *indices;
+    uint32_t n_prims;             /* == n_triangles + n_rects              */
+    const mtsg_triaccel *triaccel;
+    float aabb_min[3], aabb_max[3];  /* enlarged tree AABB (gkdtree.h:1213-1220) */
+    uint32_t max_depth;           /* deepest leaf (traversal stack bound)  */
+    mtsg_camera camera;
+} mtsg_scene_desc;
+
+/* ---- render ------------------------------------------------------------- */
+
+/* MonteCarloIntegrator properties (src/librender/integrator.cpp:199-234),
+ * independent sampler count, and the film region this call renders.  The
+ * counter-based RNG draws dimension j of sample s of pixel (x, y) as
+ * u = hash(seed, (y * film_w + x) * spp + s, j); see DESIGN.md. */
+typedef struct mtsg_render_params {
+    int32_t max_depth;            /* -1 = infinite                          */
+    int32_t rr_depth;             /* default 5                              */
+    int32_t strict_normals;
+    int32_t hide_emitters;
+    uint32_t spp;
+    uint32_t seed;
+    /* pixel rectangle (film coordinates, inside the crop window) whose
+     * samples are generated by this call */
+    int32_t tile_x, tile_y, tile_w, tile_h;
+    /* multi-GPU film tiling: the rectangle is cut into 16x16 splat tiles in
+     * row-major order and this call renders tiles t with
+     * t % tile_stride == tile_offset (tile_stride 0 or 1 = all tiles).  The
+     * output block always covers the whole rectangle + border; blocks of
+     * different offsets are merged by addition (imageblock.h:103-107). */
+    int32_t tile_stride, tile_offset;
+} mtsg_render_params;
+
+/* Statistics of the last render call on a handle. */
+typedef struct mtsg_stats {
+    double ms_total;              /* wall time of the render call           */
+    double ms_trace_closest;      /* summed kernel time (HIP events)        */
+    double ms_trace_shadow;
+    double ms_shade;
+    double ms_camera;
+    double ms_splat;
+    uint64_t launches_trace_closest;
+    uint64_t rays_closest;        /* closest-hit rays traced                */
+    uint64_t rays_shadow;         /* shadow rays traced                     */
+    uint64_t samples;
+    /* algorithmic traversal work (only when MTSG_FLAG_COUNT is set):
+     * closest-hit rays, then shadow rays                                    */
+    uint64_t nodes_visited;
+    uint64_t leaf_refs;
+    uint64_t tri_tests;
+    uint64_t shadow_nodes_visited;
+    uint64_t shadow_leaf_refs;
+    uint64_t shadow_tri_tests;
+} mtsg_stats;
+
+enum {
+    MTSG_FLAG_TIMING = 1,         /* bracket every kernel with HIP events   */
+    MTSG_FLAG_COUNT  = 2          /* instrumented traversal (slower)        */
+};
+
+typedef struct mtsg_scene mtsg_scene;
+
+/* Number of visible gfx950 devices. */
+int  mtsg_device_count(void);
+
+/* Upload a scene to `device`; *out receives the handle. */
+int  mtsg_scene_create(const mtsg_scene_desc *desc, int device, mtsg_scene **out);
+
+/* Render the tile described by params.  `rgbaw_out` is a host buffer of
+ * (tile_w + 2*border) * (tile_h + 2*border) * 5 floats holding the
+ * ImageBlock (R, G, B, alpha, weight) of the tile including its filter
+ * border (src/librender/renderproc.cpp:41-50, imageblock.h:124-204).  The
+ * buffer is overwritten.  Blocking. */
+int  mtsg_render(mtsg_scene *scene, const mtsg_render_params *params,
+                 float *rgbaw_out);
+
+/* Same, but accumulates into a device-resident buffer of the same layout
+ * (must be zeroed by the caller before the first call) and does not copy
+ * to the host.  Used by the benchmark (inputs and outputs stay in HBM). */
+int  mtsg_render_device(mtsg_scene *scene, const mtsg_render_params *params,
+                        float *rgbaw_device);
+
+/* Device buffer helpers for mtsg_render_device (plain hipMalloc/hipMemcpy). */
+int  mtsg_device_alloc(mtsg_scene *scene, size_t bytes, void **out);
+int  mtsg_device_free(mtsg_scene *scene, void *ptr);
+int  mtsg_device_memset(mtsg_scene *scene, void *ptr, size_t bytes);
+int  mtsg_device_to_host(mtsg_scene *scene, void *dst, const void *src, size_t bytes);
+
+/* Cancel a running render on this handle (async-safe flag). */
+void mtsg_cancel(mtsg_scene *scene);
+
+int  mtsg_set_flags(mtsg_scene *scene, uint32_t flags);
+int  mtsg_get_stats(mtsg_scene *scene, mtsg_stats *out);
+
+/* Wavefront batch size in paths (default chosen from device memory). */
+int  mtsg_set_batch_paths(mtsg_scene *scene, uint32_t paths);
+
+/* Debug/parity entry points over SoA rays (host buffers).  Semantics of
+ * ShapeKDTree::rayIntersect (src/librender/skdtree.cpp:112-142) including
+ * the adaptive epsilon when mint == 1e-4 (Epsilon).  Misses give
+ * prim = 0xFFFFFFFF.  rays: 8 floats per ray {ox,oy,oz,dx,dy,dz,mint,maxt}. */
+int  mtsg_trace_closest(mtsg_scene *scene, uint32_t n, const float *rays,
+                        float *t, float *u, float *v, uint32_t *prim);
+/* Shadow variant (skdtree.cpp:207-226): occluded[i] = 1 if any hit. */
+int  mtsg_trace_shadow(mtsg_scene *scene, uint32_t n, const float *rays,
+                       uint8_t *occluded);
+
+void mtsg_scene_destroy(mtsg_scene *scene);
+
+/* Copies the last error message of the calling thread. */
+void mtsg_last_error(char *buf, size_t size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTSG_H */

@@ -1,0 +1,58 @@
+/*
+ * mtsh.h -- host-side (Mitsuba-mirror) C API: scene loading and film I/O.
+ *
+ * This library stands in for the CPU parts of Mitsuba that stay on the
+ * reference side of the boundary: the XML SceneHandler
+ * (src/librender/scenehandler.cpp), shape/BSDF/emitter plugin parameter
+ * parsing, Scene::initialize and the SAH kd-tree build
+ * (src/librender/scene.cpp:340-408, skdtree.cpp:68-110).  It produces the
+ * flat mtsg_scene_desc consumed by libmtsg (include/mtsg.h).  No GPU code.
+ */
+#ifndef MTSH_H
+#define MTSH_H
+
+#include "mtsg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mtsh_scene mtsh_scene;
+
+typedef struct mtsh_scene_info {
+    uint32_t n_triangles, n_rects, n_shapes, n_emitters, n_bsdfs;
+    uint32_t kd_nodes, kd_indices, kd_max_depth, kd_leaves, kd_nonempty_leaves;
+    double kd_build_seconds;
+    int32_t film_w, film_h, spp;
+    int32_t border;           /* reconstruction filter border (rfilter.cpp:50) */
+    int32_t max_depth;        /* integrator maxDepth                           */
+} mtsh_scene_info;
+
+/* Load a Mitsuba XML scene; defines are "name=value" strings (-D).
+ * Returns NULL on error (see mtsh_last_error). */
+mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_defines);
+
+/* Override kd-tree build parameters before loading (0 = default). */
+void mtsh_set_kd_threads(int threads);
+
+const mtsg_scene_desc *mtsh_scene_desc(const mtsh_scene *scene);
+
+/* Integrator properties + sampleCount of the scene; tile = full film. */
+void mtsh_scene_render_params(const mtsh_scene *scene, mtsg_render_params *out);
+
+void mtsh_scene_get_info(const mtsh_scene *scene, mtsh_scene_info *out);
+
+void mtsh_scene_free(mtsh_scene *scene);
+
+/* hdrfilm develop (fmtconv.cpp:962-974): rgb = (sum w*L) / (sum w). */
+void mtsh_develop(const float *rgbaw, int w, int h, float *rgb_out);
+
+/* Write an RGB float image as PFM (bitmap.cpp:347-398). Returns 0 on success. */
+int mtsh_write_pfm(const char *path, int w, int h, const float *rgb);
+
+void mtsh_last_error(char *buf, size_t size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTSH_H */

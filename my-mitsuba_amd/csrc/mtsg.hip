@@ -1,0 +1,1521 @@
+// mtsg.hip -- MI355X (gfx950, CDNA4) wavefront unidirectional path tracer
+// behind the C-ABI in include/mtsg.h.
+//
+// Replaces, for the `path` plugin, the reference's per-sample CPU loop
+//   SamplingIntegrator::renderBlock   src/librender/integrator.cpp:144-197
+//   MIPathTracer::Li                  src/integrators/path/path.cpp:119-294
+//   ShapeKDTree::rayIntersect         src/librender/skdtree.cpp:112-226
+//   SAHKDTree3D::rayIntersectHavran   include/mitsuba/render/sahkdtree3.h:178-308
+//   TriAccel::rayIntersect            include/mitsuba/render/triaccel.h:96-158
+//   diffuse / roughconductor / dielectric sample, eval, pdf
+//   AreaLight + Scene::sampleEmitterDirect / pdfEmitterDirect
+//   ImageBlock::put                   include/mitsuba/render/imageblock.h:124-204
+// with a wavefront of SoA path states in HBM:
+//   k_camera -> [ k_trace_closest -> k_shade -> k_trace_shadow ] x bounces -> k_splat
+// Active paths are compacted into queues with wave-aggregated atomics
+// (__ballot / __popcll / mbcnt on 64-lane waves); the kd-tree traversal
+// keeps a short stack in LDS (kd-restart on overflow); the film is splatted
+// per 16x16 tile into LDS and flushed with one float atomic per texel.
+// No MFMA: the path has no dense contraction.  See DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+#include <chrono>
+
+#include "../../include/mtsg.h"
+#include "device_math.h"
+
+using namespace mtsg;
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// device-side scene and path state
+// ---------------------------------------------------------------------------
+struct DevScene {
+    const uint2 *__restrict__ nodes;
+    const uint32_t *__restrict__ indices;
+    const float4 *__restrict__ tri;        // 3 float4 per prim (TriAccel)
+    const float4 *__restrict__ vpos;       // xyz
+    const float4 *__restrict__ vnrm;       // xyz
+    const uint4 *__restrict__ tidx;        // i0, i1, i2, shape
+    const float4 *__restrict__ tdpdu;      // dpdu xyz
+    const mtsg_rect *__restrict__ rects;
+    const mtsg_shape *__restrict__ shapes;
+    const mtsg_bsdf *__restrict__ bsdfs;
+    const mtsg_emitter *__restrict__ emitters;
+    const float *__restrict__ emitter_cdf;
+    const float *__restrict__ emitter_tri_cdf;
+    uint32_t n_emitters, n_tri;
+    float bmin[3], bmax[3];
+};
+
+struct DevCamera {
+    float s2c[16];
+    float c2w[12];
+    float near_clip, far_clip, inv_res_x, inv_res_y;
+    int film_w, film_h;
+    float filter_radius, filter_scale;
+    int border, has_alpha;
+    float filter_values[32];
+};
+
+struct DevIntegrator {
+    int max_depth, rr_depth, strict_normals, hide_emitters;
+    uint32_t spp, seed;
+};
+
+// wavefront batch: tiles [tile0, tile0 + ntiles) x samples [s0, s0 + ns)
+struct DevBatch {
+    int rect_x, rect_y, rect_w, rect_h;   // render rectangle (film coords)
+    int tiles_x;                          // tiles per row of the rectangle
+    int tile0, ntiles;                    // virtual tile range of this batch
+    int tstride, toffset;                 // global tile = toffset + virtual * tstride
+    uint32_t s0, ns;
+    uint32_t nslots;
+};
+
+enum : uint32_t { F_SCATTERED = 1u << 16, F_DELTA = 1u << 17 };
+
+struct DevPaths {
+    float4 *ray_o;    // o.xyz, mint
+    float4 *ray_d;    // d.xyz, maxt
+    float4 *hit;      // t, u, v, prim (bits)
+    float4 *L;        // rgb, alpha
+    float4 *T;        // rgb, eta
+    float4 *aux;      // refN.xyz of the previous vertex, bsdf pdf
+    uint2 *key;       // counter-RNG key
+    uint2 *st;        // x: depth | flags, y: next RNG dimension
+    float4 *sh_o;     // shadow ray origin, maxt
+    float4 *sh_d;     // shadow ray direction
+    float4 *sh_c;     // NEE contribution
+    uint32_t *q[2];   // path queues (ping-pong)
+    uint32_t *qs;     // shadow queue
+    uint32_t *cnt;    // [0..1] queue sizes, [2] shadow size, [3] trace fetch, [4] shadow fetch
+    unsigned long long *ctr;  // traversal counters (nodes, refs, tests)
+};
+
+constexpr int TILE = 16;                    // splat tile edge (256 pixels)
+constexpr int BLOCK = 256;
+constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traversal
+constexpr int SHORT_STACK = 8;              // LDS short stack entries per lane
+
+// ---------------------------------------------------------------------------
+// wave helpers (64 lanes)
+// ---------------------------------------------------------------------------
+DEV uint32_t lane_id() { return __lane_id(); }
+
+// Wave-aggregated queue append: one atomic per wave, lanes get consecutive slots.
+DEV uint32_t wave_append(uint32_t *counter, bool pred) {
+    unsigned long long m = __ballot(pred);
+    uint32_t n = (uint32_t)__popcll(m);
+    uint32_t base = 0;
+    uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
+    if (n) {
+        if (lane_id() == leader) base = atomicAdd(counter, n);
+        base = __shfl(base, (int)leader);
+    }
+    uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+    return base + rank;
+}
+
+// ---------------------------------------------------------------------------
+// primitive tests
+// ---------------------------------------------------------------------------
+// TriAccel::rayIntersect (triaccel.h:96-158)
+DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, float3 d, float mint, float maxt,
+                  float &u, float &v, float &t) {
+    const uint32_t k = __float_as_uint(f0.x);
+    float o_u, o_v, o_k, d_u, d_v, d_k;
+    if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
+    else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
+    else { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+    const float n_u = f0.y, n_v = f0.z, n_d = f0.w;
+    t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
+    if (!(t >= mint && t <= maxt)) return false;
+    const float hu = o_u + t * d_u - f1.x;
+    const float hv = o_v + t * d_v - f1.y;
+    u = hv * f1.z + hu * f1.w;
+    v = hu * f2.x + hv * f2.y;
+    return u >= 0 && v >= 0 && u + v <= 1.0f && k < 3;
+}
+
+// Rectangle::rayIntersect (rectangle.cpp:115-139)
+DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float maxt, float &t, float &lx, float &ly) {
+    const float *m = r.to_object;
+    float3 o = mk3(m[0] * wo.x + m[1] * wo.y + m[2] * wo.z + m[3], m[4] * wo.x + m[5] * wo.y + m[6] * wo.z + m[7],
+                   m[8] * wo.x + m[9] * wo.y + m[10] * wo.z + m[11]);
+    float3 d = mk3(m[0] * wd.x + m[1] * wd.y + m[2] * wd.z, m[4] * wd.x + m[5] * wd.y + m[6] * wd.z,
+                   m[8] * wd.x + m[9] * wd.y + m[10] * wd.z);
+    float hit = -o.z / d.z;
+    if (!(hit >= mint && hit <= maxt)) return false;
+    float x = o.x + d.x * hit, y = o.y + d.y * hit;
+    if (fabsf(x) <= 1 && fabsf(y) <= 1) { t = hit; lx = x; ly = y; return true; }
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// kd-tree traversal: t-interval front-to-back order with an LDS short stack
+// and kd-restart when the short stack has overflowed (Horn et al. 2007).
+// Finds the same closest primitive as the Havran loop: every leaf overlapping
+// the ray segment is visited until the best hit lies before the current
+// leaf's exit distance (sahkdtree3.h:299-300).
+// ---------------------------------------------------------------------------
+struct TraceCounts { uint32_t nodes, refs, tests; };
+
+template <bool SHADOW, bool COUNT>
+DEV bool kd_traverse(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, float &best, float &bu,
+                     float &bv, uint32_t &bprim, uint2 *stk, TraceCounts &cnt) {
+    const float3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    // AABB::rayIntersect (aabb.h:308-338)
+    float nearT = -INFINITY, farT = INFINITY;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float oi = comp(o, i), di = comp(d, i), ii = comp(inv, i);
+        if (di == 0.0f) {
+            if (oi < S.bmin[i] || oi > S.bmax[i]) return false;
+        } else {
+            float t1 = (S.bmin[i] - oi) * ii, t2 = (S.bmax[i] - oi) * ii;
+            nearT = fmaxf(fminf(t1, t2), nearT);
+            farT = fminf(fmaxf(t1, t2), farT);
+        }
+    }
+    if (!(nearT <= farT)) return false;
+    // adaptive ray epsilon (skdtree.cpp:126-129 closest, :213-216 shadow)
+    float rayMinT = rayMint;
+    if (rayMinT == kEpsilon) {
+        float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+        if (!SHADOW) m = fmaxf(m, kEpsilon);
+        rayMinT *= m;
+    }
+    const float mint = fmaxf(nearT, rayMinT);
+    float maxt = fminf(farT, rayMaxt);
+    if (!(maxt > mint)) return false;
+
+    best = maxt;
+    bool found = false;
+    float tmin = mint, tmax = maxt;
+    uint32_t node = 0;
+    uint32_t sp = 0, bottom = 0;
+    for (;;) {
+        // descend to a leaf
+        uint2 n = S.nodes[node];
+        if (COUNT) cnt.nodes++;
+        while (!(n.x & 0x80000000u)) {
+            const uint32_t axis = n.x & 3u;
+            const float split = __uint_as_float(n.y);
+            const uint32_t left = node + ((n.x & ~(3u | 0x40000000u)) >> 2);
+            const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+            const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+            const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
+            float tsplit = (split - oa) * ia;
+            if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
+            const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
+            const uint32_t first = belowFirst ? left : left + 1;
+            const uint32_t second = belowFirst ? left + 1 : left;
+            if (tsplit > tmax || tsplit <= 0.0f) {
+                node = first;
+            } else if (tsplit < tmin) {
+                node = second;
+            } else {
+                stk[(sp & (SHORT_STACK - 1)) * TRACE_BLOCK] = make_uint2(second, __float_as_uint(tmax));
+                ++sp;
+                if (sp - bottom > SHORT_STACK) ++bottom;
+                node = first;
+                tmax = tsplit;
+            }
+            n = S.nodes[node];
+            if (COUNT) cnt.nodes++;
+        }
+        // leaf: test every primitive against [mint, best] (skdtree.h:248-304)
+        for (uint32_t e = n.x & 0x7FFFFFFFu; e < n.y; ++e) {
+            const uint32_t p = S.indices[e];
+            if (COUNT) { cnt.refs++; cnt.tests++; }
+            const float4 f0 = S.tri[3 * p];
+            float t, u, v;
+            bool h;
+            if (__float_as_uint(f0.x) != MTSG_TRIACCEL_SHAPE) {
+                const float4 f1 = S.tri[3 * p + 1], f2 = S.tri[3 * p + 2];
+                h = tri_test(f0, f1, f2, o, d, mint, best, u, v, t);
+            } else {
+                const uint32_t ri = __float_as_uint(S.tri[3 * p + 2].w);
+                h = rect_test(S.rects[ri], o, d, mint, best, t, u, v);
+            }
+            if (h) {
+                if (SHADOW) return true;
+                best = t; bu = u; bv = v; bprim = p;
+                found = true;
+            }
+        }
+        if (found && best <= tmax) break;
+        // pop (or restart from the root if entries were dropped)
+        if (sp == bottom) {
+            if (bottom == 0) break;
+            sp = bottom = 0;
+            tmin = tmax;
+            tmax = best;
+            if (!(tmin < tmax)) break;
+            node = 0;
+            continue;
+        }
+        --sp;
+        const uint2 e = stk[(sp & (SHORT_STACK - 1)) * TRACE_BLOCK];
+        node = e.x;
+        tmin = tmax;
+        tmax = fminf(__uint_as_float(e.y), best);
+    }
+    return found;
+}
+
+// ---------------------------------------------------------------------------
+// kernels: traversal
+// ---------------------------------------------------------------------------
+template <bool COUNT>
+DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
+    if (!COUNT) return;
+    // wave reduction then one atomic per wave
+    unsigned long long a = c.nodes, b = c.refs, t = c.tests;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_down(a, off);
+        b += __shfl_down(b, off);
+        t += __shfl_down(t, off);
+    }
+    if (lane_id() == 0) { atomicAdd(ctr + 0, a); atomicAdd(ctr + 1, b); atomicAdd(ctr + 2, t); }
+}
+
+// Persistent closest-hit kernel: each wave fetches 64 queue entries at a time.
+template <bool COUNT>
+__global__ void __launch_bounds__(TRACE_BLOCK) k_trace_closest(DevScene S, DevPaths P, int qin, int cntIdx) {
+    __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
+    uint2 *stk = stack + threadIdx.x;
+    const uint32_t count = *((volatile uint32_t *)&P.cnt[cntIdx]);
+    const uint32_t *q = P.q[qin];
+    TraceCounts c{0, 0, 0};
+    for (;;) {
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(&P.cnt[3], 64u);
+        base = __shfl(base, 0);
+        if (base >= count) break;
+        const uint32_t i = base + lane_id();
+        if (i < count) {
+            const uint32_t slot = q[i];
+            const float4 ro = P.ray_o[slot], rd = P.ray_d[slot];
+            float best, u = 0, v = 0;
+            uint32_t prim = 0xFFFFFFFFu;
+            bool hit = kd_traverse<false, COUNT>(S, xyz(ro), xyz(rd), ro.w, rd.w, best, u, v, prim, stk, c);
+            P.hit[slot] = hit ? make_float4(best, u, v, __uint_as_float(prim))
+                              : make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+        }
+    }
+    flush_counts<COUNT>(P.ctr, c);
+}
+
+// Persistent shadow kernel (skdtree.cpp:207-226); unoccluded -> L += contribution
+template <bool COUNT>
+__global__ void __launch_bounds__(TRACE_BLOCK) k_trace_shadow(DevScene S, DevPaths P) {
+    __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
+    uint2 *stk = stack + threadIdx.x;
+    const uint32_t count = *((volatile uint32_t *)&P.cnt[2]);
+    TraceCounts c{0, 0, 0};
+    for (;;) {
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(&P.cnt[4], 64u);
+        base = __shfl(base, 0);
+        if (base >= count) break;
+        const uint32_t i = base + lane_id();
+        if (i < count) {
+            const uint32_t slot = P.qs[i];
+            const float4 so = P.sh_o[slot], sd = P.sh_d[slot];
+            float best, u, v;
+            uint32_t prim;
+            bool occ = kd_traverse<true, COUNT>(S, xyz(so), xyz(sd), kEpsilon, so.w, best, u, v, prim, stk, c);
+            if (!occ) {
+                const float4 con = P.sh_c[slot];
+                float4 L = P.L[slot];
+                L.x += con.x; L.y += con.y; L.z += con.z;
+                P.L[slot] = L;
+            }
+        }
+    }
+    flush_counts<COUNT>(P.ctr + 3, c);
+}
+
+// Debug entry points over caller-provided rays
+template <bool SHADOW>
+__global__ void __launch_bounds__(TRACE_BLOCK) k_trace_rays(DevScene S, const float *rays, uint32_t n, float *t,
+                                                            float *u, float *v, uint32_t *prim, uint8_t *occ) {
+    __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
+    uint2 *stk = stack + threadIdx.x;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float *r = rays + 8 * (size_t)i;
+    TraceCounts c{0, 0, 0};
+    float best, bu = 0, bv = 0;
+    uint32_t bp = 0xFFFFFFFFu;
+    bool h = kd_traverse<SHADOW, false>(S, mk3(r[0], r[1], r[2]), mk3(r[3], r[4], r[5]), r[6], r[7], best, bu, bv, bp, stk, c);
+    if (SHADOW) {
+        occ[i] = h ? 1 : 0;
+    } else if (h) {
+        // report triangle index, or 0x80000000 | rect for analytic rectangles
+        const float4 f0 = S.tri[3 * bp];
+        uint32_t id = __float_as_uint(S.tri[3 * bp + 2].w);
+        prim[i] = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE ? (0x80000000u | id) : id;
+        t[i] = best; u[i] = bu; v[i] = bv;
+    } else {
+        prim[i] = 0xFFFFFFFFu;
+        t[i] = INFINITY; u[i] = v[i] = 0.f;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// camera rays (PerspectiveCamera::sampleRayDifferential, perspective.cpp:271-298)
+// ---------------------------------------------------------------------------
+DEV void slot_pixel(const DevBatch &B, uint32_t slot, int &x, int &y, uint32_t &s) {
+    const uint32_t pix = slot & (TILE * TILE - 1);
+    const uint32_t rest = slot >> 8;
+    const uint32_t sl = rest % B.ns;
+    const uint32_t tl = rest / B.ns;
+    const int tile = B.toffset + (B.tile0 + (int)tl) * B.tstride;
+    const int tx = tile % B.tiles_x, ty = tile / B.tiles_x;
+    x = B.rect_x + tx * TILE + (int)(pix % TILE);
+    y = B.rect_y + ty * TILE + (int)(pix / TILE);
+    s = B.s0 + sl;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P) {
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    bool alive = false;
+    if (slot < B.nslots) {
+        int x, y;
+        uint32_t s;
+        slot_pixel(B, slot, x, y, s);
+        alive = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
+        if (alive) {
+            const uint64_t sid = ((uint64_t)y * (uint64_t)C.film_w + (uint64_t)x) * I.spp + s;
+            const uint64_t key = counterKey(I.seed, sid);
+            const float a = counterFloat(key, 0), b = counterFloat(key, 1);
+            const float sx = ((float)x + a) * C.inv_res_x, sy = ((float)y + b) * C.inv_res_y;
+            const float *m = C.s2c;
+            float px = m[0] * sx + m[1] * sy + m[3], py = m[4] * sx + m[5] * sy + m[7];
+            float pz = m[8] * sx + m[9] * sy + m[11], pw = m[12] * sx + m[13] * sy + m[15];
+            float3 nearP = pw == 1.0f ? mk3(px, py, pz) : mk3(px, py, pz) / pw;
+            float3 d = normalize(nearP);
+            float invZ = 1.0f / d.z;
+            const float *t = C.c2w;
+            float3 wd = mk3(t[0] * d.x + t[1] * d.y + t[2] * d.z, t[4] * d.x + t[5] * d.y + t[6] * d.z,
+                            t[8] * d.x + t[9] * d.y + t[10] * d.z);
+            P.ray_o[slot] = make_float4(t[3], t[7], t[11], C.near_clip * invZ);
+            P.ray_d[slot] = make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ);
+            P.L[slot] = make_float4(0.f, 0.f, 0.f, 1.0f);
+            P.T[slot] = make_float4(1.f, 1.f, 1.f, 1.f);
+            P.key[slot] = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
+            P.st[slot] = make_uint2(1u, 2u);   // depth 1, next dimension 2
+        } else {
+            P.L[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    const uint32_t qi = wave_append(&P.cnt[0], alive);
+    if (alive) P.q[0][qi] = slot;
+}
+
+// ---------------------------------------------------------------------------
+// BSDFs (local shading frame)
+// ---------------------------------------------------------------------------
+struct BsdfSample {
+    float3 wo, weight;
+    float pdf, eta;
+    uint32_t delta;
+};
+
+// warp.cpp:43-52,81-102
+DEV float3 cosine_hemisphere(float sx, float sy) {
+    float r1 = 2.0f * sx - 1.0f, r2 = 2.0f * sy - 1.0f;
+    float phi, r;
+    if (r1 == 0 && r2 == 0) { r = phi = 0; }
+    else if (r1 * r1 > r2 * r2) { r = r1; phi = (kPi / 4.0f) * (r2 / r1); }
+    else { r = r2; phi = (kPi / 2.0f) - (r1 / r2) * (kPi / 4.0f); }
+    float sinPhi, cosPhi;
+    sincosf(phi, &sinPhi, &cosPhi);
+    float px = r * cosPhi, py = r * sinPhi;
+    float z = sqrtf(fmaxf(0.0f, 1.0f - px * px - py * py));
+    if (z == 0) z = 1e-10f;
+    return mk3(px, py, z);
+}
+
+// math.cpp:25-70
+DEV float erfinv_m(float x) {
+    float w = -logf((1.0f - x) * (1.0f + x));
+    float p;
+    if (w < 5.0f) {
+        w = w - 2.5f;
+        p = 2.81022636e-08f;
+        p = 3.43273939e-07f + p * w;
+        p = -3.5233877e-06f + p * w;
+        p = -4.39150654e-06f + p * w;
+        p = 0.00021858087f + p * w;
+        p = -0.00125372503f + p * w;
+        p = -0.00417768164f + p * w;
+        p = 0.246640727f + p * w;
+        p = 1.50140941f + p * w;
+    } else {
+        w = sqrtf(w) - 3.0f;
+        p = -0.000200214257f;
+        p = 0.000100950558f + p * w;
+        p = 0.00134934322f + p * w;
+        p = -0.00367342844f + p * w;
+        p = 0.00573950773f + p * w;
+        p = -0.0076224613f + p * w;
+        p = 0.00943887047f + p * w;
+        p = 1.00167406f + p * w;
+        p = 2.83297682f + p * w;
+    }
+    return p * x;
+}
+DEV float erf_m(float x) {
+    const float a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f;
+    const float a4 = -1.453152027f, a5 = 1.061405429f, p = 0.3275911f;
+    float sign = copysignf(1.0f, x);
+    x = fabsf(x);
+    float t = 1.0f / (1.0f + p * x);
+    float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * expf(-x * x);
+    return sign * y;
+}
+DEV float hypot2_m(float a, float b) {   // math.cpp:74-86
+    float r;
+    if (fabsf(a) > fabsf(b)) { r = b / a; r = fabsf(a) * sqrtf(1.0f + r * r); }
+    else if (b != 0.0f) { r = a / b; r = fabsf(b) * sqrtf(1.0f + r * r); }
+    else r = 0.0f;
+    return r;
+}
+
+// MicrofacetDistribution, isotropic (microfacet.h:191-697)
+struct MF {
+    int type;
+    float a;
+    bool visible;
+    DEV float D(float3 m) const {
+        if (m.z <= 0) return 0.0f;
+        float ct2 = m.z * m.z;
+        float be = ((m.x * m.x) / (a * a) + (m.y * m.y) / (a * a)) / ct2;
+        float result;
+        if (type == MTSG_MF_BECKMANN) result = expf(-be) / (kPi * a * a * ct2 * ct2);
+        else { float root = (1.0f + be) * ct2; result = 1.0f / (kPi * a * a * root * root); }
+        if (result * m.z < 1e-20f) result = 0;
+        return result;
+    }
+    DEV float G1(float3 v, float3 m) const {
+        if (dot(v, m) * v.z <= 0) return 0.0f;
+        float temp = 1 - v.z * v.z;
+        float tt = temp <= 0.0f ? 0.0f : fabsf(sqrtf(temp) / v.z);
+        if (tt == 0.0f) return 1.0f;
+        if (type == MTSG_MF_BECKMANN) {
+            float aa = 1.0f / (a * tt);
+            if (aa >= 1.6f) return 1.0f;
+            float aSqr = aa * aa;
+            return (3.535f * aa + 2.181f * aSqr) / (1.0f + 2.276f * aa + 2.577f * aSqr);
+        }
+        return 2.0f / (1.0f + hypot2_m(1.0f, a * tt));
+    }
+    DEV void visible11(float thetaI, float sx, float sy, float &slx, float &sly) const {
+        if (type == MTSG_MF_BECKMANN) {
+            const float SQRT_PI_INV = 0.56418958354775628695f;
+            if (thetaI < 1e-4f) {
+                float r = sqrtf(-logf(1.0f - sx));
+                float sp, cp;
+                sincosf(2 * kPi * sy, &sp, &cp);
+                slx = r * cp; sly = r * sp;
+                return;
+            }
+            float tanThetaI = tanf(thetaI), cotThetaI = 1 / tanThetaI;
+            float aa = -1, c = erf_m(cotThetaI);
+            float sample_x = fmaxf(sx, 1e-6f);
+            float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
+            float b = c - (1 + c) * powf(1 - sample_x, fit);
+            float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * expf(-cotThetaI * cotThetaI));
+            int it = 0;
+            while (++it < 10) {
+                if (!(b >= aa && b <= c)) b = 0.5f * (aa + c);
+                float invErf = erfinv_m(b);
+                float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * expf(-invErf * invErf)) - sample_x;
+                float derivative = normalization * (1 - invErf * tanThetaI);
+                if (fabsf(value) < 1e-5f) break;
+                if (value > 0) c = b; else aa = b;
+                b -= value / derivative;
+            }
+            slx = erfinv_m(b);
+            sly = erfinv_m(2.0f * fmaxf(sy, 1e-6f) - 1.0f);
+            return;
+        }
+        if (thetaI < 1e-4f) {
+            float r = sqrtf(fmaxf(0.0f, sx / (1 - sx)));
+            float sp, cp;
+            sincosf(2 * kPi * sy, &sp, &cp);
+            slx = r * cp; sly = r * sp;
+            return;
+        }
+        float tanThetaI = tanf(thetaI);
+        float aa = 1 / tanThetaI;
+        float G1v = 2.0f / (1.0f + sqrtf(fmaxf(0.0f, 1.0f + 1.0f / (aa * aa))));
+        float A = 2.0f * sx / G1v - 1.0f;
+        if (fabsf(A) == 1) A -= copysignf(1.0f, A) * kEpsilon;
+        float tmp = 1.0f / (A * A - 1.0f);
+        float B = tanThetaI;
+        float D = sqrtf(fmaxf(0.0f, B * B * tmp * tmp - (A * A - B * B) * tmp));
+        float s1 = B * tmp - D, s2 = B * tmp + D;
+        slx = (A < 0.0f || s2 > 1.0f / tanThetaI) ? s1 : s2;
+        float S;
+        if (sy > 0.5f) { S = 1.0f; sy = 2.0f * (sy - 0.5f); }
+        else { S = -1.0f; sy = 2.0f * (0.5f - sy); }
+        float z = (sy * (sy * (sy * (-0.365728915865723f) + 0.790235037209296f) - 0.424965825137544f) + 0.000152998850436920f) /
+                  (sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) - 0.539825872510702f);
+        sly = S * z * sqrtf(1.0f + slx * slx);
+    }
+    DEV float3 sample(float3 wi_, float sx, float sy, float &pdf) const {
+        if (visible) {
+            float3 wi = normalize(mk3(a * wi_.x, a * wi_.y, wi_.z));
+            float theta = 0, phi = 0;
+            if (wi.z < 0.99999f) { theta = acosf(wi.z); phi = atan2f(wi.y, wi.x); }
+            float sinPhi, cosPhi;
+            sincosf(phi, &sinPhi, &cosPhi);
+            float slx, sly;
+            visible11(theta, sx, sy, slx, sly);
+            float rx = cosPhi * slx - sinPhi * sly, ry = sinPhi * slx + cosPhi * sly;
+            rx *= a; ry *= a;
+            float normalization = 1.0f / sqrtf(rx * rx + ry * ry + 1.0f);
+            float3 m = mk3(-rx * normalization, -ry * normalization, normalization);
+            pdf = wi_.z == 0 ? 0.0f : G1(wi_, m) * fabsf(dot(wi_, m)) * D(m) / fabsf(wi_.z);
+            return m;
+        }
+        float alphaSqr = a * a;
+        float sinPhiM, cosPhiM;
+        sincosf((2.0f * kPi) * sy, &sinPhiM, &cosPhiM);
+        float cosThetaM;
+        if (type == MTSG_MF_BECKMANN) {
+            float t2 = alphaSqr * -logf(1.0f - sx);
+            cosThetaM = 1.0f / sqrtf(1.0f + t2);
+            pdf = (1.0f - sx) / (kPi * a * a * cosThetaM * cosThetaM * cosThetaM);
+        } else {
+            float t2 = alphaSqr * sx / (1.0f - sx);
+            cosThetaM = 1.0f / sqrtf(1.0f + t2);
+            float temp = 1 + t2 / alphaSqr;
+            pdf = kInvPi / (a * a * cosThetaM * cosThetaM * cosThetaM * temp * temp);
+        }
+        if (pdf < 1e-20f) pdf = 0;
+        float sinThetaM = sqrtf(fmaxf(0.0f, 1 - cosThetaM * cosThetaM));
+        return mk3(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
+    }
+};
+
+// util.cpp:739-761
+DEV float3 fresnel_conductor(float cosThetaI, float3 eta, float3 k) {
+    float c2 = cosThetaI * cosThetaI, s2 = 1 - c2, s4 = s2 * s2;
+    float3 temp1 = eta * eta - k * k - mk3(s2, s2, s2);
+    float3 a2pb2 = sqrtSafe3(temp1 * temp1 + k * k * eta * eta * 4);
+    float3 aa = sqrtSafe3((a2pb2 + temp1) * 0.5f);
+    float3 term1 = a2pb2 + mk3(c2, c2, c2), term2 = aa * (2 * cosThetaI);
+    float3 Rs2 = (term1 - term2) / (term1 + term2);
+    float3 term3 = a2pb2 * c2 + mk3(s4, s4, s4), term4 = term2 * s2;
+    float3 Rp2 = Rs2 * (term3 - term4) / (term3 + term4);
+    return (Rp2 + Rs2) * 0.5f;
+}
+
+// util.cpp:651-681
+DEV float fresnel_dielectric(float cosThetaI_, float &cosThetaT_, float eta) {
+    if (eta == 1) { cosThetaT_ = -cosThetaI_; return 0.0f; }
+    float scale = (cosThetaI_ > 0) ? 1 / eta : eta, c2 = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
+    if (c2 <= 0.0f) { cosThetaT_ = 0.0f; return 1.0f; }
+    float ci = fabsf(cosThetaI_), ct = sqrtf(c2);
+    float Rs = (ci - eta * ct) / (ci + eta * ct), Rp = (eta * ci - ct) / (eta * ci + ct);
+    cosThetaT_ = (cosThetaI_ > 0) ? -ct : ct;
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+
+// BSDF::eval * cos (ESolidAngle) and pdf for the smooth BSDFs
+DEV float3 bsdf_eval(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
+    pdf = 0.0f;
+    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:107-126
+        if (!b.smooth || wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
+        pdf = kInvPi * wo.z;
+        return ld3(b.reflectance) * (kInvPi * wo.z);
+    }
+    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:235-293
+        if (wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
+        float3 H = normalize(wo + wi);
+        MF mf{b.distribution, b.alpha_u, b.sample_visible != 0};
+        const float Dv = mf.D(H);
+        if (mf.visible) pdf = Dv * mf.G1(wi, H) / (4.0f * wi.z);
+        else pdf = Dv * H.z / (4 * fabsf(dot(wo, H)));
+        if (Dv == 0) return mk3(0, 0, 0);
+        float3 F = fresnel_conductor(dot(wi, H), ld3(b.eta), ld3(b.k)) * ld3(b.spec_refl);
+        const float G = mf.G1(wi, H) * mf.G1(wo, H);
+        float model = Dv * G / (4.0f * wi.z);
+        return F * model;
+    }
+    return mk3(0, 0, 0);   // dielectric: delta components only
+}
+
+DEV bool bsdf_sample(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r) {
+    r.eta = 1.0f;
+    r.delta = 0;
+    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
+        if (wi.z <= 0) return false;
+        r.wo = cosine_hemisphere(sx, sy);
+        r.pdf = kInvPi * r.wo.z;
+        r.weight = ld3(b.reflectance);
+        return !isZero(r.weight);
+    }
+    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:345-394
+        if (wi.z < 0) return false;
+        MF mf{b.distribution, b.alpha_u, b.sample_visible != 0};
+        float pdf;
+        float3 m = mf.sample(wi, sx, sy, pdf);
+        if (pdf == 0) return false;
+        r.wo = m * (2 * dot(wi, m)) - wi;
+        if (r.wo.z <= 0) return false;
+        float3 F = fresnel_conductor(dot(wi, m), ld3(b.eta), ld3(b.k)) * ld3(b.spec_refl);
+        float weight;
+        if (mf.visible) weight = mf.G1(r.wo, m);
+        else weight = mf.D(m) * mf.G1(wi, m) * mf.G1(r.wo, m) * dot(wi, m) / (pdf * wi.z);
+        r.pdf = pdf / (4.0f * dot(r.wo, m));
+        r.weight = F * weight;
+        return !isZero(r.weight);
+    }
+    if (b.type == MTSG_BSDF_DIELECTRIC) {   // dielectric.cpp:277-333
+        float cosThetaT;
+        float F = fresnel_dielectric(wi.z, cosThetaT, b.ior_eta);
+        r.delta = 1;
+        if (sx <= F) {
+            r.wo = mk3(-wi.x, -wi.y, wi.z);
+            r.pdf = F;
+            r.weight = ld3(b.spec_refl);
+        } else {
+            float scale = -(cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta);
+            r.wo = mk3(scale * wi.x, scale * wi.y, cosThetaT);
+            r.eta = cosThetaT < 0 ? b.ior_eta : b.ior_inv_eta;
+            r.pdf = 1 - F;
+            float factor = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;
+            r.weight = ld3(b.spec_trans) * (factor * factor);
+        }
+        return !isZero(r.weight);
+    }
+    return false;
+}
+
+DEV float mis(float pdfA, float pdfB) {   // path.cpp:296-300
+    pdfA *= pdfA;
+    pdfB *= pdfB;
+    return pdfA / (pdfA + pdfB);
+}
+
+// DiscreteDistribution::sampleReuse (pmf.h:128-188): lower_bound over cdf[0..n]
+DEV uint32_t pmf_sample_reuse(const float *cdf, uint32_t n, float &x, float &pdf) {
+    uint32_t lo = 0, len = n + 1;
+    while (len > 0) {   // std::lower_bound
+        uint32_t half = len >> 1;
+        if (cdf[lo + half] < x) { lo += half + 1; len -= half + 1; }
+        else len = half;
+    }
+    int idx = (int)lo - 1;
+    uint32_t index = (uint32_t)min((int)n - 1, max(0, idx));
+    while ((cdf[index + 1] - cdf[index]) == 0 && index < n) ++index;
+    float c0 = cdf[index], c1 = cdf[index + 1];
+    pdf = c1 - c0;
+    x = (x - c0) / (c1 - c0);
+    return index;
+}
+
+// ---------------------------------------------------------------------------
+// shading
+// ---------------------------------------------------------------------------
+struct Its {
+    float3 p, geoN;
+    Frame3 sh;
+    int shape;
+};
+
+// ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428) + computeShadingFrame (util.cpp:603-608)
+DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, Its &its) {
+    const uint32_t p = __float_as_uint(h.w);
+    const float4 f0 = S.tri[3 * p];
+    float3 dpdu, n;
+    if (__float_as_uint(f0.x) != MTSG_TRIACCEL_SHAPE) {
+        const uint4 ti = S.tidx[p];
+        its.shape = (int)ti.w;
+        const float bx = 1 - h.y - h.z, by = h.y, bz = h.z;
+        const float3 p0 = xyz(S.vpos[ti.x]), p1 = xyz(S.vpos[ti.y]), p2 = xyz(S.vpos[ti.z]);
+        its.p = p0 * bx + p1 * by + p2 * bz;
+        float3 fn = cross(p1 - p0, p2 - p0);
+        if (!isZero(fn)) fn = fn / length(fn);
+        dpdu = xyz(S.tdpdu[p]);
+        if (!S.shapes[ti.w].face_normals) {
+            n = normalize(xyz(S.vnrm[ti.x]) * bx + xyz(S.vnrm[ti.y]) * by + xyz(S.vnrm[ti.z]) * bz);
+            if (dot(fn, n) < 0) fn = -fn;
+        } else {
+            n = fn;
+        }
+        its.geoN = fn;
+    } else {
+        const uint32_t ri = __float_as_uint(S.tri[3 * p + 2].w);
+        const mtsg_rect &r = S.rects[ri];
+        its.shape = (int)r.shape_index;
+        its.geoN = ld3(r.frame_n);
+        n = its.geoN;
+        dpdu = ld3(r.dpdu);
+        its.p = ro + rd * h.x;
+    }
+    its.sh.n = n;
+    its.sh.s = normalize(dpdu - n * dot(n, dpdu));
+    its.sh.t = cross(n, its.sh.s);
+}
+
+// Shape::sampleDirect over TriMesh / Rectangle samplePosition (shape.cpp:102-115,
+// trimesh.cpp:412-423, triangle.cpp:24-60, rectangle.cpp:200-207)
+DEV void emitter_sample_position(const DevScene &S, const mtsg_emitter &em, float sx, float sy, float3 &p, float3 &n) {
+    const mtsg_shape &sh = S.shapes[em.shape];
+    if (sh.type == MTSG_SHAPE_MESH) {
+        float pdfDummy;
+        uint32_t index = pmf_sample_reuse(S.emitter_tri_cdf + em.cdf_offset, sh.tri_count, sy, pdfDummy);
+        const uint4 ti = S.tidx[sh.tri_begin + index];
+        const float3 p0 = xyz(S.vpos[ti.x]), p1 = xyz(S.vpos[ti.y]), p2 = xyz(S.vpos[ti.z]);
+        float a = sqrtf(fmaxf(0.0f, 1.0f - sx));
+        float bx = 1 - a, by = a * sy;
+        float3 sideA = p1 - p0, sideB = p2 - p0;
+        p = p0 + (sideA * bx) + (sideB * by);
+        if (!sh.face_normals)
+            n = normalize(xyz(S.vnrm[ti.x]) * (1.0f - bx - by) + xyz(S.vnrm[ti.y]) * bx + xyz(S.vnrm[ti.z]) * by);
+        else
+            n = normalize(cross(sideA, sideB));
+    } else {
+        const mtsg_rect &r = S.rects[sh.rect];
+        const float *m = r.to_world;
+        float x = sx * 2 - 1, y = sy * 2 - 1;
+        p = mk3(m[0] * x + m[1] * y + m[3], m[4] * x + m[5] * y + m[7], m[8] * x + m[9] * y + m[11]);
+        n = ld3(r.frame_n);
+    }
+}
+
+DEV void enqueue_path(const DevPaths &P, uint32_t *cnt, uint32_t *q, bool pred, uint32_t slot) {
+    const uint32_t i = wave_append(cnt, pred);
+    if (pred) q[i] = slot;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, DevPaths P, int bounce, int qin,
+                                                 int cntIn, int hasAlpha) {
+    const uint32_t count = *((volatile uint32_t *)&P.cnt[cntIn]);
+    const uint32_t nIter = (count + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
+    const int qout = qin ^ 1;
+    for (uint32_t it = 0; it < nIter; ++it) {
+        const uint32_t i = (it * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+        bool alive = i < count;
+        bool cont = false, shadow = false;
+        uint32_t slot = 0;
+        if (alive) {
+            slot = P.q[qin][i];
+            const float4 h = P.hit[slot];
+            const float4 ro4 = P.ray_o[slot], rd4 = P.ray_d[slot];
+            const float3 ro = xyz(ro4), rd = xyz(rd4);
+            float4 L4 = P.L[slot];
+            float4 T4 = P.T[slot];
+            uint2 st = P.st[slot];
+            const uint2 kk = P.key[slot];
+            const uint64_t key = (uint64_t)kk.x | ((uint64_t)kk.y << 32);
+            float3 L = xyz(L4), T = xyz(T4);
+            float eta = T4.w;
+            uint32_t depth = st.x & 0xFFFFu;
+            uint32_t flags = st.x & 0xFFFF0000u;
+            uint32_t dim = st.y;
+            const bool valid = __float_as_uint(h.w) != 0xFFFFFFFFu;
+            bool done = false;
+            Its its;
+            if (valid) fill_its(S, ro, rd, h, its);
+            if (bounce == 0) {
+                // RadianceQueryRecord::rayIntersect (records.inl:117-143)
+                if (hasAlpha) L4.w = valid ? 1.0f : 0.0f;
+                if (!valid) done = true;   // no environment emitter (path.cpp:136-143)
+            } else {
+                // tail of the previous iteration after scene->rayIntersect (path.cpp:226-286)
+                if (!valid) {
+                    done = true;
+                } else {
+                    const int em = S.shapes[its.shape].emitter;
+                    if (em >= 0) {
+                        const mtsg_emitter &E = S.emitters[em];
+                        const float3 value = dot(its.sh.n, -rd) > 0 ? ld3(E.radiance) : mk3(0, 0, 0);
+                        float lumPdf = 0.0f;
+                        if (!(flags & F_DELTA)) {
+                            // Scene::pdfEmitterDirect with dRec.setQuery(ray, its)
+                            const float4 ax = P.aux[slot];
+                            const float3 refN = xyz(ax);
+                            if (dot(rd, refN) >= 0 && dot(rd, its.sh.n) < 0)
+                                lumPdf = E.inv_area * (h.x * h.x) / fabsf(dot(rd, its.sh.n));
+                            lumPdf *= E.pdf_discrete;
+                        }
+                        L += T * value * mis(P.aux[slot].w, lumPdf);
+                    }
+                    if (depth++ >= (uint32_t)I.rr_depth) {
+                        float q = fminf(maxc(T) * eta * eta, 0.95f);
+                        if (counterFloat(key, dim++) >= q) done = true;
+                        else T = T / q;
+                    }
+                }
+            }
+            if (!done && !((int)depth <= I.max_depth || I.max_depth < 0)) done = true;
+            if (!done) {
+                const mtsg_shape &shp = S.shapes[its.shape];
+                const mtsg_bsdf &bsdf = S.bsdfs[shp.bsdf];
+                const float3 wi = its.sh.toLocal(-rd);
+                if (bounce == 0 && shp.emitter >= 0 && !I.hide_emitters) {
+                    if (dot(its.sh.n, -rd) > 0) L += T * ld3(S.emitters[shp.emitter].radiance);
+                }
+                if (((int)depth >= I.max_depth && I.max_depth > 0) ||
+                    (I.strict_normals && dot(rd, its.geoN) * wi.z >= 0)) {
+                    done = true;
+                } else {
+                    const float3 refN = bsdf.ref_n_zero ? mk3(0, 0, 0) : its.sh.n;
+                    // ---- direct illumination (path.cpp:172-200)
+                    if (bsdf.smooth) {
+                        float sx = counterFloat(key, dim++), sy = counterFloat(key, dim++);
+                        float emPdf;
+                        const uint32_t ei = pmf_sample_reuse(S.emitter_cdf, S.n_emitters, sx, emPdf);
+                        const mtsg_emitter &E = S.emitters[ei];
+                        float3 ep, en;
+                        emitter_sample_position(S, E, sx, sy, ep, en);
+                        float3 dd = ep - its.p;
+                        const float distSquared = dot(dd, dd);
+                        const float dist = sqrtf(distSquared);
+                        dd = dd / dist;
+                        const float dp = fabsf(dot(dd, en));
+                        float pdf = E.inv_area * (dp != 0 ? (distSquared / dp) : 0.0f);
+                        if (dot(dd, refN) >= 0 && dot(dd, en) < 0 && pdf != 0) {
+                            float3 value = ld3(E.radiance) / pdf;
+                            pdf *= emPdf;
+                            value = value / emPdf;
+                            const float3 wo = its.sh.toLocal(dd);
+                            float bpdf;
+                            const float3 bval = bsdf_eval(bsdf, wi, wo, bpdf);
+                            if (!isZero(bval) && (!I.strict_normals || dot(its.geoN, dd) * wo.z > 0)) {
+                                const float weight = mis(pdf, bpdf);
+                                const float3 c = T * value * bval * weight;
+                                if (!isZero(c)) {
+                                    shadow = true;
+                                    P.sh_o[slot] = make_float4(its.p.x, its.p.y, its.p.z, dist * (1 - kShadowEpsilon));
+                                    P.sh_d[slot] = make_float4(dd.x, dd.y, dd.z, 0.f);
+                                    P.sh_c[slot] = make_float4(c.x, c.y, c.z, 0.f);
+                                }
+                            }
+                        }
+                    }
+                    // ---- BSDF sampling (path.cpp:206-221)
+                    float sx = counterFloat(key, dim++), sy = counterFloat(key, dim++);
+                    BsdfSample bs;
+                    if (!bsdf_sample(bsdf, wi, sx, sy, bs)) {
+                        done = true;
+                    } else {
+                        flags |= F_SCATTERED;
+                        const float3 wo = its.sh.toWorld(bs.wo);
+                        if (I.strict_normals && dot(its.geoN, wo) * bs.wo.z <= 0) {
+                            done = true;
+                        } else {
+                            T = T * bs.weight;
+                            eta *= bs.eta;
+                            flags = bs.delta ? (flags | F_DELTA) : (flags & ~F_DELTA);
+                            P.ray_o[slot] = make_float4(its.p.x, its.p.y, its.p.z, kEpsilon);
+                            P.ray_d[slot] = make_float4(wo.x, wo.y, wo.z, INFINITY);
+                            P.aux[slot] = make_float4(refN.x, refN.y, refN.z, bs.pdf);
+                            cont = true;
+                        }
+                    }
+                }
+            }
+            P.L[slot] = make_float4(L.x, L.y, L.z, L4.w);
+            if (cont) {
+                P.T[slot] = make_float4(T.x, T.y, T.z, eta);
+                P.st[slot] = make_uint2(depth | flags, dim);
+            }
+        }
+        enqueue_path(P, &P.cnt[2], P.qs, shadow, slot);
+        enqueue_path(P, &P.cnt[cntIn ^ 1], P.q[qout], cont, slot);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// film splat: one workgroup per 16x16 tile, LDS accumulation of the
+// discretized reconstruction filter (imageblock.h:124-204), then one float
+// atomic per texel into the tile+border block in HBM.
+// ---------------------------------------------------------------------------
+constexpr int MAX_BORDER = 4;
+constexpr int LT = TILE + 2 * MAX_BORDER;   // LDS tile edge
+
+__global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P, float *film,
+                                                 int blockW, int blockH) {
+    __shared__ float acc[5][LT * LT];
+    const int ch = C.has_alpha ? 5 : 4;
+    for (int k = threadIdx.x; k < 5 * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
+    __syncthreads();
+    const int tl = blockIdx.x;
+    const int tile = B.toffset + (B.tile0 + tl) * B.tstride;
+    const int tx = tile % B.tiles_x, ty = tile / B.tiles_x;
+    const int x0 = B.rect_x + tx * TILE, y0 = B.rect_y + ty * TILE;   // tile origin (film coords)
+    const int bord = C.border;
+    const float r = C.filter_radius;
+    const int pix = threadIdx.x;
+    const int x = x0 + (pix % TILE), y = y0 + (pix / TILE);
+    const bool inside = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
+    if (inside) {
+        for (uint32_t sl = 0; sl < B.ns; ++sl) {
+            const uint32_t slot = ((uint32_t)tl * B.ns + sl) * (TILE * TILE) + pix;
+            const float4 L = P.L[slot];
+            const uint2 kk = P.key[slot];
+            const uint64_t key = (uint64_t)kk.x | ((uint64_t)kk.y << 32);
+            const float spx = (float)x + counterFloat(key, 0), spy = (float)y + counterFloat(key, 1);
+            // invalid samples are rejected (imageblock.h:147-151)
+            if (!(isfinite(L.x) && isfinite(L.y) && isfinite(L.z) && L.x >= 0 && L.y >= 0 && L.z >= 0)) continue;
+            // position relative to the LDS tile origin (x0 - MAX_BORDER)
+            const float px = spx - 0.5f - (float)(x0 - MAX_BORDER), py = spy - 0.5f - (float)(y0 - MAX_BORDER);
+            // clamp to the block of this render call (tile rect + border)
+            const int bx0 = B.rect_x - bord - (x0 - MAX_BORDER), by0 = B.rect_y - bord - (y0 - MAX_BORDER);
+            const int bx1 = bx0 + blockW - 1, by1 = by0 + blockH - 1;
+            const int minx = max((int)ceilf(px - r), max(bx0, 0)), miny = max((int)ceilf(py - r), max(by0, 0));
+            const int maxx = min((int)floorf(px + r), min(bx1, LT - 1)), maxy = min((int)floorf(py + r), min(by1, LT - 1));
+            for (int yy = miny; yy <= maxy; ++yy) {
+                const float wy = C.filter_values[min((int)fabsf(((float)yy - py) * C.filter_scale), 31)];
+                for (int xx = minx; xx <= maxx; ++xx) {
+                    const float wgt = C.filter_values[min((int)fabsf(((float)xx - px) * C.filter_scale), 31)] * wy;
+                    const int o = yy * LT + xx;
+                    atomicAdd(&acc[0][o], wgt * L.x);
+                    atomicAdd(&acc[1][o], wgt * L.y);
+                    atomicAdd(&acc[2][o], wgt * L.z);
+                    if (ch == 5) atomicAdd(&acc[3][o], wgt * L.w);
+                    atomicAdd(&acc[4][o], wgt);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // flush into the HBM block (blockW x blockH x 5, origin = rect - border)
+    for (int k = threadIdx.x; k < LT * LT; k += BLOCK) {
+        const int ly = k / LT, lx = k % LT;
+        const int fx = x0 - MAX_BORDER + lx - (B.rect_x - bord), fy = y0 - MAX_BORDER + ly - (B.rect_y - bord);
+        if (fx < 0 || fy < 0 || fx >= blockW || fy >= blockH) continue;
+        const float w = acc[4][k];
+        if (w == 0.0f) continue;
+        float *dst = film + ((size_t)fy * blockW + fx) * 5;
+        unsafeAtomicAdd(dst + 0, acc[0][k]);
+        unsafeAtomicAdd(dst + 1, acc[1][k]);
+        unsafeAtomicAdd(dst + 2, acc[2][k]);
+        unsafeAtomicAdd(dst + 3, ch == 5 ? acc[3][k] : w);   // no alpha channel: alpha == 1 per sample
+        unsafeAtomicAdd(dst + 4, w);
+    }
+}
+
+__global__ void k_reset(uint32_t *cnt, int next, int cntCur) {
+    // zero the next queue, shadow queue and fetch counters for this bounce
+    if (threadIdx.x == 0) {
+        cnt[next] = 0;
+        cnt[2] = 0;
+        cnt[3] = 0;
+        cnt[4] = 0;
+        (void)cntCur;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+thread_local std::string g_err;
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            g_err = std::string(#expr) + ": " + hipGetErrorString(_e);                 \
+            return _e == hipErrorOutOfMemory ? MTSG_ERR_OOM : MTSG_ERR_DEVICE;         \
+        }                                                                              \
+    } while (0)
+
+template <class T>
+int upload(const T *src, size_t n, T **dst) {
+    *dst = nullptr;
+    if (n == 0) return MTSG_OK;
+    HIP_TRY(hipMalloc((void **)dst, n * sizeof(T)));
+    HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return MTSG_OK;
+}
+
+}  // namespace
+
+struct mtsg_scene {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevScene ds{};
+    DevCamera cam{};
+    std::vector<void *> allocs;
+    // batch buffers
+    uint32_t capacity = 0;         // paths per batch
+    uint32_t requestedBatch = 0;
+    DevPaths P{};
+    std::vector<void *> batchAllocs;
+    uint32_t *hostCnt = nullptr;   // pinned copy of the queue counters
+    int cuCount = 0;
+    int traceGrid = 0, shadeGrid = 0;
+    uint32_t flags = 0;
+    std::atomic<int> cancel{0};
+    mtsg_stats stats{};
+    std::vector<hipEvent_t> evPool;
+    size_t evUsed = 0;
+    std::vector<std::pair<int, size_t>> timed;   // (kind, event index)
+};
+
+namespace {
+
+int set_device(mtsg_scene *s) {
+    HIP_TRY(hipSetDevice(s->device));
+    return MTSG_OK;
+}
+
+void free_batch(mtsg_scene *s) {
+    for (void *p : s->batchAllocs) hipFree(p);
+    s->batchAllocs.clear();
+    s->capacity = 0;
+}
+
+int ensure_batch(mtsg_scene *s, uint32_t paths) {
+    if (s->capacity >= paths) return MTSG_OK;
+    free_batch(s);
+    auto alloc = [&](size_t bytes, void **p) -> int {
+        HIP_TRY(hipMalloc(p, bytes));
+        s->batchAllocs.push_back(*p);
+        return MTSG_OK;
+    };
+    size_t n = paths;
+    DevPaths &P = s->P;
+    int rc = MTSG_OK;
+#define A(field, T) if ((rc = alloc(n * sizeof(T), (void **)&P.field)) != MTSG_OK) return rc
+    A(ray_o, float4); A(ray_d, float4); A(hit, float4); A(L, float4); A(T, float4); A(aux, float4);
+    A(key, uint2); A(st, uint2); A(sh_o, float4); A(sh_d, float4); A(sh_c, float4);
+    A(q[0], uint32_t); A(q[1], uint32_t); A(qs, uint32_t);
+#undef A
+    if ((rc = alloc(64 * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
+    if ((rc = alloc(8 * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
+    HIP_TRY(hipMemset(P.ctr, 0, 8 * sizeof(unsigned long long)));
+    s->capacity = paths;
+    return MTSG_OK;
+}
+
+enum { K_CAMERA = 0, K_CLOSEST, K_SHADOW, K_SHADE, K_SPLAT };
+
+hipEvent_t next_event(mtsg_scene *s) {
+    if (s->evUsed == s->evPool.size()) {
+        hipEvent_t e;
+        hipEventCreate(&e);
+        s->evPool.push_back(e);
+    }
+    return s->evPool[s->evUsed++];
+}
+
+// bracket a launch with events when timing is enabled
+template <class F>
+void timed_launch(mtsg_scene *s, int kind, F f) {
+    if (!(s->flags & MTSG_FLAG_TIMING)) { f(); return; }
+    size_t i0 = s->evUsed;
+    hipEventRecord(next_event(s), s->stream);
+    f();
+    hipEventRecord(next_event(s), s->stream);
+    s->timed.emplace_back(kind, i0);
+}
+
+int validate(const mtsg_render_params *p, const mtsg_scene *s) {
+    if (!p) { g_err = "null params"; return MTSG_ERR_INVALID; }
+    if (p->spp == 0) { g_err = "spp must be > 0"; return MTSG_ERR_INVALID; }
+    if (p->rr_depth <= 0) { g_err = "'rrDepth' must be set to a value greater than zero!"; return MTSG_ERR_INVALID; }
+    if (p->max_depth <= 0 && p->max_depth != -1) { g_err = "'maxDepth' must be set to -1 (infinite) or a value greater than zero!"; return MTSG_ERR_INVALID; }
+    if (p->tile_w <= 0 || p->tile_h <= 0 || p->tile_x < 0 || p->tile_y < 0 ||
+        p->tile_x + p->tile_w > s->cam.film_w || p->tile_y + p->tile_h > s->cam.film_h) {
+        g_err = "tile rectangle outside the film";
+        return MTSG_ERR_INVALID;
+    }
+    if (p->tile_stride < 0 || (p->tile_stride > 1 && (p->tile_offset < 0 || p->tile_offset >= p->tile_stride))) {
+        g_err = "invalid tile_stride / tile_offset";
+        return MTSG_ERR_INVALID;
+    }
+    return MTSG_OK;
+}
+
+int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
+    int rc;
+    if ((rc = validate(p, s)) != MTSG_OK) return rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    auto t0 = std::chrono::steady_clock::now();
+    const uint32_t maxPaths = s->requestedBatch ? s->requestedBatch : (1u << 22);
+    const uint32_t tilesX = (uint32_t)(p->tile_w + TILE - 1) / TILE, tilesY = (uint32_t)(p->tile_h + TILE - 1) / TILE;
+    const uint32_t allTiles = tilesX * tilesY;
+    const uint32_t tstride = p->tile_stride > 1 ? (uint32_t)p->tile_stride : 1u;
+    const uint32_t toffset = p->tile_stride > 1 ? (uint32_t)p->tile_offset : 0u;
+    const uint32_t ntiles = toffset < allTiles ? (allTiles - toffset + tstride - 1) / tstride : 0u;
+    const uint32_t sppPerBatch = std::max(1u, std::min(p->spp, maxPaths / (TILE * TILE)));
+    const uint32_t tilesPerBatch = std::max(1u, maxPaths / (TILE * TILE * sppPerBatch));
+    if ((rc = ensure_batch(s, tilesPerBatch * sppPerBatch * TILE * TILE)) != MTSG_OK) return rc;
+    const int blockW = p->tile_w + 2 * s->cam.border, blockH = p->tile_h + 2 * s->cam.border;
+    DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed};
+    memset(&s->stats, 0, sizeof(s->stats));
+    s->evUsed = 0;
+    s->timed.clear();
+    s->cancel.store(0);
+    const bool count = (s->flags & MTSG_FLAG_COUNT) != 0;
+    if (count) HIP_TRY(hipMemsetAsync(s->P.ctr, 0, 8 * sizeof(unsigned long long), s->stream));
+    DevPaths &P = s->P;
+    hipEvent_t cntEv[2];
+    HIP_TRY(hipEventCreateWithFlags(&cntEv[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&cntEv[1], hipEventDisableTiming));
+    int result = MTSG_OK;
+    for (uint32_t t0i = 0; t0i < ntiles && result == MTSG_OK; t0i += tilesPerBatch) {
+        for (uint32_t s0 = 0; s0 < p->spp; s0 += sppPerBatch) {
+            if (s->cancel.load()) { result = MTSG_ERR_CANCELLED; g_err = "cancelled"; break; }
+            DevBatch B;
+            B.rect_x = p->tile_x; B.rect_y = p->tile_y; B.rect_w = p->tile_w; B.rect_h = p->tile_h;
+            B.tiles_x = (int)tilesX;
+            B.tile0 = (int)t0i;
+            B.tstride = (int)tstride;
+            B.toffset = (int)toffset;
+            B.ntiles = (int)std::min(tilesPerBatch, ntiles - t0i);
+            B.s0 = s0;
+            B.ns = std::min(sppPerBatch, p->spp - s0);
+            B.nslots = (uint32_t)B.ntiles * B.ns * TILE * TILE;
+            HIP_TRY(hipMemsetAsync(P.cnt, 0, 64 * sizeof(uint32_t), s->stream));
+            timed_launch(s, K_CAMERA, [&]() {
+                hipLaunchKernelGGL(k_camera, dim3((B.nslots + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s->stream, s->cam, I, B, P);
+            });
+            int cur = 0;
+            const int maxBounces = p->max_depth > 0 ? p->max_depth : 1 << 30;
+            int last = -1;
+            auto account = [&](int bb) {
+                // hostCnt slot of bounce bb: [consumed queue, produced queue, shadow]
+                const uint32_t *hc = s->hostCnt + 4 * (bb & 1);
+                const int c = bb & 1;   // queue index consumed by bounce bb
+                s->stats.rays_closest += hc[c];
+                s->stats.rays_shadow += hc[2];
+                s->stats.launches_trace_closest++;
+                return hc[c ^ 1];
+            };
+            for (int b = 0; b < maxBounces; ++b) {
+                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, cur ^ 1, cur);
+                timed_launch(s, K_CLOSEST, [&]() {
+                    if (count)
+                        hipLaunchKernelGGL(k_trace_closest<true>, dim3(s->traceGrid), dim3(TRACE_BLOCK), 0, s->stream, s->ds, P, cur, cur);
+                    else
+                        hipLaunchKernelGGL(k_trace_closest<false>, dim3(s->traceGrid), dim3(TRACE_BLOCK), 0, s->stream, s->ds, P, cur, cur);
+                });
+                timed_launch(s, K_SHADE, [&]() {
+                    hipLaunchKernelGGL(k_shade, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, P, b, cur, cur, s->cam.has_alpha);
+                });
+                timed_launch(s, K_SHADOW, [&]() {
+                    if (count)
+                        hipLaunchKernelGGL(k_trace_shadow<true>, dim3(s->traceGrid), dim3(TRACE_BLOCK), 0, s->stream, s->ds, P);
+                    else
+                        hipLaunchKernelGGL(k_trace_shadow<false>, dim3(s->traceGrid), dim3(TRACE_BLOCK), 0, s->stream, s->ds, P);
+                });
+                HIP_TRY(hipMemcpyAsync(s->hostCnt + 4 * (b & 1), P.cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(hipEventRecord(cntEv[b & 1], s->stream));
+                cur ^= 1;
+                last = b;
+                if (b >= 1) {
+                    // lagged check: if bounce b-1 produced nothing, bounce b was empty
+                    HIP_TRY(hipEventSynchronize(cntEv[(b - 1) & 1]));
+                    if (account(b - 1) == 0) break;
+                }
+            }
+            if (last >= 0) {
+                HIP_TRY(hipEventSynchronize(cntEv[last & 1]));
+                account(last);
+            }
+            timed_launch(s, K_SPLAT, [&]() {
+                hipLaunchKernelGGL(k_splat, dim3(B.ntiles), dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
+            });
+            s->stats.samples += (uint64_t)B.nslots;
+        }
+    }
+    hipError_t e = hipStreamSynchronize(s->stream);
+    hipEventDestroy(cntEv[0]);
+    hipEventDestroy(cntEv[1]);
+    if (e != hipSuccess) { g_err = std::string("render: ") + hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    e = hipGetLastError();
+    if (e != hipSuccess) { g_err = std::string("kernel launch: ") + hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    if (result != MTSG_OK) return result;
+    // samples actually inside the rectangle (all tiles of this call)
+    if (tstride == 1) s->stats.samples = (uint64_t)p->tile_w * p->tile_h * p->spp;
+    if (s->flags & MTSG_FLAG_TIMING) {
+        for (auto &te : s->timed) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, s->evPool[te.second], s->evPool[te.second + 1]);
+            switch (te.first) {
+                case K_CAMERA: s->stats.ms_camera += ms; break;
+                case K_CLOSEST: s->stats.ms_trace_closest += ms; break;
+                case K_SHADOW: s->stats.ms_trace_shadow += ms; break;
+                case K_SHADE: s->stats.ms_shade += ms; break;
+                case K_SPLAT: s->stats.ms_splat += ms; break;
+            }
+        }
+    }
+    if (count) {
+        unsigned long long c[6];
+        HIP_TRY(hipMemcpy(c, P.ctr, sizeof(c), hipMemcpyDeviceToHost));
+        s->stats.nodes_visited = c[0];
+        s->stats.leaf_refs = c[1];
+        s->stats.tri_tests = c[2];
+        s->stats.shadow_nodes_visited = c[3];
+        s->stats.shadow_leaf_refs = c[4];
+        s->stats.shadow_tri_tests = c[5];
+    }
+    s->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return MTSG_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int mtsg_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int gfx950 = 0;
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, i) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0) ++gfx950;
+    }
+    return gfx950;
+}
+
+int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
+    if (!d || !out) { g_err = "null argument"; return MTSG_ERR_INVALID; }
+    *out = nullptr;
+    if (d->abi_version != MTSG_ABI_VERSION) { g_err = "ABI version mismatch"; return MTSG_ERR_INVALID; }
+    if (d->n_prims != d->n_triangles + d->n_rects || d->n_nodes == 0 || d->n_emitters == 0) {
+        g_err = "inconsistent scene description";
+        return MTSG_ERR_INVALID;
+    }
+    if (d->camera.border > MAX_BORDER) { g_err = "reconstruction filter radius too large (border > 4)"; return MTSG_ERR_INVALID; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        g_err = "no such HIP device";
+        return MTSG_ERR_NODEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        g_err = std::string("device is not gfx950: ") + prop.gcnArchName;
+        return MTSG_ERR_NODEVICE;
+    }
+    auto *s = new mtsg_scene();
+    s->device = device;
+    auto fail = [&](int rc) { mtsg_scene_destroy(s); return rc; };
+    if (hipSetDevice(device) != hipSuccess) { g_err = "hipSetDevice failed"; delete s; return MTSG_ERR_DEVICE; }
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) { g_err = "stream"; delete s; return MTSG_ERR_DEVICE; }
+    s->cuCount = prop.multiProcessorCount;
+    // ---- convert + upload (host-side SoA -> device layout)
+    std::vector<float4> vpos(d->n_vertices), vnrm(d->n_vertices);
+    for (uint32_t i = 0; i < d->n_vertices; ++i) {
+        vpos[i] = make_float4(d->vtx_pos[3 * i], d->vtx_pos[3 * i + 1], d->vtx_pos[3 * i + 2], 0.f);
+        vnrm[i] = make_float4(d->vtx_nrm[3 * i], d->vtx_nrm[3 * i + 1], d->vtx_nrm[3 * i + 2], 0.f);
+    }
+    std::vector<uint4> tidx(d->n_triangles);
+    std::vector<float4> tdpdu(d->n_triangles);
+    for (uint32_t t = 0; t < d->n_triangles; ++t) {
+        tidx[t] = make_uint4(d->tri_idx[3 * t], d->tri_idx[3 * t + 1], d->tri_idx[3 * t + 2], 0);
+        tdpdu[t] = make_float4(d->tri_dpdu[3 * t], d->tri_dpdu[3 * t + 1], d->tri_dpdu[3 * t + 2], 0.f);
+    }
+    for (uint32_t sh = 0; sh < d->n_shapes; ++sh)
+        if (d->shapes[sh].type == MTSG_SHAPE_MESH)
+            for (uint32_t t = 0; t < d->shapes[sh].tri_count; ++t) tidx[d->shapes[sh].tri_begin + t].w = sh;
+    int rc;
+    DevScene &ds = s->ds;
+    auto up = [&](auto *src, size_t n, auto **dst) {
+        int r = upload(src, n, dst);
+        if (r == MTSG_OK && *dst) s->allocs.push_back((void *)*dst);
+        return r;
+    };
+    uint2 *nodes; uint32_t *indices; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu; uint4 *dtidx;
+    mtsg_rect *rects; mtsg_shape *shapes; mtsg_bsdf *bsdfs; mtsg_emitter *emitters; float *ecdf, *etcdf;
+    if ((rc = up((const uint2 *)d->nodes, d->n_nodes, &nodes)) ||
+        (rc = up(d->indices, d->n_indices, &indices)) ||
+        (rc = up((const float4 *)d->triaccel, (size_t)d->n_prims * 3, &tri)) ||
+        (rc = up(vpos.data(), vpos.size(), &dvpos)) || (rc = up(vnrm.data(), vnrm.size(), &dvnrm)) ||
+        (rc = up(tidx.data(), tidx.size(), &dtidx)) || (rc = up(tdpdu.data(), tdpdu.size(), &dtdpdu)) ||
+        (rc = up(d->rects, d->n_rects, &rects)) || (rc = up(d->shapes, d->n_shapes, &shapes)) ||
+        (rc = up(d->bsdfs, d->n_bsdfs, &bsdfs)) || (rc = up(d->emitters, d->n_emitters, &emitters)) ||
+        (rc = up(d->emitter_cdf, d->n_emitters + 1, &ecdf)) ||
+        (rc = up(d->emitter_tri_cdf, d->n_emitter_tri_cdf, &etcdf)))
+        return fail(rc);
+    ds.nodes = nodes; ds.indices = indices; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
+    ds.tidx = dtidx; ds.tdpdu = dtdpdu; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
+    ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
+    ds.n_emitters = d->n_emitters;
+    ds.n_tri = d->n_triangles;
+    for (int k = 0; k < 3; ++k) { ds.bmin[k] = d->aabb_min[k]; ds.bmax[k] = d->aabb_max[k]; }
+    DevCamera &c = s->cam;
+    const mtsg_camera &hc = d->camera;
+    memcpy(c.s2c, hc.sample_to_camera, sizeof(c.s2c));
+    memcpy(c.c2w, hc.camera_to_world, sizeof(c.c2w));
+    c.near_clip = hc.near_clip; c.far_clip = hc.far_clip; c.inv_res_x = hc.inv_res_x; c.inv_res_y = hc.inv_res_y;
+    c.film_w = hc.film_w; c.film_h = hc.film_h;
+    c.filter_radius = hc.filter_radius; c.filter_scale = hc.filter_scale; c.border = hc.border;
+    c.has_alpha = hc.has_alpha;
+    memcpy(c.filter_values, hc.filter_values, sizeof(c.filter_values));
+    // persistent grids from the occupancy query
+    int perCU = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace_closest<false>, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
+        perCU = 8;
+    s->traceGrid = s->cuCount * perCU;
+    s->shadeGrid = s->cuCount * 8;
+    if (hipHostMalloc((void **)&s->hostCnt, 16 * sizeof(uint32_t)) != hipSuccess) { g_err = "pinned alloc"; return fail(MTSG_ERR_OOM); }
+    *out = s;
+    return MTSG_OK;
+}
+
+int mtsg_set_batch_paths(mtsg_scene *s, uint32_t paths) {
+    if (!s || paths < TILE * TILE) { g_err = "batch must hold at least 256 paths"; return MTSG_ERR_INVALID; }
+    s->requestedBatch = paths;
+    return MTSG_OK;
+}
+
+int mtsg_set_flags(mtsg_scene *s, uint32_t flags) {
+    if (!s) return MTSG_ERR_INVALID;
+    s->flags = flags;
+    return MTSG_OK;
+}
+
+int mtsg_get_stats(mtsg_scene *s, mtsg_stats *out) {
+    if (!s || !out) return MTSG_ERR_INVALID;
+    *out = s->stats;
+    return MTSG_OK;
+}
+
+void mtsg_cancel(mtsg_scene *s) {
+    if (s) s->cancel.store(1);
+}
+
+int mtsg_device_alloc(mtsg_scene *s, size_t bytes, void **out) {
+    if (!s || !out) return MTSG_ERR_INVALID;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    HIP_TRY(hipMalloc(out, bytes));
+    return MTSG_OK;
+}
+int mtsg_device_free(mtsg_scene *s, void *ptr) {
+    if (!s) return MTSG_ERR_INVALID;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    HIP_TRY(hipFree(ptr));
+    return MTSG_OK;
+}
+int mtsg_device_memset(mtsg_scene *s, void *ptr, size_t bytes) {
+    if (!s) return MTSG_ERR_INVALID;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    HIP_TRY(hipMemsetAsync(ptr, 0, bytes, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return MTSG_OK;
+}
+int mtsg_device_to_host(mtsg_scene *s, void *dst, const void *src, size_t bytes) {
+    if (!s) return MTSG_ERR_INVALID;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return MTSG_OK;
+}
+
+int mtsg_render_device(mtsg_scene *s, const mtsg_render_params *p, float *film) {
+    if (!s || !film) { g_err = "null argument"; return MTSG_ERR_INVALID; }
+    return render_impl(s, p, film);
+}
+
+int mtsg_render(mtsg_scene *s, const mtsg_render_params *p, float *rgbaw_out) {
+    if (!s || !rgbaw_out) { g_err = "null argument"; return MTSG_ERR_INVALID; }
+    int rc;
+    if ((rc = validate(p, s)) != MTSG_OK) return rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    const size_t bytes = (size_t)(p->tile_w + 2 * s->cam.border) * (p->tile_h + 2 * s->cam.border) * 5 * sizeof(float);
+    float *film = nullptr;
+    HIP_TRY(hipMalloc((void **)&film, bytes));
+    hipError_t e = hipMemsetAsync(film, 0, bytes, s->stream);
+    if (e != hipSuccess) { hipFree(film); g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    rc = render_impl(s, p, film);
+    if (rc == MTSG_OK) {
+        e = hipMemcpy(rgbaw_out, film, bytes, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) { g_err = hipGetErrorString(e); rc = MTSG_ERR_DEVICE; }
+    }
+    hipFree(film);
+    return rc;
+}
+
+static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, float *u, float *v, uint32_t *prim,
+                      uint8_t *occ, bool shadow) {
+    if (!s || (!rays && n)) return MTSG_ERR_INVALID;
+    if (n == 0) return MTSG_OK;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    float *dr = nullptr, *dt = nullptr, *du = nullptr, *dv = nullptr;
+    uint32_t *dp = nullptr;
+    uint8_t *docc = nullptr;
+    auto cleanup = [&]() { hipFree(dr); hipFree(dt); hipFree(du); hipFree(dv); hipFree(dp); hipFree(docc); };
+    hipError_t e = hipMalloc((void **)&dr, (size_t)n * 8 * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !shadow) e = hipMalloc((void **)&dt, n * sizeof(float));
+    if (e == hipSuccess && !shadow) e = hipMalloc((void **)&du, n * sizeof(float));
+    if (e == hipSuccess && !shadow) e = hipMalloc((void **)&dv, n * sizeof(float));
+    if (e == hipSuccess && !shadow) e = hipMalloc((void **)&dp, n * sizeof(uint32_t));
+    if (e == hipSuccess && shadow) e = hipMalloc((void **)&docc, n);
+    if (e != hipSuccess) { g_err = hipGetErrorString(e); cleanup(); return MTSG_ERR_DEVICE; }
+    dim3 grid((n + TRACE_BLOCK - 1) / TRACE_BLOCK);
+    if (shadow) hipLaunchKernelGGL(k_trace_rays<true>, grid, dim3(TRACE_BLOCK), 0, s->stream, s->ds, dr, n, dt, du, dv, dp, docc);
+    else hipLaunchKernelGGL(k_trace_rays<false>, grid, dim3(TRACE_BLOCK), 0, s->stream, s->ds, dr, n, dt, du, dv, dp, docc);
+    e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) {
+        if (shadow) e = hipMemcpy(occ, docc, n, hipMemcpyDeviceToHost);
+        else {
+            e = hipMemcpy(t, dt, n * sizeof(float), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(u, du, n * sizeof(float), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(v, dv, n * sizeof(float), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(prim, dp, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+        }
+    }
+    cleanup();
+    if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    return MTSG_OK;
+}
+
+int mtsg_trace_closest(mtsg_scene *s, uint32_t n, const float *rays, float *t, float *u, float *v, uint32_t *prim) {
+    return trace_rays(s, n, rays, t, u, v, prim, nullptr, false);
+}
+
+int mtsg_trace_shadow(mtsg_scene *s, uint32_t n, const float *rays, uint8_t *occluded) {
+    return trace_rays(s, n, rays, nullptr, nullptr, nullptr, nullptr, occluded, true);
+}
+
+void mtsg_scene_destroy(mtsg_scene *s) {
+    if (!s) return;
+    hipSetDevice(s->device);
+    if (s->stream) hipStreamSynchronize(s->stream);
+    free_batch(s);
+    for (void *p : s->allocs) hipFree(p);
+    for (hipEvent_t e : s->evPool) hipEventDestroy(e);
+    if (s->hostCnt) hipHostFree(s->hostCnt);
+    if (s->stream) hipStreamDestroy(s->stream);
+    delete s;
+}
+
+void mtsg_last_error(char *buf, size_t size) {
+    if (!buf || !size) return;
+    strncpy(buf, g_err.c_str(), size - 1);
+    buf[size - 1] = 0;
+}
+
+}  // extern "C"

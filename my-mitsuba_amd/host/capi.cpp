@@ -1,0 +1,105 @@
+// extern "C" surface of the host-side scene library (include/mtsh.h).
+#include <cstring>
+#include <string>
+
+#include "../../include/mtsh.h"
+#include "scene.h"
+
+struct mtsh_scene {
+    std::unique_ptr<mtsh::Scene> scene;
+};
+
+namespace {
+thread_local std::string g_err;
+}
+
+extern "C" {
+
+void mtsh_set_kd_threads(int threads) { mtsh::g_defaultKDThreads = threads; }
+
+mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_defines) {
+    try {
+        std::map<std::string, std::string> defs;
+        for (int i = 0; i < n_defines; ++i) {
+            std::string d = defines[i];
+            size_t eq = d.find('=');
+            if (eq == std::string::npos) throw std::runtime_error("define must be name=value: " + d);
+            defs[d.substr(0, eq)] = d.substr(eq + 1);
+        }
+        auto s = std::make_unique<mtsh_scene>();
+        s->scene = mtsh::loadScene(path, defs);
+        return s.release();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+const mtsg_scene_desc *mtsh_scene_desc(const mtsh_scene *s) { return &s->scene->desc; }
+
+void mtsh_scene_render_params(const mtsh_scene *s, mtsg_render_params *p) {
+    memset(p, 0, sizeof(*p));
+    const mtsh::Scene &sc = *s->scene;
+    p->max_depth = sc.integrator.maxDepth;
+    p->rr_depth = sc.integrator.rrDepth;
+    p->strict_normals = sc.integrator.strictNormals;
+    p->hide_emitters = sc.integrator.hideEmitters;
+    p->spp = (uint32_t)sc.sampleCount;
+    p->seed = 0;
+    p->tile_x = sc.film.cropX;
+    p->tile_y = sc.film.cropY;
+    p->tile_w = sc.film.cropW;
+    p->tile_h = sc.film.cropH;
+    p->tile_stride = 1;
+    p->tile_offset = 0;
+}
+
+void mtsh_scene_get_info(const mtsh_scene *s, mtsh_scene_info *out) {
+    const mtsh::Scene &sc = *s->scene;
+    memset(out, 0, sizeof(*out));
+    out->n_triangles = sc.desc.n_triangles;
+    out->n_rects = sc.desc.n_rects;
+    out->n_shapes = sc.desc.n_shapes;
+    out->n_emitters = sc.desc.n_emitters;
+    out->n_bsdfs = sc.desc.n_bsdfs;
+    out->kd_nodes = sc.desc.n_nodes;
+    out->kd_indices = sc.desc.n_indices;
+    out->kd_max_depth = sc.tree.maxDepth;
+    out->kd_leaves = (uint32_t)sc.tree.leafCount;
+    out->kd_nonempty_leaves = (uint32_t)sc.tree.nonEmptyLeaves;
+    out->kd_build_seconds = sc.tree.buildSeconds;
+    out->film_w = sc.film.width;
+    out->film_h = sc.film.height;
+    out->spp = sc.sampleCount;
+    out->border = sc.camera.border;
+    out->max_depth = sc.integrator.maxDepth;
+}
+
+void mtsh_scene_free(mtsh_scene *s) { delete s; }
+
+void mtsh_develop(const float *rgbaw, int w, int h, float *rgb) {
+    for (size_t i = 0; i < (size_t)w * h; ++i) {
+        float wt = rgbaw[5 * i + 4];
+        float inv = wt != 0 ? 1.0f / wt : 0.0f;
+        for (int k = 0; k < 3; ++k) rgb[3 * i + k] = rgbaw[5 * i + k] * inv;
+    }
+}
+
+int mtsh_write_pfm(const char *path, int w, int h, const float *rgb) {
+    try {
+        std::vector<float> v(rgb, rgb + (size_t)w * h * 3);
+        mtsh::writePFM(path, w, h, v);
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+void mtsh_last_error(char *buf, size_t size) {
+    if (!size) return;
+    strncpy(buf, g_err.c_str(), size - 1);
+    buf[size - 1] = 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1041 @@
+// Mitsuba 0.5/0.6 XML scene loading for the `path` hot path.
+//
+// Mirrors the SceneHandler semantics the configs need
+// (reference src/librender/scenehandler.cpp:70-106 tag table, :461-625
+// value tags, :700-780 object creation) and the shape/BSDF/emitter plugin
+// constructors' parameter parsing:
+//   shapes  ply (src/shapes/ply.cpp), obj (src/shapes/obj.cpp),
+//           rectangle (src/shapes/rectangle.cpp), cube (src/shapes/cube.cpp),
+//           shapegroup/instance (src/shapes/shapegroup.cpp, instance.cpp;
+//           flattened into world-space meshes here)
+//   bsdfs   diffuse (diffuse.cpp:75-84), roughconductor
+//           (roughconductor.cpp:168-203, microfacet.h:99-146),
+//           dielectric (dielectric.cpp:148-170)
+//   emitter area (area.cpp:67-78)
+//   sensor  perspective (perspective.cpp, sensor.cpp:150-262)
+//   film    hdrfilm (hdrfilm.cpp:209-220), rfilter gaussian/box
+//   sampler independent (independent.cpp:55-58)
+//   integrator path (integrator.cpp:199-234)
+#include <algorithm>
+#include <cctype>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <sstream>
+
+#include "scene.h"
+
+namespace mtsh {
+
+// ---------------------------------------------------------------------------
+// Properties
+// ---------------------------------------------------------------------------
+static std::runtime_error err(const std::string &m) { return std::runtime_error(m); }
+
+float Properties::getFloat(const std::string &n, float def) const {
+    auto it = floats.find(n);
+    if (it != floats.end()) return it->second;
+    auto ii = ints.find(n);
+    if (ii != ints.end()) return (float)ii->second;
+    return def;
+}
+float Properties::getFloat(const std::string &n) const {
+    if (!floats.count(n) && !ints.count(n)) throw err("Property \"" + n + "\" has not been specified!");
+    return getFloat(n, 0.0f);
+}
+long long Properties::getInt(const std::string &n, long long def) const {
+    auto it = ints.find(n);
+    return it != ints.end() ? it->second : def;
+}
+bool Properties::getBool(const std::string &n, bool def) const {
+    auto it = bools.find(n);
+    return it != bools.end() ? it->second : def;
+}
+std::string Properties::getString(const std::string &n, const std::string &def) const {
+    auto it = strings.find(n);
+    return it != strings.end() ? it->second : def;
+}
+V3 Properties::getSpectrum(const std::string &n, const V3 &def) const {
+    auto it = spectra.find(n);
+    if (it != spectra.end()) return it->second;
+    auto f = floats.find(n);
+    if (f != floats.end()) return V3(f->second);
+    return def;
+}
+Transform Properties::getTransform(const std::string &n, const Transform &def) const {
+    auto it = transforms.find(n);
+    return it != transforms.end() ? it->second : def;
+}
+
+// ---------------------------------------------------------------------------
+// Minimal XML DOM
+// ---------------------------------------------------------------------------
+struct XNode {
+    std::string tag;
+    std::vector<std::pair<std::string, std::string>> attrs;
+    std::vector<std::unique_ptr<XNode>> children;
+    int line = 0;
+    bool hasAttr(const std::string &k) const {
+        for (auto &a : attrs) if (a.first == k) return true;
+        return false;
+    }
+    std::string attr(const std::string &k, const std::string &def = "") const {
+        for (auto &a : attrs) if (a.first == k) return a.second;
+        return def;
+    }
+};
+
+namespace {
+struct XParser {
+    const std::string &s;
+    size_t i = 0;
+    int line = 1;
+    std::string file;
+    explicit XParser(const std::string &src, const std::string &f) : s(src), file(f) {}
+    [[noreturn]] void fail(const std::string &m) {
+        throw err(file + ":" + std::to_string(line) + ": XML parse error: " + m);
+    }
+    void adv(size_t n = 1) {
+        for (size_t k = 0; k < n && i < s.size(); ++k, ++i)
+            if (s[i] == '\n') ++line;
+    }
+    bool starts(const char *p) const { return s.compare(i, strlen(p), p) == 0; }
+    void ws() { while (i < s.size() && isspace((unsigned char)s[i])) adv(); }
+    void skipMisc() {
+        for (;;) {
+            ws();
+            if (starts("<!--")) {
+                size_t e = s.find("-->", i);
+                if (e == std::string::npos) fail("unterminated comment");
+                adv(e + 3 - i);
+            } else if (starts("<?")) {
+                size_t e = s.find("?>", i);
+                if (e == std::string::npos) fail("unterminated declaration");
+                adv(e + 2 - i);
+            } else if (starts("<!")) {
+                size_t e = s.find('>', i);
+                if (e == std::string::npos) fail("unterminated doctype");
+                adv(e + 1 - i);
+            } else {
+                return;
+            }
+        }
+    }
+    static std::string unescape(const std::string &v) {
+        std::string o;
+        for (size_t k = 0; k < v.size(); ++k) {
+            if (v[k] == '&') {
+                size_t e = v.find(';', k);
+                std::string ent = v.substr(k + 1, e - k - 1);
+                if (ent == "lt") o += '<';
+                else if (ent == "gt") o += '>';
+                else if (ent == "amp") o += '&';
+                else if (ent == "quot") o += '"';
+                else if (ent == "apos") o += '\'';
+                else o += "&" + ent + ";";
+                k = e;
+            } else {
+                o += v[k];
+            }
+        }
+        return o;
+    }
+    std::string name() {
+        size_t b = i;
+        while (i < s.size() && (isalnum((unsigned char)s[i]) || s[i] == '_' || s[i] == '-' || s[i] == ':' || s[i] == '.')) adv();
+        if (b == i) fail("expected a name");
+        return s.substr(b, i - b);
+    }
+    std::unique_ptr<XNode> element() {
+        skipMisc();
+        if (i >= s.size() || s[i] != '<') fail("expected '<'");
+        adv();
+        auto node = std::make_unique<XNode>();
+        node->line = line;
+        node->tag = name();
+        for (;;) {
+            ws();
+            if (starts("/>")) { adv(2); return node; }
+            if (starts(">")) { adv(); break; }
+            std::string k = name();
+            ws();
+            if (i >= s.size() || s[i] != '=') fail("expected '=' after attribute " + k);
+            adv(); ws();
+            char q = s[i];
+            if (q != '"' && q != '\'') fail("expected quoted attribute value");
+            adv();
+            size_t e = s.find(q, i);
+            if (e == std::string::npos) fail("unterminated attribute value");
+            std::string v = unescape(s.substr(i, e - i));
+            adv(e + 1 - i);
+            node->attrs.emplace_back(k, v);
+        }
+        for (;;) {
+            // skip text content
+            while (i < s.size() && s[i] != '<') adv();
+            if (starts("<!--")) { skipMisc(); continue; }
+            if (starts("</")) {
+                adv(2);
+                std::string n = name();
+                if (n != node->tag) fail("mismatched </" + n + "> for <" + node->tag + ">");
+                ws();
+                if (s[i] != '>') fail("expected '>'");
+                adv();
+                return node;
+            }
+            if (i >= s.size()) fail("unexpected end of file inside <" + node->tag + ">");
+            node->children.push_back(element());
+        }
+    }
+};
+
+std::string readFile(const std::string &path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw err("Unable to open \"" + path + "\"");
+    std::stringstream ss;
+    ss << f.rdbuf();
+    return ss.str();
+}
+
+std::string dirName(const std::string &p) {
+    size_t k = p.find_last_of('/');
+    return k == std::string::npos ? std::string(".") : p.substr(0, k);
+}
+
+std::string lower(std::string s) {
+    for (auto &c : s) c = (char)tolower((unsigned char)c);
+    return s;
+}
+
+std::vector<std::string> tokenize(const std::string &s, const char *delims) {
+    std::vector<std::string> out;
+    std::string cur;
+    for (char c : s) {
+        if (strchr(delims, c)) {
+            if (!cur.empty()) out.push_back(cur);
+            cur.clear();
+        } else {
+            cur += c;
+        }
+    }
+    if (!cur.empty()) out.push_back(cur);
+    return out;
+}
+
+float parseF(const std::string &v, int line) {
+    char *end = nullptr;
+    std::string t = v;
+    while (!t.empty() && isspace((unsigned char)t.back())) t.pop_back();
+    size_t b = 0;
+    while (b < t.size() && isspace((unsigned char)t[b])) ++b;
+    t = t.substr(b);
+    float f = strtof(t.c_str(), &end);
+    if (t.empty() || *end != '\0') throw err("line " + std::to_string(line) + ": could not parse floating point value \"" + v + "\"");
+    return f;
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Mesh loaders
+// ---------------------------------------------------------------------------
+namespace {
+struct PlyProp {
+    std::string name, type, countType;
+    bool list = false;
+};
+struct PlyElem {
+    std::string name;
+    size_t count = 0;
+    std::vector<PlyProp> props;
+};
+size_t plyTypeSize(const std::string &t) {
+    if (t == "char" || t == "uchar" || t == "int8" || t == "uint8") return 1;
+    if (t == "short" || t == "ushort" || t == "int16" || t == "uint16") return 2;
+    if (t == "int" || t == "uint" || t == "float" || t == "int32" || t == "uint32" || t == "float32") return 4;
+    if (t == "double" || t == "float64") return 8;
+    throw err("PLY: unknown property type " + t);
+}
+double plyRead(const unsigned char *p, const std::string &t, bool swap) {
+    unsigned char b[8];
+    size_t n = plyTypeSize(t);
+    for (size_t k = 0; k < n; ++k) b[k] = swap ? p[n - 1 - k] : p[k];
+    if (t == "char" || t == "int8") return (double)(int8_t)b[0];
+    if (t == "uchar" || t == "uint8") return (double)b[0];
+    if (t == "short" || t == "int16") { int16_t v; memcpy(&v, b, 2); return v; }
+    if (t == "ushort" || t == "uint16") { uint16_t v; memcpy(&v, b, 2); return v; }
+    if (t == "int" || t == "int32") { int32_t v; memcpy(&v, b, 4); return v; }
+    if (t == "uint" || t == "uint32") { uint32_t v; memcpy(&v, b, 4); return v; }
+    if (t == "float" || t == "float32") { float v; memcpy(&v, b, 4); return v; }
+    double v; memcpy(&v, b, 8); return v;
+}
+}  // namespace
+
+void loadPLY(const std::string &path, Mesh &mesh) {
+    std::string data = readFile(path);
+    size_t hdrEnd = data.find("end_header");
+    if (data.compare(0, 3, "ply") != 0 || hdrEnd == std::string::npos)
+        throw err("\"" + path + "\": not a PLY file");
+    size_t bodyStart = data.find('\n', hdrEnd);
+    if (bodyStart == std::string::npos) throw err("PLY: truncated header");
+    ++bodyStart;
+    std::istringstream hs(data.substr(0, hdrEnd));
+    std::string line, format;
+    std::vector<PlyElem> elems;
+    while (std::getline(hs, line)) {
+        auto tok = tokenize(line, " \t\r");
+        if (tok.empty()) continue;
+        if (tok[0] == "format") format = tok.at(1);
+        else if (tok[0] == "element") { PlyElem e; e.name = tok.at(1); e.count = std::stoull(tok.at(2)); elems.push_back(e); }
+        else if (tok[0] == "property") {
+            if (elems.empty()) throw err("PLY: property before element");
+            PlyProp p;
+            if (tok.at(1) == "list") { p.list = true; p.countType = tok.at(2); p.type = tok.at(3); p.name = tok.at(4); }
+            else { p.type = tok.at(1); p.name = tok.at(2); }
+            elems.back().props.push_back(p);
+        }
+    }
+    bool ascii = format == "ascii";
+    bool swap = format == "binary_big_endian";
+    if (!ascii && format != "binary_little_endian" && !swap) throw err("PLY: unknown format " + format);
+
+    const unsigned char *p = (const unsigned char *)data.data() + bodyStart;
+    const unsigned char *end = (const unsigned char *)data.data() + data.size();
+    std::istringstream as(ascii ? data.substr(bodyStart) : std::string());
+
+    bool hasN = false, hasUV = false;
+    for (auto &e : elems) {
+        if (e.name != "vertex") continue;
+        for (auto &pr : e.props) {
+            if (pr.name == "nx") hasN = true;
+            if (pr.name == "u" || pr.name == "s" || pr.name == "texture_u" || pr.name == "texture_s") hasUV = true;
+        }
+    }
+    auto readVal = [&](const std::string &t) -> double {
+        if (ascii) { double v; if (!(as >> v)) throw err("PLY: truncated ascii body"); return v; }
+        size_t n = plyTypeSize(t);
+        if (p + n > end) throw err("PLY: truncated binary body");
+        double v = plyRead(p, t, swap);
+        p += n;
+        return v;
+    };
+    for (auto &e : elems) {
+        if (e.name == "vertex") {
+            mesh.p.resize(e.count);
+            if (hasN) mesh.n.resize(e.count);
+            if (hasUV) mesh.uv.resize(2 * e.count);
+            for (size_t v = 0; v < e.count; ++v) {
+                for (auto &pr : e.props) {
+                    if (pr.list) { size_t c = (size_t)readVal(pr.countType); for (size_t k = 0; k < c; ++k) readVal(pr.type); continue; }
+                    double x = readVal(pr.type);
+                    const std::string &nm = pr.name;
+                    if (nm == "x") mesh.p[v].x = (float)x;
+                    else if (nm == "y") mesh.p[v].y = (float)x;
+                    else if (nm == "z") mesh.p[v].z = (float)x;
+                    else if (nm == "nx") mesh.n[v].x = (float)x;
+                    else if (nm == "ny") mesh.n[v].y = (float)x;
+                    else if (nm == "nz") mesh.n[v].z = (float)x;
+                    else if (nm == "u" || nm == "s" || nm == "texture_u" || nm == "texture_s") mesh.uv[2 * v] = (float)x;
+                    else if (nm == "v" || nm == "t" || nm == "texture_v" || nm == "texture_t") mesh.uv[2 * v + 1] = (float)x;
+                }
+            }
+        } else if (e.name == "face") {
+            mesh.idx.reserve(e.count * 3);
+            for (size_t f = 0; f < e.count; ++f) {
+                for (auto &pr : e.props) {
+                    if (!pr.list) { readVal(pr.type); continue; }
+                    size_t c = (size_t)readVal(pr.countType);
+                    uint32_t ids[4];
+                    if (pr.name != "vertex_indices" && pr.name != "vertex_index") { for (size_t k = 0; k < c; ++k) readVal(pr.type); continue; }
+                    if (c != 3 && c != 4) throw err("Encountered a face with " + std::to_string(c) + " vertices! Only triangle and quad-based PLY meshes are supported for now.");
+                    for (size_t k = 0; k < c; ++k) {
+                        double id = readVal(pr.type);
+                        if (id < 0 || (size_t)id >= mesh.p.size()) throw err("PLY: vertex index out of range");
+                        ids[k] = (uint32_t)id;
+                    }
+                    // ply.cpp:276-289 (quad -> (0,1,2), (3,0,2))
+                    mesh.idx.insert(mesh.idx.end(), {ids[0], ids[1], ids[2]});
+                    if (c == 4) mesh.idx.insert(mesh.idx.end(), {ids[3], ids[0], ids[2]});
+                }
+            }
+        } else {
+            for (size_t r = 0; r < e.count; ++r)
+                for (auto &pr : e.props) {
+                    if (pr.list) { size_t c = (size_t)readVal(pr.countType); for (size_t k = 0; k < c; ++k) readVal(pr.type); }
+                    else readVal(pr.type);
+                }
+        }
+    }
+}
+
+void loadOBJ(const std::string &path, Mesh &mesh, bool flipTexCoords) {
+    // Simplified obj.cpp: all groups collapsed into one mesh, polygon fans
+    // (obj.cpp:309-322), vertices deduplicated by (p, n, uv) (obj.cpp:577-660)
+    std::ifstream f(path);
+    if (!f) throw err("Unable to open \"" + path + "\"");
+    std::vector<V3> P, N;
+    std::vector<std::pair<float, float>> T;
+    struct Key { int p, n, t; bool operator<(const Key &o) const { return std::tie(p, n, t) < std::tie(o.p, o.n, o.t); } };
+    std::map<Key, uint32_t> vmap;
+    std::vector<Key> verts;
+    std::vector<uint32_t> idx;
+    bool anyN = false, anyT = false;
+    std::string line;
+    auto parseIdx = [&](const std::string &tok) {
+        Key k{0, 0, 0};
+        auto parts = std::vector<std::string>();
+        std::string cur;
+        for (char c : tok) { if (c == '/') { parts.push_back(cur); cur.clear(); } else cur += c; }
+        parts.push_back(cur);
+        auto conv = [](const std::string &s, size_t n) -> int {
+            if (s.empty()) return 0;
+            int v = std::stoi(s);
+            return v < 0 ? (int)n + v + 1 : v;
+        };
+        k.p = conv(parts[0], P.size());
+        if (parts.size() > 1) k.t = conv(parts[1], T.size());
+        if (parts.size() > 2) k.n = conv(parts[2], N.size());
+        if (k.n) anyN = true;
+        if (k.t) anyT = true;
+        auto it = vmap.find(k);
+        if (it != vmap.end()) return it->second;
+        uint32_t id = (uint32_t)verts.size();
+        vmap[k] = id;
+        verts.push_back(k);
+        return id;
+    };
+    while (std::getline(f, line)) {
+        std::istringstream iss(line);
+        std::string t;
+        if (!(iss >> t)) continue;
+        if (t == "v") { V3 v; iss >> v.x >> v.y >> v.z; P.push_back(v); }
+        else if (t == "vn") { V3 v; iss >> v.x >> v.y >> v.z; N.push_back(v); }
+        else if (t == "vt") { float u = 0, v = 0; iss >> u >> v; if (flipTexCoords) v = 1 - v; T.emplace_back(u, v); }
+        else if (t == "f") {
+            std::vector<std::string> toks;
+            std::string s;
+            while (iss >> s) toks.push_back(s);
+            if (toks.size() < 3) continue;
+            uint32_t a = parseIdx(toks[0]), b = parseIdx(toks[1]), c = parseIdx(toks[2]);
+            idx.insert(idx.end(), {a, b, c});
+            for (size_t k = 3; k < toks.size(); ++k) {
+                b = c;
+                c = parseIdx(toks[k]);
+                idx.insert(idx.end(), {a, b, c});
+            }
+        }
+    }
+    mesh.p.resize(verts.size());
+    if (anyN) mesh.n.resize(verts.size());
+    if (anyT) mesh.uv.resize(2 * verts.size());
+    for (size_t i = 0; i < verts.size(); ++i) {
+        const Key &k = verts[i];
+        if (k.p <= 0 || (size_t)k.p > P.size()) throw err("OBJ: vertex index out of range");
+        mesh.p[i] = P[k.p - 1];
+        if (anyN) mesh.n[i] = (k.n > 0 && (size_t)k.n <= N.size()) ? N[k.n - 1] : V3(0.0f);
+        if (anyT && k.t > 0 && (size_t)k.t <= T.size()) { mesh.uv[2 * i] = T[k.t - 1].first; mesh.uv[2 * i + 1] = T[k.t - 1].second; }
+    }
+    mesh.idx = std::move(idx);
+}
+
+// trimesh.cpp:608-681
+static float unitAngle(const V3 &u, const V3 &v) {
+    if (dot(u, v) < 0) return (float)M_PI - 2.0f * std::asin(0.5f * length(v + u));
+    return 2.0f * std::asin(0.5f * length(v - u));
+}
+
+void computeNormals(Mesh &mesh, bool flipNormals) {
+    if (mesh.faceNormals) {
+        mesh.n.clear();
+        if (flipNormals)
+            for (size_t i = 0; i < mesh.idx.size(); i += 3) std::swap(mesh.idx[i], mesh.idx[i + 1]);
+        return;
+    }
+    if (!mesh.n.empty()) {
+        if (flipNormals) for (auto &n : mesh.n) n = -n;
+        return;
+    }
+    mesh.n.assign(mesh.p.size(), V3(0.0f));
+    for (size_t t = 0; t < mesh.idx.size(); t += 3) {
+        V3 n(0.0f);
+        for (int i = 0; i < 3; ++i) {
+            const V3 &v0 = mesh.p[mesh.idx[t + i]];
+            const V3 &v1 = mesh.p[mesh.idx[t + (i + 1) % 3]];
+            const V3 &v2 = mesh.p[mesh.idx[t + (i + 2) % 3]];
+            V3 sideA = v1 - v0, sideB = v2 - v0;
+            if (i == 0) {
+                n = cross(sideA, sideB);
+                float len = length(n);
+                if (len == 0) break;
+                n /= len;
+            }
+            float angle = unitAngle(normalize(sideA), normalize(sideB));
+            mesh.n[mesh.idx[t + i]] += n * angle;
+        }
+    }
+    for (auto &n : mesh.n) {
+        float len = length(n);
+        if (flipNormals) len *= -1;
+        if (len != 0) n /= len;
+        else n = V3(1, 0, 0);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// IOR tables
+// ---------------------------------------------------------------------------
+namespace {
+struct ConductorEntry { const char *name; float eta[3]; float k[3]; };
+const ConductorEntry kConductors[] = {
+#include "ior_table.inc"
+};
+// src/bsdfs/ior.h:38-66
+const struct { const char *name; float value; } kIOR[] = {
+    {"vacuum", 1.0f}, {"helium", 1.000036f}, {"hydrogen", 1.000132f}, {"air", 1.000277f},
+    {"carbon dioxide", 1.00045f}, {"water", 1.3330f}, {"acetone", 1.36f}, {"ethanol", 1.361f},
+    {"carbon tetrachloride", 1.461f}, {"glycerol", 1.4729f}, {"benzene", 1.501f},
+    {"silicone oil", 1.52045f}, {"bromine", 1.661f}, {"water ice", 1.31f}, {"fused quartz", 1.458f},
+    {"pyrex", 1.470f}, {"acrylic glass", 1.49f}, {"polypropylene", 1.49f}, {"bk7", 1.5046f},
+    {"sodium chloride", 1.544f}, {"amber", 1.55f}, {"pet", 1.5750f}, {"diamond", 2.419f}};
+}  // namespace
+
+bool lookupConductor(const std::string &name, V3 &eta, V3 &k) {
+    for (auto &c : kConductors)
+        if (name == c.name) { eta = V3(c.eta[0], c.eta[1], c.eta[2]); k = V3(c.k[0], c.k[1], c.k[2]); return true; }
+    return false;
+}
+
+float lookupIOR(const std::string &name) {
+    std::string l = lower(name);
+    for (auto &e : kIOR) if (l == e.name) return e.value;
+    throw err("Unable to find an IOR value for \"" + l + "\"!");
+}
+
+static float lookupIORProp(const Properties &props, const std::string &n, const std::string &def) {
+    if (props.floats.count(n)) return props.floats.at(n);
+    return lookupIOR(props.getString(n, def));
+}
+
+void writePFM(const std::string &path, int w, int h, const std::vector<float> &rgb) {
+    FILE *f = fopen(path.c_str(), "wb");
+    if (!f) throw err("cannot write " + path);
+    fprintf(f, "PF\n%d %d\n-1\n", w, h);
+    // PFM stores rows bottom-to-top (bitmap.cpp:347-398)
+    for (int y = h - 1; y >= 0; --y) fwrite(&rgb[(size_t)y * w * 3], sizeof(float), (size_t)w * 3, f);
+    fclose(f);
+}
+
+// ---------------------------------------------------------------------------
+// Scene handler
+// ---------------------------------------------------------------------------
+namespace {
+
+struct ShapeGroup {
+    std::vector<Mesh> meshes;   // object space
+    std::vector<Rect> rects;
+};
+
+struct Loader {
+    Scene &scene;
+    std::map<std::string, std::string> defines;
+    std::map<std::string, int> bsdfIds;
+    std::map<std::string, ShapeGroup> groups;
+    std::map<std::string, int> namedEmitters;
+    std::vector<std::string> dirStack;
+
+    explicit Loader(Scene &s) : scene(s) {}
+
+    std::string subst(const std::string &v) {
+        // $name substitution from -D / <default> (scenehandler.cpp:211)
+        std::string o;
+        for (size_t k = 0; k < v.size(); ++k) {
+            if (v[k] == '$') {
+                size_t e = k + 1;
+                while (e < v.size() && (isalnum((unsigned char)v[e]) || v[e] == '_')) ++e;
+                std::string key = v.substr(k + 1, e - k - 1);
+                auto it = defines.find(key);
+                if (it == defines.end()) throw err("Unresolved parameter \"$" + key + "\"");
+                o += it->second;
+                k = e - 1;
+            } else {
+                o += v[k];
+            }
+        }
+        return o;
+    }
+
+    void substAll(XNode &n) {
+        for (auto &a : n.attrs) a.second = subst(a.second);
+    }
+
+    std::string resolve(const std::string &f) {
+        if (!f.empty() && f[0] == '/') return f;
+        for (auto it = dirStack.rbegin(); it != dirStack.rend(); ++it) {
+            std::string p = *it + "/" + f;
+            std::ifstream t(p);
+            if (t.good()) return p;
+        }
+        return dirStack.back() + "/" + f;
+    }
+
+    Transform parseTransform(XNode &n) {
+        Transform t;
+        for (auto &cp : n.children) {
+            XNode &c = *cp;
+            substAll(c);
+            const std::string &tag = c.tag;
+            if (tag == "translate") {
+                t = Transform::translate(V3(parseF(c.attr("x", "0"), c.line), parseF(c.attr("y", "0"), c.line), parseF(c.attr("z", "0"), c.line))) * t;
+            } else if (tag == "rotate") {
+                V3 ax(parseF(c.attr("x", "0"), c.line), parseF(c.attr("y", "0"), c.line), parseF(c.attr("z", "0"), c.line));
+                t = Transform::rotate(ax, parseF(c.attr("angle"), c.line)) * t;
+            } else if (tag == "scale") {
+                bool hasXYZ = c.hasAttr("x") || c.hasAttr("y") || c.hasAttr("z");
+                V3 s;
+                if (hasXYZ && c.hasAttr("value")) throw err("<scale>: provided both xyz and value arguments!");
+                if (hasXYZ) s = V3(parseF(c.attr("x", "1"), c.line), parseF(c.attr("y", "1"), c.line), parseF(c.attr("z", "1"), c.line));
+                else if (c.hasAttr("value")) s = V3(parseF(c.attr("value"), c.line));
+                else throw err("<scale>: provided neither xyz nor value arguments!");
+                t = Transform::scale(s) * t;
+            } else if (tag == "lookat" || tag == "lookAt") {
+                auto o = tokenize(c.attr("origin"), ", "), tg = tokenize(c.attr("target"), ", "), up = tokenize(c.attr("up"), ", ");
+                if (o.size() != 3) throw err("<lookat>: invalid 'origin' argument");
+                if (tg.size() != 3) throw err("<lookat>: invalid 'target' argument");
+                V3 O(parseF(o[0], c.line), parseF(o[1], c.line), parseF(o[2], c.line));
+                V3 T(parseF(tg[0], c.line), parseF(tg[1], c.line), parseF(tg[2], c.line));
+                V3 U(0.0f);
+                if (up.size() == 3) U = V3(parseF(up[0], c.line), parseF(up[1], c.line), parseF(up[2], c.line));
+                else if (!up.empty()) throw err("<lookat>: invalid 'up' argument");
+                if (dot(U, U) == 0) { V3 unused; coordinateSystem(normalize(T - O), U, unused); }
+                t = Transform::lookAt(O, T, U) * t;
+            } else if (tag == "matrix") {
+                auto tok = tokenize(c.attr("value"), ", ");
+                if (tok.size() != 16) throw err("Invalid matrix specified");
+                double m[4][4];
+                for (int k = 0; k < 16; ++k) m[k / 4][k % 4] = parseF(tok[k], c.line);
+                t = Transform::fromMatrix(m) * t;
+            } else {
+                throw err("line " + std::to_string(c.line) + ": unsupported transform element <" + tag + ">");
+            }
+        }
+        return t;
+    }
+
+    V3 parseRGB(const std::string &v, int line) {
+        auto tok = tokenize(v, ", ");
+        if (tok.size() == 1 && tok[0].size() == 7 && tok[0][0] == '#') {
+            int enc = (int)strtol(tok[0].c_str() + 1, nullptr, 16);
+            return V3(((enc & 0xFF0000) >> 16) / 255.0f, ((enc & 0x00FF00) >> 8) / 255.0f, (enc & 0xFF) / 255.0f);
+        }
+        if (tok.size() == 1) return V3(parseF(tok[0], line));
+        if (tok.size() == 3) return V3(parseF(tok[0], line), parseF(tok[1], line), parseF(tok[2], line));
+        throw err("Invalid RGB value specified");
+    }
+
+    static float srgbToLinear(float v) {
+        if (v <= 0.04045f) return v * (1.0f / 12.92f);
+        return std::pow((v + 0.055f) * (1.0f / 1.055f), 2.4f);
+    }
+
+    // Parse value children of a plugin element into props; returns nested
+    // plugin elements for the caller.
+    void parseProps(XNode &n, Properties &props, std::vector<XNode *> &nested) {
+        for (auto &cp : n.children) {
+            XNode &c = *cp;
+            substAll(c);
+            const std::string name = c.attr("name");
+            const std::string &tag = c.tag;
+            if (tag == "float") props.floats[name] = parseF(c.attr("value"), c.line);
+            else if (tag == "integer") {
+                long long v = std::stoll(c.attr("value"));
+                props.ints[name] = v;
+            } else if (tag == "boolean") {
+                std::string v = lower(c.attr("value"));
+                if (v != "true" && v != "false") throw err("line " + std::to_string(c.line) + ": could not parse boolean \"" + v + "\"");
+                props.bools[name] = v == "true";
+            } else if (tag == "string") props.strings[name] = c.attr("value");
+            else if (tag == "rgb") props.spectra[name] = parseRGB(c.attr("value"), c.line);
+            else if (tag == "srgb") { V3 v = parseRGB(c.attr("value"), c.line); props.spectra[name] = V3(srgbToLinear(v.x), srgbToLinear(v.y), srgbToLinear(v.z)); }
+            else if (tag == "spectrum") {
+                if (c.hasAttr("filename")) throw err("<spectrum filename=...> is not supported in RGB mode by this loader");
+                auto tok = tokenize(c.attr("value"), ", ");
+                if (tok.size() == 1 && tok[0].find(':') == std::string::npos) {
+                    // RGB mode: reflectance -> constant, illuminant -> D65 * v = v (spectrum.cpp:164)
+                    props.spectra[name] = V3(parseF(tok[0], c.line));
+                } else if (tok.size() == 3 && tok[0].find(':') == std::string::npos) {
+                    props.spectra[name] = V3(parseF(tok[0], c.line), parseF(tok[1], c.line), parseF(tok[2], c.line));
+                } else {
+                    throw err("line " + std::to_string(c.line) + ": wavelength:value spectra are not supported by this loader");
+                }
+            } else if (tag == "point" || tag == "vector") {
+                props.points[name] = V3(parseF(c.attr("x", "0"), c.line), parseF(c.attr("y", "0"), c.line), parseF(c.attr("z", "0"), c.line));
+            } else if (tag == "transform") {
+                props.transforms[name] = parseTransform(c);
+            } else {
+                nested.push_back(&c);
+            }
+        }
+    }
+
+    int parseBsdf(XNode &n) {
+        substAll(n);
+        Properties props;
+        std::vector<XNode *> nested;
+        parseProps(n, props, nested);
+        std::string type = lower(n.attr("type"));
+        Bsdf b;
+        b.id = n.attr("id");
+        mtsg_bsdf &d = b.d;
+        if (type == "diffuse") {
+            // diffuse.cpp:77-84, configure() keeps the component iff max > 0
+            V3 r = props.getSpectrum(props.has("reflectance") ? "reflectance" : "diffuseReflectance", V3(0.5f));
+            float mx = std::max(r.x, std::max(r.y, r.z));
+            if (mx > 1.0f) r = r * (1.0f / mx);   // ensureEnergyConservation (bsdf.cpp)
+            d.type = MTSG_BSDF_DIFFUSE;
+            d.reflectance[0] = r.x; d.reflectance[1] = r.y; d.reflectance[2] = r.z;
+            d.smooth = mx > 0;
+            d.ref_n_zero = 0;
+        } else if (type == "roughconductor") {
+            // roughconductor.cpp:168-203
+            V3 spec = props.getSpectrum("specularReflectance", V3(1.0f));
+            std::string material = props.getString("material", "Cu");
+            V3 intEta, intK;
+            if (lower(material) == "none") { intEta = V3(0.0f); intK = V3(1.0f); }
+            else if (!lookupConductor(material, intEta, intK)) throw err("roughconductor: unknown material \"" + material + "\"");
+            float extEta = lookupIORProp(props, "extEta", "air");
+            V3 eta = props.getSpectrum("eta", intEta) / extEta;
+            V3 k = props.getSpectrum("k", intK) / extEta;
+            // MicrofacetDistribution(props) (microfacet.h:99-146)
+            int distr = MTSG_MF_BECKMANN;
+            if (props.strings.count("distribution")) {
+                std::string dn = lower(props.strings["distribution"]);
+                if (dn == "beckmann") distr = MTSG_MF_BECKMANN;
+                else if (dn == "ggx") distr = MTSG_MF_GGX;
+                else throw err("Specified an invalid distribution \"" + dn + "\" (this build supports beckmann, ggx)");
+            }
+            float au = 0.1f, av = 0.1f;
+            if (props.has("alpha")) {
+                if (props.has("alphaU") || props.has("alphaV")) throw err("Microfacet model: please specify either 'alpha' or 'alphaU'/'alphaV'.");
+                au = av = props.getFloat("alpha");
+            } else if (props.has("alphaU") || props.has("alphaV")) {
+                if (!props.has("alphaU") || !props.has("alphaV")) throw err("Microfacet model: both 'alphaU' and 'alphaV' must be specified.");
+                au = props.getFloat("alphaU"); av = props.getFloat("alphaV");
+            }
+            if (au != av) throw err("roughconductor: anisotropic roughness needs UV tangents, not supported by this build");
+            au = std::max(au, 1e-4f); av = std::max(av, 1e-4f);
+            d.type = MTSG_BSDF_ROUGHCONDUCTOR;
+            d.distribution = distr;
+            d.sample_visible = props.getBool("sampleVisible", true) ? 1 : 0;
+            d.alpha_u = au; d.alpha_v = av;
+            for (int i = 0; i < 3; ++i) { d.eta[i] = eta[i]; d.k[i] = k[i]; d.spec_refl[i] = spec[i]; }
+            d.smooth = 1;
+            d.ref_n_zero = 0;
+        } else if (type == "dielectric") {
+            // dielectric.cpp:148-170
+            float intIOR = lookupIORProp(props, "intIOR", "bk7");
+            float extIOR = lookupIORProp(props, "extIOR", "air");
+            if (intIOR < 0 || extIOR < 0) throw err("The interior and exterior indices of refraction must be positive!");
+            V3 sr = props.getSpectrum("specularReflectance", V3(1.0f));
+            V3 st = props.getSpectrum("specularTransmittance", V3(1.0f));
+            d.type = MTSG_BSDF_DIELECTRIC;
+            d.ior_eta = intIOR / extIOR;
+            d.ior_inv_eta = 1 / d.ior_eta;
+            for (int i = 0; i < 3; ++i) { d.spec_refl[i] = sr[i]; d.spec_trans[i] = st[i]; }
+            d.smooth = 0;        // delta components only
+            d.ref_n_zero = 1;    // ETransmission | EBackSide
+        } else {
+            throw err("line " + std::to_string(n.line) + ": BSDF plugin \"" + type + "\" is outside this build's scope");
+        }
+        scene.bsdfs.push_back(b);
+        int id = (int)scene.bsdfs.size() - 1;
+        if (!b.id.empty()) bsdfIds[b.id] = id;
+        return id;
+    }
+
+    int defaultBsdf(bool emitter) {
+        // Shape::configure (src/librender/shape.cpp:47-70): all-absorbing
+        // diffuse on emitters, 0.5 Lambertian otherwise
+        Bsdf b;
+        float r = emitter ? 0.0f : 0.5f;
+        b.d.type = MTSG_BSDF_DIFFUSE;
+        b.d.reflectance[0] = b.d.reflectance[1] = b.d.reflectance[2] = r;
+        b.d.smooth = r > 0;
+        scene.bsdfs.push_back(b);
+        return (int)scene.bsdfs.size() - 1;
+    }
+
+    int parseEmitter(XNode &n) {
+        substAll(n);
+        Properties props;
+        std::vector<XNode *> nested;
+        parseProps(n, props, nested);
+        std::string type = lower(n.attr("type"));
+        if (type != "area") throw err("line " + std::to_string(n.line) + ": emitter plugin \"" + type + "\" is outside this build's scope");
+        if (props.transforms.count("toWorld")) throw err("Found a 'toWorld' transformation -- this is not allowed -- the area light inherits this transformation from its parent shape");
+        Emitter e;
+        e.radiance = props.getSpectrum("radiance", V3(1.0f));   // D65 == 1 in RGB mode
+        e.samplingWeight = props.getFloat("samplingWeight", 1.0f);
+        scene.emitters.push_back(e);
+        return (int)scene.emitters.size() - 1;
+    }
+
+    // Returns meshes/rects in object->world space given the toWorld transform
+    void parseShape(XNode &n, std::vector<Mesh> &meshes, std::vector<Rect> &rects, bool inGroup) {
+        substAll(n);
+        std::string type = lower(n.attr("type"));
+        if (type == "shapegroup") {
+            ShapeGroup g;
+            for (auto &cp : n.children) {
+                substAll(*cp);
+                if (cp->tag != "shape") throw err("shapegroup may only contain shapes");
+                parseShape(*cp, g.meshes, g.rects, true);
+            }
+            std::string id = n.attr("id");
+            if (id.empty()) throw err("shapegroup needs an id");
+            groups[id] = std::move(g);
+            return;
+        }
+        Properties props;
+        std::vector<XNode *> nested;
+        parseProps(n, props, nested);
+        int bsdf = -1, emitter = -1;
+        std::string instRef;
+        for (XNode *c : nested) {
+            substAll(*c);
+            if (c->tag == "bsdf") bsdf = parseBsdf(*c);
+            else if (c->tag == "emitter") {
+                if (inGroup) throw err("emitters inside shapegroups are not supported");
+                emitter = parseEmitter(*c);
+            } else if (c->tag == "ref") {
+                std::string id = c->attr("id");
+                if (bsdfIds.count(id)) bsdf = bsdfIds[id];
+                else if (groups.count(id)) instRef = id;
+                else throw err("Referenced object '" + id + "' not found!");
+            } else {
+                throw err("line " + std::to_string(c->line) + ": unsupported element <" + c->tag + "> inside <shape>");
+            }
+        }
+        Transform toWorld = props.getTransform("toWorld", Transform());
+        bool flip = props.getBool("flipNormals", false);
+        if (type == "instance") {
+            if (instRef.empty()) throw err("instance: missing <ref> to a shapegroup");
+            const ShapeGroup &g = groups[instRef];
+            for (const Mesh &m0 : g.meshes) {
+                Mesh m = m0;
+                for (auto &p : m.p) p = toWorld.point(p);
+                for (auto &nn : m.n) nn = normalize(toWorld.normal(nn));
+                meshes.push_back(std::move(m));
+            }
+            for (const Rect &r0 : g.rects) {
+                Rect r = r0;
+                r.toWorld = toWorld * r0.toWorld;
+                rects.push_back(r);
+            }
+            return;
+        }
+        if (bsdf < 0) bsdf = defaultBsdf(emitter >= 0);
+        if (type == "rectangle") {
+            Rect r;
+            r.toWorld = toWorld;
+            if (flip) r.toWorld = r.toWorld * Transform::scale(V3(1, 1, -1));
+            r.bsdf = bsdf;
+            r.emitter = emitter;
+            rects.push_back(r);
+            return;
+        }
+        Mesh m;
+        if (type == "ply") {
+            loadPLY(resolve(props.getString("filename", "")), m);
+        } else if (type == "obj") {
+            loadOBJ(resolve(props.getString("filename", "")), m, props.getBool("flipTexCoords", true));
+        } else if (type == "cube") {
+            buildCube(m);
+        } else {
+            throw err("line " + std::to_string(n.line) + ": shape plugin \"" + type + "\" is outside this build's scope");
+        }
+        m.faceNormals = props.getBool("faceNormals", false);
+        for (auto &p : m.p) p = toWorld.point(p);
+        for (auto &nn : m.n) nn = normalize(toWorld.normal(nn));
+        computeNormals(m, flip);
+        m.bsdf = bsdf;
+        m.emitter = emitter;
+        meshes.push_back(std::move(m));
+    }
+
+    static void buildCube(Mesh &m) {
+        // src/shapes/cube.cpp:24-30 data, restated as 6 faces of 4 vertices
+        // with per-face normals and [0,1]^2 texcoords
+        static const float P[24][3] = {
+            {1, -1, -1}, {1, -1, 1}, {-1, -1, 1}, {-1, -1, -1}, {1, 1, -1}, {-1, 1, -1}, {-1, 1, 1}, {1, 1, 1},
+            {1, -1, -1}, {1, 1, -1}, {1, 1, 1}, {1, -1, 1}, {1, -1, 1}, {1, 1, 1}, {-1, 1, 1}, {-1, -1, 1},
+            {-1, -1, 1}, {-1, 1, 1}, {-1, 1, -1}, {-1, -1, -1}, {1, 1, -1}, {1, -1, -1}, {-1, -1, -1}, {-1, 1, -1}};
+        static const float N[24][3] = {
+            {0, -1, 0}, {0, -1, 0}, {0, -1, 0}, {0, -1, 0}, {0, 1, 0}, {0, 1, 0}, {0, 1, 0}, {0, 1, 0},
+            {1, 0, 0}, {1, 0, 0}, {1, 0, 0}, {1, 0, 0}, {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 0, 1},
+            {-1, 0, 0}, {-1, 0, 0}, {-1, 0, 0}, {-1, 0, 0}, {0, 0, -1}, {0, 0, -1}, {0, 0, -1}, {0, 0, -1}};
+        static const float T[24][2] = {
+            {0, 1}, {1, 1}, {1, 0}, {0, 0}, {0, 1}, {1, 1}, {1, 0}, {0, 0}, {0, 1}, {1, 1}, {1, 0}, {0, 0},
+            {0, 1}, {1, 1}, {1, 0}, {0, 0}, {0, 1}, {1, 1}, {1, 0}, {0, 0}, {0, 1}, {1, 1}, {1, 0}, {0, 0}};
+        for (int i = 0; i < 24; ++i) {
+            m.p.emplace_back(P[i][0], P[i][1], P[i][2]);
+            m.n.emplace_back(N[i][0], N[i][1], N[i][2]);
+            m.uv.push_back(T[i][0]);
+            m.uv.push_back(T[i][1]);
+        }
+        for (uint32_t f = 0; f < 6; ++f) {
+            uint32_t b = 4 * f;
+            m.idx.insert(m.idx.end(), {b + 0, b + 1, b + 2, b + 3, b + 0, b + 2});
+        }
+    }
+
+    void parseScene(XNode &root) {
+        for (auto &cp : root.children) {
+            XNode &c = *cp;
+            substAll(c);
+            const std::string &tag = c.tag;
+            if (tag == "default") {
+                std::string name = c.attr("name");
+                if (!defines.count(name)) defines[name] = c.attr("value");
+            } else if (tag == "include") {
+                std::string path = resolve(c.attr("filename"));
+                std::string src = readFile(path);
+                XParser p(src, path);
+                p.skipMisc();
+                auto sub = p.element();
+                dirStack.push_back(dirName(path));
+                parseScene(*sub);
+                dirStack.pop_back();
+            } else if (tag == "integrator") {
+                Properties props;
+                std::vector<XNode *> nested;
+                parseProps(c, props, nested);
+                std::string type = lower(c.attr("type"));
+                if (type != "path") throw err("line " + std::to_string(c.line) + ": integrator \"" + type + "\" is outside this build's scope (only 'path')");
+                IntegratorProps &ip = scene.integrator;
+                ip.type = type;
+                ip.rrDepth = (int)props.getInt("rrDepth", 5);
+                ip.maxDepth = (int)props.getInt("maxDepth", -1);
+                ip.strictNormals = props.getBool("strictNormals", false);
+                ip.hideEmitters = props.getBool("hideEmitters", false);
+                if (ip.rrDepth <= 0) throw err("'rrDepth' must be set to a value greater than zero!");
+                if (ip.maxDepth <= 0 && ip.maxDepth != -1) throw err("'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
+            } else if (tag == "sensor" || tag == "camera") {
+                parseSensor(c);
+            } else if (tag == "bsdf") {
+                parseBsdf(c);
+            } else if (tag == "shape") {
+                std::vector<Mesh> meshes;
+                std::vector<Rect> rects;
+                parseShape(c, meshes, rects, false);
+                addShapes(meshes, rects);
+            } else if (tag == "emitter") {
+                throw err("line " + std::to_string(c.line) + ": emitter \"" + c.attr("type") + "\" outside a shape is outside this build's scope");
+            } else if (tag == "ref") {
+                // scene-level refs are ignored
+            } else {
+                throw err("line " + std::to_string(c.line) + ": unsupported element <" + tag + ">");
+            }
+        }
+    }
+
+    void addShapes(std::vector<Mesh> &meshes, std::vector<Rect> &rects) {
+        for (auto &m : meshes) {
+            scene.meshes.push_back(std::move(m));
+            int si = (int)scene.shapes.size();
+            scene.shapes.push_back({MTSG_SHAPE_MESH, (int)scene.meshes.size() - 1});
+            if (scene.meshes.back().emitter >= 0) scene.emitters[scene.meshes.back().emitter].shape = si;
+        }
+        for (auto &r : rects) {
+            scene.rects.push_back(r);
+            int si = (int)scene.shapes.size();
+            scene.shapes.push_back({MTSG_SHAPE_RECT, (int)scene.rects.size() - 1});
+            if (r.emitter >= 0) scene.emitters[r.emitter].shape = si;
+        }
+    }
+
+    void parseSensor(XNode &c) {
+        Properties props;
+        std::vector<XNode *> nested;
+        parseProps(c, props, nested);
+        std::string type = lower(c.attr("type"));
+        if (type != "perspective") throw err("line " + std::to_string(c.line) + ": sensor \"" + type + "\" is outside this build's scope");
+        Sensor &s = scene.sensor;
+        s.present = true;
+        s.toWorld = props.getTransform("toWorld", Transform());
+        s.nearClip = props.getFloat("nearClip", 1e-2f);
+        s.farClip = props.getFloat("farClip", 1e4f);
+        if (s.nearClip <= 0) throw err("The 'nearClip' parameter must be greater than zero!");
+        if (s.nearClip >= s.farClip) throw err("The 'nearClip' parameter must be smaller than 'farClip'.");
+        if (props.has("fov")) s.fov = props.getFloat("fov");
+        else if (props.strings.count("focalLength")) throw err("focalLength is not supported by this loader; use fov");
+        else s.fov = -1;  // default focal length 50mm handled in finalize
+        s.fovAxis = lower(props.getString("fovAxis", "x"));
+        for (XNode *n : nested) {
+            substAll(*n);
+            if (n->tag == "film") parseFilm(*n);
+            else if (n->tag == "sampler") {
+                Properties sp;
+                std::vector<XNode *> sn;
+                parseProps(*n, sp, sn);
+                std::string st = lower(n->attr("type"));
+                if (st != "independent") throw err("sampler \"" + st + "\" is outside this build's scope (only 'independent')");
+                scene.samplerType = st;
+                scene.sampleCount = (int)sp.getInt("sampleCount", 4);
+            } else {
+                throw err("unsupported element <" + n->tag + "> inside <sensor>");
+            }
+        }
+    }
+
+    void parseFilm(XNode &c) {
+        Properties props;
+        std::vector<XNode *> nested;
+        parseProps(c, props, nested);
+        std::string type = lower(c.attr("type"));
+        if (type != "hdrfilm") throw err("film \"" + type + "\" is outside this build's scope (only 'hdrfilm')");
+        Film &f = scene.film;
+        f.width = (int)props.getInt("width", 768);
+        f.height = (int)props.getInt("height", 576);
+        f.cropX = (int)props.getInt("cropOffsetX", 0);
+        f.cropY = (int)props.getInt("cropOffsetY", 0);
+        f.cropW = (int)props.getInt("cropWidth", f.width);
+        f.cropH = (int)props.getInt("cropHeight", f.height);
+        f.pixelFormat = lower(props.getString("pixelFormat", "rgb"));
+        f.hasAlpha = f.pixelFormat.find('a') != std::string::npos;
+        for (XNode *n : nested) {
+            substAll(*n);
+            if (n->tag != "rfilter") throw err("unsupported element <" + n->tag + "> inside <film>");
+            Properties fp;
+            std::vector<XNode *> fn;
+            parseProps(*n, fp, fn);
+            std::string ft = lower(n->attr("type"));
+            if (ft == "gaussian") { f.filter = ft; f.stddev = fp.getFloat("stddev", 0.5f); }
+            else if (ft == "box") { f.filter = ft; f.boxRadius = fp.getFloat("radius", 0.5f); }
+            else throw err("rfilter \"" + ft + "\" is outside this build's scope");
+        }
+    }
+};
+}  // namespace
+
+int g_defaultKDThreads = 0;
+
+std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::string, std::string> &defines) {
+    auto scene = std::make_unique<Scene>();
+    scene->kd.threads = g_defaultKDThreads;
+    Loader L(*scene);
+    L.defines = defines;
+    L.dirStack.push_back(dirName(path));
+    std::string src = readFile(path);
+    XParser p(src, path);
+    p.skipMisc();
+    auto root = p.element();
+    if (root->tag != "scene") throw err("root element must be <scene>");
+    L.parseScene(*root);
+    if (!scene->sensor.present) throw err("scene has no <sensor>");
+    for (auto &e : scene->emitters)
+        if (e.shape < 0) throw err("area emitter without a parent shape");
+    scene->finalize();
+    return scene;
+}
+
+}  // namespace mtsh

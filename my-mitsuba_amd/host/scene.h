@@ -1,0 +1,171 @@
+// Host-side scene model: the Mitsuba-mirror side of the drop-in boundary.
+// It stands in for the parts of Mitsuba that stay on the CPU in the
+// reference (XML SceneHandler, shape plugins, Scene::initialize, the SAH
+// kd-tree build) and produces the flat mtsg_scene_desc handed to libmtsg.
+#pragma once
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "hmath.h"
+#include "../../include/mtsg.h"
+
+namespace mtsh {
+
+struct Properties {
+    // typed property bag (include/mitsuba/core/properties.h)
+    std::map<std::string, float> floats;
+    std::map<std::string, long long> ints;
+    std::map<std::string, bool> bools;
+    std::map<std::string, std::string> strings;
+    std::map<std::string, V3> spectra;   // RGB mode: 3 samples
+    std::map<std::string, V3> points;
+    std::map<std::string, Transform> transforms;
+    std::map<std::string, bool> queried;
+
+    bool has(const std::string &n) const {
+        return floats.count(n) || ints.count(n) || bools.count(n) || strings.count(n) ||
+               spectra.count(n) || points.count(n) || transforms.count(n);
+    }
+    float getFloat(const std::string &n, float def) const;
+    float getFloat(const std::string &n) const;
+    long long getInt(const std::string &n, long long def) const;
+    bool getBool(const std::string &n, bool def) const;
+    std::string getString(const std::string &n, const std::string &def) const;
+    V3 getSpectrum(const std::string &n, const V3 &def) const;
+    Transform getTransform(const std::string &n, const Transform &def) const;
+};
+
+struct Mesh {
+    std::string name;
+    std::vector<V3> p, n;            // n empty when faceNormals
+    std::vector<float> uv;           // 2 per vertex, may be empty
+    std::vector<uint32_t> idx;       // 3 per triangle
+    bool faceNormals = false;
+    int bsdf = -1, emitter = -1;
+};
+
+struct Rect {
+    Transform toWorld;
+    int bsdf = -1, emitter = -1;
+};
+
+struct Bsdf {
+    mtsg_bsdf d{};
+    std::string id;
+};
+
+struct Emitter {
+    int type = MTSG_EMITTER_AREA;
+    V3 radiance{1, 1, 1};
+    float samplingWeight = 1.0f;
+    int shape = -1;                  // index into Scene::shapes
+};
+
+struct ShapeRef {                    // m_shapes order in the kd-tree
+    int type;                        // MTSG_SHAPE_*
+    int index;                       // into meshes / rects
+};
+
+struct Sensor {
+    Transform toWorld;
+    float fov = -1;
+    std::string fovAxis = "x";
+    float nearClip = 1e-2f, farClip = 1e4f;
+    bool present = false;
+};
+
+struct Film {
+    int width = 768, height = 576;
+    int cropX = 0, cropY = 0, cropW = -1, cropH = -1;
+    std::string filter = "gaussian";
+    float stddev = 0.5f, boxRadius = 0.5f;
+    bool hasAlpha = false;
+    std::string pixelFormat = "rgb";
+};
+
+struct IntegratorProps {
+    std::string type = "path";
+    int maxDepth = -1, rrDepth = 5;
+    bool strictNormals = false, hideEmitters = false;
+};
+
+struct KDBuildParams {                // gkdtree.h:734-744 defaults
+    float traversalCost = 15, queryCost = 20, emptySpaceBonus = 0.9f;
+    int stopPrims = 6, maxBadRefines = 3, minMaxBins = 128;
+    int exactPrimThreshold = 65536;
+    bool clip = true;
+    int maxDepth = 0;                 // 0 = 8 + 1.3 log2(N) (gkdtree.h:986-988)
+    int threads = 0;                  // 0 = hardware concurrency
+};
+
+struct KDTree {
+    std::vector<mtsg_kdnode> nodes;
+    std::vector<uint32_t> indices;
+    AABB aabb;                         // enlarged
+    AABB tightAABB;
+    uint32_t maxDepth = 0;
+    double buildSeconds = 0;
+    double sahCost = 0;
+    size_t leafCount = 0, nonEmptyLeaves = 0;
+};
+
+struct Scene {
+    std::vector<Mesh> meshes;
+    std::vector<Rect> rects;
+    std::vector<ShapeRef> shapes;     // in kd-tree order
+    std::vector<Bsdf> bsdfs;
+    std::vector<Emitter> emitters;
+    Sensor sensor;
+    Film film;
+    IntegratorProps integrator;
+    int sampleCount = 4;
+    std::string samplerType = "independent";
+    KDBuildParams kd;
+
+    // ---- flattened (filled by finalize()) ----
+    std::vector<float> vtxPos, vtxNrm, triDpdu, emitterCdf, emitterTriCdf;
+    std::vector<uint32_t> triIdx;
+    std::vector<mtsg_rect> rectDesc;
+    std::vector<mtsg_shape> shapeDesc;
+    std::vector<mtsg_bsdf> bsdfDesc;
+    std::vector<mtsg_emitter> emitterDesc;
+    std::vector<mtsg_triaccel> triaccel;
+    KDTree tree;
+    mtsg_camera camera{};
+    mtsg_scene_desc desc{};
+
+    void finalize();                  // normals, tangents, CDFs, kd-tree, desc
+};
+
+extern int g_defaultKDThreads;   // 0 = hardware concurrency
+
+// XML loading (src/librender/scenehandler.cpp), `-D name=value` defines
+std::unique_ptr<Scene> loadScene(const std::string &path,
+                                 const std::map<std::string, std::string> &defines);
+
+// Mesh loaders
+void loadPLY(const std::string &path, Mesh &mesh);   // src/shapes/ply.cpp
+void loadOBJ(const std::string &path, Mesh &mesh, bool flipTexCoords);  // src/shapes/obj.cpp
+
+// TriMesh::computeNormals (src/librender/trimesh.cpp:608-681)
+void computeNormals(Mesh &mesh, bool flipNormals);
+
+// SAH kd-tree over `n` primitives with the given (clippable) geometry
+struct PrimSource {
+    virtual ~PrimSource() = default;
+    virtual size_t count() const = 0;
+    virtual AABB bounds(size_t i) const = 0;
+    virtual AABB clippedBounds(size_t i, const AABB &box) const = 0;
+};
+void buildKDTree(const PrimSource &src, const KDBuildParams &params, KDTree &out);
+
+// Conductor IOR lookup (generated from data/ior/*.spd), dielectric lookupIOR
+bool lookupConductor(const std::string &name, V3 &eta, V3 &k);
+float lookupIOR(const std::string &name);
+
+// Film developing (hdrfilm.cpp:481-492, fmtconv.cpp:962-974) and PFM output
+void writePFM(const std::string &path, int w, int h, const std::vector<float> &rgb);
+
+}  // namespace mtsh

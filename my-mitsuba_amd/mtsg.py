@@ -1,0 +1,275 @@
+"""ctypes bindings for the MI355X `path` integrator.
+
+Two shared libraries, both built in-tree by ``make`` (``__graft_entry__.build()``):
+
+* ``libmtsg_host.so`` -- Mitsuba-side scene loading + SAH kd-tree build
+  (include/mtsh.h); no GPU code.
+* ``libmtsg.so``      -- the HIP/gfx950 wavefront path tracer behind the C-ABI
+  drop-in boundary (include/mtsg.h).
+
+This module is the Python mirror of the reference's plugin surface used by the
+tests and the benchmark.  It never falls back to a CPU path: if the HIP
+library is missing, :func:`device_lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+
+MTSG_OK = 0
+MTSG_FLAG_TIMING = 1
+MTSG_FLAG_COUNT = 2
+
+
+class RenderParams(C.Structure):
+    """mtsg_render_params (include/mtsg.h)."""
+    _fields_ = [
+        ("max_depth", C.c_int32), ("rr_depth", C.c_int32),
+        ("strict_normals", C.c_int32), ("hide_emitters", C.c_int32),
+        ("spp", C.c_uint32), ("seed", C.c_uint32),
+        ("tile_x", C.c_int32), ("tile_y", C.c_int32),
+        ("tile_w", C.c_int32), ("tile_h", C.c_int32),
+        ("tile_stride", C.c_int32), ("tile_offset", C.c_int32),
+    ]
+
+    def copy(self) -> "RenderParams":
+        p = RenderParams()
+        C.memmove(C.byref(p), C.byref(self), C.sizeof(RenderParams))
+        return p
+
+
+class Stats(C.Structure):
+    """mtsg_stats."""
+    _fields_ = [
+        ("ms_total", C.c_double), ("ms_trace_closest", C.c_double),
+        ("ms_trace_shadow", C.c_double), ("ms_shade", C.c_double),
+        ("ms_camera", C.c_double), ("ms_splat", C.c_double),
+        ("launches_trace_closest", C.c_uint64),
+        ("rays_closest", C.c_uint64), ("rays_shadow", C.c_uint64),
+        ("samples", C.c_uint64),
+        ("nodes_visited", C.c_uint64), ("leaf_refs", C.c_uint64),
+        ("tri_tests", C.c_uint64),
+        ("shadow_nodes_visited", C.c_uint64), ("shadow_leaf_refs", C.c_uint64),
+        ("shadow_tri_tests", C.c_uint64),
+    ]
+
+
+class SceneInfo(C.Structure):
+    """mtsh_scene_info."""
+    _fields_ = [
+        ("n_triangles", C.c_uint32), ("n_rects", C.c_uint32), ("n_shapes", C.c_uint32),
+        ("n_emitters", C.c_uint32), ("n_bsdfs", C.c_uint32),
+        ("kd_nodes", C.c_uint32), ("kd_indices", C.c_uint32), ("kd_max_depth", C.c_uint32),
+        ("kd_leaves", C.c_uint32), ("kd_nonempty_leaves", C.c_uint32),
+        ("kd_build_seconds", C.c_double),
+        ("film_w", C.c_int32), ("film_h", C.c_int32), ("spp", C.c_int32),
+        ("border", C.c_int32), ("max_depth", C.c_int32),
+    ]
+
+
+_host = None
+_dev = None
+
+DEVICE_SYMBOLS = [
+    "mtsg_device_count", "mtsg_scene_create", "mtsg_render", "mtsg_render_device",
+    "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
+    "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths",
+    "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_scene_destroy", "mtsg_last_error",
+]
+HOST_SYMBOLS = [
+    "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_scene_desc", "mtsh_scene_render_params",
+    "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_last_error",
+]
+
+
+def host_lib() -> C.CDLL:
+    global _host
+    if _host is None:
+        path = os.path.join(PKG_DIR, "libmtsg_host.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: run `make host` (or __graft_entry__.build())")
+        lib = C.CDLL(path)
+        lib.mtsh_scene_load.restype = C.c_void_p
+        lib.mtsh_scene_load.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_int]
+        lib.mtsh_scene_desc.restype = C.c_void_p
+        lib.mtsh_scene_desc.argtypes = [C.c_void_p]
+        lib.mtsh_scene_render_params.argtypes = [C.c_void_p, C.POINTER(RenderParams)]
+        lib.mtsh_scene_get_info.argtypes = [C.c_void_p, C.POINTER(SceneInfo)]
+        lib.mtsh_scene_free.argtypes = [C.c_void_p]
+        lib.mtsh_develop.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        lib.mtsh_write_pfm.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p]
+        lib.mtsh_last_error.argtypes = [C.c_char_p, C.c_size_t]
+        lib.mtsh_set_kd_threads.argtypes = [C.c_int]
+        _host = lib
+    return _host
+
+
+def device_lib() -> C.CDLL:
+    """The HIP library.  Raises (never falls back) when it is missing."""
+    global _dev
+    if _dev is None:
+        path = os.path.join(PKG_DIR, "libmtsg.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: the HIP extension was not built "
+                               "(run `make device` / __graft_entry__.build()); no CPU fallback exists")
+        lib = C.CDLL(path)
+        lib.mtsg_device_count.restype = C.c_int
+        lib.mtsg_scene_create.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+        lib.mtsg_render.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
+        lib.mtsg_render_device.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
+        lib.mtsg_device_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
+        lib.mtsg_device_free.argtypes = [C.c_void_p, C.c_void_p]
+        lib.mtsg_device_memset.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.mtsg_device_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.mtsg_cancel.argtypes = [C.c_void_p]
+        lib.mtsg_set_flags.argtypes = [C.c_void_p, C.c_uint32]
+        lib.mtsg_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
+        lib.mtsg_set_batch_paths.argtypes = [C.c_void_p, C.c_uint32]
+        lib.mtsg_trace_closest.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.mtsg_trace_shadow.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        lib.mtsg_scene_destroy.argtypes = [C.c_void_p]
+        lib.mtsg_last_error.argtypes = [C.c_char_p, C.c_size_t]
+        _dev = lib
+    return _dev
+
+
+def _err(lib, fn) -> str:
+    buf = C.create_string_buffer(4096)
+    getattr(lib, fn)(buf, 4096)
+    return buf.value.decode(errors="replace")
+
+
+def _ptr(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+class Scene:
+    """A loaded Mitsuba XML scene (host side; owns the flat descriptor)."""
+
+    def __init__(self, path: str, defines: dict | None = None, kd_threads: int = 0):
+        lib = host_lib()
+        lib.mtsh_set_kd_threads(kd_threads)
+        defs = [f"{k}={v}".encode() for k, v in (defines or {}).items()]
+        arr = (C.c_char_p * max(1, len(defs)))(*defs)
+        self._h = lib.mtsh_scene_load(path.encode(), arr, len(defs))
+        if not self._h:
+            raise RuntimeError("scene load failed: " + _err(lib, "mtsh_last_error"))
+        self.path = path
+        self.info = SceneInfo()
+        lib.mtsh_scene_get_info(self._h, C.byref(self.info))
+
+    @property
+    def desc(self) -> C.c_void_p:
+        return C.c_void_p(host_lib().mtsh_scene_desc(self._h))
+
+    def params(self, **overrides) -> RenderParams:
+        p = RenderParams()
+        host_lib().mtsh_scene_render_params(self._h, C.byref(p))
+        for k, v in overrides.items():
+            setattr(p, k, v)
+        return p
+
+    @property
+    def border(self) -> int:
+        return self.info.border
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            host_lib().mtsh_scene_free(self._h)
+            self._h = None
+
+
+def develop(rgbaw: np.ndarray) -> np.ndarray:
+    """hdrfilm develop: rgb = sum(w L) / sum(w) (fmtconv.cpp:962-974)."""
+    rgbaw = np.ascontiguousarray(rgbaw, dtype=np.float32)
+    h, w = rgbaw.shape[:2]
+    out = np.zeros((h, w, 3), dtype=np.float32)
+    host_lib().mtsh_develop(_ptr(rgbaw), w, h, _ptr(out))
+    return out
+
+
+def write_pfm(path: str, rgb: np.ndarray) -> None:
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    if host_lib().mtsh_write_pfm(path.encode(), rgb.shape[1], rgb.shape[0], _ptr(rgb)) != 0:
+        raise RuntimeError(_err(host_lib(), "mtsh_last_error"))
+
+
+class GPUScene:
+    """A scene resident in HBM on one device (mtsg_scene_create)."""
+
+    def __init__(self, scene: Scene, device: int = 0):
+        lib = device_lib()
+        h = C.c_void_p()
+        rc = lib.mtsg_scene_create(scene.desc, device, C.byref(h))
+        if rc != MTSG_OK:
+            raise RuntimeError(f"mtsg_scene_create failed ({rc}): " + _err(lib, "mtsg_last_error"))
+        self._h = h
+        self.scene = scene
+        self.device = device
+
+    def _check(self, rc, what):
+        if rc != MTSG_OK:
+            raise RuntimeError(f"{what} failed ({rc}): " + _err(device_lib(), "mtsg_last_error"))
+
+    def render(self, params: RenderParams, border: int) -> np.ndarray:
+        out = np.zeros((params.tile_h + 2 * border, params.tile_w + 2 * border, 5), dtype=np.float32)
+        self._check(device_lib().mtsg_render(self._h, C.byref(params), _ptr(out)), "mtsg_render")
+        return out
+
+    def set_flags(self, flags: int) -> None:
+        self._check(device_lib().mtsg_set_flags(self._h, flags), "mtsg_set_flags")
+
+    def set_batch_paths(self, n: int) -> None:
+        self._check(device_lib().mtsg_set_batch_paths(self._h, n), "mtsg_set_batch_paths")
+
+    def stats(self) -> Stats:
+        s = Stats()
+        self._check(device_lib().mtsg_get_stats(self._h, C.byref(s)), "mtsg_get_stats")
+        return s
+
+    def trace_closest(self, rays: np.ndarray):
+        rays = np.ascontiguousarray(rays, dtype=np.float32)
+        n = rays.shape[0]
+        t = np.empty(n, np.float32); u = np.empty(n, np.float32); v = np.empty(n, np.float32)
+        prim = np.empty(n, np.uint32)
+        self._check(device_lib().mtsg_trace_closest(self._h, n, _ptr(rays), _ptr(t), _ptr(u), _ptr(v), _ptr(prim)),
+                    "mtsg_trace_closest")
+        return t, u, v, prim
+
+    def trace_shadow(self, rays: np.ndarray) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, dtype=np.float32)
+        occ = np.empty(rays.shape[0], np.uint8)
+        self._check(device_lib().mtsg_trace_shadow(self._h, rays.shape[0], _ptr(rays), _ptr(occ)), "mtsg_trace_shadow")
+        return occ
+
+    # device-resident film for the benchmark
+    def alloc(self, nbytes: int) -> C.c_void_p:
+        p = C.c_void_p()
+        self._check(device_lib().mtsg_device_alloc(self._h, nbytes, C.byref(p)), "mtsg_device_alloc")
+        self._check(device_lib().mtsg_device_memset(self._h, p, nbytes), "mtsg_device_memset")
+        return p
+
+    def free(self, p: C.c_void_p) -> None:
+        device_lib().mtsg_device_free(self._h, p)
+
+    def render_device(self, params: RenderParams, film: C.c_void_p) -> None:
+        self._check(device_lib().mtsg_render_device(self._h, C.byref(params), film), "mtsg_render_device")
+
+    def download(self, film: C.c_void_p, shape) -> np.ndarray:
+        out = np.zeros(shape, dtype=np.float32)
+        self._check(device_lib().mtsg_device_to_host(self._h, _ptr(out), film, out.nbytes), "mtsg_device_to_host")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            device_lib().mtsg_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()

@@ -1,0 +1,1408 @@
+// oracle.cpp -- TEST INFRASTRUCTURE ONLY (see oracle.h).
+//
+// Scalar CPU restatement of the reference's `path` hot path, written to follow
+// the reference's own control flow line by line (AoS records, virtual-free
+// switch dispatch, Havran kd-tree traversal), so that the HIP wavefront
+// implementation can be checked against it.  Every function cites the
+// reference file:line it restates (paths relative to the reference root).
+#include "oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+// ---------------------------------------------------------------------------
+// math (include/mitsuba/core/vector.h, frame.h)
+// ---------------------------------------------------------------------------
+struct Vec {
+    float x, y, z;
+    Vec() : x(0), y(0), z(0) {}
+    Vec(float a, float b, float c) : x(a), y(b), z(c) {}
+    explicit Vec(float a) : x(a), y(a), z(a) {}
+    float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    float &operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+};
+inline Vec operator+(Vec a, Vec b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline Vec operator-(Vec a, Vec b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline Vec operator-(Vec a) { return {-a.x, -a.y, -a.z}; }
+inline Vec operator*(Vec a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline Vec operator*(float s, Vec a) { return {a.x * s, a.y * s, a.z * s}; }
+inline Vec operator/(Vec a, float s) { float r = 1.0f / s; return {a.x * r, a.y * r, a.z * r}; }
+inline float dot(Vec a, Vec b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline float absDot(Vec a, Vec b) { return std::abs(dot(a, b)); }
+inline Vec cross(Vec a, Vec b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline float length(Vec a) { return std::sqrt(dot(a, a)); }
+inline Vec normalize(Vec a) { return a / length(a); }
+
+// RGB Spectrum (SPECTRUM_SAMPLES = 3)
+struct Spec {
+    float s[3];
+    Spec() { s[0] = s[1] = s[2] = 0; }
+    explicit Spec(float v) { s[0] = s[1] = s[2] = v; }
+    Spec(float a, float b, float c) { s[0] = a; s[1] = b; s[2] = c; }
+    static Spec of(const float *p) { return Spec(p[0], p[1], p[2]); }
+    bool isZero() const { return s[0] == 0 && s[1] == 0 && s[2] == 0; }
+    float max() const { return std::max(s[0], std::max(s[1], s[2])); }
+};
+inline Spec operator*(Spec a, Spec b) { return {a.s[0] * b.s[0], a.s[1] * b.s[1], a.s[2] * b.s[2]}; }
+inline Spec operator*(Spec a, float f) { return {a.s[0] * f, a.s[1] * f, a.s[2] * f}; }
+inline Spec operator/(Spec a, float f) { float r = 1.0f / f; return {a.s[0] * r, a.s[1] * r, a.s[2] * r}; }
+inline Spec operator+(Spec a, Spec b) { return {a.s[0] + b.s[0], a.s[1] + b.s[1], a.s[2] + b.s[2]}; }
+inline Spec operator-(Spec a, Spec b) { return {a.s[0] - b.s[0], a.s[1] - b.s[1], a.s[2] - b.s[2]}; }
+inline Spec operator/(Spec a, Spec b) { return {a.s[0] / b.s[0], a.s[1] / b.s[1], a.s[2] / b.s[2]}; }
+inline Spec &operator+=(Spec &a, Spec b) { a = a + b; return a; }
+inline Spec &operator*=(Spec &a, Spec b) { a = a * b; return a; }
+inline Spec sqrtSafe(Spec a) { return {std::sqrt(std::max(0.f, a.s[0])), std::sqrt(std::max(0.f, a.s[1])), std::sqrt(std::max(0.f, a.s[2]))}; }
+
+// util.cpp:590-600
+void coordinateSystem(const Vec &a, Vec &b, Vec &c) {
+    if (std::abs(a.x) > std::abs(a.y)) {
+        float invLen = 1.0f / std::sqrt(a.x * a.x + a.z * a.z);
+        c = Vec(a.z * invLen, 0.0f, -a.x * invLen);
+    } else {
+        float invLen = 1.0f / std::sqrt(a.y * a.y + a.z * a.z);
+        c = Vec(0.0f, a.z * invLen, -a.y * invLen);
+    }
+    b = cross(c, a);
+}
+
+struct Frame {
+    Vec s, t, n;
+    Frame() {}
+    explicit Frame(const Vec &nn) : n(nn) { coordinateSystem(nn, s, t); }   // frame.h:55-57
+    Vec toLocal(const Vec &v) const { return Vec(dot(v, s), dot(v, t), dot(v, n)); }
+    Vec toWorld(const Vec &v) const { return s * v.x + t * v.y + n * v.z; }
+};
+inline float cosTheta(const Vec &v) { return v.z; }
+inline float cosTheta2(const Vec &v) { return v.z * v.z; }
+inline float sinTheta2(const Vec &v) { return 1.0f - v.z * v.z; }
+inline float tanTheta(const Vec &v) {   // frame.h:122-127
+    float temp = 1 - v.z * v.z;
+    if (temp <= 0.0f) return 0.0f;
+    return std::sqrt(temp) / v.z;
+}
+
+// util.cpp:603-608
+void computeShadingFrame(const Vec &n, const Vec &dpdu, Frame &frame) {
+    frame.n = n;
+    frame.s = normalize(dpdu - frame.n * dot(frame.n, dpdu));
+    frame.t = cross(frame.n, frame.s);
+}
+
+// math.h:184-199 (Linux x86_64 variant)
+inline float fastexp(float v) { return (float)::exp((double)v); }
+inline float fastlog(float v) { return (float)::log((double)v); }
+inline float signum(float v) { return copysignf(1.0f, v); }
+inline float safe_sqrt(float v) { return std::sqrt(std::max(0.0f, v)); }
+
+// math.cpp:25-70
+float erfinv(float x) {
+    float w = -fastlog((1.0f - x) * (1.0f + x));
+    float p;
+    if (w < 5.0f) {
+        w = w - 2.5f;
+        p = 2.81022636e-08f;
+        p = 3.43273939e-07f + p * w;
+        p = -3.5233877e-06f + p * w;
+        p = -4.39150654e-06f + p * w;
+        p = 0.00021858087f + p * w;
+        p = -0.00125372503f + p * w;
+        p = -0.00417768164f + p * w;
+        p = 0.246640727f + p * w;
+        p = 1.50140941f + p * w;
+    } else {
+        w = std::sqrt(w) - 3.0f;
+        p = -0.000200214257f;
+        p = 0.000100950558f + p * w;
+        p = 0.00134934322f + p * w;
+        p = -0.00367342844f + p * w;
+        p = 0.00573950773f + p * w;
+        p = -0.0076224613f + p * w;
+        p = 0.00943887047f + p * w;
+        p = 1.00167406f + p * w;
+        p = 2.83297682f + p * w;
+    }
+    return p * x;
+}
+float erf(float x) {
+    const float a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f;
+    const float a4 = -1.453152027f, a5 = 1.061405429f, p = 0.3275911f;
+    float sign = signum(x);
+    x = std::abs(x);
+    float t = 1.0f / (1.0f + p * x);
+    float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * fastexp(-x * x);
+    return sign * y;
+}
+// math.cpp:74-86
+float hypot2(float a, float b) {
+    float r;
+    if (std::abs(a) > std::abs(b)) { r = b / a; r = std::abs(a) * std::sqrt(1.0f + r * r); }
+    else if (b != 0.0f) { r = a / b; r = std::abs(b) * std::sqrt(1.0f + r * r); }
+    else r = 0.0f;
+    return r;
+}
+
+const float kEpsilon = 1e-4f;        // constants.h:28
+const float kShadowEpsilon = 1e-3f;  // constants.h:29
+const float kDeltaEpsilon = 1e-3f;   // constants.h:31
+const float kInvPi = 0.31830988618379067154f;
+
+// ---------------------------------------------------------------------------
+// SFMT-19937 (src/libcore/random.cpp:66-81 parameters, :130-640)
+// ---------------------------------------------------------------------------
+const int MEXP = 19937, N128 = MEXP / 128 + 1, N32 = N128 * 4, N64 = N128 * 2;
+const int POS1 = 122, SL1 = 18, SL2 = 1, SR1 = 11, SR2 = 1;
+const uint32_t MSK[4] = {0xdfffffefU, 0xddfecb7fU, 0xbffaffffU, 0xbffffff6U};
+const uint32_t PARITY[4] = {0x00000001U, 0x00000000U, 0x00000000U, 0x13c9e684U};
+
+struct Sfmt {
+    union {
+        uint32_t u32[N32];
+        uint64_t u64[N64];
+    };
+    int idx = -1;
+
+    static void rshift128(uint32_t out[4], const uint32_t in[4], int shift) {
+        uint64_t th = ((uint64_t)in[3] << 32) | in[2], tl = ((uint64_t)in[1] << 32) | in[0];
+        uint64_t oh = th >> (shift * 8), ol = tl >> (shift * 8);
+        ol |= th << (64 - shift * 8);
+        out[0] = (uint32_t)ol; out[1] = (uint32_t)(ol >> 32); out[2] = (uint32_t)oh; out[3] = (uint32_t)(oh >> 32);
+    }
+    static void lshift128(uint32_t out[4], const uint32_t in[4], int shift) {
+        uint64_t th = ((uint64_t)in[3] << 32) | in[2], tl = ((uint64_t)in[1] << 32) | in[0];
+        uint64_t oh = th << (shift * 8), ol = tl << (shift * 8);
+        oh |= tl >> (64 - shift * 8);
+        out[0] = (uint32_t)ol; out[1] = (uint32_t)(ol >> 32); out[2] = (uint32_t)oh; out[3] = (uint32_t)(oh >> 32);
+    }
+    static void doRecursion(uint32_t r[4], const uint32_t a[4], const uint32_t b[4], const uint32_t c[4], const uint32_t d[4]) {
+        uint32_t x[4], y[4];
+        lshift128(x, a, SL2);
+        rshift128(y, c, SR2);
+        for (int k = 0; k < 4; ++k) r[k] = a[k] ^ x[k] ^ ((b[k] >> SR1) & MSK[k]) ^ y[k] ^ (d[k] << SL1);
+    }
+    void genRandAll() {   // random.cpp:353-392 (scalar branch)
+        uint32_t *r1 = &u32[4 * (N128 - 2)], *r2 = &u32[4 * (N128 - 1)];
+        int i;
+        for (i = 0; i < N128 - POS1; ++i) {
+            uint32_t out[4];
+            doRecursion(out, &u32[4 * i], &u32[4 * (i + POS1)], r1, r2);
+            memcpy(&u32[4 * i], out, 16);
+            r1 = r2;
+            r2 = &u32[4 * i];
+        }
+        for (; i < N128; ++i) {
+            uint32_t out[4];
+            doRecursion(out, &u32[4 * i], &u32[4 * (i + POS1 - N128)], r1, r2);
+            memcpy(&u32[4 * i], out, 16);
+            r1 = r2;
+            r2 = &u32[4 * i];
+        }
+    }
+    void periodCertification() {   // random.cpp:322-351
+        int inner = 0;
+        for (int i = 0; i < 4; ++i) inner ^= u32[i] & PARITY[i];
+        for (int i = 16; i > 0; i >>= 1) inner ^= inner >> i;
+        inner &= 1;
+        if (inner == 1) return;
+        for (int i = 0; i < 4; ++i) {
+            uint32_t work = 1;
+            for (int j = 0; j < 32; ++j) {
+                if ((work & PARITY[i]) != 0) { u32[i] ^= work; return; }
+                work = work << 1;
+            }
+        }
+    }
+    void initGenRand(uint64_t seed) {   // random.cpp:397-406
+        u64[0] = seed;
+        for (int i = 1; i < N64; ++i) u64[i] = 6364136223846793005ULL * (u64[i - 1] ^ (u64[i - 1] >> 62)) + (uint64_t)i;
+        idx = N32;
+        periodCertification();
+    }
+    static uint32_t func1(uint32_t x) { return (x ^ (x >> 27)) * (uint32_t)1664525UL; }
+    static uint32_t func2(uint32_t x) { return (x ^ (x >> 27)) * (uint32_t)1566083941UL; }
+    void initByArray(const uint32_t *key, int keyLength) {   // random.cpp:408-470
+        int i, j, count;
+        uint32_t r;
+        const int size = N32, lag = 11, mid = (size - lag) / 2;
+        memset(u32, 0x8b, sizeof(u32));
+        count = keyLength + 1 > N32 ? keyLength + 1 : N32;
+        r = func1(u32[0] ^ u32[mid] ^ u32[N32 - 1]);
+        u32[mid] += r;
+        r += keyLength;
+        u32[mid + lag] += r;
+        u32[0] = r;
+        count--;
+        for (i = 1, j = 0; (j < count) && (j < keyLength); j++) {
+            r = func1(u32[i] ^ u32[(i + mid) % N32] ^ u32[(i + N32 - 1) % N32]);
+            u32[(i + mid) % N32] += r;
+            r += key[j] + i;
+            u32[(i + mid + lag) % N32] += r;
+            u32[i] = r;
+            i = (i + 1) % N32;
+        }
+        for (; j < count; j++) {
+            r = func1(u32[i] ^ u32[(i + mid) % N32] ^ u32[(i + N32 - 1) % N32]);
+            u32[(i + mid) % N32] += r;
+            r += i;
+            u32[(i + mid + lag) % N32] += r;
+            u32[i] = r;
+            i = (i + 1) % N32;
+        }
+        for (j = 0; j < N32; j++) {
+            r = func2(u32[i] + u32[(i + mid) % N32] + u32[(i + N32 - 1) % N32]);
+            u32[(i + mid) % N32] ^= r;
+            r -= i;
+            u32[(i + mid + lag) % N32] ^= r;
+            u32[i] = r;
+            i = (i + 1) % N32;
+        }
+        idx = N32;
+        periodCertification();
+    }
+    void seedFrom(Sfmt &parent) {   // random.cpp:528-546 Random::seed(Random*)
+        uint64_t buf[N64];
+        for (int i = 0; i < N64; ++i) buf[i] = parent.nextULong();
+        initByArray(reinterpret_cast<const uint32_t *>(buf), N64 * 2);
+    }
+    uint64_t nextULong() {   // gen_rand64
+        if (idx >= N32) { genRandAll(); idx = 0; }
+        uint64_t r = u64[idx / 2];
+        idx += 2;
+        return r;
+    }
+    float nextFloat() {   // random.cpp:629-639
+        union { uint32_t u; float f; } x;
+        x.u = (uint32_t)(((nextULong() & 0xFFFFFFFFULL) >> 9) | 0x3f800000UL);
+        return x.f - 1.0f;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// counter-mode RNG (shared spec with the GPU; DESIGN.md "RNG")
+// ---------------------------------------------------------------------------
+inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ULL;
+    x ^= x >> 27; x *= 0x94D049BB133111EBULL;
+    x ^= x >> 31;
+    return x;
+}
+inline uint64_t counterKey(uint32_t seed, uint64_t sampleId) {
+    return mix64(sampleId * 0x9E3779B97F4A7C15ULL + (uint64_t)seed);
+}
+inline float counterFloat(uint64_t key, uint32_t dim) {
+    uint32_t u = (uint32_t)(mix64(key + (uint64_t)(dim + 1) * 0xD1B54A32D192ED03ULL) >> 32);
+    union { uint32_t u; float f; } x;
+    x.u = (u >> 9) | 0x3f800000U;
+    return x.f - 1.0f;
+}
+
+struct Sampler {
+    int mode;
+    Sfmt *sfmt = nullptr;
+    uint64_t key = 0;
+    uint32_t dim = 0;
+    float next1D() { return mode == ORACLE_RNG_SFMT ? sfmt->nextFloat() : counterFloat(key, dim++); }
+    void next2D(float &a, float &b) { a = next1D(); b = next1D(); }   // independent.cpp:99-103
+};
+
+// ---------------------------------------------------------------------------
+// Ray (include/mitsuba/core/ray.h:45-143)
+// ---------------------------------------------------------------------------
+struct Ray {
+    Vec o, d, dRcp;
+    float mint, maxt;
+    void setDirection(const Vec &dd) { d = dd; dRcp = Vec(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+    Vec operator()(float t) const { return o + d * t; }
+};
+
+struct Counters {
+    uint64_t nodes = 0, refs = 0, tests = 0, closest = 0, shadow = 0;
+};
+
+// ---------------------------------------------------------------------------
+// Scene view over the flat descriptor
+// ---------------------------------------------------------------------------
+struct Its {
+    float t = std::numeric_limits<float>::infinity();
+    Vec p;
+    Frame geoFrame, shFrame;
+    Vec dpdu, wi;
+    int shape = -1;
+    bool valid() const { return t != std::numeric_limits<float>::infinity(); }
+    Vec toLocal(const Vec &v) const { return shFrame.toLocal(v); }
+    Vec toWorld(const Vec &v) const { return shFrame.toWorld(v); }
+};
+
+struct Cache { uint32_t shapeIndex, primIndex; float u, v, rx, ry; };
+
+struct SceneView {
+    const mtsg_scene_desc &d;
+    explicit SceneView(const mtsg_scene_desc &dd) : d(dd) {}
+
+    Vec vtx(uint32_t i) const { return Vec(d.vtx_pos[3 * i], d.vtx_pos[3 * i + 1], d.vtx_pos[3 * i + 2]); }
+    Vec nrm(uint32_t i) const { return Vec(d.vtx_nrm[3 * i], d.vtx_nrm[3 * i + 1], d.vtx_nrm[3 * i + 2]); }
+
+    // AABB::rayIntersect (aabb.h:308-338)
+    bool aabbIntersect(const Ray &ray, float &nearT, float &farT) const {
+        nearT = -std::numeric_limits<float>::infinity();
+        farT = std::numeric_limits<float>::infinity();
+        for (int i = 0; i < 3; i++) {
+            const float origin = ray.o[i], minVal = d.aabb_min[i], maxVal = d.aabb_max[i];
+            if (ray.d[i] == 0) {
+                if (origin < minVal || origin > maxVal) return false;
+            } else {
+                float t1 = (minVal - origin) * ray.dRcp[i];
+                float t2 = (maxVal - origin) * ray.dRcp[i];
+                if (t1 > t2) std::swap(t1, t2);
+                nearT = std::max(t1, nearT);
+                farT = std::min(t2, farT);
+                if (!(nearT <= farT)) return false;
+            }
+        }
+        return true;
+    }
+
+    // TriAccel::rayIntersect (triaccel.h:96-158)
+    static bool triIntersect(const mtsg_triaccel &ta, const Ray &ray, float mint, float maxt, float &u, float &v, float &t) {
+        float o_u, o_v, o_k, d_u, d_v, d_k;
+        switch (ta.k) {
+            case 0: o_u = ray.o.y; o_v = ray.o.z; o_k = ray.o.x; d_u = ray.d.y; d_v = ray.d.z; d_k = ray.d.x; break;
+            case 1: o_u = ray.o.z; o_v = ray.o.x; o_k = ray.o.y; d_u = ray.d.z; d_v = ray.d.x; d_k = ray.d.y; break;
+            case 2: o_u = ray.o.x; o_v = ray.o.y; o_k = ray.o.z; d_u = ray.d.x; d_v = ray.d.y; d_k = ray.d.z; break;
+            default: return false;
+        }
+        t = (ta.n_d - o_u * ta.n_u - o_v * ta.n_v - o_k) / (d_u * ta.n_u + d_v * ta.n_v + d_k);
+        if (t < mint || t > maxt) return false;
+        const float hu = o_u + t * d_u - ta.a_u;
+        const float hv = o_v + t * d_v - ta.a_v;
+        u = hv * ta.b_nu + hu * ta.b_nv;
+        v = hu * ta.c_nu + hv * ta.c_nv;
+        return u >= 0 && v >= 0 && u + v <= 1.0f;
+    }
+
+    // Rectangle::rayIntersect (rectangle.cpp:115-139): object-space plane test
+    bool rectIntersect(const mtsg_rect &r, const Ray &wr, float mint, float maxt, float &t, float &lx, float &ly) const {
+        const float *m = r.to_object;
+        Vec o(m[0] * wr.o.x + m[1] * wr.o.y + m[2] * wr.o.z + m[3],
+              m[4] * wr.o.x + m[5] * wr.o.y + m[6] * wr.o.z + m[7],
+              m[8] * wr.o.x + m[9] * wr.o.y + m[10] * wr.o.z + m[11]);
+        Vec dd(m[0] * wr.d.x + m[1] * wr.d.y + m[2] * wr.d.z,
+               m[4] * wr.d.x + m[5] * wr.d.y + m[6] * wr.d.z,
+               m[8] * wr.d.x + m[9] * wr.d.y + m[10] * wr.d.z);
+        float hit = -o.z / dd.z;
+        if (!(hit >= mint && hit <= maxt)) return false;
+        Vec local = o + dd * hit;
+        if (std::abs(local.x) <= 1 && std::abs(local.y) <= 1) {
+            t = hit; lx = local.x; ly = local.y;
+            return true;
+        }
+        return false;
+    }
+
+    // ShapeKDTree::intersect (skdtree.h:248-337)
+    bool primIntersect(const Ray &ray, uint32_t idx, float mint, float maxt, float &t, Cache *cache) const {
+        const mtsg_triaccel &ta = d.triaccel[idx];
+        if (ta.k != MTSG_TRIACCEL_SHAPE) {
+            float u, v, tt;
+            if (triIntersect(ta, ray, mint, maxt, u, v, tt)) {
+                t = tt;
+                if (cache) { cache->shapeIndex = ta.shape_index; cache->primIndex = ta.prim_index; cache->u = u; cache->v = v; }
+                return true;
+            }
+            return false;
+        }
+        float tt, lx, ly;
+        if (rectIntersect(d.rects[ta.prim_index], ray, mint, maxt, tt, lx, ly)) {
+            t = tt;
+            if (cache) { cache->shapeIndex = ta.shape_index; cache->primIndex = 0xFFFFFFFFu; cache->rx = lx; cache->ry = ly; }
+            return true;
+        }
+        return false;
+    }
+
+    // SAHKDTree3D::rayIntersectHavran (sahkdtree3.h:178-308), with the
+    // 8-entry hashed mailbox (sahkdtree3.h:30-32,138-152)
+    template <bool shadowRay, bool count>
+    bool havran(const Ray &ray, float mint, float maxt, float &t, Cache *cache, Counters *ctr) const {
+        struct Entry { uint32_t node; float t; uint32_t prev; Vec p; };
+        Entry stack[48];
+        uint32_t mailbox[8];
+        memset(mailbox, 0xFF, sizeof(mailbox));
+        uint32_t enPt = 0;
+        stack[enPt].t = mint;
+        stack[enPt].p = ray(mint);
+        uint32_t exPt = 1;
+        stack[exPt].t = maxt;
+        stack[exPt].p = ray(maxt);
+        stack[exPt].node = 0xFFFFFFFFu;
+        bool found = false;
+        uint32_t cur = 0;
+        Cache tmp;
+        while (cur != 0xFFFFFFFFu) {
+            for (;;) {
+                if (count) ctr->nodes++;
+                const mtsg_kdnode &node = d.nodes[cur];
+                if (node.combined & 0x80000000u) break;
+                float splitVal;
+                memcpy(&splitVal, &node.data, 4);
+                const int axis = (int)(node.combined & 3u);
+                const uint32_t left = cur + ((node.combined & ~(3u | 0x40000000u)) >> 2);
+                uint32_t farChild;
+                if (stack[enPt].p[axis] <= splitVal) {
+                    if (stack[exPt].p[axis] <= splitVal) { cur = left; continue; }
+                    if (stack[enPt].p[axis] == splitVal) { cur = left + 1; continue; }
+                    cur = left;
+                    farChild = cur + 1;
+                } else {
+                    if (splitVal < stack[exPt].p[axis]) { cur = left + 1; continue; }
+                    farChild = left;
+                    cur = farChild + 1;
+                }
+                float distToSplit = (splitVal - ray.o[axis]) * ray.dRcp[axis];
+                const uint32_t tmpPt = exPt++;
+                if (exPt == enPt) ++exPt;
+                if (exPt >= 48) { g_err = "kd-tree stack overflow"; return found; }
+                stack[exPt].prev = tmpPt;
+                stack[exPt].t = distToSplit;
+                stack[exPt].node = farChild;
+                stack[exPt].p = ray(distToSplit);
+                stack[exPt].p[axis] = splitVal;
+            }
+            const mtsg_kdnode &leaf = d.nodes[cur];
+            for (uint32_t entry = leaf.combined & 0x7FFFFFFFu, last = leaf.data; entry != last; entry++) {
+                const uint32_t primIdx = d.indices[entry];
+                if (count) ctr->refs++;
+                if (mailbox[primIdx & 7] == primIdx) continue;
+                if (count) ctr->tests++;
+                bool result;
+                if (!shadowRay) result = primIntersect(ray, primIdx, mint, maxt, t, &tmp);
+                else { float tt; result = primIntersect(ray, primIdx, mint, maxt, tt, nullptr); }
+                if (result) {
+                    if (shadowRay) return true;
+                    maxt = t;
+                    found = true;
+                    if (cache) *cache = tmp;
+                }
+                mailbox[primIdx & 7] = primIdx;
+            }
+            if (stack[exPt].t > maxt) break;
+            enPt = exPt;
+            cur = stack[exPt].node;
+            exPt = stack[enPt].prev;
+        }
+        return found;
+    }
+
+    // ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428)
+    void fill(const Ray &ray, const Cache &c, Its &its) const {
+        its.shape = (int)c.shapeIndex;
+        const mtsg_shape &sh = d.shapes[c.shapeIndex];
+        if (c.primIndex != 0xFFFFFFFFu) {
+            const uint32_t g = c.primIndex;
+            const uint32_t i0 = d.tri_idx[3 * g], i1 = d.tri_idx[3 * g + 1], i2 = d.tri_idx[3 * g + 2];
+            const float bx = 1 - c.u - c.v, by = c.u, bz = c.v;
+            const Vec p0 = vtx(i0), p1 = vtx(i1), p2 = vtx(i2);
+            its.p = p0 * bx + p1 * by + p2 * bz;
+            Vec side1 = p1 - p0, side2 = p2 - p0;
+            Vec faceNormal = cross(side1, side2);
+            float len = length(faceNormal);
+            if (!(faceNormal.x == 0 && faceNormal.y == 0 && faceNormal.z == 0)) faceNormal = faceNormal / len;
+            its.dpdu = Vec(d.tri_dpdu[3 * g], d.tri_dpdu[3 * g + 1], d.tri_dpdu[3 * g + 2]);
+            if (!sh.face_normals) {
+                const Vec n0 = nrm(i0), n1 = nrm(i1), n2 = nrm(i2);
+                its.shFrame.n = normalize(n0 * bx + n1 * by + n2 * bz);
+                if (dot(faceNormal, its.shFrame.n) < 0) faceNormal = -faceNormal;
+            } else {
+                its.shFrame.n = faceNormal;
+            }
+            its.geoFrame = Frame(faceNormal);
+        } else {
+            // Rectangle::fillIntersectionRecord (rectangle.cpp:145-158)
+            const mtsg_rect &r = d.rects[sh.rect];
+            its.geoFrame.s = Vec(r.frame_s[0], r.frame_s[1], r.frame_s[2]);
+            its.geoFrame.t = Vec(r.frame_t[0], r.frame_t[1], r.frame_t[2]);
+            its.geoFrame.n = Vec(r.frame_n[0], r.frame_n[1], r.frame_n[2]);
+            its.shFrame.n = its.geoFrame.n;
+            its.dpdu = Vec(r.dpdu[0], r.dpdu[1], r.dpdu[2]);
+            its.p = ray(its.t);
+        }
+        computeShadingFrame(its.shFrame.n, its.dpdu, its.shFrame);
+        its.wi = its.toLocal(-ray.d);
+    }
+
+    // ShapeKDTree::rayIntersect (skdtree.cpp:112-142)
+    template <bool count>
+    bool rayIntersect(const Ray &ray, Its &its, Cache *outCache, Counters *ctr) const {
+        its.t = std::numeric_limits<float>::infinity();
+        if (count) ctr->closest++;
+        float mint, maxt;
+        if (aabbIntersect(ray, mint, maxt)) {
+            float rayMinT = ray.mint;
+            if (rayMinT == kEpsilon)
+                rayMinT *= std::max(std::max(std::max(std::abs(ray.o.x), std::abs(ray.o.y)), std::abs(ray.o.z)), kEpsilon);
+            if (rayMinT > mint) mint = rayMinT;
+            if (ray.maxt < maxt) maxt = ray.maxt;
+            if (maxt > mint) {
+                Cache c;
+                float t = its.t;
+                if (havran<false, count>(ray, mint, maxt, t, &c, ctr)) {
+                    its.t = t;
+                    fill(ray, c, its);
+                    if (outCache) *outCache = c;
+                    return true;
+                }
+            }
+        }
+        its.t = std::numeric_limits<float>::infinity();
+        return false;
+    }
+
+    // ShapeKDTree::rayIntersect(const Ray&) shadow variant (skdtree.cpp:207-226)
+    template <bool count>
+    bool rayIntersectShadow(const Ray &ray, Counters *ctr) const {
+        float mint, maxt, t = std::numeric_limits<float>::infinity();
+        if (count) ctr->shadow++;
+        if (aabbIntersect(ray, mint, maxt)) {
+            float rayMinT = ray.mint;
+            if (rayMinT == kEpsilon)
+                rayMinT *= std::max(std::max(std::abs(ray.o.x), std::abs(ray.o.y)), std::abs(ray.o.z));
+            if (rayMinT > mint) mint = rayMinT;
+            if (ray.maxt < maxt) maxt = ray.maxt;
+            if (maxt > mint)
+                if (havran<true, count>(ray, mint, maxt, t, nullptr, ctr)) return true;
+        }
+        return false;
+    }
+
+    // ---- emitters -------------------------------------------------------
+    // DiscreteDistribution::sample / sampleReuse (pmf.h:128-188)
+    static size_t pmfSample(const float *cdf, size_t n, float x) {
+        const float *entry = std::lower_bound(cdf, cdf + n + 1, x);
+        size_t index = std::min(n - 1, (size_t)std::max((ptrdiff_t)0, entry - cdf - 1));
+        while ((cdf[index + 1] - cdf[index]) == 0 && index < n) ++index;
+        return index;
+    }
+    static size_t pmfSampleReuse(const float *cdf, size_t n, float &x, float &pdf) {
+        size_t index = pmfSample(cdf, n, x);
+        pdf = cdf[index + 1] - cdf[index];
+        x = (x - cdf[index]) / (cdf[index + 1] - cdf[index]);
+        return index;
+    }
+
+    struct DRec {   // DirectSamplingRecord (common.h:238-255)
+        Vec p, n, ref, refN, d;
+        float pdf = 0, dist = 0;
+        int measureSolidAngle = 1;
+        int emitter = -1;
+    };
+
+    // Shape::sampleDirect (shape.cpp:102-115) over TriMesh::samplePosition
+    // (trimesh.cpp:412-423) / Rectangle::samplePosition (rectangle.cpp:200-207)
+    void shapeSampleDirect(const mtsg_emitter &em, DRec &dRec, float sx, float sy) const {
+        const mtsg_shape &sh = d.shapes[em.shape];
+        if (sh.type == MTSG_SHAPE_MESH) {
+            const float *cdf = d.emitter_tri_cdf + em.cdf_offset;
+            float pdfDummy;
+            size_t index = pmfSampleReuse(cdf, sh.tri_count, sy, pdfDummy);
+            uint32_t g = sh.tri_begin + (uint32_t)index;
+            const uint32_t i0 = d.tri_idx[3 * g], i1 = d.tri_idx[3 * g + 1], i2 = d.tri_idx[3 * g + 2];
+            const Vec p0 = vtx(i0), p1 = vtx(i1), p2 = vtx(i2);
+            // Triangle::sample (triangle.cpp:24-60), squareToUniformTriangle (warp.cpp:76-79)
+            float a = safe_sqrt(1.0f - sx);
+            float bx = 1 - a, by = a * sy;
+            Vec sideA = p1 - p0, sideB = p2 - p0;
+            dRec.p = p0 + (sideA * bx) + (sideB * by);
+            if (!sh.face_normals) {
+                dRec.n = normalize(nrm(i0) * (1.0f - bx - by) + nrm(i1) * bx + nrm(i2) * by);
+            } else {
+                dRec.n = normalize(cross(sideA, sideB));
+            }
+        } else {
+            const mtsg_rect &r = d.rects[sh.rect];
+            const float *m = r.to_world;
+            float x = sx * 2 - 1, y = sy * 2 - 1;
+            dRec.p = Vec(m[0] * x + m[1] * y + m[3], m[4] * x + m[5] * y + m[7], m[8] * x + m[9] * y + m[11]);
+            dRec.n = Vec(r.frame_n[0], r.frame_n[1], r.frame_n[2]);
+        }
+        dRec.pdf = em.inv_area;
+        dRec.d = dRec.p - dRec.ref;
+        float distSquared = dot(dRec.d, dRec.d);
+        dRec.dist = std::sqrt(distSquared);
+        dRec.d = dRec.d / dRec.dist;
+        float dp = absDot(dRec.d, dRec.n);
+        dRec.pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
+        dRec.measureSolidAngle = 1;
+    }
+
+    // Scene::sampleEmitterDirect (scene.cpp:910-947) + AreaLight::sampleDirect (area.cpp:150-165)
+    template <bool count>
+    Spec sampleEmitterDirect(DRec &dRec, float sx, float sy, Counters *ctr) const {
+        float emPdf;
+        size_t index = pmfSampleReuse(d.emitter_cdf, d.n_emitters, sx, emPdf);
+        const mtsg_emitter &em = d.emitters[index];
+        shapeSampleDirect(em, dRec, sx, sy);
+        Spec value;
+        if (dot(dRec.d, dRec.refN) >= 0 && dot(dRec.d, dRec.n) < 0 && dRec.pdf != 0) {
+            value = Spec::of(em.radiance) / dRec.pdf;
+        } else {
+            dRec.pdf = 0.0f;
+            value = Spec(0.0f);
+        }
+        if (dRec.pdf != 0) {
+            Ray ray;
+            ray.o = dRec.ref;
+            ray.setDirection(dRec.d);
+            ray.mint = kEpsilon;
+            ray.maxt = dRec.dist * (1 - kShadowEpsilon);
+            if (rayIntersectShadow<count>(ray, ctr)) return Spec(0.0f);
+            dRec.emitter = (int)index;
+            dRec.pdf *= emPdf;
+            value = value / emPdf;
+            return value;
+        }
+        return Spec(0.0f);
+    }
+
+    // Scene::pdfEmitterDirect (scene.cpp:1067-1071), AreaLight::pdfDirect (area.cpp:167-176),
+    // Shape::pdfDirect (shape.cpp:117-126)
+    float pdfEmitterDirect(const DRec &dRec) const {
+        const mtsg_emitter &em = d.emitters[dRec.emitter];
+        float pdf = 0.0f;
+        if (dot(dRec.d, dRec.refN) >= 0 && dot(dRec.d, dRec.n) < 0) {
+            float pdfPos = em.inv_area;
+            pdf = pdfPos * (dRec.dist * dRec.dist) / absDot(dRec.d, dRec.n);
+        }
+        return pdf * em.pdf_discrete;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// BSDFs
+// ---------------------------------------------------------------------------
+enum { EDeltaReflection = 4, EDeltaTransmission = 16, EGlossyReflection = 2, EDiffuseReflection = 1 };
+
+struct BRec {   // BSDFSamplingRecord (bsdf.h:40-193)
+    Vec wi, wo;
+    float eta = 1.0f;
+    int sampledType = 0;
+};
+
+// warp.cpp:81-102 + 43-52
+Vec squareToCosineHemisphere(float sx, float sy) {
+    float r1 = 2.0f * sx - 1.0f, r2 = 2.0f * sy - 1.0f;
+    float phi, r;
+    if (r1 == 0 && r2 == 0) { r = phi = 0; }
+    else if (r1 * r1 > r2 * r2) { r = r1; phi = (float)(M_PI / 4.0f) * (r2 / r1); }
+    else { r = r2; phi = (float)(M_PI / 2.0f) - (r1 / r2) * (float)(M_PI / 4.0f); }
+    float cosPhi = std::cos(phi), sinPhi = std::sin(phi);
+    float px = r * cosPhi, py = r * sinPhi;
+    float z = safe_sqrt(1.0f - px * px - py * py);
+    if (z == 0) z = 1e-10f;
+    return Vec(px, py, z);
+}
+
+// MicrofacetDistribution (microfacet.h), isotropic alphaU == alphaV
+struct Microfacet {
+    int type;
+    float au, av;
+    bool sampleVisible;
+    float eval(const Vec &m) const {   // microfacet.h:191-234
+        if (cosTheta(m) <= 0) return 0.0f;
+        float ct2 = cosTheta2(m);
+        float be = ((m.x * m.x) / (au * au) + (m.y * m.y) / (av * av)) / ct2;
+        float result;
+        if (type == MTSG_MF_BECKMANN) {
+            result = fastexp(-be) / ((float)M_PI * au * av * ct2 * ct2);
+        } else {
+            float root = (1.0f + be) * ct2;
+            result = 1.0f / ((float)M_PI * au * av * root * root);
+        }
+        if (result * cosTheta(m) < 1e-20f) result = 0;
+        return result;
+    }
+    float projectRoughness(const Vec &v) const {   // microfacet.h (isotropic)
+        float invSinTheta2 = 1 / sinTheta2(v);
+        if (au == av || invSinTheta2 <= 0) return au;
+        float cosPhi2 = v.x * v.x * invSinTheta2, sinPhi2 = v.y * v.y * invSinTheta2;
+        return std::sqrt(cosPhi2 * au * au + sinPhi2 * av * av);
+    }
+    float smithG1(const Vec &v, const Vec &m) const {   // microfacet.h:477-514
+        if (dot(v, m) * cosTheta(v) <= 0) return 0.0f;
+        float tt = std::abs(tanTheta(v));
+        if (tt == 0.0f) return 1.0f;
+        float alpha = projectRoughness(v);
+        if (type == MTSG_MF_BECKMANN) {
+            float a = 1.0f / (alpha * tt);
+            if (a >= 1.6f) return 1.0f;
+            float aSqr = a * a;
+            return (3.535f * a + 2.181f * aSqr) / (1.0f + 2.276f * a + 2.577f * aSqr);
+        }
+        float root = alpha * tt;
+        return 2.0f / (1.0f + hypot2(1.0f, root));
+    }
+    float G(const Vec &wi, const Vec &wo, const Vec &m) const { return smithG1(wi, m) * smithG1(wo, m); }
+    void sampleVisible11(float thetaI, float sx, float sy, float &slx, float &sly) const {   // :573-697
+        const float SQRT_PI_INV = 1 / std::sqrt((float)M_PI);
+        if (type == MTSG_MF_BECKMANN) {
+            if (thetaI < 1e-4f) {
+                float r = std::sqrt(-fastlog(1.0f - sx));
+                float sinPhi = std::sin(2 * (float)M_PI * sy), cosPhi = std::cos(2 * (float)M_PI * sy);
+                slx = r * cosPhi; sly = r * sinPhi;
+                return;
+            }
+            float tanThetaI = std::tan(thetaI);
+            float cotThetaI = 1 / tanThetaI;
+            float a = -1, c = erf(cotThetaI);
+            float sample_x = std::max(sx, 1e-6f);
+            float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
+            float b = c - (1 + c) * std::pow(1 - sample_x, fit);
+            float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * std::exp(-cotThetaI * cotThetaI));
+            int it = 0;
+            while (++it < 10) {
+                if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+                float invErf = erfinv(b);
+                float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * std::exp(-invErf * invErf)) - sample_x;
+                float derivative = normalization * (1 - invErf * tanThetaI);
+                if (std::abs(value) < 1e-5f) break;
+                if (value > 0) c = b; else a = b;
+                b -= value / derivative;
+            }
+            slx = erfinv(b);
+            sly = erfinv(2.0f * std::max(sy, 1e-6f) - 1.0f);
+            return;
+        }
+        // GGX
+        if (thetaI < 1e-4f) {
+            float r = safe_sqrt(sx / (1 - sx));
+            float sinPhi = std::sin(2 * (float)M_PI * sy), cosPhi = std::cos(2 * (float)M_PI * sy);
+            slx = r * cosPhi; sly = r * sinPhi;
+            return;
+        }
+        float tanThetaI = std::tan(thetaI);
+        float a = 1 / tanThetaI;
+        float G1 = 2.0f / (1.0f + safe_sqrt(1.0f + 1.0f / (a * a)));
+        float A = 2.0f * sx / G1 - 1.0f;
+        if (std::abs(A) == 1) A -= signum(A) * kEpsilon;
+        float tmp = 1.0f / (A * A - 1.0f);
+        float B = tanThetaI;
+        float D = safe_sqrt(B * B * tmp * tmp - (A * A - B * B) * tmp);
+        float slope_x_1 = B * tmp - D, slope_x_2 = B * tmp + D;
+        slx = (A < 0.0f || slope_x_2 > 1.0f / tanThetaI) ? slope_x_1 : slope_x_2;
+        float S;
+        if (sy > 0.5f) { S = 1.0f; sy = 2.0f * (sy - 0.5f); }
+        else { S = -1.0f; sy = 2.0f * (0.5f - sy); }
+        float z = (sy * (sy * (sy * (-0.365728915865723f) + 0.790235037209296f) - 0.424965825137544f) + 0.000152998850436920f) /
+                  (sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) - 0.539825872510702f);
+        sly = S * z * std::sqrt(1.0f + slx * slx);
+    }
+    Vec sampleVisibleN(const Vec &wi_, float sx, float sy) const {   // :421-459
+        Vec wi = normalize(Vec(au * wi_.x, av * wi_.y, wi_.z));
+        float theta = 0, phi = 0;
+        if (wi.z < 0.99999f) { theta = std::acos(wi.z); phi = std::atan2(wi.y, wi.x); }
+        float sinPhi = std::sin(phi), cosPhi = std::cos(phi);
+        float slx, sly;
+        sampleVisible11(theta, sx, sy, slx, sly);
+        float rx = cosPhi * slx - sinPhi * sly;
+        float ry = sinPhi * slx + cosPhi * sly;
+        rx *= au; ry *= av;
+        float normalization = 1.0f / std::sqrt(rx * rx + ry * ry + 1.0f);
+        return Vec(-rx * normalization, -ry * normalization, normalization);
+    }
+    float pdfVisible(const Vec &wi, const Vec &m) const {   // :462-466
+        if (cosTheta(wi) == 0) return 0.0f;
+        return smithG1(wi, m) * absDot(wi, m) * eval(m) / std::abs(cosTheta(wi));
+    }
+    Vec sampleAll(float sx, float sy, float &pdf) const {   // :280-418 (isotropic)
+        float alphaSqr = au * au;
+        float sinPhiM = std::sin((2.0f * (float)M_PI) * sy), cosPhiM = std::cos((2.0f * (float)M_PI) * sy);
+        float cosThetaM;
+        if (type == MTSG_MF_BECKMANN) {
+            float tanThetaMSqr = alphaSqr * -fastlog(1.0f - sx);
+            cosThetaM = 1.0f / std::sqrt(1.0f + tanThetaMSqr);
+            pdf = (1.0f - sx) / ((float)M_PI * au * av * cosThetaM * cosThetaM * cosThetaM);
+        } else {
+            float tanThetaMSqr = alphaSqr * sx / (1.0f - sx);
+            cosThetaM = 1.0f / std::sqrt(1.0f + tanThetaMSqr);
+            float temp = 1 + tanThetaMSqr / alphaSqr;
+            pdf = kInvPi / (au * av * cosThetaM * cosThetaM * cosThetaM * temp * temp);
+        }
+        if (pdf < 1e-20f) pdf = 0;
+        float sinThetaM = std::sqrt(std::max(0.0f, 1 - cosThetaM * cosThetaM));
+        return Vec(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
+    }
+    Vec sample(const Vec &wi, float sx, float sy, float &pdf) const {   // :240-251
+        if (sampleVisible) {
+            Vec m = sampleVisibleN(wi, sx, sy);
+            pdf = pdfVisible(wi, m);
+            return m;
+        }
+        return sampleAll(sx, sy, pdf);
+    }
+    float pdf(const Vec &wi, const Vec &m) const {
+        return sampleVisible ? pdfVisible(wi, m) : eval(m) * cosTheta(m);
+    }
+};
+
+inline Microfacet mfOf(const mtsg_bsdf &b) { return Microfacet{b.distribution, b.alpha_u, b.alpha_v, b.sample_visible != 0}; }
+
+// util.cpp:651-681
+float fresnelDielectricExt(float cosThetaI_, float &cosThetaT_, float eta) {
+    if (eta == 1) { cosThetaT_ = -cosThetaI_; return 0.0f; }
+    float scale = (cosThetaI_ > 0) ? 1 / eta : eta, cosThetaTSqr = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
+    if (cosThetaTSqr <= 0.0f) { cosThetaT_ = 0.0f; return 1.0f; }
+    float cosThetaI = std::abs(cosThetaI_), cosThetaT = std::sqrt(cosThetaTSqr);
+    float Rs = (cosThetaI - eta * cosThetaT) / (cosThetaI + eta * cosThetaT);
+    float Rp = (eta * cosThetaI - cosThetaT) / (eta * cosThetaI + cosThetaT);
+    cosThetaT_ = (cosThetaI_ > 0) ? -cosThetaT : cosThetaT;
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+
+// util.cpp:739-761
+Spec fresnelConductorExact(float cosThetaI, const Spec &eta, const Spec &k) {
+    float cosThetaI2 = cosThetaI * cosThetaI, sinThetaI2 = 1 - cosThetaI2, sinThetaI4 = sinThetaI2 * sinThetaI2;
+    Spec temp1 = eta * eta - k * k - Spec(sinThetaI2);
+    Spec a2pb2 = sqrtSafe(temp1 * temp1 + k * k * eta * eta * 4);
+    Spec a = sqrtSafe((a2pb2 + temp1) * 0.5f);
+    Spec term1 = a2pb2 + Spec(cosThetaI2), term2 = a * (2 * cosThetaI);
+    Spec Rs2 = (term1 - term2) / (term1 + term2);
+    Spec term3 = a2pb2 * cosThetaI2 + Spec(sinThetaI4), term4 = term2 * sinThetaI2;
+    Spec Rp2 = Rs2 * (term3 - term4) / (term3 + term4);
+    return (Rp2 + Rs2) * 0.5f;
+}
+
+inline Vec reflectM(const Vec &wi, const Vec &m) { return m * (2 * dot(wi, m)) - wi; }
+
+// BSDF::eval (measure = ESolidAngle for smooth BSDFs; dielectric only
+// evaluates EDiscrete, so it returns 0 here: dielectric.cpp:228-250)
+Spec bsdfEval(const mtsg_bsdf &b, const BRec &r) {
+    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:107-116
+        if (!b.smooth || cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return Spec(0.0f);
+        return Spec::of(b.reflectance) * (kInvPi * cosTheta(r.wo));
+    }
+    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:235-268
+        if (cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return Spec(0.0f);
+        Vec H = normalize(r.wo + r.wi);
+        Microfacet distr = mfOf(b);
+        const float D = distr.eval(H);
+        if (D == 0) return Spec(0.0f);
+        const Spec F = fresnelConductorExact(dot(r.wi, H), Spec::of(b.eta), Spec::of(b.k)) * Spec::of(b.spec_refl);
+        const float G = distr.G(r.wi, r.wo, H);
+        float model = D * G / (4.0f * cosTheta(r.wi));
+        return F * model;
+    }
+    return Spec(0.0f);
+}
+
+float bsdfPdf(const mtsg_bsdf &b, const BRec &r) {
+    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:118-126
+        if (!b.smooth || cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return 0.0f;
+        return kInvPi * cosTheta(r.wo);
+    }
+    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:270-293
+        if (cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return 0.0f;
+        Vec H = normalize(r.wo + r.wi);
+        Microfacet distr = mfOf(b);
+        if (distr.sampleVisible) return distr.eval(H) * distr.smithG1(r.wi, H) / (4.0f * cosTheta(r.wi));
+        return distr.pdf(r.wi, H) / (4 * absDot(r.wo, H));
+    }
+    return 0.0f;
+}
+
+// BSDF::sample(bRec, pdf, sample)
+Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy) {
+    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
+        if (cosTheta(r.wi) <= 0) return Spec(0.0f);
+        r.wo = squareToCosineHemisphere(sx, sy);
+        r.eta = 1.0f;
+        r.sampledType = EDiffuseReflection;
+        pdf = kInvPi * cosTheta(r.wo);
+        return Spec::of(b.reflectance);
+    }
+    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:345-394
+        if (cosTheta(r.wi) < 0) return Spec(0.0f);
+        Microfacet distr = mfOf(b);
+        Vec m = distr.sample(r.wi, sx, sy, pdf);
+        if (pdf == 0) return Spec(0.0f);
+        r.wo = reflectM(r.wi, m);
+        r.eta = 1.0f;
+        r.sampledType = EGlossyReflection;
+        if (cosTheta(r.wo) <= 0) return Spec(0.0f);
+        Spec F = fresnelConductorExact(dot(r.wi, m), Spec::of(b.eta), Spec::of(b.k)) * Spec::of(b.spec_refl);
+        float weight;
+        if (distr.sampleVisible) weight = distr.smithG1(r.wo, m);
+        else weight = distr.eval(m) * distr.G(r.wi, r.wo, m) * dot(r.wi, m) / (pdf * cosTheta(r.wi));
+        pdf /= 4.0f * dot(r.wo, m);
+        return F * weight;
+    }
+    if (b.type == MTSG_BSDF_DIELECTRIC) {   // dielectric.cpp:277-333 (both components)
+        float cosThetaT;
+        float F = fresnelDielectricExt(cosTheta(r.wi), cosThetaT, b.ior_eta);
+        if (sx <= F) {
+            r.sampledType = EDeltaReflection;
+            r.wo = Vec(-r.wi.x, -r.wi.y, r.wi.z);
+            r.eta = 1.0f;
+            pdf = F;
+            return Spec::of(b.spec_refl);
+        }
+        r.sampledType = EDeltaTransmission;
+        float scale = -(cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta);
+        r.wo = Vec(scale * r.wi.x, scale * r.wi.y, cosThetaT);
+        r.eta = cosThetaT < 0 ? b.ior_eta : b.ior_inv_eta;
+        pdf = 1 - F;
+        float factor = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;   // ERadiance
+        return Spec::of(b.spec_trans) * (factor * factor);
+    }
+    return Spec(0.0f);
+}
+
+inline float miWeight(float pdfA, float pdfB) {   // path.cpp:296-300
+    pdfA *= pdfA;
+    pdfB *= pdfB;
+    return pdfA / (pdfA + pdfB);
+}
+
+// ---------------------------------------------------------------------------
+// MIPathTracer::Li (src/integrators/path/path.cpp:119-294)
+// ---------------------------------------------------------------------------
+struct Integrator {
+    int maxDepth, rrDepth;
+    bool strictNormals, hideEmitters;
+};
+
+enum {
+    EEmittedRadiance = 0x0001, EDirectSurfaceRadiance = 0x0004, EIndirectSurfaceRadiance = 0x0008,
+    EIntersection = 0x0200, EOpacity = 0x0400
+};
+
+template <bool count>
+Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, float &alpha, int &depthOut, Counters *ctr, bool hasAlpha) {
+    Its its;
+    Spec Li(0.0f);
+    bool scattered = false;
+    int type = EEmittedRadiance | EDirectSurfaceRadiance | EIndirectSurfaceRadiance | EIntersection | (hasAlpha ? EOpacity : 0);
+    int depth = 1;
+    // RadianceQueryRecord::rayIntersect (records.inl:117-143)
+    scene.rayIntersect<count>(ray, its, nullptr, ctr);
+    alpha = 1.0f;
+    if (type & EOpacity) alpha = its.valid() ? 1.0f : 0.0f;
+    ray.mint = kEpsilon;
+    Spec throughput(1.0f);
+    float eta = 1.0f;
+    while (depth <= I.maxDepth || I.maxDepth < 0) {
+        if (!its.valid()) {
+            // no environment emitter in this build's scenes: evalEnvironment = 0
+            break;
+        }
+        const mtsg_shape &sh = scene.d.shapes[its.shape];
+        const mtsg_bsdf &bsdf = scene.d.bsdfs[sh.bsdf];
+        if (sh.emitter >= 0 && (type & EEmittedRadiance) && (!I.hideEmitters || scattered)) {
+            // AreaLight::eval (area.cpp:104-109)
+            if (dot(its.shFrame.n, -ray.d) > 0) Li += throughput * Spec::of(scene.d.emitters[sh.emitter].radiance);
+        }
+        if ((depth >= I.maxDepth && I.maxDepth > 0) ||
+            (I.strictNormals && dot(ray.d, its.geoFrame.n) * cosTheta(its.wi) >= 0))
+            break;
+
+        // DirectSamplingRecord dRec(its) (records.inl:160-164)
+        SceneView::DRec dRec;
+        dRec.ref = its.p;
+        dRec.refN = bsdf.ref_n_zero ? Vec(0.0f) : its.shFrame.n;
+        if ((type & EDirectSurfaceRadiance) && bsdf.smooth) {
+            float s0, s1;
+            sampler.next2D(s0, s1);
+            Spec value = scene.sampleEmitterDirect<count>(dRec, s0, s1, ctr);
+            if (!value.isZero()) {
+                BRec bRec;
+                bRec.wi = its.wi;
+                bRec.wo = its.toLocal(dRec.d);
+                const Spec bsdfVal = bsdfEval(bsdf, bRec);
+                if (!bsdfVal.isZero() && (!I.strictNormals || dot(its.geoFrame.n, dRec.d) * cosTheta(bRec.wo) > 0)) {
+                    float bsdfPdfV = bsdfPdf(bsdf, bRec);   // area emitter: on surface, solid angle
+                    float weight = miWeight(dRec.pdf, bsdfPdfV);
+                    Li += throughput * value * bsdfVal * weight;
+                }
+            }
+        }
+
+        float bsdfPdfS;
+        BRec bRec;
+        bRec.wi = its.wi;
+        float s0, s1;
+        sampler.next2D(s0, s1);
+        Spec bsdfWeight = bsdfSample(bsdf, bRec, bsdfPdfS, s0, s1);
+        if (bsdfWeight.isZero()) break;
+        scattered |= bRec.sampledType != 0;
+        const Vec wo = its.toWorld(bRec.wo);
+        float woDotGeoN = dot(its.geoFrame.n, wo);
+        if (I.strictNormals && woDotGeoN * cosTheta(bRec.wo) <= 0) break;
+
+        bool hitEmitter = false;
+        Spec value;
+        Ray next;
+        next.o = its.p;
+        next.setDirection(wo);
+        next.mint = kEpsilon;
+        next.maxt = std::numeric_limits<float>::infinity();
+        ray = next;
+        if (scene.rayIntersect<count>(ray, its, nullptr, ctr)) {
+            const mtsg_shape &hs = scene.d.shapes[its.shape];
+            if (hs.emitter >= 0) {
+                value = dot(its.shFrame.n, -ray.d) > 0 ? Spec::of(scene.d.emitters[hs.emitter].radiance) : Spec(0.0f);
+                // dRec.setQuery(ray, its) (records.inl:170-176)
+                dRec.p = its.p;
+                dRec.n = its.shFrame.n;
+                dRec.measureSolidAngle = 1;
+                dRec.emitter = hs.emitter;
+                dRec.d = ray.d;
+                dRec.dist = its.t;
+                hitEmitter = true;
+            }
+        } else {
+            break;   // no environment emitter
+        }
+        throughput *= bsdfWeight;
+        eta *= bRec.eta;
+        if (hitEmitter && (type & EDirectSurfaceRadiance)) {
+            const float lumPdf = !(bRec.sampledType & (EDeltaReflection | EDeltaTransmission)) ? scene.pdfEmitterDirect(dRec) : 0;
+            Li += throughput * value * miWeight(bsdfPdfS, lumPdf);
+        }
+        if (!its.valid() || !(type & EIndirectSurfaceRadiance)) break;
+        type = type & ~EEmittedRadiance & ~EOpacity;
+        if (depth++ >= I.rrDepth) {
+            float q = std::min(throughput.max() * eta * eta, 0.95f);
+            if (sampler.next1D() >= q) break;
+            throughput = throughput / q;
+        }
+    }
+    depthOut = depth;
+    return Li;
+}
+
+// PerspectiveCamera::sampleRayDifferential (perspective.cpp:271-298), without differentials
+Ray cameraRay(const mtsg_camera &c, float px, float py) {
+    const float *m = c.sample_to_camera;
+    float sx = px * c.inv_res_x, sy = py * c.inv_res_y;
+    float x = m[0] * sx + m[1] * sy + m[3];
+    float y = m[4] * sx + m[5] * sy + m[7];
+    float z = m[8] * sx + m[9] * sy + m[11];
+    float w = m[12] * sx + m[13] * sy + m[15];
+    Vec nearP = w == 1.0f ? Vec(x, y, z) : Vec(x, y, z) / w;
+    Vec d = normalize(nearP);
+    float invZ = 1.0f / d.z;
+    Ray ray;
+    ray.mint = c.near_clip * invZ;
+    ray.maxt = c.far_clip * invZ;
+    const float *t = c.camera_to_world;
+    ray.o = Vec(t[3], t[7], t[11]);
+    ray.setDirection(Vec(t[0] * d.x + t[1] * d.y + t[2] * d.z, t[4] * d.x + t[5] * d.y + t[6] * d.z, t[8] * d.x + t[9] * d.y + t[10] * d.z));
+    return ray;
+}
+
+// ImageBlock::put (imageblock.h:124-204) into a tile+border block
+struct Block {
+    int ox, oy, w, h, border;   // offset of the tile, tile size
+    float *data;                // (w+2b)*(h+2b)*5
+    const mtsg_camera *cam;
+    bool put(float spx, float spy, const Spec &spec, float alpha) {
+        float value[5] = {spec.s[0], spec.s[1], spec.s[2], alpha, 1.0f};
+        for (int i = 0; i < 5; ++i)
+            if (!std::isfinite(value[i]) || value[i] < 0) return false;
+        const float r = cam->filter_radius;
+        const int W = w + 2 * border, H = h + 2 * border;
+        const float px = spx - 0.5f - (float)(ox - border), py = spy - 0.5f - (float)(oy - border);
+        int minx = std::max((int)std::ceil(px - r), 0), miny = std::max((int)std::ceil(py - r), 0);
+        int maxx = std::min((int)std::floor(px + r), W - 1), maxy = std::min((int)std::floor(py + r), H - 1);
+        float wx[8], wy[8];
+        auto disc = [&](float x) { return cam->filter_values[std::min((int)std::abs(x * cam->filter_scale), 31)]; };
+        for (int x = minx, i = 0; x <= maxx && i < 8; ++x, ++i) wx[i] = disc((float)x - px);
+        for (int y = miny, i = 0; y <= maxy && i < 8; ++y, ++i) wy[i] = disc((float)y - py);
+        for (int y = miny, yr = 0; y <= maxy; ++y, ++yr) {
+            float *dst = data + ((size_t)y * W + minx) * 5;
+            for (int x = minx, xr = 0; x <= maxx; ++x, ++xr) {
+                float weight = wx[xr] * wy[yr];
+                for (int k = 0; k < 5; ++k) *dst++ += weight * value[k];
+            }
+        }
+        return true;
+    }
+};
+
+int hwThreads(int t) { return t > 0 ? t : std::max(1u, std::thread::hardware_concurrency()); }
+
+}  // namespace
+
+namespace {
+Ray rayFrom(const float *r) {
+    Ray ray;
+    ray.o = Vec(r[0], r[1], r[2]);
+    ray.setDirection(Vec(r[3], r[4], r[5]));
+    ray.mint = r[6];
+    ray.maxt = r[7];
+    return ray;
+}
+
+template <class F>
+void parallelFor(uint32_t n, int threads, F f) {
+    int T = std::min<int>(hwThreads(threads), (int)std::max<uint32_t>(1, n / 1024 + 1));
+    std::vector<std::thread> pool;
+    std::atomic<uint32_t> next{0};
+    for (int t = 0; t < T; ++t)
+        pool.emplace_back([&]() {
+            for (;;) {
+                uint32_t b = next.fetch_add(1024);
+                if (b >= n) break;
+                uint32_t e = std::min(n, b + 1024);
+                for (uint32_t i = b; i < e; ++i) f(i);
+            }
+        });
+    for (auto &th : pool) th.join();
+}
+
+}  // namespace
+
+// ===========================================================================
+// C API
+// ===========================================================================
+struct oracle_sfmt { Sfmt s; };
+
+extern "C" {
+
+oracle_sfmt *oracle_sfmt_new(uint64_t seed) {
+    auto *r = new oracle_sfmt;
+    r->s.initGenRand(seed);
+    return r;
+}
+oracle_sfmt *oracle_sfmt_clone(oracle_sfmt *parent) {
+    auto *r = new oracle_sfmt;
+    r->s.seedFrom(parent->s);
+    return r;
+}
+uint64_t oracle_sfmt_next_ulong(oracle_sfmt *r) { return r->s.nextULong(); }
+float oracle_sfmt_next_float(oracle_sfmt *r) { return r->s.nextFloat(); }
+void oracle_sfmt_free(oracle_sfmt *r) { delete r; }
+
+float oracle_counter_float(uint32_t seed, uint64_t sample_id, uint32_t dim) {
+    return counterFloat(counterKey(seed, sample_id), dim);
+}
+
+const char *oracle_last_error(void) { return g_err.c_str(); }
+
+int oracle_trace_closest(const mtsg_scene_desc *d, uint32_t n, const float *rays, float *t, float *u, float *v,
+                         uint32_t *prim, int threads) {
+    SceneView sv(*d);
+    parallelFor(n, threads, [&](uint32_t i) {
+        Ray ray = rayFrom(rays + 8 * i);
+        Its its;
+        Cache c;
+        Counters dummy;
+        if (sv.rayIntersect<false>(ray, its, &c, &dummy)) {
+            t[i] = its.t;
+            if (c.primIndex != 0xFFFFFFFFu) { u[i] = c.u; v[i] = c.v; prim[i] = c.primIndex; }
+            else { u[i] = c.rx; v[i] = c.ry; prim[i] = 0x80000000u | d->shapes[c.shapeIndex].rect; }
+        } else {
+            t[i] = std::numeric_limits<float>::infinity();
+            u[i] = v[i] = 0;
+            prim[i] = 0xFFFFFFFFu;
+        }
+    });
+    return 0;
+}
+
+int oracle_trace_shadow(const mtsg_scene_desc *d, uint32_t n, const float *rays, uint8_t *occ, int threads) {
+    SceneView sv(*d);
+    parallelFor(n, threads, [&](uint32_t i) {
+        Counters dummy;
+        occ[i] = sv.rayIntersectShadow<false>(rayFrom(rays + 8 * i), &dummy) ? 1 : 0;
+    });
+    return 0;
+}
+
+int oracle_trace_closest_brute(const mtsg_scene_desc *d, uint32_t n, const float *rays, float *t, uint32_t *prim) {
+    SceneView sv(*d);
+    parallelFor(n, 0, [&](uint32_t i) {
+        Ray ray = rayFrom(rays + 8 * i);
+        float mint, maxt;
+        t[i] = std::numeric_limits<float>::infinity();
+        prim[i] = 0xFFFFFFFFu;
+        if (!sv.aabbIntersect(ray, mint, maxt)) return;
+        float rayMinT = ray.mint;
+        if (rayMinT == kEpsilon)
+            rayMinT *= std::max(std::max(std::max(std::abs(ray.o.x), std::abs(ray.o.y)), std::abs(ray.o.z)), kEpsilon);
+        if (rayMinT > mint) mint = rayMinT;
+        if (ray.maxt < maxt) maxt = ray.maxt;
+        if (!(maxt > mint)) return;
+        for (uint32_t p = 0; p < d->n_prims; ++p) {
+            float tt;
+            Cache c;
+            if (sv.primIntersect(ray, p, mint, maxt, tt, &c)) {
+                maxt = tt;
+                t[i] = tt;
+                prim[i] = c.primIndex != 0xFFFFFFFFu ? c.primIndex : (0x80000000u | d->triaccel[p].prim_index);
+            }
+        }
+    });
+    return 0;
+}
+
+int oracle_pixel_samples(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, float *out) {
+    SceneView sv(*d);
+    Integrator I{p->max_depth, p->rr_depth, p->strict_normals != 0, p->hide_emitters != 0};
+    for (uint32_t s = 0; s < p->spp; ++s) {
+        Sampler smp;
+        smp.mode = ORACLE_RNG_COUNTER;
+        uint64_t sid = ((uint64_t)y * d->camera.film_w + x) * p->spp + s;
+        smp.key = counterKey(p->seed, sid);
+        float a, b;
+        smp.next2D(a, b);
+        Ray ray = cameraRay(d->camera, x + a, y + b);
+        float alpha;
+        int depth;
+        Counters c;
+        Spec L = Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0);
+        out[3 * s] = L.s[0]; out[3 * s + 1] = L.s[1]; out[3 * s + 2] = L.s[2];
+    }
+    return 0;
+}
+
+int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng_mode, int threads, float *rgbaw,
+                  oracle_stats *stats) {
+    try {
+        const mtsg_camera &cam = d->camera;
+        const int B = cam.border;
+        const int W = p->tile_w + 2 * B, H = p->tile_h + 2 * B;
+        std::fill(rgbaw, rgbaw + (size_t)W * H * 5, 0.0f);
+        SceneView sv(*d);
+        Integrator I{p->max_depth, p->rr_depth, p->strict_normals != 0, p->hide_emitters != 0};
+        int T = hwThreads(threads);
+        const int BS = 32;   // scene.cpp:27 block size
+        int nbx = (p->tile_w + BS - 1) / BS, nby = (p->tile_h + BS - 1) / BS;
+        // BlockedImageProcess spiral order (imageproc.cpp:28-78)
+        std::vector<std::pair<int, int>> blocks;
+        {
+            int cx = nbx / 2, cy = nby / 2, dir = 0, stepsLeft = 1, numSteps = 1;
+            int total = nbx * nby;
+            while ((int)blocks.size() < total) {
+                if (cx >= 0 && cy >= 0 && cx < nbx && cy < nby) blocks.emplace_back(cx, cy);
+                if ((int)blocks.size() == total) break;
+                switch (dir) { case 0: ++cx; break; case 1: ++cy; break; case 2: --cx; break; default: --cy; }
+                if (--stepsLeft == 0) {
+                    dir = (dir + 1) % 4;
+                    if (dir == 0 || dir == 2) ++numSteps;
+                    stepsLeft = numSteps;
+                }
+            }
+        }
+        Sfmt parent;
+        parent.initGenRand(5489ULL);
+        std::vector<Sfmt> clones(T);
+        for (int t = 0; t < T; ++t) clones[t].seedFrom(parent);   // renderjob.cpp:57-69
+
+        std::atomic<size_t> nextBlock{0};
+        std::mutex filmMutex;
+        std::vector<Counters> ctrs(T);
+        std::vector<uint64_t> pathVerts(T, 0), samples(T, 0);
+        auto t0 = std::chrono::steady_clock::now();
+        auto worker = [&](int tid) {
+            Sampler smp;
+            smp.mode = rng_mode;
+            smp.sfmt = &clones[tid];
+            std::vector<float> local;
+            for (;;) {
+                size_t bi = nextBlock.fetch_add(1);
+                if (bi >= blocks.size()) break;
+                int bx0 = p->tile_x + blocks[bi].first * BS, by0 = p->tile_y + blocks[bi].second * BS;
+                int bw = std::min(BS, p->tile_x + p->tile_w - bx0), bh = std::min(BS, p->tile_y + p->tile_h - by0);
+                local.assign((size_t)(bw + 2 * B) * (bh + 2 * B) * 5, 0.0f);
+                Block blk{bx0, by0, bw, bh, B, local.data(), &cam};
+                for (int y = by0; y < by0 + bh; ++y)
+                    for (int x = bx0; x < bx0 + bw; ++x)
+                        for (uint32_t s = 0; s < p->spp; ++s) {
+                            if (rng_mode == ORACLE_RNG_COUNTER) {
+                                smp.key = counterKey(p->seed, ((uint64_t)y * cam.film_w + x) * p->spp + s);
+                                smp.dim = 0;
+                            }
+                            float a, b;
+                            smp.next2D(a, b);
+                            float spx = x + a, spy = y + b;
+                            Ray ray = cameraRay(cam, spx, spy);
+                            float alpha;
+                            int depth;
+                            Spec L = stats && (stats->threads < 0)
+                                         ? Li<true>(sv, I, ray, smp, alpha, depth, &ctrs[tid], cam.has_alpha != 0)
+                                         : Li<false>(sv, I, ray, smp, alpha, depth, &ctrs[tid], cam.has_alpha != 0);
+                            pathVerts[tid] += depth;
+                            samples[tid]++;
+                            blk.put(spx, spy, L, alpha);
+                        }
+                // BlockedRenderProcess::processResult -> Film::put (renderproc.cpp:142-149)
+                std::lock_guard<std::mutex> g(filmMutex);
+                for (int yy = 0; yy < bh + 2 * B; ++yy) {
+                    int fy = by0 - p->tile_y + yy;   // row in the tile block (border-relative)
+                    int fx0 = bx0 - p->tile_x;
+                    float *dst = rgbaw + ((size_t)fy * W + fx0) * 5;
+                    const float *src = local.data() + (size_t)yy * (bw + 2 * B) * 5;
+                    for (int k = 0; k < (bw + 2 * B) * 5; ++k) dst[k] += src[k];
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 0; t < T; ++t) pool.emplace_back(worker, t);
+        for (auto &th : pool) th.join();
+        double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (stats) {
+            bool counting = stats->threads < 0;
+            memset(stats, 0, sizeof(*stats));
+            stats->seconds = secs;
+            stats->threads = T;
+            for (int t = 0; t < T; ++t) {
+                stats->samples += samples[t];
+                stats->path_vertices += pathVerts[t];
+                if (counting) {
+                    stats->rays_closest += ctrs[t].closest;
+                    stats->rays_shadow += ctrs[t].shadow;
+                    stats->nodes_visited += ctrs[t].nodes;
+                    stats->leaf_refs += ctrs[t].refs;
+                    stats->tri_tests += ctrs[t].tests;
+                }
+            }
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int oracle_bsdf_sample(const mtsg_bsdf *b, const float wi[3], float s0, float s1, float wo[3], float *pdf, float weight[3]) {
+    BRec r;
+    r.wi = Vec(wi[0], wi[1], wi[2]);
+    float p = 0;
+    Spec w = bsdfSample(*b, r, p, s0, s1);
+    wo[0] = r.wo.x; wo[1] = r.wo.y; wo[2] = r.wo.z;
+    *pdf = p;
+    weight[0] = w.s[0]; weight[1] = w.s[1]; weight[2] = w.s[2];
+    return r.sampledType;
+}
+
+int oracle_bsdf_eval(const mtsg_bsdf *b, const float wi[3], const float wo[3], float value[3], float *pdf) {
+    BRec r;
+    r.wi = Vec(wi[0], wi[1], wi[2]);
+    r.wo = Vec(wo[0], wo[1], wo[2]);
+    Spec v = bsdfEval(*b, r);
+    value[0] = v.s[0]; value[1] = v.s[1]; value[2] = v.s[2];
+    *pdf = bsdfPdf(*b, r);
+    return 0;
+}
+
+}  // extern "C"

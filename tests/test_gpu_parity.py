@@ -1,0 +1,163 @@
+"""GPU parity: the HIP wavefront path (through the C-ABI) against the CPU
+oracle on identical inputs.  Bars (DESIGN.md "Parity"):
+  * traversal: identical closest primitive except exact-distance ties,
+    t/u/v within 1e-4 relative;
+  * render (counter-mode RNG, identical random numbers per pixel/sample/
+    dimension): mean per-pixel L1 of the developed image < 1e-3 of the
+    mean radiance, filter-weight channel within 1e-5 relative."""
+import os
+
+import numpy as np
+import pytest
+
+import mtsg
+from oracle import pyoracle as O
+from conftest import SCENES
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu_cbox(cbox_small):
+    g = mtsg.GPUScene(cbox_small, 0)
+    yield g
+    g.close()
+
+
+@pytest.fixture(scope="module")
+def gpu_bunny(bunny_small):
+    g = mtsg.GPUScene(bunny_small, 0)
+    yield g
+    g.close()
+
+
+def random_rays(n, lo, hi, seed, mint=1e-4):
+    rng = np.random.default_rng(seed)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = rng.uniform(lo, hi, (n, 3))
+    d = rng.normal(size=(n, 3))
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 6] = mint
+    rays[:, 7] = np.inf
+    return rays
+
+
+def compare_closest(scene, g, rays):
+    t0, u0, v0, p0 = O.trace_closest(scene.desc, rays)
+    t1, u1, v1, p1 = g.trace_closest(rays)
+    hit0, hit1 = p0 != 0xFFFFFFFF, p1 != 0xFFFFFFFF
+    assert (hit0 != hit1).mean() < 1e-4
+    both = hit0 & hit1
+    same = both & (p0 == p1)
+    # differing primitives only on (near-)ties of the hit distance
+    diff = both & (p0 != p1)
+    assert np.all(np.abs(t0[diff] - t1[diff]) <= 1e-4 * np.abs(t0[diff]) + 1e-6)
+    assert same.sum() >= 0.999 * both.sum()
+    np.testing.assert_allclose(t1[same], t0[same], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(u1[same], u0[same], rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(v1[same], v0[same], rtol=1e-3, atol=1e-4)
+    return both.mean()
+
+
+def test_device_visible():
+    assert mtsg.device_lib().mtsg_device_count() >= 1
+
+
+def test_trace_closest_cbox(cbox_small, gpu_cbox):
+    assert compare_closest(cbox_small, gpu_cbox, random_rays(100000, -0.95, 0.95, 1)) > 0.5
+
+
+def test_trace_closest_bunny_chords(bunny_small, gpu_bunny):
+    # kdbench / test_kd.cpp style incoherent chords through the instanced bunnies
+    rng = np.random.default_rng(2)
+    n = 200000
+    def sph(k):
+        v = rng.normal(size=(k, 3))
+        return v / np.linalg.norm(v, axis=1, keepdims=True)
+    c = np.array([0.0, 0.45, 0.0])
+    a = c + 3.2 * sph(n)
+    b = c + 3.2 * sph(n)
+    d = b - a
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = a; rays[:, 3:6] = d; rays[:, 6] = 0.0; rays[:, 7] = np.inf
+    assert compare_closest(bunny_small, gpu_bunny, rays) > 0.2
+
+
+def test_trace_shadow(cbox_small, gpu_cbox, bunny_small, gpu_bunny):
+    for scene, g, lo, hi in ((cbox_small, gpu_cbox, -0.9, 0.9), (bunny_small, gpu_bunny, -2.5, 2.5)):
+        rays = random_rays(100000, lo, hi, 11)
+        rays[:, 7] = np.random.default_rng(12).uniform(0.05, 3.0, len(rays))
+        o0 = O.trace_shadow(scene.desc, rays)
+        o1 = g.trace_shadow(rays)
+        assert (o0 != o1).mean() < 1e-4
+
+
+def render_pair(scene, g, **over):
+    p = scene.params(**over)
+    b = scene.border
+    img_c, _ = O.render(scene.desc, p, b, rng=O.RNG_COUNTER)
+    img_g = g.render(p, b)
+    return p, img_c, img_g
+
+
+def check_render(img_c, img_g):
+    w_c, w_g = img_c[..., 4], img_g[..., 4]
+    np.testing.assert_allclose(w_g, w_c, rtol=1e-5, atol=1e-5)
+    rgb_c, rgb_g = mtsg.develop(img_c), mtsg.develop(img_g)
+    l1 = np.abs(rgb_c - rgb_g).mean()
+    mean = rgb_c.mean()
+    assert mean > 0
+    assert l1 < 1e-3 * max(mean, 1e-3) + 1e-6, (l1, mean)
+    return l1, mean
+
+
+def test_render_cbox_parity(cbox_small, gpu_cbox):
+    _, c, g = render_pair(cbox_small, gpu_cbox)
+    check_render(c, g)
+
+
+def test_render_cbox_maxdepth_and_hide_emitters(cbox_small, gpu_cbox):
+    for over in ({"max_depth": 1}, {"max_depth": 2}, {"max_depth": 8, "hide_emitters": 1},
+                 {"max_depth": 3, "strict_normals": 1}, {"rr_depth": 1}):
+        _, c, g = render_pair(cbox_small, gpu_cbox, **over)
+        check_render(c, g)
+
+
+def test_render_tile_and_seed(cbox_small, gpu_cbox):
+    # a ragged sub-rectangle (not a multiple of the 16x16 splat tile)
+    _, c, g = render_pair(cbox_small, gpu_cbox, tile_x=5, tile_y=7, tile_w=37, tile_h=19, seed=3)
+    check_render(c, g)
+
+
+def test_render_bunny_roughconductor_parity(bunny_small, gpu_bunny):
+    _, c, g = render_pair(bunny_small, gpu_bunny)
+    check_render(c, g)
+
+
+def test_tiling_is_additive(cbox_small, gpu_cbox):
+    # film tiled over 2 "GPUs" (two calls) + additive border merge == one call
+    p = cbox_small.params()
+    b = cbox_small.border
+    full = gpu_cbox.render(p, b)
+    left = gpu_cbox.render(cbox_small.params(tile_w=32), b)
+    right = gpu_cbox.render(cbox_small.params(tile_x=32, tile_w=32), b)
+    merged = np.zeros_like(full)
+    merged[:, 0:32 + 2 * b] += left
+    merged[:, 32:64 + 2 * b] += right
+    np.testing.assert_allclose(merged, full, rtol=2e-5, atol=2e-5)
+
+
+def test_dielectric_scene_parity(tmp_path):
+    xml = open(os.path.join(SCENES, "cbox.xml")).read().replace(
+        '<!-- short box -->\n\t<shape type="cube">',
+        '<!-- short box -->\n\t<shape type="cube">\n\t\t<bsdf type="dielectric"/>').replace(
+        '\t\t</transform>\n\t\t<ref id="white"/>\n\t</shape>\n\t<!-- tall box -->',
+        '\t\t</transform>\n\t</shape>\n\t<!-- tall box -->')
+    path = tmp_path / "cbox_glass.xml"
+    path.write_text(xml)
+    scene = mtsg.Scene(str(path), {"width": 48, "height": 48, "spp": 8})
+    g = mtsg.GPUScene(scene, 0)
+    _, c, gi = render_pair(scene, g)
+    check_render(c, gi)
+    g.close()

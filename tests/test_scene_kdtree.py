@@ -1,0 +1,103 @@
+"""Host scene loading + SAH kd-tree: the tree must give the brute-force
+closest hit for every ray (traversal restated from sahkdtree3.h:178-308),
+including the test_kd.cpp chord workload through the bunny."""
+import os
+
+import numpy as np
+
+import mtsg
+from oracle import pyoracle as O
+from conftest import SCENES
+
+
+def chords(n, center, radius, seed):
+    # test_kd.cpp:112-118: chords between two uniform points on a sphere
+    rng = np.random.default_rng(seed)
+    def sph(k):
+        v = rng.normal(size=(k, 3))
+        return v / np.linalg.norm(v, axis=1, keepdims=True)
+    a = center + radius * sph(n)
+    b = center + radius * sph(n)
+    d = b - a
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = a
+    rays[:, 3:6] = d
+    rays[:, 6] = 0.0
+    rays[:, 7] = np.inf
+    return rays
+
+
+def check_against_brute(scene, rays):
+    t, u, v, prim = O.trace_closest(scene.desc, rays)
+    tb, pb = O.trace_closest_brute(scene.desc, rays)
+    hit = prim != 0xFFFFFFFF
+    assert np.array_equal(hit, pb != 0xFFFFFFFF)
+    # identical closest distance; primitive ids may differ only on exact ties
+    assert np.array_equal(t[hit], tb[hit])
+    return hit.mean()
+
+
+def test_cbox_loads(cbox_small):
+    i = cbox_small.info
+    assert i.n_triangles == 24 and i.n_rects == 6 and i.n_emitters == 1
+    assert i.film_w == 64 and i.film_h == 48 and i.spp == 8 and i.border == 2
+    p = cbox_small.params()
+    assert (p.max_depth, p.rr_depth, p.spp) == (-1, 5, 8)
+
+
+def test_cbox_kdtree_matches_brute_force(cbox_small):
+    rng = np.random.default_rng(3)
+    n = 20000
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = rng.uniform(-0.95, 0.95, (n, 3))
+    d = rng.normal(size=(n, 3))
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 6] = 1e-4     # Epsilon -> adaptive epsilon path (skdtree.cpp:126-129)
+    rays[:, 7] = np.inf
+    frac = check_against_brute(cbox_small, rays)
+    assert frac > 0.5
+
+
+def test_bunny_instances_flattened(bunny_small):
+    i = bunny_small.info
+    assert i.n_triangles == 15 * 69451 == 1041765
+    assert i.n_rects == 2
+    assert i.kd_max_depth <= 48
+
+
+def test_bunny_kdtree_chords(bunny_small):
+    # bounding sphere of one instance region; brute force over 1M triangles is
+    # O(n * prims), so keep n small
+    rays = chords(64, np.array([0.0, 0.45, 0.0]), 0.8, 7)
+    frac = check_against_brute(bunny_small, rays)
+    assert frac > 0.3
+
+
+def test_shadow_queries_consistent(cbox_small):
+    rng = np.random.default_rng(5)
+    n = 5000
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = rng.uniform(-0.9, 0.9, (n, 3))
+    d = rng.normal(size=(n, 3))
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 6] = 1e-4
+    rays[:, 7] = rng.uniform(0.05, 2.0, n)
+    occ = O.trace_shadow(cbox_small.desc, rays)
+    t, _, _, prim = O.trace_closest(cbox_small.desc, rays)
+    # a shadow ray is occluded iff a closest hit exists within [mint, maxt]
+    # (the shadow variant drops the 1e-4 floor of the adaptive epsilon)
+    closest = (prim != 0xFFFFFFFF)
+    agree = (occ.astype(bool) == closest)
+    assert agree.mean() > 0.999
+
+
+def test_bad_scene_reports_error(tmp_path):
+    p = tmp_path / "bad.xml"
+    p.write_text('<scene version="0.5.0"><integrator type="bdpt"/></scene>')
+    try:
+        mtsg.Scene(str(p))
+    except RuntimeError as e:
+        assert "bdpt" in str(e)
+    else:
+        raise AssertionError("expected an error")
