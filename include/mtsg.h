@@ -275,6 +275,12 @@ int  mtsg_trace_closest(mtsg_scene *scene, uint32_t n, const float *rays,
 int  mtsg_trace_shadow(mtsg_scene *scene, uint32_t n, const float *rays,
                        uint8_t *occluded);
 
+/* Debug/parity entry point: render params' tile (must fit one wavefront
+ * batch) and return the per-sample path radiance instead of the film:
+ * L_out[((y - tile_y) * tile_w + (x - tile_x)) * spp + s] = {R, G, B, alpha}. */
+int  mtsg_render_samples(mtsg_scene *scene, const mtsg_render_params *params,
+                         float *L_out);
+
 void mtsg_scene_destroy(mtsg_scene *scene);
 
 /* Copies the last error message of the calling thread. */

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -97,9 +98,16 @@ struct DevPaths {
     float4 *sh_c;     // NEE contribution
     uint32_t *q[2];   // path queues (ping-pong)
     uint32_t *qs;     // shadow queue
-    uint32_t *cnt;    // [0..1] queue sizes, [2] shadow size, [3] trace fetch, [4] shadow fetch
+    uint32_t *cnt;    // counters, each on its own 256-B line (see CNT_*)
     unsigned long long *ctr;  // traversal counters (nodes, refs, tests)
 };
+
+// queue / fetch counters live on separate 256-byte lines: a single
+// contended address serialises at ~11 ns per atomic (MI355X_MICROARCH.md,
+// row "dequeue"), and counters sharing a line would serialise together
+constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S = 128, CNT_FETCH = 192, CNT_SFETCH = 256, CNT_WORDS = 320;
+constexpr int HOSTCNT_STRIDE = 192;
+DEV int cnt_q(int q) { return q ? CNT_Q1 : CNT_Q0; }
 
 constexpr int TILE = 16;                    // splat tile edge (256 pixels)
 constexpr int BLOCK = 256;
@@ -128,14 +136,22 @@ DEV uint32_t wave_append(uint32_t *counter, bool pred) {
 // ---------------------------------------------------------------------------
 // primitive tests
 // ---------------------------------------------------------------------------
+// Select component `axis` of (a, b, c) with bit masks.  A ternary chain on
+// struct members gets folded by InstCombine into a load through a selected
+// address, which defeats SROA and demotes the whole ray state to scratch.
+DEV float sel3(uint32_t axis, float a, float b, float c) {
+    const uint32_t m0 = 0u - (uint32_t)(axis == 0), m1 = 0u - (uint32_t)(axis == 1), m2 = 0u - (uint32_t)(axis == 2);
+    return __uint_as_float((__float_as_uint(a) & m0) | (__float_as_uint(b) & m1) | (__float_as_uint(c) & m2));
+}
+
 // TriAccel::rayIntersect (triaccel.h:96-158)
 DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, float3 d, float mint, float maxt,
                   float &u, float &v, float &t) {
     const uint32_t k = __float_as_uint(f0.x);
-    float o_u, o_v, o_k, d_u, d_v, d_k;
-    if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
-    else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
-    else { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+    // (u, v, k) = (1,2,0) | (2,0,1) | (0,1,2): bit-mask selects (see sel3)
+    const uint32_t ku = k == 0 ? 1u : (k == 1 ? 2u : 0u), kv = k == 0 ? 2u : (k == 1 ? 0u : 1u);
+    const float o_u = sel3(ku, o.x, o.y, o.z), o_v = sel3(kv, o.x, o.y, o.z), o_k = sel3(k, o.x, o.y, o.z);
+    const float d_u = sel3(ku, d.x, d.y, d.z), d_v = sel3(kv, d.x, d.y, d.z), d_k = sel3(k, d.x, d.y, d.z);
     const float n_u = f0.y, n_v = f0.z, n_d = f0.w;
     t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
     if (!(t >= mint && t <= maxt)) return false;
@@ -169,108 +185,142 @@ DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float m
 // ---------------------------------------------------------------------------
 struct TraceCounts { uint32_t nodes, refs, tests; };
 
-template <bool SHADOW, bool COUNT>
-DEV bool kd_traverse(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, float &best, float &bu,
-                     float &bv, uint32_t &bprim, uint2 *stk, TraceCounts &cnt) {
-    const float3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+// Resumable traversal state of one ray (lives in VGPRs; the short stack in LDS).
+struct KdRay {
+    float3 o, d, inv;
+    float mint;          // clipped lower bound for primitive tests
+    float best;          // upper bound, shrinks with hits
+    float tmin, tmax;    // current node interval
+    float bu, bv;
+    uint32_t bprim;
+    uint32_t node, sp, bottom;
+    bool found;
+};
+
+// Scene-AABB clip + adaptive epsilon (skdtree.cpp:112-142 / 207-226).
+// Returns false when the ray misses the scene bounds.
+template <bool SHADOW>
+DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, KdRay &r) {
+    r.o = o;
+    r.d = d;
+    r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     // AABB::rayIntersect (aabb.h:308-338)
     float nearT = -INFINITY, farT = INFINITY;
+    bool ok = true;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        const float oi = comp(o, i), di = comp(d, i), ii = comp(inv, i);
+        const float oi = comp(o, i), di = comp(d, i), ii = comp(r.inv, i);
         if (di == 0.0f) {
-            if (oi < S.bmin[i] || oi > S.bmax[i]) return false;
+            if (oi < S.bmin[i] || oi > S.bmax[i]) ok = false;
         } else {
             float t1 = (S.bmin[i] - oi) * ii, t2 = (S.bmax[i] - oi) * ii;
             nearT = fmaxf(fminf(t1, t2), nearT);
             farT = fminf(fmaxf(t1, t2), farT);
         }
     }
-    if (!(nearT <= farT)) return false;
-    // adaptive ray epsilon (skdtree.cpp:126-129 closest, :213-216 shadow)
+    if (!ok || !(nearT <= farT)) return false;
     float rayMinT = rayMint;
     if (rayMinT == kEpsilon) {
         float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
         if (!SHADOW) m = fmaxf(m, kEpsilon);
         rayMinT *= m;
     }
-    const float mint = fmaxf(nearT, rayMinT);
-    float maxt = fminf(farT, rayMaxt);
-    if (!(maxt > mint)) return false;
+    r.mint = fmaxf(nearT, rayMinT);
+    r.best = fminf(farT, rayMaxt);
+    if (!(r.best > r.mint)) return false;
+    r.tmin = r.mint;
+    r.tmax = r.best;
+    r.node = 0;
+    r.sp = r.bottom = 0;
+    r.found = false;
+    r.bu = r.bv = 0.f;
+    r.bprim = 0xFFFFFFFFu;
+    return true;
+}
 
-    best = maxt;
-    bool found = false;
-    float tmin = mint, tmax = maxt;
-    uint32_t node = 0;
-    uint32_t sp = 0, bottom = 0;
-    for (;;) {
-        // descend to a leaf
-        uint2 n = S.nodes[node];
+// Process one leaf: descend from r.node, test the leaf's primitives, then pop
+// (or restart).  Returns true when the ray is finished.
+template <bool SHADOW, bool COUNT>
+DEV bool kd_step(const DevScene &S, KdRay &r, uint2 *stk, TraceCounts &cnt) {
+    uint32_t node = r.node;
+    float tmin = r.tmin, tmax = r.tmax;
+    uint2 n = S.nodes[node];
+    if (COUNT) cnt.nodes++;
+    while (!(n.x & 0x80000000u)) {
+        const uint32_t axis = n.x & 3u;
+        const float split = __uint_as_float(n.y);
+        const uint32_t left = node + ((n.x & ~(3u | 0x40000000u)) >> 2);
+        const float oa = sel3(axis, r.o.x, r.o.y, r.o.z);
+        const float da = sel3(axis, r.d.x, r.d.y, r.d.z);
+        const float ia = sel3(axis, r.inv.x, r.inv.y, r.inv.z);
+        float tsplit = (split - oa) * ia;
+        if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
+        const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
+        const uint32_t first = belowFirst ? left : left + 1;
+        const uint32_t second = belowFirst ? left + 1 : left;
+        if (tsplit > tmax || tsplit <= 0.0f) {
+            node = first;
+        } else if (tsplit < tmin) {
+            node = second;
+        } else {
+            stk[(r.sp & (SHORT_STACK - 1)) * TRACE_BLOCK] = make_uint2(second, __float_as_uint(tmax));
+            ++r.sp;
+            if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
+            node = first;
+            tmax = tsplit;
+        }
+        n = S.nodes[node];
         if (COUNT) cnt.nodes++;
-        while (!(n.x & 0x80000000u)) {
-            const uint32_t axis = n.x & 3u;
-            const float split = __uint_as_float(n.y);
-            const uint32_t left = node + ((n.x & ~(3u | 0x40000000u)) >> 2);
-            const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-            const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-            const float ia = axis == 0 ? inv.x : (axis == 1 ? inv.y : inv.z);
-            float tsplit = (split - oa) * ia;
-            if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
-            const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
-            const uint32_t first = belowFirst ? left : left + 1;
-            const uint32_t second = belowFirst ? left + 1 : left;
-            if (tsplit > tmax || tsplit <= 0.0f) {
-                node = first;
-            } else if (tsplit < tmin) {
-                node = second;
-            } else {
-                stk[(sp & (SHORT_STACK - 1)) * TRACE_BLOCK] = make_uint2(second, __float_as_uint(tmax));
-                ++sp;
-                if (sp - bottom > SHORT_STACK) ++bottom;
-                node = first;
-                tmax = tsplit;
-            }
-            n = S.nodes[node];
-            if (COUNT) cnt.nodes++;
-        }
-        // leaf: test every primitive against [mint, best] (skdtree.h:248-304)
-        for (uint32_t e = n.x & 0x7FFFFFFFu; e < n.y; ++e) {
-            const uint32_t p = S.indices[e];
-            if (COUNT) { cnt.refs++; cnt.tests++; }
-            const float4 f0 = S.tri[3 * p];
-            float t, u, v;
-            bool h;
-            if (__float_as_uint(f0.x) != MTSG_TRIACCEL_SHAPE) {
-                const float4 f1 = S.tri[3 * p + 1], f2 = S.tri[3 * p + 2];
-                h = tri_test(f0, f1, f2, o, d, mint, best, u, v, t);
-            } else {
-                const uint32_t ri = __float_as_uint(S.tri[3 * p + 2].w);
-                h = rect_test(S.rects[ri], o, d, mint, best, t, u, v);
-            }
-            if (h) {
-                if (SHADOW) return true;
-                best = t; bu = u; bv = v; bprim = p;
-                found = true;
-            }
-        }
-        if (found && best <= tmax) break;
-        // pop (or restart from the root if entries were dropped)
-        if (sp == bottom) {
-            if (bottom == 0) break;
-            sp = bottom = 0;
-            tmin = tmax;
-            tmax = best;
-            if (!(tmin < tmax)) break;
-            node = 0;
-            continue;
-        }
-        --sp;
-        const uint2 e = stk[(sp & (SHORT_STACK - 1)) * TRACE_BLOCK];
-        node = e.x;
-        tmin = tmax;
-        tmax = fminf(__uint_as_float(e.y), best);
     }
-    return found;
+    // leaf: test every primitive against [mint, best] (skdtree.h:248-304)
+    for (uint32_t e = n.x & 0x7FFFFFFFu; e < n.y; ++e) {
+        const uint32_t p = S.indices[e];
+        if (COUNT) { cnt.refs++; cnt.tests++; }
+        const float4 f0 = S.tri[3 * p];
+        float t, u, v;
+        bool h;
+        if (__float_as_uint(f0.x) != MTSG_TRIACCEL_SHAPE) {
+            const float4 f1 = S.tri[3 * p + 1], f2 = S.tri[3 * p + 2];
+            h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+        } else {
+            const uint32_t ri = __float_as_uint(S.tri[3 * p + 2].w);
+            h = rect_test(S.rects[ri], r.o, r.d, r.mint, r.best, t, u, v);
+        }
+        if (h) {
+            r.found = true;
+            if (SHADOW) return true;
+            r.best = t; r.bu = u; r.bv = v; r.bprim = p;
+        }
+    }
+    // Havran exits once the leaf's exit distance exceeds the best hit
+    // (`stack[exPt].t > maxt`, sahkdtree3.h:299): on an exact tie the next
+    // leaf is still visited, and a coplanar primitive there can win
+    if (r.found && r.best < tmax) return true;
+    // pop (or restart from the root if entries were dropped)
+    if (r.sp == r.bottom) {
+        if (r.bottom == 0) return true;
+        r.sp = r.bottom = 0;
+        r.tmin = tmax;
+        r.tmax = r.best;
+        r.node = 0;
+        return !(r.tmin < r.tmax);
+    }
+    --r.sp;
+    const uint2 e = stk[(r.sp & (SHORT_STACK - 1)) * TRACE_BLOCK];
+    r.node = e.x;
+    r.tmin = tmax;
+    r.tmax = fminf(__uint_as_float(e.y), r.best);
+    return false;
+}
+
+template <bool SHADOW, bool COUNT>
+DEV bool kd_traverse(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, float &best, float &bu,
+                     float &bv, uint32_t &bprim, uint2 *stk, TraceCounts &cnt) {
+    KdRay r;
+    if (!kd_init<SHADOW>(S, o, d, rayMint, rayMaxt, r)) return false;
+    while (!kd_step<SHADOW, COUNT>(S, r, stk, cnt)) {}
+    best = r.best; bu = r.bu; bv = r.bv; bprim = r.bprim;
+    return r.found;
 }
 
 // ---------------------------------------------------------------------------
@@ -289,61 +339,145 @@ DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
     if (lane_id() == 0) { atomicAdd(ctr + 0, a); atomicAdd(ctr + 1, b); atomicAdd(ctr + 2, t); }
 }
 
-// Persistent closest-hit kernel: each wave fetches 64 queue entries at a time.
-template <bool COUNT>
-__global__ void __launch_bounds__(TRACE_BLOCK) k_trace_closest(DevScene S, DevPaths P, int qin, int cntIdx) {
+// Persistent traversal kernel with lane-level refill (the "while-while +
+// dynamic fetch" structure of Aila & Laine 2009, re-tiled for 64-lane waves):
+// a wave reserves FETCH queue entries with ONE atomic into a wave-uniform
+// pool (SGPRs), and lanes whose ray finished take the next pool entries after
+// every leaf, so SIMD lanes stay busy and the contended fetch counter sees
+// 1/FETCH of the rays.
+//   SHADOW = false: closest hit of queue qin (qin < 0: identity over nIdentity
+//                   slots, bounce 0), result -> P.hit
+//   SHADOW = true : any hit of the shadow queue; unoccluded -> L += contribution
+// Classic persistent kernel: a wave takes ROUNDS x 64 consecutive queue
+// entries per atomic and traces them 64 at a time (one ray per lane, no refill).
+template <bool SHADOW, bool COUNT, int ROUNDS>
+__global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
     __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
     uint2 *stk = stack + threadIdx.x;
-    const uint32_t count = *((volatile uint32_t *)&P.cnt[cntIdx]);
-    const uint32_t *q = P.q[qin];
+    uint32_t count = nIdentity;
+    if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
+    else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
+    const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
+    uint32_t *fetch = &P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH];
     TraceCounts c{0, 0, 0};
     for (;;) {
         uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(&P.cnt[3], 64u);
+        if (lane_id() == 0) base = atomicAdd(fetch, 64u * ROUNDS);
         base = __shfl(base, 0);
         if (base >= count) break;
-        const uint32_t i = base + lane_id();
-        if (i < count) {
-            const uint32_t slot = q[i];
-            const float4 ro = P.ray_o[slot], rd = P.ray_d[slot];
+        for (int rnd = 0; rnd < ROUNDS; ++rnd) {
+            const uint32_t i = base + 64u * rnd + lane_id();
+            if (i >= count) break;
+            const uint32_t slot = q ? q[i] : i;
+            float4 ro, rd;
+            if (SHADOW) { ro = P.sh_o[slot]; rd = P.sh_d[slot]; rd.w = ro.w; ro.w = kEpsilon; }
+            else { ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
+            if (!SHADOW && rd.w < 0.0f) continue;   // dead slot
             float best, u = 0, v = 0;
             uint32_t prim = 0xFFFFFFFFu;
-            bool hit = kd_traverse<false, COUNT>(S, xyz(ro), xyz(rd), ro.w, rd.w, best, u, v, prim, stk, c);
-            P.hit[slot] = hit ? make_float4(best, u, v, __uint_as_float(prim))
-                              : make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
-        }
-    }
-    flush_counts<COUNT>(P.ctr, c);
-}
-
-// Persistent shadow kernel (skdtree.cpp:207-226); unoccluded -> L += contribution
-template <bool COUNT>
-__global__ void __launch_bounds__(TRACE_BLOCK) k_trace_shadow(DevScene S, DevPaths P) {
-    __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
-    uint2 *stk = stack + threadIdx.x;
-    const uint32_t count = *((volatile uint32_t *)&P.cnt[2]);
-    TraceCounts c{0, 0, 0};
-    for (;;) {
-        uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(&P.cnt[4], 64u);
-        base = __shfl(base, 0);
-        if (base >= count) break;
-        const uint32_t i = base + lane_id();
-        if (i < count) {
-            const uint32_t slot = P.qs[i];
-            const float4 so = P.sh_o[slot], sd = P.sh_d[slot];
-            float best, u, v;
-            uint32_t prim;
-            bool occ = kd_traverse<true, COUNT>(S, xyz(so), xyz(sd), kEpsilon, so.w, best, u, v, prim, stk, c);
-            if (!occ) {
-                const float4 con = P.sh_c[slot];
-                float4 L = P.L[slot];
-                L.x += con.x; L.y += con.y; L.z += con.z;
-                P.L[slot] = L;
+            const bool hit = kd_traverse<SHADOW, COUNT>(S, xyz(ro), xyz(rd), ro.w, rd.w, best, u, v, prim, stk, c);
+            if (SHADOW) {
+                if (!hit) {
+                    const float4 con = P.sh_c[slot];
+                    float4 L = P.L[slot];
+                    L.x += con.x; L.y += con.y; L.z += con.z;
+                    P.L[slot] = L;
+                }
+            } else {
+                P.hit[slot] = hit ? make_float4(best, u, v, __uint_as_float(prim))
+                                  : make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
             }
         }
     }
-    flush_counts<COUNT>(P.ctr + 3, c);
+    flush_counts<COUNT>(P.ctr + (SHADOW ? 3 : 0), c);
+}
+
+constexpr uint32_t FETCH = 256;
+
+template <bool SHADOW, bool COUNT, int MIN_IDLE>
+__global__ void __launch_bounds__(TRACE_BLOCK) k_trace(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
+    __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
+    uint2 *stk = stack + threadIdx.x;
+    uint32_t count = nIdentity;   // explicit branches: a ternary over a volatile load
+    if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);   // demotes the argument to scratch
+    else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
+    const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
+    uint32_t *fetch = &P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH];
+    TraceCounts c{0, 0, 0};
+    uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
+    bool exhausted = false;
+    bool active = false;
+    uint32_t slot = 0;
+    KdRay r;
+    const unsigned long long below = (1ull << lane_id()) - 1ull;
+    for (;;) {
+        // ---- refill idle lanes from the wave's pool
+        unsigned long long idle = __ballot(!active);
+        // refill only once MIN_IDLE lanes are idle (or the wave has nothing left)
+        if ((uint32_t)__popcll(idle) < (uint32_t)MIN_IDLE && __any(active)) idle = 0;
+        while (idle && !exhausted) {
+            if (poolLeft == 0) {
+                uint32_t b = 0;
+                if (lane_id() == 0) b = atomicAdd(fetch, FETCH);
+                b = __shfl(b, 0);
+                if (b >= count) { exhausted = true; break; }
+                poolBase = b;
+                poolLeft = min(FETCH, count - b);
+            }
+            const uint32_t nIdle = (uint32_t)__popcll(idle);
+            const uint32_t take = min(nIdle, poolLeft);
+            const uint32_t rank = (uint32_t)__popcll(idle & below);
+            bool got = false;
+            if (!active && rank < take) {
+                const uint32_t i = poolBase + rank;
+                slot = q ? q[i] : i;
+                float4 ro, rd;
+                if (SHADOW) { ro = P.sh_o[slot]; rd = P.sh_d[slot]; rd.w = ro.w; ro.w = kEpsilon; }
+                else { ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
+                got = true;
+                if (!SHADOW && rd.w < 0.0f) {
+                    got = false;   // dead slot (outside the render rectangle): no hit record needed
+                } else if (kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r)) {
+                    active = true;
+                } else {
+                    // misses the scene bounds: finish immediately
+                    if (SHADOW) {
+                        const float4 con = P.sh_c[slot];
+                        float4 L = P.L[slot];
+                        L.x += con.x; L.y += con.y; L.z += con.z;
+                        P.L[slot] = L;
+                    } else {
+                        P.hit[slot] = make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+                    }
+                }
+            }
+            (void)got;
+            poolBase += take;
+            poolLeft -= take;
+            idle = __ballot(!active);
+            if (take == nIdle) break;
+        }
+        if (!__any(active)) {
+            if (exhausted) break;
+            continue;
+        }
+        // ---- one leaf of traversal for the active lanes
+        if (active && kd_step<SHADOW, COUNT>(S, r, stk, c)) {
+            active = false;
+            if (SHADOW) {
+                if (!r.found) {
+                    const float4 con = P.sh_c[slot];
+                    float4 L = P.L[slot];
+                    L.x += con.x; L.y += con.y; L.z += con.z;
+                    P.L[slot] = L;
+                }
+            } else {
+                P.hit[slot] = r.found ? make_float4(r.best, r.bu, r.bv, __uint_as_float(r.bprim))
+                                      : make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+            }
+        }
+    }
+    flush_counts<COUNT>(P.ctr + (SHADOW ? 3 : 0), c);
 }
 
 // Debug entry points over caller-provided rays
@@ -417,11 +551,12 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
             P.key[slot] = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
             P.st[slot] = make_uint2(1u, 2u);   // depth 1, next dimension 2
         } else {
+            // dead slot: bounce 0 runs over the identity queue and skips it
+            P.ray_d[slot] = make_float4(0.f, 0.f, 1.f, -1.0f);
+            P.st[slot] = make_uint2(0u, 0u);
             P.L[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
-    const uint32_t qi = wave_append(&P.cnt[0], alive);
-    if (alive) P.q[0][qi] = slot;
 }
 
 // ---------------------------------------------------------------------------
@@ -800,23 +935,53 @@ DEV void emitter_sample_position(const DevScene &S, const mtsg_emitter &em, floa
     }
 }
 
-DEV void enqueue_path(const DevPaths &P, uint32_t *cnt, uint32_t *q, bool pred, uint32_t slot) {
-    const uint32_t i = wave_append(cnt, pred);
-    if (pred) q[i] = slot;
+// Block-aggregated queue append: one LDS atomic per wave, one global atomic
+// per workgroup and queue (a contended global word costs ~11 ns per atomic).
+struct BlockAppend {
+    uint32_t cnt[2];
+    uint32_t base[2];
+};
+
+DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p0, bool p1, uint32_t &i0, uint32_t &i1) {
+    if (threadIdx.x == 0) { ba.cnt[0] = 0; ba.cnt[1] = 0; }
+    __syncthreads();
+    const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1);
+    const unsigned long long below = (1ull << lane_id()) - 1ull;
+    uint32_t w0 = 0, w1 = 0;
+    if (lane_id() == 0) {
+        if (m0) w0 = atomicAdd(&ba.cnt[0], (uint32_t)__popcll(m0));
+        if (m1) w1 = atomicAdd(&ba.cnt[1], (uint32_t)__popcll(m1));
+    }
+    w0 = __shfl(w0, 0);
+    w1 = __shfl(w1, 0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ba.base[0] = ba.cnt[0] ? atomicAdd(gcnt0, ba.cnt[0]) : 0u;
+        ba.base[1] = ba.cnt[1] ? atomicAdd(gcnt1, ba.cnt[1]) : 0u;
+    }
+    __syncthreads();
+    i0 = ba.base[0] + w0 + (uint32_t)__popcll(m0 & below);
+    i1 = ba.base[1] + w1 + (uint32_t)__popcll(m1 & below);
 }
 
+// qin < 0: bounce 0 over the identity queue of nIdentity slots
 __global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, DevPaths P, int bounce, int qin,
-                                                 int cntIn, int hasAlpha) {
-    const uint32_t count = *((volatile uint32_t *)&P.cnt[cntIn]);
+                                                 uint32_t nIdentity, int hasAlpha) {
+    __shared__ BlockAppend ba;
+    uint32_t count = nIdentity;
+    if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     const uint32_t nIter = (count + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
-    const int qout = qin ^ 1;
+    const int qout = qin < 0 ? 1 : (qin ^ 1);
     for (uint32_t it = 0; it < nIter; ++it) {
         const uint32_t i = (it * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
         bool alive = i < count;
         bool cont = false, shadow = false;
         uint32_t slot = 0;
         if (alive) {
-            slot = P.q[qin][i];
+            slot = qin < 0 ? i : P.q[qin][i];
+            if (qin < 0 && P.st[slot].x == 0u) alive = false;   // dead slot
+        }
+        if (alive) {
             const float4 h = P.hit[slot];
             const float4 ro4 = P.ray_o[slot], rd4 = P.ray_d[slot];
             const float3 ro = xyz(ro4), rd = xyz(rd4);
@@ -939,8 +1104,10 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, De
                 P.st[slot] = make_uint2(depth | flags, dim);
             }
         }
-        enqueue_path(P, &P.cnt[2], P.qs, shadow, slot);
-        enqueue_path(P, &P.cnt[cntIn ^ 1], P.q[qout], cont, slot);
+        uint32_t is, ic;
+        block_append2(ba, &P.cnt[CNT_S], &P.cnt[cnt_q(qout)], shadow, cont, is, ic);
+        if (shadow) P.qs[is] = slot;
+        if (cont) P.q[qout][ic] = slot;
     }
 }
 
@@ -951,77 +1118,107 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, De
 // ---------------------------------------------------------------------------
 constexpr int MAX_BORDER = 4;
 constexpr int LT = TILE + 2 * MAX_BORDER;   // LDS tile edge
+constexpr int SPLAT_CHUNK = 16;             // samples per pixel per workgroup
 
-__global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P, float *film,
-                                                 int blockW, int blockH) {
-    __shared__ float acc[5][LT * LT];
-    const int ch = C.has_alpha ? 5 : 4;
-    for (int k = threadIdx.x; k < 5 * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
-    __syncthreads();
+// One workgroup = one 16x16 tile x one chunk of SPLAT_CHUNK samples per pixel.
+// Each thread owns one pixel: all its samples fall in [x, x+1) x [y, y+1), so
+// their filter footprints lie in the K x K window centred on the pixel
+// (K = 2 * border + 1).  The thread accumulates that window in registers
+// (weights of texels outside a sample's [ceil, floor] range are exactly 0,
+// as evalDiscretized returns m_values[31] = 0 there), then the workgroup
+// reduces the windows into an LDS tile in K*K conflict-free phases (each
+// phase shifts every window by the same offset, so no two threads touch the
+// same texel: no atomics, fixed order) and flushes the tile with one float
+// atomic per texel and channel into the HBM ImageBlock.
+template <int K, int CH>
+__global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevBatch B, DevPaths P, float *film, int blockW, int blockH) {
+    __shared__ float acc[CH][LT * LT];
+    constexpr int R = K / 2;
+    for (int k = threadIdx.x; k < CH * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
     const int tl = blockIdx.x;
     const int tile = B.toffset + (B.tile0 + tl) * B.tstride;
     const int tx = tile % B.tiles_x, ty = tile / B.tiles_x;
     const int x0 = B.rect_x + tx * TILE, y0 = B.rect_y + ty * TILE;   // tile origin (film coords)
     const int bord = C.border;
-    const float r = C.filter_radius;
     const int pix = threadIdx.x;
-    const int x = x0 + (pix % TILE), y = y0 + (pix / TILE);
+    const int lx = pix % TILE, ly = pix / TILE;
+    const int x = x0 + lx, y = y0 + ly;
     const bool inside = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
+    // block (tile rect + border) bounds relative to the window origin (x - R, y - R)
+    const int bx0 = (B.rect_x - bord) - (x - R), by0 = (B.rect_y - bord) - (y - R);
+    float win[K][K][CH];
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int h = 0; h < CH; ++h) win[r][c][h] = 0.0f;
+    const uint32_t sBeg = blockIdx.y * SPLAT_CHUNK, sEnd = min(B.ns, sBeg + SPLAT_CHUNK);
     if (inside) {
-        for (uint32_t sl = 0; sl < B.ns; ++sl) {
+        for (uint32_t sl = sBeg; sl < sEnd; ++sl) {
             const uint32_t slot = ((uint32_t)tl * B.ns + sl) * (TILE * TILE) + pix;
             const float4 L = P.L[slot];
             const uint2 kk = P.key[slot];
             const uint64_t key = (uint64_t)kk.x | ((uint64_t)kk.y << 32);
-            const float spx = (float)x + counterFloat(key, 0), spy = (float)y + counterFloat(key, 1);
             // invalid samples are rejected (imageblock.h:147-151)
             if (!(isfinite(L.x) && isfinite(L.y) && isfinite(L.z) && L.x >= 0 && L.y >= 0 && L.z >= 0)) continue;
-            // position relative to the LDS tile origin (x0 - MAX_BORDER)
-            const float px = spx - 0.5f - (float)(x0 - MAX_BORDER), py = spy - 0.5f - (float)(y0 - MAX_BORDER);
-            // clamp to the block of this render call (tile rect + border)
-            const int bx0 = B.rect_x - bord - (x0 - MAX_BORDER), by0 = B.rect_y - bord - (y0 - MAX_BORDER);
-            const int bx1 = bx0 + blockW - 1, by1 = by0 + blockH - 1;
-            const int minx = max((int)ceilf(px - r), max(bx0, 0)), miny = max((int)ceilf(py - r), max(by0, 0));
-            const int maxx = min((int)floorf(px + r), min(bx1, LT - 1)), maxy = min((int)floorf(py + r), min(by1, LT - 1));
-            for (int yy = miny; yy <= maxy; ++yy) {
-                const float wy = C.filter_values[min((int)fabsf(((float)yy - py) * C.filter_scale), 31)];
-                for (int xx = minx; xx <= maxx; ++xx) {
-                    const float wgt = C.filter_values[min((int)fabsf(((float)xx - px) * C.filter_scale), 31)] * wy;
-                    const int o = yy * LT + xx;
-                    atomicAdd(&acc[0][o], wgt * L.x);
-                    atomicAdd(&acc[1][o], wgt * L.y);
-                    atomicAdd(&acc[2][o], wgt * L.z);
-                    if (ch == 5) atomicAdd(&acc[3][o], wgt * L.w);
-                    atomicAdd(&acc[4][o], wgt);
-                }
+            // sample position relative to the window origin, as ImageBlock::put
+            // computes it relative to the block origin (imageblock.h:158-160)
+            const float px = ((float)x + counterFloat(key, 0)) - 0.5f - (float)(x - R);
+            const float py = ((float)y + counterFloat(key, 1)) - 0.5f - (float)(y - R);
+            float wx[K], wy[K];
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const bool okx = c >= bx0 && c < bx0 + blockW;
+                const bool oky = c >= by0 && c < by0 + blockH;
+                wx[c] = okx ? C.filter_values[min((int)fabsf(((float)c - px) * C.filter_scale), 31)] : 0.0f;
+                wy[c] = oky ? C.filter_values[min((int)fabsf(((float)c - py) * C.filter_scale), 31)] : 0.0f;
             }
+            const float v[5] = {L.x, L.y, L.z, L.w, 1.0f};
+#pragma unroll
+            for (int r = 0; r < K; ++r)
+#pragma unroll
+                for (int c = 0; c < K; ++c) {
+                    const float w = wx[c] * wy[r];
+#pragma unroll
+                    for (int h = 0; h < CH; ++h) win[r][c][h] += w * v[CH == 5 ? h : (h == 3 ? 4 : h)];
+                }
         }
     }
     __syncthreads();
+    // K*K shifted phases: texel (ly + r + MAX_BORDER - R, lx + c + MAX_BORDER - R)
+#pragma unroll
+    for (int r = 0; r < K; ++r)
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const int o = (ly + r + MAX_BORDER - R) * LT + (lx + c + MAX_BORDER - R);
+#pragma unroll
+            for (int h = 0; h < CH; ++h) acc[h][o] += win[r][c][h];
+            __syncthreads();
+        }
     // flush into the HBM block (blockW x blockH x 5, origin = rect - border)
     for (int k = threadIdx.x; k < LT * LT; k += BLOCK) {
-        const int ly = k / LT, lx = k % LT;
-        const int fx = x0 - MAX_BORDER + lx - (B.rect_x - bord), fy = y0 - MAX_BORDER + ly - (B.rect_y - bord);
+        const int ty2 = k / LT, tx2 = k % LT;
+        const int fx = x0 - MAX_BORDER + tx2 - (B.rect_x - bord), fy = y0 - MAX_BORDER + ty2 - (B.rect_y - bord);
         if (fx < 0 || fy < 0 || fx >= blockW || fy >= blockH) continue;
-        const float w = acc[4][k];
+        const float w = acc[CH - 1][k];
         if (w == 0.0f) continue;
         float *dst = film + ((size_t)fy * blockW + fx) * 5;
         unsafeAtomicAdd(dst + 0, acc[0][k]);
         unsafeAtomicAdd(dst + 1, acc[1][k]);
         unsafeAtomicAdd(dst + 2, acc[2][k]);
-        unsafeAtomicAdd(dst + 3, ch == 5 ? acc[3][k] : w);   // no alpha channel: alpha == 1 per sample
+        unsafeAtomicAdd(dst + 3, CH == 5 ? acc[3][k] : w);   // no alpha channel: alpha == 1 per sample
         unsafeAtomicAdd(dst + 4, w);
     }
 }
 
-__global__ void k_reset(uint32_t *cnt, int next, int cntCur) {
-    // zero the next queue, shadow queue and fetch counters for this bounce
+__global__ void k_reset(uint32_t *cnt, int qout) {
+    // zero this bounce's output queue, the shadow queue and the fetch counters
     if (threadIdx.x == 0) {
-        cnt[next] = 0;
-        cnt[2] = 0;
-        cnt[3] = 0;
-        cnt[4] = 0;
-        (void)cntCur;
+        cnt[qout ? CNT_Q1 : CNT_Q0] = 0;
+        cnt[CNT_S] = 0;
+        cnt[CNT_FETCH] = 0;
+        cnt[CNT_SFETCH] = 0;
     }
 }
 
@@ -1065,6 +1262,8 @@ struct mtsg_scene {
     int cuCount = 0;
     int traceGrid = 0, shadeGrid = 0;
     uint32_t flags = 0;
+    int traceMode = 0;
+    float *dumpL = nullptr;
     std::atomic<int> cancel{0};
     mtsg_stats stats{};
     std::vector<hipEvent_t> evPool;
@@ -1101,7 +1300,7 @@ int ensure_batch(mtsg_scene *s, uint32_t paths) {
     A(key, uint2); A(st, uint2); A(sh_o, float4); A(sh_d, float4); A(sh_c, float4);
     A(q[0], uint32_t); A(q[1], uint32_t); A(qs, uint32_t);
 #undef A
-    if ((rc = alloc(64 * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
+    if ((rc = alloc(CNT_WORDS * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
     if ((rc = alloc(8 * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
     HIP_TRY(hipMemset(P.ctr, 0, 8 * sizeof(unsigned long long)));
     s->capacity = paths;
@@ -1130,6 +1329,25 @@ void timed_launch(mtsg_scene *s, int kind, F f) {
     s->timed.emplace_back(kind, i0);
 }
 
+// Traversal kernel variants (MTSG_TRACE_MODE, for measurement):
+//   0 = wave fetch 64 / atomic, 1 = wave fetch 4x64 / atomic,
+//   2 = lane refill at >= 1 idle lane, 3 = lane refill at >= 32 idle lanes
+template <bool SHADOW, bool COUNT>
+void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
+    dim3 g(s->traceGrid), blk(TRACE_BLOCK);
+    switch (s->traceMode) {
+        case 0: hipLaunchKernelGGL((k_trace_wave<SHADOW, COUNT, 1>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 1: hipLaunchKernelGGL((k_trace_wave<SHADOW, COUNT, 4>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 2: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 1>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        default: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+    }
+}
+template <bool SHADOW>
+void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int qin, uint32_t n) {
+    if (count) launch_trace_c<SHADOW, true>(s, P, qin, n);
+    else launch_trace_c<SHADOW, false>(s, P, qin, n);
+}
+
 int validate(const mtsg_render_params *p, const mtsg_scene *s) {
     if (!p) { g_err = "null params"; return MTSG_ERR_INVALID; }
     if (p->spp == 0) { g_err = "spp must be > 0"; return MTSG_ERR_INVALID; }
@@ -1153,6 +1371,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     if ((rc = set_device(s)) != MTSG_OK) return rc;
     auto t0 = std::chrono::steady_clock::now();
     const uint32_t maxPaths = s->requestedBatch ? s->requestedBatch : (1u << 22);
+    if (s->dumpL && (uint64_t)p->tile_w * p->tile_h * p->spp > maxPaths) { g_err = "render_samples: tile does not fit one batch"; return MTSG_ERR_INVALID; }
     const uint32_t tilesX = (uint32_t)(p->tile_w + TILE - 1) / TILE, tilesY = (uint32_t)(p->tile_h + TILE - 1) / TILE;
     const uint32_t allTiles = tilesX * tilesY;
     const uint32_t tstride = p->tile_stride > 1 ? (uint32_t)p->tile_stride : 1u;
@@ -1187,42 +1406,32 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             B.s0 = s0;
             B.ns = std::min(sppPerBatch, p->spp - s0);
             B.nslots = (uint32_t)B.ntiles * B.ns * TILE * TILE;
-            HIP_TRY(hipMemsetAsync(P.cnt, 0, 64 * sizeof(uint32_t), s->stream));
+            HIP_TRY(hipMemsetAsync(P.cnt, 0, CNT_WORDS * sizeof(uint32_t), s->stream));
             timed_launch(s, K_CAMERA, [&]() {
                 hipLaunchKernelGGL(k_camera, dim3((B.nslots + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s->stream, s->cam, I, B, P);
             });
-            int cur = 0;
             const int maxBounces = p->max_depth > 0 ? p->max_depth : 1 << 30;
             int last = -1;
+            // bounce b consumes queue qin(b) (identity for b = 0) and produces qout(b) = (b & 1) ^ 1
             auto account = [&](int bb) {
-                // hostCnt slot of bounce bb: [consumed queue, produced queue, shadow]
-                const uint32_t *hc = s->hostCnt + 4 * (bb & 1);
-                const int c = bb & 1;   // queue index consumed by bounce bb
-                s->stats.rays_closest += hc[c];
-                s->stats.rays_shadow += hc[2];
+                const uint32_t *hc = s->hostCnt + HOSTCNT_STRIDE * (bb & 1);
+                const uint32_t consumed = bb == 0 ? B.nslots : hc[(bb & 1) ? CNT_Q1 : CNT_Q0];
+                s->stats.rays_closest += consumed;
+                s->stats.rays_shadow += hc[CNT_S];
                 s->stats.launches_trace_closest++;
-                return hc[c ^ 1];
+                return hc[((bb & 1) ^ 1) ? CNT_Q1 : CNT_Q0];
             };
             for (int b = 0; b < maxBounces; ++b) {
-                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, cur ^ 1, cur);
-                timed_launch(s, K_CLOSEST, [&]() {
-                    if (count)
-                        hipLaunchKernelGGL(k_trace_closest<true>, dim3(s->traceGrid), dim3(TRACE_BLOCK), 0, s->stream, s->ds, P, cur, cur);
-                    else
-                        hipLaunchKernelGGL(k_trace_closest<false>, dim3(s->traceGrid), dim3(TRACE_BLOCK), 0, s->stream, s->ds, P, cur, cur);
-                });
+                const int qin = b == 0 ? -1 : (b & 1);
+                const int qout = (b & 1) ^ 1;
+                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, qout);
+                timed_launch(s, K_CLOSEST, [&]() { launch_trace<false>(s, count, P, qin, B.nslots); });
                 timed_launch(s, K_SHADE, [&]() {
-                    hipLaunchKernelGGL(k_shade, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, P, b, cur, cur, s->cam.has_alpha);
+                    hipLaunchKernelGGL(k_shade, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, P, b, qin, B.nslots, s->cam.has_alpha);
                 });
-                timed_launch(s, K_SHADOW, [&]() {
-                    if (count)
-                        hipLaunchKernelGGL(k_trace_shadow<true>, dim3(s->traceGrid), dim3(TRACE_BLOCK), 0, s->stream, s->ds, P);
-                    else
-                        hipLaunchKernelGGL(k_trace_shadow<false>, dim3(s->traceGrid), dim3(TRACE_BLOCK), 0, s->stream, s->ds, P);
-                });
-                HIP_TRY(hipMemcpyAsync(s->hostCnt + 4 * (b & 1), P.cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+                timed_launch(s, K_SHADOW, [&]() { launch_trace<true>(s, count, P, 0, 0u); });
+                HIP_TRY(hipMemcpyAsync(s->hostCnt + HOSTCNT_STRIDE * (b & 1), P.cnt, (CNT_S + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
                 HIP_TRY(hipEventRecord(cntEv[b & 1], s->stream));
-                cur ^= 1;
                 last = b;
                 if (b >= 1) {
                     // lagged check: if bounce b-1 produced nothing, bounce b was empty
@@ -1235,9 +1444,31 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 account(last);
             }
             timed_launch(s, K_SPLAT, [&]() {
-                hipLaunchKernelGGL(k_splat, dim3(B.ntiles), dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
+                dim3 g(B.ntiles, (B.ns + SPLAT_CHUNK - 1) / SPLAT_CHUNK);
+                const int K = 2 * s->cam.border + 1;
+                if (K == 5 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<5, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
+                else if (K == 5) hipLaunchKernelGGL((k_splat<5, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
+                else if (K <= 3 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<3, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
+                else if (K <= 3) hipLaunchKernelGGL((k_splat<3, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
+                else if (!s->cam.has_alpha) hipLaunchKernelGGL((k_splat<9, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
+                else hipLaunchKernelGGL((k_splat<9, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
             });
             s->stats.samples += (uint64_t)B.nslots;
+            if (s->dumpL) {
+                // debug: copy the batch's per-slot radiance (single batch only)
+                std::vector<float4> L(B.nslots);
+                HIP_TRY(hipMemcpyAsync(L.data(), P.L, B.nslots * sizeof(float4), hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(hipStreamSynchronize(s->stream));
+                for (uint32_t slot = 0; slot < B.nslots; ++slot) {
+                    const uint32_t pix = slot & (TILE * TILE - 1), rest = slot >> 8;
+                    const uint32_t sl = rest % B.ns, tl = rest / B.ns;
+                    const int tile = B.toffset + (B.tile0 + (int)tl) * B.tstride;
+                    const int x = (tile % B.tiles_x) * TILE + (int)(pix % TILE), y = (tile / B.tiles_x) * TILE + (int)(pix / TILE);
+                    if (x >= p->tile_w || y >= p->tile_h) continue;
+                    float *o = s->dumpL + (((size_t)y * p->tile_w + x) * p->spp + B.s0 + sl) * 4;
+                    o[0] = L[slot].x; o[1] = L[slot].y; o[2] = L[slot].z; o[3] = L[slot].w;
+                }
+            }
         }
     }
     hipError_t e = hipStreamSynchronize(s->stream);
@@ -1370,11 +1601,12 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     memcpy(c.filter_values, hc.filter_values, sizeof(c.filter_values));
     // persistent grids from the occupancy query
     int perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace_closest<false>, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace_wave<false, false, 4>, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;
+    if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     s->shadeGrid = s->cuCount * 8;
-    if (hipHostMalloc((void **)&s->hostCnt, 16 * sizeof(uint32_t)) != hipSuccess) { g_err = "pinned alloc"; return fail(MTSG_ERR_OOM); }
+    if (hipHostMalloc((void **)&s->hostCnt, 2 * HOSTCNT_STRIDE * sizeof(uint32_t)) != hipSuccess) { g_err = "pinned alloc"; return fail(MTSG_ERR_OOM); }
     *out = s;
     return MTSG_OK;
 }
@@ -1452,6 +1684,14 @@ int mtsg_render(mtsg_scene *s, const mtsg_render_params *p, float *rgbaw_out) {
         if (e != hipSuccess) { g_err = hipGetErrorString(e); rc = MTSG_ERR_DEVICE; }
     }
     hipFree(film);
+    return rc;
+}
+
+int mtsg_render_samples(mtsg_scene *s, const mtsg_render_params *p, float *L_out) {
+    if (!s || !L_out) { g_err = "null argument"; return MTSG_ERR_INVALID; }
+    s->dumpL = L_out;
+    int rc = mtsg_render(s, p, std::vector<float>((size_t)(p->tile_w + 2 * s->cam.border) * (p->tile_h + 2 * s->cam.border) * 5).data());
+    s->dumpL = nullptr;
     return rc;
 }
 

@@ -79,7 +79,8 @@ DEVICE_SYMBOLS = [
     "mtsg_device_count", "mtsg_scene_create", "mtsg_render", "mtsg_render_device",
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths",
-    "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_scene_destroy", "mtsg_last_error",
+    "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
+    "mtsg_last_error",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_scene_desc", "mtsh_scene_render_params",
@@ -113,7 +114,8 @@ def device_lib() -> C.CDLL:
     """The HIP library.  Raises (never falls back) when it is missing."""
     global _dev
     if _dev is None:
-        path = os.path.join(PKG_DIR, "libmtsg.so")
+        # MTSG_LIB: alternative in-tree build (measurement experiments only)
+        path = os.path.join(PKG_DIR, os.environ.get("MTSG_LIB", "libmtsg.so"))
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is missing: the HIP extension was not built "
                                "(run `make device` / __graft_entry__.build()); no CPU fallback exists")
@@ -133,6 +135,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_trace_closest.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_trace_shadow.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        lib.mtsg_render_samples.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
         lib.mtsg_scene_destroy.argtypes = [C.c_void_p]
         lib.mtsg_last_error.argtypes = [C.c_char_p, C.c_size_t]
         _dev = lib
@@ -220,6 +223,12 @@ class GPUScene:
     def render(self, params: RenderParams, border: int) -> np.ndarray:
         out = np.zeros((params.tile_h + 2 * border, params.tile_w + 2 * border, 5), dtype=np.float32)
         self._check(device_lib().mtsg_render(self._h, C.byref(params), _ptr(out)), "mtsg_render")
+        return out
+
+    def render_samples(self, params: RenderParams) -> np.ndarray:
+        """Per-sample radiance (tile_h, tile_w, spp, 4) -- debug/parity entry point."""
+        out = np.zeros((params.tile_h, params.tile_w, params.spp, 4), dtype=np.float32)
+        self._check(device_lib().mtsg_render_samples(self._h, C.byref(params), _ptr(out)), "mtsg_render_samples")
         return out
 
     def set_flags(self, flags: int) -> None:

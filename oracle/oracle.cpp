@@ -11,6 +11,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <limits>
 #include <mutex>
@@ -21,6 +22,8 @@
 namespace {
 
 thread_local std::string g_err;
+int g_debug = 0;   // oracle_debug_pixel_sample(): print the path to stderr
+#define DBG(...) do { if (g_debug) fprintf(stderr, __VA_ARGS__); } while (0)
 
 // ---------------------------------------------------------------------------
 // math (include/mitsuba/core/vector.h, frame.h)
@@ -994,6 +997,7 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
     int depth = 1;
     // RadianceQueryRecord::rayIntersect (records.inl:117-143)
     scene.rayIntersect<count>(ray, its, nullptr, ctr);
+    DBG("camera o=(%g %g %g) d=(%g %g %g) mint=%g maxt=%g -> t=%g shape=%d p=(%g %g %g)\n", ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z, ray.mint, ray.maxt, its.t, its.shape, its.p.x, its.p.y, its.p.z);
     alpha = 1.0f;
     if (type & EOpacity) alpha = its.valid() ? 1.0f : 0.0f;
     ray.mint = kEpsilon;
@@ -1022,6 +1026,7 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
             float s0, s1;
             sampler.next2D(s0, s1);
             Spec value = scene.sampleEmitterDirect<count>(dRec, s0, s1, ctr);
+            DBG("  depth %d NEE s=(%g %g) value=(%g %g %g) pdf=%g d=(%g %g %g) dist=%g\n", depth, s0, s1, value.s[0], value.s[1], value.s[2], dRec.pdf, dRec.d.x, dRec.d.y, dRec.d.z, dRec.dist);
             if (!value.isZero()) {
                 BRec bRec;
                 bRec.wi = its.wi;
@@ -1041,6 +1046,7 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
         float s0, s1;
         sampler.next2D(s0, s1);
         Spec bsdfWeight = bsdfSample(bsdf, bRec, bsdfPdfS, s0, s1);
+        DBG("  depth %d bsdf type=%d s=(%g %g) wi=(%g %g %g) wo=(%g %g %g) w=(%g %g %g) pdf=%g sampled=%d\n", depth, bsdf.type, s0, s1, bRec.wi.x, bRec.wi.y, bRec.wi.z, bRec.wo.x, bRec.wo.y, bRec.wo.z, bsdfWeight.s[0], bsdfWeight.s[1], bsdfWeight.s[2], bsdfPdfS, bRec.sampledType);
         if (bsdfWeight.isZero()) break;
         scattered |= bRec.sampledType != 0;
         const Vec wo = its.toWorld(bRec.wo);
@@ -1055,7 +1061,9 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
         next.mint = kEpsilon;
         next.maxt = std::numeric_limits<float>::infinity();
         ray = next;
-        if (scene.rayIntersect<count>(ray, its, nullptr, ctr)) {
+        bool hitNext = scene.rayIntersect<count>(ray, its, nullptr, ctr);
+        DBG("  trace o=(%g %g %g) d=(%g %g %g) -> hit=%d t=%g shape=%d p=(%g %g %g) n=(%g %g %g)\n", ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z, (int)hitNext, its.t, its.shape, its.p.x, its.p.y, its.p.z, its.shFrame.n.x, its.shFrame.n.y, its.shFrame.n.z);
+        if (hitNext) {
             const mtsg_shape &hs = scene.d.shapes[its.shape];
             if (hs.emitter >= 0) {
                 value = dot(its.shFrame.n, -ray.d) > 0 ? Spec::of(scene.d.emitters[hs.emitter].radiance) : Spec(0.0f);
@@ -1086,6 +1094,7 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
         }
     }
     depthOut = depth;
+    DBG("  -> L=(%g %g %g) depth=%d\n", Li.s[0], Li.s[1], Li.s[2], depth);
     return Li;
 }
 
@@ -1252,6 +1261,27 @@ int oracle_trace_closest_brute(const mtsg_scene_desc *d, uint32_t n, const float
             }
         }
     });
+    return 0;
+}
+
+int oracle_debug_pixel_sample(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, int s) {
+    std::vector<float> out(3 * p->spp);
+    g_debug = 1;
+    mtsg_render_params q = *p;
+    SceneView sv(*d);
+    Integrator I{p->max_depth, p->rr_depth, p->strict_normals != 0, p->hide_emitters != 0};
+    Sampler smp;
+    smp.mode = ORACLE_RNG_COUNTER;
+    smp.key = counterKey(p->seed, ((uint64_t)y * d->camera.film_w + x) * p->spp + s);
+    float a, b;
+    smp.next2D(a, b);
+    Ray ray = cameraRay(d->camera, x + a, y + b);
+    float alpha;
+    int depth;
+    Counters c;
+    Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0);
+    g_debug = 0;
+    (void)q;
     return 0;
 }
 

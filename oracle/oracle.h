@@ -66,6 +66,9 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
 int oracle_pixel_samples(const mtsg_scene_desc *d, const mtsg_render_params *p,
                          int x, int y, float *out);
 
+/* Print the path of one counter-mode sample to stderr (debugging). */
+int oracle_debug_pixel_sample(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, int s);
+
 /* BSDF / emitter building blocks for statistical tests (local frame). */
 /* sample: returns weight (3), pdf, wo(3), sampled type flags */
 int oracle_bsdf_sample(const mtsg_bsdf *b, const float wi[3], float s0, float s1,
