@@ -173,16 +173,20 @@ def main():
         nodes_per_ray = cs.nodes_visited / max(1, rays_c)
         refs_per_ray = cs.leaf_refs / max(1, rays_c)
         tests_per_ray = cs.tri_tests / max(1, rays_c)
-        # B_ray = 8 nodes + 4 leaf refs + 48 TriAccel tests, plus the
-        # ray record in (32 B), hit out (16 B) and the queue index (4 B)
-        b_ray = 8 * nodes_per_ray + 4 * refs_per_ray + 48 * tests_per_ray + 32 + 16 + 4
+        # Algorithmic bytes per closest-hit ray in the device layout (DESIGN.md
+        # "Roofline"): one 16-B sibling-pair load per inner node descended, one
+        # 48-B TriAccel record per primitive test (leaf-ordered, no index
+        # indirection), the 32-B ray record in, the 16-B hit out, the 4-B queue
+        # entry.  (SURVEY §8d's Mitsuba-layout figure, 8 B/node + 4 B/ref +
+        # 48 B/test, is reported beside it as bytes_per_ray_mitsuba_layout.)
+        b_ray = 16 * nodes_per_ray + 48 * tests_per_ray + 32 + 16 + 4
         launches = max(1, st.launches_trace_closest)
         bytes_per_launch = b_ray * st.rays_closest / launches
         avg_launch_s = st.ms_trace_closest / 1e3 / launches
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "k_trace_closest", "bytes_per_ray": round(b_ray, 1),
+                    "kernel": "k_trace<closest>", "bytes_per_ray": round(b_ray, 1),
                     "nodes_per_ray": round(nodes_per_ray, 2), "leaf_refs_per_ray": round(refs_per_ray, 2),
                     "tri_tests_per_ray": round(tests_per_ray, 2), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                     "launches_per_frame": launches}

@@ -28,6 +28,7 @@
 #include <string>
 #include <vector>
 #include <chrono>
+#include <functional>
 
 #include "../../include/mtsg.h"
 #include "device_math.h"
@@ -40,9 +41,14 @@ namespace {
 // device-side scene and path state
 // ---------------------------------------------------------------------------
 struct DevScene {
-    const uint2 *__restrict__ nodes;
-    const uint32_t *__restrict__ indices;
-    const float4 *__restrict__ tri;        // 3 float4 per prim (TriAccel)
+    // device kd-tree layout (built from Mitsuba's KDNode array at upload):
+    //   node (8 B)  inner: axis | pairIndex << 2, split  /  leaf: 1<<31 | start, end
+    //   pairs[k]    = {left child node, right child node} -> one 16 B load per step
+    //   triL        = TriAccel records copied in leaf order (3 float4 each)
+    const uint4 *__restrict__ pairs;
+    const float4 *__restrict__ triL;
+    uint2 root;
+    const float4 *__restrict__ tri;        // 3 float4 per prim (TriAccel, prim order)
     const float4 *__restrict__ vpos;       // xyz
     const float4 *__restrict__ vnrm;       // xyz
     const uint4 *__restrict__ tidx;        // i0, i1, i2, shape
@@ -105,13 +111,22 @@ struct DevPaths {
 // queue / fetch counters live on separate 256-byte lines: a single
 // contended address serialises at ~11 ns per atomic (MI355X_MICROARCH.md,
 // row "dequeue"), and counters sharing a line would serialise together
-constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S = 128, CNT_FETCH = 192, CNT_SFETCH = 256, CNT_WORDS = 320;
+constexpr int XGROUPS = 8;                  // XCDs: blocks b and b + 8 share one
+constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S = 128;
+constexpr int CNT_FETCH = 192;                           // XGROUPS counters, 32 words apart
+constexpr int CNT_SFETCH = CNT_FETCH + 32 * XGROUPS;     // XGROUPS counters, 32 words apart
+constexpr int CNT_WORDS = CNT_SFETCH + 32 * XGROUPS;
 constexpr int HOSTCNT_STRIDE = 192;
 DEV int cnt_q(int q) { return q ? CNT_Q1 : CNT_Q0; }
 
 constexpr int TILE = 16;                    // splat tile edge (256 pixels)
 constexpr int BLOCK = 256;
 constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traversal
+// Paths per wavefront batch (172 B of SoA state per path -> 5.5 GiB of HBM).
+// Each bounce launch needs several rays per resident lane to amortise the
+// slowest rays (tail) -- measured on the 1M-triangle scene: 4M paths 421,
+// 16M 629, 32M 698 Msamples/s.
+constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 25;
 constexpr int SHORT_STACK = 8;              // LDS short stack entries per lane
 
 // ---------------------------------------------------------------------------
@@ -192,9 +207,16 @@ struct KdRay {
     float best;          // upper bound, shrinks with hits
     float tmin, tmax;    // current node interval
     float bu, bv;
-    uint32_t bprim;
-    uint32_t node, sp, bottom;
-    bool found;
+    uint32_t bprim;      // triangle index, or 0x80000000 | rectangle index
+    uint2 cur;           // current node
+    uint32_t sp, bottom;
+    uint32_t found;
+};
+
+// LDS short stack: far-child node data and its exit distance, SoA by lane
+struct KdStack {
+    uint2 *node;
+    float *t;
 };
 
 // Scene-AABB clip + adaptive epsilon (skdtree.cpp:112-142 / 207-226).
@@ -230,66 +252,62 @@ DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float ray
     if (!(r.best > r.mint)) return false;
     r.tmin = r.mint;
     r.tmax = r.best;
-    r.node = 0;
+    r.cur = S.root;
     r.sp = r.bottom = 0;
-    r.found = false;
+    r.found = 0;
     r.bu = r.bv = 0.f;
     r.bprim = 0xFFFFFFFFu;
     return true;
 }
 
-// Process one leaf: descend from r.node, test the leaf's primitives, then pop
-// (or restart).  Returns true when the ray is finished.
+// Process one leaf: descend from r.cur (one 16-byte sibling-pair load per
+// inner node), test the leaf's primitives, then pop (or restart).  Returns
+// true when the ray is finished.
 template <bool SHADOW, bool COUNT>
-DEV bool kd_step(const DevScene &S, KdRay &r, uint2 *stk, TraceCounts &cnt) {
-    uint32_t node = r.node;
+DEV bool kd_step(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
+    uint2 n = r.cur;
     float tmin = r.tmin, tmax = r.tmax;
-    uint2 n = S.nodes[node];
-    if (COUNT) cnt.nodes++;
     while (!(n.x & 0x80000000u)) {
         const uint32_t axis = n.x & 3u;
         const float split = __uint_as_float(n.y);
-        const uint32_t left = node + ((n.x & ~(3u | 0x40000000u)) >> 2);
+        const uint4 pr = S.pairs[n.x >> 2];
+        if (COUNT) cnt.nodes++;
         const float oa = sel3(axis, r.o.x, r.o.y, r.o.z);
         const float da = sel3(axis, r.d.x, r.d.y, r.d.z);
         const float ia = sel3(axis, r.inv.x, r.inv.y, r.inv.z);
         float tsplit = (split - oa) * ia;
         if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
         const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
-        const uint32_t first = belowFirst ? left : left + 1;
-        const uint32_t second = belowFirst ? left + 1 : left;
+        const uint2 first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
+        const uint2 second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
         if (tsplit > tmax || tsplit <= 0.0f) {
-            node = first;
+            n = first;
         } else if (tsplit < tmin) {
-            node = second;
+            n = second;
         } else {
-            stk[(r.sp & (SHORT_STACK - 1)) * TRACE_BLOCK] = make_uint2(second, __float_as_uint(tmax));
+            const uint32_t k = (r.sp & (SHORT_STACK - 1)) * TRACE_BLOCK;
+            stk.node[k] = second;
+            stk.t[k] = tmax;
             ++r.sp;
             if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
-            node = first;
+            n = first;
             tmax = tsplit;
         }
-        n = S.nodes[node];
-        if (COUNT) cnt.nodes++;
     }
     // leaf: test every primitive against [mint, best] (skdtree.h:248-304)
     for (uint32_t e = n.x & 0x7FFFFFFFu; e < n.y; ++e) {
-        const uint32_t p = S.indices[e];
         if (COUNT) { cnt.refs++; cnt.tests++; }
-        const float4 f0 = S.tri[3 * p];
+        const float4 f0 = S.triL[3 * e], f1 = S.triL[3 * e + 1], f2 = S.triL[3 * e + 2];
         float t, u, v;
         bool h;
-        if (__float_as_uint(f0.x) != MTSG_TRIACCEL_SHAPE) {
-            const float4 f1 = S.tri[3 * p + 1], f2 = S.tri[3 * p + 2];
-            h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-        } else {
-            const uint32_t ri = __float_as_uint(S.tri[3 * p + 2].w);
-            h = rect_test(S.rects[ri], r.o, r.d, r.mint, r.best, t, u, v);
-        }
+        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
+        if (!isRect) h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+        else h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
         if (h) {
-            r.found = true;
+            r.found = 1;
             if (SHADOW) return true;
-            r.best = t; r.bu = u; r.bv = v; r.bprim = p;
+            r.best = t; r.bu = u; r.bv = v;
+            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
         }
     }
     // Havran exits once the leaf's exit distance exceeds the best hit
@@ -302,20 +320,20 @@ DEV bool kd_step(const DevScene &S, KdRay &r, uint2 *stk, TraceCounts &cnt) {
         r.sp = r.bottom = 0;
         r.tmin = tmax;
         r.tmax = r.best;
-        r.node = 0;
+        r.cur = S.root;
         return !(r.tmin < r.tmax);
     }
     --r.sp;
-    const uint2 e = stk[(r.sp & (SHORT_STACK - 1)) * TRACE_BLOCK];
-    r.node = e.x;
+    const uint32_t k = (r.sp & (SHORT_STACK - 1)) * TRACE_BLOCK;
+    r.cur = stk.node[k];
     r.tmin = tmax;
-    r.tmax = fminf(__uint_as_float(e.y), r.best);
+    r.tmax = fminf(stk.t[k], r.best);
     return false;
 }
 
 template <bool SHADOW, bool COUNT>
 DEV bool kd_traverse(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, float &best, float &bu,
-                     float &bv, uint32_t &bprim, uint2 *stk, TraceCounts &cnt) {
+                     float &bv, uint32_t &bprim, KdStack stk, TraceCounts &cnt) {
     KdRay r;
     if (!kd_init<SHADOW>(S, o, d, rayMint, rayMaxt, r)) return false;
     while (!kd_step<SHADOW, COUNT>(S, r, stk, cnt)) {}
@@ -348,110 +366,140 @@ DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
 //   SHADOW = false: closest hit of queue qin (qin < 0: identity over nIdentity
 //                   slots, bounce 0), result -> P.hit
 //   SHADOW = true : any hit of the shadow queue; unoccluded -> L += contribution
+#define KD_STACK_DECL                                                   \
+    __shared__ uint2 stkNode[SHORT_STACK * TRACE_BLOCK];                \
+    __shared__ float stkT[SHORT_STACK * TRACE_BLOCK];                   \
+    KdStack stk{stkNode + threadIdx.x, stkT + threadIdx.x};
+
+// XCD-partitioned work fetch: the queue is cut into XGROUPS contiguous
+// ranges; workgroup b draws from range b % XGROUPS first (blocks b, b + 8
+// share an XCD, so coherent neighbouring rays share that XCD's L2) and then
+// steals from the other ranges.  Each range has its own fetch counter on its
+// own cache line (a contended word serialises at ~11 ns per atomic).
+struct Fetch {
+    uint32_t *ctr;
+    uint32_t count;
+    uint32_t group;    // range currently drained (wave-uniform)
+    uint32_t tried;
+    DEV uint32_t lo(uint32_t g) const { return (uint32_t)(((uint64_t)count * g) / XGROUPS); }
+    // returns false when every range is exhausted; else [base, base + n)
+    DEV bool next(uint32_t want, uint32_t &base, uint32_t &n) {
+        while (tried < XGROUPS) {
+            const uint32_t beg = lo(group), end = lo(group + 1);
+            uint32_t off = 0;
+            if (__lane_id() == 0) off = atomicAdd(&ctr[32 * group], want);
+            off = __shfl(off, 0);
+            if (beg + off < end) {
+                base = beg + off;
+                n = min(want, end - base);
+                return true;
+            }
+            group = (group + 1) % XGROUPS;
+            ++tried;
+        }
+        return false;
+    }
+};
+
+DEV void shadow_unoccluded(const DevPaths &P, uint32_t slot) {
+    const float4 con = P.sh_c[slot];
+    float4 L = P.L[slot];
+    L.x += con.x; L.y += con.y; L.z += con.z;
+    P.L[slot] = L;
+}
+
+DEV void load_ray(const DevPaths &P, bool shadow, uint32_t slot, float4 &ro, float4 &rd) {
+    if (shadow) { ro = P.sh_o[slot]; rd = P.sh_d[slot]; rd.w = ro.w; ro.w = kEpsilon; }
+    else { ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
+}
+
+DEV float4 hit_record(const KdRay &r) {
+    return r.found ? make_float4(r.best, r.bu, r.bv, __uint_as_float(r.bprim))
+                   : make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+}
+
 // Classic persistent kernel: a wave takes ROUNDS x 64 consecutive queue
 // entries per atomic and traces them 64 at a time (one ray per lane, no refill).
 template <bool SHADOW, bool COUNT, int ROUNDS>
 __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
-    __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
-    uint2 *stk = stack + threadIdx.x;
+    KD_STACK_DECL
     uint32_t count = nIdentity;
     if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
-    uint32_t *fetch = &P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH];
+    Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
     TraceCounts c{0, 0, 0};
-    for (;;) {
-        uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(fetch, 64u * ROUNDS);
-        base = __shfl(base, 0);
-        if (base >= count) break;
-        for (int rnd = 0; rnd < ROUNDS; ++rnd) {
-            const uint32_t i = base + 64u * rnd + lane_id();
-            if (i >= count) break;
+    uint32_t base, n;
+    while (F.next(64u * ROUNDS, base, n)) {
+        for (uint32_t rnd = 0; rnd * 64 < n; ++rnd) {
+            const uint32_t i = base + 64u * rnd + __lane_id();
+            if (i >= base + n) break;
             const uint32_t slot = q ? q[i] : i;
             float4 ro, rd;
-            if (SHADOW) { ro = P.sh_o[slot]; rd = P.sh_d[slot]; rd.w = ro.w; ro.w = kEpsilon; }
-            else { ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
+            load_ray(P, SHADOW, slot, ro, rd);
             if (!SHADOW && rd.w < 0.0f) continue;   // dead slot
-            float best, u = 0, v = 0;
-            uint32_t prim = 0xFFFFFFFFu;
-            const bool hit = kd_traverse<SHADOW, COUNT>(S, xyz(ro), xyz(rd), ro.w, rd.w, best, u, v, prim, stk, c);
-            if (SHADOW) {
-                if (!hit) {
-                    const float4 con = P.sh_c[slot];
-                    float4 L = P.L[slot];
-                    L.x += con.x; L.y += con.y; L.z += con.z;
-                    P.L[slot] = L;
-                }
-            } else {
-                P.hit[slot] = hit ? make_float4(best, u, v, __uint_as_float(prim))
-                                  : make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
-            }
+            KdRay r;
+            const bool live = kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
+            r.found = 0;
+            if (live) while (!kd_step<SHADOW, COUNT>(S, r, stk, c)) {}
+            if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
+            else P.hit[slot] = hit_record(r);
         }
     }
     flush_counts<COUNT>(P.ctr + (SHADOW ? 3 : 0), c);
 }
 
+// Persistent traversal kernel with lane-level refill (the "while-while +
+// dynamic fetch" structure of Aila & Laine 2009, re-tiled for 64-lane waves):
+// a wave reserves FETCH queue entries with ONE atomic into a wave-uniform
+// pool (SGPRs), and once MIN_IDLE lanes have finished their rays they take
+// the next pool entries, so SIMD lanes stay busy and the fetch counters see
+// 1/FETCH of the rays.
+//   SHADOW = false: closest hit of queue qin (qin < 0: identity over nIdentity
+//                   slots, bounce 0), result -> P.hit
+//   SHADOW = true : any hit of the shadow queue; unoccluded -> L += contribution
 constexpr uint32_t FETCH = 256;
 
 template <bool SHADOW, bool COUNT, int MIN_IDLE>
 __global__ void __launch_bounds__(TRACE_BLOCK) k_trace(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
-    __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
-    uint2 *stk = stack + threadIdx.x;
+    KD_STACK_DECL
     uint32_t count = nIdentity;   // explicit branches: a ternary over a volatile load
     if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);   // demotes the argument to scratch
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
-    uint32_t *fetch = &P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH];
+    Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
     TraceCounts c{0, 0, 0};
     uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
     bool exhausted = false;
     bool active = false;
     uint32_t slot = 0;
     KdRay r;
-    const unsigned long long below = (1ull << lane_id()) - 1ull;
+    const unsigned long long below = (1ull << __lane_id()) - 1ull;
     for (;;) {
         // ---- refill idle lanes from the wave's pool
         unsigned long long idle = __ballot(!active);
         // refill only once MIN_IDLE lanes are idle (or the wave has nothing left)
         if ((uint32_t)__popcll(idle) < (uint32_t)MIN_IDLE && __any(active)) idle = 0;
         while (idle && !exhausted) {
-            if (poolLeft == 0) {
-                uint32_t b = 0;
-                if (lane_id() == 0) b = atomicAdd(fetch, FETCH);
-                b = __shfl(b, 0);
-                if (b >= count) { exhausted = true; break; }
-                poolBase = b;
-                poolLeft = min(FETCH, count - b);
-            }
+            if (poolLeft == 0 && !F.next(FETCH, poolBase, poolLeft)) { exhausted = true; break; }
             const uint32_t nIdle = (uint32_t)__popcll(idle);
             const uint32_t take = min(nIdle, poolLeft);
             const uint32_t rank = (uint32_t)__popcll(idle & below);
-            bool got = false;
             if (!active && rank < take) {
                 const uint32_t i = poolBase + rank;
                 slot = q ? q[i] : i;
                 float4 ro, rd;
-                if (SHADOW) { ro = P.sh_o[slot]; rd = P.sh_d[slot]; rd.w = ro.w; ro.w = kEpsilon; }
-                else { ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
-                got = true;
+                load_ray(P, SHADOW, slot, ro, rd);
                 if (!SHADOW && rd.w < 0.0f) {
-                    got = false;   // dead slot (outside the render rectangle): no hit record needed
+                    // dead slot (outside the render rectangle): no hit record needed
                 } else if (kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r)) {
                     active = true;
+                } else if (SHADOW) {
+                    shadow_unoccluded(P, slot);   // misses the scene bounds
                 } else {
-                    // misses the scene bounds: finish immediately
-                    if (SHADOW) {
-                        const float4 con = P.sh_c[slot];
-                        float4 L = P.L[slot];
-                        L.x += con.x; L.y += con.y; L.z += con.z;
-                        P.L[slot] = L;
-                    } else {
-                        P.hit[slot] = make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
-                    }
+                    P.hit[slot] = make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
                 }
             }
-            (void)got;
             poolBase += take;
             poolLeft -= take;
             idle = __ballot(!active);
@@ -464,17 +512,8 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace(DevScene S, DevPaths P, i
         // ---- one leaf of traversal for the active lanes
         if (active && kd_step<SHADOW, COUNT>(S, r, stk, c)) {
             active = false;
-            if (SHADOW) {
-                if (!r.found) {
-                    const float4 con = P.sh_c[slot];
-                    float4 L = P.L[slot];
-                    L.x += con.x; L.y += con.y; L.z += con.z;
-                    P.L[slot] = L;
-                }
-            } else {
-                P.hit[slot] = r.found ? make_float4(r.best, r.bu, r.bv, __uint_as_float(r.bprim))
-                                      : make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
-            }
+            if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
+            else P.hit[slot] = hit_record(r);
         }
     }
     flush_counts<COUNT>(P.ctr + (SHADOW ? 3 : 0), c);
@@ -484,22 +523,18 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace(DevScene S, DevPaths P, i
 template <bool SHADOW>
 __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_rays(DevScene S, const float *rays, uint32_t n, float *t,
                                                             float *u, float *v, uint32_t *prim, uint8_t *occ) {
-    __shared__ uint2 stack[SHORT_STACK * TRACE_BLOCK];
-    uint2 *stk = stack + threadIdx.x;
+    KD_STACK_DECL
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float *r = rays + 8 * (size_t)i;
+    const float *rr = rays + 8 * (size_t)i;
     TraceCounts c{0, 0, 0};
     float best, bu = 0, bv = 0;
     uint32_t bp = 0xFFFFFFFFu;
-    bool h = kd_traverse<SHADOW, false>(S, mk3(r[0], r[1], r[2]), mk3(r[3], r[4], r[5]), r[6], r[7], best, bu, bv, bp, stk, c);
+    bool h = kd_traverse<SHADOW, false>(S, mk3(rr[0], rr[1], rr[2]), mk3(rr[3], rr[4], rr[5]), rr[6], rr[7], best, bu, bv, bp, stk, c);
     if (SHADOW) {
         occ[i] = h ? 1 : 0;
     } else if (h) {
-        // report triangle index, or 0x80000000 | rect for analytic rectangles
-        const float4 f0 = S.tri[3 * bp];
-        uint32_t id = __float_as_uint(S.tri[3 * bp + 2].w);
-        prim[i] = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE ? (0x80000000u | id) : id;
+        prim[i] = bp;   // triangle index, or 0x80000000 | rectangle index
         t[i] = best; u[i] = bu; v[i] = bv;
     } else {
         prim[i] = 0xFFFFFFFFu;
@@ -876,10 +911,9 @@ struct Its {
 
 // ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428) + computeShadingFrame (util.cpp:603-608)
 DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, Its &its) {
-    const uint32_t p = __float_as_uint(h.w);
-    const float4 f0 = S.tri[3 * p];
+    const uint32_t p = __float_as_uint(h.w);   // triangle, or 0x80000000 | rectangle
     float3 dpdu, n;
-    if (__float_as_uint(f0.x) != MTSG_TRIACCEL_SHAPE) {
+    if (!(p & 0x80000000u)) {
         const uint4 ti = S.tidx[p];
         its.shape = (int)ti.w;
         const float bx = 1 - h.y - h.z, by = h.y, bz = h.z;
@@ -896,8 +930,7 @@ DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, Its &its) {
         }
         its.geoN = fn;
     } else {
-        const uint32_t ri = __float_as_uint(S.tri[3 * p + 2].w);
-        const mtsg_rect &r = S.rects[ri];
+        const mtsg_rect &r = S.rects[p & 0x7FFFFFFFu];
         its.shape = (int)r.shape_index;
         its.geoN = ld3(r.frame_n);
         n = its.geoN;
@@ -1217,8 +1250,10 @@ __global__ void k_reset(uint32_t *cnt, int qout) {
     if (threadIdx.x == 0) {
         cnt[qout ? CNT_Q1 : CNT_Q0] = 0;
         cnt[CNT_S] = 0;
-        cnt[CNT_FETCH] = 0;
-        cnt[CNT_SFETCH] = 0;
+    }
+    if (threadIdx.x < XGROUPS) {
+        cnt[CNT_FETCH + 32 * threadIdx.x] = 0;
+        cnt[CNT_SFETCH + 32 * threadIdx.x] = 0;
     }
 }
 
@@ -1262,7 +1297,7 @@ struct mtsg_scene {
     int cuCount = 0;
     int traceGrid = 0, shadeGrid = 0;
     uint32_t flags = 0;
-    int traceMode = 0;
+    int traceMode = 3;
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
     mtsg_stats stats{};
@@ -1370,7 +1405,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     if ((rc = validate(p, s)) != MTSG_OK) return rc;
     if ((rc = set_device(s)) != MTSG_OK) return rc;
     auto t0 = std::chrono::steady_clock::now();
-    const uint32_t maxPaths = s->requestedBatch ? s->requestedBatch : (1u << 22);
+    const uint32_t maxPaths = s->requestedBatch ? s->requestedBatch : DEFAULT_BATCH_PATHS;
     if (s->dumpL && (uint64_t)p->tile_w * p->tile_h * p->spp > maxPaths) { g_err = "render_samples: tile does not fit one batch"; return MTSG_ERR_INVALID; }
     const uint32_t tilesX = (uint32_t)(p->tile_w + TILE - 1) / TILE, tilesY = (uint32_t)(p->tile_h + TILE - 1) / TILE;
     const uint32_t allTiles = tilesX * tilesY;
@@ -1572,10 +1607,45 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         if (r == MTSG_OK && *dst) s->allocs.push_back((void *)*dst);
         return r;
     };
-    uint2 *nodes; uint32_t *indices; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu; uint4 *dtidx;
+    // ---- device kd-tree layout from Mitsuba's KDNode array (same splits and
+    // leaves, re-laid out): sibling pairs + leaf-ordered TriAccel copies
+    std::vector<uint4> pairs;
+    std::vector<float4> triL;
+    pairs.reserve(d->n_nodes / 2 + 1);
+    triL.reserve((size_t)d->n_indices * 3);
+    bool layoutOk = true;
+    std::function<uint2(uint32_t, int)> convert = [&](uint32_t ni, int depth) -> uint2 {
+        const mtsg_kdnode &N = d->nodes[ni];
+        if (depth > 64 || ni >= d->n_nodes) { layoutOk = false; return make_uint2(0x80000000u, 0u); }
+        if (N.combined & 0x80000000u) {
+            const uint32_t start = (uint32_t)(triL.size() / 3);
+            for (uint32_t e = N.combined & 0x7FFFFFFFu; e < N.data; ++e) {
+                const uint32_t p = e < d->n_indices ? d->indices[e] : 0xFFFFFFFFu;
+                if (p >= d->n_prims) { layoutOk = false; break; }
+                const float4 *t = (const float4 *)(d->triaccel + p);
+                triL.push_back(t[0]); triL.push_back(t[1]); triL.push_back(t[2]);
+            }
+            return make_uint2(0x80000000u | start, (uint32_t)(triL.size() / 3));
+        }
+        const uint32_t left = ni + ((N.combined & ~(3u | 0x40000000u)) >> 2);
+        const uint32_t pi = (uint32_t)pairs.size();
+        pairs.push_back(make_uint4(0, 0, 0, 0));
+        const uint2 L = convert(left, depth + 1);
+        const uint2 R = convert(left + 1, depth + 1);
+        pairs[pi] = make_uint4(L.x, L.y, R.x, R.y);
+        return make_uint2((N.combined & 3u) | (pi << 2), N.data);
+    };
+    const uint2 root = convert(0, 0);
+    if (!layoutOk || pairs.size() >= (1u << 29) || triL.size() / 3 >= (1u << 31)) {
+        g_err = "malformed or oversized kd-tree";
+        return fail(MTSG_ERR_INVALID);
+    }
+    if (pairs.empty()) pairs.push_back(make_uint4(0, 0, 0, 0));
+    if (triL.empty()) triL.resize(3, make_float4(0, 0, 0, 0));
+    uint4 *dpairs; float4 *dtriL; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu; uint4 *dtidx;
     mtsg_rect *rects; mtsg_shape *shapes; mtsg_bsdf *bsdfs; mtsg_emitter *emitters; float *ecdf, *etcdf;
-    if ((rc = up((const uint2 *)d->nodes, d->n_nodes, &nodes)) ||
-        (rc = up(d->indices, d->n_indices, &indices)) ||
+    if ((rc = up(pairs.data(), pairs.size(), &dpairs)) ||
+        (rc = up(triL.data(), triL.size(), &dtriL)) ||
         (rc = up((const float4 *)d->triaccel, (size_t)d->n_prims * 3, &tri)) ||
         (rc = up(vpos.data(), vpos.size(), &dvpos)) || (rc = up(vnrm.data(), vnrm.size(), &dvnrm)) ||
         (rc = up(tidx.data(), tidx.size(), &dtidx)) || (rc = up(tdpdu.data(), tdpdu.size(), &dtdpdu)) ||
@@ -1584,7 +1654,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         (rc = up(d->emitter_cdf, d->n_emitters + 1, &ecdf)) ||
         (rc = up(d->emitter_tri_cdf, d->n_emitter_tri_cdf, &etcdf)))
         return fail(rc);
-    ds.nodes = nodes; ds.indices = indices; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
+    ds.pairs = dpairs; ds.triL = dtriL; ds.root = root; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
     ds.tidx = dtidx; ds.tdpdu = dtdpdu; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
     ds.n_emitters = d->n_emitters;

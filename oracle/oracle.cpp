@@ -23,6 +23,7 @@ namespace {
 
 thread_local std::string g_err;
 int g_debug = 0;   // oracle_debug_pixel_sample(): print the path to stderr
+std::vector<float> *g_rayLog = nullptr;   // closest-hit rays of the debugged path
 #define DBG(...) do { if (g_debug) fprintf(stderr, __VA_ARGS__); } while (0)
 
 // ---------------------------------------------------------------------------
@@ -547,6 +548,7 @@ struct SceneView {
     // ShapeKDTree::rayIntersect (skdtree.cpp:112-142)
     template <bool count>
     bool rayIntersect(const Ray &ray, Its &its, Cache *outCache, Counters *ctr) const {
+        if (g_rayLog) g_rayLog->insert(g_rayLog->end(), {ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z, ray.mint, ray.maxt});
         its.t = std::numeric_limits<float>::infinity();
         if (count) ctr->closest++;
         float mint, maxt;
@@ -1262,6 +1264,28 @@ int oracle_trace_closest_brute(const mtsg_scene_desc *d, uint32_t n, const float
         }
     });
     return 0;
+}
+
+int oracle_debug_path_rays(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, int s,
+                           float *rays_out, int max_rays) {
+    std::vector<float> log;
+    g_rayLog = &log;
+    SceneView sv(*d);
+    Integrator I{p->max_depth, p->rr_depth, p->strict_normals != 0, p->hide_emitters != 0};
+    Sampler smp;
+    smp.mode = ORACLE_RNG_COUNTER;
+    smp.key = counterKey(p->seed, ((uint64_t)y * d->camera.film_w + x) * p->spp + s);
+    float a, b;
+    smp.next2D(a, b);
+    Ray ray = cameraRay(d->camera, x + a, y + b);
+    float alpha;
+    int depth;
+    Counters c;
+    Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0);
+    g_rayLog = nullptr;
+    int n = std::min<int>((int)log.size() / 8, max_rays);
+    std::copy(log.begin(), log.begin() + 8 * n, rays_out);
+    return n;
 }
 
 int oracle_debug_pixel_sample(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, int s) {

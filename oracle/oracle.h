@@ -69,6 +69,11 @@ int oracle_pixel_samples(const mtsg_scene_desc *d, const mtsg_render_params *p,
 /* Print the path of one counter-mode sample to stderr (debugging). */
 int oracle_debug_pixel_sample(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, int s);
 
+/* Closest-hit rays traced along one counter-mode sample (8 floats each);
+ * returns the count. */
+int oracle_debug_path_rays(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, int s,
+                           float *rays_out, int max_rays);
+
 /* BSDF / emitter building blocks for statistical tests (local frame). */
 /* sample: returns weight (3), pdf, wo(3), sampled type flags */
 int oracle_bsdf_sample(const mtsg_bsdf *b, const float wi[3], float s0, float s1,

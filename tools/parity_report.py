@@ -35,7 +35,7 @@ def main():
     g.close()
 
 
-if __name__ == "__main__" and "--samples" not in sys.argv:
+if __name__ == "__main__" and "--samples" not in sys.argv and "--replay" not in sys.argv:
     main()
 
 
@@ -63,3 +63,29 @@ def samples_diff(path, defs, maxshow=12):
 
 if __name__ == "__main__" and "--samples" in sys.argv:
     samples_diff(sys.argv[1], dict(a.split("=", 1) for a in sys.argv[2:] if "=" in a))
+
+
+def replay(path, defs, cases):
+    """Replay the oracle's closest-hit rays of diverging samples on the GPU."""
+    import ctypes as C
+    scene = mtsg.Scene(path, defs)
+    p = scene.params()
+    g = mtsg.GPUScene(scene, 0)
+    L = O.lib()
+    L.oracle_debug_path_rays.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int]
+    for (x, y, s) in cases:
+        buf = np.zeros((64, 8), np.float32)
+        n = L.oracle_debug_path_rays(scene.desc, C.byref(p), x, y, s, buf.ctypes.data, 64)
+        rays = buf[:n]
+        t0, u0, v0, p0 = O.trace_closest(scene.desc, rays)
+        t1, u1, v1, p1 = g.trace_closest(rays)
+        print(f"  sample ({x},{y},{s}): {n} rays")
+        for i in range(n):
+            flag = "" if (p0[i] == p1[i] and (t0[i] == t1[i] or abs(t0[i] - t1[i]) < 1e-6 * abs(t0[i]))) else "  <-- DIFF"
+            print(f"    ray {i}: cpu prim {p0[i]:#x} t {t0[i]:.9g} | gpu prim {p1[i]:#x} t {t1[i]:.9g}{flag}")
+    g.close()
+
+
+if __name__ == "__main__" and "--replay" in sys.argv:
+    replay(sys.argv[1], dict(a.split("=", 1) for a in sys.argv[2:] if "=" in a),
+           [(14, 21, 0), (1, 20, 3), (12, 21, 6), (9, 16, 0)])
