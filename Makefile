@@ -56,3 +56,13 @@ $(ORACLE_FAST): oracle/oracle.cpp oracle/oracle.h include/mtsg.h
 
 clean:
 	rm -f $(HOST_LIB) $(DEV_LIB) $(PATH_LIB) $(CLI) $(ORACLE) $(ORACLE_FAST)
+
+# Measurement variants of the device library (build/var/, loaded with MTSG_LIB=...)
+VARIANTS := nont:-DMTSG_NT=0 pf:-DMTSG_LEAF_PREFETCH=1 pfw5:-DMTSG_LEAF_PREFETCH=1@-DMTSG_TRACE_WAVES=5
+VAR_LIBS := $(foreach v,$(VARIANTS),build/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
+.PHONY: variants
+variants: $(VAR_LIBS)
+build/var/libmtsg_%.so: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p build/var
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -munsafe-fp-atomics -Wno-unused-value \
+	    -Wno-unused-result $(subst @, ,$(word 2,$(subst :, ,$(filter $*:%,$(VARIANTS))))) -o $@ $(DEV_SRC)

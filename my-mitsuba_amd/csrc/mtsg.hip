@@ -48,6 +48,11 @@ struct DevScene {
     const uint4 *__restrict__ pairs;
     const float4 *__restrict__ triL;
     uint2 root;
+    // compact alternative (MTSG_LEAF_MODE=1): leaves index Mitsuba's primitive
+    // index list, TriAccel records are read in primitive order from `tri`
+    const uint4 *__restrict__ pairsIdx;
+    const uint32_t *__restrict__ lidx;
+    uint2 rootIdx;
     const float4 *__restrict__ tri;        // 3 float4 per prim (TriAccel, prim order)
     const float4 *__restrict__ vpos;       // xyz
     const float4 *__restrict__ vnrm;       // xyz
@@ -122,31 +127,72 @@ DEV int cnt_q(int q) { return q ? CNT_Q1 : CNT_Q0; }
 constexpr int TILE = 16;                    // splat tile edge (256 pixels)
 constexpr int BLOCK = 256;
 constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traversal
-// Paths per wavefront batch (172 B of SoA state per path -> 5.5 GiB of HBM).
-// Each bounce launch needs several rays per resident lane to amortise the
-// slowest rays (tail) -- measured on the 1M-triangle scene: 4M paths 421,
-// 16M 629, 32M 698 Msamples/s.
-constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 25;
-constexpr int SHORT_STACK = 8;              // LDS short stack entries per lane
+// Paths per wavefront batch (172 B of SoA state per path; 2^28 paths = 46 GB
+// of the 288 GB HBM, capped at 60% of free device memory at run time).
+// Every traversal launch ends with a tail of ~0.5-0.8 ms while its longest
+// rays finish, and late bounces hold few paths, so the batch should be as
+// large as the frame -- measured on the 1M-triangle scene (Msamples/s):
+// 4M paths 421, 16M 672, 32M 803, 64M 884, 128M 934, whole frame 960.
+constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 28;
+constexpr size_t PATH_STATE_BYTES = 172;    // SoA bytes per path slot (DevPaths)
+#ifndef MTSG_SHORT_STACK
+#define MTSG_SHORT_STACK 8
+#endif
+constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per lane
+#ifndef MTSG_LEAF_PREFETCH
+#define MTSG_LEAF_PREFETCH 0
+#endif
+#ifndef MTSG_TRACE_WAVES
+#define MTSG_TRACE_WAVES 0
+#endif
+#if MTSG_TRACE_WAVES > 0
+#define TRACE_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_TRACE_WAVES)))
+#else
+#define TRACE_ATTR __launch_bounds__(TRACE_BLOCK)
+#endif
+// streaming (non-temporal) access to the per-path SoA state: the state of a
+// 32M-path batch is GBs per bounce and would otherwise evict the kd-tree from
+// the 256 MB Infinity Cache (experiment switch MTSG_NT)
+#ifndef MTSG_NT
+#define MTSG_NT 1
+#endif
+typedef float nf4 __attribute__((ext_vector_type(4)));
+typedef uint32_t nu2 __attribute__((ext_vector_type(2)));
+DEV float4 ldS(const float4 *p) {
+#if MTSG_NT
+    const nf4 v = __builtin_nontemporal_load((const nf4 *)p);
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+DEV uint2 ldS(const uint2 *p) {
+#if MTSG_NT
+    const nu2 v = __builtin_nontemporal_load((const nu2 *)p);
+    return make_uint2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
+DEV void stS(float4 *p, const float4 &v) {
+#if MTSG_NT
+    __builtin_nontemporal_store((nf4){v.x, v.y, v.z, v.w}, (nf4 *)p);
+#else
+    *p = v;
+#endif
+}
+DEV void stS(uint2 *p, const uint2 &v) {
+#if MTSG_NT
+    __builtin_nontemporal_store((nu2){v.x, v.y}, (nu2 *)p);
+#else
+    *p = v;
+#endif
+}
 
 // ---------------------------------------------------------------------------
 // wave helpers (64 lanes)
 // ---------------------------------------------------------------------------
 DEV uint32_t lane_id() { return __lane_id(); }
-
-// Wave-aggregated queue append: one atomic per wave, lanes get consecutive slots.
-DEV uint32_t wave_append(uint32_t *counter, bool pred) {
-    unsigned long long m = __ballot(pred);
-    uint32_t n = (uint32_t)__popcll(m);
-    uint32_t base = 0;
-    uint32_t leader = (uint32_t)__ffsll((long long)m) - 1;
-    if (n) {
-        if (lane_id() == leader) base = atomicAdd(counter, n);
-        base = __shfl(base, (int)leader);
-    }
-    uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
-    return base + rank;
-}
 
 // ---------------------------------------------------------------------------
 // primitive tests
@@ -162,23 +208,28 @@ DEV float sel3(uint32_t axis, float a, float b, float c) {
 // TriAccel::rayIntersect (triaccel.h:96-158)
 DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, float3 d, float mint, float maxt,
                   float &u, float &v, float &t) {
+    // no FMA contraction: bit-identical t, u, v to the oracle (and Mitsuba's SSE2 build)
+#pragma clang fp contract(off)
     const uint32_t k = __float_as_uint(f0.x);
     // (u, v, k) = (1,2,0) | (2,0,1) | (0,1,2): bit-mask selects (see sel3)
     const uint32_t ku = k == 0 ? 1u : (k == 1 ? 2u : 0u), kv = k == 0 ? 2u : (k == 1 ? 0u : 1u);
     const float o_u = sel3(ku, o.x, o.y, o.z), o_v = sel3(kv, o.x, o.y, o.z), o_k = sel3(k, o.x, o.y, o.z);
     const float d_u = sel3(ku, d.x, d.y, d.z), d_v = sel3(kv, d.x, d.y, d.z), d_k = sel3(k, d.x, d.y, d.z);
     const float n_u = f0.y, n_v = f0.z, n_d = f0.w;
+    // branch-free on purpose: with an early `t` rejection the compiler sinks
+    // the loads of f1/f2 behind it, turning one 48-byte fetch into two or
+    // three dependent memory round trips per primitive
     t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
-    if (!(t >= mint && t <= maxt)) return false;
     const float hu = o_u + t * d_u - f1.x;
     const float hv = o_v + t * d_v - f1.y;
     u = hv * f1.z + hu * f1.w;
     v = hu * f2.x + hv * f2.y;
-    return u >= 0 && v >= 0 && u + v <= 1.0f && k < 3;
+    return (t >= mint) & (t <= maxt) & (u >= 0) & (v >= 0) & (u + v <= 1.0f) & (k < 3);
 }
 
 // Rectangle::rayIntersect (rectangle.cpp:115-139)
 DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float maxt, float &t, float &lx, float &ly) {
+#pragma clang fp contract(off)
     const float *m = r.to_object;
     float3 o = mk3(m[0] * wo.x + m[1] * wo.y + m[2] * wo.z + m[3], m[4] * wo.x + m[5] * wo.y + m[6] * wo.z + m[7],
                    m[8] * wo.x + m[9] * wo.y + m[10] * wo.z + m[11]);
@@ -221,7 +272,7 @@ struct KdStack {
 
 // Scene-AABB clip + adaptive epsilon (skdtree.cpp:112-142 / 207-226).
 // Returns false when the ray misses the scene bounds.
-template <bool SHADOW>
+template <bool SHADOW, bool LEAFIDX = false>
 DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, KdRay &r) {
     r.o = o;
     r.d = d;
@@ -252,7 +303,7 @@ DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float ray
     if (!(r.best > r.mint)) return false;
     r.tmin = r.mint;
     r.tmax = r.best;
-    r.cur = S.root;
+    r.cur = LEAFIDX ? S.rootIdx : S.root;
     r.sp = r.bottom = 0;
     r.found = 0;
     r.bu = r.bv = 0.f;
@@ -263,14 +314,14 @@ DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float ray
 // Process one leaf: descend from r.cur (one 16-byte sibling-pair load per
 // inner node), test the leaf's primitives, then pop (or restart).  Returns
 // true when the ray is finished.
-template <bool SHADOW, bool COUNT>
+template <bool SHADOW, bool COUNT, bool LEAFIDX = false>
 DEV bool kd_step(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
     uint2 n = r.cur;
     float tmin = r.tmin, tmax = r.tmax;
     while (!(n.x & 0x80000000u)) {
         const uint32_t axis = n.x & 3u;
         const float split = __uint_as_float(n.y);
-        const uint4 pr = S.pairs[n.x >> 2];
+        const uint4 pr = LEAFIDX ? S.pairsIdx[n.x >> 2] : S.pairs[n.x >> 2];
         if (COUNT) cnt.nodes++;
         const float oa = sel3(axis, r.o.x, r.o.y, r.o.z);
         const float da = sel3(axis, r.d.x, r.d.y, r.d.z);
@@ -285,7 +336,7 @@ DEV bool kd_step(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
         } else if (tsplit < tmin) {
             n = second;
         } else {
-            const uint32_t k = (r.sp & (SHORT_STACK - 1)) * TRACE_BLOCK;
+            const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
             stk.node[k] = second;
             stk.t[k] = tmax;
             ++r.sp;
@@ -295,14 +346,29 @@ DEV bool kd_step(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
         }
     }
     // leaf: test every primitive against [mint, best] (skdtree.h:248-304)
+#if MTSG_LEAF_PREFETCH
+    // software pipelining: the next record's loads are issued before this
+    // record is tested (one dependent-load latency per leaf, not per primitive)
+    float4 g0, g1, g2;
+    {
+        const uint32_t e0 = n.x & 0x7FFFFFFFu;
+        if (e0 < n.y) { const float4 *rec = S.triL + 3 * (size_t)e0; g0 = rec[0]; g1 = rec[1]; g2 = rec[2]; }
+    }
+#endif
     for (uint32_t e = n.x & 0x7FFFFFFFu; e < n.y; ++e) {
         if (COUNT) { cnt.refs++; cnt.tests++; }
-        const float4 f0 = S.triL[3 * e], f1 = S.triL[3 * e + 1], f2 = S.triL[3 * e + 2];
+#if MTSG_LEAF_PREFETCH
+        const float4 f0 = g0, f1 = g1, f2 = g2;
+        if (e + 1 < n.y) { const float4 *rec = S.triL + 3 * (size_t)(e + 1); g0 = rec[0]; g1 = rec[1]; g2 = rec[2]; }
+#else
+        const float4 *rec = LEAFIDX ? S.tri + 3 * (size_t)S.lidx[e] : S.triL + 3 * (size_t)e;
+        const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
+#endif
         float t, u, v;
-        bool h;
+        // a rectangle record (k = 0xFFFFFFFF) fails the triangle test
+        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
         const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
-        if (!isRect) h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-        else h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
         if (h) {
             r.found = 1;
             if (SHADOW) return true;
@@ -320,11 +386,11 @@ DEV bool kd_step(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
         r.sp = r.bottom = 0;
         r.tmin = tmax;
         r.tmax = r.best;
-        r.cur = S.root;
+        r.cur = LEAFIDX ? S.rootIdx : S.root;
         return !(r.tmin < r.tmax);
     }
     --r.sp;
-    const uint32_t k = (r.sp & (SHORT_STACK - 1)) * TRACE_BLOCK;
+    const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
     r.cur = stk.node[k];
     r.tmin = tmax;
     r.tmax = fminf(stk.t[k], r.best);
@@ -402,15 +468,15 @@ struct Fetch {
 };
 
 DEV void shadow_unoccluded(const DevPaths &P, uint32_t slot) {
-    const float4 con = P.sh_c[slot];
-    float4 L = P.L[slot];
+    const float4 con = ldS(&P.sh_c[slot]);
+    float4 L = ldS(&P.L[slot]);
     L.x += con.x; L.y += con.y; L.z += con.z;
-    P.L[slot] = L;
+    stS(&P.L[slot], L);
 }
 
 DEV void load_ray(const DevPaths &P, bool shadow, uint32_t slot, float4 &ro, float4 &rd) {
-    if (shadow) { ro = P.sh_o[slot]; rd = P.sh_d[slot]; rd.w = ro.w; ro.w = kEpsilon; }
-    else { ro = P.ray_o[slot]; rd = P.ray_d[slot]; }
+    if (shadow) { ro = ldS(&P.sh_o[slot]); rd = ldS(&P.sh_d[slot]); rd.w = ro.w; ro.w = kEpsilon; }
+    else { ro = ldS(&P.ray_o[slot]); rd = ldS(&P.ray_d[slot]); }
 }
 
 DEV float4 hit_record(const KdRay &r) {
@@ -443,7 +509,7 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths
             r.found = 0;
             if (live) while (!kd_step<SHADOW, COUNT>(S, r, stk, c)) {}
             if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
-            else P.hit[slot] = hit_record(r);
+            else stS(&P.hit[slot], hit_record(r));
         }
     }
     flush_counts<COUNT>(P.ctr + (SHADOW ? 3 : 0), c);
@@ -460,8 +526,8 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths
 //   SHADOW = true : any hit of the shadow queue; unoccluded -> L += contribution
 constexpr uint32_t FETCH = 256;
 
-template <bool SHADOW, bool COUNT, int MIN_IDLE>
-__global__ void __launch_bounds__(TRACE_BLOCK) k_trace(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
+template <bool SHADOW, bool COUNT, int MIN_IDLE, bool LEAFIDX = false>
+__global__ void TRACE_ATTR k_trace(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
     KD_STACK_DECL
     uint32_t count = nIdentity;   // explicit branches: a ternary over a volatile load
     if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);   // demotes the argument to scratch
@@ -490,14 +556,17 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace(DevScene S, DevPaths P, i
                 slot = q ? q[i] : i;
                 float4 ro, rd;
                 load_ray(P, SHADOW, slot, ro, rd);
-                if (!SHADOW && rd.w < 0.0f) {
-                    // dead slot (outside the render rectangle): no hit record needed
-                } else if (kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r)) {
+                // kd_init before the dead-slot test so that both ray loads are
+                // issued together (a dead slot has maxt = -1 and fails kd_init)
+                const bool live = kd_init<SHADOW, LEAFIDX>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
+                if (live) {
                     active = true;
+                } else if (!SHADOW && rd.w < 0.0f) {
+                    // dead slot (outside the render rectangle): no hit record needed
                 } else if (SHADOW) {
                     shadow_unoccluded(P, slot);   // misses the scene bounds
                 } else {
-                    P.hit[slot] = make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
+                    stS(&P.hit[slot], make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)));
                 }
             }
             poolBase += take;
@@ -510,10 +579,10 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace(DevScene S, DevPaths P, i
             continue;
         }
         // ---- one leaf of traversal for the active lanes
-        if (active && kd_step<SHADOW, COUNT>(S, r, stk, c)) {
+        if (active && kd_step<SHADOW, COUNT, LEAFIDX>(S, r, stk, c)) {
             active = false;
             if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
-            else P.hit[slot] = hit_record(r);
+            else stS(&P.hit[slot], hit_record(r));
         }
     }
     flush_counts<COUNT>(P.ctr + (SHADOW ? 3 : 0), c);
@@ -579,17 +648,17 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
             const float *t = C.c2w;
             float3 wd = mk3(t[0] * d.x + t[1] * d.y + t[2] * d.z, t[4] * d.x + t[5] * d.y + t[6] * d.z,
                             t[8] * d.x + t[9] * d.y + t[10] * d.z);
-            P.ray_o[slot] = make_float4(t[3], t[7], t[11], C.near_clip * invZ);
-            P.ray_d[slot] = make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ);
-            P.L[slot] = make_float4(0.f, 0.f, 0.f, 1.0f);
-            P.T[slot] = make_float4(1.f, 1.f, 1.f, 1.f);
-            P.key[slot] = make_uint2((uint32_t)key, (uint32_t)(key >> 32));
-            P.st[slot] = make_uint2(1u, 2u);   // depth 1, next dimension 2
+            stS(&P.ray_o[slot], make_float4(t[3], t[7], t[11], C.near_clip * invZ));
+            stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
+            stS(&P.L[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
+            stS(&P.T[slot], make_float4(1.f, 1.f, 1.f, 1.f));
+            stS(&P.key[slot], make_uint2((uint32_t)key, (uint32_t)(key >> 32)));
+            stS(&P.st[slot], make_uint2(1u, 2u));   // depth 1, next dimension 2
         } else {
             // dead slot: bounce 0 runs over the identity queue and skips it
-            P.ray_d[slot] = make_float4(0.f, 0.f, 1.f, -1.0f);
-            P.st[slot] = make_uint2(0u, 0u);
-            P.L[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+            stS(&P.ray_d[slot], make_float4(0.f, 0.f, 1.f, -1.0f));
+            stS(&P.st[slot], make_uint2(0u, 0u));
+            stS(&P.L[slot], make_float4(0.f, 0.f, 0.f, 0.f));
         }
     }
 }
@@ -1012,16 +1081,16 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, De
         uint32_t slot = 0;
         if (alive) {
             slot = qin < 0 ? i : P.q[qin][i];
-            if (qin < 0 && P.st[slot].x == 0u) alive = false;   // dead slot
+            if (qin < 0 && ldS(&P.st[slot]).x == 0u) alive = false;   // dead slot
         }
         if (alive) {
-            const float4 h = P.hit[slot];
-            const float4 ro4 = P.ray_o[slot], rd4 = P.ray_d[slot];
+            const float4 h = ldS(&P.hit[slot]);
+            const float4 ro4 = ldS(&P.ray_o[slot]), rd4 = ldS(&P.ray_d[slot]);
             const float3 ro = xyz(ro4), rd = xyz(rd4);
-            float4 L4 = P.L[slot];
-            float4 T4 = P.T[slot];
-            uint2 st = P.st[slot];
-            const uint2 kk = P.key[slot];
+            float4 L4 = ldS(&P.L[slot]);
+            float4 T4 = ldS(&P.T[slot]);
+            uint2 st = ldS(&P.st[slot]);
+            const uint2 kk = ldS(&P.key[slot]);
             const uint64_t key = (uint64_t)kk.x | ((uint64_t)kk.y << 32);
             float3 L = xyz(L4), T = xyz(T4);
             float eta = T4.w;
@@ -1048,13 +1117,13 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, De
                         float lumPdf = 0.0f;
                         if (!(flags & F_DELTA)) {
                             // Scene::pdfEmitterDirect with dRec.setQuery(ray, its)
-                            const float4 ax = P.aux[slot];
+                            const float4 ax = ldS(&P.aux[slot]);
                             const float3 refN = xyz(ax);
                             if (dot(rd, refN) >= 0 && dot(rd, its.sh.n) < 0)
                                 lumPdf = E.inv_area * (h.x * h.x) / fabsf(dot(rd, its.sh.n));
                             lumPdf *= E.pdf_discrete;
                         }
-                        L += T * value * mis(P.aux[slot].w, lumPdf);
+                        L += T * value * mis(ldS(&P.aux[slot]).w, lumPdf);
                     }
                     if (depth++ >= (uint32_t)I.rr_depth) {
                         float q = fminf(maxc(T) * eta * eta, 0.95f);
@@ -1102,9 +1171,9 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, De
                                 const float3 c = T * value * bval * weight;
                                 if (!isZero(c)) {
                                     shadow = true;
-                                    P.sh_o[slot] = make_float4(its.p.x, its.p.y, its.p.z, dist * (1 - kShadowEpsilon));
-                                    P.sh_d[slot] = make_float4(dd.x, dd.y, dd.z, 0.f);
-                                    P.sh_c[slot] = make_float4(c.x, c.y, c.z, 0.f);
+                                    stS(&P.sh_o[slot], make_float4(its.p.x, its.p.y, its.p.z, dist * (1 - kShadowEpsilon)));
+                                    stS(&P.sh_d[slot], make_float4(dd.x, dd.y, dd.z, 0.f));
+                                    stS(&P.sh_c[slot], make_float4(c.x, c.y, c.z, 0.f));
                                 }
                             }
                         }
@@ -1123,18 +1192,18 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, De
                             T = T * bs.weight;
                             eta *= bs.eta;
                             flags = bs.delta ? (flags | F_DELTA) : (flags & ~F_DELTA);
-                            P.ray_o[slot] = make_float4(its.p.x, its.p.y, its.p.z, kEpsilon);
-                            P.ray_d[slot] = make_float4(wo.x, wo.y, wo.z, INFINITY);
-                            P.aux[slot] = make_float4(refN.x, refN.y, refN.z, bs.pdf);
+                            stS(&P.ray_o[slot], make_float4(its.p.x, its.p.y, its.p.z, kEpsilon));
+                            stS(&P.ray_d[slot], make_float4(wo.x, wo.y, wo.z, INFINITY));
+                            stS(&P.aux[slot], make_float4(refN.x, refN.y, refN.z, bs.pdf));
                             cont = true;
                         }
                     }
                 }
             }
-            P.L[slot] = make_float4(L.x, L.y, L.z, L4.w);
+            stS(&P.L[slot], make_float4(L.x, L.y, L.z, L4.w));
             if (cont) {
-                P.T[slot] = make_float4(T.x, T.y, T.z, eta);
-                P.st[slot] = make_uint2(depth | flags, dim);
+                stS(&P.T[slot], make_float4(T.x, T.y, T.z, eta));
+                stS(&P.st[slot], make_uint2(depth | flags, dim));
             }
         }
         uint32_t is, ic;
@@ -1190,8 +1259,8 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevBatch B, DevPat
     if (inside) {
         for (uint32_t sl = sBeg; sl < sEnd; ++sl) {
             const uint32_t slot = ((uint32_t)tl * B.ns + sl) * (TILE * TILE) + pix;
-            const float4 L = P.L[slot];
-            const uint2 kk = P.key[slot];
+            const float4 L = ldS(&P.L[slot]);
+            const uint2 kk = ldS(&P.key[slot]);
             const uint64_t key = (uint64_t)kk.x | ((uint64_t)kk.y << 32);
             // invalid samples are rejected (imageblock.h:147-151)
             if (!(isfinite(L.x) && isfinite(L.y) && isfinite(L.z) && L.x >= 0 && L.y >= 0 && L.z >= 0)) continue;
@@ -1366,7 +1435,8 @@ void timed_launch(mtsg_scene *s, int kind, F f) {
 
 // Traversal kernel variants (MTSG_TRACE_MODE, for measurement):
 //   0 = wave fetch 64 / atomic, 1 = wave fetch 4x64 / atomic,
-//   2 = lane refill at >= 1 idle lane, 3 = lane refill at >= 32 idle lanes
+//   2 = lane refill at >= 1 idle lane, 3 = lane refill at >= 32 idle lanes,
+//   4 = as 3 with indexed leaves (compact tree, one extra dependent load)
 template <bool SHADOW, bool COUNT>
 void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
     dim3 g(s->traceGrid), blk(TRACE_BLOCK);
@@ -1374,6 +1444,7 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
         case 0: hipLaunchKernelGGL((k_trace_wave<SHADOW, COUNT, 1>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 1: hipLaunchKernelGGL((k_trace_wave<SHADOW, COUNT, 4>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 2: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 1>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 4: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         default: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
     }
 }
@@ -1405,7 +1476,14 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     if ((rc = validate(p, s)) != MTSG_OK) return rc;
     if ((rc = set_device(s)) != MTSG_OK) return rc;
     auto t0 = std::chrono::steady_clock::now();
-    const uint32_t maxPaths = s->requestedBatch ? s->requestedBatch : DEFAULT_BATCH_PATHS;
+    uint32_t maxPaths = s->requestedBatch ? s->requestedBatch : DEFAULT_BATCH_PATHS;
+    if (!s->requestedBatch && s->capacity < maxPaths) {
+        size_t freeB = 0, totalB = 0;
+        if (hipMemGetInfo(&freeB, &totalB) == hipSuccess) {
+            const size_t fit = (size_t)((freeB + (size_t)s->capacity * PATH_STATE_BYTES) * 0.6 / PATH_STATE_BYTES);
+            maxPaths = (uint32_t)std::max<size_t>(TILE * TILE, std::min<size_t>(maxPaths, fit));
+        }
+    }
     if (s->dumpL && (uint64_t)p->tile_w * p->tile_h * p->spp > maxPaths) { g_err = "render_samples: tile does not fit one batch"; return MTSG_ERR_INVALID; }
     const uint32_t tilesX = (uint32_t)(p->tile_w + TILE - 1) / TILE, tilesY = (uint32_t)(p->tile_h + TILE - 1) / TILE;
     const uint32_t allTiles = tilesX * tilesY;
@@ -1413,7 +1491,11 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     const uint32_t toffset = p->tile_stride > 1 ? (uint32_t)p->tile_offset : 0u;
     const uint32_t ntiles = toffset < allTiles ? (allTiles - toffset + tstride - 1) / tstride : 0u;
     const uint32_t sppPerBatch = std::max(1u, std::min(p->spp, maxPaths / (TILE * TILE)));
-    const uint32_t tilesPerBatch = std::max(1u, maxPaths / (TILE * TILE * sppPerBatch));
+    // equal-sized batches: a nearly empty last batch costs a full set of
+    // bounce launches (and their tails) for a sliver of the work
+    const uint32_t tilesMax = std::max(1u, maxPaths / (TILE * TILE * sppPerBatch));
+    const uint32_t nTileBatches = std::max(1u, (ntiles + tilesMax - 1) / tilesMax);
+    const uint32_t tilesPerBatch = std::max(1u, (ntiles + nTileBatches - 1) / nTileBatches);
     if ((rc = ensure_batch(s, tilesPerBatch * sppPerBatch * TILE * TILE)) != MTSG_OK) return rc;
     const int blockW = p->tile_w + 2 * s->cam.border, blockH = p->tile_h + 2 * s->cam.border;
     DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed};
@@ -1609,14 +1691,17 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     };
     // ---- device kd-tree layout from Mitsuba's KDNode array (same splits and
     // leaves, re-laid out): sibling pairs + leaf-ordered TriAccel copies
-    std::vector<uint4> pairs;
+    std::vector<uint4> pairs, pairsIdx;
     std::vector<float4> triL;
     pairs.reserve(d->n_nodes / 2 + 1);
+    pairsIdx.reserve(d->n_nodes / 2 + 1);
     triL.reserve((size_t)d->n_indices * 3);
     bool layoutOk = true;
-    std::function<uint2(uint32_t, int)> convert = [&](uint32_t ni, int depth) -> uint2 {
+    // returns the node in both leaf encodings: .x/.y leaf-ordered copies,
+    // .z/.w Mitsuba's index range (inner nodes are identical in both)
+    std::function<uint4(uint32_t, int)> convert = [&](uint32_t ni, int depth) -> uint4 {
         const mtsg_kdnode &N = d->nodes[ni];
-        if (depth > 64 || ni >= d->n_nodes) { layoutOk = false; return make_uint2(0x80000000u, 0u); }
+        if (depth > 64 || ni >= d->n_nodes) { layoutOk = false; return make_uint4(0x80000000u, 0u, 0x80000000u, 0u); }
         if (N.combined & 0x80000000u) {
             const uint32_t start = (uint32_t)(triL.size() / 3);
             for (uint32_t e = N.combined & 0x7FFFFFFFu; e < N.data; ++e) {
@@ -1625,27 +1710,34 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
                 const float4 *t = (const float4 *)(d->triaccel + p);
                 triL.push_back(t[0]); triL.push_back(t[1]); triL.push_back(t[2]);
             }
-            return make_uint2(0x80000000u | start, (uint32_t)(triL.size() / 3));
+            return make_uint4(0x80000000u | start, (uint32_t)(triL.size() / 3), N.combined, N.data);
         }
         const uint32_t left = ni + ((N.combined & ~(3u | 0x40000000u)) >> 2);
         const uint32_t pi = (uint32_t)pairs.size();
         pairs.push_back(make_uint4(0, 0, 0, 0));
-        const uint2 L = convert(left, depth + 1);
-        const uint2 R = convert(left + 1, depth + 1);
+        pairsIdx.push_back(make_uint4(0, 0, 0, 0));
+        const uint4 L = convert(left, depth + 1);
+        const uint4 R = convert(left + 1, depth + 1);
         pairs[pi] = make_uint4(L.x, L.y, R.x, R.y);
-        return make_uint2((N.combined & 3u) | (pi << 2), N.data);
+        pairsIdx[pi] = make_uint4(L.z, L.w, R.z, R.w);
+        const uint32_t inner = (N.combined & 3u) | (pi << 2);
+        return make_uint4(inner, N.data, inner, N.data);
     };
-    const uint2 root = convert(0, 0);
+    const uint4 root4 = convert(0, 0);
+    const uint2 root = make_uint2(root4.x, root4.y);
+    ds.rootIdx = make_uint2(root4.z, root4.w);
     if (!layoutOk || pairs.size() >= (1u << 29) || triL.size() / 3 >= (1u << 31)) {
         g_err = "malformed or oversized kd-tree";
         return fail(MTSG_ERR_INVALID);
     }
-    if (pairs.empty()) pairs.push_back(make_uint4(0, 0, 0, 0));
+    if (pairs.empty()) { pairs.push_back(make_uint4(0, 0, 0, 0)); pairsIdx.push_back(make_uint4(0, 0, 0, 0)); }
     if (triL.empty()) triL.resize(3, make_float4(0, 0, 0, 0));
-    uint4 *dpairs; float4 *dtriL; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu; uint4 *dtidx;
+    uint4 *dpairs, *dpairsIdx; float4 *dtriL; uint32_t *dlidx; const uint32_t zero = 0; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu; uint4 *dtidx;
     mtsg_rect *rects; mtsg_shape *shapes; mtsg_bsdf *bsdfs; mtsg_emitter *emitters; float *ecdf, *etcdf;
     if ((rc = up(pairs.data(), pairs.size(), &dpairs)) ||
         (rc = up(triL.data(), triL.size(), &dtriL)) ||
+        (rc = up(pairsIdx.data(), pairsIdx.size(), &dpairsIdx)) ||
+        (rc = d->n_indices ? up(d->indices, d->n_indices, &dlidx) : up(&zero, 1, &dlidx)) ||
         (rc = up((const float4 *)d->triaccel, (size_t)d->n_prims * 3, &tri)) ||
         (rc = up(vpos.data(), vpos.size(), &dvpos)) || (rc = up(vnrm.data(), vnrm.size(), &dvnrm)) ||
         (rc = up(tidx.data(), tidx.size(), &dtidx)) || (rc = up(tdpdu.data(), tdpdu.size(), &dtdpdu)) ||
@@ -1654,7 +1746,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         (rc = up(d->emitter_cdf, d->n_emitters + 1, &ecdf)) ||
         (rc = up(d->emitter_tri_cdf, d->n_emitter_tri_cdf, &etcdf)))
         return fail(rc);
-    ds.pairs = dpairs; ds.triL = dtriL; ds.root = root; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
+    ds.pairs = dpairs; ds.triL = dtriL; ds.root = root; ds.pairsIdx = dpairsIdx; ds.lidx = dlidx; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
     ds.tidx = dtidx; ds.tdpdu = dtdpdu; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
     ds.n_emitters = d->n_emitters;
@@ -1671,7 +1763,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     memcpy(c.filter_values, hc.filter_values, sizeof(c.filter_values));
     // persistent grids from the occupancy query
     int perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace_wave<false, false, 4>, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace<false, false, 32>, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;
     if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);

@@ -114,8 +114,10 @@ def device_lib() -> C.CDLL:
     """The HIP library.  Raises (never falls back) when it is missing."""
     global _dev
     if _dev is None:
-        # MTSG_LIB: alternative in-tree build (measurement experiments only)
-        path = os.path.join(PKG_DIR, os.environ.get("MTSG_LIB", "libmtsg.so"))
+        # MTSG_LIB: alternative in-tree build, relative to the repository root
+        # (measurement variants under build/var/ only)
+        alt = os.environ.get("MTSG_LIB")
+        path = os.path.join(os.path.dirname(PKG_DIR), alt) if alt else os.path.join(PKG_DIR, "libmtsg.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is missing: the HIP extension was not built "
                                "(run `make device` / __graft_entry__.build()); no CPU fallback exists")

@@ -1,0 +1,19 @@
+#!/usr/bin/env python3
+"""One-line summary of a bench.py JSON log (value and per-kernel ms)."""
+import json
+import sys
+
+for path in sys.argv[1:]:
+    line = ""
+    for l in open(path):
+        if l.startswith("{"):
+            line = l
+    if not line:
+        print("no-json")
+        continue
+    j = json.loads(line)
+    k = j.get("kernels", {})
+    r = j.get("roofline") or {}
+    print(f"{j['value']:.1f} Ms/s  closest {k.get('trace_closest_ms', 0):.1f} shadow {k.get('trace_shadow_ms', 0):.1f} "
+          f"shade {k.get('shade_ms', 0):.1f} splat {k.get('splat_ms', 0):.1f} cam {k.get('camera_ms', 0):.1f} "
+          f"frame {k.get('frame_ms', 0):.1f}  GB/s {r.get('achieved', 0)}")
