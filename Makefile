@@ -37,7 +37,7 @@ $(DEV_LIB): $(DEV_SRC) $(DEV_HDR)
 	    -munsafe-fp-atomics -Wno-unused-value -Wno-unused-result -o $@ $(DEV_SRC)
 
 # Host-side `path` integrator plugin mirror: tiles the film over GPUs
-$(PATH_LIB): $(PKG)/host/path_integrator.cc $(HOST_LIB) $(DEV_LIB) include/mtsg.h include/mtsh.h
+$(PATH_LIB): $(PKG)/host/path_integrator.cc $(HOST_LIB) $(DEV_LIB) include/mtsg.h include/mtsh.h include/mtsg_path.h
 	$(CXX) -std=c++17 -O2 -fPIC -shared -Wall -o $@ $(PKG)/host/path_integrator.cc \
 	    -L$(PKG) -lmtsg_host -lmtsg -Wl,-rpath,'$$ORIGIN' -lpthread
 

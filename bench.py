@@ -29,6 +29,24 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+TRAFFIC_KERNEL = "k_trace<false, false, 32, false>"
+
+
+def pmc_traffic(workload):
+    """Memory-side bytes per launch of the closest-hit traversal from the
+    newest committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+    (profiles/rNN_traffic.json, written by tools/traffic_summary.py; PMC
+    counters need their own profiler runs, so they cannot be read live)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_traffic.json")))
+    for f in reversed(files):
+        try:
+            j = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if j.get("workload") == workload and j.get("kernel") == TRAFFIC_KERNEL:
+            return j, os.path.relpath(f, REPO)
+    return None, None
 
 
 def parse():
@@ -184,8 +202,16 @@ def main():
         bytes_per_launch = b_ray * st.rays_closest / launches
         avg_launch_s = st.ms_trace_closest / 1e3 / launches
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        tj, tsrc = pmc_traffic(a.workload)
+        traffic = None
+        if tj and avg_launch_s > 0 and a.workload == "bunny15" and params.spp == 256 and world == 1:
+            traffic = round(tj["traffic_bytes_per_launch"] / avg_launch_s / 1e9, 1)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": (f"{tsrc}: FETCH_SIZE x2 + WRITE_SIZE per launch "
+                                       f"({tj['traffic_bytes_per_launch'] / 1e9:.2f} GB) / this run's avg launch time"
+                                       if traffic is not None else None),
+                    "algorithmic_bytes_per_launch": round(bytes_per_launch),
                     "kernel": "k_trace<closest>", "bytes_per_ray": round(b_ray, 1),
                     "nodes_per_ray": round(nodes_per_ray, 2), "leaf_refs_per_ray": round(refs_per_ray, 2),
                     "tri_tests_per_ray": round(tests_per_ray, 2), "avg_launch_ms": round(avg_launch_s * 1e3, 3),

@@ -10,8 +10,7 @@
 #include "../../include/mtsg.h"
 #include "../../include/mtsh.h"
 
-extern "C" int mtsh_path_render(const mtsh_scene *scene, const mtsg_render_params *params, int n_gpus,
-                                float *rgbaw_out, double *seconds_out);
+#include "../../include/mtsg_path.h"
 
 int main(int argc, char **argv) {
     std::vector<std::string> defs;

@@ -15,6 +15,7 @@
 
 #include "../../include/mtsg.h"
 #include "../../include/mtsh.h"
+#include "../../include/mtsg_path.h"
 
 extern "C" {
 

@@ -42,3 +42,13 @@ def test_python_binding_lists_match_headers():
     import mtsg
     assert sorted(mtsg.DEVICE_SYMBOLS) == declared("mtsg.h")
     assert sorted(mtsg.HOST_SYMBOLS) == declared("mtsh.h")
+
+
+def test_path_library_exports_api():
+    lib = os.path.join(REPO, "my-mitsuba_amd", "libmtsg_path.so")
+    if not os.path.exists(lib):
+        subprocess.check_call(["make", "-C", REPO, "all"])
+    names = declared("mtsg_path.h")
+    assert names == ["mtsh_path_render"]
+    missing = [n for n in names if n not in exported(lib)]
+    assert not missing, missing
