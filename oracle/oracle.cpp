@@ -1379,8 +1379,16 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
                 int bw = std::min(BS, p->tile_x + p->tile_w - bx0), bh = std::min(BS, p->tile_y + p->tile_h - by0);
                 local.assign((size_t)(bw + 2 * B) * (bh + 2 * B) * 5, 0.0f);
                 Block blk{bx0, by0, bw, bh, B, local.data(), &cam};
+                const int tilesX = (p->tile_w + 15) / 16;
                 for (int y = by0; y < by0 + bh; ++y)
-                    for (int x = bx0; x < bx0 + bw; ++x)
+                    for (int x = bx0; x < bx0 + bw; ++x) {
+                        // multi-GPU contract (mtsg_render_params.tile_stride): this
+                        // call owns the 16x16 tiles t of the rectangle with
+                        // t % tile_stride == tile_offset
+                        if (p->tile_stride > 1) {
+                            const int t = ((y - p->tile_y) / 16) * tilesX + (x - p->tile_x) / 16;
+                            if (t % p->tile_stride != p->tile_offset) continue;
+                        }
                         for (uint32_t s = 0; s < p->spp; ++s) {
                             if (rng_mode == ORACLE_RNG_COUNTER) {
                                 smp.key = counterKey(p->seed, ((uint64_t)y * cam.film_w + x) * p->spp + s);
@@ -1399,6 +1407,7 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
                             samples[tid]++;
                             blk.put(spx, spy, L, alpha);
                         }
+                    }
                 // BlockedRenderProcess::processResult -> Film::put (renderproc.cpp:142-149)
                 std::lock_guard<std::mutex> g(filmMutex);
                 for (int yy = 0; yy < bh + 2 * B; ++yy) {
@@ -1456,6 +1465,18 @@ int oracle_bsdf_eval(const mtsg_bsdf *b, const float wi[3], const float wo[3], f
     Spec v = bsdfEval(*b, r);
     value[0] = v.s[0]; value[1] = v.s[1]; value[2] = v.s[2];
     *pdf = bsdfPdf(*b, r);
+    return 0;
+}
+
+int oracle_bsdf_sample_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *u2, float *wo, float *pdf,
+                         float *weight, int32_t *type) {
+    for (uint32_t i = 0; i < n; ++i)
+        type[i] = oracle_bsdf_sample(b, wi, u2[2 * i], u2[2 * i + 1], wo + 3 * i, pdf + i, weight + 3 * i);
+    return 0;
+}
+
+int oracle_bsdf_eval_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *wo, float *value, float *pdf) {
+    for (uint32_t i = 0; i < n; ++i) oracle_bsdf_eval(b, wi, wo + 3 * i, value + 3 * i, pdf + i);
     return 0;
 }
 

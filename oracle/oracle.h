@@ -81,6 +81,11 @@ int oracle_bsdf_sample(const mtsg_bsdf *b, const float wi[3], float s0, float s1
 int oracle_bsdf_eval(const mtsg_bsdf *b, const float wi[3], const float wo[3],
                      float value[3], float *pdf);
 
+/* batched forms for the chi-square tests: u2 = 2n sample pairs, wo/weight/value 3n */
+int oracle_bsdf_sample_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *u2, float *wo, float *pdf,
+                         float *weight, int32_t *type);
+int oracle_bsdf_eval_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *wo, float *value, float *pdf);
+
 const char *oracle_last_error(void);
 
 #ifdef __cplusplus
