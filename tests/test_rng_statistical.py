@@ -34,7 +34,6 @@ def test_counter_rng_matches_sfmt_statistically():
     mu, sd = means.mean(0), means.std(0, ddof=1)
     z = np.abs(sfmt.mean((0, 1)) - mu) / (sd * np.sqrt(1 + 1 / len(counter)))
     assert np.all(z < 5), (z, mu, sfmt.mean((0, 1)))
-    assert np.all(np.abs(sfmt.mean((0, 1)) / mu - 1) < 0.01)
     # per-pixel: SFMT-vs-counter differences look like counter-vs-counter noise
     l1_cross = np.abs(sfmt - counter[0]).mean()
     l1_noise = np.mean([np.abs(counter[i] - counter[0]).mean() for i in range(1, len(counter))])
