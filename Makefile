@@ -58,7 +58,7 @@ clean:
 	rm -f $(HOST_LIB) $(DEV_LIB) $(PATH_LIB) $(CLI) $(ORACLE) $(ORACLE_FAST)
 
 # Measurement variants of the device library (build/var/, loaded with MTSG_LIB=...)
-VARIANTS := nont:-DMTSG_NT=0 pf:-DMTSG_LEAF_PREFETCH=1 pfw5:-DMTSG_LEAF_PREFETCH=1@-DMTSG_TRACE_WAVES=5
+VARIANTS := s6:-DMTSG_SHORT_STACK=6 s6f128:-DMTSG_SHORT_STACK=6@-DMTSG_FETCH=128 s6f512:-DMTSG_SHORT_STACK=6@-DMTSG_FETCH=512 s5:-DMTSG_SHORT_STACK=5
 VAR_LIBS := $(foreach v,$(VARIANTS),build/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
 .PHONY: variants
 variants: $(VAR_LIBS)

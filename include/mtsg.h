@@ -221,6 +221,12 @@ typedef struct mtsg_stats {
     uint64_t shadow_nodes_visited;
     uint64_t shadow_leaf_refs;
     uint64_t shadow_tri_tests;
+    /* SIMD efficiency of the persistent traversal kernels (MTSG_FLAG_COUNT,
+     * refill modes 2-4): per wave, max-over-lanes inner-node and primitive
+     * iterations, traversal steps, and active lanes summed over steps.
+     * efficiency = nodes_visited / (64 * wave_node_iters), etc. */
+    uint64_t wave_node_iters, wave_test_iters, wave_steps, wave_active_lanes;
+    uint64_t shadow_wave_node_iters, shadow_wave_test_iters, shadow_wave_steps, shadow_wave_active_lanes;
 } mtsg_stats;
 
 enum {

@@ -136,7 +136,7 @@ constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traver
 constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 28;
 constexpr size_t PATH_STATE_BYTES = 172;    // SoA bytes per path slot (DevPaths)
 #ifndef MTSG_SHORT_STACK
-#define MTSG_SHORT_STACK 8
+#define MTSG_SHORT_STACK 6   // 6 x 12 B x 64 lanes = 4.6 KB LDS/wave -> 8 waves/SIMD (8: 6.5, 12: 4.2)
 #endif
 constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per lane
 #ifndef MTSG_LEAF_PREFETCH
@@ -249,7 +249,10 @@ DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float m
 // the ray segment is visited until the best hit lies before the current
 // leaf's exit distance (sahkdtree3.h:299-300).
 // ---------------------------------------------------------------------------
-struct TraceCounts { uint32_t nodes, refs, tests; };
+// Algorithmic work (per lane) and, for the SIMD-efficiency figures, the
+// wave-level iteration counts (accumulated by lane 0 only): a wave pays
+// max-over-lanes of the inner-node and primitive iterations of every step.
+struct TraceCounts { uint32_t nodes, refs, tests, wnodes, wtests, wsteps, wactive; };
 
 // Resumable traversal state of one ray (lives in VGPRs; the short stack in LDS).
 struct KdRay {
@@ -413,14 +416,19 @@ DEV bool kd_traverse(const DevScene &S, float3 o, float3 d, float rayMint, float
 template <bool COUNT>
 DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
     if (!COUNT) return;
-    // wave reduction then one atomic per wave
-    unsigned long long a = c.nodes, b = c.refs, t = c.tests;
-    for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_down(a, off);
-        b += __shfl_down(b, off);
-        t += __shfl_down(t, off);
-    }
-    if (lane_id() == 0) { atomicAdd(ctr + 0, a); atomicAdd(ctr + 1, b); atomicAdd(ctr + 2, t); }
+    // wave reduction then one atomic per counter per wave
+    unsigned long long v[7] = {c.nodes, c.refs, c.tests, c.wnodes, c.wtests, c.wsteps, c.wactive};
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_down(v[k], off);
+    if (lane_id() == 0)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) atomicAdd(ctr + k, v[k]);
+}
+
+DEV uint32_t wave_max(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
 }
 
 // Persistent traversal kernel with lane-level refill (the "while-while +
@@ -494,7 +502,7 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
     Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
-    TraceCounts c{0, 0, 0};
+    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
     uint32_t base, n;
     while (F.next(64u * ROUNDS, base, n)) {
         for (uint32_t rnd = 0; rnd * 64 < n; ++rnd) {
@@ -512,7 +520,7 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths
             else stS(&P.hit[slot], hit_record(r));
         }
     }
-    flush_counts<COUNT>(P.ctr + (SHADOW ? 3 : 0), c);
+    flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
 }
 
 // Persistent traversal kernel with lane-level refill (the "while-while +
@@ -524,7 +532,10 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths
 //   SHADOW = false: closest hit of queue qin (qin < 0: identity over nIdentity
 //                   slots, bounce 0), result -> P.hit
 //   SHADOW = true : any hit of the shadow queue; unoccluded -> L += contribution
-constexpr uint32_t FETCH = 256;
+#ifndef MTSG_FETCH
+#define MTSG_FETCH 256
+#endif
+constexpr uint32_t FETCH = MTSG_FETCH;
 
 template <bool SHADOW, bool COUNT, int MIN_IDLE, bool LEAFIDX = false>
 __global__ void TRACE_ATTR k_trace(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
@@ -534,7 +545,7 @@ __global__ void TRACE_ATTR k_trace(DevScene S, DevPaths P, int qin, uint32_t nId
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
     Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
-    TraceCounts c{0, 0, 0};
+    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
     uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
     bool exhausted = false;
     bool active = false;
@@ -579,13 +590,171 @@ __global__ void TRACE_ATTR k_trace(DevScene S, DevPaths P, int qin, uint32_t nId
             continue;
         }
         // ---- one leaf of traversal for the active lanes
+        const uint32_t n0 = c.nodes, t0 = c.tests;
+        const uint32_t nActive = COUNT ? (uint32_t)__popcll(__ballot(active)) : 0u;
         if (active && kd_step<SHADOW, COUNT, LEAFIDX>(S, r, stk, c)) {
             active = false;
             if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
             else stS(&P.hit[slot], hit_record(r));
         }
+        if (COUNT) {
+            const uint32_t wn = wave_max(c.nodes - n0), wt = wave_max(c.tests - t0);
+            if (__lane_id() == 0) { c.wnodes += wn; c.wtests += wt; c.wsteps += 1; c.wactive += nActive; }
+        }
     }
-    flush_counts<COUNT>(P.ctr + (SHADOW ? 3 : 0), c);
+    flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
+}
+
+// ---------------------------------------------------------------------------
+// Unified traversal ("if-if" order, one fetch per iteration): every iteration
+// advances each active lane by exactly ONE inner node or ONE primitive, and a
+// lane whose leaf is exhausted pops (or restarts) in the same iteration.  The
+// while-while structure above runs, per step, the slowest lane's whole
+// descent and then the largest leaf, which measured 25% (descent) and 17%
+// (leaf) SIMD efficiency on 64-lane waves; here the wave pays one node+prim
+// iteration for the work of up to 64 lanes.  Both fetches (the 16-B sibling
+// pair and the 48-B TriAccel record) are issued by every lane before any
+// branch -- idle lanes read element 0, one cached line -- so an iteration
+// costs one memory latency, not one per branch.
+// ---------------------------------------------------------------------------
+template <bool SHADOW, bool COUNT>
+DEV bool kd_iter(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
+    const uint2 n = r.cur;
+    const bool inner = !(n.x & 0x80000000u);
+    const uint32_t e = n.x & 0x7FFFFFFFu;
+    const bool prim = !inner && e < n.y;
+    const uint4 pr = S.pairs[inner ? (n.x >> 2) : 0u];
+    const float4 *rec = S.triL + 3 * (size_t)(prim ? e : 0u);
+    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
+    // keep the four loads in flight together: without this use the compiler
+    // sinks each load into the branch that consumes it
+    asm volatile("" ::"v"(pr.x), "v"(pr.y), "v"(pr.z), "v"(pr.w), "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
+                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
+    if (inner) {
+        if (COUNT) cnt.nodes++;
+        const uint32_t axis = n.x & 3u;
+        const float split = __uint_as_float(n.y);
+        const float oa = sel3(axis, r.o.x, r.o.y, r.o.z);
+        const float da = sel3(axis, r.d.x, r.d.y, r.d.z);
+        const float ia = sel3(axis, r.inv.x, r.inv.y, r.inv.z);
+        float tsplit = (split - oa) * ia;
+        if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
+        const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
+        const uint2 first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
+        const uint2 second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+        if (tsplit > r.tmax || tsplit <= 0.0f) {
+            r.cur = first;
+        } else if (tsplit < r.tmin) {
+            r.cur = second;
+        } else {
+            const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
+            stk.node[k] = second;
+            stk.t[k] = r.tmax;
+            ++r.sp;
+            if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
+            r.cur = first;
+            r.tmax = tsplit;
+        }
+    } else if (prim) {
+        if (COUNT) { cnt.refs++; cnt.tests++; }
+        float t, u, v;
+        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
+        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+        if (h) {
+            r.found = 1;
+            if (SHADOW) return true;
+            r.best = t; r.bu = u; r.bv = v;
+            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
+        }
+        r.cur.x = n.x + 1u;
+    }
+    // leaf exhausted (also an empty leaf reached by this iteration's descent)
+    const uint2 c = r.cur;
+    if ((c.x & 0x80000000u) && (c.x & 0x7FFFFFFFu) >= c.y) {
+        // Havran's exit test `stack[exPt].t > maxt` (sahkdtree3.h:299)
+        if (r.found && r.best < r.tmax) return true;
+        if (r.sp == r.bottom) {
+            if (r.bottom == 0) return true;
+            r.sp = r.bottom = 0;   // short stack overflowed: kd-restart
+            r.tmin = r.tmax;
+            r.tmax = r.best;
+            r.cur = S.root;
+            return !(r.tmin < r.tmax);
+        }
+        --r.sp;
+        const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
+        r.cur = stk.node[k];
+        r.tmin = r.tmax;
+        r.tmax = fminf(stk.t[k], r.best);
+    }
+    return false;
+}
+
+template <bool SHADOW, bool COUNT, int MIN_IDLE>
+__global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
+    KD_STACK_DECL
+    uint32_t count = nIdentity;
+    if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
+    else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
+    const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
+    Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
+    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
+    uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
+    bool exhausted = false;
+    bool active = false;
+    uint32_t slot = 0;
+    KdRay r;
+    const unsigned long long below = (1ull << __lane_id()) - 1ull;
+    for (;;) {
+        unsigned long long idle = __ballot(!active);
+        if ((uint32_t)__popcll(idle) < (uint32_t)MIN_IDLE && __any(active)) idle = 0;
+        while (idle && !exhausted) {
+            if (poolLeft == 0 && !F.next(FETCH, poolBase, poolLeft)) { exhausted = true; break; }
+            const uint32_t nIdle = (uint32_t)__popcll(idle);
+            const uint32_t take = min(nIdle, poolLeft);
+            const uint32_t rank = (uint32_t)__popcll(idle & below);
+            if (!active && rank < take) {
+                const uint32_t i = poolBase + rank;
+                slot = q ? q[i] : i;
+                float4 ro, rd;
+                load_ray(P, SHADOW, slot, ro, rd);
+                const bool live = kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
+                if (live) {
+                    active = true;
+                } else if (!SHADOW && rd.w < 0.0f) {
+                    // dead slot (outside the render rectangle)
+                } else if (SHADOW) {
+                    shadow_unoccluded(P, slot);
+                } else {
+                    stS(&P.hit[slot], make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)));
+                }
+            }
+            poolBase += take;
+            poolLeft -= take;
+            idle = __ballot(!active);
+            if (take == nIdle) break;
+        }
+        if (!__any(active)) {
+            if (exhausted) break;
+            continue;
+        }
+        if (COUNT && __lane_id() == 0) c.wsteps += 1;
+        if (COUNT) {
+            const uint2 n = r.cur;
+            const bool inner = active && !(n.x & 0x80000000u);
+            const bool prim = active && (n.x & 0x80000000u) && (n.x & 0x7FFFFFFFu) < n.y;
+            const bool anyInner = __any(inner), anyPrim = __any(prim);
+            const uint32_t nActive = (uint32_t)__popcll(__ballot(active));
+            if (__lane_id() == 0) { c.wnodes += anyInner; c.wtests += anyPrim; c.wactive += nActive; }
+        }
+        if (active && kd_iter<SHADOW, COUNT>(S, r, stk, c)) {
+            active = false;
+            if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
+            else stS(&P.hit[slot], hit_record(r));
+        }
+    }
+    flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
 }
 
 // Debug entry points over caller-provided rays
@@ -596,7 +765,7 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_rays(DevScene S, const fl
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float *rr = rays + 8 * (size_t)i;
-    TraceCounts c{0, 0, 0};
+    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
     float best, bu = 0, bv = 0;
     uint32_t bp = 0xFFFFFFFFu;
     bool h = kd_traverse<SHADOW, false>(S, mk3(rr[0], rr[1], rr[2]), mk3(rr[3], rr[4], rr[5]), rr[6], rr[7], best, bu, bv, bp, stk, c);
@@ -1366,7 +1535,7 @@ struct mtsg_scene {
     int cuCount = 0;
     int traceGrid = 0, shadeGrid = 0;
     uint32_t flags = 0;
-    int traceMode = 3;
+    int traceMode = 6;            // unified traversal, refill at 16 idle lanes (measured best)
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
     mtsg_stats stats{};
@@ -1405,8 +1574,8 @@ int ensure_batch(mtsg_scene *s, uint32_t paths) {
     A(q[0], uint32_t); A(q[1], uint32_t); A(qs, uint32_t);
 #undef A
     if ((rc = alloc(CNT_WORDS * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
-    if ((rc = alloc(8 * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
-    HIP_TRY(hipMemset(P.ctr, 0, 8 * sizeof(unsigned long long)));
+    if ((rc = alloc(16 * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
+    HIP_TRY(hipMemset(P.ctr, 0, 16 * sizeof(unsigned long long)));
     s->capacity = paths;
     return MTSG_OK;
 }
@@ -1436,7 +1605,8 @@ void timed_launch(mtsg_scene *s, int kind, F f) {
 // Traversal kernel variants (MTSG_TRACE_MODE, for measurement):
 //   0 = wave fetch 64 / atomic, 1 = wave fetch 4x64 / atomic,
 //   2 = lane refill at >= 1 idle lane, 3 = lane refill at >= 32 idle lanes,
-//   4 = as 3 with indexed leaves (compact tree, one extra dependent load)
+//   4 = as 3 with indexed leaves (compact tree, one extra dependent load),
+//   5/6/7 = unified one-node-or-one-primitive iterations, refill at 32/16/8 idle lanes
 template <bool SHADOW, bool COUNT>
 void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
     dim3 g(s->traceGrid), blk(TRACE_BLOCK);
@@ -1445,6 +1615,9 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
         case 1: hipLaunchKernelGGL((k_trace_wave<SHADOW, COUNT, 4>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 2: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 1>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 4: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 5: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 6: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 7: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 8>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         default: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
     }
 }
@@ -1504,7 +1677,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     s->timed.clear();
     s->cancel.store(0);
     const bool count = (s->flags & MTSG_FLAG_COUNT) != 0;
-    if (count) HIP_TRY(hipMemsetAsync(s->P.ctr, 0, 8 * sizeof(unsigned long long), s->stream));
+    if (count) HIP_TRY(hipMemsetAsync(s->P.ctr, 0, 16 * sizeof(unsigned long long), s->stream));
     DevPaths &P = s->P;
     hipEvent_t cntEv[2];
     HIP_TRY(hipEventCreateWithFlags(&cntEv[0], hipEventDisableTiming));
@@ -1611,14 +1784,22 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
         }
     }
     if (count) {
-        unsigned long long c[6];
+        unsigned long long c[16];
         HIP_TRY(hipMemcpy(c, P.ctr, sizeof(c), hipMemcpyDeviceToHost));
         s->stats.nodes_visited = c[0];
         s->stats.leaf_refs = c[1];
         s->stats.tri_tests = c[2];
-        s->stats.shadow_nodes_visited = c[3];
-        s->stats.shadow_leaf_refs = c[4];
-        s->stats.shadow_tri_tests = c[5];
+        s->stats.wave_node_iters = c[3];
+        s->stats.wave_test_iters = c[4];
+        s->stats.wave_steps = c[5];
+        s->stats.wave_active_lanes = c[6];
+        s->stats.shadow_nodes_visited = c[8];
+        s->stats.shadow_leaf_refs = c[9];
+        s->stats.shadow_tri_tests = c[10];
+        s->stats.shadow_wave_node_iters = c[11];
+        s->stats.shadow_wave_test_iters = c[12];
+        s->stats.shadow_wave_steps = c[13];
+        s->stats.shadow_wave_active_lanes = c[14];
     }
     s->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MTSG_OK;
@@ -1762,11 +1943,12 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     c.has_alpha = hc.has_alpha;
     memcpy(c.filter_values, hc.filter_values, sizeof(c.filter_values));
     // persistent grids from the occupancy query
+    if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     int perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace<false, false, 32>, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
+    const void *occKernel = s->traceMode >= 5 ? (const void *)k_trace_u<false, false, 32> : (const void *)k_trace<false, false, 32>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, occKernel, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;
-    if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     s->shadeGrid = s->cuCount * 8;
     if (hipHostMalloc((void **)&s->hostCnt, 2 * HOSTCNT_STRIDE * sizeof(uint32_t)) != hipSuccess) { g_err = "pinned alloc"; return fail(MTSG_ERR_OOM); }
     *out = s;

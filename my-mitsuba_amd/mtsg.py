@@ -56,6 +56,10 @@ class Stats(C.Structure):
         ("tri_tests", C.c_uint64),
         ("shadow_nodes_visited", C.c_uint64), ("shadow_leaf_refs", C.c_uint64),
         ("shadow_tri_tests", C.c_uint64),
+        ("wave_node_iters", C.c_uint64), ("wave_test_iters", C.c_uint64),
+        ("wave_steps", C.c_uint64), ("wave_active_lanes", C.c_uint64),
+        ("shadow_wave_node_iters", C.c_uint64), ("shadow_wave_test_iters", C.c_uint64),
+        ("shadow_wave_steps", C.c_uint64), ("shadow_wave_active_lanes", C.c_uint64),
     ]
 
 

@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_trace<false, false, 32, false>"
+KERNEL = "k_trace_u<false, false, 16>"
 
 
 def launches(path, counter):
