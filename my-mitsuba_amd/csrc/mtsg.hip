@@ -197,6 +197,11 @@ DEV uint32_t lane_id() { return __lane_id(); }
 // ---------------------------------------------------------------------------
 // primitive tests
 // ---------------------------------------------------------------------------
+// Make three values opaque to the optimiser (no instruction): a select
+// between struct members is otherwise folded into a load through a selected
+// address, which demotes the whole ray state to scratch (see sel3).
+DEV void launder3(float &a, float &b, float &c) { asm("" : "+v"(a), "+v"(b), "+v"(c)); }
+
 // Select component `axis` of (a, b, c) with bit masks.  A ternary chain on
 // struct members gets folded by InstCombine into a load through a selected
 // address, which defeats SROA and demotes the whole ray state to scratch.
@@ -211,10 +216,14 @@ DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, f
     // no FMA contraction: bit-identical t, u, v to the oracle (and Mitsuba's SSE2 build)
 #pragma clang fp contract(off)
     const uint32_t k = __float_as_uint(f0.x);
-    // (u, v, k) = (1,2,0) | (2,0,1) | (0,1,2): bit-mask selects (see sel3)
-    const uint32_t ku = k == 0 ? 1u : (k == 1 ? 2u : 0u), kv = k == 0 ? 2u : (k == 1 ? 0u : 1u);
-    const float o_u = sel3(ku, o.x, o.y, o.z), o_v = sel3(kv, o.x, o.y, o.z), o_k = sel3(k, o.x, o.y, o.z);
-    const float d_u = sel3(ku, d.x, d.y, d.z), d_v = sel3(kv, d.x, d.y, d.z), d_k = sel3(k, d.x, d.y, d.z);
+    // (u, v, k) = (1,2,0) | (2,0,1) | (0,1,2): a rotation of (x, y, z) by k, so
+    // two compares and two selects per component (k >= 3 never hits)
+    const bool k0 = k == 0u, k1 = k == 1u;
+    launder3(o.x, o.y, o.z);
+    launder3(d.x, d.y, d.z);
+    const float o_k = k0 ? o.x : (k1 ? o.y : o.z), d_k = k0 ? d.x : (k1 ? d.y : d.z);
+    const float o_u = k0 ? o.y : (k1 ? o.z : o.x), d_u = k0 ? d.y : (k1 ? d.z : d.x);
+    const float o_v = k0 ? o.z : (k1 ? o.x : o.y), d_v = k0 ? d.z : (k1 ? d.x : d.y);
     const float n_u = f0.y, n_v = f0.z, n_d = f0.w;
     // branch-free on purpose: with an early `t` rejection the compiler sinks
     // the loads of f1/f2 behind it, turning one 48-byte fetch into two or
@@ -265,6 +274,7 @@ struct KdRay {
     uint2 cur;           // current node
     uint32_t sp, bottom;
     uint32_t found;
+    uint32_t dneg;       // bit a: d[a] <= 0 (Havran's tie rule for o[a] == split)
 };
 
 // LDS short stack: far-child node data and its exit distance, SoA by lane
@@ -280,6 +290,7 @@ DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float ray
     r.o = o;
     r.d = d;
     r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.dneg = (d.x <= 0.0f ? 1u : 0u) | (d.y <= 0.0f ? 2u : 0u) | (d.z <= 0.0f ? 4u : 0u);
     // AABB::rayIntersect (aabb.h:308-338)
     float nearT = -INFINITY, farT = INFINITY;
     bool ok = true;
@@ -314,6 +325,24 @@ DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float ray
     return true;
 }
 
+// One kd inner-node decision (sahkdtree3.h:207-262 restated for the
+// t-interval form): tsplit and the near/far children from the sibling pair.
+DEV void kd_node(const KdRay &r, uint2 n, const uint4 &pr, float &tsplit, uint2 &first, uint2 &second) {
+    const uint32_t axis = n.x & 3u;
+    const float split = __uint_as_float(n.y);
+    const bool a0 = axis == 0u, a1 = axis == 1u;
+    float ox = r.o.x, oy = r.o.y, oz = r.o.z, ix = r.inv.x, iy = r.inv.y, iz = r.inv.z;
+    launder3(ox, oy, oz);
+    launder3(ix, iy, iz);
+    const float oa = a0 ? ox : (a1 ? oy : oz);
+    const float ia = a0 ? ix : (a1 ? iy : iz);
+    tsplit = (split - oa) * ia;
+    if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
+    const bool belowFirst = (oa < split) || (oa == split && ((r.dneg >> axis) & 1u));
+    first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
+    second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+}
+
 // Process one leaf: descend from r.cur (one 16-byte sibling-pair load per
 // inner node), test the leaf's primitives, then pop (or restart).  Returns
 // true when the ray is finished.
@@ -322,18 +351,11 @@ DEV bool kd_step(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
     uint2 n = r.cur;
     float tmin = r.tmin, tmax = r.tmax;
     while (!(n.x & 0x80000000u)) {
-        const uint32_t axis = n.x & 3u;
-        const float split = __uint_as_float(n.y);
         const uint4 pr = LEAFIDX ? S.pairsIdx[n.x >> 2] : S.pairs[n.x >> 2];
         if (COUNT) cnt.nodes++;
-        const float oa = sel3(axis, r.o.x, r.o.y, r.o.z);
-        const float da = sel3(axis, r.d.x, r.d.y, r.d.z);
-        const float ia = sel3(axis, r.inv.x, r.inv.y, r.inv.z);
-        float tsplit = (split - oa) * ia;
-        if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
-        const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
-        const uint2 first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
-        const uint2 second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+        float tsplit;
+        uint2 first, second;
+        kd_node(r, n, pr, tsplit, first, second);
         if (tsplit > tmax || tsplit <= 0.0f) {
             n = first;
         } else if (tsplit < tmin) {
@@ -632,16 +654,9 @@ DEV bool kd_iter(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
                  "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
     if (inner) {
         if (COUNT) cnt.nodes++;
-        const uint32_t axis = n.x & 3u;
-        const float split = __uint_as_float(n.y);
-        const float oa = sel3(axis, r.o.x, r.o.y, r.o.z);
-        const float da = sel3(axis, r.d.x, r.d.y, r.d.z);
-        const float ia = sel3(axis, r.inv.x, r.inv.y, r.inv.z);
-        float tsplit = (split - oa) * ia;
-        if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
-        const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
-        const uint2 first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
-        const uint2 second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+        float tsplit;
+        uint2 first, second;
+        kd_node(r, n, pr, tsplit, first, second);
         if (tsplit > r.tmax || tsplit <= 0.0f) {
             r.cur = first;
         } else if (tsplit < r.tmin) {
@@ -691,7 +706,79 @@ DEV bool kd_iter(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
     return false;
 }
 
-template <bool SHADOW, bool COUNT, int MIN_IDLE>
+// Phase-separated variant: an iteration is either a NODE phase (lanes at
+// inner nodes descend one level; one 16-B fetch) or a PRIMITIVE phase (lanes
+// at leaves test one record; one 48-B fetch), chosen per wave from how many
+// lanes are ready for each.  A mixed iteration executes both code paths for
+// every lane (the SIMDs are 16 wide: each wave64 VALU op costs 4 cycles, and
+// the traversal is VALU-throughput bound), so separating them trades a few
+// more iterations for far fewer issued instructions.
+template <bool SHADOW, bool COUNT>
+DEV bool kd_iter_phase(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt, bool primPhase) {
+    const uint2 n = r.cur;
+    const bool inner = !(n.x & 0x80000000u);
+    const uint32_t e = n.x & 0x7FFFFFFFu;
+    if (!primPhase) {
+        if (inner) {
+            if (COUNT) cnt.nodes++;
+            const uint4 pr = S.pairs[n.x >> 2];
+            float tsplit;
+            uint2 first, second;
+            kd_node(r, n, pr, tsplit, first, second);
+            if (tsplit > r.tmax || tsplit <= 0.0f) {
+                r.cur = first;
+            } else if (tsplit < r.tmin) {
+                r.cur = second;
+            } else {
+                const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
+                stk.node[k] = second;
+                stk.t[k] = r.tmax;
+                ++r.sp;
+                if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
+                r.cur = first;
+                r.tmax = tsplit;
+            }
+        }
+    } else if (!inner && e < n.y) {
+        if (COUNT) { cnt.refs++; cnt.tests++; }
+        const float4 *rec = S.triL + 3 * (size_t)e;
+        const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
+        float t, u, v;
+        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
+        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+        if (h) {
+            r.found = 1;
+            if (SHADOW) return true;
+            r.best = t; r.bu = u; r.bv = v;
+            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
+        }
+        r.cur.x = n.x + 1u;
+    }
+    const uint2 c = r.cur;
+    if ((c.x & 0x80000000u) && (c.x & 0x7FFFFFFFu) >= c.y) {
+        if (r.found && r.best < r.tmax) return true;
+        if (r.sp == r.bottom) {
+            if (r.bottom == 0) return true;
+            r.sp = r.bottom = 0;
+            r.tmin = r.tmax;
+            r.tmax = r.best;
+            r.cur = S.root;
+            return !(r.tmin < r.tmax);
+        }
+        --r.sp;
+        const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
+        r.cur = stk.node[k];
+        r.tmin = r.tmax;
+        r.tmax = fminf(stk.t[k], r.best);
+    }
+    return false;
+}
+
+// PRIM_RATIO = 0: unified iterations (kd_iter); otherwise phase-separated
+// (kd_iter_phase) with a primitive phase once primLanes * PRIM_RATIO >=
+// 4 * nodeLanes, or when no lane is at an inner node.
+template <bool SHADOW, bool COUNT, int MIN_IDLE, int PRIM_RATIO = 0>
 __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
     KD_STACK_DECL
     uint32_t count = nIdentity;
@@ -740,7 +827,18 @@ __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t n
             continue;
         }
         if (COUNT && __lane_id() == 0) c.wsteps += 1;
-        if (COUNT) {
+        bool primPhase = false;
+        if (PRIM_RATIO > 0) {
+            const uint2 n = r.cur;
+            const bool inner = active && !(n.x & 0x80000000u);
+            const bool prim = active && (n.x & 0x80000000u) && (n.x & 0x7FFFFFFFu) < n.y;
+            const uint32_t nInner = (uint32_t)__popcll(__ballot(inner)), nPrim = (uint32_t)__popcll(__ballot(prim));
+            primPhase = nPrim > 0 && (nInner == 0 || nPrim * PRIM_RATIO >= 4 * nInner);
+            if (COUNT && __lane_id() == 0) {
+                c.wnodes += !primPhase; c.wtests += primPhase;
+                c.wactive += (uint32_t)__popcll(__ballot(active));
+            }
+        } else if (COUNT) {
             const uint2 n = r.cur;
             const bool inner = active && !(n.x & 0x80000000u);
             const bool prim = active && (n.x & 0x80000000u) && (n.x & 0x7FFFFFFFu) < n.y;
@@ -748,7 +846,12 @@ __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t n
             const uint32_t nActive = (uint32_t)__popcll(__ballot(active));
             if (__lane_id() == 0) { c.wnodes += anyInner; c.wtests += anyPrim; c.wactive += nActive; }
         }
-        if (active && kd_iter<SHADOW, COUNT>(S, r, stk, c)) {
+        bool done = false;
+        if (active) {
+            if (PRIM_RATIO > 0) done = kd_iter_phase<SHADOW, COUNT>(S, r, stk, c, primPhase);
+            else done = kd_iter<SHADOW, COUNT>(S, r, stk, c);
+        }
+        if (done) {
             active = false;
             if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
             else stS(&P.hit[slot], hit_record(r));
@@ -1606,7 +1709,9 @@ void timed_launch(mtsg_scene *s, int kind, F f) {
 //   0 = wave fetch 64 / atomic, 1 = wave fetch 4x64 / atomic,
 //   2 = lane refill at >= 1 idle lane, 3 = lane refill at >= 32 idle lanes,
 //   4 = as 3 with indexed leaves (compact tree, one extra dependent load),
-//   5/6/7 = unified one-node-or-one-primitive iterations, refill at 32/16/8 idle lanes
+//   5/6/7 = unified one-node-or-one-primitive iterations, refill at 32/16/8 idle lanes,
+//   8/9/10/11 = phase-separated iterations, primitive phase once
+//               primLanes >= nodeLanes x 1 / 0.5 / 0.25 / 2
 template <bool SHADOW, bool COUNT>
 void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
     dim3 g(s->traceGrid), blk(TRACE_BLOCK);
@@ -1618,6 +1723,10 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
         case 5: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 6: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 7: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 8>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 8: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 4>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 9: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 8>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 10: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 16>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 11: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 2>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         default: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
     }
 }
