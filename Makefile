@@ -58,7 +58,7 @@ clean:
 	rm -f $(HOST_LIB) $(DEV_LIB) $(PATH_LIB) $(CLI) $(ORACLE) $(ORACLE_FAST)
 
 # Measurement variants of the device library (build/var/, loaded with MTSG_LIB=...)
-VARIANTS := s6:-DMTSG_SHORT_STACK=6 s6f128:-DMTSG_SHORT_STACK=6@-DMTSG_FETCH=128 s6f512:-DMTSG_SHORT_STACK=6@-DMTSG_FETCH=512 s5:-DMTSG_SHORT_STACK=5
+VARIANTS := sh4:-DMTSG_SHADE_WAVES=4 sh5:-DMTSG_SHADE_WAVES=5 sh6:-DMTSG_SHADE_WAVES=6 sh8:-DMTSG_SHADE_WAVES=8
 VAR_LIBS := $(foreach v,$(VARIANTS),build/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
 .PHONY: variants
 variants: $(VAR_LIBS)

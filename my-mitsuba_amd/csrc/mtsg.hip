@@ -1339,7 +1339,15 @@ DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p
 }
 
 // qin < 0: bounce 0 over the identity queue of nIdentity slots
-__global__ void __launch_bounds__(BLOCK) k_shade(DevScene S, DevIntegrator I, DevPaths P, int bounce, int qin,
+#ifndef MTSG_SHADE_WAVES
+#define MTSG_SHADE_WAVES 4   // 127 VGPRs: 4 waves/SIMD (3 at 144; 5+ spill heavily)
+#endif
+#if MTSG_SHADE_WAVES > 0
+#define SHADE_ATTR __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SHADE_WAVES)))
+#else
+#define SHADE_ATTR __launch_bounds__(BLOCK)
+#endif
+__global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int bounce, int qin,
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
     uint32_t count = nIdentity;
