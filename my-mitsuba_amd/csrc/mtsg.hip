@@ -53,6 +53,13 @@ struct DevScene {
     const uint4 *__restrict__ pairsIdx;
     const uint32_t *__restrict__ lidx;
     uint2 rootIdx;
+    // two-level blocks (MTSG_TRACE_MODE 12-13): a block root's 64-B block holds
+    // {children pair, left child's pair, right child's pair, pad}, so one
+    // fetch descends two levels.  Node words: leaf as above; block root
+    // axis | blockIndex << 3; pair-only node (odd level) axis | 4 | slot << 3
+    // with slot = 4 * block + 1|2 (uint4 units).
+    const uint4 *__restrict__ blocks;
+    uint2 root2;
     const float4 *__restrict__ tri;        // 3 float4 per prim (TriAccel, prim order)
     const float4 *__restrict__ vpos;       // xyz
     const float4 *__restrict__ vnrm;       // xyz
@@ -327,7 +334,8 @@ DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float ray
 
 // One kd inner-node decision (sahkdtree3.h:207-262 restated for the
 // t-interval form): tsplit and the near/far children from the sibling pair.
-DEV void kd_node(const KdRay &r, uint2 n, const uint4 &pr, float &tsplit, uint2 &first, uint2 &second) {
+DEV void kd_node(const KdRay &r, uint2 n, const uint4 &pr, float &tsplit, uint2 &first, uint2 &second,
+                 bool &leftFirst) {
     const uint32_t axis = n.x & 3u;
     const float split = __uint_as_float(n.y);
     const bool a0 = axis == 0u, a1 = axis == 1u;
@@ -341,6 +349,7 @@ DEV void kd_node(const KdRay &r, uint2 n, const uint4 &pr, float &tsplit, uint2 
     const bool belowFirst = (oa < split) || (oa == split && ((r.dneg >> axis) & 1u));
     first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
     second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+    leftFirst = belowFirst;
 }
 
 // Process one leaf: descend from r.cur (one 16-byte sibling-pair load per
@@ -355,7 +364,8 @@ DEV bool kd_step(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
         if (COUNT) cnt.nodes++;
         float tsplit;
         uint2 first, second;
-        kd_node(r, n, pr, tsplit, first, second);
+        bool leftFirst;
+        kd_node(r, n, pr, tsplit, first, second, leftFirst);
         if (tsplit > tmax || tsplit <= 0.0f) {
             n = first;
         } else if (tsplit < tmin) {
@@ -656,7 +666,8 @@ DEV bool kd_iter(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
         if (COUNT) cnt.nodes++;
         float tsplit;
         uint2 first, second;
-        kd_node(r, n, pr, tsplit, first, second);
+        bool leftFirst;
+        kd_node(r, n, pr, tsplit, first, second, leftFirst);
         if (tsplit > r.tmax || tsplit <= 0.0f) {
             r.cur = first;
         } else if (tsplit < r.tmin) {
@@ -713,6 +724,87 @@ DEV bool kd_iter(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
 // every lane (the SIMDs are 16 wide: each wave64 VALU op costs 4 cycles, and
 // the traversal is VALU-throughput bound), so separating them trades a few
 // more iterations for far fewer issued instructions.
+// One inner-node step of the t-interval traversal: choose the near child,
+// push the far one when both intervals are non-empty.  Returns the next node.
+DEV uint2 kd_descend(KdRay &r, uint2 n, const uint4 &pr, KdStack stk, bool &nearIsLeft) {
+    float tsplit;
+    uint2 first, second;
+    kd_node(r, n, pr, tsplit, first, second, nearIsLeft);
+    if (tsplit > r.tmax || tsplit <= 0.0f) return first;
+    if (tsplit < r.tmin) { nearIsLeft = !nearIsLeft; return second; }
+    const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
+    stk.node[k] = second;
+    stk.t[k] = r.tmax;
+    ++r.sp;
+    if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
+    r.tmax = tsplit;
+    return first;
+}
+
+// Unified iteration over the two-level block layout: a lane at a block root
+// descends up to two levels per fetch (the 64-B block carries the
+// grandchildren pairs); a lane at a pair-only node (popped from the stack)
+// descends one level.  Otherwise as kd_iter.
+template <bool SHADOW, bool COUNT>
+DEV bool kd_iter2(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
+    const uint2 n = r.cur;
+    const bool inner = !(n.x & 0x80000000u);
+    const bool rootKind = inner && !(n.x & 4u);
+    const uint32_t e = n.x & 0x7FFFFFFFu;
+    const bool prim = !inner && e < n.y;
+    const uint4 *blk = S.blocks + (inner ? (rootKind ? 4u * (n.x >> 3) : (n.x >> 3)) : 0u);
+    const uint4 p0 = blk[0], p1 = blk[1], p2 = blk[2];
+    const float4 *rec = S.triL + 3 * (size_t)(prim ? e : 0u);
+    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
+    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(p1.x), "v"(p1.y), "v"(p1.z), "v"(p1.w),
+                 "v"(p2.x), "v"(p2.y), "v"(p2.z), "v"(p2.w), "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
+                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
+    if (inner) {
+        if (COUNT) cnt.nodes++;
+        bool nearLeft;
+        const uint2 c = kd_descend(r, n, p0, stk, nearLeft);
+        r.cur = c;
+        if (rootKind && !(c.x & 0x80000000u)) {
+            // second level from the same block (c is a pair-only node)
+            if (COUNT) cnt.nodes++;
+            const uint4 pc = nearLeft ? p1 : p2;
+            bool dummy;
+            r.cur = kd_descend(r, c, pc, stk, dummy);
+        }
+    } else if (prim) {
+        if (COUNT) { cnt.refs++; cnt.tests++; }
+        float t, u, v;
+        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
+        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+        if (h) {
+            r.found = 1;
+            if (SHADOW) return true;
+            r.best = t; r.bu = u; r.bv = v;
+            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
+        }
+        r.cur.x = n.x + 1u;
+    }
+    const uint2 c = r.cur;
+    if ((c.x & 0x80000000u) && (c.x & 0x7FFFFFFFu) >= c.y) {
+        if (r.found && r.best < r.tmax) return true;
+        if (r.sp == r.bottom) {
+            if (r.bottom == 0) return true;
+            r.sp = r.bottom = 0;
+            r.tmin = r.tmax;
+            r.tmax = r.best;
+            r.cur = S.root2;
+            return !(r.tmin < r.tmax);
+        }
+        --r.sp;
+        const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
+        r.cur = stk.node[k];
+        r.tmin = r.tmax;
+        r.tmax = fminf(stk.t[k], r.best);
+    }
+    return false;
+}
+
 template <bool SHADOW, bool COUNT>
 DEV bool kd_iter_phase(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt, bool primPhase) {
     const uint2 n = r.cur;
@@ -724,7 +816,8 @@ DEV bool kd_iter_phase(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cn
             const uint4 pr = S.pairs[n.x >> 2];
             float tsplit;
             uint2 first, second;
-            kd_node(r, n, pr, tsplit, first, second);
+            bool leftFirst;
+            kd_node(r, n, pr, tsplit, first, second, leftFirst);
             if (tsplit > r.tmax || tsplit <= 0.0f) {
                 r.cur = first;
             } else if (tsplit < r.tmin) {
@@ -778,7 +871,7 @@ DEV bool kd_iter_phase(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cn
 // PRIM_RATIO = 0: unified iterations (kd_iter); otherwise phase-separated
 // (kd_iter_phase) with a primitive phase once primLanes * PRIM_RATIO >=
 // 4 * nodeLanes, or when no lane is at an inner node.
-template <bool SHADOW, bool COUNT, int MIN_IDLE, int PRIM_RATIO = 0>
+template <bool SHADOW, bool COUNT, int MIN_IDLE, int PRIM_RATIO = 0, bool LAYOUT2 = false>
 __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
     KD_STACK_DECL
     uint32_t count = nIdentity;
@@ -807,6 +900,7 @@ __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t n
                 float4 ro, rd;
                 load_ray(P, SHADOW, slot, ro, rd);
                 const bool live = kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
+                if (LAYOUT2) r.cur = S.root2;
                 if (live) {
                     active = true;
                 } else if (!SHADOW && rd.w < 0.0f) {
@@ -848,7 +942,8 @@ __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t n
         }
         bool done = false;
         if (active) {
-            if (PRIM_RATIO > 0) done = kd_iter_phase<SHADOW, COUNT>(S, r, stk, c, primPhase);
+            if (LAYOUT2) done = kd_iter2<SHADOW, COUNT>(S, r, stk, c);
+            else if (PRIM_RATIO > 0) done = kd_iter_phase<SHADOW, COUNT>(S, r, stk, c, primPhase);
             else done = kd_iter<SHADOW, COUNT>(S, r, stk, c);
         }
         if (done) {
@@ -1646,7 +1741,7 @@ struct mtsg_scene {
     int cuCount = 0;
     int traceGrid = 0, shadeGrid = 0;
     uint32_t flags = 0;
-    int traceMode = 6;            // unified traversal, refill at 16 idle lanes (measured best)
+    int traceMode = 12;           // unified traversal over two-level blocks, refill at 16 idle lanes (measured best)
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
     mtsg_stats stats{};
@@ -1719,7 +1814,8 @@ void timed_launch(mtsg_scene *s, int kind, F f) {
 //   4 = as 3 with indexed leaves (compact tree, one extra dependent load),
 //   5/6/7 = unified one-node-or-one-primitive iterations, refill at 32/16/8 idle lanes,
 //   8/9/10/11 = phase-separated iterations, primitive phase once
-//               primLanes >= nodeLanes x 1 / 0.5 / 0.25 / 2
+//               primLanes >= nodeLanes x 1 / 0.5 / 0.25 / 2,
+//   12/13 = unified iterations over the two-level block layout, refill at 16/32
 template <bool SHADOW, bool COUNT>
 void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
     dim3 g(s->traceGrid), blk(TRACE_BLOCK);
@@ -1735,6 +1831,8 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
         case 9: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 8>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 10: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 16>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 11: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 2>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 12: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 0, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 13: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 32, 0, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         default: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
     }
 }
@@ -2029,12 +2127,36 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         return fail(MTSG_ERR_INVALID);
     }
     if (pairs.empty()) { pairs.push_back(make_uint4(0, 0, 0, 0)); pairsIdx.push_back(make_uint4(0, 0, 0, 0)); }
+    // ---- two-level blocks from the binary pair layout
+    std::vector<uint4> blocks;
+    blocks.reserve(pairs.size() * 2 + 8);
+    std::function<uint2(uint2, bool, uint32_t)> conv2 = [&](uint2 w, bool root, uint32_t slot) -> uint2 {
+        if (w.x & 0x80000000u) return w;                       // leaf: unchanged
+        const uint4 pr = pairs[w.x >> 2];
+        const uint2 L = make_uint2(pr.x, pr.y), R = make_uint2(pr.z, pr.w);
+        if (root) {
+            const uint32_t b = (uint32_t)(blocks.size() / 4);
+            blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));
+            const uint2 nL = conv2(L, false, 4 * b + 1);
+            const uint2 nR = conv2(R, false, 4 * b + 2);
+            blocks[4 * b] = make_uint4(nL.x, nL.y, nR.x, nR.y);
+            return make_uint2((w.x & 3u) | (b << 3), w.y);
+        }
+        // pair-only node: its children are block roots (or leaves)
+        const uint2 nL = conv2(L, true, 0), nR = conv2(R, true, 0);
+        blocks[slot] = make_uint4(nL.x, nL.y, nR.x, nR.y);
+        return make_uint2((w.x & 3u) | 4u | (slot << 3), w.y);
+    };
+    const uint2 root2 = conv2(root, true, 0);
+    blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));   // slack for the 3-slot fetch of the last slot
+    if (blocks.size() >= (1u << 29)) { g_err = "kd-tree too large for the two-level layout"; return fail(MTSG_ERR_INVALID); }
     if (triL.empty()) triL.resize(3, make_float4(0, 0, 0, 0));
-    uint4 *dpairs, *dpairsIdx; float4 *dtriL; uint32_t *dlidx; const uint32_t zero = 0; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu; uint4 *dtidx;
+    uint4 *dpairs, *dpairsIdx, *dblocks; float4 *dtriL; uint32_t *dlidx; const uint32_t zero = 0; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu; uint4 *dtidx;
     mtsg_rect *rects; mtsg_shape *shapes; mtsg_bsdf *bsdfs; mtsg_emitter *emitters; float *ecdf, *etcdf;
     if ((rc = up(pairs.data(), pairs.size(), &dpairs)) ||
         (rc = up(triL.data(), triL.size(), &dtriL)) ||
         (rc = up(pairsIdx.data(), pairsIdx.size(), &dpairsIdx)) ||
+        (rc = up(blocks.data(), blocks.size(), &dblocks)) ||
         (rc = d->n_indices ? up(d->indices, d->n_indices, &dlidx) : up(&zero, 1, &dlidx)) ||
         (rc = up((const float4 *)d->triaccel, (size_t)d->n_prims * 3, &tri)) ||
         (rc = up(vpos.data(), vpos.size(), &dvpos)) || (rc = up(vnrm.data(), vnrm.size(), &dvnrm)) ||
@@ -2044,6 +2166,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         (rc = up(d->emitter_cdf, d->n_emitters + 1, &ecdf)) ||
         (rc = up(d->emitter_tri_cdf, d->n_emitter_tri_cdf, &etcdf)))
         return fail(rc);
+    ds.blocks = dblocks; ds.root2 = root2;
     ds.pairs = dpairs; ds.triL = dtriL; ds.root = root; ds.pairsIdx = dpairsIdx; ds.lidx = dlidx; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
     ds.tidx = dtidx; ds.tdpdu = dtdpdu; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
@@ -2062,7 +2185,8 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     // persistent grids from the occupancy query
     if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     int perCU = 0;
-    const void *occKernel = s->traceMode >= 5 ? (const void *)k_trace_u<false, false, 32> : (const void *)k_trace<false, false, 32>;
+    const void *occKernel = s->traceMode >= 12 ? (const void *)k_trace_u<false, false, 16, 0, true>
+                          : s->traceMode >= 5 ? (const void *)k_trace_u<false, false, 32> : (const void *)k_trace<false, false, 32>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, occKernel, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;

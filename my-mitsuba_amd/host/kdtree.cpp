@@ -190,7 +190,7 @@ struct Builder {
             jobs->push_back(std::move(j));
             return;
         }
-        Split sp = (N <= 2048 || N <= (size_t)P.exactPrimThreshold / 32) ? findExact(box, prims) : findBinned(box, prims);
+        Split sp = N <= (size_t)P.exactSweepLimit ? findExact(box, prims) : findBinned(box, prims);
         if (sp.axis < 0) { makeLeaf(s, slot, prims, depth); return; }
         if (sp.cost >= leafCost) {
             if ((sp.cost > 4 * leafCost && N < 16) || badRefines >= P.maxBadRefines) { makeLeaf(s, slot, prims, depth); return; }

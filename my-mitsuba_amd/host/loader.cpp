@@ -1022,6 +1022,13 @@ int g_defaultKDThreads = 0;
 std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::string, std::string> &defines) {
     auto scene = std::make_unique<Scene>();
     scene->kd.threads = g_defaultKDThreads;
+    // build-parameter overrides (tree-quality experiments; defaults follow gkdtree.h:734-744)
+    if (const char *v = getenv("MTSH_KD_TRAVERSAL")) scene->kd.traversalCost = (float)atof(v);
+    if (const char *v = getenv("MTSH_KD_QUERY")) scene->kd.queryCost = (float)atof(v);
+    if (const char *v = getenv("MTSH_KD_EMPTY_BONUS")) scene->kd.emptySpaceBonus = (float)atof(v);
+    if (const char *v = getenv("MTSH_KD_STOP_PRIMS")) scene->kd.stopPrims = atoi(v);
+    if (const char *v = getenv("MTSH_KD_EXACT_LIMIT")) scene->kd.exactSweepLimit = atoi(v);
+    if (const char *v = getenv("MTSH_KD_MAX_DEPTH")) scene->kd.maxDepth = atoi(v);
     Loader L(*scene);
     L.defines = defines;
     L.dirStack.push_back(dirName(path));

@@ -95,6 +95,7 @@ struct KDBuildParams {                // gkdtree.h:734-744 defaults
     float traversalCost = 15, queryCost = 20, emptySpaceBonus = 0.9f;
     int stopPrims = 6, maxBadRefines = 3, minMaxBins = 128;
     int exactPrimThreshold = 65536;
+    int exactSweepLimit = 65536;      // exact O(n log n) sweep below exactPrimThreshold (gkdtree.h:980, 1510), binned above
     bool clip = true;
     int maxDepth = 0;                 // 0 = 8 + 1.3 log2(N) (gkdtree.h:986-988)
     int threads = 0;                  // 0 = hardware concurrency
