@@ -58,7 +58,7 @@ clean:
 	rm -f $(HOST_LIB) $(DEV_LIB) $(PATH_LIB) $(CLI) $(ORACLE) $(ORACLE_FAST)
 
 # Measurement variants of the device library (build/var/, loaded with MTSG_LIB=...)
-VARIANTS := sh4:-DMTSG_SHADE_WAVES=4 sh5:-DMTSG_SHADE_WAVES=5 sh6:-DMTSG_SHADE_WAVES=6 sh8:-DMTSG_SHADE_WAVES=8
+VARIANTS := w8:-DMTSG_TRACE_WAVES=8 s5:-DMTSG_SHORT_STACK=5 s8:-DMTSG_SHORT_STACK=8
 VAR_LIBS := $(foreach v,$(VARIANTS),build/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
 .PHONY: variants
 variants: $(VAR_LIBS)

@@ -65,6 +65,9 @@ struct DevScene {
     const float4 *__restrict__ vnrm;       // xyz
     const uint4 *__restrict__ tidx;        // i0, i1, i2, shape
     const float4 *__restrict__ tdpdu;      // dpdu xyz
+    // per-triangle shading record, 6 float4 (96 B, one contiguous fetch per hit):
+    //   p0 p1 p2 | n0 n1 n2 | dpdu | shape, bsdf | faceNormals << 31, emitter
+    const float4 *__restrict__ shrec;
     const mtsg_rect *__restrict__ rects;
     const mtsg_shape *__restrict__ shapes;
     const mtsg_bsdf *__restrict__ bsdfs;
@@ -1342,7 +1345,7 @@ DEV uint32_t pmf_sample_reuse(const float *cdf, uint32_t n, float &x, float &pdf
 struct Its {
     float3 p, geoN;
     Frame3 sh;
-    int shape;
+    int shape, bsdf, emitter;
 };
 
 // ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428) + computeShadingFrame (util.cpp:603-608)
@@ -1350,16 +1353,21 @@ DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, Its &its) {
     const uint32_t p = __float_as_uint(h.w);   // triangle, or 0x80000000 | rectangle
     float3 dpdu, n;
     if (!(p & 0x80000000u)) {
-        const uint4 ti = S.tidx[p];
-        its.shape = (int)ti.w;
+        const float4 *rec = S.shrec + 6 * (size_t)p;
+        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3], r4 = rec[4], r5 = rec[5];
+        const float3 p0 = mk3(r0.x, r0.y, r0.z), p1 = mk3(r0.w, r1.x, r1.y), p2 = mk3(r1.z, r1.w, r2.x);
+        const float3 n0 = mk3(r2.y, r2.z, r2.w), n1 = mk3(r3.x, r3.y, r3.z), n2 = mk3(r3.w, r4.x, r4.y);
+        dpdu = mk3(r4.z, r4.w, r5.x);
+        its.shape = (int)__float_as_uint(r5.y);
+        const uint32_t bw = __float_as_uint(r5.z);
+        its.bsdf = (int)(bw & 0x7FFFFFFFu);
+        its.emitter = (int)__float_as_uint(r5.w);
         const float bx = 1 - h.y - h.z, by = h.y, bz = h.z;
-        const float3 p0 = xyz(S.vpos[ti.x]), p1 = xyz(S.vpos[ti.y]), p2 = xyz(S.vpos[ti.z]);
         its.p = p0 * bx + p1 * by + p2 * bz;
         float3 fn = cross(p1 - p0, p2 - p0);
         if (!isZero(fn)) fn = fn / length(fn);
-        dpdu = xyz(S.tdpdu[p]);
-        if (!S.shapes[ti.w].face_normals) {
-            n = normalize(xyz(S.vnrm[ti.x]) * bx + xyz(S.vnrm[ti.y]) * by + xyz(S.vnrm[ti.z]) * bz);
+        if (!(bw & 0x80000000u)) {
+            n = normalize(n0 * bx + n1 * by + n2 * bz);
             if (dot(fn, n) < 0) fn = -fn;
         } else {
             n = fn;
@@ -1368,6 +1376,8 @@ DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, Its &its) {
     } else {
         const mtsg_rect &r = S.rects[p & 0x7FFFFFFFu];
         its.shape = (int)r.shape_index;
+        its.bsdf = S.shapes[its.shape].bsdf;
+        its.emitter = S.shapes[its.shape].emitter;
         its.geoN = ld3(r.frame_n);
         n = its.geoN;
         dpdu = ld3(r.dpdu);
@@ -1485,7 +1495,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
                 if (!valid) {
                     done = true;
                 } else {
-                    const int em = S.shapes[its.shape].emitter;
+                    const int em = its.emitter;
                     if (em >= 0) {
                         const mtsg_emitter &E = S.emitters[em];
                         const float3 value = dot(its.sh.n, -rd) > 0 ? ld3(E.radiance) : mk3(0, 0, 0);
@@ -1509,11 +1519,10 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
             }
             if (!done && !((int)depth <= I.max_depth || I.max_depth < 0)) done = true;
             if (!done) {
-                const mtsg_shape &shp = S.shapes[its.shape];
-                const mtsg_bsdf &bsdf = S.bsdfs[shp.bsdf];
+                const mtsg_bsdf &bsdf = S.bsdfs[its.bsdf];
                 const float3 wi = its.sh.toLocal(-rd);
-                if (bounce == 0 && shp.emitter >= 0 && !I.hide_emitters) {
-                    if (dot(its.sh.n, -rd) > 0) L += T * ld3(S.emitters[shp.emitter].radiance);
+                if (bounce == 0 && its.emitter >= 0 && !I.hide_emitters) {
+                    if (dot(its.sh.n, -rd) > 0) L += T * ld3(S.emitters[its.emitter].radiance);
                 }
                 if (((int)depth >= I.max_depth && I.max_depth > 0) ||
                     (I.strict_normals && dot(rd, its.geoN) * wi.z >= 0)) {
@@ -2078,6 +2087,25 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     for (uint32_t sh = 0; sh < d->n_shapes; ++sh)
         if (d->shapes[sh].type == MTSG_SHAPE_MESH)
             for (uint32_t t = 0; t < d->shapes[sh].tri_count; ++t) tidx[d->shapes[sh].tri_begin + t].w = sh;
+    std::vector<float4> shrec((size_t)d->n_triangles * 6);
+    for (uint32_t t = 0; t < d->n_triangles; ++t) {
+        const uint4 ti = tidx[t];
+        if (ti.x >= d->n_vertices || ti.y >= d->n_vertices || ti.z >= d->n_vertices || ti.w >= d->n_shapes) {
+            g_err = "triangle index out of range";
+            return fail(MTSG_ERR_INVALID);
+        }
+        const float *P = d->vtx_pos, *N = d->vtx_nrm;
+        float f[24];
+        for (int k = 0; k < 3; ++k) {
+            f[k] = P[3 * ti.x + k]; f[3 + k] = P[3 * ti.y + k]; f[6 + k] = P[3 * ti.z + k];
+            f[9 + k] = N[3 * ti.x + k]; f[12 + k] = N[3 * ti.y + k]; f[15 + k] = N[3 * ti.z + k];
+            f[18 + k] = d->tri_dpdu[3 * t + k];
+        }
+        const mtsg_shape &sh = d->shapes[ti.w];
+        uint32_t u[3] = {ti.w, (uint32_t)sh.bsdf | (sh.face_normals ? 0x80000000u : 0u), (uint32_t)sh.emitter};
+        memcpy(f + 21, u, sizeof(u));
+        memcpy(&shrec[6 * (size_t)t], f, sizeof(f));
+    }
     int rc;
     DevScene &ds = s->ds;
     auto up = [&](auto *src, size_t n, auto **dst) {
@@ -2151,7 +2179,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));   // slack for the 3-slot fetch of the last slot
     if (blocks.size() >= (1u << 29)) { g_err = "kd-tree too large for the two-level layout"; return fail(MTSG_ERR_INVALID); }
     if (triL.empty()) triL.resize(3, make_float4(0, 0, 0, 0));
-    uint4 *dpairs, *dpairsIdx, *dblocks; float4 *dtriL; uint32_t *dlidx; const uint32_t zero = 0; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu; uint4 *dtidx;
+    uint4 *dpairs, *dpairsIdx, *dblocks; float4 *dtriL; uint32_t *dlidx; const uint32_t zero = 0; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu, *dshrec; uint4 *dtidx;
     mtsg_rect *rects; mtsg_shape *shapes; mtsg_bsdf *bsdfs; mtsg_emitter *emitters; float *ecdf, *etcdf;
     if ((rc = up(pairs.data(), pairs.size(), &dpairs)) ||
         (rc = up(triL.data(), triL.size(), &dtriL)) ||
@@ -2161,6 +2189,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         (rc = up((const float4 *)d->triaccel, (size_t)d->n_prims * 3, &tri)) ||
         (rc = up(vpos.data(), vpos.size(), &dvpos)) || (rc = up(vnrm.data(), vnrm.size(), &dvnrm)) ||
         (rc = up(tidx.data(), tidx.size(), &dtidx)) || (rc = up(tdpdu.data(), tdpdu.size(), &dtdpdu)) ||
+        (rc = up(shrec.data(), shrec.size(), &dshrec)) ||
         (rc = up(d->rects, d->n_rects, &rects)) || (rc = up(d->shapes, d->n_shapes, &shapes)) ||
         (rc = up(d->bsdfs, d->n_bsdfs, &bsdfs)) || (rc = up(d->emitters, d->n_emitters, &emitters)) ||
         (rc = up(d->emitter_cdf, d->n_emitters + 1, &ecdf)) ||
@@ -2168,7 +2197,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         return fail(rc);
     ds.blocks = dblocks; ds.root2 = root2;
     ds.pairs = dpairs; ds.triL = dtriL; ds.root = root; ds.pairsIdx = dpairsIdx; ds.lidx = dlidx; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
-    ds.tidx = dtidx; ds.tdpdu = dtdpdu; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
+    ds.tidx = dtidx; ds.tdpdu = dtdpdu; ds.shrec = dshrec; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
     ds.n_emitters = d->n_emitters;
     ds.n_tri = d->n_triangles;
