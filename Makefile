@@ -23,7 +23,7 @@ ORACLE      := oracle/liboracle.so
 ORACLE_FAST := oracle/liboracle_fast.so
 
 .PHONY: all host device oracle clean
-all: host device oracle $(PATH_LIB) $(CLI)
+all: host device oracle $(PATH_LIB) $(CLI) scenes/sky512.pfm
 host: $(HOST_LIB)
 device: $(DEV_LIB)
 oracle: $(ORACLE) $(ORACLE_FAST)
@@ -54,11 +54,15 @@ $(ORACLE_FAST): oracle/oracle.cpp oracle/oracle.h include/mtsg.h
 	$(CXX) -std=c++17 -O3 -msse2 -march=nocona -funsafe-math-optimizations -fPIC -shared \
 	    -o $@ oracle/oracle.cpp -lpthread
 
+# synthetic HDR environment for the envmap scenes (tools/gen_envmap.py)
+scenes/sky512.pfm: tools/gen_envmap.py
+	python3 tools/gen_envmap.py $@ 512 256
+
 clean:
 	rm -f $(HOST_LIB) $(DEV_LIB) $(PATH_LIB) $(CLI) $(ORACLE) $(ORACLE_FAST)
 
 # Measurement variants of the device library (build/var/, loaded with MTSG_LIB=...)
-VARIANTS := w8:-DMTSG_TRACE_WAVES=8 s5:-DMTSG_SHORT_STACK=5 s8:-DMTSG_SHORT_STACK=8
+VARIANTS := nofma:-ffp-contract=off
 VAR_LIBS := $(foreach v,$(VARIANTS),build/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
 .PHONY: variants
 variants: $(VAR_LIBS)

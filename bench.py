@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="bunny15", choices=["bunny15", "cbox"])
+    ap.add_argument("--workload", default="bunny15", choices=["bunny15", "cbox", "c5"])
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
@@ -96,6 +96,11 @@ def max_over_ranks(pg, x):
 
 
 def scene_args(a):
+    if a.workload == "c5":
+        # C5: dielectric + rough copper bunnies under an HDR environment, maxDepth 64
+        # (scenes/env_glass.xml; 1920x1080x1024 unless overridden)
+        path = os.path.join(REPO, "scenes", "env_glass.xml")
+        return path, {"width": a.width, "height": a.height, "spp": a.spp, "maxDepth": 64}
     path = os.path.join(REPO, "scenes", "bunny15.xml" if a.workload == "bunny15" else "cbox.xml")
     defs = {"width": a.width, "height": a.height, "spp": a.spp, "maxDepth": 8}
     return path, defs
@@ -236,9 +241,11 @@ def main():
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": ("C3 instanced bunny x15 (1,041,765 tris), roughconductor Cu GGX 0.2"
-                                    if a.workload == "bunny15" else "C2 Cornell box, diffuse + area emitter"),
-                       "resolution": f"{params.tile_w}x{params.tile_h}", "spp": params.spp, "max_depth": 8,
+            "config": {"workload": {"bunny15": "C3 instanced bunny x15 (1,041,765 tris), roughconductor Cu GGX 0.2",
+                                    "cbox": "C2 Cornell box, diffuse + area emitter",
+                                    "c5": "C5 dielectric + roughconductor bunnies, HDR envmap, maxDepth 64"}[a.workload],
+                       "resolution": f"{params.tile_w}x{params.tile_h}", "spp": params.spp,
+                       "max_depth": 64 if a.workload == "c5" else 8,
                        "samples_per_step": params.tile_w * params.tile_h * params.spp,
                        "parallelism": f"film tiles round-robin over {world} GPU(s)",
                        "scene_load_s": round(load_s, 2)},

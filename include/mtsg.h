@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MTSG_ABI_VERSION 1
+#define MTSG_ABI_VERSION 2
 
 /* ---- error codes (mtsg_last_error() gives the message) ------------------ */
 enum {
@@ -113,7 +113,31 @@ typedef struct mtsg_bsdf {
     float ior_eta, ior_inv_eta; /* dielectric intIOR/extIOR and inverse     */
 } mtsg_bsdf;
 
-enum { MTSG_EMITTER_AREA = 1 };
+enum { MTSG_EMITTER_AREA = 1, MTSG_EMITTER_ENVMAP = 2 };
+
+#define MTSG_ENVMAP_MAX_LEVELS 24
+#define MTSG_MIPMAP_LUT_SIZE 64      /* MTS_MIPMAP_LUT_SIZE (mipmap.h:37) */
+
+/* Environment emitter (src/emitters/envmap.cpp:99-660): lat-long RGB MIP
+ * pyramid (texel values already rounded to half precision, as Mitsuba's
+ * TMIPMap<Spectrum, SpectrumHalf> stores them), row/column CDFs for
+ * importance sampling, and the scene bounding sphere the shadow rays end on.
+ * Boundary conditions: u repeats, v clamps (envmap.cpp:160-161). */
+typedef struct mtsg_envmap {
+    int32_t levels;
+    int32_t level_w[MTSG_ENVMAP_MAX_LEVELS], level_h[MTSG_ENVMAP_MAX_LEVELS];
+    uint32_t level_offset[MTSG_ENVMAP_MAX_LEVELS];   /* float offset of each level in texels (RGB) */
+    float size_ratio_x[MTSG_ENVMAP_MAX_LEVELS], size_ratio_y[MTSG_ENVMAP_MAX_LEVELS];
+    float scale;                  /* 'scale' property                        */
+    float to_world[9], to_local[9];  /* rotation part of toWorld and its inverse (row-major) */
+    float bsphere_center[3], bsphere_radius;   /* scene bsphere x 1.5 (envmap.cpp:321-325) */
+    float normalization;          /* envmap.cpp:300-301                      */
+    float pixel_size[2];          /* (2 pi / w, pi / h)                      */
+    float max_anisotropy;         /* 10 (envmap.cpp:144)                     */
+    float weight_lut[MTSG_MIPMAP_LUT_SIZE];   /* EWA Gaussian (mipmap.h:296-301) */
+    int32_t emitter;              /* index into emitters                     */
+    int32_t pad[3];
+} mtsg_envmap;
 
 typedef struct mtsg_emitter {
     int32_t type;
@@ -175,6 +199,14 @@ typedef struct mtsg_scene_desc {
     float aabb_min[3], aabb_max[3];  /* enlarged tree AABB (gkdtree.h:1213-1220) */
     uint32_t max_depth;           /* deepest leaf (traversal stack bound)  */
     mtsg_camera camera;
+    /* environment emitter (has_envmap = 0: none) */
+    int32_t has_envmap;
+    uint32_t n_env_texels;        /* floats: 3 per texel over all levels    */
+    const float *env_texels;
+    const float *env_cdf_rows;    /* level-0 height + 1                      */
+    const float *env_cdf_cols;    /* (level-0 width + 1) * height            */
+    const float *env_row_weights; /* height                                  */
+    mtsg_envmap envmap;
 } mtsg_scene_desc;
 
 /* ---- render ------------------------------------------------------------- */
@@ -275,6 +307,12 @@ int  mtsg_set_batch_paths(mtsg_scene *scene, uint32_t paths);
  * ShapeKDTree::rayIntersect (src/librender/skdtree.cpp:112-142) including
  * the adaptive epsilon when mint == 1e-4 (Epsilon).  Misses give
  * prim = 0xFFFFFFFF.  rays: 8 floats per ray {ox,oy,oz,dx,dy,dz,mint,maxt}. */
+/* Debug: environment radiance (x scale) along n world directions (3n
+ * floats); rx/ry = NULL -> bilinear level-0 lookup (BSDF-sampled rays), else
+ * EWA lookup with those differential directions (camera rays).
+ * EnvironmentMap::evalEnvironment, src/emitters/envmap.cpp:380-410. */
+int  mtsg_env_eval(mtsg_scene *scene, uint32_t n, const float *dirs, const float *rx, const float *ry, float *out);
+
 int  mtsg_trace_closest(mtsg_scene *scene, uint32_t n, const float *rays,
                         float *t, float *u, float *v, uint32_t *prim);
 /* Shadow variant (skdtree.cpp:207-226): occluded[i] = 1 if any hit. */

@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef DEV
 #define DEV __device__ __forceinline__
+#endif
 
 namespace mtsg {
 

@@ -32,6 +32,7 @@
 
 #include "../../include/mtsg.h"
 #include "device_math.h"
+#include "envmap.h"
 
 using namespace mtsg;
 
@@ -76,6 +77,8 @@ struct DevScene {
     const float *__restrict__ emitter_tri_cdf;
     uint32_t n_emitters, n_tri;
     float bmin[3], bmax[3];
+    int has_env;
+    DevEnv env;
 };
 
 struct DevCamera {
@@ -86,6 +89,8 @@ struct DevCamera {
     float filter_radius, filter_scale;
     int border, has_alpha;
     float filter_values[32];
+    float dx[3], dy[3];   // near-plane differentials (perspective.cpp:160-170)
+    int has_env;          // store primary-ray differentials for the environment lookup
 };
 
 struct DevIntegrator {
@@ -958,6 +963,19 @@ __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t n
     flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
 }
 
+// Debug entry point: environment radiance along directions (rx/ry null:
+// bilinear level-0 lookup; else EWA with those differential directions)
+__global__ void k_env_eval(DevScene S, const float *dirs, const float *rx, const float *ry, uint32_t n, float *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float3 d = mk3(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+    const bool diff = rx != nullptr;
+    const float3 x = diff ? mk3(rx[3 * i], rx[3 * i + 1], rx[3 * i + 2]) : d;
+    const float3 y = diff ? mk3(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]) : d;
+    const float3 v = env_eval(S.env, d, diff, x, y);
+    out[3 * i] = v.x; out[3 * i + 1] = v.y; out[3 * i + 2] = v.z;
+}
+
 // Debug entry points over caller-provided rays
 template <bool SHADOW>
 __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_rays(DevScene S, const float *rays, uint32_t n, float *t,
@@ -1020,6 +1038,19 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
                             t[8] * d.x + t[9] * d.y + t[10] * d.z);
             stS(&P.ray_o[slot], make_float4(t[3], t[7], t[11], C.near_clip * invZ));
             stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
+            if (C.has_env) {
+                // rx/ryDirection scaled by 1/sqrt(spp) (integrator.cpp:148-149, ray.h:163-168),
+                // parked in the shadow-ray slots until bounce 0 is shaded
+                const float3 rxc = normalize(nearP + ld3(C.dx)), ryc = normalize(nearP + ld3(C.dy));
+                const float3 rx = mk3(t[0] * rxc.x + t[1] * rxc.y + t[2] * rxc.z, t[4] * rxc.x + t[5] * rxc.y + t[6] * rxc.z,
+                                      t[8] * rxc.x + t[9] * rxc.y + t[10] * rxc.z);
+                const float3 ry = mk3(t[0] * ryc.x + t[1] * ryc.y + t[2] * ryc.z, t[4] * ryc.x + t[5] * ryc.y + t[6] * ryc.z,
+                                      t[8] * ryc.x + t[9] * ryc.y + t[10] * ryc.z);
+                const float scale = 1.0f / sqrtf((float)I.spp);
+                const float3 rxs = wd + (rx - wd) * scale, rys = wd + (ry - wd) * scale;
+                stS(&P.sh_o[slot], make_float4(rxs.x, rxs.y, rxs.z, 0.f));
+                stS(&P.sh_d[slot], make_float4(rys.x, rys.y, rys.z, 0.f));
+            }
             stS(&P.L[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
             stS(&P.T[slot], make_float4(1.f, 1.f, 1.f, 1.f));
             stS(&P.key[slot], make_uint2((uint32_t)key, (uint32_t)(key >> 32)));
@@ -1452,6 +1483,9 @@ DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p
 #else
 #define SHADE_ATTR __launch_bounds__(BLOCK)
 #endif
+// ENV: the scene has an environment emitter (the variant without it keeps
+// the environment code, and its registers, out of the common case)
+template <bool ENV>
 __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int bounce, int qin,
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
@@ -1489,10 +1523,29 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
             if (bounce == 0) {
                 // RadianceQueryRecord::rayIntersect (records.inl:117-143)
                 if (hasAlpha) L4.w = valid ? 1.0f : 0.0f;
-                if (!valid) done = true;   // no environment emitter (path.cpp:136-143)
+                if (!valid) {
+                    // Scene::evalEnvironment of the differential camera ray (path.cpp:136-143)
+                    if (ENV && !I.hide_emitters) {
+                        const float3 rxd = xyz(ldS(&P.sh_o[slot])), ryd = xyz(ldS(&P.sh_d[slot]));
+                        L += T * env_eval(S.env, rd, true, rxd, ryd);
+                    }
+                    done = true;
+                }
             } else {
                 // tail of the previous iteration after scene->rayIntersect (path.cpp:226-286)
                 if (!valid) {
+                    // environment hit by the BSDF sample (path.cpp:236-246, 257-265)
+                    if (ENV && !(I.hide_emitters && !(flags & F_SCATTERED))) {
+                        const float3 value = env_eval(S.env, rd, false, rd, rd);
+                        float nearT, farT;
+                        if (env_sphere(S.env, ro, rd, nearT, farT) && !(nearT > 0) && !(farT < 0)) {
+                            float lumPdf = 0.0f;
+                            if (!(flags & F_DELTA))   // Scene::pdfEmitterDirect -> EnvironmentMap::pdfDirect
+                                lumPdf = env_internal_pdf(S.env, env_rot(S.env.E->to_local, rd)) *
+                                         S.emitters[S.env.E->emitter].pdf_discrete;
+                            L += T * value * mis(ldS(&P.aux[slot]).w, lumPdf);
+                        }
+                    }
                     done = true;
                 } else {
                     const int em = its.emitter;
@@ -1535,16 +1588,24 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
                         float emPdf;
                         const uint32_t ei = pmf_sample_reuse(S.emitter_cdf, S.n_emitters, sx, emPdf);
                         const mtsg_emitter &E = S.emitters[ei];
-                        float3 ep, en;
-                        emitter_sample_position(S, E, sx, sy, ep, en);
-                        float3 dd = ep - its.p;
-                        const float distSquared = dot(dd, dd);
-                        const float dist = sqrtf(distSquared);
-                        dd = dd / dist;
-                        const float dp = fabsf(dot(dd, en));
-                        float pdf = E.inv_area * (dp != 0 ? (distSquared / dp) : 0.0f);
-                        if (dot(dd, refN) >= 0 && dot(dd, en) < 0 && pdf != 0) {
-                            float3 value = ld3(E.radiance) / pdf;
+                        float3 dd, value;
+                        float dist, pdf;
+                        bool accepted;
+                        if (ENV && E.type == MTSG_EMITTER_ENVMAP) {
+                            accepted = env_sample_direct(S.env, its.p, sx, sy, dd, dist, value, pdf);
+                        } else {
+                            float3 ep, en;
+                            emitter_sample_position(S, E, sx, sy, ep, en);
+                            dd = ep - its.p;
+                            const float distSquared = dot(dd, dd);
+                            dist = sqrtf(distSquared);
+                            dd = dd / dist;
+                            const float dp = fabsf(dot(dd, en));
+                            pdf = E.inv_area * (dp != 0 ? (distSquared / dp) : 0.0f);
+                            accepted = dot(dd, refN) >= 0 && dot(dd, en) < 0 && pdf != 0;
+                            if (accepted) value = ld3(E.radiance) / pdf;
+                        }
+                        if (accepted) {
                             pdf *= emPdf;
                             value = value / emPdf;
                             const float3 wo = its.sh.toLocal(dd);
@@ -1941,7 +2002,10 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, qout);
                 timed_launch(s, K_CLOSEST, [&]() { launch_trace<false>(s, count, P, qin, B.nslots); });
                 timed_launch(s, K_SHADE, [&]() {
-                    hipLaunchKernelGGL(k_shade, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, P, b, qin, B.nslots, s->cam.has_alpha);
+                    if (s->ds.has_env)
+                        hipLaunchKernelGGL(k_shade<true>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, P, b, qin, B.nslots, s->cam.has_alpha);
+                    else
+                        hipLaunchKernelGGL(k_shade<false>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, P, b, qin, B.nslots, s->cam.has_alpha);
                 });
                 timed_launch(s, K_SHADOW, [&]() { launch_trace<true>(s, count, P, 0, 0u); });
                 HIP_TRY(hipMemcpyAsync(s->hostCnt + HOSTCNT_STRIDE * (b & 1), P.cnt, (CNT_S + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
@@ -2199,6 +2263,28 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     ds.pairs = dpairs; ds.triL = dtriL; ds.root = root; ds.pairsIdx = dpairsIdx; ds.lidx = dlidx; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
     ds.tidx = dtidx; ds.tdpdu = dtdpdu; ds.shrec = dshrec; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
+    // environment emitter tables (envmap.h)
+    ds.has_env = d->has_envmap ? 1 : 0;
+    ds.env = DevEnv{nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (d->has_envmap) {
+        const mtsg_envmap &E = d->envmap;
+        if (E.levels <= 0 || E.levels > MTSG_ENVMAP_MAX_LEVELS || !d->env_texels || !d->env_cdf_rows || !d->env_cdf_cols ||
+            !d->env_row_weights || E.emitter < 0 || (uint32_t)E.emitter >= d->n_emitters) {
+            g_err = "inconsistent environment map description";
+            return fail(MTSG_ERR_INVALID);
+        }
+        size_t need = 0;
+        for (int l = 0; l < E.levels; ++l)
+            need = std::max(need, (size_t)E.level_offset[l] + 3 * (size_t)E.level_w[l] * E.level_h[l]);
+        if (need > d->n_env_texels) { g_err = "environment map texel array too small"; return fail(MTSG_ERR_INVALID); }
+        mtsg_envmap *dE; float *dt, *dr, *dc, *dw;
+        const int W = E.level_w[0], H = E.level_h[0];
+        if ((rc = up(&E, 1, &dE)) || (rc = up(d->env_texels, d->n_env_texels, &dt)) ||
+            (rc = up(d->env_cdf_rows, (size_t)H + 1, &dr)) || (rc = up(d->env_cdf_cols, (size_t)(W + 1) * H, &dc)) ||
+            (rc = up(d->env_row_weights, (size_t)H, &dw)))
+            return fail(rc);
+        ds.env = DevEnv{dE, dt, dr, dc, dw};
+    }
     ds.n_emitters = d->n_emitters;
     ds.n_tri = d->n_triangles;
     for (int k = 0; k < 3; ++k) { ds.bmin[k] = d->aabb_min[k]; ds.bmax[k] = d->aabb_max[k]; }
@@ -2211,6 +2297,9 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     c.filter_radius = hc.filter_radius; c.filter_scale = hc.filter_scale; c.border = hc.border;
     c.has_alpha = hc.has_alpha;
     memcpy(c.filter_values, hc.filter_values, sizeof(c.filter_values));
+    memcpy(c.dx, hc.dx, sizeof(c.dx));
+    memcpy(c.dy, hc.dy, sizeof(c.dy));
+    c.has_env = d->has_envmap ? 1 : 0;
     // persistent grids from the occupancy query
     if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     int perCU = 0;
@@ -2341,6 +2430,32 @@ static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, fl
             if (e == hipSuccess) e = hipMemcpy(prim, dp, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
         }
     }
+    cleanup();
+    if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    return MTSG_OK;
+}
+
+int mtsg_env_eval(mtsg_scene *s, uint32_t n, const float *dirs, const float *rx, const float *ry, float *out) {
+    if (!s || (!dirs && n) || (!out && n) || ((rx == nullptr) != (ry == nullptr))) { g_err = "invalid arguments"; return MTSG_ERR_INVALID; }
+    if (!s->ds.has_env) { g_err = "scene has no environment emitter"; return MTSG_ERR_INVALID; }
+    if (n == 0) return MTSG_OK;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    const size_t bytes = (size_t)n * 3 * sizeof(float);
+    float *dd = nullptr, *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    auto cleanup = [&]() { hipFree(dd); hipFree(dx); hipFree(dy); hipFree(dout); };
+    hipError_t e = hipMalloc((void **)&dd, bytes);
+    if (e == hipSuccess) e = hipMalloc((void **)&dout, bytes);
+    if (e == hipSuccess && rx) e = hipMalloc((void **)&dx, bytes);
+    if (e == hipSuccess && ry) e = hipMalloc((void **)&dy, bytes);
+    if (e == hipSuccess) e = hipMemcpy(dd, dirs, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && rx) e = hipMemcpy(dx, rx, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess && ry) e = hipMemcpy(dy, ry, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_env_eval, dim3((n + 255) / 256), dim3(256), 0, s->stream, s->ds, dd, dx, dy, n, dout);
+        e = hipStreamSynchronize(s->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
     cleanup();
     if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
     return MTSG_OK;

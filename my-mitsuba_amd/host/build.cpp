@@ -207,6 +207,12 @@ void Scene::finalize() {
         ed.type = e.type;
         ed.shape = e.shape;
         for (int k = 0; k < 3; ++k) ed.radiance[k] = e.radiance[k];
+        if (e.type == MTSG_EMITTER_ENVMAP) {   // tables are built after the kd-tree (needs its AABB)
+            emitterDesc.push_back(ed);
+            wsum += e.samplingWeight;
+            emitterCdf.push_back(wsum);
+            continue;
+        }
         const mtsg_shape &sd = shapeDesc[e.shape];
         if (sd.type == MTSG_SHAPE_MESH) {
             ed.cdf_offset = (uint32_t)emitterTriCdf.size();
@@ -378,6 +384,22 @@ void Scene::finalize() {
     for (int k = 0; k < 3; ++k) { d.aabb_min[k] = tree.aabb.mn[k]; d.aabb_max[k] = tree.aabb.mx[k]; }
     d.max_depth = tree.maxDepth;
     d.camera = cam;
+    // ---------------- environment emitter ----------------
+    d.has_envmap = 0;
+    for (size_t i = 0; i < emitters.size(); ++i) {
+        if (emitters[i].type != MTSG_EMITTER_ENVMAP) continue;
+        float aabbMin[3], aabbMax[3], camPos[3];
+        for (int k = 0; k < 3; ++k) { aabbMin[k] = d.aabb_min[k]; aabbMax[k] = d.aabb_max[k]; }
+        camPos[0] = cam.camera_to_world[3]; camPos[1] = cam.camera_to_world[7]; camPos[2] = cam.camera_to_world[11];
+        buildEnvmap(emitters[i], aabbMin, aabbMax, camPos, envTexels, envCdfRows, envCdfCols, envRowWeights, d.envmap);
+        d.envmap.emitter = (int)i;
+        d.has_envmap = 1;
+        d.n_env_texels = (uint32_t)envTexels.size();
+        d.env_texels = envTexels.data();
+        d.env_cdf_rows = envCdfRows.data();
+        d.env_cdf_cols = envCdfCols.data();
+        d.env_row_weights = envRowWeights.data();
+    }
 }
 
 }  // namespace mtsh

@@ -779,6 +779,36 @@ struct Loader {
         return (int)scene.emitters.size() - 1;
     }
 
+    // Scene-level emitter: only `envmap` (envmap.cpp:105-185); area lights
+    // must be nested in a shape
+    void parseSceneEmitter(XNode &n) {
+        substAll(n);
+        Properties props;
+        std::vector<XNode *> nested;
+        parseProps(n, props, nested);
+        std::string type = lower(n.attr("type"));
+        if (type != "envmap")
+            throw err("line " + std::to_string(n.line) + ": emitter \"" + type + "\" outside a shape is outside this build's scope");
+        for (auto &e : scene.emitters)
+            if (e.type == MTSG_EMITTER_ENVMAP) throw err("only one environment emitter is supported (Scene::m_environmentEmitter)");
+        Emitter e;
+        e.type = MTSG_EMITTER_ENVMAP;
+        e.samplingWeight = props.getFloat("samplingWeight", 1.0f);
+        e.scale = props.getFloat("scale", 1.0f);
+        if (props.has("intensityScale")) throw err("The 'intensityScale' parameter has been deprecated and is now called scale.");
+        e.toWorld = props.getTransform("toWorld", Transform());
+        std::string file = props.getString("filename", "");
+        if (file.empty()) throw err("envmap: missing 'filename'");
+        std::string path = resolve(file);
+        std::string ext = lower(path.size() > 4 ? path.substr(path.size() - 4) : path);
+        if (ext != ".pfm")
+            throw err("envmap \"" + file + "\": only PFM images are supported (no OpenEXR decoder in this build; re-encode as PFM)");
+        std::string e2;
+        if (!readPFM(path, e.width, e.height, e.rgb, e2)) throw err("envmap \"" + file + "\": " + e2);
+        if (std::max(e.width, e.height) > 0xFFFF) throw err("Environment maps images must be smaller than 65536 pixels in width and height");
+        scene.emitters.push_back(std::move(e));
+    }
+
     // Returns meshes/rects in object->world space given the toWorld transform
     void parseShape(XNode &n, std::vector<Mesh> &meshes, std::vector<Rect> &rects, bool inGroup) {
         substAll(n);
@@ -929,7 +959,7 @@ struct Loader {
                 parseShape(c, meshes, rects, false);
                 addShapes(meshes, rects);
             } else if (tag == "emitter") {
-                throw err("line " + std::to_string(c.line) + ": emitter \"" + c.attr("type") + "\" outside a shape is outside this build's scope");
+                parseSceneEmitter(c);
             } else if (tag == "ref") {
                 // scene-level refs are ignored
             } else {
@@ -1017,6 +1047,45 @@ struct Loader {
 };
 }  // namespace
 
+bool readPFM(const std::string &path, int &w, int &h, std::vector<float> &rgb, std::string &err) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot open " + path; return false; }
+    auto token = [&](std::string &out) {
+        out.clear();
+        int c;
+        while ((c = fgetc(f)) != EOF && isspace(c)) {}
+        while (c != EOF && !isspace(c)) { out.push_back((char)c); c = fgetc(f); }
+        return !out.empty();
+    };
+    std::string magic, ws, hs, ss;
+    bool ok = token(magic) && token(ws) && token(hs) && token(ss);
+    if (!ok || (magic != "PF" && magic != "Pf")) { fclose(f); err = "invalid PFM header"; return false; }
+    const bool color = magic == "PF";
+    w = atoi(ws.c_str()); h = atoi(hs.c_str());
+    const float scaleAndOrder = (float)strtod(ss.c_str(), nullptr);
+    if (w <= 0 || h <= 0) { fclose(f); err = "invalid PFM size"; return false; }
+    const size_t ch = color ? 3 : 1, n = (size_t)w * h * ch;
+    std::vector<float> data(n);
+    if (fread(data.data(), sizeof(float), n, f) != n) { fclose(f); err = "truncated PFM"; return false; }
+    fclose(f);
+    if (scaleAndOrder > 0) {   // big endian
+        for (auto &v : data) {
+            uint32_t u;
+            memcpy(&u, &v, 4);
+            u = __builtin_bswap32(u);
+            memcpy(&v, &u, 4);
+        }
+    }
+    const float scale = std::fabs(scaleAndOrder);
+    if (scale != 1) for (auto &v : data) v *= scale;
+    rgb.assign((size_t)w * h * 3, 0.0f);
+    for (int y = 0; y < h; ++y)   // flipVertically(): PFM rows are bottom-up
+        for (int x = 0; x < w; ++x)
+            for (int k = 0; k < 3; ++k)
+                rgb[((size_t)y * w + x) * 3 + k] = data[((size_t)(h - 1 - y) * w + x) * ch + (color ? k : 0)];
+    return true;
+}
+
 int g_defaultKDThreads = 0;
 
 std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::string, std::string> &defines) {
@@ -1040,7 +1109,7 @@ std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::st
     L.parseScene(*root);
     if (!scene->sensor.present) throw err("scene has no <sensor>");
     for (auto &e : scene->emitters)
-        if (e.shape < 0) throw err("area emitter without a parent shape");
+        if (e.type == MTSG_EMITTER_AREA && e.shape < 0) throw err("area emitter without a parent shape");
     scene->finalize();
     return scene;
 }

@@ -60,7 +60,12 @@ struct Emitter {
     int type = MTSG_EMITTER_AREA;
     V3 radiance{1, 1, 1};
     float samplingWeight = 1.0f;
-    int shape = -1;                  // index into Scene::shapes
+    int shape = -1;                  // index into Scene::shapes (area lights)
+    // envmap (src/emitters/envmap.cpp)
+    int width = 0, height = 0;       // level-0 size
+    std::vector<float> rgb;          // level 0, RGB float, top row first (after the PFM flip)
+    float scale = 1.0f;
+    Transform toWorld;
 };
 
 struct ShapeRef {                    // m_shapes order in the kd-tree
@@ -133,6 +138,7 @@ struct Scene {
     std::vector<mtsg_bsdf> bsdfDesc;
     std::vector<mtsg_emitter> emitterDesc;
     std::vector<mtsg_triaccel> triaccel;
+    std::vector<float> envTexels, envCdfRows, envCdfCols, envRowWeights;
     KDTree tree;
     mtsg_camera camera{};
     mtsg_scene_desc desc{};
@@ -141,6 +147,14 @@ struct Scene {
 };
 
 extern int g_defaultKDThreads;   // 0 = hardware concurrency
+
+// Environment emitter tables (envmap.cpp in this directory)
+void buildEnvmap(const Emitter &e, const float aabbMin[3], const float aabbMax[3], const float camPos[3],
+                 std::vector<float> &texels, std::vector<float> &cdfRows, std::vector<float> &cdfCols,
+                 std::vector<float> &rowWeights, mtsg_envmap &env);
+
+// PFM image (src/libcore/bitmap.cpp:3764-3814): RGB float, rows top-down
+bool readPFM(const std::string &path, int &w, int &h, std::vector<float> &rgb, std::string &err);
 
 // XML loading (src/librender/scenehandler.cpp), `-D name=value` defines
 std::unique_ptr<Scene> loadScene(const std::string &path,

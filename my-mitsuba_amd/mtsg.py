@@ -84,7 +84,7 @@ DEVICE_SYMBOLS = [
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
-    "mtsg_last_error",
+    "mtsg_last_error", "mtsg_env_eval",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_scene_desc", "mtsh_scene_render_params",
@@ -142,6 +142,7 @@ def device_lib() -> C.CDLL:
                                            C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_trace_shadow.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
         lib.mtsg_render_samples.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
+        lib.mtsg_env_eval.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_scene_destroy.argtypes = [C.c_void_p]
         lib.mtsg_last_error.argtypes = [C.c_char_p, C.c_size_t]
         _dev = lib
@@ -256,6 +257,18 @@ class GPUScene:
         self._check(device_lib().mtsg_trace_closest(self._h, n, _ptr(rays), _ptr(t), _ptr(u), _ptr(v), _ptr(prim)),
                     "mtsg_trace_closest")
         return t, u, v, prim
+
+    def env_eval(self, dirs: np.ndarray, rx: np.ndarray | None = None, ry: np.ndarray | None = None) -> np.ndarray:
+        """Environment radiance along world directions (debug entry point)."""
+        dirs = np.ascontiguousarray(dirs, dtype=np.float32)
+        out = np.empty((dirs.shape[0], 3), np.float32)
+        px = py = None
+        if rx is not None:
+            rx = np.ascontiguousarray(rx, dtype=np.float32)
+            ry = np.ascontiguousarray(ry, dtype=np.float32)
+            px, py = _ptr(rx), _ptr(ry)
+        self._check(device_lib().mtsg_env_eval(self._h, dirs.shape[0], _ptr(dirs), px, py, _ptr(out)), "mtsg_env_eval")
+        return out
 
     def trace_shadow(self, rays: np.ndarray) -> np.ndarray:
         rays = np.ascontiguousarray(rays, dtype=np.float32)

@@ -58,6 +58,7 @@ struct Spec {
     static Spec of(const float *p) { return Spec(p[0], p[1], p[2]); }
     bool isZero() const { return s[0] == 0 && s[1] == 0 && s[2] == 0; }
     float max() const { return std::max(s[0], std::max(s[1], s[2])); }
+    float luminance() const { return s[0] * 0.212671f + s[1] * 0.715160f + s[2] * 0.072169f; }   // spectrum.h (RGB)
 };
 inline Spec operator*(Spec a, Spec b) { return {a.s[0] * b.s[0], a.s[1] * b.s[1], a.s[2] * b.s[2]}; }
 inline Spec operator*(Spec a, float f) { return {a.s[0] * f, a.s[1] * f, a.s[2] * f}; }
@@ -161,6 +162,7 @@ const float kEpsilon = 1e-4f;        // constants.h:28
 const float kShadowEpsilon = 1e-3f;  // constants.h:29
 const float kDeltaEpsilon = 1e-3f;   // constants.h:31
 const float kInvPi = 0.31830988618379067154f;
+const float kInvTwoPi = 0.15915494309189533577f;   // constants.h:65
 
 // ---------------------------------------------------------------------------
 // SFMT-19937 (src/libcore/random.cpp:66-81 parameters, :130-640)
@@ -650,19 +652,237 @@ struct SceneView {
         dRec.measureSolidAngle = 1;
     }
 
+    // ------------------------------------------------------------------
+    // EnvironmentMap (src/emitters/envmap.cpp) over TMIPMap (mipmap.h)
+    // ------------------------------------------------------------------
+    static int modulo(int a, int b) { int r = a % b; return r < 0 ? r + b : r; }
+    static float log2f_m(float v) {   // math.cpp:103-106
+        const float invLn2 = 1.0f / std::log(2.0f);
+        return (float)std::log((double)v) * invLn2;
+    }
+    // TMIPMap::evalTexel (mipmap.h:503-562): u repeats, v clamps
+    Spec envTexel(int level, int x, int y) const {
+        const mtsg_envmap &E = d.envmap;
+        const int w = E.level_w[level], h = E.level_h[level];
+        if (x < 0 || x >= w) x = modulo(x, w);
+        if (y < 0 || y >= h) y = std::min(std::max(y, 0), h - 1);
+        const float *t = d.env_texels + E.level_offset[level] + 3 * ((size_t)y * w + x);
+        return Spec::of(t);
+    }
+    Spec envBox(int level, float u, float v) const {   // mipmap.h:566-569
+        const mtsg_envmap &E = d.envmap;
+        return envTexel(level, (int)std::floor(u * E.level_w[level]), (int)std::floor(v * E.level_h[level]));
+    }
+    Spec envBilinear(int level, float ux, float uy) const {   // mipmap.h:575-596
+        const mtsg_envmap &E = d.envmap;
+        if (!std::isfinite(ux) || !std::isfinite(uy)) return Spec(0.0f);
+        if (level >= E.levels) return envBox(E.levels - 1, ux, uy);
+        const float u = ux * E.level_w[level] - 0.5f, v = uy * E.level_h[level] - 0.5f;
+        const int xPos = (int)std::floor(u), yPos = (int)std::floor(v);
+        const float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
+        return envTexel(level, xPos, yPos) * dx2 * dy2 + envTexel(level, xPos, yPos + 1) * dx2 * dy1 +
+               envTexel(level, xPos + 1, yPos) * dx1 * dy2 + envTexel(level, xPos + 1, yPos + 1) * dx1 * dy1;
+    }
+    Spec envEWA(int level, float ux, float uy, float A, float B, float C) const {   // mipmap.h:775-840
+        const mtsg_envmap &E = d.envmap;
+        if (!std::isfinite(A + B + C + ux + uy)) return Spec(0.0f);
+        if (level >= E.levels) return envBox(E.levels - 1, ux, uy);
+        const float u = ux * E.level_w[level] - 0.5f, v = uy * E.level_h[level] - 0.5f;
+        const float rx = E.size_ratio_x[level], ry = E.size_ratio_y[level];
+        A /= rx * rx;
+        B /= rx * ry;
+        C /= ry * ry;
+        const float invDet = 1.0f / (-B * B + 4.0f * A * C), deltaU = 2.0f * std::sqrt(C * invDet),
+                    deltaV = 2.0f * std::sqrt(A * invDet);
+        const int u0 = (int)std::ceil(u - deltaU), u1 = (int)std::floor(u + deltaU);
+        const int v0 = (int)std::ceil(v - deltaV), v1 = (int)std::floor(v + deltaV);
+        const float As = A * MTSG_MIPMAP_LUT_SIZE, Bs = B * MTSG_MIPMAP_LUT_SIZE, Cs = C * MTSG_MIPMAP_LUT_SIZE;
+        Spec result(0.0f);
+        float denominator = 0.0f;
+        const float ddq = 2 * As, uu0 = (float)u0 - u;
+        for (int vt = v0; vt <= v1; ++vt) {
+            const float vv = (float)vt - v;
+            float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
+            float dq = As * (2 * uu0 + 1) + Bs * vv;
+            for (int ut = u0; ut <= u1; ++ut) {
+                if (q < (float)MTSG_MIPMAP_LUT_SIZE) {
+                    const uint32_t qi = (uint32_t)q;
+                    if (qi < MTSG_MIPMAP_LUT_SIZE) {
+                        const float weight = E.weight_lut[(int)q];
+                        result += envTexel(level, ut, vt) * weight;
+                        denominator += weight;
+                    }
+                }
+                q += dq;
+                dq += ddq;
+            }
+        }
+        if (denominator == 0) return envBilinear(level, ux, uy);
+        return result / denominator;
+    }
+    // TMIPMap::eval (mipmap.h:633-722), filter type EWA
+    Spec envFiltered(float ux, float uy, float d0x, float d0y, float d1x, float d1y) const {
+        const mtsg_envmap &E = d.envmap;
+        const float du0 = d0x * E.level_w[0], dv0 = d0y * E.level_h[0], du1 = d1x * E.level_w[0], dv1 = d1y * E.level_h[0];
+        float A = dv0 * dv0 + dv1 * dv1, B = -2.0f * (du0 * dv0 + du1 * dv1), C = du0 * du0 + du1 * du1,
+              F = A * C - B * B * 0.25f;
+        const float root = hypot2(A - C, B), Aprime = 0.5f * (A + C - root), Cprime = 0.5f * (A + C + root);
+        float majorRadius = Aprime != 0 ? std::sqrt(F / Aprime) : 0, minorRadius = Cprime != 0 ? std::sqrt(F / Cprime) : 0;
+        if (!(minorRadius > 0) || !(majorRadius > 0) || F < 0) {
+            const float level = log2f_m(std::max(majorRadius, kEpsilon));
+            const int ilevel = (int)std::floor(level);
+            if (ilevel < 0) return envBilinear(0, ux, uy);
+            const float a = level - ilevel;
+            return envBilinear(ilevel, ux, uy) * (1.0f - a) + envBilinear(ilevel + 1, ux, uy) * a;
+        }
+        if (minorRadius * E.max_anisotropy < majorRadius) {
+            minorRadius = majorRadius / E.max_anisotropy;
+            const float theta = 0.5f * std::atan(B / (A - C));
+            const float sinTheta = std::sin(theta), cosTheta = std::cos(theta);
+            const float a2 = majorRadius * majorRadius, b2 = minorRadius * minorRadius, sinTheta2 = sinTheta * sinTheta,
+                        cosTheta2 = cosTheta * cosTheta, sin2Theta = 2 * sinTheta * cosTheta;
+            A = a2 * cosTheta2 + b2 * sinTheta2;
+            B = (a2 - b2) * sin2Theta;
+            C = a2 * sinTheta2 + b2 * cosTheta2;
+            F = a2 * b2;
+        }
+        const float scale = 1.0f / F;
+        A *= scale; B *= scale; C *= scale;
+        const float level = std::max(0.0f, log2f_m(minorRadius));
+        const int ilevel = (int)level;
+        const float a = level - ilevel;
+        if (majorRadius < 1 || !(A > 0 && C > 0)) return envBilinear(ilevel, ux, uy);
+        return envEWA(ilevel, ux, uy, A, B, C) * (1.0f - a) + envEWA(ilevel + 1, ux, uy, A, B, C) * a;
+    }
+    Vec envToLocal(const Vec &v) const {
+        const float *m = d.envmap.to_local;
+        return Vec(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z, m[6] * v.x + m[7] * v.y + m[8] * v.z);
+    }
+    Vec envToWorld(const Vec &v) const {
+        const float *m = d.envmap.to_world;
+        return Vec(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z, m[6] * v.x + m[7] * v.y + m[8] * v.z);
+    }
+    // EnvironmentMap::evalEnvironment (envmap.cpp:380-410)
+    Spec envEvalEnvironment(const Ray &ray, bool hasDiff, const Vec &rxD, const Vec &ryD) const {
+        const Vec v = envToLocal(ray.d);
+        const float ux = std::atan2(v.x, -v.z) * kInvTwoPi, uy = std::acos(std::min(1.0f, std::max(-1.0f, v.y))) * kInvPi;
+        Spec value;
+        if (!hasDiff) {
+            value = envBilinear(0, ux, uy);
+        } else {
+            const Vec dvdx = envToLocal(rxD) - v, dvdy = envToLocal(ryD) - v;
+            const float t1 = kInvTwoPi / (v.x * v.x + v.z * v.z),
+                        t2 = -kInvPi / std::max(safe_sqrt(1.0f - v.y * v.y), kEpsilon);
+            value = envFiltered(ux, uy, t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y, t1 * (dvdy.z * v.x - dvdy.x * v.z),
+                                t2 * dvdy.y);
+        }
+        return value * d.envmap.scale;
+    }
+    // sampleReuse (envmap.cpp:628-633)
+    static uint32_t envSampleReuse(const float *cdf, uint32_t size, float &sample) {
+        const float *entry = std::lower_bound(cdf, cdf + size + 1, sample);
+        const uint32_t index = std::min((uint32_t)std::max((ptrdiff_t)0, entry - cdf - 1), size - 1);
+        sample = (sample - cdf[index]) / (cdf[index + 1] - cdf[index]);
+        return index;
+    }
+    static float intervalToTent(float sample) {   // warp.cpp:143-155
+        float sign;
+        if (sample < 0.5f) { sign = 1; sample *= 2; }
+        else { sign = -1; sample = 2 * (sample - 0.5f); }
+        return sign * (1 - std::sqrt(sample));
+    }
+    // envmap.cpp:574-600
+    void envInternalSample(float sx, float sy, Vec &dOut, Spec &value, float &pdf) const {
+        const mtsg_envmap &E = d.envmap;
+        const int W = E.level_w[0], H = E.level_h[0];
+        const uint32_t row = envSampleReuse(d.env_cdf_rows, H, sy);
+        const uint32_t col = envSampleReuse(d.env_cdf_cols + row * (W + 1), W, sx);
+        const float px = (float)col + intervalToTent(sx), py = (float)row + intervalToTent(sy);
+        const int xPos = (int)std::floor(px), yPos = (int)std::floor(py);
+        const float dx1 = px - xPos, dx2 = 1.0f - dx1, dy1 = py - yPos, dy2 = 1.0f - dy1;
+        const Spec value1 = envTexel(0, xPos, yPos) * dx2 * dy2 + envTexel(0, xPos + 1, yPos) * dx1 * dy2;
+        const Spec value2 = envTexel(0, xPos, yPos + 1) * dx2 * dy1 + envTexel(0, xPos + 1, yPos + 1) * dx1 * dy1;
+        value = (value1 + value2) * E.scale;
+        pdf = (value1.luminance() * d.env_row_weights[std::min(std::max(yPos, 0), H - 1)] +
+               value2.luminance() * d.env_row_weights[std::min(std::max(yPos + 1, 0), H - 1)]) * E.normalization;
+        const float sinPhi = std::sin(E.pixel_size[0] * (px + 0.5f)), cosPhi = std::cos(E.pixel_size[0] * (px + 0.5f));
+        const float sinTheta = std::sin(E.pixel_size[1] * (py + 0.5f)), cosTheta = std::cos(E.pixel_size[1] * (py + 0.5f));
+        dOut = Vec(sinPhi * sinTheta, cosTheta, -cosPhi * sinTheta);
+        pdf /= std::max(std::fabs(sinTheta), kEpsilon);
+    }
+    // envmap.cpp:603-633
+    float envInternalPdf(const Vec &dl) const {
+        const mtsg_envmap &E = d.envmap;
+        const int W = E.level_w[0], H = E.level_h[0];
+        const float ux = std::atan2(dl.x, -dl.z) * kInvTwoPi, uy = std::acos(std::min(1.0f, std::max(-1.0f, dl.y))) * kInvPi;
+        if (!std::isfinite(ux) || !std::isfinite(uy)) return 0.0f;
+        const float u = ux * W - 0.5f, v = uy * H - 0.5f;
+        const int xPos = (int)std::floor(u), yPos = (int)std::floor(v);
+        const float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
+        const Spec value1 = envTexel(0, xPos, yPos) * dx2 * dy2 + envTexel(0, xPos + 1, yPos) * dx1 * dy2;
+        const Spec value2 = envTexel(0, xPos, yPos + 1) * dx2 * dy1 + envTexel(0, xPos + 1, yPos + 1) * dx1 * dy1;
+        const float sinTheta = safe_sqrt(1 - dl.y * dl.y);
+        return (value1.luminance() * d.env_row_weights[std::min(std::max(yPos, 0), H - 1)] +
+                value2.luminance() * d.env_row_weights[std::min(std::max(yPos + 1, 0), H - 1)]) *
+               E.normalization / std::max(std::fabs(sinTheta), kEpsilon);
+    }
+    // BSphere::rayIntersect (bsphere.h:88-95) + solveQuadratic (util.cpp:447-485)
+    bool envSphere(const Vec &o, const Vec &dir, float &nearT, float &farT) const {
+        const mtsg_envmap &E = d.envmap;
+        const Vec oc = o - Vec(E.bsphere_center[0], E.bsphere_center[1], E.bsphere_center[2]);
+        const float A = dot(dir, dir), B = 2 * dot(oc, dir), C = dot(oc, oc) - E.bsphere_radius * E.bsphere_radius;
+        if (A == 0) {
+            if (B != 0) { nearT = farT = -C / B; return true; }
+            return false;
+        }
+        const float discrim = B * B - 4.0f * A * C;
+        if (discrim < 0) return false;
+        const float sq = std::sqrt(discrim), temp = B < 0 ? -0.5f * (B - sq) : -0.5f * (B + sq);
+        nearT = temp / A;
+        farT = C / temp;
+        if (nearT > farT) std::swap(nearT, farT);
+        return true;
+    }
+    // EnvironmentMap::sampleDirect (envmap.cpp:516-543)
+    Spec envSampleDirect(DRec &dRec, float sx, float sy) const {
+        Vec dl;
+        Spec value;
+        float pdf;
+        envInternalSample(sx, sy, dl, value, pdf);
+        const Vec dw = envToWorld(dl);
+        Ray r;
+        r.o = dRec.ref;
+        r.setDirection(dw);
+        float nearT, farT;
+        if (value.isZero() || pdf == 0 || !envSphere(r.o, r.d, nearT, farT) || nearT >= 0 || farT <= 0) {
+            dRec.pdf = 0.0f;
+            return Spec(0.0f);
+        }
+        dRec.pdf = pdf;
+        dRec.p = r.o + r.d * farT;
+        dRec.d = r.d;
+        dRec.dist = farT;
+        dRec.measureSolidAngle = 1;
+        return value / pdf;
+    }
+
     // Scene::sampleEmitterDirect (scene.cpp:910-947) + AreaLight::sampleDirect (area.cpp:150-165)
     template <bool count>
     Spec sampleEmitterDirect(DRec &dRec, float sx, float sy, Counters *ctr) const {
         float emPdf;
         size_t index = pmfSampleReuse(d.emitter_cdf, d.n_emitters, sx, emPdf);
         const mtsg_emitter &em = d.emitters[index];
-        shapeSampleDirect(em, dRec, sx, sy);
         Spec value;
-        if (dot(dRec.d, dRec.refN) >= 0 && dot(dRec.d, dRec.n) < 0 && dRec.pdf != 0) {
-            value = Spec::of(em.radiance) / dRec.pdf;
+        if (em.type == MTSG_EMITTER_ENVMAP) {
+            value = envSampleDirect(dRec, sx, sy);
         } else {
-            dRec.pdf = 0.0f;
-            value = Spec(0.0f);
+            shapeSampleDirect(em, dRec, sx, sy);
+            if (dot(dRec.d, dRec.refN) >= 0 && dot(dRec.d, dRec.n) < 0 && dRec.pdf != 0) {
+                value = Spec::of(em.radiance) / dRec.pdf;
+            } else {
+                dRec.pdf = 0.0f;
+                value = Spec(0.0f);
+            }
         }
         if (dRec.pdf != 0) {
             Ray ray;
@@ -683,6 +903,8 @@ struct SceneView {
     // Shape::pdfDirect (shape.cpp:117-126)
     float pdfEmitterDirect(const DRec &dRec) const {
         const mtsg_emitter &em = d.emitters[dRec.emitter];
+        if (em.type == MTSG_EMITTER_ENVMAP)   // EnvironmentMap::pdfDirect, solid angle (envmap.cpp:545-556)
+            return envInternalPdf(envToLocal(dRec.d)) * em.pdf_discrete;
         float pdf = 0.0f;
         if (dot(dRec.d, dRec.refN) >= 0 && dot(dRec.d, dRec.n) < 0) {
             float pdfPos = em.inv_area;
@@ -990,8 +1212,17 @@ enum {
     EIntersection = 0x0200, EOpacity = 0x0400
 };
 
+// Camera-ray differentials (PerspectiveCamera::sampleRayDifferential scaled
+// by 1/sqrt(spp), integrator.cpp:148-149,188); used only by the environment
+// lookup of primary rays that leave the scene.
+struct RayDiff {
+    bool has = false;
+    Vec rx, ry;
+};
+
 template <bool count>
-Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, float &alpha, int &depthOut, Counters *ctr, bool hasAlpha) {
+Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, float &alpha, int &depthOut, Counters *ctr,
+        bool hasAlpha, const RayDiff &diff = RayDiff()) {
     Its its;
     Spec Li(0.0f);
     bool scattered = false;
@@ -1007,7 +1238,9 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
     float eta = 1.0f;
     while (depth <= I.maxDepth || I.maxDepth < 0) {
         if (!its.valid()) {
-            // no environment emitter in this build's scenes: evalEnvironment = 0
+            // Scene::evalEnvironment of the (differential) camera ray
+            if ((type & EEmittedRadiance) && (!I.hideEmitters || scattered) && scene.d.has_envmap)
+                Li += throughput * scene.envEvalEnvironment(ray, diff.has, diff.rx, diff.ry);
             break;
         }
         const mtsg_shape &sh = scene.d.shapes[its.shape];
@@ -1078,8 +1311,22 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
                 dRec.dist = its.t;
                 hitEmitter = true;
             }
+        } else if (scene.d.has_envmap) {
+            if (I.hideEmitters && !scattered) break;
+            value = scene.envEvalEnvironment(ray, false, Vec(0.0f), Vec(0.0f));
+            // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
+            float nearT, farT;
+            if (!scene.envSphere(ray.o, ray.d, nearT, farT) || nearT > 0 || farT < 0) break;
+            dRec.p = ray.o + ray.d * farT;
+            dRec.n = normalize(Vec(scene.d.envmap.bsphere_center[0], scene.d.envmap.bsphere_center[1],
+                                   scene.d.envmap.bsphere_center[2]) - dRec.p);
+            dRec.measureSolidAngle = 1;
+            dRec.emitter = scene.d.envmap.emitter;
+            dRec.d = ray.d;
+            dRec.dist = farT;
+            hitEmitter = true;
         } else {
-            break;   // no environment emitter
+            break;
         }
         throughput *= bsdfWeight;
         eta *= bRec.eta;
@@ -1100,8 +1347,8 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
     return Li;
 }
 
-// PerspectiveCamera::sampleRayDifferential (perspective.cpp:271-298), without differentials
-Ray cameraRay(const mtsg_camera &c, float px, float py) {
+// PerspectiveCamera::sampleRayDifferential (perspective.cpp:271-298)
+Ray cameraRay(const mtsg_camera &c, float px, float py, RayDiff *diff = nullptr, uint32_t spp = 1) {
     const float *m = c.sample_to_camera;
     float sx = px * c.inv_res_x, sy = py * c.inv_res_y;
     float x = m[0] * sx + m[1] * sy + m[3];
@@ -1117,6 +1364,17 @@ Ray cameraRay(const mtsg_camera &c, float px, float py) {
     const float *t = c.camera_to_world;
     ray.o = Vec(t[3], t[7], t[11]);
     ray.setDirection(Vec(t[0] * d.x + t[1] * d.y + t[2] * d.z, t[4] * d.x + t[5] * d.y + t[6] * d.z, t[8] * d.x + t[9] * d.y + t[10] * d.z));
+    if (diff) {
+        auto toWorld = [&](const Vec &v) {
+            return Vec(t[0] * v.x + t[1] * v.y + t[2] * v.z, t[4] * v.x + t[5] * v.y + t[6] * v.z, t[8] * v.x + t[9] * v.y + t[10] * v.z);
+        };
+        const Vec rx = toWorld(normalize(nearP + Vec(c.dx[0], c.dx[1], c.dx[2])));
+        const Vec ry = toWorld(normalize(nearP + Vec(c.dy[0], c.dy[1], c.dy[2])));
+        const float scale = 1.0f / std::sqrt((float)spp);   // RayDifferential::scaleDifferential
+        diff->has = true;
+        diff->rx = ray.d + (rx - ray.d) * scale;
+        diff->ry = ray.d + (ry - ray.d) * scale;
+    }
     return ray;
 }
 
@@ -1277,11 +1535,12 @@ int oracle_debug_path_rays(const mtsg_scene_desc *d, const mtsg_render_params *p
     smp.key = counterKey(p->seed, ((uint64_t)y * d->camera.film_w + x) * p->spp + s);
     float a, b;
     smp.next2D(a, b);
-    Ray ray = cameraRay(d->camera, x + a, y + b);
+    RayDiff diff;
+    Ray ray = cameraRay(d->camera, x + a, y + b, &diff, p->spp);
     float alpha;
     int depth;
     Counters c;
-    Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0);
+    Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0, diff);
     g_rayLog = nullptr;
     int n = std::min<int>((int)log.size() / 8, max_rays);
     std::copy(log.begin(), log.begin() + 8 * n, rays_out);
@@ -1299,11 +1558,12 @@ int oracle_debug_pixel_sample(const mtsg_scene_desc *d, const mtsg_render_params
     smp.key = counterKey(p->seed, ((uint64_t)y * d->camera.film_w + x) * p->spp + s);
     float a, b;
     smp.next2D(a, b);
-    Ray ray = cameraRay(d->camera, x + a, y + b);
+    RayDiff diff;
+    Ray ray = cameraRay(d->camera, x + a, y + b, &diff, p->spp);
     float alpha;
     int depth;
     Counters c;
-    Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0);
+    Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0, diff);
     g_debug = 0;
     (void)q;
     return 0;
@@ -1319,11 +1579,12 @@ int oracle_pixel_samples(const mtsg_scene_desc *d, const mtsg_render_params *p, 
         smp.key = counterKey(p->seed, sid);
         float a, b;
         smp.next2D(a, b);
-        Ray ray = cameraRay(d->camera, x + a, y + b);
+        RayDiff diff;
+    Ray ray = cameraRay(d->camera, x + a, y + b, &diff, p->spp);
         float alpha;
         int depth;
         Counters c;
-        Spec L = Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0);
+        Spec L = Li<false>(sv, I, ray, smp, alpha, depth, &c, d->camera.has_alpha != 0, diff);
         out[3 * s] = L.s[0]; out[3 * s + 1] = L.s[1]; out[3 * s + 2] = L.s[2];
     }
     return 0;
@@ -1397,12 +1658,13 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
                             float a, b;
                             smp.next2D(a, b);
                             float spx = x + a, spy = y + b;
-                            Ray ray = cameraRay(cam, spx, spy);
+                            RayDiff diff;
+                            Ray ray = cameraRay(cam, spx, spy, &diff, p->spp);
                             float alpha;
                             int depth;
                             Spec L = stats && (stats->threads < 0)
-                                         ? Li<true>(sv, I, ray, smp, alpha, depth, &ctrs[tid], cam.has_alpha != 0)
-                                         : Li<false>(sv, I, ray, smp, alpha, depth, &ctrs[tid], cam.has_alpha != 0);
+                                         ? Li<true>(sv, I, ray, smp, alpha, depth, &ctrs[tid], cam.has_alpha != 0, diff)
+                                         : Li<false>(sv, I, ray, smp, alpha, depth, &ctrs[tid], cam.has_alpha != 0, diff);
                             pathVerts[tid] += depth;
                             samples[tid]++;
                             blk.put(spx, spy, L, alpha);
@@ -1477,6 +1739,47 @@ int oracle_bsdf_sample_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, cons
 
 int oracle_bsdf_eval_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *wo, float *value, float *pdf) {
     for (uint32_t i = 0; i < n; ++i) oracle_bsdf_eval(b, wi, wo + 3 * i, value + 3 * i, pdf + i);
+    return 0;
+}
+
+// EnvironmentMap::sampleDirect / pdfDirect from a reference point (the
+// EmitterAdapter of src/tests/test_chisquare.cpp:342-388)
+int oracle_env_sample_direct_n(const mtsg_scene_desc *d, uint32_t n, const float *u2, const float ref[3], float *dir,
+                               float *pdf, float *value) {
+    if (!d || !d->has_envmap) { g_err = "scene has no environment emitter"; return -1; }
+    SceneView sv(*d);
+    for (uint32_t i = 0; i < n; ++i) {
+        SceneView::DRec dRec;
+        dRec.ref = Vec(ref[0], ref[1], ref[2]);
+        Spec v = sv.envSampleDirect(dRec, u2[2 * i], u2[2 * i + 1]);
+        dir[3 * i] = dRec.d.x; dir[3 * i + 1] = dRec.d.y; dir[3 * i + 2] = dRec.d.z;
+        pdf[i] = dRec.pdf;
+        value[3 * i] = v.s[0]; value[3 * i + 1] = v.s[1]; value[3 * i + 2] = v.s[2];
+    }
+    return 0;
+}
+
+int oracle_env_pdf_direct_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, float *pdf) {
+    if (!d || !d->has_envmap) { g_err = "scene has no environment emitter"; return -1; }
+    SceneView sv(*d);
+    for (uint32_t i = 0; i < n; ++i) pdf[i] = sv.envInternalPdf(sv.envToLocal(Vec(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2])));
+    return 0;
+}
+
+/* Environment radiance along world directions (no differentials: bilinear
+ * level 0) and with camera-style differentials (EWA). */
+int oracle_env_eval_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, const float *rx, const float *ry, float *out) {
+    if (!d || !d->has_envmap) { g_err = "scene has no environment emitter"; return -1; }
+    SceneView sv(*d);
+    for (uint32_t i = 0; i < n; ++i) {
+        Ray r;
+        r.o = Vec(0.0f);
+        r.setDirection(Vec(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]));
+        const bool diff = rx && ry;
+        const Spec v = sv.envEvalEnvironment(r, diff, diff ? Vec(rx[3 * i], rx[3 * i + 1], rx[3 * i + 2]) : Vec(0.0f),
+                                             diff ? Vec(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]) : Vec(0.0f));
+        out[3 * i] = v.s[0]; out[3 * i + 1] = v.s[1]; out[3 * i + 2] = v.s[2];
+    }
     return 0;
 }
 

@@ -86,6 +86,12 @@ int oracle_bsdf_sample_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, cons
                          float *weight, int32_t *type);
 int oracle_bsdf_eval_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *wo, float *value, float *pdf);
 
+/* environment emitter (EmitterAdapter of test_chisquare.cpp:342-388) */
+int oracle_env_sample_direct_n(const mtsg_scene_desc *d, uint32_t n, const float *u2, const float ref[3], float *dir,
+                               float *pdf, float *value);
+int oracle_env_pdf_direct_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, float *pdf);
+int oracle_env_eval_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, const float *rx, const float *ry, float *out);
+
 const char *oracle_last_error(void);
 
 #ifdef __cplusplus

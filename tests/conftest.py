@@ -23,6 +23,8 @@ def _ensure_built():
                                              "oracle/liboracle_fast.so")]
     if not all(os.path.exists(p) for p in need):
         subprocess.check_call(["make", "-C", REPO, "-j4", "host", "oracle"])
+    if not os.path.exists(os.path.join(REPO, "scenes", "sky512.pfm")):
+        subprocess.check_call(["make", "-C", REPO, "scenes/sky512.pfm"])
 
 
 _ensure_built()

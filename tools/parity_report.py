@@ -62,7 +62,8 @@ def samples_diff(path, defs, maxshow=12):
 
 
 if __name__ == "__main__" and "--samples" in sys.argv:
-    samples_diff(sys.argv[1], dict(a.split("=", 1) for a in sys.argv[2:] if "=" in a))
+    args = [a for a in sys.argv[1:] if a != "--samples"]
+    samples_diff(args[0], dict(a.split("=", 1) for a in args[1:] if "=" in a))
 
 
 def replay(path, defs, cases):
