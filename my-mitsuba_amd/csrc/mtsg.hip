@@ -290,6 +290,10 @@ struct KdRay {
     uint32_t sp, bottom;
     uint32_t found;
     uint32_t dneg;       // bit a: d[a] <= 0 (Havran's tie rule for o[a] == split)
+    // speculative traversal (kd_iter_spec): the leaf under test and its exit
+    uint32_t lfE, lfEnd; // remaining primitive range (lfE >= lfEnd: none)
+    float lfTmax;        // exit distance of that leaf; < 0: no leaf under test
+    uint32_t travDone;   // traversal has no node left (leaf may still be under test)
 };
 
 // LDS short stack: far-child node data and its exit distance, SoA by lane
@@ -337,6 +341,9 @@ DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float ray
     r.found = 0;
     r.bu = r.bv = 0.f;
     r.bprim = 0xFFFFFFFFu;
+    r.lfE = r.lfEnd = 0;
+    r.lfTmax = -1.0f;
+    r.travDone = 0;
     return true;
 }
 
@@ -813,6 +820,91 @@ DEV bool kd_iter2(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
     return false;
 }
 
+// Speculative traversal over the two-level blocks (the "speculative
+// while-while" idea of Aila & Laine 2009 recast as unified iterations): a
+// lane tests one primitive of the leaf it holds AND descends its traversal
+// towards the next leaf in the same iteration, so both code paths do useful
+// work for most lanes.  The traversal pauses on reaching a leaf until the
+// held leaf is finished; Havran's exit test (`best < leaf exit`) is applied
+// when a held leaf is exhausted, and to empty leaves when none is held.
+// Extra leaves visited speculatively can only be tested against [mint, best],
+// so the closest hit is unchanged (every primitive is referenced by all the
+// leaves it overlaps).
+template <bool SHADOW, bool COUNT>
+DEV bool kd_iter_spec(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
+    const uint2 n = r.cur;
+    const bool inner = !r.travDone && !(n.x & 0x80000000u);
+    const bool prim = r.lfE < r.lfEnd;
+    const bool rootKind = inner && !(n.x & 4u);
+    const uint4 *blk = S.blocks + (inner ? (rootKind ? 4u * (n.x >> 3) : (n.x >> 3)) : 0u);
+    const uint4 p0 = blk[0], p1 = blk[1], p2 = blk[2];
+    const float4 *rec = S.triL + 3 * (size_t)(prim ? r.lfE : 0u);
+    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
+    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(p1.x), "v"(p1.y), "v"(p1.z), "v"(p1.w),
+                 "v"(p2.x), "v"(p2.y), "v"(p2.z), "v"(p2.w), "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
+                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
+    if (prim) {
+        if (COUNT) { cnt.refs++; cnt.tests++; }
+        float t, u, v;
+        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
+        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+        if (h) {
+            r.found = 1;
+            if (SHADOW) return true;
+            r.best = t; r.bu = u; r.bv = v;
+            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
+        }
+        ++r.lfE;
+    }
+    if (inner) {
+        if (COUNT) cnt.nodes++;
+        bool nearLeft;
+        const uint2 c = kd_descend(r, n, p0, stk, nearLeft);
+        r.cur = c;
+        if (rootKind && !(c.x & 0x80000000u)) {
+            if (COUNT) cnt.nodes++;
+            const uint4 pc = nearLeft ? p1 : p2;
+            bool dummy;
+            r.cur = kd_descend(r, c, pc, stk, dummy);
+        }
+    }
+    // the held leaf is finished: Havran's exit test
+    if (r.lfTmax >= 0.0f && r.lfE >= r.lfEnd) {
+        if (r.found && r.best < r.lfTmax) return true;
+        r.lfTmax = -1.0f;
+    }
+    // take the leaf the traversal reached (if none is held), then advance
+    const uint2 c = r.cur;
+    if (r.lfTmax < 0.0f && !r.travDone && (c.x & 0x80000000u)) {
+        const uint32_t st = c.x & 0x7FFFFFFFu;
+        if (st < c.y) {
+            r.lfE = st; r.lfEnd = c.y; r.lfTmax = r.tmax;
+        } else if (r.found && r.best < r.tmax) {
+            return true;   // empty leaf, nothing held: exit test as in Havran
+        }
+        // pop the next far child, restart after a short-stack overflow, or finish
+        if (r.sp == r.bottom) {
+            if (r.bottom == 0) {
+                r.travDone = 1;
+            } else {
+                r.sp = r.bottom = 0;
+                r.tmin = r.tmax;
+                r.tmax = r.best;
+                r.cur = S.root2;
+                if (!(r.tmin < r.tmax)) r.travDone = 1;
+            }
+        } else {
+            --r.sp;
+            const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
+            r.cur = stk.node[k];
+            r.tmin = r.tmax;
+            r.tmax = fminf(stk.t[k], r.best);
+        }
+    }
+    return r.travDone && r.lfTmax < 0.0f;
+}
+
 template <bool SHADOW, bool COUNT>
 DEV bool kd_iter_phase(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt, bool primPhase) {
     const uint2 n = r.cur;
@@ -879,7 +971,7 @@ DEV bool kd_iter_phase(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cn
 // PRIM_RATIO = 0: unified iterations (kd_iter); otherwise phase-separated
 // (kd_iter_phase) with a primitive phase once primLanes * PRIM_RATIO >=
 // 4 * nodeLanes, or when no lane is at an inner node.
-template <bool SHADOW, bool COUNT, int MIN_IDLE, int PRIM_RATIO = 0, bool LAYOUT2 = false>
+template <bool SHADOW, bool COUNT, int MIN_IDLE, int PRIM_RATIO = 0, bool LAYOUT2 = false, bool SPEC = false>
 __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
     KD_STACK_DECL
     uint32_t count = nIdentity;
@@ -950,7 +1042,8 @@ __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t n
         }
         bool done = false;
         if (active) {
-            if (LAYOUT2) done = kd_iter2<SHADOW, COUNT>(S, r, stk, c);
+            if (SPEC) done = kd_iter_spec<SHADOW, COUNT>(S, r, stk, c);
+            else if (LAYOUT2) done = kd_iter2<SHADOW, COUNT>(S, r, stk, c);
             else if (PRIM_RATIO > 0) done = kd_iter_phase<SHADOW, COUNT>(S, r, stk, c, primPhase);
             else done = kd_iter<SHADOW, COUNT>(S, r, stk, c);
         }
@@ -974,6 +1067,206 @@ __global__ void k_env_eval(DevScene S, const float *dirs, const float *rx, const
     const float3 y = diff ? mk3(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]) : d;
     const float3 v = env_eval(S.env, d, diff, x, y);
     out[3 * i] = v.x; out[3 * i + 1] = v.y; out[3 * i + 2] = v.z;
+}
+
+// ---------------------------------------------------------------------------
+// Speculative traversal with compact per-lane state (the default): as
+// kd_iter_spec, with the stack counters, direction signs and flags packed in
+// one word and hit records written through on every hit (so u, v and the
+// primitive index are not kept live).  19 state registers instead of 27, for
+// 8 waves per SIMD.
+// ---------------------------------------------------------------------------
+struct SpecRay {
+    float3 o, d, inv;
+    float mint, best;    // primitive-test interval (best shrinks with hits)
+    float tmin, tmax;    // traversal interval of r.cur
+    uint2 cur;           // traversal node (two-level encoding)
+    uint32_t lfE, lfEnd; // primitive range of the held leaf
+    float lfTmax;        // exit distance of the held leaf; < 0: none held
+    uint32_t bits;       // sp | bottom << 8 | dneg << 16 | travDone << 19 | found << 20
+};
+enum : uint32_t { SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20 };
+
+template <bool SHADOW>
+DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, SpecRay &r) {
+    KdRay k;
+    if (!kd_init<SHADOW>(S, o, d, rayMint, rayMaxt, k)) return false;
+    r.o = k.o; r.d = k.d; r.inv = k.inv;
+    r.mint = k.mint; r.best = k.best; r.tmin = k.tmin; r.tmax = k.tmax;
+    r.cur = S.root2;
+    r.lfE = r.lfEnd = 0;
+    r.lfTmax = -1.0f;
+    r.bits = k.dneg << 16;
+    return true;
+}
+
+// inner-node step with the packed short-stack counters (as kd_descend)
+DEV uint2 spec_descend(SpecRay &r, uint2 n, const uint4 &pr, KdStack stk, bool &nearIsLeft) {
+    const uint32_t axis = n.x & 3u;
+    const float split = __uint_as_float(n.y);
+    const bool a0 = axis == 0u, a1 = axis == 1u;
+    float ox = r.o.x, oy = r.o.y, oz = r.o.z, ix = r.inv.x, iy = r.inv.y, iz = r.inv.z;
+    launder3(ox, oy, oz);
+    launder3(ix, iy, iz);
+    const float oa = a0 ? ox : (a1 ? oy : oz);
+    const float ia = a0 ? ix : (a1 ? iy : iz);
+    float tsplit = (split - oa) * ia;
+    if (tsplit != tsplit) tsplit = INFINITY;
+    const bool belowFirst = (oa < split) || (oa == split && ((r.bits >> (16 + axis)) & 1u));
+    const uint2 first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
+    const uint2 second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+    nearIsLeft = belowFirst;
+    if (tsplit > r.tmax || tsplit <= 0.0f) return first;
+    if (tsplit < r.tmin) { nearIsLeft = !belowFirst; return second; }
+    const uint32_t sp = r.bits & 0xFFu;
+    const uint32_t k = (sp % SHORT_STACK) * TRACE_BLOCK;
+    stk.node[k] = second;
+    stk.t[k] = r.tmax;
+    r.bits += 1u;
+    if ((sp + 1u) - ((r.bits >> 8) & 0xFFu) > (uint32_t)SHORT_STACK) r.bits += 0x100u;
+    r.tmax = tsplit;
+    return first;
+}
+
+template <bool SHADOW, bool COUNT>
+DEV bool spec_iter(const DevScene &S, SpecRay &r, KdStack stk, TraceCounts &cnt, float4 *hitOut) {
+    const uint2 n = r.cur;
+    const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
+    const bool prim = r.lfE < r.lfEnd;
+    const bool rootKind = inner && !(n.x & 4u);
+    const uint4 *blk = S.blocks + (inner ? (rootKind ? 4u * (n.x >> 3) : (n.x >> 3)) : 0u);
+    const uint4 p0 = blk[0], p1 = blk[1], p2 = blk[2];
+    const float4 *rec = S.triL + 3 * (size_t)(prim ? r.lfE : 0u);
+    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
+    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(p1.x), "v"(p1.y), "v"(p1.z), "v"(p1.w),
+                 "v"(p2.x), "v"(p2.y), "v"(p2.z), "v"(p2.w), "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
+                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
+    if (prim) {
+        if (COUNT) { cnt.refs++; cnt.tests++; }
+        float t, u, v;
+        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
+        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+        if (h) {
+            r.bits |= SB_FOUND;
+            if (SHADOW) return true;
+            r.best = t;
+            stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
+        }
+        ++r.lfE;
+    }
+    if (inner) {
+        if (COUNT) cnt.nodes++;
+        bool nearLeft;
+        const uint2 c = spec_descend(r, n, p0, stk, nearLeft);
+        r.cur = c;
+        if (rootKind && !(c.x & 0x80000000u)) {
+            if (COUNT) cnt.nodes++;
+            const uint4 pc = nearLeft ? p1 : p2;
+            bool dummy;
+            r.cur = spec_descend(r, c, pc, stk, dummy);
+        }
+    }
+    const bool found = (r.bits & SB_FOUND) != 0;
+    if (r.lfTmax >= 0.0f && r.lfE >= r.lfEnd) {
+        if (found && r.best < r.lfTmax) return true;
+        r.lfTmax = -1.0f;
+    }
+    const uint2 c = r.cur;
+    if (r.lfTmax < 0.0f && !(r.bits & SB_TRAVDONE) && (c.x & 0x80000000u)) {
+        const uint32_t st = c.x & 0x7FFFFFFFu;
+        if (st < c.y) {
+            r.lfE = st; r.lfEnd = c.y; r.lfTmax = r.tmax;
+        } else if (found && r.best < r.tmax) {
+            return true;
+        }
+        const uint32_t sp = r.bits & 0xFFu, bottom = (r.bits >> 8) & 0xFFu;
+        if (sp == bottom) {
+            if (bottom == 0) {
+                r.bits |= SB_TRAVDONE;
+            } else {
+                r.bits &= ~0xFFFFu;   // kd-restart
+                r.tmin = r.tmax;
+                r.tmax = r.best;
+                r.cur = S.root2;
+                if (!(r.tmin < r.tmax)) r.bits |= SB_TRAVDONE;
+            }
+        } else {
+            r.bits -= 1u;
+            const uint32_t k = ((sp - 1u) % SHORT_STACK) * TRACE_BLOCK;
+            r.cur = stk.node[k];
+            r.tmin = r.tmax;
+            r.tmax = fminf(stk.t[k], r.best);
+        }
+    }
+    return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
+}
+
+template <bool SHADOW, bool COUNT, int MIN_IDLE>
+__global__ void TRACE_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
+    KD_STACK_DECL
+    uint32_t count = nIdentity;
+    if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
+    else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
+    const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
+    Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
+    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
+    uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
+    bool exhausted = false;
+    bool active = false;
+    uint32_t slot = 0;
+    SpecRay r;
+    const unsigned long long below = (1ull << __lane_id()) - 1ull;
+    for (;;) {
+        unsigned long long idle = __ballot(!active);
+        if ((uint32_t)__popcll(idle) < (uint32_t)MIN_IDLE && __any(active)) idle = 0;
+        while (idle && !exhausted) {
+            if (poolLeft == 0 && !F.next(FETCH, poolBase, poolLeft)) { exhausted = true; break; }
+            const uint32_t nIdle = (uint32_t)__popcll(idle);
+            const uint32_t take = min(nIdle, poolLeft);
+            const uint32_t rank = (uint32_t)__popcll(idle & below);
+            if (!active && rank < take) {
+                const uint32_t i = poolBase + rank;
+                slot = q ? q[i] : i;
+                float4 ro, rd;
+                load_ray(P, SHADOW, slot, ro, rd);
+                const bool live = spec_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
+                if (live) {
+                    active = true;
+                } else if (!SHADOW && rd.w < 0.0f) {
+                    // dead slot (outside the render rectangle)
+                } else if (SHADOW) {
+                    shadow_unoccluded(P, slot);
+                } else {
+                    stS(&P.hit[slot], make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)));
+                }
+            }
+            poolBase += take;
+            poolLeft -= take;
+            idle = __ballot(!active);
+            if (take == nIdle) break;
+        }
+        if (!__any(active)) {
+            if (exhausted) break;
+            continue;
+        }
+        if (COUNT) {
+            const uint2 n = r.cur;
+            const bool inner = active && !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
+            const bool prim = active && r.lfE < r.lfEnd;
+            const bool anyInner = __any(inner), anyPrim = __any(prim);
+            const uint32_t nActive = (uint32_t)__popcll(__ballot(active));
+            if (__lane_id() == 0) { c.wsteps += 1; c.wnodes += anyInner; c.wtests += anyPrim; c.wactive += nActive; }
+        }
+        if (active && spec_iter<SHADOW, COUNT>(S, r, stk, c, P.hit + slot)) {
+            active = false;
+            // shadow: any hit returns before SB_FOUND is set; closest: hits were
+            // written through, only a miss needs a record
+            if (SHADOW) { if (!(r.bits & SB_FOUND)) shadow_unoccluded(P, slot); }
+            else if (!(r.bits & SB_FOUND)) stS(&P.hit[slot], make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)));
+        }
+    }
+    flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
 }
 
 // Debug entry points over caller-provided rays
@@ -1885,7 +2178,9 @@ void timed_launch(mtsg_scene *s, int kind, F f) {
 //   5/6/7 = unified one-node-or-one-primitive iterations, refill at 32/16/8 idle lanes,
 //   8/9/10/11 = phase-separated iterations, primitive phase once
 //               primLanes >= nodeLanes x 1 / 0.5 / 0.25 / 2,
-//   12/13 = unified iterations over the two-level block layout, refill at 16/32
+//   12/13 = unified iterations over the two-level block layout, refill at 16/32,
+//   14/15 = speculative unified iterations over the two-level layout, refill at 16/32,
+//   16/17 = speculative with compact state (k_trace_s), refill at 16/32
 template <bool SHADOW, bool COUNT>
 void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
     dim3 g(s->traceGrid), blk(TRACE_BLOCK);
@@ -1903,6 +2198,10 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
         case 11: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 2>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 12: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 0, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         case 13: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 32, 0, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 14: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 0, true, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 15: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 32, 0, true, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 16: hipLaunchKernelGGL((k_trace_s<SHADOW, COUNT, 16>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
+        case 17: hipLaunchKernelGGL((k_trace_s<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
         default: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
     }
 }
@@ -2303,7 +2602,9 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     // persistent grids from the occupancy query
     if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     int perCU = 0;
-    const void *occKernel = s->traceMode >= 12 ? (const void *)k_trace_u<false, false, 16, 0, true>
+    const void *occKernel = s->traceMode >= 16 ? (const void *)k_trace_s<false, false, 16>
+                          : s->traceMode >= 14 ? (const void *)k_trace_u<false, false, 16, 0, true, true>
+                          : s->traceMode >= 12 ? (const void *)k_trace_u<false, false, 16, 0, true>
                           : s->traceMode >= 5 ? (const void *)k_trace_u<false, false, 32> : (const void *)k_trace<false, false, 32>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, occKernel, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
         perCU = 8;
