@@ -29,7 +29,7 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-TRAFFIC_KERNEL = "k_trace_u<false, false, 16, 0, true>"
+TRAFFIC_KERNEL = "k_trace_s<false, false, 16>"
 
 
 def pmc_traffic(workload):
@@ -217,7 +217,7 @@ def main():
                                        f"({tj['traffic_bytes_per_launch'] / 1e9:.2f} GB) / this run's avg launch time"
                                        if traffic is not None else None),
                     "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                    "kernel": "k_trace_u<closest>", "bytes_per_ray": round(b_ray, 1),
+                    "kernel": "k_trace_s<closest>", "bytes_per_ray": round(b_ray, 1),
                     "nodes_per_ray": round(nodes_per_ray, 2), "leaf_refs_per_ray": round(refs_per_ray, 2),
                     "tri_tests_per_ray": round(tests_per_ray, 2), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                     "launches_per_frame": launches,

@@ -160,6 +160,11 @@ constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per l
 #ifndef MTSG_TRACE_WAVES
 #define MTSG_TRACE_WAVES 0
 #endif
+// the compact speculative traversal is sized for 8 waves per SIMD (64 VGPRs)
+#ifndef MTSG_SPEC_WAVES
+#define MTSG_SPEC_WAVES 8
+#endif
+#define SPEC_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SPEC_WAVES)))
 #if MTSG_TRACE_WAVES > 0
 #define TRACE_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_TRACE_WAVES)))
 #else
@@ -1087,6 +1092,37 @@ struct SpecRay {
 };
 enum : uint32_t { SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20 };
 
+// short stack of the compact traversal: entry k of lane i at [k * TRACE_BLOCK
+// + i].  Only the lane index is kept in a register (laundered at every use so
+// the two scaled addresses are not hoisted into two loop-invariant registers).
+__shared__ uint2 s_specNode[SHORT_STACK * TRACE_BLOCK];
+__shared__ float s_specT[SHORT_STACK * TRACE_BLOCK];
+struct SpecStack {
+    uint32_t lane;
+    DEV uint32_t at(uint32_t k) const {
+        uint32_t l = lane;
+        asm volatile("" : "+v"(l));
+        return k * TRACE_BLOCK + l;
+    }
+    DEV void push(uint32_t k, uint2 node, float t) const {
+        const uint32_t i = at(k);
+        s_specNode[i] = node;
+        s_specT[i] = t;
+    }
+    DEV uint2 node(uint32_t k) const { return s_specNode[at(k)]; }
+    DEV float t(uint32_t k) const { return s_specT[at(k)]; }
+};
+
+// constant 4-vector built at its use (keeps the compiler from holding it in
+// registers across the traversal loop)
+DEV float4 miss_record() {
+    float4 m;
+    uint32_t inf = 0x7F800000u, z = 0u, ff = 0xFFFFFFFFu;
+    asm volatile("" : "+v"(inf), "+v"(z), "+v"(ff));
+    m.x = __uint_as_float(inf); m.y = __uint_as_float(z); m.z = __uint_as_float(z); m.w = __uint_as_float(ff);
+    return m;
+}
+
 template <bool SHADOW>
 DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, SpecRay &r) {
     KdRay k;
@@ -1100,8 +1136,10 @@ DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float r
     return true;
 }
 
-// inner-node step with the packed short-stack counters (as kd_descend)
-DEV uint2 spec_descend(SpecRay &r, uint2 n, const uint4 &pr, KdStack stk, bool &nearIsLeft) {
+// inner-node step with the packed short-stack counters (as kd_descend), split
+// in two: spec_plan needs only the node word (axis, split), so the child to
+// visit is known before the node's children are fetched; spec_take applies it.
+DEV void spec_plan(const SpecRay &r, uint2 n, float &tsplit, bool &goLeft, bool &push) {
     const uint32_t axis = n.x & 3u;
     const float split = __uint_as_float(n.y);
     const bool a0 = axis == 0u, a1 = axis == 1u;
@@ -1110,36 +1148,47 @@ DEV uint2 spec_descend(SpecRay &r, uint2 n, const uint4 &pr, KdStack stk, bool &
     launder3(ix, iy, iz);
     const float oa = a0 ? ox : (a1 ? oy : oz);
     const float ia = a0 ? ix : (a1 ? iy : iz);
-    float tsplit = (split - oa) * ia;
+    tsplit = (split - oa) * ia;
     if (tsplit != tsplit) tsplit = INFINITY;
     const bool belowFirst = (oa < split) || (oa == split && ((r.bits >> (16 + axis)) & 1u));
-    const uint2 first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
-    const uint2 second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
-    nearIsLeft = belowFirst;
-    if (tsplit > r.tmax || tsplit <= 0.0f) return first;
-    if (tsplit < r.tmin) { nearIsLeft = !belowFirst; return second; }
-    const uint32_t sp = r.bits & 0xFFu;
-    const uint32_t k = (sp % SHORT_STACK) * TRACE_BLOCK;
-    stk.node[k] = second;
-    stk.t[k] = r.tmax;
-    r.bits += 1u;
-    if ((sp + 1u) - ((r.bits >> 8) & 0xFFu) > (uint32_t)SHORT_STACK) r.bits += 0x100u;
-    r.tmax = tsplit;
-    return first;
+    const bool onlyFirst = tsplit > r.tmax || tsplit <= 0.0f;
+    const bool goSecond = !onlyFirst && tsplit < r.tmin;
+    push = !onlyFirst && !goSecond;
+    goLeft = belowFirst != goSecond;
+}
+
+DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push, SpecStack stk) {
+    const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
+    if (push) {
+        const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+        const uint32_t sp = r.bits & 0xFFu;
+        stk.push(sp % SHORT_STACK, other, r.tmax);
+        r.bits += 1u;
+        if ((sp + 1u) - ((r.bits >> 8) & 0xFFu) > (uint32_t)SHORT_STACK) r.bits += 0x100u;
+        r.tmax = tsplit;
+    }
+    return c;
 }
 
 template <bool SHADOW, bool COUNT>
-DEV bool spec_iter(const DevScene &S, SpecRay &r, KdStack stk, TraceCounts &cnt, float4 *hitOut) {
+DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cnt, float4 *hitOut) {
     const uint2 n = r.cur;
     const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
     const bool prim = r.lfE < r.lfEnd;
     const bool rootKind = inner && !(n.x & 4u);
-    const uint4 *blk = S.blocks + (inner ? (rootKind ? 4u * (n.x >> 3) : (n.x >> 3)) : 0u);
-    const uint4 p0 = blk[0], p1 = blk[1], p2 = blk[2];
+    // the first step is planned from the node word alone, so only the pair
+    // of the grandchildren on the side taken is fetched (block root: {children,
+    // left grandchildren, right grandchildren})
+    float tsplit;
+    bool goLeft, push;
+    spec_plan(r, n, tsplit, goLeft, push);
+    const uint32_t bi = inner ? (rootKind ? 4u * (n.x >> 3) : (n.x >> 3)) : 0u;
+    const uint4 *blk = S.blocks + bi;
+    const uint4 p0 = blk[0], pc = blk[rootKind ? (goLeft ? 1 : 2) : 0];
     const float4 *rec = S.triL + 3 * (size_t)(prim ? r.lfE : 0u);
     const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(p1.x), "v"(p1.y), "v"(p1.z), "v"(p1.w),
-                 "v"(p2.x), "v"(p2.y), "v"(p2.z), "v"(p2.w), "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
+    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
+                 "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
                  "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
     if (prim) {
         if (COUNT) { cnt.refs++; cnt.tests++; }
@@ -1157,14 +1206,14 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, KdStack stk, TraceCounts &cnt,
     }
     if (inner) {
         if (COUNT) cnt.nodes++;
-        bool nearLeft;
-        const uint2 c = spec_descend(r, n, p0, stk, nearLeft);
+        const uint2 c = spec_take(r, p0, tsplit, goLeft, push, stk);
         r.cur = c;
         if (rootKind && !(c.x & 0x80000000u)) {
             if (COUNT) cnt.nodes++;
-            const uint4 pc = nearLeft ? p1 : p2;
-            bool dummy;
-            r.cur = spec_descend(r, c, pc, stk, dummy);
+            float ts2;
+            bool gl2, push2;
+            spec_plan(r, c, ts2, gl2, push2);
+            r.cur = spec_take(r, pc, ts2, gl2, push2, stk);
         }
     }
     const bool found = (r.bits & SB_FOUND) != 0;
@@ -1193,18 +1242,18 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, KdStack stk, TraceCounts &cnt,
             }
         } else {
             r.bits -= 1u;
-            const uint32_t k = ((sp - 1u) % SHORT_STACK) * TRACE_BLOCK;
-            r.cur = stk.node[k];
+            const uint32_t k = (sp - 1u) % SHORT_STACK;
+            r.cur = stk.node(k);
             r.tmin = r.tmax;
-            r.tmax = fminf(stk.t[k], r.best);
+            r.tmax = fminf(stk.t(k), r.best);
         }
     }
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
 }
 
 template <bool SHADOW, bool COUNT, int MIN_IDLE>
-__global__ void TRACE_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
-    KD_STACK_DECL
+__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
+    const SpecStack stk{threadIdx.x};
     uint32_t count = nIdentity;
     if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
@@ -1238,7 +1287,7 @@ __global__ void TRACE_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t n
                 } else if (SHADOW) {
                     shadow_unoccluded(P, slot);
                 } else {
-                    stS(&P.hit[slot], make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)));
+                    stS(&P.hit[slot], miss_record());
                 }
             }
             poolBase += take;
@@ -1263,7 +1312,7 @@ __global__ void TRACE_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t n
             // shadow: any hit returns before SB_FOUND is set; closest: hits were
             // written through, only a miss needs a record
             if (SHADOW) { if (!(r.bits & SB_FOUND)) shadow_unoccluded(P, slot); }
-            else if (!(r.bits & SB_FOUND)) stS(&P.hit[slot], make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)));
+            else if (!(r.bits & SB_FOUND)) stS(&P.hit[slot], miss_record());
         }
     }
     flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
@@ -2104,7 +2153,7 @@ struct mtsg_scene {
     int cuCount = 0;
     int traceGrid = 0, shadeGrid = 0;
     uint32_t flags = 0;
-    int traceMode = 12;           // unified traversal over two-level blocks, refill at 16 idle lanes (measured best)
+    int traceMode = 16;           // speculative compact traversal over two-level blocks, refill at 16 idle lanes (measured best)
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
     mtsg_stats stats{};
