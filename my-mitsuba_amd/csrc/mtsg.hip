@@ -1088,9 +1088,15 @@ struct SpecRay {
     uint2 cur;           // traversal node (two-level encoding)
     uint32_t lfE, lfEnd; // primitive range of the held leaf
     float lfTmax;        // exit distance of the held leaf; < 0: none held
-    uint32_t bits;       // sp | bottom << 8 | dneg << 16 | travDone << 19 | found << 20
+    uint32_t bits;       // see SB_*
 };
-enum : uint32_t { SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20 };
+// bits: top slot of the circular short stack (0-2), entries held (3-5),
+// entries dropped since the last restart (6), ray direction signs (16-18),
+// traversal done (19), hit found (20)
+enum : uint32_t {
+    SB_TOP = 7u, SB_N = 7u << 3, SB_N1 = 1u << 3, SB_DROPPED = 1u << 6, SB_STACK = 0x7Fu,
+    SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20
+};
 
 // short stack of the compact traversal: entry k of lane i at [k * TRACE_BLOCK
 // + i].  Only the lane index is kept in a register (laundered at every use so
@@ -1132,7 +1138,7 @@ DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float r
     r.cur = S.root2;
     r.lfE = r.lfEnd = 0;
     r.lfTmax = -1.0f;
-    r.bits = k.dneg << 16;
+    r.bits = k.dneg << SB_DNEG;
     return true;
 }
 
@@ -1150,21 +1156,23 @@ DEV void spec_plan(const SpecRay &r, uint2 n, float &tsplit, bool &goLeft, bool 
     const float ia = a0 ? ix : (a1 ? iy : iz);
     tsplit = (split - oa) * ia;
     if (tsplit != tsplit) tsplit = INFINITY;
-    const bool belowFirst = (oa < split) || (oa == split && ((r.bits >> (16 + axis)) & 1u));
-    const bool onlyFirst = tsplit > r.tmax || tsplit <= 0.0f;
-    const bool goSecond = !onlyFirst && tsplit < r.tmin;
-    push = !onlyFirst && !goSecond;
+    // bitwise, not short-circuit: no exec-mask branches for these
+    const bool belowFirst = (oa < split) | ((oa == split) & (bool)((r.bits >> (SB_DNEG + axis)) & 1u));
+    const bool onlyFirst = (tsplit > r.tmax) | (tsplit <= 0.0f);
+    const bool goSecond = !onlyFirst & (tsplit < r.tmin);
+    push = !onlyFirst & !goSecond;
     goLeft = belowFirst != goSecond;
 }
 
 DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push, SpecStack stk) {
     const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
     if (push) {
+        // circular short stack: a push onto a full stack drops the oldest entry
         const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
-        const uint32_t sp = r.bits & 0xFFu;
-        stk.push(sp % SHORT_STACK, other, r.tmax);
-        r.bits += 1u;
-        if ((sp + 1u) - ((r.bits >> 8) & 0xFFu) > (uint32_t)SHORT_STACK) r.bits += 0x100u;
+        const uint32_t b = r.bits, top = b & SB_TOP;
+        stk.push(top, other, r.tmax);
+        const bool full = (b & SB_N) == (uint32_t)SHORT_STACK * SB_N1;
+        r.bits = ((b & ~SB_TOP) | (top == SHORT_STACK - 1 ? 0u : top + 1u)) + (full ? SB_DROPPED - (b & SB_DROPPED) : SB_N1);
         r.tmax = tsplit;
     }
     return c;
@@ -1182,10 +1190,12 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     float tsplit;
     bool goLeft, push;
     spec_plan(r, n, tsplit, goLeft, push);
-    const uint32_t bi = inner ? (rootKind ? 4u * (n.x >> 3) : (n.x >> 3)) : 0u;
-    const uint4 *blk = S.blocks + bi;
-    const uint4 p0 = blk[0], pc = blk[rootKind ? (goLeft ? 1 : 2) : 0];
-    const float4 *rec = S.triL + 3 * (size_t)(prim ? r.lfE : 0u);
+    // block root: 64-B block n.x >> 3; pair-only node: 16-B pair n.x >> 3
+    const uint32_t base = inner ? (n.x >> 3) << ((~n.x >> 1) & 2u) : 0u;
+    const uint32_t off = rootKind ? 2u - (uint32_t)goLeft : 0u;
+    const uint32_t pi = prim ? r.lfE : 0u;
+    const uint4 p0 = S.blocks[base], pc = S.blocks[base + off];
+    const float4 *rec = S.triL + 3 * (size_t)pi;
     const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
     asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
                  "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
@@ -1217,35 +1227,35 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         }
     }
     const bool found = (r.bits & SB_FOUND) != 0;
-    if (r.lfTmax >= 0.0f && r.lfE >= r.lfEnd) {
-        if (found && r.best < r.lfTmax) return true;
-        r.lfTmax = -1.0f;
-    }
+    // the held leaf is finished: Havran's exit, or let the descent take over
+    const bool leafDone = (r.lfTmax >= 0.0f) & (r.lfE >= r.lfEnd);
+    if (leafDone & found & (r.best < r.lfTmax)) return true;
+    r.lfTmax = leafDone ? -1.0f : r.lfTmax;
     const uint2 c = r.cur;
-    if (r.lfTmax < 0.0f && !(r.bits & SB_TRAVDONE) && (c.x & 0x80000000u)) {
+    if ((r.lfTmax < 0.0f) & !(r.bits & SB_TRAVDONE) & (bool)(c.x >> 31)) {
+        // the descent reached a leaf: adopt it, then continue from the stack
         const uint32_t st = c.x & 0x7FFFFFFFu;
-        if (st < c.y) {
-            r.lfE = st; r.lfEnd = c.y; r.lfTmax = r.tmax;
-        } else if (found && r.best < r.tmax) {
-            return true;
-        }
-        const uint32_t sp = r.bits & 0xFFu, bottom = (r.bits >> 8) & 0xFFu;
-        if (sp == bottom) {
-            if (bottom == 0) {
-                r.bits |= SB_TRAVDONE;
-            } else {
-                r.bits &= ~0xFFFFu;   // kd-restart
-                r.tmin = r.tmax;
-                r.tmax = r.best;
-                r.cur = S.root2;
-                if (!(r.tmin < r.tmax)) r.bits |= SB_TRAVDONE;
-            }
-        } else {
-            r.bits -= 1u;
-            const uint32_t k = (sp - 1u) % SHORT_STACK;
+        const bool nonEmpty = st < c.y;
+        if (!nonEmpty & found & (r.best < r.tmax)) return true;
+        r.lfE = nonEmpty ? st : r.lfE;
+        r.lfEnd = nonEmpty ? c.y : r.lfEnd;
+        r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
+        const uint32_t b = r.bits;
+        if (b & SB_N) {
+            const uint32_t top = b & SB_TOP, k = top == 0 ? SHORT_STACK - 1 : top - 1u;
             r.cur = stk.node(k);
+            const float t = stk.t(k);
+            r.bits = ((b & ~SB_TOP) | k) - SB_N1;
             r.tmin = r.tmax;
-            r.tmax = fminf(stk.t(k), r.best);
+            r.tmax = fminf(t, r.best);
+        } else {
+            // empty: done, or a kd-restart behind this leaf if entries were dropped
+            const bool restart = (b & SB_DROPPED) != 0;
+            const float t0 = r.tmax;
+            r.tmin = restart ? t0 : r.tmin;
+            r.tmax = restart ? r.best : r.tmax;
+            r.cur = restart ? S.root2 : c;
+            r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
         }
     }
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
