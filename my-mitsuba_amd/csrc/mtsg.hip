@@ -96,6 +96,7 @@ struct DevCamera {
 struct DevIntegrator {
     int max_depth, rr_depth, strict_normals, hide_emitters;
     uint32_t spp, seed;
+    uint32_t film_w;   // sample id = (y * film_w + x) * spp + s
 };
 
 // wavefront batch: tiles [tile0, tile0 + ntiles) x samples [s0, s0 + ns)
@@ -110,20 +111,27 @@ struct DevBatch {
 
 enum : uint32_t { F_SCATTERED = 1u << 16, F_DELTA = 1u << 17 };
 
+// Path state.  The paths of a bounce are stored densely by their position in
+// that bounce's work list (the camera's slot order at bounce 0, then the order
+// in which k_shade appended the surviving paths), so every kernel streams its
+// state with coalesced 16-B accesses instead of gathering it through a queue of
+// slot indices.  k_shade writes the survivors into the n_* arrays at their new
+// position; the host swaps the two sets after each bounce.  Only the final
+// radiance is kept per sample slot (L, written when a path terminates).
 struct DevPaths {
     float4 *ray_o;    // o.xyz, mint
     float4 *ray_d;    // d.xyz, maxt
-    float4 *hit;      // t, u, v, prim (bits)
-    float4 *L;        // rgb, alpha
-    float4 *T;        // rgb, eta
-    float4 *aux;      // refN.xyz of the previous vertex, bsdf pdf
-    uint2 *key;       // counter-RNG key
-    uint2 *st;        // x: depth | flags, y: next RNG dimension
-    float4 *sh_o;     // shadow ray origin, maxt
-    float4 *sh_d;     // shadow ray direction
-    float4 *sh_c;     // NEE contribution
-    uint32_t *q[2];   // path queues (ping-pong)
-    uint32_t *qs;     // shadow queue
+    float4 *T;        // throughput rgb, eta        (bounce 0: x-differential direction)
+    float4 *aux;      // refN.xyz of the previous vertex, bsdf pdf (bounce 0: y-differential)
+    float4 *Lp;       // radiance so far, alpha
+    uint4 *meta;      // depth | flags, next RNG dimension, sample slot, 0
+    float4 *n_ray_o, *n_ray_d, *n_T, *n_aux, *n_Lp;   // next bounce (compacted)
+    uint4 *n_meta;
+    float4 *hit;      // t, u, v, prim (bits) of ray i
+    float4 *L;        // per sample slot: final radiance, alpha (k_splat input)
+    float4 *sh_o;     // shadow ray i: origin, maxt
+    float4 *sh_d;     // direction, mint
+    float4 *sh_c;     // NEE contribution, target (bits): next-bounce position, or 1 << 31 | slot
     uint32_t *cnt;    // counters, each on its own 256-B line (see CNT_*)
     unsigned long long *ctr;  // traversal counters (nodes, refs, tests)
 };
@@ -142,14 +150,14 @@ DEV int cnt_q(int q) { return q ? CNT_Q1 : CNT_Q0; }
 constexpr int TILE = 16;                    // splat tile edge (256 pixels)
 constexpr int BLOCK = 256;
 constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traversal
-// Paths per wavefront batch (172 B of SoA state per path; 2^28 paths = 46 GB
+// Paths per wavefront batch (272 B of state per path; 2^28 paths = 73 GB
 // of the 288 GB HBM, capped at 60% of free device memory at run time).
 // Every traversal launch ends with a tail of ~0.5-0.8 ms while its longest
 // rays finish, and late bounces hold few paths, so the batch should be as
 // large as the frame -- measured on the 1M-triangle scene (Msamples/s):
 // 4M paths 421, 16M 672, 32M 803, 64M 884, 128M 934, whole frame 960.
 constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 28;
-constexpr size_t PATH_STATE_BYTES = 172;    // SoA bytes per path slot (DevPaths)
+constexpr size_t PATH_STATE_BYTES = 272;    // bytes per path slot (DevPaths: 2 x 96 dense + hit, L, 3 x shadow)
 #ifndef MTSG_SHORT_STACK
 #define MTSG_SHORT_STACK 6   // 6 x 12 B x 64 lanes = 4.6 KB LDS/wave -> 8 waves/SIMD (8: 6.5, 12: 4.2)
 #endif
@@ -197,6 +205,22 @@ DEV uint2 ldS(const uint2 *p) {
 DEV void stS(float4 *p, const float4 &v) {
 #if MTSG_NT
     __builtin_nontemporal_store((nf4){v.x, v.y, v.z, v.w}, (nf4 *)p);
+#else
+    *p = v;
+#endif
+}
+typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
+DEV uint4 ldS(const uint4 *p) {
+#if MTSG_NT
+    const nu4 v = __builtin_nontemporal_load((const nu4 *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+DEV void stS(uint4 *p, const uint4 &v) {
+#if MTSG_NT
+    __builtin_nontemporal_store((nu4){v.x, v.y, v.z, v.w}, (nu4 *)p);
 #else
     *p = v;
 #endif
@@ -527,16 +551,20 @@ struct Fetch {
     }
 };
 
-DEV void shadow_unoccluded(const DevPaths &P, uint32_t slot) {
-    const float4 con = ldS(&P.sh_c[slot]);
-    float4 L = ldS(&P.L[slot]);
-    L.x += con.x; L.y += con.y; L.z += con.z;
-    stS(&P.L[slot], L);
+// unoccluded shadow ray i: its contribution goes to the path's radiance, at
+// the path's next-bounce position or, if the path ended, to its final slot
+DEV void shadow_unoccluded(const DevPaths &P, uint32_t i) {
+    const float4 con = ldS(&P.sh_c[i]);
+    const uint32_t tgt = __float_as_uint(con.w);
+    float4 *L = (tgt & 0x80000000u) ? &P.L[tgt & 0x7FFFFFFFu] : &P.n_Lp[tgt];
+    float4 v = ldS(L);
+    v.x += con.x; v.y += con.y; v.z += con.z;
+    stS(L, v);
 }
 
-DEV void load_ray(const DevPaths &P, bool shadow, uint32_t slot, float4 &ro, float4 &rd) {
-    if (shadow) { ro = ldS(&P.sh_o[slot]); rd = ldS(&P.sh_d[slot]); rd.w = ro.w; ro.w = kEpsilon; }
-    else { ro = ldS(&P.ray_o[slot]); rd = ldS(&P.ray_d[slot]); }
+DEV void load_ray(const DevPaths &P, bool shadow, uint32_t i, float4 &ro, float4 &rd) {
+    if (shadow) { ro = ldS(&P.sh_o[i]); rd = ldS(&P.sh_d[i]); const float mint = rd.w; rd.w = ro.w; ro.w = mint; }
+    else { ro = ldS(&P.ray_o[i]); rd = ldS(&P.ray_d[i]); }
 }
 
 DEV float4 hit_record(const KdRay &r) {
@@ -552,7 +580,6 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths
     uint32_t count = nIdentity;
     if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
     Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
     TraceCounts c{0, 0, 0, 0, 0, 0, 0};
     uint32_t base, n;
@@ -560,7 +587,7 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths
         for (uint32_t rnd = 0; rnd * 64 < n; ++rnd) {
             const uint32_t i = base + 64u * rnd + __lane_id();
             if (i >= base + n) break;
-            const uint32_t slot = q ? q[i] : i;
+            const uint32_t slot = i;
             float4 ro, rd;
             load_ray(P, SHADOW, slot, ro, rd);
             if (!SHADOW && rd.w < 0.0f) continue;   // dead slot
@@ -595,7 +622,6 @@ __global__ void TRACE_ATTR k_trace(DevScene S, DevPaths P, int qin, uint32_t nId
     uint32_t count = nIdentity;   // explicit branches: a ternary over a volatile load
     if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);   // demotes the argument to scratch
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
     Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
     TraceCounts c{0, 0, 0, 0, 0, 0, 0};
     uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
@@ -616,7 +642,7 @@ __global__ void TRACE_ATTR k_trace(DevScene S, DevPaths P, int qin, uint32_t nId
             const uint32_t rank = (uint32_t)__popcll(idle & below);
             if (!active && rank < take) {
                 const uint32_t i = poolBase + rank;
-                slot = q ? q[i] : i;
+                slot = i;
                 float4 ro, rd;
                 load_ray(P, SHADOW, slot, ro, rd);
                 // kd_init before the dead-slot test so that both ray loads are
@@ -982,7 +1008,6 @@ __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t n
     uint32_t count = nIdentity;
     if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
     Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
     TraceCounts c{0, 0, 0, 0, 0, 0, 0};
     uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
@@ -1001,7 +1026,7 @@ __global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t n
             const uint32_t rank = (uint32_t)__popcll(idle & below);
             if (!active && rank < take) {
                 const uint32_t i = poolBase + rank;
-                slot = q ? q[i] : i;
+                slot = i;
                 float4 ro, rd;
                 load_ray(P, SHADOW, slot, ro, rd);
                 const bool live = kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
@@ -1267,7 +1292,6 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t nI
     uint32_t count = nIdentity;
     if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
     else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    const uint32_t *q = SHADOW ? P.qs : (qin < 0 ? nullptr : P.q[qin]);
     Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
     TraceCounts c{0, 0, 0, 0, 0, 0, 0};
     uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
@@ -1286,7 +1310,7 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t nI
             const uint32_t rank = (uint32_t)__popcll(idle & below);
             if (!active && rank < take) {
                 const uint32_t i = poolBase + rank;
-                slot = q ? q[i] : i;
+                slot = i;
                 float4 ro, rd;
                 load_ray(P, SHADOW, slot, ro, rd);
                 const bool live = spec_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
@@ -1392,7 +1416,6 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
             stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
             if (C.has_env) {
                 // rx/ryDirection scaled by 1/sqrt(spp) (integrator.cpp:148-149, ray.h:163-168),
-                // parked in the shadow-ray slots until bounce 0 is shaded
                 const float3 rxc = normalize(nearP + ld3(C.dx)), ryc = normalize(nearP + ld3(C.dy));
                 const float3 rx = mk3(t[0] * rxc.x + t[1] * rxc.y + t[2] * rxc.z, t[4] * rxc.x + t[5] * rxc.y + t[6] * rxc.z,
                                       t[8] * rxc.x + t[9] * rxc.y + t[10] * rxc.z);
@@ -1400,17 +1423,19 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
                                       t[8] * ryc.x + t[9] * ryc.y + t[10] * ryc.z);
                 const float scale = 1.0f / sqrtf((float)I.spp);
                 const float3 rxs = wd + (rx - wd) * scale, rys = wd + (ry - wd) * scale;
-                stS(&P.sh_o[slot], make_float4(rxs.x, rxs.y, rxs.z, 0.f));
-                stS(&P.sh_d[slot], make_float4(rys.x, rys.y, rys.z, 0.f));
+                // parked in T and aux (throughput 1, no previous vertex) until
+                // bounce 0 is shaded
+                stS(&P.T[slot], make_float4(rxs.x, rxs.y, rxs.z, 1.f));
+                stS(&P.aux[slot], make_float4(rys.x, rys.y, rys.z, 0.f));
+            } else {
+                stS(&P.T[slot], make_float4(1.f, 1.f, 1.f, 1.f));
             }
-            stS(&P.L[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
-            stS(&P.T[slot], make_float4(1.f, 1.f, 1.f, 1.f));
-            stS(&P.key[slot], make_uint2((uint32_t)key, (uint32_t)(key >> 32)));
-            stS(&P.st[slot], make_uint2(1u, 2u));   // depth 1, next dimension 2
+            stS(&P.Lp[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
+            stS(&P.meta[slot], make_uint4(1u, 2u, slot, 0u));   // depth 1, next dimension 2
         } else {
-            // dead slot: bounce 0 runs over the identity queue and skips it
+            // dead slot: bounce 0 runs over all slots and skips it
             stS(&P.ray_d[slot], make_float4(0.f, 0.f, 1.f, -1.0f));
-            stS(&P.st[slot], make_uint2(0u, 0u));
+            stS(&P.meta[slot], make_uint4(0u, 0u, slot, 0u));
             stS(&P.L[slot], make_float4(0.f, 0.f, 0.f, 0.f));
         }
     }
@@ -1826,6 +1851,13 @@ DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p
     i1 = ba.base[1] + w1 + (uint32_t)__popcll(m1 & below);
 }
 
+// outgoing records of one workgroup (36 KB: 4 workgroups per CU at 4 waves/SIMD)
+struct ShadeStage {
+    float4 o[BLOCK], d[BLOCK], T[BLOCK], aux[BLOCK], L[BLOCK];
+    uint4 meta[BLOCK];
+    float4 sho[BLOCK], shd[BLOCK], shc[BLOCK];
+};
+
 // qin < 0: bounce 0 over the identity queue of nIdentity slots
 #ifndef MTSG_SHADE_WAVES
 #define MTSG_SHADE_WAVES 4   // 127 VGPRs: 4 waves/SIMD (3 at 144; 5+ spill heavily)
@@ -1838,9 +1870,10 @@ DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p
 // ENV: the scene has an environment emitter (the variant without it keeps
 // the environment code, and its registers, out of the common case)
 template <bool ENV>
-__global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int bounce, int qin,
+__global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int bounce, int qin,
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
+    __shared__ ShadeStage stage;
     uint32_t count = nIdentity;
     if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     const uint32_t nIter = (count + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
@@ -1849,25 +1882,30 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
         const uint32_t i = (it * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
         bool alive = i < count;
         bool cont = false, shadow = false;
-        uint32_t slot = 0;
+        uint4 meta = make_uint4(0u, 0u, 0u, 0u);
         if (alive) {
-            slot = qin < 0 ? i : P.q[qin][i];
-            if (qin < 0 && ldS(&P.st[slot]).x == 0u) alive = false;   // dead slot
+            meta = ldS(&P.meta[i]);
+            if (meta.x == 0u) alive = false;   // dead slot (bounce 0)
         }
+        const uint32_t slot = meta.z;
         if (alive) {
-            const float4 h = ldS(&P.hit[slot]);
-            const float4 ro4 = ldS(&P.ray_o[slot]), rd4 = ldS(&P.ray_d[slot]);
+            const float4 h = ldS(&P.hit[i]);
+            const float4 ro4 = ldS(&P.ray_o[i]), rd4 = ldS(&P.ray_d[i]);
             const float3 ro = xyz(ro4), rd = xyz(rd4);
-            float4 L4 = ldS(&P.L[slot]);
-            float4 T4 = ldS(&P.T[slot]);
-            uint2 st = ldS(&P.st[slot]);
-            const uint2 kk = ldS(&P.key[slot]);
-            const uint64_t key = (uint64_t)kk.x | ((uint64_t)kk.y << 32);
+            float4 L4 = ldS(&P.Lp[i]);
+            float4 T4 = ldS(&P.T[i]);
+            uint64_t key;
+            {
+                int x, y;
+                uint32_t sIdx;
+                slot_pixel(B, slot, x, y, sIdx);
+                key = counterKey(I.seed, ((uint64_t)y * (uint64_t)I.film_w + (uint64_t)x) * I.spp + sIdx);
+            }
             float3 L = xyz(L4), T = xyz(T4);
             float eta = T4.w;
-            uint32_t depth = st.x & 0xFFFFu;
-            uint32_t flags = st.x & 0xFFFF0000u;
-            uint32_t dim = st.y;
+            uint32_t depth = meta.x & 0xFFFFu;
+            uint32_t flags = meta.x & 0xFFFF0000u;
+            uint32_t dim = meta.y;
             const bool valid = __float_as_uint(h.w) != 0xFFFFFFFFu;
             bool done = false;
             Its its;
@@ -1878,11 +1916,12 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
                 if (!valid) {
                     // Scene::evalEnvironment of the differential camera ray (path.cpp:136-143)
                     if (ENV && !I.hide_emitters) {
-                        const float3 rxd = xyz(ldS(&P.sh_o[slot])), ryd = xyz(ldS(&P.sh_d[slot]));
-                        L += T * env_eval(S.env, rd, true, rxd, ryd);
+                        const float3 rxd = T, ryd = xyz(ldS(&P.aux[i]));
+                        L += env_eval(S.env, rd, true, rxd, ryd);   // throughput 1
                     }
                     done = true;
                 }
+                if (ENV) T = mk3(1.f, 1.f, 1.f);   // T held the x-differential
             } else {
                 // tail of the previous iteration after scene->rayIntersect (path.cpp:226-286)
                 if (!valid) {
@@ -1895,7 +1934,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
                             if (!(flags & F_DELTA))   // Scene::pdfEmitterDirect -> EnvironmentMap::pdfDirect
                                 lumPdf = env_internal_pdf(S.env, env_rot(S.env.E->to_local, rd)) *
                                          S.emitters[S.env.E->emitter].pdf_discrete;
-                            L += T * value * mis(ldS(&P.aux[slot]).w, lumPdf);
+                            L += T * value * mis(ldS(&P.aux[i]).w, lumPdf);
                         }
                     }
                     done = true;
@@ -1907,13 +1946,13 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
                         float lumPdf = 0.0f;
                         if (!(flags & F_DELTA)) {
                             // Scene::pdfEmitterDirect with dRec.setQuery(ray, its)
-                            const float4 ax = ldS(&P.aux[slot]);
+                            const float4 ax = ldS(&P.aux[i]);
                             const float3 refN = xyz(ax);
                             if (dot(rd, refN) >= 0 && dot(rd, its.sh.n) < 0)
                                 lumPdf = E.inv_area * (h.x * h.x) / fabsf(dot(rd, its.sh.n));
                             lumPdf *= E.pdf_discrete;
                         }
-                        L += T * value * mis(ldS(&P.aux[slot]).w, lumPdf);
+                        L += T * value * mis(ldS(&P.aux[i]).w, lumPdf);
                     }
                     if (depth++ >= (uint32_t)I.rr_depth) {
                         float q = fminf(maxc(T) * eta * eta, 0.95f);
@@ -1968,9 +2007,9 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
                                 const float3 c = T * value * bval * weight;
                                 if (!isZero(c)) {
                                     shadow = true;
-                                    stS(&P.sh_o[slot], make_float4(its.p.x, its.p.y, its.p.z, dist * (1 - kShadowEpsilon)));
-                                    stS(&P.sh_d[slot], make_float4(dd.x, dd.y, dd.z, 0.f));
-                                    stS(&P.sh_c[slot], make_float4(c.x, c.y, c.z, 0.f));
+                                    stage.sho[threadIdx.x] = make_float4(its.p.x, its.p.y, its.p.z, dist * (1 - kShadowEpsilon));
+                                    stage.shd[threadIdx.x] = make_float4(dd.x, dd.y, dd.z, kEpsilon);
+                                    stage.shc[threadIdx.x] = make_float4(c.x, c.y, c.z, 0.f);
                                 }
                             }
                         }
@@ -1989,24 +2028,45 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevPaths P, int 
                             T = T * bs.weight;
                             eta *= bs.eta;
                             flags = bs.delta ? (flags | F_DELTA) : (flags & ~F_DELTA);
-                            stS(&P.ray_o[slot], make_float4(its.p.x, its.p.y, its.p.z, kEpsilon));
-                            stS(&P.ray_d[slot], make_float4(wo.x, wo.y, wo.z, INFINITY));
-                            stS(&P.aux[slot], make_float4(refN.x, refN.y, refN.z, bs.pdf));
+                            stage.o[threadIdx.x] = make_float4(its.p.x, its.p.y, its.p.z, kEpsilon);
+                            stage.d[threadIdx.x] = make_float4(wo.x, wo.y, wo.z, INFINITY);
+                            stage.aux[threadIdx.x] = make_float4(refN.x, refN.y, refN.z, bs.pdf);
                             cont = true;
                         }
                     }
                 }
             }
-            stS(&P.L[slot], make_float4(L.x, L.y, L.z, L4.w));
+            const float4 finalL = make_float4(L.x, L.y, L.z, L4.w);
             if (cont) {
-                stS(&P.T[slot], make_float4(T.x, T.y, T.z, eta));
-                stS(&P.st[slot], make_uint2(depth | flags, dim));
+                stage.T[threadIdx.x] = make_float4(T.x, T.y, T.z, eta);
+                stage.L[threadIdx.x] = finalL;
+                stage.meta[threadIdx.x] = make_uint4(depth | flags, dim, slot, 0u);
+            } else {
+                stS(&P.L[slot], finalL);   // path ended: its sample's final radiance
             }
         }
+        // The output positions come from the workgroup-aggregated append; the
+        // outgoing records wait for it in LDS (lane-private rows) rather than
+        // in registers live across its barriers.
+        const int tid = threadIdx.x;
         uint32_t is, ic;
         block_append2(ba, &P.cnt[CNT_S], &P.cnt[cnt_q(qout)], shadow, cont, is, ic);
-        if (shadow) P.qs[is] = slot;
-        if (cont) P.q[qout][ic] = slot;
+        if (cont) {
+            // survivor: compacted into the next bounce's arrays
+            stS(&P.n_ray_o[ic], stage.o[tid]);
+            stS(&P.n_ray_d[ic], stage.d[tid]);
+            stS(&P.n_T[ic], stage.T[tid]);
+            stS(&P.n_aux[ic], stage.aux[tid]);
+            stS(&P.n_Lp[ic], stage.L[tid]);
+            stS(&P.n_meta[ic], stage.meta[tid]);
+        }
+        if (shadow) {
+            float4 c = stage.shc[tid];
+            c.w = __uint_as_float(cont ? ic : (0x80000000u | slot));
+            stS(&P.sh_o[is], stage.sho[tid]);
+            stS(&P.sh_d[is], stage.shd[tid]);
+            stS(&P.sh_c[is], c);
+        }
     }
 }
 
@@ -2030,7 +2090,7 @@ constexpr int SPLAT_CHUNK = 16;             // samples per pixel per workgroup
 // same texel: no atomics, fixed order) and flushes the tile with one float
 // atomic per texel and channel into the HBM ImageBlock.
 template <int K, int CH>
-__global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevBatch B, DevPaths P, float *film, int blockW, int blockH) {
+__global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P, float *film, int blockW, int blockH) {
     __shared__ float acc[CH][LT * LT];
     constexpr int R = K / 2;
     for (int k = threadIdx.x; k < CH * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
@@ -2057,8 +2117,7 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevBatch B, DevPat
         for (uint32_t sl = sBeg; sl < sEnd; ++sl) {
             const uint32_t slot = ((uint32_t)tl * B.ns + sl) * (TILE * TILE) + pix;
             const float4 L = ldS(&P.L[slot]);
-            const uint2 kk = ldS(&P.key[slot]);
-            const uint64_t key = (uint64_t)kk.x | ((uint64_t)kk.y << 32);
+            const uint64_t key = counterKey(I.seed, ((uint64_t)y * (uint64_t)I.film_w + (uint64_t)x) * I.spp + B.s0 + sl);
             // invalid samples are rejected (imageblock.h:147-151)
             if (!(isfinite(L.x) && isfinite(L.y) && isfinite(L.z) && L.x >= 0 && L.y >= 0 && L.z >= 0)) continue;
             // sample position relative to the window origin, as ImageBlock::put
@@ -2197,9 +2256,9 @@ int ensure_batch(mtsg_scene *s, uint32_t paths) {
     DevPaths &P = s->P;
     int rc = MTSG_OK;
 #define A(field, T) if ((rc = alloc(n * sizeof(T), (void **)&P.field)) != MTSG_OK) return rc
-    A(ray_o, float4); A(ray_d, float4); A(hit, float4); A(L, float4); A(T, float4); A(aux, float4);
-    A(key, uint2); A(st, uint2); A(sh_o, float4); A(sh_d, float4); A(sh_c, float4);
-    A(q[0], uint32_t); A(q[1], uint32_t); A(qs, uint32_t);
+    A(ray_o, float4); A(ray_d, float4); A(T, float4); A(aux, float4); A(Lp, float4); A(meta, uint4);
+    A(n_ray_o, float4); A(n_ray_d, float4); A(n_T, float4); A(n_aux, float4); A(n_Lp, float4); A(n_meta, uint4);
+    A(hit, float4); A(L, float4); A(sh_o, float4); A(sh_d, float4); A(sh_c, float4);
 #undef A
     if ((rc = alloc(CNT_WORDS * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
     if ((rc = alloc(16 * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
@@ -2209,6 +2268,16 @@ int ensure_batch(mtsg_scene *s, uint32_t paths) {
 }
 
 enum { K_CAMERA = 0, K_CLOSEST, K_SHADOW, K_SHADE, K_SPLAT };
+
+// the survivors k_shade compacted into n_* are the next bounce's paths
+void swap_bounce(DevPaths &P) {
+    std::swap(P.ray_o, P.n_ray_o);
+    std::swap(P.ray_d, P.n_ray_d);
+    std::swap(P.T, P.n_T);
+    std::swap(P.aux, P.n_aux);
+    std::swap(P.Lp, P.n_Lp);
+    std::swap(P.meta, P.n_meta);
+}
 
 hipEvent_t next_event(mtsg_scene *s) {
     if (s->evUsed == s->evPool.size()) {
@@ -2314,7 +2383,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     const uint32_t tilesPerBatch = std::max(1u, (ntiles + nTileBatches - 1) / nTileBatches);
     if ((rc = ensure_batch(s, tilesPerBatch * sppPerBatch * TILE * TILE)) != MTSG_OK) return rc;
     const int blockW = p->tile_w + 2 * s->cam.border, blockH = p->tile_h + 2 * s->cam.border;
-    DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed};
+    DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed, (uint32_t)s->cam.film_w};
     memset(&s->stats, 0, sizeof(s->stats));
     s->evUsed = 0;
     s->timed.clear();
@@ -2361,11 +2430,12 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 timed_launch(s, K_CLOSEST, [&]() { launch_trace<false>(s, count, P, qin, B.nslots); });
                 timed_launch(s, K_SHADE, [&]() {
                     if (s->ds.has_env)
-                        hipLaunchKernelGGL(k_shade<true>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, P, b, qin, B.nslots, s->cam.has_alpha);
+                        hipLaunchKernelGGL(k_shade<true>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
                     else
-                        hipLaunchKernelGGL(k_shade<false>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, P, b, qin, B.nslots, s->cam.has_alpha);
+                        hipLaunchKernelGGL(k_shade<false>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
                 });
                 timed_launch(s, K_SHADOW, [&]() { launch_trace<true>(s, count, P, 0, 0u); });
+                swap_bounce(P);
                 HIP_TRY(hipMemcpyAsync(s->hostCnt + HOSTCNT_STRIDE * (b & 1), P.cnt, (CNT_S + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
                 HIP_TRY(hipEventRecord(cntEv[b & 1], s->stream));
                 last = b;
@@ -2382,12 +2452,12 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             timed_launch(s, K_SPLAT, [&]() {
                 dim3 g(B.ntiles, (B.ns + SPLAT_CHUNK - 1) / SPLAT_CHUNK);
                 const int K = 2 * s->cam.border + 1;
-                if (K == 5 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<5, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
-                else if (K == 5) hipLaunchKernelGGL((k_splat<5, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
-                else if (K <= 3 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<3, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
-                else if (K <= 3) hipLaunchKernelGGL((k_splat<3, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
-                else if (!s->cam.has_alpha) hipLaunchKernelGGL((k_splat<9, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
-                else hipLaunchKernelGGL((k_splat<9, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, B, P, film, blockW, blockH);
+                if (K == 5 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<5, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
+                else if (K == 5) hipLaunchKernelGGL((k_splat<5, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
+                else if (K <= 3 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<3, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
+                else if (K <= 3) hipLaunchKernelGGL((k_splat<3, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
+                else if (!s->cam.has_alpha) hipLaunchKernelGGL((k_splat<9, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
+                else hipLaunchKernelGGL((k_splat<9, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
             });
             s->stats.samples += (uint64_t)B.nslots;
             if (s->dumpL) {
@@ -2758,40 +2828,72 @@ int mtsg_render_samples(mtsg_scene *s, const mtsg_render_params *p, float *L_out
     return rc;
 }
 
+// Ray queries run the production traversal kernel (the one the integrator
+// launches, selected by traceMode) over a work list of n rays.
 static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, float *u, float *v, uint32_t *prim,
                       uint8_t *occ, bool shadow) {
     if (!s || (!rays && n)) return MTSG_ERR_INVALID;
     if (n == 0) return MTSG_OK;
     int rc;
     if ((rc = set_device(s)) != MTSG_OK) return rc;
-    float *dr = nullptr, *dt = nullptr, *du = nullptr, *dv = nullptr;
-    uint32_t *dp = nullptr;
-    uint8_t *docc = nullptr;
-    auto cleanup = [&]() { hipFree(dr); hipFree(dt); hipFree(du); hipFree(dv); hipFree(dp); hipFree(docc); };
-    hipError_t e = hipMalloc((void **)&dr, (size_t)n * 8 * sizeof(float));
-    if (e == hipSuccess) e = hipMemcpy(dr, rays, (size_t)n * 8 * sizeof(float), hipMemcpyHostToDevice);
-    if (e == hipSuccess && !shadow) e = hipMalloc((void **)&dt, n * sizeof(float));
-    if (e == hipSuccess && !shadow) e = hipMalloc((void **)&du, n * sizeof(float));
-    if (e == hipSuccess && !shadow) e = hipMalloc((void **)&dv, n * sizeof(float));
-    if (e == hipSuccess && !shadow) e = hipMalloc((void **)&dp, n * sizeof(uint32_t));
-    if (e == hipSuccess && shadow) e = hipMalloc((void **)&docc, n);
-    if (e != hipSuccess) { g_err = hipGetErrorString(e); cleanup(); return MTSG_ERR_DEVICE; }
-    dim3 grid((n + TRACE_BLOCK - 1) / TRACE_BLOCK);
-    if (shadow) hipLaunchKernelGGL(k_trace_rays<true>, grid, dim3(TRACE_BLOCK), 0, s->stream, s->ds, dr, n, dt, du, dv, dp, docc);
-    else hipLaunchKernelGGL(k_trace_rays<false>, grid, dim3(TRACE_BLOCK), 0, s->stream, s->ds, dr, n, dt, du, dv, dp, docc);
-    e = hipStreamSynchronize(s->stream);
-    if (e == hipSuccess) e = hipGetLastError();
-    if (e == hipSuccess) {
-        if (shadow) e = hipMemcpy(occ, docc, n, hipMemcpyDeviceToHost);
-        else {
-            e = hipMemcpy(t, dt, n * sizeof(float), hipMemcpyDeviceToHost);
-            if (e == hipSuccess) e = hipMemcpy(u, du, n * sizeof(float), hipMemcpyDeviceToHost);
-            if (e == hipSuccess) e = hipMemcpy(v, dv, n * sizeof(float), hipMemcpyDeviceToHost);
-            if (e == hipSuccess) e = hipMemcpy(prim, dp, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    std::vector<float4> a(n), b(n), c(shadow ? n : 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        const float *r = rays + 8 * (size_t)i;   // o.xyz, d.xyz, mint, maxt
+        if (shadow) {
+            a[i] = make_float4(r[0], r[1], r[2], r[7]);
+            b[i] = make_float4(r[3], r[4], r[5], r[6]);
+            uint32_t tgt = 0x80000000u | i;
+            float ft;
+            memcpy(&ft, &tgt, 4);
+            c[i] = make_float4(1.f, 0.f, 0.f, ft);   // unoccluded -> L[i].x = 1
+        } else {
+            a[i] = make_float4(r[0], r[1], r[2], r[6]);
+            b[i] = make_float4(r[3], r[4], r[5], r[7]);
         }
     }
+    std::vector<float4> out(n, make_float4(INFINITY, 0.f, 0.f, 0.f));
+    if (!shadow) {
+        const uint32_t miss = 0xFFFFFFFFu;
+        for (auto &o : out) memcpy(&o.w, &miss, 4);
+    } else {
+        for (auto &o : out) o = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    DevPaths D{};
+    std::vector<void *> mem;
+    auto cleanup = [&]() { for (void *m : mem) hipFree(m); };
+    const size_t f4 = (size_t)n * sizeof(float4);
+    auto alloc = [&](void **ptr, size_t bytes, const void *src) -> hipError_t {
+        hipError_t e = hipMalloc(ptr, bytes);
+        if (e != hipSuccess) return e;
+        mem.push_back(*ptr);
+        return src ? hipMemcpy(*ptr, src, bytes, hipMemcpyHostToDevice) : hipMemset(*ptr, 0, bytes);
+    };
+    float4 **pa = shadow ? &D.sh_o : &D.ray_o, **pb = shadow ? &D.sh_d : &D.ray_d, **po = shadow ? &D.L : &D.hit;
+    hipError_t e = alloc((void **)pa, f4, a.data());
+    if (e == hipSuccess) e = alloc((void **)pb, f4, b.data());
+    if (e == hipSuccess) e = alloc((void **)po, f4, out.data());
+    if (e == hipSuccess && shadow) e = alloc((void **)&D.sh_c, f4, c.data());
+    if (e == hipSuccess) e = alloc((void **)&D.cnt, CNT_WORDS * sizeof(uint32_t), nullptr);
+    if (e == hipSuccess) e = alloc((void **)&D.ctr, 16 * sizeof(unsigned long long), nullptr);
+    if (e == hipSuccess && shadow) e = hipMemcpy(D.cnt + CNT_S, &n, sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { g_err = hipGetErrorString(e); cleanup(); return MTSG_ERR_DEVICE; }
+    if (shadow) launch_trace<true>(s, false, D, 0, 0u);
+    else launch_trace<false>(s, false, D, -1, n);
+    e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out.data(), *po, f4, hipMemcpyDeviceToHost);
     cleanup();
     if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    for (uint32_t i = 0; i < n; ++i) {
+        if (shadow) {
+            occ[i] = out[i].x == 0.f ? 1 : 0;
+        } else {
+            uint32_t pb2;
+            memcpy(&pb2, &out[i].w, 4);
+            prim[i] = pb2;   // triangle index, 0x80000000 | rectangle index, or ~0 (miss)
+            t[i] = out[i].x; u[i] = out[i].y; v[i] = out[i].z;
+        }
+    }
     return MTSG_OK;
 }
 
