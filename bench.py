@@ -29,7 +29,7 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-TRAFFIC_KERNEL = "k_trace_s<false, false, 16>"
+TRAFFIC_KERNEL = "k_trace_s<false, 16>"
 
 
 def pmc_traffic(workload):
@@ -161,29 +161,36 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    # per-kernel HIP events on the library's stream stay on through the timed
+    # steps (two event records per launch); the per-frame figures are summed
+    gpu.set_flags(mtsg.MTSG_FLAG_TIMING)
+    acc = {}
     barrier(pg)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+        st = gpu.stats()
+        for f in ("ms_trace_closest", "ms_trace_shadow", "ms_shade", "ms_camera", "ms_splat", "ms_total",
+                  "rays_closest", "rays_shadow", "launches_trace_closest", "launches_trace_shadow"):
+            acc[f] = acc.get(f, 0) + getattr(st, f)
     barrier(pg)
     elapsed = max_over_ranks(pg, time.perf_counter() - t0)
+    gpu.set_flags(0)
     samples_total = params.tile_w * params.tile_h * params.spp * a.steps
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
 
-    # ---- per-kernel timing (HIP events on the library's stream) and the
-    # instrumented traversal for algorithmic bytes; separate, untimed passes
+    # ---- roofline of the traversal kernel: HIP-event times of the timed
+    # steps, algorithmic work from an instrumented (untimed) pass
     roofline = None
     kernels = {}
     if rank == 0:
-        gpu.set_flags(mtsg.MTSG_FLAG_TIMING)
-        mtsg.device_lib().mtsg_device_memset(gpu._h, film, nbytes)
-        gpu.render_device(params, film)
-        st = gpu.stats()
-        kernels = {"trace_closest_ms": st.ms_trace_closest, "trace_shadow_ms": st.ms_trace_shadow,
-                   "shade_ms": st.ms_shade, "camera_ms": st.ms_camera, "splat_ms": st.ms_splat,
-                   "frame_ms": st.ms_total, "closest_rays": st.rays_closest, "shadow_rays": st.rays_shadow,
-                   "closest_launches": st.launches_trace_closest}
+        k = a.steps
+        kernels = {"trace_ms": (acc["ms_trace_closest"] + acc["ms_trace_shadow"]) / k,
+                   "shade_ms": acc["ms_shade"] / k, "camera_ms": acc["ms_camera"] / k, "splat_ms": acc["ms_splat"] / k,
+                   "frame_ms": acc["ms_total"] / k, "closest_rays": acc["rays_closest"] // k,
+                   "shadow_rays": acc["rays_shadow"] // k,
+                   "trace_launches": (acc["launches_trace_closest"] + acc["launches_trace_shadow"]) // k}
         # instrumented pass at reduced spp (per-ray counts are spp-independent)
         pc = params.copy()
         pc.spp = max(1, min(params.spp, 16))
@@ -192,20 +199,21 @@ def main():
         gpu.render_device(pc, film)
         cs = gpu.stats()
         gpu.set_flags(0)
-        rays_c = cs.rays_closest
-        nodes_per_ray = cs.nodes_visited / max(1, rays_c)
-        refs_per_ray = cs.leaf_refs / max(1, rays_c)
-        tests_per_ray = cs.tri_tests / max(1, rays_c)
-        # Algorithmic bytes per closest-hit ray in the device layout (DESIGN.md
-        # "Roofline"): one 16-B sibling-pair load per inner node descended, one
-        # 48-B TriAccel record per primitive test (leaf-ordered, no index
-        # indirection), the 32-B ray record in, the 16-B hit out, the 4-B queue
-        # entry.  (SURVEY §8d's Mitsuba-layout figure, 8 B/node + 4 B/ref +
-        # 48 B/test, is reported beside it as bytes_per_ray_mitsuba_layout.)
-        b_ray = 16 * nodes_per_ray + 48 * tests_per_ray + 32 + 16 + 4
-        launches = max(1, st.launches_trace_closest)
-        bytes_per_launch = b_ray * st.rays_closest / launches
-        avg_launch_s = st.ms_trace_closest / 1e3 / launches
+        per = lambda v, n: v / max(1, n)  # noqa: E731
+        nodes_c, tests_c = per(cs.nodes_visited, cs.rays_closest), per(cs.tri_tests, cs.rays_closest)
+        nodes_s, tests_s = per(cs.shadow_nodes_visited, cs.rays_shadow), per(cs.shadow_tri_tests, cs.rays_shadow)
+        # Algorithmic bytes per ray in the device layout (DESIGN.md "Roofline"):
+        # 16 B of node pair per inner node descended, one 48-B TriAccel record
+        # per primitive test (leaf-ordered, no index indirection), the 32-B ray
+        # record in, and 16 B out (closest: the hit record; shadow: the 16-B
+        # contribution record read when unoccluded, counted for every ray).
+        b_c = 16 * nodes_c + 48 * tests_c + 48
+        b_s = 16 * nodes_s + 48 * tests_s + 48
+        launches = max(1, acc["launches_trace_closest"] + acc["launches_trace_shadow"])
+        trace_s = (acc["ms_trace_closest"] + acc["ms_trace_shadow"]) / 1e3
+        bytes_total = b_c * acc["rays_closest"] + b_s * acc["rays_shadow"]
+        bytes_per_launch = bytes_total / launches
+        avg_launch_s = trace_s / launches
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         tj, tsrc = pmc_traffic(a.workload)
         traffic = None
@@ -216,15 +224,16 @@ def main():
                     "traffic_source": (f"{tsrc}: FETCH_SIZE x2 + WRITE_SIZE per launch "
                                        f"({tj['traffic_bytes_per_launch'] / 1e9:.2f} GB) / this run's avg launch time"
                                        if traffic is not None else None),
-                    "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                    "kernel": "k_trace_s<closest>", "bytes_per_ray": round(b_ray, 1),
-                    "nodes_per_ray": round(nodes_per_ray, 2), "leaf_refs_per_ray": round(refs_per_ray, 2),
-                    "tri_tests_per_ray": round(tests_per_ray, 2), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                    "launches_per_frame": launches,
+                    "kernel": "k_trace_s (closest + shadow rays)",
+                    "algorithmic_bytes_per_launch": round(bytes_per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                    "launches_per_frame": launches // a.steps,
+                    "bytes_per_closest_ray": round(b_c, 1), "bytes_per_shadow_ray": round(b_s, 1),
+                    "nodes_per_closest_ray": round(nodes_c, 2), "tests_per_closest_ray": round(tests_c, 2),
+                    "nodes_per_shadow_ray": round(nodes_s, 2), "tests_per_shadow_ray": round(tests_s, 2),
                     # SIMD efficiency of the traversal waves (instrumented pass)
-                    "simd_active_lanes": round(cs.wave_active_lanes / max(1, 64 * cs.wave_steps), 3),
-                    "simd_eff_inner": round(cs.nodes_visited / max(1, 64 * cs.wave_node_iters), 3),
-                    "simd_eff_leaf": round(cs.tri_tests / max(1, 64 * cs.wave_test_iters), 3)}
+                    "simd_active_lanes": round(per(cs.wave_active_lanes, 64 * cs.wave_steps), 3),
+                    "simd_eff_inner": round(per(cs.nodes_visited + cs.shadow_nodes_visited, 64 * cs.wave_node_iters), 3),
+                    "simd_eff_leaf": round(per(cs.tri_tests + cs.shadow_tri_tests, 64 * cs.wave_test_iters), 3)}
         if a.save:
             img = mtsg.develop(host_block[border:H - border, border:W - border])
             np.save(a.save, img)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MTSG_ABI_VERSION 2
+#define MTSG_ABI_VERSION 3
 
 /* ---- error codes (mtsg_last_error() gives the message) ------------------ */
 enum {
@@ -236,7 +236,11 @@ typedef struct mtsg_render_params {
 /* Statistics of the last render call on a handle. */
 typedef struct mtsg_stats {
     double ms_total;              /* wall time of the render call           */
-    double ms_trace_closest;      /* summed kernel time (HIP events)        */
+    /* summed kernel times (HIP events).  A trace launch traces one bounce's
+     * closest-hit rays together with the previous bounce's shadow rays:
+     * ms_trace_closest sums those launches (launches_trace_closest of them),
+     * ms_trace_shadow the final shadow-only launch of each batch.           */
+    double ms_trace_closest;
     double ms_trace_shadow;
     double ms_shade;
     double ms_camera;
@@ -253,12 +257,14 @@ typedef struct mtsg_stats {
     uint64_t shadow_nodes_visited;
     uint64_t shadow_leaf_refs;
     uint64_t shadow_tri_tests;
-    /* SIMD efficiency of the persistent traversal kernels (MTSG_FLAG_COUNT,
-     * refill modes 2-4): per wave, max-over-lanes inner-node and primitive
-     * iterations, traversal steps, and active lanes summed over steps.
-     * efficiency = nodes_visited / (64 * wave_node_iters), etc. */
+    /* SIMD efficiency of the persistent traversal kernel (MTSG_FLAG_COUNT):
+     * per wave, max-over-lanes inner-node and primitive iterations,
+     * traversal steps, and active lanes summed over steps, over waves of
+     * both ray kinds (booked in the wave_* fields; shadow_wave_* stay 0).
+     * efficiency = (nodes_visited + shadow_nodes_visited) / (64 * wave_node_iters), etc. */
     uint64_t wave_node_iters, wave_test_iters, wave_steps, wave_active_lanes;
     uint64_t shadow_wave_node_iters, shadow_wave_test_iters, shadow_wave_steps, shadow_wave_active_lanes;
+    uint64_t launches_trace_shadow;   /* shadow-only trace launches (one per batch) */
 } mtsg_stats;
 
 enum {

@@ -42,30 +42,19 @@ namespace {
 // device-side scene and path state
 // ---------------------------------------------------------------------------
 struct DevScene {
-    // device kd-tree layout (built from Mitsuba's KDNode array at upload):
-    //   node (8 B)  inner: axis | pairIndex << 2, split  /  leaf: 1<<31 | start, end
-    //   pairs[k]    = {left child node, right child node} -> one 16 B load per step
-    //   triL        = TriAccel records copied in leaf order (3 float4 each)
-    const uint4 *__restrict__ pairs;
-    const float4 *__restrict__ triL;
-    uint2 root;
-    // compact alternative (MTSG_LEAF_MODE=1): leaves index Mitsuba's primitive
-    // index list, TriAccel records are read in primitive order from `tri`
-    const uint4 *__restrict__ pairsIdx;
-    const uint32_t *__restrict__ lidx;
-    uint2 rootIdx;
-    // two-level blocks (MTSG_TRACE_MODE 12-13): a block root's 64-B block holds
-    // {children pair, left child's pair, right child's pair, pad}, so one
-    // fetch descends two levels.  Node words: leaf as above; block root
-    // axis | blockIndex << 3; pair-only node (odd level) axis | 4 | slot << 3
-    // with slot = 4 * block + 1|2 (uint4 units).
+    // device kd-tree (built from Mitsuba's KDNode array at upload: same splits
+    // and leaves, re-laid out as two-level blocks).  A block root's 64-B block
+    // holds {children pair, left child's pair, right child's pair, pad}, so one
+    // fetch descends two levels.  Node words (8 B):
+    //   leaf            1 << 31 | start, end   (range of triL records)
+    //   block root      axis | block << 3, split
+    //   pair-only node  axis | 4 | slot << 3, split  (slot = 4 * block + 1|2, uint4 units)
     const uint4 *__restrict__ blocks;
     uint2 root2;
-    const float4 *__restrict__ tri;        // 3 float4 per prim (TriAccel, prim order)
+    const float4 *__restrict__ triL;       // TriAccel records in leaf order (3 float4 each)
     const float4 *__restrict__ vpos;       // xyz
     const float4 *__restrict__ vnrm;       // xyz
     const uint4 *__restrict__ tidx;        // i0, i1, i2, shape
-    const float4 *__restrict__ tdpdu;      // dpdu xyz
     // per-triangle shading record, 6 float4 (96 B, one contiguous fetch per hit):
     //   p0 p1 p2 | n0 n1 n2 | dpdu | shape, bsdf | faceNormals << 31, emitter
     const float4 *__restrict__ shrec;
@@ -140,11 +129,13 @@ struct DevPaths {
 // contended address serialises at ~11 ns per atomic (MI355X_MICROARCH.md,
 // row "dequeue"), and counters sharing a line would serialise together
 constexpr int XGROUPS = 8;                  // XCDs: blocks b and b + 8 share one
-constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S = 128;
-constexpr int CNT_FETCH = 192;                           // XGROUPS counters, 32 words apart
-constexpr int CNT_SFETCH = CNT_FETCH + 32 * XGROUPS;     // XGROUPS counters, 32 words apart
-constexpr int CNT_WORDS = CNT_SFETCH + 32 * XGROUPS;
-constexpr int HOSTCNT_STRIDE = 192;
+// Q0/Q1: paths of the next bounce (ping-pong); S0/S1: shadow rays of a bounce
+// (ping-pong: bounce b appends to S(b & 1) while its trace reads S((b-1) & 1))
+constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S0 = 128, CNT_S1 = 192;
+constexpr int CNT_FETCH = 256;                           // XGROUPS counters, 32 words apart
+constexpr int CNT_WORDS = CNT_FETCH + 32 * XGROUPS;
+constexpr int HOSTCNT_STRIDE = 256;
+__host__ __device__ constexpr int cnt_s(int k) { return k ? CNT_S1 : CNT_S0; }
 DEV int cnt_q(int q) { return q ? CNT_Q1 : CNT_Q0; }
 
 constexpr int TILE = 16;                    // splat tile edge (256 pixels)
@@ -162,22 +153,11 @@ constexpr size_t PATH_STATE_BYTES = 272;    // bytes per path slot (DevPaths: 2 
 #define MTSG_SHORT_STACK 6   // 6 x 12 B x 64 lanes = 4.6 KB LDS/wave -> 8 waves/SIMD (8: 6.5, 12: 4.2)
 #endif
 constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per lane
-#ifndef MTSG_LEAF_PREFETCH
-#define MTSG_LEAF_PREFETCH 0
-#endif
-#ifndef MTSG_TRACE_WAVES
-#define MTSG_TRACE_WAVES 0
-#endif
 // the compact speculative traversal is sized for 8 waves per SIMD (64 VGPRs)
 #ifndef MTSG_SPEC_WAVES
 #define MTSG_SPEC_WAVES 8
 #endif
 #define SPEC_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SPEC_WAVES)))
-#if MTSG_TRACE_WAVES > 0
-#define TRACE_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_TRACE_WAVES)))
-#else
-#define TRACE_ATTR __launch_bounds__(TRACE_BLOCK)
-#endif
 // streaming (non-temporal) access to the per-path SoA state: the state of a
 // 32M-path batch is GBs per bounce and would otherwise evict the kd-tree from
 // the 256 MB Infinity Cache (experiment switch MTSG_NT)
@@ -185,19 +165,10 @@ constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per l
 #define MTSG_NT 1
 #endif
 typedef float nf4 __attribute__((ext_vector_type(4)));
-typedef uint32_t nu2 __attribute__((ext_vector_type(2)));
 DEV float4 ldS(const float4 *p) {
 #if MTSG_NT
     const nf4 v = __builtin_nontemporal_load((const nf4 *)p);
     return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-DEV uint2 ldS(const uint2 *p) {
-#if MTSG_NT
-    const nu2 v = __builtin_nontemporal_load((const nu2 *)p);
-    return make_uint2(v.x, v.y);
 #else
     return *p;
 #endif
@@ -225,13 +196,6 @@ DEV void stS(uint4 *p, const uint4 &v) {
     *p = v;
 #endif
 }
-DEV void stS(uint2 *p, const uint2 &v) {
-#if MTSG_NT
-    __builtin_nontemporal_store((nu2){v.x, v.y}, (nu2 *)p);
-#else
-    *p = v;
-#endif
-}
 
 // ---------------------------------------------------------------------------
 // wave helpers (64 lanes)
@@ -243,16 +207,8 @@ DEV uint32_t lane_id() { return __lane_id(); }
 // ---------------------------------------------------------------------------
 // Make three values opaque to the optimiser (no instruction): a select
 // between struct members is otherwise folded into a load through a selected
-// address, which demotes the whole ray state to scratch (see sel3).
+// address, which demotes the whole ray state to scratch.
 DEV void launder3(float &a, float &b, float &c) { asm("" : "+v"(a), "+v"(b), "+v"(c)); }
-
-// Select component `axis` of (a, b, c) with bit masks.  A ternary chain on
-// struct members gets folded by InstCombine into a load through a selected
-// address, which defeats SROA and demotes the whole ray state to scratch.
-DEV float sel3(uint32_t axis, float a, float b, float c) {
-    const uint32_t m0 = 0u - (uint32_t)(axis == 0), m1 = 0u - (uint32_t)(axis == 1), m2 = 0u - (uint32_t)(axis == 2);
-    return __uint_as_float((__float_as_uint(a) & m0) | (__float_as_uint(b) & m1) | (__float_as_uint(c) & m2));
-}
 
 // TriAccel::rayIntersect (triaccel.h:96-158)
 DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, float3 d, float mint, float maxt,
@@ -296,199 +252,18 @@ DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float m
 }
 
 // ---------------------------------------------------------------------------
-// kd-tree traversal: t-interval front-to-back order with an LDS short stack
-// and kd-restart when the short stack has overflowed (Horn et al. 2007).
-// Finds the same closest primitive as the Havran loop: every leaf overlapping
-// the ray segment is visited until the best hit lies before the current
-// leaf's exit distance (sahkdtree3.h:299-300).
+// kd-tree traversal (ShapeKDTree::rayIntersectHavran, sahkdtree3.h:246-358):
+// t-interval front-to-back order with an LDS short stack and kd-restart when
+// the short stack has overflowed (Horn et al. 2007).  Finds the same closest
+// primitive as the Havran loop: every leaf overlapping the ray segment is
+// visited until the best hit lies before the current leaf's exit distance
+// (sahkdtree3.h:299-300).
 // ---------------------------------------------------------------------------
 // Algorithmic work (per lane) and, for the SIMD-efficiency figures, the
 // wave-level iteration counts (accumulated by lane 0 only): a wave pays
 // max-over-lanes of the inner-node and primitive iterations of every step.
 struct TraceCounts { uint32_t nodes, refs, tests, wnodes, wtests, wsteps, wactive; };
 
-// Resumable traversal state of one ray (lives in VGPRs; the short stack in LDS).
-struct KdRay {
-    float3 o, d, inv;
-    float mint;          // clipped lower bound for primitive tests
-    float best;          // upper bound, shrinks with hits
-    float tmin, tmax;    // current node interval
-    float bu, bv;
-    uint32_t bprim;      // triangle index, or 0x80000000 | rectangle index
-    uint2 cur;           // current node
-    uint32_t sp, bottom;
-    uint32_t found;
-    uint32_t dneg;       // bit a: d[a] <= 0 (Havran's tie rule for o[a] == split)
-    // speculative traversal (kd_iter_spec): the leaf under test and its exit
-    uint32_t lfE, lfEnd; // remaining primitive range (lfE >= lfEnd: none)
-    float lfTmax;        // exit distance of that leaf; < 0: no leaf under test
-    uint32_t travDone;   // traversal has no node left (leaf may still be under test)
-};
-
-// LDS short stack: far-child node data and its exit distance, SoA by lane
-struct KdStack {
-    uint2 *node;
-    float *t;
-};
-
-// Scene-AABB clip + adaptive epsilon (skdtree.cpp:112-142 / 207-226).
-// Returns false when the ray misses the scene bounds.
-template <bool SHADOW, bool LEAFIDX = false>
-DEV bool kd_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, KdRay &r) {
-    r.o = o;
-    r.d = d;
-    r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    r.dneg = (d.x <= 0.0f ? 1u : 0u) | (d.y <= 0.0f ? 2u : 0u) | (d.z <= 0.0f ? 4u : 0u);
-    // AABB::rayIntersect (aabb.h:308-338)
-    float nearT = -INFINITY, farT = INFINITY;
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const float oi = comp(o, i), di = comp(d, i), ii = comp(r.inv, i);
-        if (di == 0.0f) {
-            if (oi < S.bmin[i] || oi > S.bmax[i]) ok = false;
-        } else {
-            float t1 = (S.bmin[i] - oi) * ii, t2 = (S.bmax[i] - oi) * ii;
-            nearT = fmaxf(fminf(t1, t2), nearT);
-            farT = fminf(fmaxf(t1, t2), farT);
-        }
-    }
-    if (!ok || !(nearT <= farT)) return false;
-    float rayMinT = rayMint;
-    if (rayMinT == kEpsilon) {
-        float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-        if (!SHADOW) m = fmaxf(m, kEpsilon);
-        rayMinT *= m;
-    }
-    r.mint = fmaxf(nearT, rayMinT);
-    r.best = fminf(farT, rayMaxt);
-    if (!(r.best > r.mint)) return false;
-    r.tmin = r.mint;
-    r.tmax = r.best;
-    r.cur = LEAFIDX ? S.rootIdx : S.root;
-    r.sp = r.bottom = 0;
-    r.found = 0;
-    r.bu = r.bv = 0.f;
-    r.bprim = 0xFFFFFFFFu;
-    r.lfE = r.lfEnd = 0;
-    r.lfTmax = -1.0f;
-    r.travDone = 0;
-    return true;
-}
-
-// One kd inner-node decision (sahkdtree3.h:207-262 restated for the
-// t-interval form): tsplit and the near/far children from the sibling pair.
-DEV void kd_node(const KdRay &r, uint2 n, const uint4 &pr, float &tsplit, uint2 &first, uint2 &second,
-                 bool &leftFirst) {
-    const uint32_t axis = n.x & 3u;
-    const float split = __uint_as_float(n.y);
-    const bool a0 = axis == 0u, a1 = axis == 1u;
-    float ox = r.o.x, oy = r.o.y, oz = r.o.z, ix = r.inv.x, iy = r.inv.y, iz = r.inv.z;
-    launder3(ox, oy, oz);
-    launder3(ix, iy, iz);
-    const float oa = a0 ? ox : (a1 ? oy : oz);
-    const float ia = a0 ? ix : (a1 ? iy : iz);
-    tsplit = (split - oa) * ia;
-    if (tsplit != tsplit) tsplit = INFINITY;   // o on the plane, d parallel
-    const bool belowFirst = (oa < split) || (oa == split && ((r.dneg >> axis) & 1u));
-    first = belowFirst ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
-    second = belowFirst ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
-    leftFirst = belowFirst;
-}
-
-// Process one leaf: descend from r.cur (one 16-byte sibling-pair load per
-// inner node), test the leaf's primitives, then pop (or restart).  Returns
-// true when the ray is finished.
-template <bool SHADOW, bool COUNT, bool LEAFIDX = false>
-DEV bool kd_step(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
-    uint2 n = r.cur;
-    float tmin = r.tmin, tmax = r.tmax;
-    while (!(n.x & 0x80000000u)) {
-        const uint4 pr = LEAFIDX ? S.pairsIdx[n.x >> 2] : S.pairs[n.x >> 2];
-        if (COUNT) cnt.nodes++;
-        float tsplit;
-        uint2 first, second;
-        bool leftFirst;
-        kd_node(r, n, pr, tsplit, first, second, leftFirst);
-        if (tsplit > tmax || tsplit <= 0.0f) {
-            n = first;
-        } else if (tsplit < tmin) {
-            n = second;
-        } else {
-            const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-            stk.node[k] = second;
-            stk.t[k] = tmax;
-            ++r.sp;
-            if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
-            n = first;
-            tmax = tsplit;
-        }
-    }
-    // leaf: test every primitive against [mint, best] (skdtree.h:248-304)
-#if MTSG_LEAF_PREFETCH
-    // software pipelining: the next record's loads are issued before this
-    // record is tested (one dependent-load latency per leaf, not per primitive)
-    float4 g0, g1, g2;
-    {
-        const uint32_t e0 = n.x & 0x7FFFFFFFu;
-        if (e0 < n.y) { const float4 *rec = S.triL + 3 * (size_t)e0; g0 = rec[0]; g1 = rec[1]; g2 = rec[2]; }
-    }
-#endif
-    for (uint32_t e = n.x & 0x7FFFFFFFu; e < n.y; ++e) {
-        if (COUNT) { cnt.refs++; cnt.tests++; }
-#if MTSG_LEAF_PREFETCH
-        const float4 f0 = g0, f1 = g1, f2 = g2;
-        if (e + 1 < n.y) { const float4 *rec = S.triL + 3 * (size_t)(e + 1); g0 = rec[0]; g1 = rec[1]; g2 = rec[2]; }
-#else
-        const float4 *rec = LEAFIDX ? S.tri + 3 * (size_t)S.lidx[e] : S.triL + 3 * (size_t)e;
-        const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-#endif
-        float t, u, v;
-        // a rectangle record (k = 0xFFFFFFFF) fails the triangle test
-        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
-        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
-        if (h) {
-            r.found = 1;
-            if (SHADOW) return true;
-            r.best = t; r.bu = u; r.bv = v;
-            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
-        }
-    }
-    // Havran exits once the leaf's exit distance exceeds the best hit
-    // (`stack[exPt].t > maxt`, sahkdtree3.h:299): on an exact tie the next
-    // leaf is still visited, and a coplanar primitive there can win
-    if (r.found && r.best < tmax) return true;
-    // pop (or restart from the root if entries were dropped)
-    if (r.sp == r.bottom) {
-        if (r.bottom == 0) return true;
-        r.sp = r.bottom = 0;
-        r.tmin = tmax;
-        r.tmax = r.best;
-        r.cur = LEAFIDX ? S.rootIdx : S.root;
-        return !(r.tmin < r.tmax);
-    }
-    --r.sp;
-    const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-    r.cur = stk.node[k];
-    r.tmin = tmax;
-    r.tmax = fminf(stk.t[k], r.best);
-    return false;
-}
-
-template <bool SHADOW, bool COUNT>
-DEV bool kd_traverse(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, float &best, float &bu,
-                     float &bv, uint32_t &bprim, KdStack stk, TraceCounts &cnt) {
-    KdRay r;
-    if (!kd_init<SHADOW>(S, o, d, rayMint, rayMaxt, r)) return false;
-    while (!kd_step<SHADOW, COUNT>(S, r, stk, cnt)) {}
-    best = r.best; bu = r.bu; bv = r.bv; bprim = r.bprim;
-    return r.found;
-}
-
-// ---------------------------------------------------------------------------
-// kernels: traversal
-// ---------------------------------------------------------------------------
 template <bool COUNT>
 DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
     if (!COUNT) return;
@@ -501,25 +276,6 @@ DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) atomicAdd(ctr + k, v[k]);
 }
-
-DEV uint32_t wave_max(uint32_t v) {
-    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
-    return v;
-}
-
-// Persistent traversal kernel with lane-level refill (the "while-while +
-// dynamic fetch" structure of Aila & Laine 2009, re-tiled for 64-lane waves):
-// a wave reserves FETCH queue entries with ONE atomic into a wave-uniform
-// pool (SGPRs), and lanes whose ray finished take the next pool entries after
-// every leaf, so SIMD lanes stay busy and the contended fetch counter sees
-// 1/FETCH of the rays.
-//   SHADOW = false: closest hit of queue qin (qin < 0: identity over nIdentity
-//                   slots, bounce 0), result -> P.hit
-//   SHADOW = true : any hit of the shadow queue; unoccluded -> L += contribution
-#define KD_STACK_DECL                                                   \
-    __shared__ uint2 stkNode[SHORT_STACK * TRACE_BLOCK];                \
-    __shared__ float stkT[SHORT_STACK * TRACE_BLOCK];                   \
-    KdStack stk{stkNode + threadIdx.x, stkT + threadIdx.x};
 
 // XCD-partitioned work fetch: the queue is cut into XGROUPS contiguous
 // ranges; workgroup b draws from range b % XGROUPS first (blocks b, b + 8
@@ -536,9 +292,10 @@ struct Fetch {
     DEV bool next(uint32_t want, uint32_t &base, uint32_t &n) {
         while (tried < XGROUPS) {
             const uint32_t beg = lo(group), end = lo(group + 1);
+            // called with the whole wave active: lane 0 draws for it
             uint32_t off = 0;
             if (__lane_id() == 0) off = atomicAdd(&ctr[32 * group], want);
-            off = __shfl(off, 0);
+            off = __builtin_amdgcn_readfirstlane(off);
             if (beg + off < end) {
                 base = beg + off;
                 n = min(want, end - base);
@@ -552,538 +309,15 @@ struct Fetch {
 };
 
 // unoccluded shadow ray i: its contribution goes to the path's radiance, at
-// the path's next-bounce position or, if the path ended, to its final slot
+// the path's position in the current bounce (the trace runs after the swap)
+// or, if the path ended, to its sample's final slot
 DEV void shadow_unoccluded(const DevPaths &P, uint32_t i) {
     const float4 con = ldS(&P.sh_c[i]);
     const uint32_t tgt = __float_as_uint(con.w);
-    float4 *L = (tgt & 0x80000000u) ? &P.L[tgt & 0x7FFFFFFFu] : &P.n_Lp[tgt];
+    float4 *L = (tgt & 0x80000000u) ? &P.L[tgt & 0x7FFFFFFFu] : &P.Lp[tgt];
     float4 v = ldS(L);
     v.x += con.x; v.y += con.y; v.z += con.z;
     stS(L, v);
-}
-
-DEV void load_ray(const DevPaths &P, bool shadow, uint32_t i, float4 &ro, float4 &rd) {
-    if (shadow) { ro = ldS(&P.sh_o[i]); rd = ldS(&P.sh_d[i]); const float mint = rd.w; rd.w = ro.w; ro.w = mint; }
-    else { ro = ldS(&P.ray_o[i]); rd = ldS(&P.ray_d[i]); }
-}
-
-DEV float4 hit_record(const KdRay &r) {
-    return r.found ? make_float4(r.best, r.bu, r.bv, __uint_as_float(r.bprim))
-                   : make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu));
-}
-
-// Classic persistent kernel: a wave takes ROUNDS x 64 consecutive queue
-// entries per atomic and traces them 64 at a time (one ray per lane, no refill).
-template <bool SHADOW, bool COUNT, int ROUNDS>
-__global__ void __launch_bounds__(TRACE_BLOCK) k_trace_wave(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
-    KD_STACK_DECL
-    uint32_t count = nIdentity;
-    if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
-    else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
-    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
-    uint32_t base, n;
-    while (F.next(64u * ROUNDS, base, n)) {
-        for (uint32_t rnd = 0; rnd * 64 < n; ++rnd) {
-            const uint32_t i = base + 64u * rnd + __lane_id();
-            if (i >= base + n) break;
-            const uint32_t slot = i;
-            float4 ro, rd;
-            load_ray(P, SHADOW, slot, ro, rd);
-            if (!SHADOW && rd.w < 0.0f) continue;   // dead slot
-            KdRay r;
-            const bool live = kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
-            r.found = 0;
-            if (live) while (!kd_step<SHADOW, COUNT>(S, r, stk, c)) {}
-            if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
-            else stS(&P.hit[slot], hit_record(r));
-        }
-    }
-    flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
-}
-
-// Persistent traversal kernel with lane-level refill (the "while-while +
-// dynamic fetch" structure of Aila & Laine 2009, re-tiled for 64-lane waves):
-// a wave reserves FETCH queue entries with ONE atomic into a wave-uniform
-// pool (SGPRs), and once MIN_IDLE lanes have finished their rays they take
-// the next pool entries, so SIMD lanes stay busy and the fetch counters see
-// 1/FETCH of the rays.
-//   SHADOW = false: closest hit of queue qin (qin < 0: identity over nIdentity
-//                   slots, bounce 0), result -> P.hit
-//   SHADOW = true : any hit of the shadow queue; unoccluded -> L += contribution
-#ifndef MTSG_FETCH
-#define MTSG_FETCH 256
-#endif
-constexpr uint32_t FETCH = MTSG_FETCH;
-
-template <bool SHADOW, bool COUNT, int MIN_IDLE, bool LEAFIDX = false>
-__global__ void TRACE_ATTR k_trace(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
-    KD_STACK_DECL
-    uint32_t count = nIdentity;   // explicit branches: a ternary over a volatile load
-    if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);   // demotes the argument to scratch
-    else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
-    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
-    uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
-    bool exhausted = false;
-    bool active = false;
-    uint32_t slot = 0;
-    KdRay r;
-    const unsigned long long below = (1ull << __lane_id()) - 1ull;
-    for (;;) {
-        // ---- refill idle lanes from the wave's pool
-        unsigned long long idle = __ballot(!active);
-        // refill only once MIN_IDLE lanes are idle (or the wave has nothing left)
-        if ((uint32_t)__popcll(idle) < (uint32_t)MIN_IDLE && __any(active)) idle = 0;
-        while (idle && !exhausted) {
-            if (poolLeft == 0 && !F.next(FETCH, poolBase, poolLeft)) { exhausted = true; break; }
-            const uint32_t nIdle = (uint32_t)__popcll(idle);
-            const uint32_t take = min(nIdle, poolLeft);
-            const uint32_t rank = (uint32_t)__popcll(idle & below);
-            if (!active && rank < take) {
-                const uint32_t i = poolBase + rank;
-                slot = i;
-                float4 ro, rd;
-                load_ray(P, SHADOW, slot, ro, rd);
-                // kd_init before the dead-slot test so that both ray loads are
-                // issued together (a dead slot has maxt = -1 and fails kd_init)
-                const bool live = kd_init<SHADOW, LEAFIDX>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
-                if (live) {
-                    active = true;
-                } else if (!SHADOW && rd.w < 0.0f) {
-                    // dead slot (outside the render rectangle): no hit record needed
-                } else if (SHADOW) {
-                    shadow_unoccluded(P, slot);   // misses the scene bounds
-                } else {
-                    stS(&P.hit[slot], make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)));
-                }
-            }
-            poolBase += take;
-            poolLeft -= take;
-            idle = __ballot(!active);
-            if (take == nIdle) break;
-        }
-        if (!__any(active)) {
-            if (exhausted) break;
-            continue;
-        }
-        // ---- one leaf of traversal for the active lanes
-        const uint32_t n0 = c.nodes, t0 = c.tests;
-        const uint32_t nActive = COUNT ? (uint32_t)__popcll(__ballot(active)) : 0u;
-        if (active && kd_step<SHADOW, COUNT, LEAFIDX>(S, r, stk, c)) {
-            active = false;
-            if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
-            else stS(&P.hit[slot], hit_record(r));
-        }
-        if (COUNT) {
-            const uint32_t wn = wave_max(c.nodes - n0), wt = wave_max(c.tests - t0);
-            if (__lane_id() == 0) { c.wnodes += wn; c.wtests += wt; c.wsteps += 1; c.wactive += nActive; }
-        }
-    }
-    flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
-}
-
-// ---------------------------------------------------------------------------
-// Unified traversal ("if-if" order, one fetch per iteration): every iteration
-// advances each active lane by exactly ONE inner node or ONE primitive, and a
-// lane whose leaf is exhausted pops (or restarts) in the same iteration.  The
-// while-while structure above runs, per step, the slowest lane's whole
-// descent and then the largest leaf, which measured 25% (descent) and 17%
-// (leaf) SIMD efficiency on 64-lane waves; here the wave pays one node+prim
-// iteration for the work of up to 64 lanes.  Both fetches (the 16-B sibling
-// pair and the 48-B TriAccel record) are issued by every lane before any
-// branch -- idle lanes read element 0, one cached line -- so an iteration
-// costs one memory latency, not one per branch.
-// ---------------------------------------------------------------------------
-template <bool SHADOW, bool COUNT>
-DEV bool kd_iter(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
-    const uint2 n = r.cur;
-    const bool inner = !(n.x & 0x80000000u);
-    const uint32_t e = n.x & 0x7FFFFFFFu;
-    const bool prim = !inner && e < n.y;
-    const uint4 pr = S.pairs[inner ? (n.x >> 2) : 0u];
-    const float4 *rec = S.triL + 3 * (size_t)(prim ? e : 0u);
-    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-    // keep the four loads in flight together: without this use the compiler
-    // sinks each load into the branch that consumes it
-    asm volatile("" ::"v"(pr.x), "v"(pr.y), "v"(pr.z), "v"(pr.w), "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
-                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
-    if (inner) {
-        if (COUNT) cnt.nodes++;
-        float tsplit;
-        uint2 first, second;
-        bool leftFirst;
-        kd_node(r, n, pr, tsplit, first, second, leftFirst);
-        if (tsplit > r.tmax || tsplit <= 0.0f) {
-            r.cur = first;
-        } else if (tsplit < r.tmin) {
-            r.cur = second;
-        } else {
-            const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-            stk.node[k] = second;
-            stk.t[k] = r.tmax;
-            ++r.sp;
-            if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
-            r.cur = first;
-            r.tmax = tsplit;
-        }
-    } else if (prim) {
-        if (COUNT) { cnt.refs++; cnt.tests++; }
-        float t, u, v;
-        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
-        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
-        if (h) {
-            r.found = 1;
-            if (SHADOW) return true;
-            r.best = t; r.bu = u; r.bv = v;
-            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
-        }
-        r.cur.x = n.x + 1u;
-    }
-    // leaf exhausted (also an empty leaf reached by this iteration's descent)
-    const uint2 c = r.cur;
-    if ((c.x & 0x80000000u) && (c.x & 0x7FFFFFFFu) >= c.y) {
-        // Havran's exit test `stack[exPt].t > maxt` (sahkdtree3.h:299)
-        if (r.found && r.best < r.tmax) return true;
-        if (r.sp == r.bottom) {
-            if (r.bottom == 0) return true;
-            r.sp = r.bottom = 0;   // short stack overflowed: kd-restart
-            r.tmin = r.tmax;
-            r.tmax = r.best;
-            r.cur = S.root;
-            return !(r.tmin < r.tmax);
-        }
-        --r.sp;
-        const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-        r.cur = stk.node[k];
-        r.tmin = r.tmax;
-        r.tmax = fminf(stk.t[k], r.best);
-    }
-    return false;
-}
-
-// Phase-separated variant: an iteration is either a NODE phase (lanes at
-// inner nodes descend one level; one 16-B fetch) or a PRIMITIVE phase (lanes
-// at leaves test one record; one 48-B fetch), chosen per wave from how many
-// lanes are ready for each.  A mixed iteration executes both code paths for
-// every lane (the SIMDs are 16 wide: each wave64 VALU op costs 4 cycles, and
-// the traversal is VALU-throughput bound), so separating them trades a few
-// more iterations for far fewer issued instructions.
-// One inner-node step of the t-interval traversal: choose the near child,
-// push the far one when both intervals are non-empty.  Returns the next node.
-DEV uint2 kd_descend(KdRay &r, uint2 n, const uint4 &pr, KdStack stk, bool &nearIsLeft) {
-    float tsplit;
-    uint2 first, second;
-    kd_node(r, n, pr, tsplit, first, second, nearIsLeft);
-    if (tsplit > r.tmax || tsplit <= 0.0f) return first;
-    if (tsplit < r.tmin) { nearIsLeft = !nearIsLeft; return second; }
-    const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-    stk.node[k] = second;
-    stk.t[k] = r.tmax;
-    ++r.sp;
-    if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
-    r.tmax = tsplit;
-    return first;
-}
-
-// Unified iteration over the two-level block layout: a lane at a block root
-// descends up to two levels per fetch (the 64-B block carries the
-// grandchildren pairs); a lane at a pair-only node (popped from the stack)
-// descends one level.  Otherwise as kd_iter.
-template <bool SHADOW, bool COUNT>
-DEV bool kd_iter2(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
-    const uint2 n = r.cur;
-    const bool inner = !(n.x & 0x80000000u);
-    const bool rootKind = inner && !(n.x & 4u);
-    const uint32_t e = n.x & 0x7FFFFFFFu;
-    const bool prim = !inner && e < n.y;
-    const uint4 *blk = S.blocks + (inner ? (rootKind ? 4u * (n.x >> 3) : (n.x >> 3)) : 0u);
-    const uint4 p0 = blk[0], p1 = blk[1], p2 = blk[2];
-    const float4 *rec = S.triL + 3 * (size_t)(prim ? e : 0u);
-    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(p1.x), "v"(p1.y), "v"(p1.z), "v"(p1.w),
-                 "v"(p2.x), "v"(p2.y), "v"(p2.z), "v"(p2.w), "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
-                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
-    if (inner) {
-        if (COUNT) cnt.nodes++;
-        bool nearLeft;
-        const uint2 c = kd_descend(r, n, p0, stk, nearLeft);
-        r.cur = c;
-        if (rootKind && !(c.x & 0x80000000u)) {
-            // second level from the same block (c is a pair-only node)
-            if (COUNT) cnt.nodes++;
-            const uint4 pc = nearLeft ? p1 : p2;
-            bool dummy;
-            r.cur = kd_descend(r, c, pc, stk, dummy);
-        }
-    } else if (prim) {
-        if (COUNT) { cnt.refs++; cnt.tests++; }
-        float t, u, v;
-        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
-        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
-        if (h) {
-            r.found = 1;
-            if (SHADOW) return true;
-            r.best = t; r.bu = u; r.bv = v;
-            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
-        }
-        r.cur.x = n.x + 1u;
-    }
-    const uint2 c = r.cur;
-    if ((c.x & 0x80000000u) && (c.x & 0x7FFFFFFFu) >= c.y) {
-        if (r.found && r.best < r.tmax) return true;
-        if (r.sp == r.bottom) {
-            if (r.bottom == 0) return true;
-            r.sp = r.bottom = 0;
-            r.tmin = r.tmax;
-            r.tmax = r.best;
-            r.cur = S.root2;
-            return !(r.tmin < r.tmax);
-        }
-        --r.sp;
-        const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-        r.cur = stk.node[k];
-        r.tmin = r.tmax;
-        r.tmax = fminf(stk.t[k], r.best);
-    }
-    return false;
-}
-
-// Speculative traversal over the two-level blocks (the "speculative
-// while-while" idea of Aila & Laine 2009 recast as unified iterations): a
-// lane tests one primitive of the leaf it holds AND descends its traversal
-// towards the next leaf in the same iteration, so both code paths do useful
-// work for most lanes.  The traversal pauses on reaching a leaf until the
-// held leaf is finished; Havran's exit test (`best < leaf exit`) is applied
-// when a held leaf is exhausted, and to empty leaves when none is held.
-// Extra leaves visited speculatively can only be tested against [mint, best],
-// so the closest hit is unchanged (every primitive is referenced by all the
-// leaves it overlaps).
-template <bool SHADOW, bool COUNT>
-DEV bool kd_iter_spec(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt) {
-    const uint2 n = r.cur;
-    const bool inner = !r.travDone && !(n.x & 0x80000000u);
-    const bool prim = r.lfE < r.lfEnd;
-    const bool rootKind = inner && !(n.x & 4u);
-    const uint4 *blk = S.blocks + (inner ? (rootKind ? 4u * (n.x >> 3) : (n.x >> 3)) : 0u);
-    const uint4 p0 = blk[0], p1 = blk[1], p2 = blk[2];
-    const float4 *rec = S.triL + 3 * (size_t)(prim ? r.lfE : 0u);
-    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(p1.x), "v"(p1.y), "v"(p1.z), "v"(p1.w),
-                 "v"(p2.x), "v"(p2.y), "v"(p2.z), "v"(p2.w), "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
-                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
-    if (prim) {
-        if (COUNT) { cnt.refs++; cnt.tests++; }
-        float t, u, v;
-        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
-        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
-        if (h) {
-            r.found = 1;
-            if (SHADOW) return true;
-            r.best = t; r.bu = u; r.bv = v;
-            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
-        }
-        ++r.lfE;
-    }
-    if (inner) {
-        if (COUNT) cnt.nodes++;
-        bool nearLeft;
-        const uint2 c = kd_descend(r, n, p0, stk, nearLeft);
-        r.cur = c;
-        if (rootKind && !(c.x & 0x80000000u)) {
-            if (COUNT) cnt.nodes++;
-            const uint4 pc = nearLeft ? p1 : p2;
-            bool dummy;
-            r.cur = kd_descend(r, c, pc, stk, dummy);
-        }
-    }
-    // the held leaf is finished: Havran's exit test
-    if (r.lfTmax >= 0.0f && r.lfE >= r.lfEnd) {
-        if (r.found && r.best < r.lfTmax) return true;
-        r.lfTmax = -1.0f;
-    }
-    // take the leaf the traversal reached (if none is held), then advance
-    const uint2 c = r.cur;
-    if (r.lfTmax < 0.0f && !r.travDone && (c.x & 0x80000000u)) {
-        const uint32_t st = c.x & 0x7FFFFFFFu;
-        if (st < c.y) {
-            r.lfE = st; r.lfEnd = c.y; r.lfTmax = r.tmax;
-        } else if (r.found && r.best < r.tmax) {
-            return true;   // empty leaf, nothing held: exit test as in Havran
-        }
-        // pop the next far child, restart after a short-stack overflow, or finish
-        if (r.sp == r.bottom) {
-            if (r.bottom == 0) {
-                r.travDone = 1;
-            } else {
-                r.sp = r.bottom = 0;
-                r.tmin = r.tmax;
-                r.tmax = r.best;
-                r.cur = S.root2;
-                if (!(r.tmin < r.tmax)) r.travDone = 1;
-            }
-        } else {
-            --r.sp;
-            const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-            r.cur = stk.node[k];
-            r.tmin = r.tmax;
-            r.tmax = fminf(stk.t[k], r.best);
-        }
-    }
-    return r.travDone && r.lfTmax < 0.0f;
-}
-
-template <bool SHADOW, bool COUNT>
-DEV bool kd_iter_phase(const DevScene &S, KdRay &r, KdStack stk, TraceCounts &cnt, bool primPhase) {
-    const uint2 n = r.cur;
-    const bool inner = !(n.x & 0x80000000u);
-    const uint32_t e = n.x & 0x7FFFFFFFu;
-    if (!primPhase) {
-        if (inner) {
-            if (COUNT) cnt.nodes++;
-            const uint4 pr = S.pairs[n.x >> 2];
-            float tsplit;
-            uint2 first, second;
-            bool leftFirst;
-            kd_node(r, n, pr, tsplit, first, second, leftFirst);
-            if (tsplit > r.tmax || tsplit <= 0.0f) {
-                r.cur = first;
-            } else if (tsplit < r.tmin) {
-                r.cur = second;
-            } else {
-                const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-                stk.node[k] = second;
-                stk.t[k] = r.tmax;
-                ++r.sp;
-                if (r.sp - r.bottom > SHORT_STACK) ++r.bottom;
-                r.cur = first;
-                r.tmax = tsplit;
-            }
-        }
-    } else if (!inner && e < n.y) {
-        if (COUNT) { cnt.refs++; cnt.tests++; }
-        const float4 *rec = S.triL + 3 * (size_t)e;
-        const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-        float t, u, v;
-        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
-        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
-        if (h) {
-            r.found = 1;
-            if (SHADOW) return true;
-            r.best = t; r.bu = u; r.bv = v;
-            r.bprim = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
-        }
-        r.cur.x = n.x + 1u;
-    }
-    const uint2 c = r.cur;
-    if ((c.x & 0x80000000u) && (c.x & 0x7FFFFFFFu) >= c.y) {
-        if (r.found && r.best < r.tmax) return true;
-        if (r.sp == r.bottom) {
-            if (r.bottom == 0) return true;
-            r.sp = r.bottom = 0;
-            r.tmin = r.tmax;
-            r.tmax = r.best;
-            r.cur = S.root;
-            return !(r.tmin < r.tmax);
-        }
-        --r.sp;
-        const uint32_t k = (r.sp % SHORT_STACK) * TRACE_BLOCK;
-        r.cur = stk.node[k];
-        r.tmin = r.tmax;
-        r.tmax = fminf(stk.t[k], r.best);
-    }
-    return false;
-}
-
-// PRIM_RATIO = 0: unified iterations (kd_iter); otherwise phase-separated
-// (kd_iter_phase) with a primitive phase once primLanes * PRIM_RATIO >=
-// 4 * nodeLanes, or when no lane is at an inner node.
-template <bool SHADOW, bool COUNT, int MIN_IDLE, int PRIM_RATIO = 0, bool LAYOUT2 = false, bool SPEC = false>
-__global__ void TRACE_ATTR k_trace_u(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
-    KD_STACK_DECL
-    uint32_t count = nIdentity;
-    if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
-    else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
-    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
-    uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
-    bool exhausted = false;
-    bool active = false;
-    uint32_t slot = 0;
-    KdRay r;
-    const unsigned long long below = (1ull << __lane_id()) - 1ull;
-    for (;;) {
-        unsigned long long idle = __ballot(!active);
-        if ((uint32_t)__popcll(idle) < (uint32_t)MIN_IDLE && __any(active)) idle = 0;
-        while (idle && !exhausted) {
-            if (poolLeft == 0 && !F.next(FETCH, poolBase, poolLeft)) { exhausted = true; break; }
-            const uint32_t nIdle = (uint32_t)__popcll(idle);
-            const uint32_t take = min(nIdle, poolLeft);
-            const uint32_t rank = (uint32_t)__popcll(idle & below);
-            if (!active && rank < take) {
-                const uint32_t i = poolBase + rank;
-                slot = i;
-                float4 ro, rd;
-                load_ray(P, SHADOW, slot, ro, rd);
-                const bool live = kd_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
-                if (LAYOUT2) r.cur = S.root2;
-                if (live) {
-                    active = true;
-                } else if (!SHADOW && rd.w < 0.0f) {
-                    // dead slot (outside the render rectangle)
-                } else if (SHADOW) {
-                    shadow_unoccluded(P, slot);
-                } else {
-                    stS(&P.hit[slot], make_float4(INFINITY, 0.f, 0.f, __uint_as_float(0xFFFFFFFFu)));
-                }
-            }
-            poolBase += take;
-            poolLeft -= take;
-            idle = __ballot(!active);
-            if (take == nIdle) break;
-        }
-        if (!__any(active)) {
-            if (exhausted) break;
-            continue;
-        }
-        if (COUNT && __lane_id() == 0) c.wsteps += 1;
-        bool primPhase = false;
-        if (PRIM_RATIO > 0) {
-            const uint2 n = r.cur;
-            const bool inner = active && !(n.x & 0x80000000u);
-            const bool prim = active && (n.x & 0x80000000u) && (n.x & 0x7FFFFFFFu) < n.y;
-            const uint32_t nInner = (uint32_t)__popcll(__ballot(inner)), nPrim = (uint32_t)__popcll(__ballot(prim));
-            primPhase = nPrim > 0 && (nInner == 0 || nPrim * PRIM_RATIO >= 4 * nInner);
-            if (COUNT && __lane_id() == 0) {
-                c.wnodes += !primPhase; c.wtests += primPhase;
-                c.wactive += (uint32_t)__popcll(__ballot(active));
-            }
-        } else if (COUNT) {
-            const uint2 n = r.cur;
-            const bool inner = active && !(n.x & 0x80000000u);
-            const bool prim = active && (n.x & 0x80000000u) && (n.x & 0x7FFFFFFFu) < n.y;
-            const bool anyInner = __any(inner), anyPrim = __any(prim);
-            const uint32_t nActive = (uint32_t)__popcll(__ballot(active));
-            if (__lane_id() == 0) { c.wnodes += anyInner; c.wtests += anyPrim; c.wactive += nActive; }
-        }
-        bool done = false;
-        if (active) {
-            if (SPEC) done = kd_iter_spec<SHADOW, COUNT>(S, r, stk, c);
-            else if (LAYOUT2) done = kd_iter2<SHADOW, COUNT>(S, r, stk, c);
-            else if (PRIM_RATIO > 0) done = kd_iter_phase<SHADOW, COUNT>(S, r, stk, c, primPhase);
-            else done = kd_iter<SHADOW, COUNT>(S, r, stk, c);
-        }
-        if (done) {
-            active = false;
-            if (SHADOW) { if (!r.found) shadow_unoccluded(P, slot); }
-            else stS(&P.hit[slot], hit_record(r));
-        }
-    }
-    flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
 }
 
 // Debug entry point: environment radiance along directions (rx/ry null:
@@ -1100,11 +334,11 @@ __global__ void k_env_eval(DevScene S, const float *dirs, const float *rx, const
 }
 
 // ---------------------------------------------------------------------------
-// Speculative traversal with compact per-lane state (the default): as
-// kd_iter_spec, with the stack counters, direction signs and flags packed in
-// one word and hit records written through on every hit (so u, v and the
-// primitive index are not kept live).  19 state registers instead of 27, for
-// 8 waves per SIMD.
+// Speculative traversal with compact per-lane state: each iteration issues
+// one node fetch and one primitive fetch per lane, testing the leaf it holds
+// while descending towards the next one.  Stack counters, direction signs and
+// flags are packed in one word and hit records are written through on every
+// hit (u, v and the primitive index are not kept live): 64 VGPRs, 8 waves/SIMD.
 // ---------------------------------------------------------------------------
 struct SpecRay {
     float3 o, d, inv;
@@ -1117,24 +351,30 @@ struct SpecRay {
 };
 // bits: top slot of the circular short stack (0-2), entries held (3-5),
 // entries dropped since the last restart (6), ray direction signs (16-18),
-// traversal done (19), hit found (20)
+// traversal done (19), hit found (20), shadow ray (21)
 enum : uint32_t {
     SB_TOP = 7u, SB_N = 7u << 3, SB_N1 = 1u << 3, SB_DROPPED = 1u << 6, SB_STACK = 0x7Fu,
-    SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20
+    SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20, SB_SHADOW = 1u << 21
 };
 
 // short stack of the compact traversal: entry k of lane i at [k * TRACE_BLOCK
-// + i].  Only the lane index is kept in a register (laundered at every use so
-// the two scaled addresses are not hoisted into two loop-invariant registers).
+// + i].  A workgroup is one wave, so the lane index is recomputed at every use
+// (v_mbcnt) instead of holding a register through the traversal loop.
+static_assert(TRACE_BLOCK == 64, "one wave per traversal workgroup");
 __shared__ uint2 s_specNode[SHORT_STACK * TRACE_BLOCK];
 __shared__ float s_specT[SHORT_STACK * TRACE_BLOCK];
+// lane index, recomputed where it is used (volatile: not hoisted out of loops)
+DEV uint32_t lane_here() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+// number of set bits of a wave mask below this lane
+DEV uint32_t rank_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 struct SpecStack {
-    uint32_t lane;
-    DEV uint32_t at(uint32_t k) const {
-        uint32_t l = lane;
-        asm volatile("" : "+v"(l));
-        return k * TRACE_BLOCK + l;
-    }
+    DEV static uint32_t at(uint32_t k) { return k * TRACE_BLOCK + lane_here(); }
     DEV void push(uint32_t k, uint2 node, float t) const {
         const uint32_t i = at(k);
         s_specNode[i] = node;
@@ -1154,16 +394,44 @@ DEV float4 miss_record() {
     return m;
 }
 
-template <bool SHADOW>
-DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, SpecRay &r) {
-    KdRay k;
-    if (!kd_init<SHADOW>(S, o, d, rayMint, rayMaxt, k)) return false;
-    r.o = k.o; r.d = k.d; r.inv = k.inv;
-    r.mint = k.mint; r.best = k.best; r.tmin = k.tmin; r.tmax = k.tmax;
+// Ray setup: scene-AABB clip (AABB::rayIntersect, aabb.h:308-338) and the
+// adaptive epsilon of ShapeKDTree::rayIntersect / rayIntersect for shadow
+// rays (skdtree.cpp:112-142 / 207-226).  Returns false when the ray misses
+// the scene bounds or its interval is empty.
+DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, bool shadow, SpecRay &r) {
+    r.o = o;
+    r.d = d;
+    r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const uint32_t dneg = (d.x <= 0.0f ? 1u : 0u) | (d.y <= 0.0f ? 2u : 0u) | (d.z <= 0.0f ? 4u : 0u);
+    float nearT = -INFINITY, farT = INFINITY;
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float oi = comp(o, i), di = comp(d, i), ii = comp(r.inv, i);
+        if (di == 0.0f) {
+            if (oi < S.bmin[i] || oi > S.bmax[i]) ok = false;
+        } else {
+            const float t1 = (S.bmin[i] - oi) * ii, t2 = (S.bmax[i] - oi) * ii;
+            nearT = fmaxf(fminf(t1, t2), nearT);
+            farT = fminf(fmaxf(t1, t2), farT);
+        }
+    }
+    if (!ok || !(nearT <= farT)) return false;
+    float rayMinT = rayMint;
+    if (rayMinT == kEpsilon) {
+        float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+        if (!shadow) m = fmaxf(m, kEpsilon);
+        rayMinT *= m;
+    }
+    r.mint = fmaxf(nearT, rayMinT);
+    r.best = fminf(farT, rayMaxt);
+    if (!(r.best > r.mint)) return false;
+    r.tmin = r.mint;
+    r.tmax = r.best;
     r.cur = S.root2;
     r.lfE = r.lfEnd = 0;
     r.lfTmax = -1.0f;
-    r.bits = k.dneg << SB_DNEG;
+    r.bits = dneg << SB_DNEG | (shadow ? SB_SHADOW : 0u);
     return true;
 }
 
@@ -1203,7 +471,7 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
     return c;
 }
 
-template <bool SHADOW, bool COUNT>
+template <bool COUNT>
 DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cnt, float4 *hitOut) {
     const uint2 n = r.cur;
     const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
@@ -1233,7 +501,7 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
         if (h) {
             r.bits |= SB_FOUND;
-            if (SHADOW) return true;
+            if (r.bits & SB_SHADOW) return true;   // any hit occludes
             r.best = t;
             stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
         }
@@ -1286,20 +554,35 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
 }
 
-template <bool SHADOW, bool COUNT, int MIN_IDLE>
-__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t nIdentity) {
-    const SpecStack stk{threadIdx.x};
-    uint32_t count = nIdentity;
-    if (SHADOW) count = __atomic_load_n(&P.cnt[CNT_S], __ATOMIC_RELAXED);
-    else if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    Fetch F{&P.cnt[SHADOW ? CNT_SFETCH : CNT_FETCH], count, blockIdx.x % XGROUPS, 0};
-    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
+// Persistent traversal kernel with lane-level refill (the "while-while +
+// dynamic fetch" structure of Aila & Laine 2009, re-tiled for 64-lane waves):
+// a wave reserves FETCH work-list entries with ONE atomic into a wave-uniform
+// pool (SGPRs), and once MIN_IDLE lanes have finished their rays they take the
+// next pool entries.  One launch traces this bounce's closest-hit rays and the
+// previous bounce's shadow rays as one work list (both only depend on the
+// previous k_shade), so lanes of either kind share waves and the launch has
+// one tail instead of two:
+//   [0, nC):       closest hit of P.ray_o/ray_d[i]   -> P.hit[i]
+//   [nC, nC + nS): any hit of P.sh_o/sh_d[i - nC]    -> unoccluded: L += sh_c
+//   cIn: -1 = nIdentity closest rays (bounce 0), 0/1 = count in cnt_q(cIn), -2 = none
+//   sIn: 0/1 = count in CNT_S0/CNT_S1, -1 = none
+#ifndef MTSG_FETCH
+#define MTSG_FETCH 256
+#endif
+constexpr uint32_t FETCH = MTSG_FETCH;
+
+template <bool COUNT, int MIN_IDLE>
+__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity) {
+    const SpecStack stk{};
+    const uint32_t nC = cIn == -1 ? nIdentity : (cIn >= 0 ? __atomic_load_n(&P.cnt[cnt_q(cIn)], __ATOMIC_RELAXED) : 0u);
+    const uint32_t nS = sIn >= 0 ? __atomic_load_n(&P.cnt[cnt_s(sIn)], __ATOMIC_RELAXED) : 0u;
+    Fetch F{&P.cnt[CNT_FETCH], nC + nS, blockIdx.x % XGROUPS, 0};
+    TraceCounts cc{0, 0, 0, 0, 0, 0, 0}, cs{0, 0, 0, 0, 0, 0, 0};
     uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
     bool exhausted = false;
     bool active = false;
-    uint32_t slot = 0;
+    uint32_t idx = 0;                      // index into the ray's own list
     SpecRay r;
-    const unsigned long long below = (1ull << __lane_id()) - 1ull;
     for (;;) {
         unsigned long long idle = __ballot(!active);
         if ((uint32_t)__popcll(idle) < (uint32_t)MIN_IDLE && __any(active)) idle = 0;
@@ -1307,21 +590,19 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t nI
             if (poolLeft == 0 && !F.next(FETCH, poolBase, poolLeft)) { exhausted = true; break; }
             const uint32_t nIdle = (uint32_t)__popcll(idle);
             const uint32_t take = min(nIdle, poolLeft);
-            const uint32_t rank = (uint32_t)__popcll(idle & below);
+            const uint32_t rank = rank_below(idle);
             if (!active && rank < take) {
                 const uint32_t i = poolBase + rank;
-                slot = i;
-                float4 ro, rd;
-                load_ray(P, SHADOW, slot, ro, rd);
-                const bool live = spec_init<SHADOW>(S, xyz(ro), xyz(rd), ro.w, rd.w, r);
-                if (live) {
+                const bool shadow = i >= nC;
+                idx = shadow ? i - nC : i;
+                float4 ro = ldS((shadow ? P.sh_o : P.ray_o) + idx), rd = ldS((shadow ? P.sh_d : P.ray_d) + idx);
+                if (shadow) { const float mint = rd.w; rd.w = ro.w; ro.w = mint; }   // sh_o.w = maxt, sh_d.w = mint
+                if (spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, shadow, r)) {
                     active = true;
-                } else if (!SHADOW && rd.w < 0.0f) {
-                    // dead slot (outside the render rectangle)
-                } else if (SHADOW) {
-                    shadow_unoccluded(P, slot);
-                } else {
-                    stS(&P.hit[slot], miss_record());
+                } else if (shadow) {
+                    shadow_unoccluded(P, idx);
+                } else if (!(rd.w < 0.0f)) {   // maxt < 0: dead slot outside the render rectangle
+                    stS(&P.hit[idx], miss_record());
                 }
             }
             poolBase += take;
@@ -1334,45 +615,30 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int qin, uint32_t nI
             continue;
         }
         if (COUNT) {
+            // wave-level figures are booked with the closest-hit counters
             const uint2 n = r.cur;
             const bool inner = active && !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
             const bool prim = active && r.lfE < r.lfEnd;
             const bool anyInner = __any(inner), anyPrim = __any(prim);
             const uint32_t nActive = (uint32_t)__popcll(__ballot(active));
-            if (__lane_id() == 0) { c.wsteps += 1; c.wnodes += anyInner; c.wtests += anyPrim; c.wactive += nActive; }
+            if (__lane_id() == 0) { cc.wsteps += 1; cc.wnodes += anyInner; cc.wtests += anyPrim; cc.wactive += nActive; }
         }
-        if (active && spec_iter<SHADOW, COUNT>(S, r, stk, c, P.hit + slot)) {
+        bool done = false;
+        if (active) {
+            if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx);
+            else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx);
+        }
+        if (done) {
             active = false;
-            // shadow: any hit returns before SB_FOUND is set; closest: hits were
-            // written through, only a miss needs a record
-            if (SHADOW) { if (!(r.bits & SB_FOUND)) shadow_unoccluded(P, slot); }
-            else if (!(r.bits & SB_FOUND)) stS(&P.hit[slot], miss_record());
+            // closest: hits were written through, only a miss needs a record
+            if (!(r.bits & SB_FOUND)) {
+                if (r.bits & SB_SHADOW) shadow_unoccluded(P, idx);
+                else stS(&P.hit[idx], miss_record());
+            }
         }
     }
-    flush_counts<COUNT>(P.ctr + (SHADOW ? 8 : 0), c);
-}
-
-// Debug entry points over caller-provided rays
-template <bool SHADOW>
-__global__ void __launch_bounds__(TRACE_BLOCK) k_trace_rays(DevScene S, const float *rays, uint32_t n, float *t,
-                                                            float *u, float *v, uint32_t *prim, uint8_t *occ) {
-    KD_STACK_DECL
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float *rr = rays + 8 * (size_t)i;
-    TraceCounts c{0, 0, 0, 0, 0, 0, 0};
-    float best, bu = 0, bv = 0;
-    uint32_t bp = 0xFFFFFFFFu;
-    bool h = kd_traverse<SHADOW, false>(S, mk3(rr[0], rr[1], rr[2]), mk3(rr[3], rr[4], rr[5]), rr[6], rr[7], best, bu, bv, bp, stk, c);
-    if (SHADOW) {
-        occ[i] = h ? 1 : 0;
-    } else if (h) {
-        prim[i] = bp;   // triangle index, or 0x80000000 | rectangle index
-        t[i] = best; u[i] = bu; v[i] = bv;
-    } else {
-        prim[i] = 0xFFFFFFFFu;
-        t[i] = INFINITY; u[i] = v[i] = 0.f;
-    }
+    flush_counts<COUNT>(P.ctr, cc);
+    flush_counts<COUNT>(P.ctr + 8, cs);
 }
 
 // ---------------------------------------------------------------------------
@@ -2050,7 +1316,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
         // in registers live across its barriers.
         const int tid = threadIdx.x;
         uint32_t is, ic;
-        block_append2(ba, &P.cnt[CNT_S], &P.cnt[cnt_q(qout)], shadow, cont, is, ic);
+        block_append2(ba, &P.cnt[cnt_s(bounce & 1)], &P.cnt[cnt_q(qout)], shadow, cont, is, ic);
         if (cont) {
             // survivor: compacted into the next bounce's arrays
             stS(&P.n_ray_o[ic], stage.o[tid]);
@@ -2170,16 +1436,14 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
     }
 }
 
-__global__ void k_reset(uint32_t *cnt, int qout) {
-    // zero this bounce's output queue, the shadow queue and the fetch counters
+// zero the counters bounce b appends to (next-bounce paths qout, shadow rays
+// S(sOut); sOut < 0: none) and the work-fetch counters of its trace launch
+__global__ void k_reset(uint32_t *cnt, int qout, int sOut) {
     if (threadIdx.x == 0) {
-        cnt[qout ? CNT_Q1 : CNT_Q0] = 0;
-        cnt[CNT_S] = 0;
+        if (qout >= 0) cnt[qout ? CNT_Q1 : CNT_Q0] = 0;
+        if (sOut >= 0) cnt[sOut ? CNT_S1 : CNT_S0] = 0;
     }
-    if (threadIdx.x < XGROUPS) {
-        cnt[CNT_FETCH + 32 * threadIdx.x] = 0;
-        cnt[CNT_SFETCH + 32 * threadIdx.x] = 0;
-    }
+    if (threadIdx.x < XGROUPS) cnt[CNT_FETCH + 32 * threadIdx.x] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -2222,7 +1486,7 @@ struct mtsg_scene {
     int cuCount = 0;
     int traceGrid = 0, shadeGrid = 0;
     uint32_t flags = 0;
-    int traceMode = 16;           // speculative compact traversal over two-level blocks, refill at 16 idle lanes (measured best)
+    int traceMode = 0;            // 0: refill at 16 idle lanes (measured best), 1: at 32
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
     mtsg_stats stats{};
@@ -2299,44 +1563,18 @@ void timed_launch(mtsg_scene *s, int kind, F f) {
     s->timed.emplace_back(kind, i0);
 }
 
-// Traversal kernel variants (MTSG_TRACE_MODE, for measurement):
-//   0 = wave fetch 64 / atomic, 1 = wave fetch 4x64 / atomic,
-//   2 = lane refill at >= 1 idle lane, 3 = lane refill at >= 32 idle lanes,
-//   4 = as 3 with indexed leaves (compact tree, one extra dependent load),
-//   5/6/7 = unified one-node-or-one-primitive iterations, refill at 32/16/8 idle lanes,
-//   8/9/10/11 = phase-separated iterations, primitive phase once
-//               primLanes >= nodeLanes x 1 / 0.5 / 0.25 / 2,
-//   12/13 = unified iterations over the two-level block layout, refill at 16/32,
-//   14/15 = speculative unified iterations over the two-level layout, refill at 16/32,
-//   16/17 = speculative with compact state (k_trace_s), refill at 16/32
-template <bool SHADOW, bool COUNT>
-void launch_trace_c(mtsg_scene *s, const DevPaths &P, int qin, uint32_t n) {
+// One traversal launch over a work list (see k_trace_s): closest rays cIn,
+// shadow rays sIn.  traceMode 1 refills lanes at 32 idle lanes instead of 16
+// (MTSG_TRACE_MODE, for measurement).
+template <bool COUNT>
+void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t n) {
     dim3 g(s->traceGrid), blk(TRACE_BLOCK);
-    switch (s->traceMode) {
-        case 0: hipLaunchKernelGGL((k_trace_wave<SHADOW, COUNT, 1>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 1: hipLaunchKernelGGL((k_trace_wave<SHADOW, COUNT, 4>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 2: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 1>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 4: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 5: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 6: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 7: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 8>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 8: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 4>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 9: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 8>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 10: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 16>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 11: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 2>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 12: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 0, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 13: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 32, 0, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 14: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 16, 0, true, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 15: hipLaunchKernelGGL((k_trace_u<SHADOW, COUNT, 32, 0, true, true>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 16: hipLaunchKernelGGL((k_trace_s<SHADOW, COUNT, 16>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        case 17: hipLaunchKernelGGL((k_trace_s<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-        default: hipLaunchKernelGGL((k_trace<SHADOW, COUNT, 32>), g, blk, 0, s->stream, s->ds, P, qin, n); break;
-    }
+    if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, s->stream, s->ds, P, cIn, sIn, n);
+    else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, s->stream, s->ds, P, cIn, sIn, n);
 }
-template <bool SHADOW>
-void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int qin, uint32_t n) {
-    if (count) launch_trace_c<SHADOW, true>(s, P, qin, n);
-    else launch_trace_c<SHADOW, false>(s, P, qin, n);
+void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn, uint32_t n) {
+    if (count) launch_trace_c<true>(s, P, cIn, sIn, n);
+    else launch_trace_c<false>(s, P, cIn, sIn, n);
 }
 
 int validate(const mtsg_render_params *p, const mtsg_scene *s) {
@@ -2414,29 +1652,31 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             });
             const int maxBounces = p->max_depth > 0 ? p->max_depth : 1 << 30;
             int last = -1;
-            // bounce b consumes queue qin(b) (identity for b = 0) and produces qout(b) = (b & 1) ^ 1
+            // bounce b: one trace launch over this bounce's closest rays (work
+            // list qin(b), identity for b = 0) and bounce b-1's shadow rays
+            // (S((b-1) & 1)), then k_shade appends the next bounce's paths to
+            // qout(b) = (b & 1) ^ 1 and its shadow rays to S(b & 1)
             auto account = [&](int bb) {
                 const uint32_t *hc = s->hostCnt + HOSTCNT_STRIDE * (bb & 1);
                 const uint32_t consumed = bb == 0 ? B.nslots : hc[(bb & 1) ? CNT_Q1 : CNT_Q0];
                 s->stats.rays_closest += consumed;
-                s->stats.rays_shadow += hc[CNT_S];
+                s->stats.rays_shadow += hc[cnt_s(bb & 1)];
                 s->stats.launches_trace_closest++;
                 return hc[((bb & 1) ^ 1) ? CNT_Q1 : CNT_Q0];
             };
             for (int b = 0; b < maxBounces; ++b) {
                 const int qin = b == 0 ? -1 : (b & 1);
                 const int qout = (b & 1) ^ 1;
-                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, qout);
-                timed_launch(s, K_CLOSEST, [&]() { launch_trace<false>(s, count, P, qin, B.nslots); });
+                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, qout, b & 1);
+                timed_launch(s, K_CLOSEST, [&]() { launch_trace(s, count, P, qin, b == 0 ? -1 : ((b - 1) & 1), B.nslots); });
                 timed_launch(s, K_SHADE, [&]() {
                     if (s->ds.has_env)
                         hipLaunchKernelGGL(k_shade<true>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
                     else
                         hipLaunchKernelGGL(k_shade<false>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
                 });
-                timed_launch(s, K_SHADOW, [&]() { launch_trace<true>(s, count, P, 0, 0u); });
                 swap_bounce(P);
-                HIP_TRY(hipMemcpyAsync(s->hostCnt + HOSTCNT_STRIDE * (b & 1), P.cnt, (CNT_S + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(hipMemcpyAsync(s->hostCnt + HOSTCNT_STRIDE * (b & 1), P.cnt, (CNT_S1 + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
                 HIP_TRY(hipEventRecord(cntEv[b & 1], s->stream));
                 last = b;
                 if (b >= 1) {
@@ -2446,6 +1686,10 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 }
             }
             if (last >= 0) {
+                // the last bounce's shadow rays
+                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, -1, -1);
+                timed_launch(s, K_SHADOW, [&]() { launch_trace(s, count, P, -2, last & 1, 0u); });
+                s->stats.launches_trace_shadow++;
                 HIP_TRY(hipEventSynchronize(cntEv[last & 1]));
                 account(last);
             }
@@ -2571,11 +1815,8 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         vnrm[i] = make_float4(d->vtx_nrm[3 * i], d->vtx_nrm[3 * i + 1], d->vtx_nrm[3 * i + 2], 0.f);
     }
     std::vector<uint4> tidx(d->n_triangles);
-    std::vector<float4> tdpdu(d->n_triangles);
-    for (uint32_t t = 0; t < d->n_triangles; ++t) {
+    for (uint32_t t = 0; t < d->n_triangles; ++t)
         tidx[t] = make_uint4(d->tri_idx[3 * t], d->tri_idx[3 * t + 1], d->tri_idx[3 * t + 2], 0);
-        tdpdu[t] = make_float4(d->tri_dpdu[3 * t], d->tri_dpdu[3 * t + 1], d->tri_dpdu[3 * t + 2], 0.f);
-    }
     for (uint32_t sh = 0; sh < d->n_shapes; ++sh)
         if (d->shapes[sh].type == MTSG_SHAPE_MESH)
             for (uint32_t t = 0; t < d->shapes[sh].tri_count; ++t) tidx[d->shapes[sh].tri_begin + t].w = sh;
@@ -2606,18 +1847,16 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         return r;
     };
     // ---- device kd-tree layout from Mitsuba's KDNode array (same splits and
-    // leaves, re-laid out): sibling pairs + leaf-ordered TriAccel copies
-    std::vector<uint4> pairs, pairsIdx;
+    // leaves, re-laid out): sibling pairs (host only, the input of the
+    // two-level blocks) + leaf-ordered TriAccel copies
+    std::vector<uint4> pairs;
     std::vector<float4> triL;
     pairs.reserve(d->n_nodes / 2 + 1);
-    pairsIdx.reserve(d->n_nodes / 2 + 1);
     triL.reserve((size_t)d->n_indices * 3);
     bool layoutOk = true;
-    // returns the node in both leaf encodings: .x/.y leaf-ordered copies,
-    // .z/.w Mitsuba's index range (inner nodes are identical in both)
-    std::function<uint4(uint32_t, int)> convert = [&](uint32_t ni, int depth) -> uint4 {
+    std::function<uint2(uint32_t, int)> convert = [&](uint32_t ni, int depth) -> uint2 {
         const mtsg_kdnode &N = d->nodes[ni];
-        if (depth > 64 || ni >= d->n_nodes) { layoutOk = false; return make_uint4(0x80000000u, 0u, 0x80000000u, 0u); }
+        if (depth > 64 || ni >= d->n_nodes) { layoutOk = false; return make_uint2(0x80000000u, 0u); }
         if (N.combined & 0x80000000u) {
             const uint32_t start = (uint32_t)(triL.size() / 3);
             for (uint32_t e = N.combined & 0x7FFFFFFFu; e < N.data; ++e) {
@@ -2626,27 +1865,21 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
                 const float4 *t = (const float4 *)(d->triaccel + p);
                 triL.push_back(t[0]); triL.push_back(t[1]); triL.push_back(t[2]);
             }
-            return make_uint4(0x80000000u | start, (uint32_t)(triL.size() / 3), N.combined, N.data);
+            return make_uint2(0x80000000u | start, (uint32_t)(triL.size() / 3));
         }
         const uint32_t left = ni + ((N.combined & ~(3u | 0x40000000u)) >> 2);
         const uint32_t pi = (uint32_t)pairs.size();
         pairs.push_back(make_uint4(0, 0, 0, 0));
-        pairsIdx.push_back(make_uint4(0, 0, 0, 0));
-        const uint4 L = convert(left, depth + 1);
-        const uint4 R = convert(left + 1, depth + 1);
+        const uint2 L = convert(left, depth + 1);
+        const uint2 R = convert(left + 1, depth + 1);
         pairs[pi] = make_uint4(L.x, L.y, R.x, R.y);
-        pairsIdx[pi] = make_uint4(L.z, L.w, R.z, R.w);
-        const uint32_t inner = (N.combined & 3u) | (pi << 2);
-        return make_uint4(inner, N.data, inner, N.data);
+        return make_uint2((N.combined & 3u) | (pi << 2), N.data);
     };
-    const uint4 root4 = convert(0, 0);
-    const uint2 root = make_uint2(root4.x, root4.y);
-    ds.rootIdx = make_uint2(root4.z, root4.w);
+    const uint2 root = convert(0, 0);
     if (!layoutOk || pairs.size() >= (1u << 29) || triL.size() / 3 >= (1u << 31)) {
         g_err = "malformed or oversized kd-tree";
         return fail(MTSG_ERR_INVALID);
     }
-    if (pairs.empty()) { pairs.push_back(make_uint4(0, 0, 0, 0)); pairsIdx.push_back(make_uint4(0, 0, 0, 0)); }
     // ---- two-level blocks from the binary pair layout
     std::vector<uint4> blocks;
     blocks.reserve(pairs.size() * 2 + 8);
@@ -2671,16 +1904,12 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));   // slack for the 3-slot fetch of the last slot
     if (blocks.size() >= (1u << 29)) { g_err = "kd-tree too large for the two-level layout"; return fail(MTSG_ERR_INVALID); }
     if (triL.empty()) triL.resize(3, make_float4(0, 0, 0, 0));
-    uint4 *dpairs, *dpairsIdx, *dblocks; float4 *dtriL; uint32_t *dlidx; const uint32_t zero = 0; float4 *tri; float4 *dvpos, *dvnrm, *dtdpdu, *dshrec; uint4 *dtidx;
+    uint4 *dblocks; float4 *dtriL; float4 *dvpos, *dvnrm, *dshrec; uint4 *dtidx;
     mtsg_rect *rects; mtsg_shape *shapes; mtsg_bsdf *bsdfs; mtsg_emitter *emitters; float *ecdf, *etcdf;
-    if ((rc = up(pairs.data(), pairs.size(), &dpairs)) ||
-        (rc = up(triL.data(), triL.size(), &dtriL)) ||
-        (rc = up(pairsIdx.data(), pairsIdx.size(), &dpairsIdx)) ||
+    if ((rc = up(triL.data(), triL.size(), &dtriL)) ||
         (rc = up(blocks.data(), blocks.size(), &dblocks)) ||
-        (rc = d->n_indices ? up(d->indices, d->n_indices, &dlidx) : up(&zero, 1, &dlidx)) ||
-        (rc = up((const float4 *)d->triaccel, (size_t)d->n_prims * 3, &tri)) ||
         (rc = up(vpos.data(), vpos.size(), &dvpos)) || (rc = up(vnrm.data(), vnrm.size(), &dvnrm)) ||
-        (rc = up(tidx.data(), tidx.size(), &dtidx)) || (rc = up(tdpdu.data(), tdpdu.size(), &dtdpdu)) ||
+        (rc = up(tidx.data(), tidx.size(), &dtidx)) ||
         (rc = up(shrec.data(), shrec.size(), &dshrec)) ||
         (rc = up(d->rects, d->n_rects, &rects)) || (rc = up(d->shapes, d->n_shapes, &shapes)) ||
         (rc = up(d->bsdfs, d->n_bsdfs, &bsdfs)) || (rc = up(d->emitters, d->n_emitters, &emitters)) ||
@@ -2688,8 +1917,8 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         (rc = up(d->emitter_tri_cdf, d->n_emitter_tri_cdf, &etcdf)))
         return fail(rc);
     ds.blocks = dblocks; ds.root2 = root2;
-    ds.pairs = dpairs; ds.triL = dtriL; ds.root = root; ds.pairsIdx = dpairsIdx; ds.lidx = dlidx; ds.tri = tri; ds.vpos = dvpos; ds.vnrm = dvnrm;
-    ds.tidx = dtidx; ds.tdpdu = dtdpdu; ds.shrec = dshrec; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
+    ds.triL = dtriL; ds.vpos = dvpos; ds.vnrm = dvnrm;
+    ds.tidx = dtidx; ds.shrec = dshrec; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
     // environment emitter tables (envmap.h)
     ds.has_env = d->has_envmap ? 1 : 0;
@@ -2731,10 +1960,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     // persistent grids from the occupancy query
     if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     int perCU = 0;
-    const void *occKernel = s->traceMode >= 16 ? (const void *)k_trace_s<false, false, 16>
-                          : s->traceMode >= 14 ? (const void *)k_trace_u<false, false, 16, 0, true, true>
-                          : s->traceMode >= 12 ? (const void *)k_trace_u<false, false, 16, 0, true>
-                          : s->traceMode >= 5 ? (const void *)k_trace_u<false, false, 32> : (const void *)k_trace<false, false, 32>;
+    const void *occKernel = (const void *)k_trace_s<false, 16>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, occKernel, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;
@@ -2875,10 +2101,10 @@ static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, fl
     if (e == hipSuccess && shadow) e = alloc((void **)&D.sh_c, f4, c.data());
     if (e == hipSuccess) e = alloc((void **)&D.cnt, CNT_WORDS * sizeof(uint32_t), nullptr);
     if (e == hipSuccess) e = alloc((void **)&D.ctr, 16 * sizeof(unsigned long long), nullptr);
-    if (e == hipSuccess && shadow) e = hipMemcpy(D.cnt + CNT_S, &n, sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && shadow) e = hipMemcpy(D.cnt + CNT_S0, &n, sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) { g_err = hipGetErrorString(e); cleanup(); return MTSG_ERR_DEVICE; }
-    if (shadow) launch_trace<true>(s, false, D, 0, 0u);
-    else launch_trace<false>(s, false, D, -1, n);
+    if (shadow) launch_trace(s, false, D, -2, 0, 0u);
+    else launch_trace(s, false, D, -1, -1, n);
     e = hipStreamSynchronize(s->stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpy(out.data(), *po, f4, hipMemcpyDeviceToHost);

@@ -60,6 +60,7 @@ class Stats(C.Structure):
         ("wave_steps", C.c_uint64), ("wave_active_lanes", C.c_uint64),
         ("shadow_wave_node_iters", C.c_uint64), ("shadow_wave_test_iters", C.c_uint64),
         ("shadow_wave_steps", C.c_uint64), ("shadow_wave_active_lanes", C.c_uint64),
+        ("launches_trace_shadow", C.c_uint64),
     ]
 
 

@@ -14,6 +14,7 @@ for path in sys.argv[1:]:
     j = json.loads(line)
     k = j.get("kernels", {})
     r = j.get("roofline") or {}
-    print(f"{j['value']:.1f} Ms/s  closest {k.get('trace_closest_ms', 0):.1f} shadow {k.get('trace_shadow_ms', 0):.1f} "
+    tr = k.get("trace_ms", k.get("trace_closest_ms", 0) + k.get("trace_shadow_ms", 0))
+    print(f"{j['value']:.1f} Ms/s  trace {tr:.1f} "
           f"shade {k.get('shade_ms', 0):.1f} splat {k.get('splat_ms', 0):.1f} cam {k.get('camera_ms', 0):.1f} "
           f"frame {k.get('frame_ms', 0):.1f}  GB/s {r.get('achieved', 0)}")
