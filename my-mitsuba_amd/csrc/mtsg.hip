@@ -140,6 +140,10 @@ DEV int cnt_q(int q) { return q ? CNT_Q1 : CNT_Q0; }
 
 constexpr int TILE = 16;                    // splat tile edge (256 pixels)
 constexpr int BLOCK = 256;
+#ifndef MTSG_SHADE_BLOCK
+#define MTSG_SHADE_BLOCK 256
+#endif
+constexpr int SHADE_BLOCK = MTSG_SHADE_BLOCK;   // k_shade workgroup size
 constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traversal
 // Paths per wavefront batch (272 B of state per path; 2^28 paths = 73 GB
 // of the 288 GB HBM, capped at 60% of free device memory at run time).
@@ -205,11 +209,6 @@ DEV uint32_t lane_id() { return __lane_id(); }
 // ---------------------------------------------------------------------------
 // primitive tests
 // ---------------------------------------------------------------------------
-// Make three values opaque to the optimiser (no instruction): a select
-// between struct members is otherwise folded into a load through a selected
-// address, which demotes the whole ray state to scratch.
-DEV void launder3(float &a, float &b, float &c) { asm("" : "+v"(a), "+v"(b), "+v"(c)); }
-
 // TriAccel::rayIntersect (triaccel.h:96-158)
 DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, float3 d, float mint, float maxt,
                   float &u, float &v, float &t) {
@@ -219,8 +218,6 @@ DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, f
     // (u, v, k) = (1,2,0) | (2,0,1) | (0,1,2): a rotation of (x, y, z) by k, so
     // two compares and two selects per component (k >= 3 never hits)
     const bool k0 = k == 0u, k1 = k == 1u;
-    launder3(o.x, o.y, o.z);
-    launder3(d.x, d.y, d.z);
     const float o_k = k0 ? o.x : (k1 ? o.y : o.z), d_k = k0 ? d.x : (k1 ? d.y : d.z);
     const float o_u = k0 ? o.y : (k1 ? o.z : o.x), d_u = k0 ? d.y : (k1 ? d.z : d.x);
     const float o_v = k0 ? o.z : (k1 ? o.x : o.y), d_v = k0 ? d.z : (k1 ? d.x : d.y);
@@ -442,9 +439,7 @@ DEV void spec_plan(const SpecRay &r, uint2 n, float &tsplit, bool &goLeft, bool 
     const uint32_t axis = n.x & 3u;
     const float split = __uint_as_float(n.y);
     const bool a0 = axis == 0u, a1 = axis == 1u;
-    float ox = r.o.x, oy = r.o.y, oz = r.o.z, ix = r.inv.x, iy = r.inv.y, iz = r.inv.z;
-    launder3(ox, oy, oz);
-    launder3(ix, iy, iz);
+    const float ox = r.o.x, oy = r.o.y, oz = r.o.z, ix = r.inv.x, iy = r.inv.y, iz = r.inv.z;
     const float oa = a0 ? ox : (a1 ? oy : oz);
     const float ia = a0 ? ix : (a1 ? iy : iz);
     tsplit = (split - oa) * ia;
@@ -488,7 +483,7 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     const uint32_t off = rootKind ? 2u - (uint32_t)goLeft : 0u;
     const uint32_t pi = prim ? r.lfE : 0u;
     const uint4 p0 = S.blocks[base], pc = S.blocks[base + off];
-    const float4 *rec = S.triL + 3 * (size_t)pi;
+    const float4 *rec = S.triL + (size_t)(3u * pi);   // < 2^32: checked at upload
     const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
     asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
                  "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
@@ -1119,9 +1114,9 @@ DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p
 
 // outgoing records of one workgroup (36 KB: 4 workgroups per CU at 4 waves/SIMD)
 struct ShadeStage {
-    float4 o[BLOCK], d[BLOCK], T[BLOCK], aux[BLOCK], L[BLOCK];
-    uint4 meta[BLOCK];
-    float4 sho[BLOCK], shd[BLOCK], shc[BLOCK];
+    float4 o[SHADE_BLOCK], d[SHADE_BLOCK], T[SHADE_BLOCK], aux[SHADE_BLOCK], L[SHADE_BLOCK];
+    uint4 meta[SHADE_BLOCK];
+    float4 sho[SHADE_BLOCK], shd[SHADE_BLOCK], shc[SHADE_BLOCK];
 };
 
 // qin < 0: bounce 0 over the identity queue of nIdentity slots
@@ -1129,9 +1124,9 @@ struct ShadeStage {
 #define MTSG_SHADE_WAVES 4   // 127 VGPRs: 4 waves/SIMD (3 at 144; 5+ spill heavily)
 #endif
 #if MTSG_SHADE_WAVES > 0
-#define SHADE_ATTR __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SHADE_WAVES)))
+#define SHADE_ATTR __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SHADE_WAVES)))
 #else
-#define SHADE_ATTR __launch_bounds__(BLOCK)
+#define SHADE_ATTR __launch_bounds__(SHADE_BLOCK)
 #endif
 // ENV: the scene has an environment emitter (the variant without it keeps
 // the environment code, and its registers, out of the common case)
@@ -1671,9 +1666,9 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 timed_launch(s, K_CLOSEST, [&]() { launch_trace(s, count, P, qin, b == 0 ? -1 : ((b - 1) & 1), B.nslots); });
                 timed_launch(s, K_SHADE, [&]() {
                     if (s->ds.has_env)
-                        hipLaunchKernelGGL(k_shade<true>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+                        hipLaunchKernelGGL(k_shade<true>, dim3(s->shadeGrid), dim3(SHADE_BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
                     else
-                        hipLaunchKernelGGL(k_shade<false>, dim3(s->shadeGrid), dim3(BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+                        hipLaunchKernelGGL(k_shade<false>, dim3(s->shadeGrid), dim3(SHADE_BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
                 });
                 swap_bounce(P);
                 HIP_TRY(hipMemcpyAsync(s->hostCnt + HOSTCNT_STRIDE * (b & 1), P.cnt, (CNT_S1 + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
@@ -1876,7 +1871,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         return make_uint2((N.combined & 3u) | (pi << 2), N.data);
     };
     const uint2 root = convert(0, 0);
-    if (!layoutOk || pairs.size() >= (1u << 29) || triL.size() / 3 >= (1u << 31)) {
+    if (!layoutOk || pairs.size() >= (1u << 29) || triL.size() / 3 >= (1u << 30)) {
         g_err = "malformed or oversized kd-tree";
         return fail(MTSG_ERR_INVALID);
     }
@@ -1964,7 +1959,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, occKernel, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;
-    s->shadeGrid = s->cuCount * 8;
+    s->shadeGrid = s->cuCount * 8 * 256 / SHADE_BLOCK;
     if (hipHostMalloc((void **)&s->hostCnt, 2 * HOSTCNT_STRIDE * sizeof(uint32_t)) != hipSuccess) { g_err = "pinned alloc"; return fail(MTSG_ERR_OOM); }
     *out = s;
     return MTSG_OK;

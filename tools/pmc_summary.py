@@ -8,10 +8,8 @@ from collections import defaultdict
 
 
 def family(name):
-    m = re.search(r"(k_trace\w*)<?I?L?b?([01])?", name)
     if "k_trace" in name:
-        shadow = "ILb1" in name or "<true" in name
-        return "trace_shadow" if shadow else "trace_closest"
+        return "trace"
     for k in ("k_shade", "k_splat", "k_camera", "k_reset"):
         if k in name:
             return k[2:]
