@@ -170,6 +170,34 @@ typedef struct mtsg_camera {
     int32_t pad[3];
 } mtsg_camera;
 
+/* Sampler.  The path's sample dimensions are drawn in the
+ * order of Li's next1D / next2D calls (DESIGN.md "Random numbers"):
+ *   independent  src/samplers/independent.cpp:51-116, counter-mode draws
+ *   halton       src/samplers/halton.cpp:101-404: radical inverse in the
+ *                dim-th prime base of index offset(pixel) + stride * s, with
+ *                the blocked space partition of setFilmResolution (:240-275)
+ *   hammersley   src/samplers/hammersley.cpp:90-300: first dimension s / N,
+ *                then radical inverses in the prime bases
+ *   ldsampler    src/samplers/ldsampler.cpp:80-245: Kollig-Keller scrambled
+ *                (0,2)-sequence, per-pixel random scramble and shuffle per
+ *                dimension (1D and 2D requests counted separately), drawn
+ *                from the counter RNG instead of a per-thread SFMT stream
+ * Halton / Hammersley digit permutations (faure.cpp:23-140): scramble -1 =
+ * Faure permutations (the default), 0 = none, otherwise random permutations
+ * from sampleTEA seeded with the scramble value. */
+enum {
+    MTSG_SAMPLER_INDEPENDENT = 0, MTSG_SAMPLER_HALTON = 1, MTSG_SAMPLER_HAMMERSLEY = 2,
+    MTSG_SAMPLER_LDSAMPLER = 3
+};
+#define MTSG_QMC_PRIMES 1024          /* primeTableSize (qmc.h:38)            */
+
+typedef struct mtsg_sampler {
+    int32_t type;                 /* MTSG_SAMPLER_*                          */
+    int32_t scramble;             /* halton / hammersley (default -1)        */
+    int32_t dimension;            /* ldsampler low-discrepancy dimensions (4) */
+    int32_t pad;
+} mtsg_sampler;
+
 typedef struct mtsg_scene_desc {
     uint32_t abi_version;         /* = MTSG_ABI_VERSION                     */
     uint32_t n_vertices;
@@ -207,6 +235,13 @@ typedef struct mtsg_scene_desc {
     const float *env_cdf_cols;    /* (level-0 width + 1) * height            */
     const float *env_row_weights; /* height                                  */
     mtsg_envmap envmap;
+    /* sampler and the quasi-Monte Carlo tables (halton / hammersley) */
+    mtsg_sampler sampler;
+    const uint32_t *qmc_primes;   /* MTSG_QMC_PRIMES primes                  */
+    const uint32_t *qmc_perm_offset; /* MTSG_QMC_PRIMES offsets into qmc_perm */
+    const uint16_t *qmc_perm;     /* digit permutation of base primes[i] at
+                                     qmc_perm + qmc_perm_offset[i]; NULL when
+                                     unscrambled (scramble 0) or unused     */
 } mtsg_scene_desc;
 
 /* ---- render ------------------------------------------------------------- */
@@ -318,6 +353,14 @@ int  mtsg_set_batch_paths(mtsg_scene *scene, uint32_t paths);
  * EWA lookup with those differential directions (camera rays).
  * EnvironmentMap::evalEnvironment, src/emitters/envmap.cpp:380-410. */
 int  mtsg_env_eval(mtsg_scene *scene, uint32_t n, const float *dirs, const float *rx, const float *ry, float *out);
+
+/* Debug: the scene sampler's draws for sample s of film pixel (x, y): kinds[i]
+ * = 1 (next1D, one float out) or 2 (next2D, two floats), in call order, as
+ * Sampler::next1D / next2D after Sampler::generate(pos) + setSampleIndex(s)
+ * (src/librender/sampler.cpp; samplers per mtsg_sampler).  params gives spp
+ * and seed.  The first next2D is the camera's pixel jitter. */
+int  mtsg_sampler_draws(mtsg_scene *scene, const mtsg_render_params *params, int x, int y, uint32_t s,
+                        uint32_t n, const int32_t *kinds, float *out);
 
 int  mtsg_trace_closest(mtsg_scene *scene, uint32_t n, const float *rays,
                         float *t, float *u, float *v, uint32_t *prim);

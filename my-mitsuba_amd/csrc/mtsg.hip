@@ -33,6 +33,7 @@
 #include "../../include/mtsg.h"
 #include "device_math.h"
 #include "envmap.h"
+#include "sampler.h"
 
 using namespace mtsg;
 
@@ -68,6 +69,9 @@ struct DevScene {
     float bmin[3], bmax[3];
     int has_env;
     DevEnv env;
+    // halton / hammersley tables (sampler.h); nullptr for the other samplers
+    const uint32_t *qmcPrimes, *qmcOff;
+    const uint16_t *qmcPerm;
 };
 
 struct DevCamera {
@@ -80,13 +84,44 @@ struct DevCamera {
     float filter_values[32];
     float dx[3], dy[3];   // near-plane differentials (perspective.cpp:160-170)
     int has_env;          // store primary-ray differentials for the environment lookup
+    int crop_w, crop_h;   // the sampler's space partition (setFilmResolution)
 };
 
 struct DevIntegrator {
     int max_depth, rr_depth, strict_normals, hide_emitters;
     uint32_t spp, seed;
     uint32_t film_w;   // sample id = (y * film_w + x) * spp + s
+    DevSampler smp;
 };
+
+// a path's sampler at sample s of film pixel (x, y), `dim` dimensions and
+// `n2` 2D requests into the path
+DEV PathSampler path_sampler(const DevIntegrator &I, int x, int y, uint32_t s, uint32_t dim, uint32_t n2) {
+    const uint64_t pix = (uint64_t)y * (uint64_t)I.film_w + (uint64_t)x;
+    return PathSampler{counterKey(I.seed, pix * I.spp + s), dim, n2, s, x, y, false};
+}
+DEV uint64_t pixel_index(const DevIntegrator &I, const PathSampler &p) {
+    return (uint64_t)p.y * (uint64_t)I.film_w + (uint64_t)p.x;
+}
+template <int KIND>
+DEV float next1D(const DevIntegrator &I, PathSampler &p) {
+    return smp_next1D<KIND>(I.smp, p, I.seed, pixel_index(I, p), I.spp);
+}
+template <int KIND>
+DEV void next2D(const DevIntegrator &I, PathSampler &p, float &a, float &b) {
+    smp_next2D<KIND>(I.smp, p, I.seed, pixel_index(I, p), I.spp, a, b);
+}
+// the camera's pixel jitter: the first 2D request of a sample (the sampler is
+// a run-time choice here; k_shade is instantiated per sampler)
+DEV void camera_jitter(const DevIntegrator &I, int x, int y, uint32_t s, float &a, float &b) {
+    PathSampler p = path_sampler(I, x, y, s, 0, 0);
+    switch (I.smp.type) {
+        case MTSG_SAMPLER_HALTON: next2D<MTSG_SAMPLER_HALTON>(I, p, a, b); break;
+        case MTSG_SAMPLER_HAMMERSLEY: next2D<MTSG_SAMPLER_HAMMERSLEY>(I, p, a, b); break;
+        case MTSG_SAMPLER_LDSAMPLER: next2D<MTSG_SAMPLER_LDSAMPLER>(I, p, a, b); break;
+        default: next2D<MTSG_SAMPLER_INDEPENDENT>(I, p, a, b); break;
+    }
+}
 
 // wavefront batch: tiles [tile0, tile0 + ntiles) x samples [s0, s0 + ns)
 struct DevBatch {
@@ -132,6 +167,7 @@ constexpr int XGROUPS = 8;                  // XCDs: blocks b and b + 8 share on
 // Q0/Q1: paths of the next bounce (ping-pong); S0/S1: shadow rays of a bounce
 // (ping-pong: bounce b appends to S(b & 1) while its trace reads S((b-1) & 1))
 constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S0 = 128, CNT_S1 = 192;
+constexpr int CNT_ERR = 96;   // sticky error flags (1: QMC dimension limit)
 constexpr int CNT_FETCH = 256;                           // XGROUPS counters, 32 words apart
 constexpr int CNT_WORDS = CNT_FETCH + 32 * XGROUPS;
 constexpr int HOSTCNT_STRIDE = 256;
@@ -660,9 +696,8 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
         slot_pixel(B, slot, x, y, s);
         alive = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
         if (alive) {
-            const uint64_t sid = ((uint64_t)y * (uint64_t)C.film_w + (uint64_t)x) * I.spp + s;
-            const uint64_t key = counterKey(I.seed, sid);
-            const float a = counterFloat(key, 0), b = counterFloat(key, 1);
+            float a, b;
+            camera_jitter(I, x, y, s, a, b);
             const float sx = ((float)x + a) * C.inv_res_x, sy = ((float)y + b) * C.inv_res_y;
             const float *m = C.s2c;
             float px = m[0] * sx + m[1] * sy + m[3], py = m[4] * sx + m[5] * sy + m[7];
@@ -692,7 +727,7 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
                 stS(&P.T[slot], make_float4(1.f, 1.f, 1.f, 1.f));
             }
             stS(&P.Lp[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
-            stS(&P.meta[slot], make_uint4(1u, 2u, slot, 0u));   // depth 1, next dimension 2
+            stS(&P.meta[slot], make_uint4(1u, 2u, slot, 1u));   // depth 1, 2 dimensions in one 2D request
         } else {
             // dead slot: bounce 0 runs over all slots and skips it
             stS(&P.ray_d[slot], make_float4(0.f, 0.f, 1.f, -1.0f));
@@ -1130,7 +1165,8 @@ struct ShadeStage {
 #endif
 // ENV: the scene has an environment emitter (the variant without it keeps
 // the environment code, and its registers, out of the common case)
-template <bool ENV>
+// SMP: the render's sampler (MTSG_SAMPLER_*)
+template <bool ENV, int SMP>
 __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int bounce, int qin,
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
@@ -1155,18 +1191,17 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
             const float3 ro = xyz(ro4), rd = xyz(rd4);
             float4 L4 = ldS(&P.Lp[i]);
             float4 T4 = ldS(&P.T[i]);
-            uint64_t key;
+            PathSampler smp;
             {
                 int x, y;
                 uint32_t sIdx;
                 slot_pixel(B, slot, x, y, sIdx);
-                key = counterKey(I.seed, ((uint64_t)y * (uint64_t)I.film_w + (uint64_t)x) * I.spp + sIdx);
+                smp = path_sampler(I, x, y, sIdx, meta.y, meta.w);
             }
             float3 L = xyz(L4), T = xyz(T4);
             float eta = T4.w;
             uint32_t depth = meta.x & 0xFFFFu;
             uint32_t flags = meta.x & 0xFFFF0000u;
-            uint32_t dim = meta.y;
             const bool valid = __float_as_uint(h.w) != 0xFFFFFFFFu;
             bool done = false;
             Its its;
@@ -1217,7 +1252,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                     }
                     if (depth++ >= (uint32_t)I.rr_depth) {
                         float q = fminf(maxc(T) * eta * eta, 0.95f);
-                        if (counterFloat(key, dim++) >= q) done = true;
+                        if (next1D<SMP>(I, smp) >= q) done = true;
                         else T = T / q;
                     }
                 }
@@ -1236,7 +1271,8 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                     const float3 refN = bsdf.ref_n_zero ? mk3(0, 0, 0) : its.sh.n;
                     // ---- direct illumination (path.cpp:172-200)
                     if (bsdf.smooth) {
-                        float sx = counterFloat(key, dim++), sy = counterFloat(key, dim++);
+                        float sx, sy;
+                        next2D<SMP>(I, smp, sx, sy);
                         float emPdf;
                         const uint32_t ei = pmf_sample_reuse(S.emitter_cdf, S.n_emitters, sx, emPdf);
                         const mtsg_emitter &E = S.emitters[ei];
@@ -1276,7 +1312,8 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                         }
                     }
                     // ---- BSDF sampling (path.cpp:206-221)
-                    float sx = counterFloat(key, dim++), sy = counterFloat(key, dim++);
+                    float sx, sy;
+                    next2D<SMP>(I, smp, sx, sy);
                     BsdfSample bs;
                     if (!bsdf_sample(bsdf, wi, sx, sy, bs)) {
                         done = true;
@@ -1297,11 +1334,13 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                     }
                 }
             }
+            if ((SMP == MTSG_SAMPLER_HALTON || SMP == MTSG_SAMPLER_HAMMERSLEY) && smp.dimError)
+                atomicOr(&P.cnt[CNT_ERR], 1u);   // the render fails as Mitsuba's Log(EError) would
             const float4 finalL = make_float4(L.x, L.y, L.z, L4.w);
             if (cont) {
                 stage.T[threadIdx.x] = make_float4(T.x, T.y, T.z, eta);
                 stage.L[threadIdx.x] = finalL;
-                stage.meta[threadIdx.x] = make_uint4(depth | flags, dim, slot, 0u);
+                stage.meta[threadIdx.x] = make_uint4(depth | flags, smp.dim, slot, smp.n2);
             } else {
                 stS(&P.L[slot], finalL);   // path ended: its sample's final radiance
             }
@@ -1378,13 +1417,14 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
         for (uint32_t sl = sBeg; sl < sEnd; ++sl) {
             const uint32_t slot = ((uint32_t)tl * B.ns + sl) * (TILE * TILE) + pix;
             const float4 L = ldS(&P.L[slot]);
-            const uint64_t key = counterKey(I.seed, ((uint64_t)y * (uint64_t)I.film_w + (uint64_t)x) * I.spp + B.s0 + sl);
+            float ja, jb;
+            camera_jitter(I, x, y, B.s0 + sl, ja, jb);
             // invalid samples are rejected (imageblock.h:147-151)
             if (!(isfinite(L.x) && isfinite(L.y) && isfinite(L.z) && L.x >= 0 && L.y >= 0 && L.z >= 0)) continue;
             // sample position relative to the window origin, as ImageBlock::put
             // computes it relative to the block origin (imageblock.h:158-160)
-            const float px = ((float)x + counterFloat(key, 0)) - 0.5f - (float)(x - R);
-            const float py = ((float)y + counterFloat(key, 1)) - 0.5f - (float)(y - R);
+            const float px = ((float)x + ja) - 0.5f - (float)(x - R);
+            const float py = ((float)y + jb) - 0.5f - (float)(y - R);
             float wx[K], wy[K];
 #pragma unroll
             for (int c = 0; c < K; ++c) {
@@ -1481,6 +1521,8 @@ struct mtsg_scene {
     int cuCount = 0;
     int traceGrid = 0, shadeGrid = 0;
     uint32_t flags = 0;
+    int samplerType = MTSG_SAMPLER_INDEPENDENT, samplerDim = 4;
+    int qmcInv[2][3] = {{0, 0, 0}, {0, 0, 0}};
     int traceMode = 0;            // 0: refill at 16 idle lanes (measured best), 1: at 32
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
@@ -1572,9 +1614,80 @@ void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn
     else launch_trace_c<false>(s, P, cIn, sIn, n);
 }
 
+template <bool ENV>
+void launch_shade_env(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin) {
+    dim3 g(s->shadeGrid), blk(SHADE_BLOCK);
+    switch (I.smp.type) {
+        case MTSG_SAMPLER_HALTON:
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HALTON>), g, blk, 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            break;
+        case MTSG_SAMPLER_HAMMERSLEY:
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HAMMERSLEY>), g, blk, 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            break;
+        case MTSG_SAMPLER_LDSAMPLER:
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_LDSAMPLER>), g, blk, 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            break;
+        default:
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_INDEPENDENT>), g, blk, 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+    }
+}
+void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin) {
+    if (s->ds.has_env) launch_shade_env<true>(s, I, B, P, b, qin);
+    else launch_shade_env<false>(s, I, B, P, b, qin);
+}
+
+// Sampler constants of a render (setFilmResolution with blocked = true over
+// the film's crop size: halton.cpp:240-271, hammersley.cpp:181-200)
+DevSampler make_sampler(const mtsg_scene *s, uint32_t spp) {
+    DevSampler S{};
+    S.type = s->samplerType;
+    S.ldDim = s->samplerDim;
+    while ((1u << S.ldBits) < spp) ++S.ldBits;
+    S.stride = 1;
+    S.primes = s->ds.qmcPrimes;
+    S.off = s->ds.qmcOff;
+    S.perm = s->ds.qmcPerm;
+    for (int b = 0; b < 2; ++b)
+        for (int j = 0; j < 3; ++j) S.inv[b][j] = (uint16_t)s->qmcInv[b][j];
+    const int crop[2] = {s->cam.crop_w, s->cam.crop_h};
+    if (S.type == MTSG_SAMPLER_HALTON) {
+        const uint32_t primes[2] = {2, 3};
+        for (int i = 0; i < 2; ++i) {
+            uint32_t value = 1, e = 0;
+            while ((int)value < std::min(crop[i], 128)) { value *= primes[i]; ++e; }
+            S.primePow[i] = value;
+            S.primeExp[i] = e;
+            S.stride *= value;
+        }
+        // multiplicativeInverse (halton.cpp:211-234)
+        auto inv = [](int64_t a, int64_t n) {
+            int64_t t = 0, nt = 1, r = n, nr = a % n;
+            while (nr) { int64_t q = r / nr; std::swap(t, nt); nt -= q * t; std::swap(r, nr); nr -= q * r; }
+            return (uint32_t)(t < 0 ? t + n : t);
+        };
+        S.multInv[0] = S.primePow[0] > 1 ? inv(S.primePow[1], S.primePow[0]) : 0;
+        S.multInv[1] = S.primePow[1] > 1 ? inv(S.primePow[0], S.primePow[1]) : 0;
+    } else if (S.type == MTSG_SAMPLER_HAMMERSLEY) {
+        for (int i = 0; i < 2; ++i) {
+            uint32_t r = 1;
+            while (r < (uint32_t)crop[i]) r <<= 1;
+            S.res[i] = std::min<uint32_t>(128, r);
+        }
+        S.logH = 0;
+        while ((1u << (S.logH + 1)) <= S.res[1]) ++S.logH;
+        S.factor = 1.0f / (float)((size_t)spp * S.res[0] * S.res[1]);
+        S.stride = S.res[1];
+    }
+    return S;
+}
+
 int validate(const mtsg_render_params *p, const mtsg_scene *s) {
     if (!p) { g_err = "null params"; return MTSG_ERR_INVALID; }
     if (p->spp == 0) { g_err = "spp must be > 0"; return MTSG_ERR_INVALID; }
+    if (s->samplerType == MTSG_SAMPLER_LDSAMPLER && (p->spp & (p->spp - 1))) {
+        g_err = "ldsampler: the sample count must be a power of two";
+        return MTSG_ERR_INVALID;
+    }
     if (p->rr_depth <= 0) { g_err = "'rrDepth' must be set to a value greater than zero!"; return MTSG_ERR_INVALID; }
     if (p->max_depth <= 0 && p->max_depth != -1) { g_err = "'maxDepth' must be set to -1 (infinite) or a value greater than zero!"; return MTSG_ERR_INVALID; }
     if (p->tile_w <= 0 || p->tile_h <= 0 || p->tile_x < 0 || p->tile_y < 0 ||
@@ -1616,7 +1729,8 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     const uint32_t tilesPerBatch = std::max(1u, (ntiles + nTileBatches - 1) / nTileBatches);
     if ((rc = ensure_batch(s, tilesPerBatch * sppPerBatch * TILE * TILE)) != MTSG_OK) return rc;
     const int blockW = p->tile_w + 2 * s->cam.border, blockH = p->tile_h + 2 * s->cam.border;
-    DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed, (uint32_t)s->cam.film_w};
+    DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed, (uint32_t)s->cam.film_w,
+                    make_sampler(s, p->spp)};
     memset(&s->stats, 0, sizeof(s->stats));
     s->evUsed = 0;
     s->timed.clear();
@@ -1664,12 +1778,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 const int qout = (b & 1) ^ 1;
                 hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, qout, b & 1);
                 timed_launch(s, K_CLOSEST, [&]() { launch_trace(s, count, P, qin, b == 0 ? -1 : ((b - 1) & 1), B.nslots); });
-                timed_launch(s, K_SHADE, [&]() {
-                    if (s->ds.has_env)
-                        hipLaunchKernelGGL(k_shade<true>, dim3(s->shadeGrid), dim3(SHADE_BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
-                    else
-                        hipLaunchKernelGGL(k_shade<false>, dim3(s->shadeGrid), dim3(SHADE_BLOCK), 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
-                });
+                timed_launch(s, K_SHADE, [&]() { launch_shade(s, I, B, P, b, qin); });
                 swap_bounce(P);
                 HIP_TRY(hipMemcpyAsync(s->hostCnt + HOSTCNT_STRIDE * (b & 1), P.cnt, (CNT_S1 + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
                 HIP_TRY(hipEventRecord(cntEv[b & 1], s->stream));
@@ -1687,6 +1796,12 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 s->stats.launches_trace_shadow++;
                 HIP_TRY(hipEventSynchronize(cntEv[last & 1]));
                 account(last);
+                // the error word is sticky within the batch: the last copy holds it
+                if (s->hostCnt[HOSTCNT_STRIDE * (last & 1) + CNT_ERR]) {
+                    g_err = "Lookup dimension exceeds the prime number table size! "
+                            "You may have to reduce the 'maxDepth' parameter of your integrator.";
+                    result = MTSG_ERR_INVALID;
+                }
             }
             timed_launch(s, K_SPLAT, [&]() {
                 dim3 g(B.ntiles, (B.ns + SPLAT_CHUNK - 1) / SPLAT_CHUNK);
@@ -1952,6 +2067,31 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     memcpy(c.dx, hc.dx, sizeof(c.dx));
     memcpy(c.dy, hc.dy, sizeof(c.dy));
     c.has_env = d->has_envmap ? 1 : 0;
+    c.crop_w = hc.crop_w; c.crop_h = hc.crop_h;
+    // sampler and its quasi-Monte Carlo tables
+    s->samplerType = d->sampler.type;
+    s->samplerDim = d->sampler.dimension;
+    if (s->samplerType < MTSG_SAMPLER_INDEPENDENT || s->samplerType > MTSG_SAMPLER_LDSAMPLER) {
+        g_err = "unknown sampler type";
+        return fail(MTSG_ERR_INVALID);
+    }
+    if (s->samplerType == MTSG_SAMPLER_HALTON || s->samplerType == MTSG_SAMPLER_HAMMERSLEY) {
+        if (!d->qmc_primes || !d->qmc_perm_offset) { g_err = "sampler: missing QMC tables"; return fail(MTSG_ERR_INVALID); }
+        uint32_t *dp, *doff;
+        if ((rc = up(d->qmc_primes, MTSG_QMC_PRIMES, &dp)) || (rc = up(d->qmc_perm_offset, MTSG_QMC_PRIMES, &doff)))
+            return fail(rc);
+        s->ds.qmcPrimes = dp;
+        s->ds.qmcOff = doff;
+        if (d->qmc_perm) {
+            const size_t n = (size_t)d->qmc_perm_offset[MTSG_QMC_PRIMES - 1] + d->qmc_primes[MTSG_QMC_PRIMES - 1];
+            uint16_t *dperm;
+            if ((rc = up(d->qmc_perm, n, &dperm))) return fail(rc);
+            s->ds.qmcPerm = dperm;
+            // inverse permutations of the first two bases (faure.cpp:74-78)
+            for (int b = 0; b < 2; ++b)
+                for (uint32_t j = 0; j < d->qmc_primes[b]; ++j) s->qmcInv[b][d->qmc_perm[d->qmc_perm_offset[b] + j]] = (int)j;
+        }
+    }
     // persistent grids from the occupancy query
     if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     int perCU = 0;
@@ -2141,6 +2281,73 @@ int mtsg_env_eval(mtsg_scene *s, uint32_t n, const float *dirs, const float *rx,
     if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
     cleanup();
     if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    return MTSG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+__global__ void k_sampler_draws(DevIntegrator I, int x, int y, uint32_t s, uint32_t n, const int32_t *kinds, float *out,
+                                int *err) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    PathSampler p = path_sampler(I, x, y, s, 0, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        const int t = I.smp.type;
+        if (kinds[i] == 2) {
+            float a, b;
+            if (t == MTSG_SAMPLER_HALTON) next2D<MTSG_SAMPLER_HALTON>(I, p, a, b);
+            else if (t == MTSG_SAMPLER_HAMMERSLEY) next2D<MTSG_SAMPLER_HAMMERSLEY>(I, p, a, b);
+            else if (t == MTSG_SAMPLER_LDSAMPLER) next2D<MTSG_SAMPLER_LDSAMPLER>(I, p, a, b);
+            else next2D<MTSG_SAMPLER_INDEPENDENT>(I, p, a, b);
+            *out++ = a;
+            *out++ = b;
+        } else {
+            float a;
+            if (t == MTSG_SAMPLER_HALTON) a = next1D<MTSG_SAMPLER_HALTON>(I, p);
+            else if (t == MTSG_SAMPLER_HAMMERSLEY) a = next1D<MTSG_SAMPLER_HAMMERSLEY>(I, p);
+            else if (t == MTSG_SAMPLER_LDSAMPLER) a = next1D<MTSG_SAMPLER_LDSAMPLER>(I, p);
+            else a = next1D<MTSG_SAMPLER_INDEPENDENT>(I, p);
+            *out++ = a;
+        }
+    }
+    *err = p.dimError ? 1 : 0;
+}
+}  // namespace
+
+extern "C" {
+
+int mtsg_sampler_draws(mtsg_scene *s, const mtsg_render_params *p, int x, int y, uint32_t si, uint32_t n,
+                       const int32_t *kinds, float *out) {
+    if (!s || !p || (n && (!kinds || !out)) || p->spp == 0) { g_err = "invalid arguments"; return MTSG_ERR_INVALID; }
+    if (n == 0) return MTSG_OK;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    uint32_t nOut = 0;
+    for (uint32_t i = 0; i < n; ++i) nOut += kinds[i] == 2 ? 2 : 1;
+    DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed,
+                    (uint32_t)s->cam.film_w, make_sampler(s, p->spp)};
+    int32_t *dk = nullptr;
+    float *dout = nullptr;
+    int *derr = nullptr;
+    auto cleanup = [&]() { hipFree(dk); hipFree(dout); hipFree(derr); };
+    hipError_t e = hipMalloc((void **)&dk, n * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&dout, nOut * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc((void **)&derr, sizeof(int));
+    if (e == hipSuccess) e = hipMemcpy(dk, kinds, n * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_sampler_draws, dim3(1), dim3(64), 0, s->stream, I, x, y, si, n, dk, dout, derr);
+        e = hipStreamSynchronize(s->stream);
+    }
+    int err = 0;
+    if (e == hipSuccess) e = hipMemcpy(out, dout, nOut * sizeof(float), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(&err, derr, sizeof(int), hipMemcpyDeviceToHost);
+    cleanup();
+    if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    if (err) {
+        g_err = "Lookup dimension exceeds the prime number table size! "
+                "You may have to reduce the 'maxDepth' parameter of your integrator.";
+        return MTSG_ERR_INVALID;
+    }
     return MTSG_OK;
 }
 

@@ -384,6 +384,14 @@ void Scene::finalize() {
     for (int k = 0; k < 3; ++k) { d.aabb_min[k] = tree.aabb.mn[k]; d.aabb_max[k] = tree.aabb.mx[k]; }
     d.max_depth = tree.maxDepth;
     d.camera = cam;
+    // ---------------- sampler ----------------
+    d.sampler = sampler;
+    if (sampler.type == MTSG_SAMPLER_HALTON || sampler.type == MTSG_SAMPLER_HAMMERSLEY) {
+        buildQmcTables(sampler.scramble, qmcPrimes, qmcOffsets, qmcPerm);
+        d.qmc_primes = qmcPrimes.data();
+        d.qmc_perm_offset = qmcOffsets.data();
+        d.qmc_perm = qmcPerm.empty() ? nullptr : qmcPerm.data();
+    }
     // ---------------- environment emitter ----------------
     d.has_envmap = 0;
     for (size_t i = 0; i < emitters.size(); ++i) {

@@ -14,7 +14,8 @@
 //   emitter area (area.cpp:67-78)
 //   sensor  perspective (perspective.cpp, sensor.cpp:150-262)
 //   film    hdrfilm (hdrfilm.cpp:209-220), rfilter gaussian/box
-//   sampler independent (independent.cpp:55-58)
+//   sampler independent (independent.cpp:55-58), halton (halton.cpp:113-121),
+//           hammersley (hammersley.cpp:93-101), ldsampler (ldsampler.cpp:82-95)
 //   integrator path (integrator.cpp:199-234)
 #include <algorithm>
 #include <cctype>
@@ -1008,9 +1009,28 @@ struct Loader {
                 std::vector<XNode *> sn;
                 parseProps(*n, sp, sn);
                 std::string st = lower(n->attr("type"));
-                if (st != "independent") throw err("sampler \"" + st + "\" is outside this build's scope (only 'independent')");
-                scene.samplerType = st;
+                mtsg_sampler &smp = scene.sampler;
                 scene.sampleCount = (int)sp.getInt("sampleCount", 4);
+                if (st == "independent") {
+                    smp.type = MTSG_SAMPLER_INDEPENDENT;
+                } else if (st == "halton" || st == "hammersley") {
+                    // halton.cpp:113-121, hammersley.cpp:93-101
+                    smp.type = st == "halton" ? MTSG_SAMPLER_HALTON : MTSG_SAMPLER_HAMMERSLEY;
+                    smp.scramble = (int)sp.getInt("scramble", -1);
+                } else if (st == "ldsampler") {
+                    // ldsampler.cpp:82-95: the count is rounded up to a power of two
+                    smp.type = MTSG_SAMPLER_LDSAMPLER;
+                    smp.dimension = (int)sp.getInt("dimension", 4);
+                    if (smp.dimension < 0) throw err("ldsampler: 'dimension' must be >= 0");
+                    uint32_t c = (uint32_t)std::max(1, scene.sampleCount), r = 1;
+                    while (r < c) r <<= 1;
+                    scene.sampleCount = (int)r;
+                } else {
+                    throw err("sampler \"" + st + "\" is outside this build's scope "
+                              "(independent, halton, hammersley, ldsampler)");
+                }
+                if (scene.sampleCount <= 0) throw err("sampleCount must be > 0");
+                scene.samplerType = st;
             } else {
                 throw err("unsupported element <" + n->tag + "> inside <sensor>");
             }

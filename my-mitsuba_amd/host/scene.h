@@ -128,6 +128,7 @@ struct Scene {
     IntegratorProps integrator;
     int sampleCount = 4;
     std::string samplerType = "independent";
+    mtsg_sampler sampler{MTSG_SAMPLER_INDEPENDENT, -1, 4, 0};
     KDBuildParams kd;
 
     // ---- flattened (filled by finalize()) ----
@@ -139,6 +140,8 @@ struct Scene {
     std::vector<mtsg_emitter> emitterDesc;
     std::vector<mtsg_triaccel> triaccel;
     std::vector<float> envTexels, envCdfRows, envCdfCols, envRowWeights;
+    std::vector<uint32_t> qmcPrimes, qmcOffsets;
+    std::vector<uint16_t> qmcPerm;
     KDTree tree;
     mtsg_camera camera{};
     mtsg_scene_desc desc{};
@@ -152,6 +155,12 @@ extern int g_defaultKDThreads;   // 0 = hardware concurrency
 void buildEnvmap(const Emitter &e, const float aabbMin[3], const float aabbMax[3], const float camPos[3],
                  std::vector<float> &texels, std::vector<float> &cdfRows, std::vector<float> &cdfCols,
                  std::vector<float> &rowWeights, mtsg_envmap &env);
+
+// Halton / Hammersley tables (qmc.cpp in this directory): the first 1024
+// primes, offsets of each base's digit permutation, and the permutations
+// (empty for scramble 0)
+void buildQmcTables(int scramble, std::vector<uint32_t> &primes, std::vector<uint32_t> &offsets,
+                    std::vector<uint16_t> &perm);
 
 // PFM image (src/libcore/bitmap.cpp:3764-3814): RGB float, rows top-down
 bool readPFM(const std::string &path, int &w, int &h, std::vector<float> &rgb, std::string &err);

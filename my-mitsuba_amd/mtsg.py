@@ -85,7 +85,7 @@ DEVICE_SYMBOLS = [
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
-    "mtsg_last_error", "mtsg_env_eval",
+    "mtsg_last_error", "mtsg_env_eval", "mtsg_sampler_draws",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_scene_desc", "mtsh_scene_render_params",
@@ -144,6 +144,8 @@ def device_lib() -> C.CDLL:
         lib.mtsg_trace_shadow.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
         lib.mtsg_render_samples.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
         lib.mtsg_env_eval.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.mtsg_sampler_draws.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int, C.c_uint32,
+                                           C.c_uint32, C.c_void_p, C.c_void_p]
         lib.mtsg_scene_destroy.argtypes = [C.c_void_p]
         lib.mtsg_last_error.argtypes = [C.c_char_p, C.c_size_t]
         _dev = lib
@@ -269,6 +271,15 @@ class GPUScene:
             ry = np.ascontiguousarray(ry, dtype=np.float32)
             px, py = _ptr(rx), _ptr(ry)
         self._check(device_lib().mtsg_env_eval(self._h, dirs.shape[0], _ptr(dirs), px, py, _ptr(out)), "mtsg_env_eval")
+        return out
+
+    def sampler_draws(self, params: RenderParams, x: int, y: int, s: int, kinds) -> np.ndarray:
+        """The scene sampler's next1D (kind 1) / next2D (kind 2) draws of one
+        sample, flattened (debug entry point)."""
+        kinds = np.ascontiguousarray(kinds, dtype=np.int32)
+        out = np.empty(int(np.where(kinds == 2, 2, 1).sum()), np.float32)
+        self._check(device_lib().mtsg_sampler_draws(self._h, C.byref(params), x, y, s, kinds.size, _ptr(kinds), _ptr(out)),
+                    "mtsg_sampler_draws")
         return out
 
     def trace_shadow(self, rays: np.ndarray) -> np.ndarray:

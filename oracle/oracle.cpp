@@ -313,13 +313,266 @@ inline float counterFloat(uint64_t key, uint32_t dim) {
     return x.f - 1.0f;
 }
 
+// ---------------------------------------------------------------------------
+// Quasi-Monte Carlo samplers (src/samplers/halton.cpp, hammersley.cpp,
+// ldsampler.cpp; src/libcore/qmc.cpp).  Tables come from the scene
+// description (host/qmc.cpp); the arithmetic below restates qmc.cpp.
+// ---------------------------------------------------------------------------
+constexpr float kOneMinusEps = 0x1.fffffep-1f;   // ONE_MINUS_EPS_FLT (constants.h:56)
+
+// RINV / SCRAMBLED_RINV (qmc.cpp:141-167) with a run-time base
+float radicalInverseFast(uint32_t base, uint64_t index, const uint16_t *perm) {
+#pragma clang fp contract(off)
+    const float radical = 1.0f / (float)base;
+    uint64_t value = 0;
+    float factor = 1.0f;
+    while (index) {
+        const uint64_t next = index / base;
+        const uint64_t digit = index - next * base;
+        value = value * base + (perm ? perm[digit] : digit);
+        factor *= radical;
+        index = next;
+    }
+    float inverse;
+    if (perm) inverse = factor * ((float)value + radical * (float)perm[0] / (1 - radical));
+    else inverse = (float)value * factor;
+    return std::min(inverse, kOneMinusEps);
+}
+
+// halton.cpp:195-209 / hammersley.cpp:165-179
+uint64_t inverseScrambledRadicalInverse(uint32_t base, uint64_t inverse, uint64_t digits, const uint16_t *invPerm) {
+    uint64_t index = 0;
+    while (digits) {
+        uint64_t digit = inverse % base;
+        if (invPerm) digit = invPerm[digit];
+        inverse /= base;
+        index = index * base + digit;
+        --digits;
+    }
+    return index;
+}
+
+// halton.cpp:211-234
+void extendedGCD(int64_t a, int64_t b, int64_t &x, int64_t &y) {
+    if (b == 0) { x = 1; y = 0; return; }
+    int64_t d = a / b, x_, y_;
+    extendedGCD(b, a % b, x_, y_);
+    x = y_;
+    y = x_ - d * y_;
+}
+uint64_t multiplicativeInverse(int64_t a, int64_t n) {
+    int64_t x, y;
+    extendedGCD(a, n, x, y);
+    int64_t m = x % n;
+    return (uint64_t)(m < 0 ? m + n : m);
+}
+
+// qmc.h:43-58, 82-87
+float radicalInverse2Single(uint32_t n, uint32_t scramble) {
+    n = (n << 16) | (n >> 16);
+    n = ((n & 0x00ff00ffu) << 8) | ((n & 0xff00ff00u) >> 8);
+    n = ((n & 0x0f0f0f0fu) << 4) | ((n & 0xf0f0f0f0u) >> 4);
+    n = ((n & 0x33333333u) << 2) | ((n & 0xccccccccu) >> 2);
+    n = ((n & 0x55555555u) << 1) | ((n & 0xaaaaaaaau) >> 1);
+    n = (n >> (32 - 24)) ^ (scramble & ~(0xFFFFFFFFu << 24));
+    return (float)n / (float)(1u << 24);
+}
+float sobol2Single(uint32_t n, uint32_t scramble) {
+    for (uint32_t v = 1u << 31; n != 0; n >>= 1, v ^= v >> 1)
+        if (n & 1) scramble ^= v;
+    return (float)scramble / (float)(1ull << 32);
+}
+
+// ldsampler in counter mode: the per-pixel random shuffle of each dimension's
+// sample set (ldsampler.cpp:156,178 m_random->shuffle) as a keyed bijection
+// of [0, 2^bits) (xor, odd multiply, xorshift rounds)
+uint32_t ldShuffle(uint32_t s, uint32_t bits, uint64_t h) {
+    if (bits == 0) return 0;
+    const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : (1u << bits) - 1u;
+    uint32_t x = s & mask;
+    for (uint32_t r = 0; r < 3; ++r) {
+        const uint64_t k = mix64(h + (uint64_t)(r + 1) * 0x9E3779B97F4A7C15ULL);
+        x ^= (uint32_t)k & mask;
+        x = (x * ((uint32_t)(k >> 32) | 1u)) & mask;
+        x ^= x >> ((bits + 1) / 2);
+    }
+    return x;
+}
+constexpr uint32_t kLdSalt = 0x6C64736Du;   // "ldsm": pixel keys of the ldsampler
+constexpr const char *kDimError = "Lookup dimension exceeds the prime number table size! "
+                                  "You may have to reduce the 'maxDepth' parameter of your integrator.";
+
+// Per-render sampler constants (setFilmResolution with blocked = true, as
+// Integrator::configureSampler does for a SamplingIntegrator, integrator.cpp:39-43)
+struct Qmc {
+    int type = MTSG_SAMPLER_INDEPENDENT;
+    const uint32_t *primes = nullptr, *off = nullptr;
+    const uint16_t *perm = nullptr;
+    uint16_t inv[2][3] = {{0, 0, 0}, {0, 0, 0}};   // inverse permutations of bases 2 and 3
+    // halton.cpp:240-271
+    uint64_t stride = 1, multInv[2] = {0, 0};
+    int primePow[2] = {1, 1}, primeExp[2] = {0, 0};
+    // hammersley.cpp:181-200
+    int res[2] = {1, 1};
+    uint32_t logH = 0;
+    float factor = 1.0f;
+    int ldDim = 4;
+    uint32_t ldBits = 0;
+
+    const uint16_t *permOf(uint32_t dim) const { return perm ? perm + off[dim] : nullptr; }
+
+    Qmc(const mtsg_scene_desc &d, uint32_t spp) {
+        type = d.sampler.type;
+        ldDim = d.sampler.dimension;
+        while ((1u << ldBits) < spp) ++ldBits;
+        if (type != MTSG_SAMPLER_HALTON && type != MTSG_SAMPLER_HAMMERSLEY) return;
+        primes = d.qmc_primes;
+        off = d.qmc_perm_offset;
+        perm = d.qmc_perm;
+        if (perm)
+            for (int b = 0; b < 2; ++b)
+                for (uint32_t j = 0; j < primes[b]; ++j) inv[b][perm[off[b] + j]] = (uint16_t)j;
+        const int cw = d.camera.crop_w, ch = d.camera.crop_h;
+        const int crop[2] = {cw, ch};
+        if (type == MTSG_SAMPLER_HALTON) {
+            stride = 1;
+            for (int i = 0; i < 2; ++i) {
+                int prime = (int)primes[i], value = 1, e = 0;
+                while (value < std::min(crop[i], 128)) { value *= prime; ++e; }
+                primePow[i] = value;
+                primeExp[i] = e;
+                stride *= (uint64_t)value;
+            }
+            multInv[0] = multiplicativeInverse(primePow[1], primePow[0]);
+            multInv[1] = multiplicativeInverse(primePow[0], primePow[1]);
+        } else {
+            for (int i = 0; i < 2; ++i) {
+                uint32_t r = 1;
+                while (r < (uint32_t)crop[i]) r <<= 1;   // math::roundToPowerOfTwo
+                res[i] = (int)std::min<uint32_t>(128, r);
+            }
+            logH = 0;
+            while ((1 << (logH + 1)) <= res[1]) ++logH;   // math::log2i
+            factor = 1.0f / (float)((size_t)spp * (size_t)res[0] * (size_t)res[1]);
+            stride = (uint64_t)res[1];
+        }
+    }
+
+    // generate(pos): offset of the pixel's subsequence (halton.cpp:277-293,
+    // hammersley.cpp:206-218)
+    uint64_t pixelOffset(int x, int y, uint32_t spp) const {
+        const int pp[2] = {x % 128, y % 128};
+        if (type == MTSG_SAMPLER_HALTON) {
+            if (stride <= 1) return 0;
+            uint64_t o = 0;
+            for (int i = 0; i < 2; ++i) {
+                uint64_t v = inverseScrambledRadicalInverse(primes[i], (uint64_t)pp[i], (uint64_t)primeExp[i],
+                                                            perm ? inv[i] : nullptr);
+                o += v * (stride / (uint64_t)primePow[i]) * multInv[i];
+            }
+            return o % stride;
+        }
+        if (type == MTSG_SAMPLER_HAMMERSLEY)
+            return (uint64_t)pp[0] * (uint64_t)res[1] * spp +
+                   inverseScrambledRadicalInverse(2, (uint64_t)pp[1], logH, perm ? inv[0] : nullptr);
+        return 0;
+    }
+};
+
 struct Sampler {
     int mode;
     Sfmt *sfmt = nullptr;
     uint64_t key = 0;
-    uint32_t dim = 0;
-    float next1D() { return mode == ORACLE_RNG_SFMT ? sfmt->nextFloat() : counterFloat(key, dim++); }
-    void next2D(float &a, float &b) { a = next1D(); b = next1D(); }   // independent.cpp:99-103
+    uint32_t dim = 0;             // dimensions consumed (next1D: 1, next2D: 2)
+    uint32_t n2 = 0;              // next2D calls (ldsampler keeps 1D and 2D apart)
+    const Qmc *q = nullptr;
+    int px = 0, py = 0;
+    uint32_t s = 0;
+    uint64_t offset = 0, ldKey = 0;
+
+    // start sample s of pixel (x, y) (Sampler::generate + setSampleIndex)
+    void begin(const Qmc *qmc, uint32_t seed, int film_w, uint32_t spp, int x, int y, uint32_t si) {
+        q = qmc;
+        px = x; py = y; s = si;
+        dim = 0; n2 = 0;
+        key = counterKey(seed, ((uint64_t)y * film_w + x) * spp + si);
+        offset = q ? q->pixelOffset(x, y, spp) : 0;
+        if (q && q->type == MTSG_SAMPLER_LDSAMPLER) ldKey = counterKey(seed ^ kLdSalt, (uint64_t)y * film_w + x);
+    }
+    int kind() const { return q ? q->type : MTSG_SAMPLER_INDEPENDENT; }
+    float indep() { return mode == ORACLE_RNG_SFMT ? sfmt->nextFloat() : counterFloat(key, dim); }
+    // nextFloat of halton.cpp:343-350 / hammersley.cpp:228-236
+    float qmcFloat(uint64_t idx) {
+        const uint32_t d = dim++;
+        if (q->type == MTSG_SAMPLER_HAMMERSLEY) {
+            if (d == 0) return (float)idx * q->factor;
+            return radicalInverseFast(q->primes[d - 1], idx, q->permOf(d - 1));
+        }
+        return radicalInverseFast(q->primes[d], idx, q->permOf(d));
+    }
+    float next1D() {
+        switch (kind()) {
+            case MTSG_SAMPLER_HALTON:
+            case MTSG_SAMPLER_HAMMERSLEY:
+                if (dim >= MTSG_QMC_PRIMES) throw std::runtime_error(kDimError);
+                return qmcFloat(offset + q->stride * s);
+            case MTSG_SAMPLER_LDSAMPLER: {   // ldsampler.cpp:202-208
+                const uint32_t n1 = dim - 2 * n2;
+                if ((int)n1 < q->ldDim) {
+                    const uint64_t h = mix64(ldKey + (uint64_t)(2 * n1 + 1) * 0xD1B54A32D192ED03ULL);
+                    ++dim;
+                    return radicalInverse2Single(ldShuffle(s, q->ldBits, h), (uint32_t)(h >> 32));
+                }
+                const float v = counterFloat(key, dim);
+                ++dim;
+                return v;
+            }
+            default: {
+                const float v = indep();
+                ++dim;
+                return v;
+            }
+        }
+    }
+    void next2D(float &a, float &b) {
+        switch (kind()) {
+            case MTSG_SAMPLER_HALTON:
+            case MTSG_SAMPLER_HAMMERSLEY: {   // halton.cpp:365-386, hammersley.cpp:258-283
+                if (dim + 1 >= MTSG_QMC_PRIMES) throw std::runtime_error(kDimError);
+                const uint64_t idx = offset + q->stride * s;
+                if (dim == 0) {
+                    const bool h = q->type == MTSG_SAMPLER_HALTON;
+                    const float v1 = qmcFloat(idx), v2 = qmcFloat(idx);
+                    a = v1 * (float)(h ? q->primePow[0] : q->res[0]) - (float)(px % 128);
+                    b = v2 * (float)(h ? q->primePow[1] : q->res[1]) - (float)(py % 128);
+                } else {
+                    a = qmcFloat(idx);
+                    b = qmcFloat(idx);
+                }
+                break;
+            }
+            case MTSG_SAMPLER_LDSAMPLER: {   // ldsampler.cpp:210-216
+                if ((int)n2 < q->ldDim) {
+                    const uint64_t h = mix64(ldKey + (uint64_t)(2 * n2 + 2) * 0xD1B54A32D192ED03ULL);
+                    const uint64_t sc = mix64(h ^ 0x5851F42D4C957F2DULL);
+                    const uint32_t i = ldShuffle(s, q->ldBits, h);
+                    a = radicalInverse2Single(i, (uint32_t)sc);
+                    b = sobol2Single(i, (uint32_t)(sc >> 32));
+                    dim += 2;
+                } else {
+                    a = counterFloat(key, dim++);
+                    b = counterFloat(key, dim++);
+                }
+                ++n2;
+                break;
+            }
+            default:   // independent.cpp:99-103
+                a = next1D();
+                b = next1D();
+                ++n2;
+        }
+        if (kind() == MTSG_SAMPLER_HALTON || kind() == MTSG_SAMPLER_HAMMERSLEY) ++n2;
+    }
 };
 
 // ---------------------------------------------------------------------------
@@ -1530,9 +1783,10 @@ int oracle_debug_path_rays(const mtsg_scene_desc *d, const mtsg_render_params *p
     g_rayLog = &log;
     SceneView sv(*d);
     Integrator I{p->max_depth, p->rr_depth, p->strict_normals != 0, p->hide_emitters != 0};
+    Qmc qmc(*d, p->spp);
     Sampler smp;
     smp.mode = ORACLE_RNG_COUNTER;
-    smp.key = counterKey(p->seed, ((uint64_t)y * d->camera.film_w + x) * p->spp + s);
+    smp.begin(&qmc, p->seed, d->camera.film_w, p->spp, x, y, (uint32_t)s);
     float a, b;
     smp.next2D(a, b);
     RayDiff diff;
@@ -1553,9 +1807,10 @@ int oracle_debug_pixel_sample(const mtsg_scene_desc *d, const mtsg_render_params
     mtsg_render_params q = *p;
     SceneView sv(*d);
     Integrator I{p->max_depth, p->rr_depth, p->strict_normals != 0, p->hide_emitters != 0};
+    Qmc qmc(*d, p->spp);
     Sampler smp;
     smp.mode = ORACLE_RNG_COUNTER;
-    smp.key = counterKey(p->seed, ((uint64_t)y * d->camera.film_w + x) * p->spp + s);
+    smp.begin(&qmc, p->seed, d->camera.film_w, p->spp, x, y, (uint32_t)s);
     float a, b;
     smp.next2D(a, b);
     RayDiff diff;
@@ -1569,14 +1824,34 @@ int oracle_debug_pixel_sample(const mtsg_scene_desc *d, const mtsg_render_params
     return 0;
 }
 
-int oracle_pixel_samples(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, float *out) {
+int oracle_sampler_draws(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, uint32_t s,
+                         uint32_t n, const int32_t *kinds, float *out) try {
+    Qmc qmc(*d, p->spp);
+    Sampler smp;
+    smp.mode = ORACLE_RNG_COUNTER;
+    smp.begin(&qmc, p->seed, d->camera.film_w, p->spp, x, y, s);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (kinds[i] == 2) {
+            smp.next2D(out[0], out[1]);
+            out += 2;
+        } else {
+            *out++ = smp.next1D();
+        }
+    }
+    return 0;
+} catch (const std::exception &e) {
+    g_err = e.what();
+    return -1;
+}
+
+int oracle_pixel_samples(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, float *out) try {
     SceneView sv(*d);
     Integrator I{p->max_depth, p->rr_depth, p->strict_normals != 0, p->hide_emitters != 0};
+    Qmc qmc(*d, p->spp);
     for (uint32_t s = 0; s < p->spp; ++s) {
         Sampler smp;
         smp.mode = ORACLE_RNG_COUNTER;
-        uint64_t sid = ((uint64_t)y * d->camera.film_w + x) * p->spp + s;
-        smp.key = counterKey(p->seed, sid);
+        smp.begin(&qmc, p->seed, d->camera.film_w, p->spp, x, y, s);
         float a, b;
         smp.next2D(a, b);
         RayDiff diff;
@@ -1588,6 +1863,9 @@ int oracle_pixel_samples(const mtsg_scene_desc *d, const mtsg_render_params *p, 
         out[3 * s] = L.s[0]; out[3 * s + 1] = L.s[1]; out[3 * s + 2] = L.s[2];
     }
     return 0;
+} catch (const std::exception &e) {
+    g_err = e.what();
+    return -1;
 }
 
 int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng_mode, int threads, float *rgbaw,
@@ -1628,6 +1906,7 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
         std::vector<Counters> ctrs(T);
         std::vector<uint64_t> pathVerts(T, 0), samples(T, 0);
         auto t0 = std::chrono::steady_clock::now();
+        const Qmc qmc(*d, p->spp);
         auto worker = [&](int tid) {
             Sampler smp;
             smp.mode = rng_mode;
@@ -1651,10 +1930,7 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
                             if (t % p->tile_stride != p->tile_offset) continue;
                         }
                         for (uint32_t s = 0; s < p->spp; ++s) {
-                            if (rng_mode == ORACLE_RNG_COUNTER) {
-                                smp.key = counterKey(p->seed, ((uint64_t)y * cam.film_w + x) * p->spp + s);
-                                smp.dim = 0;
-                            }
+                            smp.begin(&qmc, p->seed, cam.film_w, p->spp, x, y, s);
                             float a, b;
                             smp.next2D(a, b);
                             float spx = x + a, spy = y + b;
@@ -1682,8 +1958,20 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
             }
         };
         std::vector<std::thread> pool;
-        for (int t = 0; t < T; ++t) pool.emplace_back(worker, t);
+        std::mutex errMutex;
+        std::string workerErr;
+        auto guarded = [&](int tid) {
+            try {
+                worker(tid);
+            } catch (const std::exception &e) {   // e.g. the QMC dimension limit
+                std::lock_guard<std::mutex> lk(errMutex);
+                workerErr = e.what();
+                nextBlock.store(blocks.size() + (size_t)T);
+            }
+        };
+        for (int t = 0; t < T; ++t) pool.emplace_back(guarded, t);
         for (auto &th : pool) th.join();
+        if (!workerErr.empty()) throw std::runtime_error(workerErr);
         double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (stats) {
             bool counting = stats->threads < 0;

@@ -92,6 +92,10 @@ int oracle_env_sample_direct_n(const mtsg_scene_desc *d, uint32_t n, const float
 int oracle_env_pdf_direct_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, float *pdf);
 int oracle_env_eval_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, const float *rx, const float *ry, float *out);
 
+/* sampler draws of one sample (kinds: 1 = next1D, 2 = next2D), as mtsg_sampler_draws */
+int oracle_sampler_draws(const mtsg_scene_desc *d, const mtsg_render_params *p, int x, int y, uint32_t s,
+                         uint32_t n, const int32_t *kinds, float *out);
+
 const char *oracle_last_error(void);
 
 #ifdef __cplusplus

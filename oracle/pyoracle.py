@@ -108,5 +108,18 @@ def render(desc, params, border: int, rng: int = RNG_COUNTER, threads: int = 0, 
 
 def pixel_samples(desc, params, x: int, y: int) -> np.ndarray:
     out = np.zeros((params.spp, 3), np.float32)
-    lib().oracle_pixel_samples(desc, C.byref(params), x, y, _p(out))
+    if lib().oracle_pixel_samples(desc, C.byref(params), x, y, _p(out)) != 0:
+        raise RuntimeError("oracle_pixel_samples: " + lib().oracle_last_error().decode())
+    return out
+
+
+def sampler_draws(desc, params, x: int, y: int, s: int, kinds) -> np.ndarray:
+    """The scene sampler's next1D (1) / next2D (2) draws of one sample, flattened."""
+    L = lib()
+    L.oracle_sampler_draws.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                       C.c_void_p, C.c_void_p]
+    kinds = np.ascontiguousarray(kinds, dtype=np.int32)
+    out = np.empty(int(np.where(kinds == 2, 2, 1).sum()), np.float32)
+    if L.oracle_sampler_draws(desc, C.byref(params), x, y, s, kinds.size, _p(kinds), _p(out)) != 0:
+        raise RuntimeError("oracle_sampler_draws: " + L.oracle_last_error().decode())
     return out
