@@ -247,9 +247,10 @@ typedef struct mtsg_scene_desc {
 /* ---- render ------------------------------------------------------------- */
 
 /* MonteCarloIntegrator properties (src/librender/integrator.cpp:199-234),
- * independent sampler count, and the film region this call renders.  The
- * counter-based RNG draws dimension j of sample s of pixel (x, y) as
- * u = hash(seed, (y * film_w + x) * spp + s, j); see DESIGN.md. */
+ * sample count, and the film region this call renders.  With the
+ * independent sampler the counter-based RNG draws dimension j of sample s of
+ * pixel (x, y) as u = hash(seed, (y * film_w + x) * spp + s, j); the other
+ * samplers are described at mtsg_sampler.  See DESIGN.md. */
 typedef struct mtsg_render_params {
     int32_t max_depth;            /* -1 = infinite                          */
     int32_t rr_depth;             /* default 5                              */
