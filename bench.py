@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--batch-paths", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="single process: render only rank 0's tile share of an N-GPU run (scaling rehearsal)")
     ap.add_argument("--save", default="", help="write the developed image (.npy) here (rank 0)")
     return ap.parse_args()
 
@@ -146,6 +148,8 @@ def main():
     params = scene.params()
     params.tile_stride = world
     params.tile_offset = rank
+    if a.emulate_ranks > 1 and world == 1:
+        params.tile_stride = a.emulate_ranks
     gpu = mtsg.GPUScene(scene, local if world > 1 else 0)
     if a.batch_paths:
         gpu.set_batch_paths(a.batch_paths)
@@ -258,6 +262,9 @@ def main():
                        "samples_per_step": params.tile_w * params.tile_h * params.spp,
                        "parallelism": f"film tiles round-robin over {world} GPU(s)",
                        "scene_load_s": round(load_s, 2)},
+            **({"emulated_ranks": a.emulate_ranks,
+                "note": "one GPU rendering rank 0's 1/N tile share; value = frame samples / that time"}
+               if a.emulate_ranks > 1 and world == 1 else {}),
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
         }
         print(json.dumps(out))

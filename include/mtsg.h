@@ -301,11 +301,16 @@ typedef struct mtsg_stats {
     uint64_t wave_node_iters, wave_test_iters, wave_steps, wave_active_lanes;
     uint64_t shadow_wave_node_iters, shadow_wave_test_iters, shadow_wave_steps, shadow_wave_active_lanes;
     uint64_t launches_trace_shadow;   /* shadow-only trace launches (one per batch) */
+    /* traversal iterations per ray (MTSG_FLAG_COUNT): maximum, and a
+     * histogram of floor(log2(iterations)), bins 0-15                      */
+    uint64_t iter_max_closest, iter_max_shadow;
+    uint64_t iter_hist_closest[16], iter_hist_shadow[16];
 } mtsg_stats;
 
 enum {
     MTSG_FLAG_TIMING = 1,         /* bracket every kernel with HIP events   */
-    MTSG_FLAG_COUNT  = 2          /* instrumented traversal (slower)        */
+    MTSG_FLAG_COUNT  = 2,         /* instrumented traversal (slower)        */
+    MTSG_FLAG_WAVETIME = 4        /* record each traversal wave's start/exit */
 };
 
 typedef struct mtsg_scene mtsg_scene;
@@ -341,6 +346,17 @@ void mtsg_cancel(mtsg_scene *scene);
 
 int  mtsg_set_flags(mtsg_scene *scene, uint32_t flags);
 int  mtsg_get_stats(mtsg_scene *scene, mtsg_stats *out);
+/* Debug: rays of the last MTSG_FLAG_COUNT render that needed >= 192
+ * traversal iterations (up to 64 captured): 8 floats each, o.xyz, d.xyz,
+ * iterations, shadow (0/1).  Returns the number captured.  No reference
+ * counterpart (instrumentation in the spirit of
+ * rayIntersectHavranCollectStatistics, sahkdtree3.h:310-432).             */
+/* Debug: with MTSG_FLAG_WAVETIME, the start and exit times (100-MHz
+ * wall-clock ticks) of every wave of the last render's traversal launches:
+ * out[launch][wave][2], up to max_launches launches of *waves waves each.
+ * Returns the number of launches recorded.                                 */
+int  mtsg_debug_wavetimes(mtsg_scene *scene, uint64_t *out, uint32_t max_launches, uint32_t *waves);
+int  mtsg_debug_stragglers(mtsg_scene *scene, float *out, uint32_t max_rays);
 
 /* Wavefront batch size in paths (default chosen from device memory). */
 int  mtsg_set_batch_paths(mtsg_scene *scene, uint32_t paths);

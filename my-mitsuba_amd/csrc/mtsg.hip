@@ -171,6 +171,14 @@ constexpr int CNT_ERR = 96;   // sticky error flags (1: QMC dimension limit)
 constexpr int CNT_FETCH = 256;                           // XGROUPS counters, 32 words apart
 constexpr int CNT_WORDS = CNT_FETCH + 32 * XGROUPS;
 constexpr int HOSTCNT_STRIDE = 256;
+// traversal counters (MTSG_FLAG_COUNT): [0,7) closest, [8,15) shadow (see
+// flush_counts), 7 / 15 the maximum iterations per ray, [16,32) / [32,48)
+// histograms of floor(log2(iterations per ray)); [48] the number of captured
+// stragglers (rays of >= STRAGGLER_ITERS iterations), [64, 64 + 8 * 64) their
+// records (o.xyz, d.xyz, iterations, shadow as float / integer bits)
+constexpr int CTR_WORDS = 64 + 8 * 64;
+constexpr uint32_t STRAGGLER_ITERS = 192, STRAGGLER_MAX = 64;
+constexpr uint32_t WT_MAX_LAUNCHES = 64;   // MTSG_FLAG_WAVETIME launches recorded per render
 __host__ __device__ constexpr int cnt_s(int k) { return k ? CNT_S1 : CNT_S0; }
 DEV int cnt_q(int q) { return q ? CNT_Q1 : CNT_Q0; }
 
@@ -188,6 +196,10 @@ constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traver
 // large as the frame -- measured on the 1M-triangle scene (Msamples/s):
 // 4M paths 421, 16M 672, 32M 803, 64M 884, 128M 934, whole frame 960.
 constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 28;
+#define MTSG_MAX_LANES 2
+#ifndef MTSG_LANES
+#define MTSG_LANES 1
+#endif
 constexpr size_t PATH_STATE_BYTES = 272;    // bytes per path slot (DevPaths: 2 x 96 dense + hit, L, 3 x shadow)
 #ifndef MTSG_SHORT_STACK
 #define MTSG_SHORT_STACK 6   // 6 x 12 B x 64 lanes = 4.6 KB LDS/wave -> 8 waves/SIMD (8: 6.5, 12: 4.2)
@@ -310,6 +322,22 @@ DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
         for (int k = 0; k < 7; ++k) atomicAdd(ctr + k, v[k]);
 }
 
+#ifndef MTSG_FETCH
+#define MTSG_FETCH 256
+#endif
+constexpr uint32_t FETCH = MTSG_FETCH;
+#ifndef MTSG_GUIDE
+#define MTSG_GUIDE 0
+#endif
+#ifndef MTSG_FETCH_MIN
+#define MTSG_FETCH_MIN 64
+#endif
+#ifndef MTSG_GUIDE_SPLIT
+#define MTSG_GUIDE_SPLIT 2
+#endif
+constexpr bool GUIDE = MTSG_GUIDE;
+constexpr uint32_t FETCH_MIN = MTSG_FETCH_MIN, GUIDE_SPLIT = MTSG_GUIDE_SPLIT;
+
 // XCD-partitioned work fetch: the queue is cut into XGROUPS contiguous
 // ranges; workgroup b draws from range b % XGROUPS first (blocks b, b + 8
 // share an XCD, so coherent neighbouring rays share that XCD's L2) and then
@@ -320,6 +348,8 @@ struct Fetch {
     uint32_t count;
     uint32_t group;    // range currently drained (wave-uniform)
     uint32_t tried;
+    uint32_t guide;    // waves per range x GUIDE_SPLIT
+    uint32_t req;      // next request size (GUIDE)
     DEV uint32_t lo(uint32_t g) const { return (uint32_t)(((uint64_t)count * g) / XGROUPS); }
     // returns false when every range is exhausted; else [base, base + n)
     DEV bool next(uint32_t want, uint32_t &base, uint32_t &n) {
@@ -327,11 +357,17 @@ struct Fetch {
             const uint32_t beg = lo(group), end = lo(group + 1);
             // called with the whole wave active: lane 0 draws for it
             uint32_t off = 0;
+            if (GUIDE) want = req;
             if (__lane_id() == 0) off = atomicAdd(&ctr[32 * group], want);
             off = __builtin_amdgcn_readfirstlane(off);
             if (beg + off < end) {
                 base = beg + off;
                 n = min(want, end - base);
+                // guided self-scheduling: size the next request by what this
+                // draw saw left of the range (no extra access to the
+                // contended counter), so the last pools are small and the
+                // waves run out of work together
+                if (GUIDE) req = max(FETCH_MIN, min(FETCH, (end - base - n) / guide));
                 return true;
             }
             group = (group + 1) % XGROUPS;
@@ -597,22 +633,20 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
 //   [nC, nC + nS): any hit of P.sh_o/sh_d[i - nC]    -> unoccluded: L += sh_c
 //   cIn: -1 = nIdentity closest rays (bounce 0), 0/1 = count in cnt_q(cIn), -2 = none
 //   sIn: 0/1 = count in CNT_S0/CNT_S1, -1 = none
-#ifndef MTSG_FETCH
-#define MTSG_FETCH 256
-#endif
-constexpr uint32_t FETCH = MTSG_FETCH;
 
 template <bool COUNT, int MIN_IDLE>
-__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity) {
+__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
     const SpecStack stk{};
+    const unsigned long long tStart = wt ? wall_clock64() : 0ull;
     const uint32_t nC = cIn == -1 ? nIdentity : (cIn >= 0 ? __atomic_load_n(&P.cnt[cnt_q(cIn)], __ATOMIC_RELAXED) : 0u);
     const uint32_t nS = sIn >= 0 ? __atomic_load_n(&P.cnt[cnt_s(sIn)], __ATOMIC_RELAXED) : 0u;
-    Fetch F{&P.cnt[CNT_FETCH], nC + nS, blockIdx.x % XGROUPS, 0};
+    Fetch F{&P.cnt[CNT_FETCH], nC + nS, blockIdx.x % XGROUPS, 0, max(1u, gridDim.x / XGROUPS * GUIDE_SPLIT), FETCH};
     TraceCounts cc{0, 0, 0, 0, 0, 0, 0}, cs{0, 0, 0, 0, 0, 0, 0};
     uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
     bool exhausted = false;
     bool active = false;
     uint32_t idx = 0;                      // index into the ray's own list
+    uint32_t iters = 0;                    // COUNT: iterations of this ray
     SpecRay r;
     for (;;) {
         unsigned long long idle = __ballot(!active);
@@ -630,6 +664,7 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
                 if (shadow) { const float mint = rd.w; rd.w = ro.w; ro.w = mint; }   // sh_o.w = maxt, sh_d.w = mint
                 if (spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, shadow, r)) {
                     active = true;
+                    if (COUNT) iters = 0;
                 } else if (shadow) {
                     shadow_unoccluded(P, idx);
                 } else if (!(rd.w < 0.0f)) {   // maxt < 0: dead slot outside the render rectangle
@@ -659,8 +694,23 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
             if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx);
             else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx);
         }
+        if (COUNT && active) ++iters;
         if (done) {
             active = false;
+            if (COUNT) {
+                const bool sh = (r.bits & SB_SHADOW) != 0;
+                atomicMax(&P.ctr[sh ? 15 : 7], (unsigned long long)iters);
+                atomicAdd(&P.ctr[(sh ? 32 : 16) + min(15, 31 - __clz(max(iters, 1u)))], 1ull);
+                if (iters >= STRAGGLER_ITERS) {
+                    const unsigned long long k = atomicAdd(&P.ctr[48], 1ull);
+                    if (k < STRAGGLER_MAX) {
+                        unsigned long long *o = P.ctr + 64 + 8 * k;
+                        o[0] = __float_as_uint(r.o.x); o[1] = __float_as_uint(r.o.y); o[2] = __float_as_uint(r.o.z);
+                        o[3] = __float_as_uint(r.d.x); o[4] = __float_as_uint(r.d.y); o[5] = __float_as_uint(r.d.z);
+                        o[6] = iters; o[7] = sh;
+                    }
+                }
+            }
             // closest: hits were written through, only a miss needs a record
             if (!(r.bits & SB_FOUND)) {
                 if (r.bits & SB_SHADOW) shadow_unoccluded(P, idx);
@@ -670,6 +720,10 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
     }
     flush_counts<COUNT>(P.ctr, cc);
     flush_counts<COUNT>(P.ctr + 8, cs);
+    if (wt && __lane_id() == 0) {
+        wt[2 * blockIdx.x] = tStart;
+        wt[2 * blockIdx.x + 1] = wall_clock64();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1513,11 +1567,14 @@ struct mtsg_scene {
     DevCamera cam{};
     std::vector<void *> allocs;
     // batch buffers
-    uint32_t capacity = 0;         // paths per batch
-    uint32_t requestedBatch = 0;
-    DevPaths P{};
+    uint32_t capacity = 0;         // paths per batch (per lane)
+    uint32_t requestedBatch = 0;   // paths in flight over all lanes
+    int lanes = MTSG_LANES;        // concurrent batches (streams) of a render
+    int lanesAlloc = 0;            // lanes with path state allocated
+    hipStream_t lstream[MTSG_MAX_LANES] = {};   // lstream[0] == stream
+    DevPaths LP[MTSG_MAX_LANES]{};
     std::vector<void *> batchAllocs;
-    uint32_t *hostCnt = nullptr;   // pinned copy of the queue counters
+    uint32_t *hostCnt = nullptr;   // pinned copy of the queue counters (2 per lane)
     int cuCount = 0;
     int traceGrid = 0, shadeGrid = 0;
     uint32_t flags = 0;
@@ -1530,6 +1587,9 @@ struct mtsg_scene {
     std::vector<hipEvent_t> evPool;
     size_t evUsed = 0;
     std::vector<std::pair<int, size_t>> timed;   // (kind, event index)
+    std::vector<unsigned long long> stragglers;  // MTSG_FLAG_COUNT: slow-ray records
+    unsigned long long *waveTimes = nullptr;     // MTSG_FLAG_WAVETIME: [launch][wave][2]
+    uint32_t wtLaunches = 0;
 };
 
 namespace {
@@ -1543,10 +1603,13 @@ void free_batch(mtsg_scene *s) {
     for (void *p : s->batchAllocs) hipFree(p);
     s->batchAllocs.clear();
     s->capacity = 0;
+    s->lanesAlloc = 0;
 }
 
-int ensure_batch(mtsg_scene *s, uint32_t paths) {
-    if (s->capacity >= paths) return MTSG_OK;
+int ensure_batch(mtsg_scene *s, uint32_t paths, int lanes) {
+    if (s->capacity >= paths && s->lanesAlloc >= lanes) return MTSG_OK;
+    paths = std::max(paths, s->capacity);
+    lanes = std::max(lanes, s->lanesAlloc);
     free_batch(s);
     auto alloc = [&](size_t bytes, void **p) -> int {
         HIP_TRY(hipMalloc(p, bytes));
@@ -1554,17 +1617,20 @@ int ensure_batch(mtsg_scene *s, uint32_t paths) {
         return MTSG_OK;
     };
     size_t n = paths;
-    DevPaths &P = s->P;
     int rc = MTSG_OK;
+    for (int l = 0; l < lanes; ++l) {
+    DevPaths &P = s->LP[l];
 #define A(field, T) if ((rc = alloc(n * sizeof(T), (void **)&P.field)) != MTSG_OK) return rc
     A(ray_o, float4); A(ray_d, float4); A(T, float4); A(aux, float4); A(Lp, float4); A(meta, uint4);
     A(n_ray_o, float4); A(n_ray_d, float4); A(n_T, float4); A(n_aux, float4); A(n_Lp, float4); A(n_meta, uint4);
     A(hit, float4); A(L, float4); A(sh_o, float4); A(sh_d, float4); A(sh_c, float4);
 #undef A
     if ((rc = alloc(CNT_WORDS * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
-    if ((rc = alloc(16 * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
-    HIP_TRY(hipMemset(P.ctr, 0, 16 * sizeof(unsigned long long)));
+    if ((rc = alloc(CTR_WORDS * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
+    HIP_TRY(hipMemset(P.ctr, 0, CTR_WORDS * sizeof(unsigned long long)));
+    }
     s->capacity = paths;
+    s->lanesAlloc = lanes;
     return MTSG_OK;
 }
 
@@ -1591,12 +1657,12 @@ hipEvent_t next_event(mtsg_scene *s) {
 
 // bracket a launch with events when timing is enabled
 template <class F>
-void timed_launch(mtsg_scene *s, int kind, F f) {
+void timed_launch(mtsg_scene *s, int kind, hipStream_t st, F f) {
     if (!(s->flags & MTSG_FLAG_TIMING)) { f(); return; }
     size_t i0 = s->evUsed;
-    hipEventRecord(next_event(s), s->stream);
+    hipEventRecord(next_event(s), st);
     f();
-    hipEventRecord(next_event(s), s->stream);
+    hipEventRecord(next_event(s), st);
     s->timed.emplace_back(kind, i0);
 }
 
@@ -1604,36 +1670,39 @@ void timed_launch(mtsg_scene *s, int kind, F f) {
 // shadow rays sIn.  traceMode 1 refills lanes at 32 idle lanes instead of 16
 // (MTSG_TRACE_MODE, for measurement).
 template <bool COUNT>
-void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t n) {
+void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t n, hipStream_t st) {
     dim3 g(s->traceGrid), blk(TRACE_BLOCK);
-    if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, s->stream, s->ds, P, cIn, sIn, n);
-    else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, s->stream, s->ds, P, cIn, sIn, n);
+    unsigned long long *wt = nullptr;
+    if ((s->flags & MTSG_FLAG_WAVETIME) && s->waveTimes && s->wtLaunches < WT_MAX_LAUNCHES)
+        wt = s->waveTimes + (size_t)2 * s->traceGrid * s->wtLaunches++;
+    if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
 }
-void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn, uint32_t n) {
-    if (count) launch_trace_c<true>(s, P, cIn, sIn, n);
-    else launch_trace_c<false>(s, P, cIn, sIn, n);
+void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn, uint32_t n, hipStream_t st) {
+    if (count) launch_trace_c<true>(s, P, cIn, sIn, n, st);
+    else launch_trace_c<false>(s, P, cIn, sIn, n, st);
 }
 
 template <bool ENV>
-void launch_shade_env(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin) {
+void launch_shade_env(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {
     dim3 g(s->shadeGrid), blk(SHADE_BLOCK);
     switch (I.smp.type) {
         case MTSG_SAMPLER_HALTON:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HALTON>), g, blk, 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HALTON>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
             break;
         case MTSG_SAMPLER_HAMMERSLEY:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HAMMERSLEY>), g, blk, 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HAMMERSLEY>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
             break;
         case MTSG_SAMPLER_LDSAMPLER:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_LDSAMPLER>), g, blk, 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_LDSAMPLER>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
             break;
         default:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_INDEPENDENT>), g, blk, 0, s->stream, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_INDEPENDENT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
     }
 }
-void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin) {
-    if (s->ds.has_env) launch_shade_env<true>(s, I, B, P, b, qin);
-    else launch_shade_env<false>(s, I, B, P, b, qin);
+void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {
+    if (s->ds.has_env) launch_shade_env<true>(s, I, B, P, b, qin, st);
+    else launch_shade_env<false>(s, I, B, P, b, qin, st);
 }
 
 // Sampler constants of a render (setFilmResolution with blocked = true over
@@ -1707,11 +1776,13 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     if ((rc = validate(p, s)) != MTSG_OK) return rc;
     if ((rc = set_device(s)) != MTSG_OK) return rc;
     auto t0 = std::chrono::steady_clock::now();
+    const bool count = (s->flags & MTSG_FLAG_COUNT) != 0;
     uint32_t maxPaths = s->requestedBatch ? s->requestedBatch : DEFAULT_BATCH_PATHS;
-    if (!s->requestedBatch && s->capacity < maxPaths) {
+    if (!s->requestedBatch) {
         size_t freeB = 0, totalB = 0;
         if (hipMemGetInfo(&freeB, &totalB) == hipSuccess) {
-            const size_t fit = (size_t)((freeB + (size_t)s->capacity * PATH_STATE_BYTES) * 0.6 / PATH_STATE_BYTES);
+            const size_t held = (size_t)s->capacity * s->lanesAlloc * PATH_STATE_BYTES;
+            const size_t fit = (size_t)((freeB + held) * 0.6 / PATH_STATE_BYTES);
             maxPaths = (uint32_t)std::max<size_t>(TILE * TILE, std::min<size_t>(maxPaths, fit));
         }
     }
@@ -1721,30 +1792,35 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     const uint32_t tstride = p->tile_stride > 1 ? (uint32_t)p->tile_stride : 1u;
     const uint32_t toffset = p->tile_stride > 1 ? (uint32_t)p->tile_offset : 0u;
     const uint32_t ntiles = toffset < allTiles ? (allTiles - toffset + tstride - 1) / tstride : 0u;
-    const uint32_t sppPerBatch = std::max(1u, std::min(p->spp, maxPaths / (TILE * TILE)));
-    // equal-sized batches: a nearly empty last batch costs a full set of
-    // bounce launches (and their tails) for a sliver of the work
-    const uint32_t tilesMax = std::max(1u, maxPaths / (TILE * TILE * sppPerBatch));
-    const uint32_t nTileBatches = std::max(1u, (ntiles + tilesMax - 1) / tilesMax);
+    // Lanes: independent batches on their own streams, issued bounce by bounce
+    // in lock step, so one lane's launch tail (its slowest rays) overlaps the
+    // other lane's launch.  The debug and counting modes use one lane.
+    const uint32_t nl = (s->dumpL || count || ntiles < 2) ? 1u : (uint32_t)s->lanes;
+    const uint32_t lanePaths = std::max<uint32_t>(TILE * TILE, maxPaths / nl);
+    const uint32_t sppPerBatch = std::max(1u, std::min(p->spp, lanePaths / (TILE * TILE)));
+    // equal-sized batches, a multiple of the lane count: a nearly empty last
+    // batch costs a full set of bounce launches (and their tails) for a
+    // sliver of the work
+    const uint32_t tilesMax = std::max(1u, lanePaths / (TILE * TILE * sppPerBatch));
+    uint32_t nTileBatches = std::max(1u, (ntiles + tilesMax - 1) / tilesMax);
+    nTileBatches = std::min(ntiles ? ntiles : 1u, (nTileBatches + nl - 1) / nl * nl);
     const uint32_t tilesPerBatch = std::max(1u, (ntiles + nTileBatches - 1) / nTileBatches);
-    if ((rc = ensure_batch(s, tilesPerBatch * sppPerBatch * TILE * TILE)) != MTSG_OK) return rc;
+    if ((rc = ensure_batch(s, tilesPerBatch * sppPerBatch * TILE * TILE, (int)nl)) != MTSG_OK) return rc;
     const int blockW = p->tile_w + 2 * s->cam.border, blockH = p->tile_h + 2 * s->cam.border;
     DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed, (uint32_t)s->cam.film_w,
                     make_sampler(s, p->spp)};
     memset(&s->stats, 0, sizeof(s->stats));
+    s->wtLaunches = 0;
+    if ((s->flags & MTSG_FLAG_WAVETIME) && !s->waveTimes)
+        HIP_TRY(hipMalloc((void **)&s->waveTimes, (size_t)2 * s->traceGrid * WT_MAX_LAUNCHES * sizeof(unsigned long long)));
     s->evUsed = 0;
     s->timed.clear();
     s->cancel.store(0);
-    const bool count = (s->flags & MTSG_FLAG_COUNT) != 0;
-    if (count) HIP_TRY(hipMemsetAsync(s->P.ctr, 0, 16 * sizeof(unsigned long long), s->stream));
-    DevPaths &P = s->P;
-    hipEvent_t cntEv[2];
-    HIP_TRY(hipEventCreateWithFlags(&cntEv[0], hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&cntEv[1], hipEventDisableTiming));
-    int result = MTSG_OK;
-    for (uint32_t t0i = 0; t0i < ntiles && result == MTSG_OK; t0i += tilesPerBatch) {
+    if (count) HIP_TRY(hipMemsetAsync(s->LP[0].ctr, 0, CTR_WORDS * sizeof(unsigned long long), s->stream));
+    // the batches of this call, tile-major
+    std::vector<DevBatch> batches;
+    for (uint32_t t0i = 0; t0i < ntiles; t0i += tilesPerBatch) {
         for (uint32_t s0 = 0; s0 < p->spp; s0 += sppPerBatch) {
-            if (s->cancel.load()) { result = MTSG_ERR_CANCELLED; g_err = "cancelled"; break; }
             DevBatch B;
             B.rect_x = p->tile_x; B.rect_y = p->tile_y; B.rect_w = p->tile_w; B.rect_h = p->tile_h;
             B.tiles_x = (int)tilesX;
@@ -1755,85 +1831,136 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             B.s0 = s0;
             B.ns = std::min(sppPerBatch, p->spp - s0);
             B.nslots = (uint32_t)B.ntiles * B.ns * TILE * TILE;
-            HIP_TRY(hipMemsetAsync(P.cnt, 0, CNT_WORDS * sizeof(uint32_t), s->stream));
-            timed_launch(s, K_CAMERA, [&]() {
-                hipLaunchKernelGGL(k_camera, dim3((B.nslots + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s->stream, s->cam, I, B, P);
+            batches.push_back(B);
+        }
+    }
+    struct LaneRun {
+        DevBatch B;
+        int last = -1;
+        bool open = false;
+        hipEvent_t cntEv[2] = {nullptr, nullptr};
+    } lr[MTSG_MAX_LANES];
+    int result = MTSG_OK;
+    for (uint32_t l = 0; l < nl && result == MTSG_OK; ++l)
+        for (int k = 0; k < 2; ++k)
+            if (hipEventCreateWithFlags(&lr[l].cntEv[k], hipEventDisableTiming) != hipSuccess) { g_err = "event"; result = MTSG_ERR_DEVICE; }
+    const int maxBounces = p->max_depth > 0 ? p->max_depth : 1 << 30;
+    // bounce b of a lane: one trace launch over this bounce's closest rays
+    // (work list qin(b), identity for b = 0) and bounce b-1's shadow rays
+    // (S((b-1) & 1)), then k_shade appends the next bounce's paths to
+    // qout(b) = (b & 1) ^ 1 and its shadow rays to S(b & 1)
+    auto hostCnt = [&](uint32_t l, int bb) { return s->hostCnt + HOSTCNT_STRIDE * (2 * l + (bb & 1)); };
+    auto account = [&](uint32_t l, int bb) {
+        const uint32_t *hc = hostCnt(l, bb);
+        const uint32_t consumed = bb == 0 ? lr[l].B.nslots : hc[(bb & 1) ? CNT_Q1 : CNT_Q0];
+        s->stats.rays_closest += consumed;
+        s->stats.rays_shadow += hc[cnt_s(bb & 1)];
+        s->stats.launches_trace_closest++;
+        return hc[((bb & 1) ^ 1) ? CNT_Q1 : CNT_Q0];
+    };
+    for (size_t k0 = 0; k0 < batches.size() && result == MTSG_OK; k0 += nl) {
+        if (s->cancel.load()) { result = MTSG_ERR_CANCELLED; g_err = "cancelled"; break; }
+        const uint32_t nb = (uint32_t)std::min<size_t>(nl, batches.size() - k0);
+        for (uint32_t l = 0; l < nb; ++l) {
+            LaneRun &L = lr[l];
+            L.B = batches[k0 + l];
+            L.last = -1;
+            L.open = true;
+            DevPaths &P = s->LP[l];
+            hipStream_t st = s->lstream[l];
+            HIP_TRY(hipMemsetAsync(P.cnt, 0, CNT_WORDS * sizeof(uint32_t), st));
+            timed_launch(s, K_CAMERA, st, [&]() {
+                hipLaunchKernelGGL(k_camera, dim3((L.B.nslots + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, s->cam, I, L.B, P);
             });
-            const int maxBounces = p->max_depth > 0 ? p->max_depth : 1 << 30;
-            int last = -1;
-            // bounce b: one trace launch over this bounce's closest rays (work
-            // list qin(b), identity for b = 0) and bounce b-1's shadow rays
-            // (S((b-1) & 1)), then k_shade appends the next bounce's paths to
-            // qout(b) = (b & 1) ^ 1 and its shadow rays to S(b & 1)
-            auto account = [&](int bb) {
-                const uint32_t *hc = s->hostCnt + HOSTCNT_STRIDE * (bb & 1);
-                const uint32_t consumed = bb == 0 ? B.nslots : hc[(bb & 1) ? CNT_Q1 : CNT_Q0];
-                s->stats.rays_closest += consumed;
-                s->stats.rays_shadow += hc[cnt_s(bb & 1)];
-                s->stats.launches_trace_closest++;
-                return hc[((bb & 1) ^ 1) ? CNT_Q1 : CNT_Q0];
-            };
-            for (int b = 0; b < maxBounces; ++b) {
+        }
+        for (int b = 0;; ++b) {
+            bool any = false;
+            for (uint32_t l = 0; l < nb; ++l) {
+                LaneRun &L = lr[l];
+                if (!L.open) continue;
+                DevPaths &P = s->LP[l];
+                hipStream_t st = s->lstream[l];
                 const int qin = b == 0 ? -1 : (b & 1);
                 const int qout = (b & 1) ^ 1;
-                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, qout, b & 1);
-                timed_launch(s, K_CLOSEST, [&]() { launch_trace(s, count, P, qin, b == 0 ? -1 : ((b - 1) & 1), B.nslots); });
-                timed_launch(s, K_SHADE, [&]() { launch_shade(s, I, B, P, b, qin); });
+                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, P.cnt, qout, b & 1);
+                timed_launch(s, K_CLOSEST, st, [&]() { launch_trace(s, count, P, qin, b == 0 ? -1 : ((b - 1) & 1), L.B.nslots, st); });
+                timed_launch(s, K_SHADE, st, [&]() { launch_shade(s, I, L.B, P, b, qin, st); });
                 swap_bounce(P);
-                HIP_TRY(hipMemcpyAsync(s->hostCnt + HOSTCNT_STRIDE * (b & 1), P.cnt, (CNT_S1 + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
-                HIP_TRY(hipEventRecord(cntEv[b & 1], s->stream));
-                last = b;
-                if (b >= 1) {
-                    // lagged check: if bounce b-1 produced nothing, bounce b was empty
-                    HIP_TRY(hipEventSynchronize(cntEv[(b - 1) & 1]));
-                    if (account(b - 1) == 0) break;
-                }
+                HIP_TRY(hipMemcpyAsync(hostCnt(l, b), P.cnt, (CNT_S1 + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipEventRecord(L.cntEv[b & 1], st));
+                L.last = b;
+                if (b + 1 >= maxBounces) L.open = false;
             }
-            if (last >= 0) {
+            for (uint32_t l = 0; l < nb; ++l) {
+                LaneRun &L = lr[l];
+                // lagged check: if bounce b-1 produced nothing, bounce b was empty
+                if (L.open && b >= 1) {
+                    HIP_TRY(hipEventSynchronize(L.cntEv[(b - 1) & 1]));
+                    if (account(l, b - 1) == 0) L.open = false;
+                }
+                any |= L.open;
+            }
+            if (!any) break;
+        }
+        for (uint32_t l = 0; l < nb; ++l) {
+            LaneRun &L = lr[l];
+            DevPaths &P = s->LP[l];
+            hipStream_t st = s->lstream[l];
+            const DevBatch &B = L.B;
+            if (L.last >= 0) {
                 // the last bounce's shadow rays
-                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s->stream, P.cnt, -1, -1);
-                timed_launch(s, K_SHADOW, [&]() { launch_trace(s, count, P, -2, last & 1, 0u); });
+                hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, P.cnt, -1, -1);
+                timed_launch(s, K_SHADOW, st, [&]() { launch_trace(s, count, P, -2, L.last & 1, 0u, st); });
                 s->stats.launches_trace_shadow++;
-                HIP_TRY(hipEventSynchronize(cntEv[last & 1]));
-                account(last);
-                // the error word is sticky within the batch: the last copy holds it
-                if (s->hostCnt[HOSTCNT_STRIDE * (last & 1) + CNT_ERR]) {
-                    g_err = "Lookup dimension exceeds the prime number table size! "
-                            "You may have to reduce the 'maxDepth' parameter of your integrator.";
-                    result = MTSG_ERR_INVALID;
-                }
             }
-            timed_launch(s, K_SPLAT, [&]() {
+            timed_launch(s, K_SPLAT, st, [&]() {
                 dim3 g(B.ntiles, (B.ns + SPLAT_CHUNK - 1) / SPLAT_CHUNK);
                 const int K = 2 * s->cam.border + 1;
-                if (K == 5 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<5, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
-                else if (K == 5) hipLaunchKernelGGL((k_splat<5, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
-                else if (K <= 3 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<3, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
-                else if (K <= 3) hipLaunchKernelGGL((k_splat<3, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
-                else if (!s->cam.has_alpha) hipLaunchKernelGGL((k_splat<9, 4>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
-                else hipLaunchKernelGGL((k_splat<9, 5>), g, dim3(BLOCK), 0, s->stream, s->cam, I, B, P, film, blockW, blockH);
+                if (K == 5 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<5, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
+                else if (K == 5) hipLaunchKernelGGL((k_splat<5, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
+                else if (K <= 3 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<3, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
+                else if (K <= 3) hipLaunchKernelGGL((k_splat<3, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
+                else if (!s->cam.has_alpha) hipLaunchKernelGGL((k_splat<9, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
+                else hipLaunchKernelGGL((k_splat<9, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
             });
             s->stats.samples += (uint64_t)B.nslots;
-            if (s->dumpL) {
-                // debug: copy the batch's per-slot radiance (single batch only)
-                std::vector<float4> L(B.nslots);
-                HIP_TRY(hipMemcpyAsync(L.data(), P.L, B.nslots * sizeof(float4), hipMemcpyDeviceToHost, s->stream));
-                HIP_TRY(hipStreamSynchronize(s->stream));
-                for (uint32_t slot = 0; slot < B.nslots; ++slot) {
-                    const uint32_t pix = slot & (TILE * TILE - 1), rest = slot >> 8;
-                    const uint32_t sl = rest % B.ns, tl = rest / B.ns;
-                    const int tile = B.toffset + (B.tile0 + (int)tl) * B.tstride;
-                    const int x = (tile % B.tiles_x) * TILE + (int)(pix % TILE), y = (tile / B.tiles_x) * TILE + (int)(pix / TILE);
-                    if (x >= p->tile_w || y >= p->tile_h) continue;
-                    float *o = s->dumpL + (((size_t)y * p->tile_w + x) * p->spp + B.s0 + sl) * 4;
-                    o[0] = L[slot].x; o[1] = L[slot].y; o[2] = L[slot].z; o[3] = L[slot].w;
-                }
+        }
+        for (uint32_t l = 0; l < nb; ++l) {
+            LaneRun &L = lr[l];
+            if (L.last < 0) continue;
+            HIP_TRY(hipEventSynchronize(L.cntEv[L.last & 1]));
+            account(l, L.last);
+            // the error word is sticky within the batch: the last copy holds it
+            if (hostCnt(l, L.last)[CNT_ERR]) {
+                g_err = "Lookup dimension exceeds the prime number table size! "
+                        "You may have to reduce the 'maxDepth' parameter of your integrator.";
+                result = MTSG_ERR_INVALID;
+            }
+        }
+        if (s->dumpL) {
+            // debug: copy the batch's per-slot radiance (single batch, one lane)
+            const DevBatch &B = lr[0].B;
+            std::vector<float4> L(B.nslots);
+            HIP_TRY(hipMemcpyAsync(L.data(), s->LP[0].L, B.nslots * sizeof(float4), hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            for (uint32_t slot = 0; slot < B.nslots; ++slot) {
+                const uint32_t pix = slot & (TILE * TILE - 1), rest = slot >> 8;
+                const uint32_t sl = rest % B.ns, tl = rest / B.ns;
+                const int tile = B.toffset + (B.tile0 + (int)tl) * B.tstride;
+                const int x = (tile % B.tiles_x) * TILE + (int)(pix % TILE), y = (tile / B.tiles_x) * TILE + (int)(pix / TILE);
+                if (x >= p->tile_w || y >= p->tile_h) continue;
+                float *o = s->dumpL + (((size_t)y * p->tile_w + x) * p->spp + B.s0 + sl) * 4;
+                o[0] = L[slot].x; o[1] = L[slot].y; o[2] = L[slot].z; o[3] = L[slot].w;
             }
         }
     }
-    hipError_t e = hipStreamSynchronize(s->stream);
-    hipEventDestroy(cntEv[0]);
-    hipEventDestroy(cntEv[1]);
+    hipError_t e = hipSuccess;
+    for (uint32_t l = 0; l < nl; ++l) {
+        const hipError_t el = hipStreamSynchronize(s->lstream[l]);
+        if (e == hipSuccess) e = el;
+        for (int k = 0; k < 2; ++k)
+            if (lr[l].cntEv[k]) hipEventDestroy(lr[l].cntEv[k]);
+    }
     if (e != hipSuccess) { g_err = std::string("render: ") + hipGetErrorString(e); return MTSG_ERR_DEVICE; }
     e = hipGetLastError();
     if (e != hipSuccess) { g_err = std::string("kernel launch: ") + hipGetErrorString(e); return MTSG_ERR_DEVICE; }
@@ -1854,8 +1981,8 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
         }
     }
     if (count) {
-        unsigned long long c[16];
-        HIP_TRY(hipMemcpy(c, P.ctr, sizeof(c), hipMemcpyDeviceToHost));
+        unsigned long long c[CTR_WORDS];
+        HIP_TRY(hipMemcpy(c, s->LP[0].ctr, sizeof(c), hipMemcpyDeviceToHost));
         s->stats.nodes_visited = c[0];
         s->stats.leaf_refs = c[1];
         s->stats.tri_tests = c[2];
@@ -1870,6 +1997,13 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
         s->stats.shadow_wave_test_iters = c[12];
         s->stats.shadow_wave_steps = c[13];
         s->stats.shadow_wave_active_lanes = c[14];
+        s->stats.iter_max_closest = c[7];
+        s->stats.iter_max_shadow = c[15];
+        for (int k = 0; k < 16; ++k) {
+            s->stats.iter_hist_closest[k] = c[16 + k];
+            s->stats.iter_hist_shadow[k] = c[32 + k];
+        }
+        s->stragglers.assign(c + 64, c + 64 + 8 * std::min<unsigned long long>(c[48], STRAGGLER_MAX));
     }
     s->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MTSG_OK;
@@ -2100,7 +2234,11 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;
     s->shadeGrid = s->cuCount * 8 * 256 / SHADE_BLOCK;
-    if (hipHostMalloc((void **)&s->hostCnt, 2 * HOSTCNT_STRIDE * sizeof(uint32_t)) != hipSuccess) { g_err = "pinned alloc"; return fail(MTSG_ERR_OOM); }
+    if (const char *l = getenv("MTSG_LANES")) s->lanes = std::max(1, std::min(MTSG_MAX_LANES, atoi(l)));
+    s->lstream[0] = s->stream;
+    for (int l = 1; l < MTSG_MAX_LANES; ++l)
+        if (hipStreamCreateWithFlags(&s->lstream[l], hipStreamNonBlocking) != hipSuccess) { g_err = "stream"; return fail(MTSG_ERR_DEVICE); }
+    if (hipHostMalloc((void **)&s->hostCnt, 2 * MTSG_MAX_LANES * HOSTCNT_STRIDE * sizeof(uint32_t)) != hipSuccess) { g_err = "pinned alloc"; return fail(MTSG_ERR_OOM); }
     *out = s;
     return MTSG_OK;
 }
@@ -2121,6 +2259,29 @@ int mtsg_get_stats(mtsg_scene *s, mtsg_stats *out) {
     if (!s || !out) return MTSG_ERR_INVALID;
     *out = s->stats;
     return MTSG_OK;
+}
+
+int mtsg_debug_wavetimes(mtsg_scene *s, uint64_t *out, uint32_t max_launches, uint32_t *waves) {
+    if (!s || !waves || (!out && max_launches)) return MTSG_ERR_INVALID;
+    *waves = (uint32_t)s->traceGrid;
+    const uint32_t n = std::min(max_launches, s->wtLaunches);
+    if (n && s->waveTimes &&
+        hipMemcpy(out, s->waveTimes, (size_t)2 * s->traceGrid * n * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return MTSG_ERR_DEVICE;
+    return (int)s->wtLaunches;
+}
+
+int mtsg_debug_stragglers(mtsg_scene *s, float *out, uint32_t max_rays) {
+    if (!s || (!out && max_rays)) return MTSG_ERR_INVALID;
+    const uint32_t n = (uint32_t)(s->stragglers.size() / 8);
+    for (uint32_t k = 0; k < std::min(n, max_rays); ++k)
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t bits = (uint32_t)s->stragglers[8 * k + j];
+            float f;
+            memcpy(&f, &bits, 4);
+            out[8 * k + j] = j < 6 ? f : (float)bits;
+        }
+    return (int)n;
 }
 
 void mtsg_cancel(mtsg_scene *s) {
@@ -2235,11 +2396,11 @@ static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, fl
     if (e == hipSuccess) e = alloc((void **)po, f4, out.data());
     if (e == hipSuccess && shadow) e = alloc((void **)&D.sh_c, f4, c.data());
     if (e == hipSuccess) e = alloc((void **)&D.cnt, CNT_WORDS * sizeof(uint32_t), nullptr);
-    if (e == hipSuccess) e = alloc((void **)&D.ctr, 16 * sizeof(unsigned long long), nullptr);
+    if (e == hipSuccess) e = alloc((void **)&D.ctr, CTR_WORDS * sizeof(unsigned long long), nullptr);
     if (e == hipSuccess && shadow) e = hipMemcpy(D.cnt + CNT_S0, &n, sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) { g_err = hipGetErrorString(e); cleanup(); return MTSG_ERR_DEVICE; }
-    if (shadow) launch_trace(s, false, D, -2, 0, 0u);
-    else launch_trace(s, false, D, -1, -1, n);
+    if (shadow) launch_trace(s, false, D, -2, 0, 0u, s->stream);
+    else launch_trace(s, false, D, -1, -1, n, s->stream);
     e = hipStreamSynchronize(s->stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpy(out.data(), *po, f4, hipMemcpyDeviceToHost);
@@ -2367,6 +2528,9 @@ void mtsg_scene_destroy(mtsg_scene *s) {
     for (void *p : s->allocs) hipFree(p);
     for (hipEvent_t e : s->evPool) hipEventDestroy(e);
     if (s->hostCnt) hipHostFree(s->hostCnt);
+    if (s->waveTimes) hipFree(s->waveTimes);
+    for (int l = 1; l < MTSG_MAX_LANES; ++l)
+        if (s->lstream[l]) hipStreamDestroy(s->lstream[l]);
     if (s->stream) hipStreamDestroy(s->stream);
     delete s;
 }

@@ -24,6 +24,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 MTSG_OK = 0
 MTSG_FLAG_TIMING = 1
 MTSG_FLAG_COUNT = 2
+MTSG_FLAG_WAVETIME = 4
 
 
 class RenderParams(C.Structure):
@@ -61,6 +62,8 @@ class Stats(C.Structure):
         ("shadow_wave_node_iters", C.c_uint64), ("shadow_wave_test_iters", C.c_uint64),
         ("shadow_wave_steps", C.c_uint64), ("shadow_wave_active_lanes", C.c_uint64),
         ("launches_trace_shadow", C.c_uint64),
+        ("iter_max_closest", C.c_uint64), ("iter_max_shadow", C.c_uint64),
+        ("iter_hist_closest", C.c_uint64 * 16), ("iter_hist_shadow", C.c_uint64 * 16),
     ]
 
 
