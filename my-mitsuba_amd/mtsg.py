@@ -88,7 +88,7 @@ DEVICE_SYMBOLS = [
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
-    "mtsg_last_error", "mtsg_env_eval", "mtsg_sampler_draws",
+    "mtsg_last_error", "mtsg_env_eval", "mtsg_sampler_draws", "mtsg_debug_wavetimes", "mtsg_debug_stragglers",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_scene_desc", "mtsh_scene_render_params",
