@@ -346,14 +346,16 @@ void mtsg_cancel(mtsg_scene *scene);
 
 int  mtsg_set_flags(mtsg_scene *scene, uint32_t flags);
 int  mtsg_get_stats(mtsg_scene *scene, mtsg_stats *out);
-/* Debug: rays of the last MTSG_FLAG_COUNT render that needed >= 192
- * traversal iterations (up to 64 captured): 8 floats each, o.xyz, d.xyz,
- * iterations, shadow (0/1).  Returns the number captured.  No reference
+/* Debug: rays of the last MTSG_FLAG_COUNT render that needed >= 300
+ * traversal iterations (up to 64 captured): 12 floats each, o.xyz, d.xyz,
+ * iterations, shadow (0/1), inner nodes, primitive tests, kd-restarts, 0.
+ * Returns the number captured.  No reference
  * counterpart (instrumentation in the spirit of
  * rayIntersectHavranCollectStatistics, sahkdtree3.h:310-432).             */
-/* Debug: with MTSG_FLAG_WAVETIME, the start and exit times (100-MHz
- * wall-clock ticks) of every wave of the last render's traversal launches:
- * out[launch][wave][2], up to max_launches launches of *waves waves each.
+/* Debug: with MTSG_FLAG_WAVETIME, per wave of the last render's traversal
+ * launches: start and exit time, the time it found the work list empty
+ * (100-MHz wall-clock ticks; 0: never) and its loop iterations after that:
+ * out[launch][wave][4], up to max_launches launches of *waves waves each.
  * Returns the number of launches recorded.                                 */
 int  mtsg_debug_wavetimes(mtsg_scene *scene, uint64_t *out, uint32_t max_launches, uint32_t *waves);
 int  mtsg_debug_stragglers(mtsg_scene *scene, float *out, uint32_t max_rays);

@@ -28,11 +28,12 @@ for kind in ("closest", "shadow"):
             print(f"  [{1 << k:6d}, {2 << k:6d}): {c:12d}  {c / tot:.2e}")
 import ctypes as C  # noqa: E402
 import numpy as np  # noqa: E402
-buf = np.zeros((64, 8), np.float32)
+buf = np.zeros((64, 12), np.float32)
 n = mtsg.device_lib().mtsg_debug_stragglers(g._h, C.c_void_p(buf.ctypes.data), 64)
 print(f"stragglers captured: {n}")
 for r in buf[:min(n, 64)]:
-    print("  o %9.4f %9.4f %9.4f  d %8.5f %8.5f %8.5f  iters %4d %s" % (*r[:6], r[6], "shadow" if r[7] else "closest"))
+    print("  o %9.4f %9.4f %9.4f  d %8.5f %8.5f %8.5f  iters %4d %-7s nodes %4d tests %4d restarts %3d"
+          % (*r[:6], r[6], "shadow" if r[7] else "closest", r[8], r[9], r[10]))
 np.save(os.path.join(REPO, "gpurun_out", "stragglers.npy"), buf[:min(n, 64)])
 g.free(film)
 g.close()
