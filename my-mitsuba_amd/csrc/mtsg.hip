@@ -158,13 +158,6 @@ struct DevPaths {
     float4 *sh_c;     // NEE contribution, target (bits): next-bounce position, or 1 << 31 | slot
     uint32_t *cnt;    // counters, each on its own 256-B line (see CNT_*)
     unsigned long long *ctr;  // traversal counters (nodes, refs, tests)
-    // ray migration queues of the traversal drain (see k_trace_s): record
-    // of slot k at mig[k * MIG_U64, (k + 1) * MIG_U64), XCD x owns slots
-    // [x * migPer, (x + 1) * migPer); migFlag[k] = epoch of the launch that
-    // published slot k
-    unsigned long long *mig;
-    uint32_t *migFlag;
-    uint32_t migPer;
 };
 
 // queue / fetch counters live on separate 256-byte lines: a single
@@ -176,10 +169,7 @@ constexpr int XGROUPS = 8;                  // XCDs: blocks b and b + 8 share on
 constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S0 = 128, CNT_S1 = 192;
 constexpr int CNT_ERR = 96;   // sticky error flags (1: QMC dimension limit)
 constexpr int CNT_FETCH = 256;                           // XGROUPS counters, 32 words apart
-// ray migration queues of the traversal drain, one per XCD x (hardware
-// XCC_ID): reserve tail at CNT_MIG + 64 x, pop head at + 512, live waves at + 1024
-constexpr int CNT_MIG = 512;
-constexpr int CNT_WORDS = CNT_MIG + 3 * 512;
+constexpr int CNT_WORDS = CNT_FETCH + 32 * XGROUPS;
 constexpr int HOSTCNT_STRIDE = 256;
 // traversal counters (MTSG_FLAG_COUNT): [0,7) closest, [8,15) shadow (see
 // flush_counts), 7 / 15 the maximum iterations per ray, [16,32) / [32,48)
@@ -639,244 +629,6 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
 }
 
-// Cooperative leaf testing for the launch tail.  Once the work list is
-// exhausted a wave holds only its last rays, and a ray's latency -- one
-// primitive per iteration, ~1 us each -- is what ends the launch (measured:
-// 10% to 100% of the waves exit over ~0.5-0.8 ms).  The idle lanes then
-// test the pending primitives of the active lanes' held leaves: each owner
-// lane gets a contiguous run of helper lanes, each helper tests one
-// primitive against the owner's ray, and a segmented min over the run picks
-// the hit.  The key (t bits, then the highest leaf position on equal t)
-// reproduces the serial loop's inclusive `t <= best` order, so t, u, v and
-// the primitive are those of the one-lane traversal.  Everything is wave
-// shuffles: no LDS beyond the short stacks (8 waves/SIMD stay resident).
-// Returns true when the lane's shadow ray is occluded.
-#ifndef MTSG_COOP_MAX
-#define MTSG_COOP_MAX 0    // active lanes at or below which a tail wave cooperates (0: off; 16 measured
-                              // 1-2% slower: the drain is issue-bound on sparse waves, see ray migration)
-#endif
-constexpr uint32_t COOP_MAX = MTSG_COOP_MAX;
-
-DEV uint32_t shfl_u(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src); }
-DEV float shfl_f(float v, uint32_t src) { return __shfl(v, (int)src); }
-
-template <bool COUNT>
-DEV bool coop_leaf(const DevScene &S, SpecRay &r, bool active, float4 *hitOut, TraceCounts &cnt) {
-    const uint32_t lane = lane_here();
-    const uint32_t pend = (active && r.lfE < r.lfEnd) ? min(r.lfEnd - r.lfE, 64u) : 0u;
-    uint32_t incl = pend;   // inclusive scan of the pending counts
-#pragma unroll
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
-        if (lane >= off) incl += v;
-    }
-    const uint32_t excl = incl - pend;
-    const uint32_t total = min(shfl_u(incl, 63), 64u);
-    if (total == 0) return false;   // wave-uniform
-    const uint32_t granted = excl < 64u ? min(pend, 64u - excl) : 0u;
-    // owner of helper lane j: the first lane whose inclusive count exceeds j
-    uint32_t owner = 0;
-#pragma unroll
-    for (uint32_t step = 32; step; step >>= 1)
-        if (shfl_u(incl, owner + step - 1) <= lane) owner += step;
-    owner = min(owner, 63u);
-    const bool helper = lane < total;
-    const uint32_t oExcl = shfl_u(excl, owner), oGrant = shfl_u(granted, owner), oE = shfl_u(r.lfE, owner);
-    const float3 o = mk3(shfl_f(r.o.x, owner), shfl_f(r.o.y, owner), shfl_f(r.o.z, owner));
-    const float3 d = mk3(shfl_f(r.d.x, owner), shfl_f(r.d.y, owner), shfl_f(r.d.z, owner));
-    const float mint = shfl_f(r.mint, owner), best = shfl_f(r.best, owner);
-    const uint32_t pos = helper ? oE + (lane - oExcl) : 0u;
-    const float4 *rec = S.triL + (size_t)(3u * pos);
-    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-    float t, u, v;
-    bool h = tri_test(f0, f1, f2, o, d, mint, best, u, v, t);
-    const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
-    if (helper && isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], o, d, mint, best, t, u, v);
-    h = h && helper;
-    const uint32_t hid = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
-    // segmented min of (t, ~position) over each owner's run of helpers
-    uint32_t kHi = h ? __float_as_uint(t) : 0xFFFFFFFFu, kLo = h ? 0xFFFFFFFFu - pos : 0xFFFFFFFFu;
-    const uint32_t segEnd = oExcl + oGrant;
-#pragma unroll
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t oHi = (uint32_t)__shfl_down((int)kHi, off), oLo = (uint32_t)__shfl_down((int)kLo, off);
-        if (lane + off < segEnd && (oHi < kHi || (oHi == kHi && oLo < kLo))) { kHi = oHi; kLo = oLo; }
-    }
-    // each owner reads its run's head, then the winning helper's u, v, id
-    const uint32_t head = granted ? excl : lane;
-    const uint32_t mHi = shfl_u(kHi, head), mLo = shfl_u(kLo, head);
-    const bool got = granted && !(mHi == 0xFFFFFFFFu && mLo == 0xFFFFFFFFu);
-    const uint32_t win = got ? excl + ((0xFFFFFFFFu - mLo) - r.lfE) : lane;
-    const float wu = shfl_f(u, win), wv = shfl_f(v, win);
-    const uint32_t wid = shfl_u(hid, win);
-    if (granted) {
-        r.lfE += granted;
-        if (COUNT) { cnt.refs += granted; cnt.tests += granted; }
-        if (got) {
-            r.bits |= SB_FOUND;
-            if (r.bits & SB_SHADOW) return true;
-            r.best = __uint_as_float(mHi);
-            stS(hitOut, make_float4(r.best, wu, wv, __uint_as_float(wid)));
-        }
-    }
-    return false;
-}
-
-// ---------------------------------------------------------------------------
-// Ray migration for the launch drain.  Once the work list is exhausted every
-// wave still holds up to 64 rays, and measured wave exits spread over
-// ~0.9 ms (C3 at 1/8 of the frame): the SIMDs stay issue-bound on waves with a
-// handful of live lanes (8 waves/SIMD each paying full-wave instruction
-// issue), so the per-iteration time stays at its loaded value until most
-// waves have left.  A drain wave with at most MIG_K live rays instead writes
-// them (ray, traversal state and its short stack: 144 B each) to its XCD's
-// queue and exits; drain waves with MIG_IDLE or more idle lanes adopt queued
-// rays into those lanes.  The rays continue exactly where they stopped, so
-// results are bit-identical.  Liveness: a wave registers on its XCD's live
-// count when it first finds the work list empty and leaves with one
-// decrement after any hand-off; the wave whose decrement empties the count
-// ("last") re-adopts whatever is queued and never hands rays off, so every
-// queued ray is adopted.  Each wave hands off at most once per launch, so an
-// XCD's queue holds at most gridDim * MIG_K records.
-// Visibility (MI355X_MICROARCH.md, inter-workgroup hand-off): records are
-// written with 8-B agent-scope (sc1, write-through) stores, drained with
-// s_waitcnt vmcnt(0), then published by an agent-scope flag store = epoch;
-// the adopter polls the flag relaxed and reads every record word with
-// agent-scope (sc1) loads, so no L2 write-back or L1 invalidate is needed;
-// a queue is only touched by waves of one XCD (hardware XCC_ID).
-// ---------------------------------------------------------------------------
-#ifndef MTSG_MIGRATE
-#define MTSG_MIGRATE 0    // live rays at or below which a drain wave hands them off (0: off; 16 measured
-                          // slower: 1445 vs 1481 Msamples/s C3, 8605 vs 9540 at 1/8 of the frame)
-#endif
-#ifndef MTSG_MIG_IDLE
-#define MTSG_MIG_IDLE 16  // idle lanes at which a drain wave adopts queued rays
-#endif
-#ifndef MTSG_MIG_GAP
-#define MTSG_MIG_GAP 16   // iterations a drain wave waits after finding its queue empty
-#endif
-constexpr uint32_t MIG_K = MTSG_MIGRATE, MIG_IDLE = MTSG_MIG_IDLE, MIG_GAP = MTSG_MIG_GAP;
-constexpr uint32_t MIG_U64 = (18 + 3 * SHORT_STACK + 1) / 2;   // 8-B words per record
-constexpr uint32_t MIG_SPIN_LIMIT = 1u << 24;                  // give-up bound of a flag poll
-
-typedef __attribute__((address_space(1))) unsigned long long g_u64;
-typedef __attribute__((address_space(1))) uint32_t g_u32;
-DEV uint32_t xcc_id() {
-    uint32_t x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    return x & 7u;
-}
-DEV void mig_st(unsigned long long *p, uint32_t lo, uint32_t hi) {
-    __hip_atomic_store((g_u64 *)p, (unsigned long long)lo | (unsigned long long)hi << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-DEV uint2 mig_ld(const unsigned long long *p) {
-    const unsigned long long v = __hip_atomic_load((g_u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-}
-DEV uint32_t cnt_ld(uint32_t *p) { return __hip_atomic_load((g_u32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// record words of a lane's ray (k-th 32-bit word; k < 2 * MIG_U64)
-DEV uint32_t mig_word(const SpecRay &r, uint32_t idx, uint32_t iters, SpecStack stk, uint32_t k) {
-    switch (k) {
-        case 0: return __float_as_uint(r.o.x);
-        case 1: return __float_as_uint(r.o.y);
-        case 2: return __float_as_uint(r.o.z);
-        case 3: return __float_as_uint(r.d.x);
-        case 4: return __float_as_uint(r.d.y);
-        case 5: return __float_as_uint(r.d.z);
-        case 6: return __float_as_uint(r.mint);
-        case 7: return __float_as_uint(r.best);
-        case 8: return __float_as_uint(r.tmin);
-        case 9: return __float_as_uint(r.tmax);
-        case 10: return r.cur.x;
-        case 11: return r.cur.y;
-        case 12: return r.lfE;
-        case 13: return r.lfEnd;
-        case 14: return __float_as_uint(r.lfTmax);
-        case 15: return r.bits;
-        case 16: return idx;
-        case 17: return iters;
-        default: {
-            const uint32_t e = (k - 18) / 3, f = (k - 18) % 3;
-            if (e >= (uint32_t)SHORT_STACK) return 0u;
-            return f == 0 ? stk.node(e).x : (f == 1 ? stk.node(e).y : __float_as_uint(stk.t(e)));
-        }
-    }
-}
-
-// hand the active lanes' rays to XCD x's queue (whole wave, wave-uniform call)
-DEV void mig_dump(const DevPaths &P, uint32_t x, uint32_t epoch, const SpecRay &r, bool active, uint32_t idx,
-                  uint32_t iters, SpecStack stk) {
-    const unsigned long long am = __ballot(active);
-    uint32_t base = 0;
-    if (__lane_id() == 0) base = atomicAdd(&P.cnt[CNT_MIG + 64 * x], (uint32_t)__popcll(am));
-    base = __builtin_amdgcn_readfirstlane(base);
-    const uint32_t slot = x * P.migPer + base + rank_below(am);
-    if (active) {
-        unsigned long long *q = P.mig + (size_t)slot * MIG_U64;
-#pragma unroll
-        for (uint32_t j = 0; j < MIG_U64; ++j)
-            mig_st(q + j, mig_word(r, idx, iters, stk, 2 * j), mig_word(r, idx, iters, stk, 2 * j + 1));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (active) __hip_atomic_store((g_u32 *)&P.migFlag[slot], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// reserve up to `want` queued records of XCD x: lane 0 advances the head by
-// CAS below the tail; returns the count (wave-uniform), first slot in base
-DEV uint32_t mig_take(const DevPaths &P, uint32_t x, uint32_t want, uint32_t &base) {
-    uint32_t got = 0, h = 0;
-    if (__lane_id() == 0) {
-        uint32_t *head = &P.cnt[CNT_MIG + 512 + 64 * x], *tail = &P.cnt[CNT_MIG + 64 * x];
-        h = cnt_ld(head);
-        for (;;) {
-            const uint32_t t = cnt_ld(tail);
-            if (h >= t) break;
-            const uint32_t n = min(want, t - h);
-            if (__hip_atomic_compare_exchange_strong((g_u32 *)head, &h, h + n, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)) { got = n; break; }
-        }
-    }
-    base = __builtin_amdgcn_readfirstlane(h);
-    return __builtin_amdgcn_readfirstlane(got);
-}
-
-// adopt record `slot`: poll its flag, then restore the ray and its short stack
-DEV bool mig_adopt(const DevPaths &P, uint32_t slot, uint32_t epoch, SpecRay &r, uint32_t &idx, uint32_t &iters, SpecStack stk) {
-    uint32_t spins = 0;
-    while (__hip_atomic_load((g_u32 *)&P.migFlag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-        if (++spins > MIG_SPIN_LIMIT) return false;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the record loads behind the poll
-    const unsigned long long *q = P.mig + (size_t)slot * MIG_U64;
-    uint32_t w[2 * MIG_U64];
-#pragma unroll
-    for (uint32_t j = 0; j < MIG_U64; ++j) {
-        const uint2 v = mig_ld(q + j);
-        w[2 * j] = v.x;
-        w[2 * j + 1] = v.y;
-    }
-    r.o = mk3(__uint_as_float(w[0]), __uint_as_float(w[1]), __uint_as_float(w[2]));
-    r.d = mk3(__uint_as_float(w[3]), __uint_as_float(w[4]), __uint_as_float(w[5]));
-    r.inv = mk3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);   // as spec_init
-    r.mint = __uint_as_float(w[6]);
-    r.best = __uint_as_float(w[7]);
-    r.tmin = __uint_as_float(w[8]);
-    r.tmax = __uint_as_float(w[9]);
-    r.cur = make_uint2(w[10], w[11]);
-    r.lfE = w[12];
-    r.lfEnd = w[13];
-    r.lfTmax = __uint_as_float(w[14]);
-    r.bits = w[15];
-    idx = w[16];
-    iters = w[17];
-#pragma unroll
-    for (uint32_t e = 0; e < (uint32_t)SHORT_STACK; ++e)
-        stk.push(e, make_uint2(w[18 + 3 * e], w[19 + 3 * e]), __uint_as_float(w[20 + 3 * e]));
-    return true;
-}
-
 // Persistent traversal kernel with lane-level refill (the "while-while +
 // dynamic fetch" structure of Aila & Laine 2009, re-tiled for 64-lane waves):
 // a wave reserves FETCH work-list entries with ONE atomic into a wave-uniform
@@ -891,8 +643,7 @@ DEV bool mig_adopt(const DevPaths &P, uint32_t slot, uint32_t epoch, SpecRay &r,
 //   sIn: 0/1 = count in CNT_S0/CNT_S1, -1 = none
 
 template <bool COUNT, int MIN_IDLE>
-__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, uint32_t epoch,
-                                    unsigned long long *wt) {
+__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
     const SpecStack stk{};
     const unsigned long long tStart = wt ? wall_clock64() : 0ull;
     const uint32_t nC = cIn == -1 ? nIdentity : (cIn >= 0 ? __atomic_load_n(&P.cnt[cnt_q(cIn)], __ATOMIC_RELAXED) : 0u);
@@ -905,9 +656,6 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
     uint32_t idx = 0;                      // index into the ray's own list
     uint32_t iters = 0;                    // COUNT: iterations of this ray
     uint32_t n0 = 0, t0c = 0, r0 = 0;      // COUNT: the lane's node / test / restart totals at its start
-    uint32_t xcc = 0;                      // drain: this wave's XCD (migration queue)
-    bool registered = false, last = false; // drain: on the XCD's live count / the wave that emptied it
-    uint32_t pollWait = 0;                 // drain: iterations before the next queue poll (wave-uniform)
     unsigned long long tExh = 0;           // wt: when the work list was found empty
     uint32_t drainIters = 0;               // wt: loop iterations after that
     SpecRay r;
@@ -947,58 +695,7 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
             idle = __ballot(!active);
             if (take == nIdle) break;
         }
-        if (MIG_K && exhausted) {
-            // drain: adopt queued rays into idle lanes, or hand a sparse wave's rays off
-            if (!registered) {
-                xcc = xcc_id();
-                if (__lane_id() == 0) atomicAdd(&P.cnt[CNT_MIG + 1024 + 64 * xcc], 1u);
-                registered = true;
-            }
-            unsigned long long am = __ballot(active);
-            uint32_t nAct = (uint32_t)__popcll(am);
-            // the queue words are shared by every drain wave of the XCD: a wave
-            // polls when it is about to hand off or leave, or (throttled) when
-            // MIG_IDLE of its lanes are idle
-            if (nAct == 0 || (nAct <= MIG_K && !last) || (64u - nAct >= MIG_IDLE && pollWait == 0)) {
-                uint32_t base;
-                const uint32_t got = mig_take(P, xcc, 64u - nAct, base);
-                pollWait = got ? 0u : MIG_GAP;
-                if (got) {
-                    const uint32_t rank = rank_below(~am);
-                    if (!active && rank < got) {
-                        active = mig_adopt(P, xcc * P.migPer + base + rank, epoch, r, idx, iters, stk);
-                        if (!active) atomicOr(&P.cnt[CNT_ERR], 2u);   // flag never published: give up loudly
-                        if (COUNT) {
-                            const TraceCounts &k = (r.bits & SB_SHADOW) ? cs : cc;
-                            n0 = k.nodes; t0c = k.tests; r0 = k.restarts;
-                            atomicAdd(&P.ctr[50], 1ull);
-                        }
-                    }
-                    am = __ballot(active);
-                    nAct = (uint32_t)__popcll(am);
-                }
-            } else if (pollWait) {
-                --pollWait;
-            }
-            if (nAct == 0 || (nAct <= MIG_K && !last)) {
-                if (last) {
-                    // nothing held: leave once the queue is empty
-                    if (cnt_ld(&P.cnt[CNT_MIG + 512 + 64 * xcc]) >= cnt_ld(&P.cnt[CNT_MIG + 64 * xcc])) break;
-                    continue;
-                }
-                if (nAct) {
-                    mig_dump(P, xcc, epoch, r, active, idx, iters, stk);
-                    if (COUNT && __lane_id() == 0) atomicAdd(&P.ctr[49], (unsigned long long)nAct);
-                    active = false;
-                }
-                uint32_t old = 0;
-                if (__lane_id() == 0) old = atomicSub(&P.cnt[CNT_MIG + 1024 + 64 * xcc], 1u);
-                if (__builtin_amdgcn_readfirstlane(old) > 1u) break;
-                last = true;   // every other drain wave of this XCD has left: adopt what is queued
-                if (COUNT && __lane_id() == 0) atomicAdd(&P.ctr[51], 1ull);
-                continue;
-            }
-        } else if (!__any(active)) {
+        if (!__any(active)) {
             if (exhausted) break;
             continue;
         }
@@ -1013,9 +710,7 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
         }
         if (WT_DRAIN && wt && exhausted) ++drainIters;
         bool done = false;
-        if (COOP_MAX && exhausted && (uint32_t)__popcll(__ballot(active)) <= COOP_MAX)   // wave-uniform
-            done = coop_leaf<COUNT>(S, r, active, P.hit + idx, (COUNT && (r.bits & SB_SHADOW)) ? cs : cc);
-        if (active && !done) {
+        if (active) {
             if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx);
             else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx);
         }
@@ -1862,8 +1557,6 @@ __global__ void k_reset(uint32_t *cnt, int qout, int sOut) {
         if (sOut >= 0) cnt[sOut ? CNT_S1 : CNT_S0] = 0;
     }
     if (threadIdx.x < XGROUPS) cnt[CNT_FETCH + 32 * threadIdx.x] = 0;
-    if (threadIdx.x < 8)
-        for (int k = 0; k < 3; ++k) cnt[CNT_MIG + 512 * k + 64 * threadIdx.x] = 0;   // migration tail, head, live
 }
 
 // ---------------------------------------------------------------------------
@@ -1921,7 +1614,6 @@ struct mtsg_scene {
     std::vector<unsigned long long> stragglers;  // MTSG_FLAG_COUNT: slow-ray records
     unsigned long long *waveTimes = nullptr;     // MTSG_FLAG_WAVETIME: [launch][wave][WT_WORDS]
     uint32_t wtLaunches = 0;
-    uint32_t traceEpoch = 0;   // traversal launches so far (ray migration flag epoch)
 };
 
 namespace {
@@ -1937,12 +1629,6 @@ void free_batch(mtsg_scene *s) {
     s->capacity = 0;
     s->lanesAlloc = 0;
 }
-
-// ray migration queue sizes: each drain wave hands off at most once per
-// launch and at most MIG_K rays, so an XCD's queue holds <= grid * MIG_K
-uint32_t mig_per_xcd(const mtsg_scene *s) { return std::max(1u, (uint32_t)s->traceGrid * std::max(1u, MIG_K)); }
-size_t mig_bytes(uint32_t per) { return (size_t)8 * per * MIG_U64 * sizeof(unsigned long long); }
-size_t mig_flag_bytes(uint32_t per) { return (size_t)8 * per * sizeof(uint32_t); }
 
 int ensure_batch(mtsg_scene *s, uint32_t paths, int lanes) {
     if (s->capacity >= paths && s->lanesAlloc >= lanes) return MTSG_OK;
@@ -1966,10 +1652,6 @@ int ensure_batch(mtsg_scene *s, uint32_t paths, int lanes) {
     if ((rc = alloc(CNT_WORDS * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
     if ((rc = alloc(CTR_WORDS * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
     HIP_TRY(hipMemset(P.ctr, 0, CTR_WORDS * sizeof(unsigned long long)));
-    P.migPer = mig_per_xcd(s);
-    if ((rc = alloc(mig_bytes(P.migPer), (void **)&P.mig)) != MTSG_OK) return rc;
-    if ((rc = alloc(mig_flag_bytes(P.migPer), (void **)&P.migFlag)) != MTSG_OK) return rc;
-    HIP_TRY(hipMemset(P.migFlag, 0, mig_flag_bytes(P.migPer)));
     }
     s->capacity = paths;
     s->lanesAlloc = lanes;
@@ -2017,9 +1699,8 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t
     unsigned long long *wt = nullptr;
     if ((s->flags & MTSG_FLAG_WAVETIME) && s->waveTimes && s->wtLaunches < WT_MAX_LAUNCHES)
         wt = s->waveTimes + (size_t)WT_WORDS * s->traceGrid * s->wtLaunches++;
-    const uint32_t epoch = ++s->traceEpoch ? s->traceEpoch : ++s->traceEpoch;   // never 0 (flags start zeroed)
-    if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, epoch, wt);
-    else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, epoch, wt);
+    if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
 }
 void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn, uint32_t n, hipStream_t st) {
     if (count) launch_trace_c<true>(s, P, cIn, sIn, n, st);
@@ -2274,11 +1955,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             HIP_TRY(hipEventSynchronize(L.cntEv[L.last & 1]));
             account(l, L.last);
             // the error word is sticky within the batch: the last copy holds it
-            const uint32_t err = hostCnt(l, L.last)[CNT_ERR];
-            if (err & 2u) {
-                g_err = "traversal drain: a migrated ray record was never published";
-                result = MTSG_ERR_DEVICE;
-            } else if (err) {
+            if (hostCnt(l, L.last)[CNT_ERR]) {
                 g_err = "Lookup dimension exceeds the prime number table size! "
                         "You may have to reduce the 'maxDepth' parameter of your integrator.";
                 result = MTSG_ERR_INVALID;
@@ -2752,9 +2429,6 @@ static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, fl
     if (e == hipSuccess && shadow) e = alloc((void **)&D.sh_c, f4, c.data());
     if (e == hipSuccess) e = alloc((void **)&D.cnt, CNT_WORDS * sizeof(uint32_t), nullptr);
     if (e == hipSuccess) e = alloc((void **)&D.ctr, CTR_WORDS * sizeof(unsigned long long), nullptr);
-    D.migPer = mig_per_xcd(s);
-    if (e == hipSuccess) e = alloc((void **)&D.mig, mig_bytes(D.migPer), nullptr);
-    if (e == hipSuccess) e = alloc((void **)&D.migFlag, mig_flag_bytes(D.migPer), nullptr);
     if (e == hipSuccess && shadow) e = hipMemcpy(D.cnt + CNT_S0, &n, sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) { g_err = hipGetErrorString(e); cleanup(); return MTSG_ERR_DEVICE; }
     if (shadow) launch_trace(s, false, D, -2, 0, 0u, s->stream);
