@@ -96,7 +96,7 @@ enum {
     MTSG_BSDF_ROUGHCONDUCTOR = 2,   /* src/bsdfs/roughconductor.cpp */
     MTSG_BSDF_DIELECTRIC     = 3    /* src/bsdfs/dielectric.cpp     */
 };
-enum { MTSG_MF_BECKMANN = 0, MTSG_MF_GGX = 1 };
+enum { MTSG_MF_BECKMANN = 0, MTSG_MF_GGX = 1, MTSG_MF_PHONG = 2 };   /* microfacet.h:49-57 */
 
 typedef struct mtsg_bsdf {
     int32_t type;

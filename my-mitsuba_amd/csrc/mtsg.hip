@@ -888,24 +888,44 @@ DEV float hypot2_m(float a, float b) {   // math.cpp:74-86
 // MicrofacetDistribution, isotropic (microfacet.h:191-697)
 struct MF {
     int type;
-    float a;
+    float au, av;        // roughness along the shading tangent / bitangent
     bool visible;
+    float eu, ev;        // Phong exponents (computePhongExponent, microfacet.h:701-704)
+    DEV bool iso() const { return au == av; }
+    // microfacet.h:545-552
+    DEV float project(float3 v) const {
+        const float invSinTheta2 = 1 / (1.0f - v.z * v.z);
+        if (iso() || invSinTheta2 <= 0) return au;
+        const float cosPhi2 = v.x * v.x * invSinTheta2, sinPhi2 = v.y * v.y * invSinTheta2;
+        return sqrtf(cosPhi2 * au * au + sinPhi2 * av * av);
+    }
+    // microfacet.h:554-565 (RCPOVERFLOW_FLT = 2^-128)
+    DEV float phong_exponent(float3 v) const {
+        const float sinTheta2 = 1.0f - v.z * v.z;
+        if (iso() || sinTheta2 <= 2.93873587705571876e-39f) return eu;
+        const float invSinTheta2 = 1 / sinTheta2;
+        return eu * (v.x * v.x * invSinTheta2) + ev * (v.y * v.y * invSinTheta2);
+    }
+    // microfacet.h:191-234
     DEV float D(float3 m) const {
         if (m.z <= 0) return 0.0f;
         float ct2 = m.z * m.z;
-        float be = ((m.x * m.x) / (a * a) + (m.y * m.y) / (a * a)) / ct2;
+        float be = ((m.x * m.x) / (au * au) + (m.y * m.y) / (av * av)) / ct2;
         float result;
-        if (type == MTSG_MF_BECKMANN) result = expf(-be) / (kPi * a * a * ct2 * ct2);
-        else { float root = (1.0f + be) * ct2; result = 1.0f / (kPi * a * a * root * root); }
+        if (type == MTSG_MF_BECKMANN) result = expf(-be) / (kPi * au * av * ct2 * ct2);
+        else if (type == MTSG_MF_GGX) { float root = (1.0f + be) * ct2; result = 1.0f / (kPi * au * av * root * root); }
+        else result = sqrtf((eu + 2) * (ev + 2)) * (0.5f * kInvPi) * powf(m.z, phong_exponent(m));
         if (result * m.z < 1e-20f) result = 0;
         return result;
     }
+    // microfacet.h:477-514 (Phong uses the Beckmann approximation)
     DEV float G1(float3 v, float3 m) const {
         if (dot(v, m) * v.z <= 0) return 0.0f;
         float temp = 1 - v.z * v.z;
         float tt = temp <= 0.0f ? 0.0f : fabsf(sqrtf(temp) / v.z);
         if (tt == 0.0f) return 1.0f;
-        if (type == MTSG_MF_BECKMANN) {
+        const float a = project(v);
+        if (type != MTSG_MF_GGX) {
             float aa = 1.0f / (a * tt);
             if (aa >= 1.6f) return 1.0f;
             float aSqr = aa * aa;
@@ -967,9 +987,10 @@ struct MF {
                   (sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) - 0.539825872510702f);
         sly = S * z * sqrtf(1.0f + slx * slx);
     }
+    // sampleVisible (microfacet.h:421-459) or sampleAll (:287-397)
     DEV float3 sample(float3 wi_, float sx, float sy, float &pdf) const {
         if (visible) {
-            float3 wi = normalize(mk3(a * wi_.x, a * wi_.y, wi_.z));
+            float3 wi = normalize(mk3(au * wi_.x, av * wi_.y, wi_.z));
             float theta = 0, phi = 0;
             if (wi.z < 0.99999f) { theta = acosf(wi.z); phi = atan2f(wi.y, wi.x); }
             float sinPhi, cosPhi;
@@ -977,31 +998,81 @@ struct MF {
             float slx, sly;
             visible11(theta, sx, sy, slx, sly);
             float rx = cosPhi * slx - sinPhi * sly, ry = sinPhi * slx + cosPhi * sly;
-            rx *= a; ry *= a;
+            rx *= au; ry *= av;
             float normalization = 1.0f / sqrtf(rx * rx + ry * ry + 1.0f);
             float3 m = mk3(-rx * normalization, -ry * normalization, normalization);
             pdf = wi_.z == 0 ? 0.0f : G1(wi_, m) * fabsf(dot(wi_, m)) * D(m) / fabsf(wi_.z);
             return m;
         }
-        float alphaSqr = a * a;
-        float sinPhiM, cosPhiM;
-        sincosf((2.0f * kPi) * sy, &sinPhiM, &cosPhiM);
-        float cosThetaM;
-        if (type == MTSG_MF_BECKMANN) {
-            float t2 = alphaSqr * -logf(1.0f - sx);
-            cosThetaM = 1.0f / sqrtf(1.0f + t2);
-            pdf = (1.0f - sx) / (kPi * a * a * cosThetaM * cosThetaM * cosThetaM);
+        float sinPhiM, cosPhiM, cosThetaM;
+        if (type == MTSG_MF_PHONG) {
+            float phiM, exponent;
+            if (iso()) {
+                phiM = (2.0f * kPi) * sy;
+                exponent = eu;
+            } else if (sy < 0.25f) {
+                phong_quadrant(4 * sy, phiM, exponent);
+            } else if (sy < 0.5f) {
+                phong_quadrant(4 * (0.5f - sy), phiM, exponent);
+                phiM = kPi - phiM;
+            } else if (sy < 0.75f) {
+                phong_quadrant(4 * (sy - 0.5f), phiM, exponent);
+                phiM += kPi;
+            } else {
+                phong_quadrant(4 * (1 - sy), phiM, exponent);
+                phiM = 2 * kPi - phiM;
+            }
+            sincosf(phiM, &sinPhiM, &cosPhiM);
+            cosThetaM = powf(sx, 1.0f / (exponent + 2.0f));
+            pdf = sqrtf((eu + 2.0f) * (ev + 2.0f)) * (0.5f * kInvPi) * powf(cosThetaM, exponent + 1.0f);
         } else {
-            float t2 = alphaSqr * sx / (1.0f - sx);
-            cosThetaM = 1.0f / sqrtf(1.0f + t2);
-            float temp = 1 + t2 / alphaSqr;
-            pdf = kInvPi / (a * a * cosThetaM * cosThetaM * cosThetaM * temp * temp);
+            float alphaSqr;
+            if (iso()) {
+                sincosf((2.0f * kPi) * sy, &sinPhiM, &cosPhiM);
+                alphaSqr = au * au;
+            } else {
+                const float phiM = atanf(av / au * tanf(kPi + 2 * kPi * sy)) + kPi * floorf(2 * sy + 0.5f);
+                sincosf(phiM, &sinPhiM, &cosPhiM);
+                const float cosSc = cosPhiM / au, sinSc = sinPhiM / av;
+                alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
+            }
+            if (type == MTSG_MF_BECKMANN) {
+                float t2 = alphaSqr * -logf(1.0f - sx);
+                cosThetaM = 1.0f / sqrtf(1.0f + t2);
+                pdf = (1.0f - sx) / (kPi * au * av * cosThetaM * cosThetaM * cosThetaM);
+            } else {
+                float t2 = alphaSqr * sx / (1.0f - sx);
+                cosThetaM = 1.0f / sqrtf(1.0f + t2);
+                float temp = 1 + t2 / alphaSqr;
+                pdf = kInvPi / (au * av * cosThetaM * cosThetaM * cosThetaM * temp * temp);
+            }
         }
         if (pdf < 1e-20f) pdf = 0;
         float sinThetaM = sqrtf(fmaxf(0.0f, 1 - cosThetaM * cosThetaM));
         return mk3(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
     }
+    // sampleFirstQuadrant (microfacet.h:707-715)
+    DEV void phong_quadrant(float u1, float &phi, float &exponent) const {
+        phi = atanf(sqrtf((eu + 2.0f) / (ev + 2.0f)) * tanf(kPi * u1 * 0.5f));
+        float sinPhi, cosPhi;
+        sincosf(phi, &sinPhi, &cosPhi);
+        exponent = eu * cosPhi * cosPhi + ev * sinPhi * sinPhi;
+    }
 };
+
+// MicrofacetDistribution(props) after the loader's clamping (microfacet.h:96-144):
+// Phong never samples visible normals
+DEV MF make_mf(const mtsg_bsdf &b) {
+    MF m;
+    m.type = b.distribution;
+    m.au = b.alpha_u;
+    m.av = b.alpha_v;
+    m.visible = b.sample_visible != 0 && b.distribution != MTSG_MF_PHONG;
+    const bool phong = b.distribution == MTSG_MF_PHONG;
+    m.eu = phong ? fmaxf(2.0f / (m.au * m.au) - 2.0f, 0.0f) : 0.0f;
+    m.ev = phong ? fmaxf(2.0f / (m.av * m.av) - 2.0f, 0.0f) : 0.0f;
+    return m;
+}
 
 // util.cpp:739-761
 DEV float3 fresnel_conductor(float cosThetaI, float3 eta, float3 k) {
@@ -1038,7 +1109,7 @@ DEV float3 bsdf_eval(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
     if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:235-293
         if (wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
         float3 H = normalize(wo + wi);
-        MF mf{b.distribution, b.alpha_u, b.sample_visible != 0};
+        const MF mf = make_mf(b);
         const float Dv = mf.D(H);
         if (mf.visible) pdf = Dv * mf.G1(wi, H) / (4.0f * wi.z);
         else pdf = Dv * H.z / (4 * fabsf(dot(wo, H)));
@@ -1063,7 +1134,7 @@ DEV bool bsdf_sample(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSamp
     }
     if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:345-394
         if (wi.z < 0) return false;
-        MF mf{b.distribution, b.alpha_u, b.sample_visible != 0};
+        const MF mf = make_mf(b);
         float pdf;
         float3 m = mf.sample(wi, sx, sy, pdf);
         if (pdf == 0) return false;

@@ -712,7 +712,8 @@ struct Loader {
                 std::string dn = lower(props.strings["distribution"]);
                 if (dn == "beckmann") distr = MTSG_MF_BECKMANN;
                 else if (dn == "ggx") distr = MTSG_MF_GGX;
-                else throw err("Specified an invalid distribution \"" + dn + "\" (this build supports beckmann, ggx)");
+                else if (dn == "phong" || dn == "as") distr = MTSG_MF_PHONG;
+                else throw err("Specified an invalid microfacet distribution \"" + dn + "\", must be \"beckmann\", \"ggx\", or \"phong\"/\"as\"!");
             }
             float au = 0.1f, av = 0.1f;
             if (props.has("alpha")) {
@@ -722,11 +723,11 @@ struct Loader {
                 if (!props.has("alphaU") || !props.has("alphaV")) throw err("Microfacet model: both 'alphaU' and 'alphaV' must be specified.");
                 au = props.getFloat("alphaU"); av = props.getFloat("alphaV");
             }
-            if (au != av) throw err("roughconductor: anisotropic roughness needs UV tangents, not supported by this build");
             au = std::max(au, 1e-4f); av = std::max(av, 1e-4f);
             d.type = MTSG_BSDF_ROUGHCONDUCTOR;
             d.distribution = distr;
-            d.sample_visible = props.getBool("sampleVisible", true) ? 1 : 0;
+            // visible-normal sampling is not supported for Phong (microfacet.h:140-144)
+            d.sample_visible = (props.getBool("sampleVisible", true) && distr != MTSG_MF_PHONG) ? 1 : 0;
             d.alpha_u = au; d.alpha_v = av;
             for (int i = 0; i < 3; ++i) { d.eta[i] = eta[i]; d.k[i] = k[i]; d.spec_refl[i] = spec[i]; }
             d.smooth = 1;

@@ -1192,11 +1192,32 @@ Vec squareToCosineHemisphere(float sx, float sy) {
     return Vec(px, py, z);
 }
 
-// MicrofacetDistribution (microfacet.h), isotropic alphaU == alphaV
+// MicrofacetDistribution (microfacet.h): Beckmann, GGX and Phong /
+// Ashikhmin-Shirley, isotropic or anisotropic
 struct Microfacet {
     int type;
     float au, av;
     bool sampleVisible;
+    float eu = 0, ev = 0;   // Phong exponents
+    Microfacet(int t, float u, float v, bool vis) : type(t), au(u), av(v), sampleVisible(vis) {
+        if (type == MTSG_MF_PHONG) {   // microfacet.h:140-144, computePhongExponent :701-704
+            sampleVisible = false;
+            eu = std::max(2.0f / (au * au) - 2.0f, 0.0f);
+            ev = std::max(2.0f / (av * av) - 2.0f, 0.0f);
+        }
+    }
+    bool isotropic() const { return au == av; }
+    float phongExponent(const Vec &v) const {   // interpolatePhongExponent :554-565
+        const float st2 = sinTheta2(v);
+        if (isotropic() || st2 <= 2.93873587705571876e-39f) return eu;
+        float inv = 1 / st2;
+        return eu * (v.x * v.x * inv) + ev * (v.y * v.y * inv);
+    }
+    void sampleFirstQuadrant(float u1, float &phi, float &exponent) const {   // :707-715
+        phi = std::atan(std::sqrt((eu + 2.0f) / (ev + 2.0f)) * std::tan((float)M_PI * u1 * 0.5f));
+        float sinPhi = std::sin(phi), cosPhi = std::cos(phi);
+        exponent = eu * cosPhi * cosPhi + ev * sinPhi * sinPhi;
+    }
     float eval(const Vec &m) const {   // microfacet.h:191-234
         if (cosTheta(m) <= 0) return 0.0f;
         float ct2 = cosTheta2(m);
@@ -1204,9 +1225,11 @@ struct Microfacet {
         float result;
         if (type == MTSG_MF_BECKMANN) {
             result = fastexp(-be) / ((float)M_PI * au * av * ct2 * ct2);
-        } else {
+        } else if (type == MTSG_MF_GGX) {
             float root = (1.0f + be) * ct2;
             result = 1.0f / ((float)M_PI * au * av * root * root);
+        } else {
+            result = std::sqrt((eu + 2) * (ev + 2)) * (float)(0.5 / M_PI) * std::pow(cosTheta(m), phongExponent(m));
         }
         if (result * cosTheta(m) < 1e-20f) result = 0;
         return result;
@@ -1222,7 +1245,7 @@ struct Microfacet {
         float tt = std::abs(tanTheta(v));
         if (tt == 0.0f) return 1.0f;
         float alpha = projectRoughness(v);
-        if (type == MTSG_MF_BECKMANN) {
+        if (type != MTSG_MF_GGX) {   // Phong uses the Beckmann approximation
             float a = 1.0f / (alpha * tt);
             if (a >= 1.6f) return 1.0f;
             float aSqr = a * a;
@@ -1303,19 +1326,49 @@ struct Microfacet {
         if (cosTheta(wi) == 0) return 0.0f;
         return smithG1(wi, m) * absDot(wi, m) * eval(m) / std::abs(cosTheta(wi));
     }
-    Vec sampleAll(float sx, float sy, float &pdf) const {   // :280-418 (isotropic)
-        float alphaSqr = au * au;
-        float sinPhiM = std::sin((2.0f * (float)M_PI) * sy), cosPhiM = std::cos((2.0f * (float)M_PI) * sy);
-        float cosThetaM;
-        if (type == MTSG_MF_BECKMANN) {
-            float tanThetaMSqr = alphaSqr * -fastlog(1.0f - sx);
-            cosThetaM = 1.0f / std::sqrt(1.0f + tanThetaMSqr);
-            pdf = (1.0f - sx) / ((float)M_PI * au * av * cosThetaM * cosThetaM * cosThetaM);
+    Vec sampleAll(float sx, float sy, float &pdf) const {   // :287-397
+        float sinPhiM, cosPhiM, cosThetaM;
+        if (type == MTSG_MF_PHONG) {
+            float phiM, exponent;
+            if (isotropic()) {
+                phiM = (2.0f * (float)M_PI) * sy;
+                exponent = eu;
+            } else if (sy < 0.25f) {
+                sampleFirstQuadrant(4 * sy, phiM, exponent);
+            } else if (sy < 0.5f) {
+                sampleFirstQuadrant(4 * (0.5f - sy), phiM, exponent);
+                phiM = (float)M_PI - phiM;
+            } else if (sy < 0.75f) {
+                sampleFirstQuadrant(4 * (sy - 0.5f), phiM, exponent);
+                phiM += (float)M_PI;
+            } else {
+                sampleFirstQuadrant(4 * (1 - sy), phiM, exponent);
+                phiM = 2 * (float)M_PI - phiM;
+            }
+            sinPhiM = std::sin(phiM); cosPhiM = std::cos(phiM);
+            cosThetaM = std::pow(sx, 1.0f / (exponent + 2.0f));
+            pdf = std::sqrt((eu + 2.0f) * (ev + 2.0f)) * (float)(0.5 / M_PI) * std::pow(cosThetaM, exponent + 1.0f);
         } else {
-            float tanThetaMSqr = alphaSqr * sx / (1.0f - sx);
-            cosThetaM = 1.0f / std::sqrt(1.0f + tanThetaMSqr);
-            float temp = 1 + tanThetaMSqr / alphaSqr;
-            pdf = kInvPi / (au * av * cosThetaM * cosThetaM * cosThetaM * temp * temp);
+            float alphaSqr;
+            if (isotropic()) {
+                sinPhiM = std::sin((2.0f * (float)M_PI) * sy); cosPhiM = std::cos((2.0f * (float)M_PI) * sy);
+                alphaSqr = au * au;
+            } else {
+                float phiM = std::atan(av / au * std::tan((float)M_PI + 2 * (float)M_PI * sy)) + (float)M_PI * std::floor(2 * sy + 0.5f);
+                sinPhiM = std::sin(phiM); cosPhiM = std::cos(phiM);
+                float cosSc = cosPhiM / au, sinSc = sinPhiM / av;
+                alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
+            }
+            if (type == MTSG_MF_BECKMANN) {
+                float tanThetaMSqr = alphaSqr * -fastlog(1.0f - sx);
+                cosThetaM = 1.0f / std::sqrt(1.0f + tanThetaMSqr);
+                pdf = (1.0f - sx) / ((float)M_PI * au * av * cosThetaM * cosThetaM * cosThetaM);
+            } else {
+                float tanThetaMSqr = alphaSqr * sx / (1.0f - sx);
+                cosThetaM = 1.0f / std::sqrt(1.0f + tanThetaMSqr);
+                float temp = 1 + tanThetaMSqr / alphaSqr;
+                pdf = kInvPi / (au * av * cosThetaM * cosThetaM * cosThetaM * temp * temp);
+            }
         }
         if (pdf < 1e-20f) pdf = 0;
         float sinThetaM = std::sqrt(std::max(0.0f, 1 - cosThetaM * cosThetaM));
@@ -1334,7 +1387,7 @@ struct Microfacet {
     }
 };
 
-inline Microfacet mfOf(const mtsg_bsdf &b) { return Microfacet{b.distribution, b.alpha_u, b.alpha_v, b.sample_visible != 0}; }
+inline Microfacet mfOf(const mtsg_bsdf &b) { return Microfacet(b.distribution, b.alpha_u, b.alpha_v, b.sample_visible != 0); }
 
 // util.cpp:651-681
 float fresnelDielectricExt(float cosThetaI_, float &cosThetaT_, float eta) {

@@ -29,7 +29,7 @@ N_SAMPLES = THETA_BINS * PHI_BINS * 1000
 WI_PER_BSDF = 5
 
 DIFFUSE, ROUGHCONDUCTOR, DIELECTRIC = 1, 2, 3
-BECKMANN, GGX = 0, 1
+BECKMANN, GGX, PHONG = 0, 1, 2
 
 
 class Bsdf(C.Structure):
@@ -42,7 +42,7 @@ class Bsdf(C.Structure):
                 ("ior_eta", C.c_float), ("ior_inv_eta", C.c_float)]
 
 
-def make_bsdf(kind, dist=GGX, alpha=0.2, visible=1, eta=1.5046):
+def make_bsdf(kind, dist=GGX, alpha=0.2, visible=1, eta=1.5046, alpha_v=None):
     b = Bsdf()
     b.type = kind
     b.distribution = dist
@@ -53,7 +53,8 @@ def make_bsdf(kind, dist=GGX, alpha=0.2, visible=1, eta=1.5046):
     b.k[:] = (3.91295, 2.45285, 2.14219)
     b.spec_refl[:] = (1.0, 1.0, 1.0)
     b.spec_trans[:] = (1.0, 1.0, 1.0)
-    b.alpha_u = b.alpha_v = alpha
+    b.alpha_u = alpha
+    b.alpha_v = alpha if alpha_v is None else alpha_v
     b.ior_eta, b.ior_inv_eta = eta, 1.0 / eta
     return b
 
@@ -87,9 +88,10 @@ def evaluate(b, wi, wo):
     return val, pdf
 
 
-def expected_counts(b, wi, n_samples, gl=12):
+def expected_counts(b, wi, n_samples, gl=32):
     """n_samples x integral of pdf(wo) sin(theta) over each (theta, phi) cell
-    (tensor Gauss-Legendre, gl x gl nodes per cell)."""
+    (tensor Gauss-Legendre, gl x gl nodes per cell: 12 under-resolves the
+    alpha = 0.1 lobes of the anisotropic cases)."""
     x, w = np.polynomial.legendre.leggauss(gl)
     dth, dph = math.pi / THETA_BINS, 2 * math.pi / PHI_BINS
     ti = np.arange(THETA_BINS)[:, None, None, None]
@@ -156,6 +158,14 @@ CASES = [
     ("ggx_0.5_classic", dict(kind=ROUGHCONDUCTOR, dist=GGX, alpha=0.5, visible=0)),
     ("beckmann_0.1_visible", dict(kind=ROUGHCONDUCTOR, dist=BECKMANN, alpha=0.1, visible=1)),
     ("beckmann_0.3_classic", dict(kind=ROUGHCONDUCTOR, dist=BECKMANN, alpha=0.3, visible=0)),
+    # anisotropic roughness (alphaU != alphaV) and the Phong / Ashikhmin-Shirley
+    # distribution, as the reference's roughconductor instances of test_chisquare
+    ("ggx_aniso_visible", dict(kind=ROUGHCONDUCTOR, dist=GGX, alpha=0.1, alpha_v=0.4, visible=1)),
+    ("ggx_aniso_classic", dict(kind=ROUGHCONDUCTOR, dist=GGX, alpha=0.4, alpha_v=0.15, visible=0)),
+    ("beckmann_aniso_visible", dict(kind=ROUGHCONDUCTOR, dist=BECKMANN, alpha=0.3, alpha_v=0.1, visible=1)),
+    ("beckmann_aniso_classic", dict(kind=ROUGHCONDUCTOR, dist=BECKMANN, alpha=0.15, alpha_v=0.4, visible=0)),
+    ("phong_0.3", dict(kind=ROUGHCONDUCTOR, dist=PHONG, alpha=0.3, visible=0)),
+    ("phong_aniso", dict(kind=ROUGHCONDUCTOR, dist=PHONG, alpha=0.2, alpha_v=0.5, visible=0)),
 ]
 
 

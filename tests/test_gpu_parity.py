@@ -210,3 +210,23 @@ def test_envmap_lookup_parity(env_scene):
         L.oracle_env_eval_n(scene.desc, n, O._p(d), px, py, O._p(ref))
         got = g.env_eval(d, *args)
         np.testing.assert_allclose(got, ref, rtol=2e-4, atol=1e-6)
+
+
+ROUGH_VARIANTS = [
+    dict(dist="ggx", alphaU=0.05, alphaV=0.3),                           # anisotropic, visible normals
+    dict(dist="beckmann", alphaU=0.3, alphaV=0.08),
+    dict(dist="ggx", alphaU=0.4, alphaV=0.15, sampleVisible="false"),   # anisotropic sampleAll
+    dict(dist="as", alphaU=0.1, alphaV=0.3),                             # test_bsdf.xml's Ashikhmin-Shirley instance
+    dict(dist="phong", alphaU=0.25, alphaV=0.25),
+]
+
+
+@pytest.mark.parametrize("defs", ROUGH_VARIANTS, ids=lambda d: "-".join(str(v) for v in d.values()))
+def test_rough_conductor_variants_parity(defs):
+    # roughconductor with anisotropic roughness and the Phong / A&S distribution
+    # (microfacet.h: eval, smithG1 with projectRoughness, sampleAll, sampleVisible)
+    scene = mtsg.Scene(os.path.join(SCENES, "cbox_rough.xml"), dict(defs, width=48, height=48, spp=8))
+    g = mtsg.GPUScene(scene, 0)
+    _, c, gi = render_pair(scene, g)
+    check_render(c, gi)
+    g.close()

@@ -101,3 +101,24 @@ def test_bad_scene_reports_error(tmp_path):
         assert "bdpt" in str(e)
     else:
         raise AssertionError("expected an error")
+
+
+def test_microfacet_distribution_parsing(tmp_path):
+    # MicrofacetDistribution(props) (microfacet.h:96-144): beckmann / ggx /
+    # phong = as, anisotropic alphaU / alphaV, the alpha-vs-alphaU/V errors
+    for d in ("as", "phong", "ggx", "beckmann"):
+        s = mtsg.Scene(os.path.join(SCENES, "cbox_rough.xml"),
+                       {"width": 16, "height": 16, "spp": 1, "dist": d, "alphaU": 0.1, "alphaV": 0.3})
+        assert s.info.n_triangles == 24
+    bad = tmp_path / "bad.xml"
+    for body, msg in (('<string name="distribution" value="blinn"/>', "invalid microfacet distribution"),
+                      ('<float name="alpha" value="0.1"/><float name="alphaU" value="0.1"/>', "either 'alpha' or"),
+                      ('<float name="alphaU" value="0.1"/>', "both 'alphaU' and 'alphaV'")):
+        bad.write_text('<scene version="0.5.0"><shape type="cube"><bsdf type="roughconductor">'
+                       + body + '</bsdf></shape></scene>')
+        try:
+            mtsg.Scene(str(bad))
+        except RuntimeError as e:
+            assert msg in str(e), str(e)
+        else:
+            raise AssertionError("expected an error for " + body)
