@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MTSG_ABI_VERSION 3
+#define MTSG_ABI_VERSION 4
 
 /* ---- error codes (mtsg_last_error() gives the message) ------------------ */
 enum {
@@ -94,23 +94,33 @@ typedef struct mtsg_shape {
 enum {
     MTSG_BSDF_DIFFUSE        = 1,   /* src/bsdfs/diffuse.cpp        */
     MTSG_BSDF_ROUGHCONDUCTOR = 2,   /* src/bsdfs/roughconductor.cpp */
-    MTSG_BSDF_DIELECTRIC     = 3    /* src/bsdfs/dielectric.cpp     */
+    MTSG_BSDF_DIELECTRIC     = 3,   /* src/bsdfs/dielectric.cpp     */
+    MTSG_BSDF_CONDUCTOR      = 4,   /* src/bsdfs/conductor.cpp      */
+    MTSG_BSDF_PLASTIC        = 5    /* src/bsdfs/plastic.cpp        */
 };
 enum { MTSG_MF_BECKMANN = 0, MTSG_MF_GGX = 1, MTSG_MF_PHONG = 2 };   /* microfacet.h:49-57 */
 
+/* One BSDF record.  `twosided` (src/bsdfs/twosided.cpp) marks the record
+ * of a twosided wrapper's front material: when the incident direction is on
+ * the back (cosTheta(wi) <= 0 for eval/pdf, < 0 for sampling) the record
+ * bsdfs[back] is used with wi.z and wo.z negated. */
 typedef struct mtsg_bsdf {
     int32_t type;
     int32_t distribution;    /* MTSG_MF_*                                   */
     int32_t sample_visible;
     int32_t smooth;          /* BSDF::ESmooth set -> NEE (path.cpp:174)     */
     int32_t ref_n_zero;      /* ETransmission|EBackSide -> refN = 0 (records.inl:160-164) */
-    int32_t pad[3];
-    float reflectance[3];    /* diffuse                                     */
-    float eta[3], k[3];      /* roughconductor, already divided by extEta   */
-    float spec_refl[3];      /* roughconductor / dielectric                 */
+    int32_t twosided;        /* twosided wrapper front record (see above)   */
+    int32_t back;            /* twosided: index of the back-side record     */
+    int32_t nonlinear;       /* plastic 'nonlinear'                         */
+    float reflectance[3];    /* diffuse; plastic diffuseReflectance         */
+    float eta[3], k[3];      /* (rough)conductor, already divided by extEta */
+    float spec_refl[3];      /* (rough)conductor / dielectric / plastic     */
     float spec_trans[3];     /* dielectric                                  */
     float alpha_u, alpha_v;  /* already clamped to >= 1e-4                  */
-    float ior_eta, ior_inv_eta; /* dielectric intIOR/extIOR and inverse     */
+    float ior_eta, ior_inv_eta; /* dielectric / plastic intIOR/extIOR and inverse */
+    float fdr_int;           /* plastic: fresnelDiffuseReflectance(1 / eta) */
+    float spec_sampling_weight; /* plastic: sAvg / (dAvg + sAvg) luminances */
 } mtsg_bsdf;
 
 enum { MTSG_EMITTER_AREA = 1, MTSG_EMITTER_ENVMAP = 2 };

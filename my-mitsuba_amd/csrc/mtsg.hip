@@ -1098,8 +1098,29 @@ DEV float fresnel_dielectric(float cosThetaI_, float &cosThetaT_, float eta) {
     return 0.5f * (Rs * Rs + Rp * Rp);
 }
 
-// BSDF::eval * cos (ESolidAngle) and pdf for the smooth BSDFs
-DEV float3 bsdf_eval(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
+// fresnelDielectricExt without the transmitted cosine (util.cpp:651-681)
+DEV float fresnel_dielectric1(float cosThetaI, float eta) {
+    float cosThetaT;
+    return fresnel_dielectric(cosThetaI, cosThetaT, eta);
+}
+
+// plastic.cpp:216-222: the diffuse base renormalised for internal reflection
+DEV float3 plastic_diffuse(const mtsg_bsdf &b) {
+    float3 diff = ld3(b.reflectance);
+    if (b.nonlinear) diff = diff / (mk3(1.0f, 1.0f, 1.0f) - diff * b.fdr_int);
+    else diff = diff / (1 - b.fdr_int);
+    return diff;
+}
+DEV float plastic_prob_specular(const mtsg_bsdf &b, float Fi) {
+    return (Fi * b.spec_sampling_weight) / (Fi * b.spec_sampling_weight + (1 - Fi) * (1 - b.spec_sampling_weight));
+}
+
+// BSDF::eval * cos (ESolidAngle) and pdf for the smooth BSDFs.  EXT: the
+// scene has conductor / plastic / twosided records (the shade kernel is
+// instantiated without them otherwise: their code costs the common
+// diffuse + roughconductor + dielectric kernel its register budget)
+template <bool EXT>
+DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
     pdf = 0.0f;
     if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:107-126
         if (!b.smooth || wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
@@ -1119,10 +1140,18 @@ DEV float3 bsdf_eval(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
         float model = Dv * G / (4.0f * wi.z);
         return F * model;
     }
-    return mk3(0, 0, 0);   // dielectric: delta components only
+    if (EXT && b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:190-263, the diffuse (ESolidAngle) part
+        if (wo.z <= 0 || wi.z <= 0) return mk3(0, 0, 0);
+        const float Fi = fresnel_dielectric1(wi.z, b.ior_eta), Fo = fresnel_dielectric1(wo.z, b.ior_eta);
+        const float invEta2 = 1 / (b.ior_eta * b.ior_eta);
+        pdf = kInvPi * wo.z * (1 - plastic_prob_specular(b, Fi));
+        return plastic_diffuse(b) * (kInvPi * wo.z * invEta2 * (1 - Fi) * (1 - Fo));
+    }
+    return mk3(0, 0, 0);   // dielectric / conductor: delta components only
 }
 
-DEV bool bsdf_sample(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r) {
+template <bool EXT>
+DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r) {
     r.eta = 1.0f;
     r.delta = 0;
     if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
@@ -1166,7 +1195,55 @@ DEV bool bsdf_sample(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSamp
         }
         return !isZero(r.weight);
     }
+    if (EXT && b.type == MTSG_BSDF_CONDUCTOR) {   // conductor.cpp:220-236
+        if (wi.z <= 0) return false;
+        r.delta = 1;
+        r.wo = mk3(-wi.x, -wi.y, wi.z);
+        r.pdf = 1.0f;
+        r.weight = ld3(b.spec_refl) * fresnel_conductor(wi.z, ld3(b.eta), ld3(b.k));
+        return !isZero(r.weight);
+    }
+    if (EXT && b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:344-375 (both components)
+        if (wi.z <= 0) return false;
+        const float Fi = fresnel_dielectric1(wi.z, b.ior_eta);
+        const float probSpecular = plastic_prob_specular(b, Fi);
+        if (sx < probSpecular) {
+            r.delta = 1;
+            r.wo = mk3(-wi.x, -wi.y, wi.z);
+            r.pdf = probSpecular;
+            r.weight = ld3(b.spec_refl) * Fi / probSpecular;
+        } else {
+            r.wo = cosine_hemisphere((sx - probSpecular) / (1 - probSpecular), sy);
+            const float Fo = fresnel_dielectric1(r.wo.z, b.ior_eta);
+            const float invEta2 = 1 / (b.ior_eta * b.ior_eta);
+            r.pdf = (1 - probSpecular) * (kInvPi * r.wo.z);
+            r.weight = plastic_diffuse(b) * (invEta2 * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
+        }
+        return !isZero(r.weight);
+    }
     return false;
+}
+
+// twosided.cpp:103-170: a twosided front record hands back-side queries to
+// bsdfs[back] with the z components negated
+template <bool EXT>
+DEV float3 bsdf_eval(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
+    if (EXT && b.twosided && !(wi.z > 0)) {
+        wi.z = -wi.z;
+        wo.z = -wo.z;
+        return bsdf_eval1<EXT>(all[b.back], wi, wo, pdf);
+    }
+    return bsdf_eval1<EXT>(b, wi, wo, pdf);
+}
+template <bool EXT>
+DEV bool bsdf_sample(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r) {
+    if (EXT && b.twosided && wi.z < 0) {
+        wi.z = -wi.z;
+        if (!bsdf_sample1<EXT>(all[b.back], wi, sx, sy, r)) return false;
+        r.wo.z = -r.wo.z;
+        return true;
+    }
+    return bsdf_sample1<EXT>(b, wi, sx, sy, r);
 }
 
 DEV float mis(float pdfA, float pdfB) {   // path.cpp:296-300
@@ -1315,7 +1392,7 @@ struct ShadeStage {
 // ENV: the scene has an environment emitter (the variant without it keeps
 // the environment code, and its registers, out of the common case)
 // SMP: the render's sampler (MTSG_SAMPLER_*)
-template <bool ENV, int SMP>
+template <bool ENV, int SMP, bool EXT>
 __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int bounce, int qin,
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
@@ -1447,7 +1524,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                             value = value / emPdf;
                             const float3 wo = its.sh.toLocal(dd);
                             float bpdf;
-                            const float3 bval = bsdf_eval(bsdf, wi, wo, bpdf);
+                            const float3 bval = bsdf_eval<EXT>(S.bsdfs, bsdf, wi, wo, bpdf);
                             if (!isZero(bval) && (!I.strict_normals || dot(its.geoN, dd) * wo.z > 0)) {
                                 const float weight = mis(pdf, bpdf);
                                 const float3 c = T * value * bval * weight;
@@ -1464,7 +1541,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                     float sx, sy;
                     next2D<SMP>(I, smp, sx, sy);
                     BsdfSample bs;
-                    if (!bsdf_sample(bsdf, wi, sx, sy, bs)) {
+                    if (!bsdf_sample<EXT>(S.bsdfs, bsdf, wi, sx, sy, bs)) {
                         done = true;
                     } else {
                         flags |= F_SCATTERED;
@@ -1685,6 +1762,7 @@ struct mtsg_scene {
     std::vector<unsigned long long> stragglers;  // MTSG_FLAG_COUNT: slow-ray records
     unsigned long long *waveTimes = nullptr;     // MTSG_FLAG_WAVETIME: [launch][wave][WT_WORDS]
     uint32_t wtLaunches = 0;
+    bool extBsdfs = false;   // conductor / plastic / twosided records present (k_shade<..., true>)
 };
 
 namespace {
@@ -1778,26 +1856,31 @@ void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn
     else launch_trace_c<false>(s, P, cIn, sIn, n, st);
 }
 
-template <bool ENV>
+template <bool ENV, bool EXT>
 void launch_shade_env(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {
     dim3 g(s->shadeGrid), blk(SHADE_BLOCK);
     switch (I.smp.type) {
         case MTSG_SAMPLER_HALTON:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HALTON>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HALTON, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
             break;
         case MTSG_SAMPLER_HAMMERSLEY:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HAMMERSLEY>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HAMMERSLEY, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
             break;
         case MTSG_SAMPLER_LDSAMPLER:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_LDSAMPLER>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_LDSAMPLER, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
             break;
         default:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_INDEPENDENT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_INDEPENDENT, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
     }
 }
 void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {
-    if (s->ds.has_env) launch_shade_env<true>(s, I, B, P, b, qin, st);
-    else launch_shade_env<false>(s, I, B, P, b, qin, st);
+    if (s->extBsdfs) {
+        if (s->ds.has_env) launch_shade_env<true, true>(s, I, B, P, b, qin, st);
+        else launch_shade_env<false, true>(s, I, B, P, b, qin, st);
+    } else {
+        if (s->ds.has_env) launch_shade_env<true, false>(s, I, B, P, b, qin, st);
+        else launch_shade_env<false, false>(s, I, B, P, b, qin, st);
+    }
 }
 
 // Sampler constants of a render (setFilmResolution with blocked = true over
@@ -2261,6 +2344,14 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
     // environment emitter tables (envmap.h)
     ds.has_env = d->has_envmap ? 1 : 0;
+    for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
+        const mtsg_bsdf &b = d->bsdfs[i];
+        if (b.type == MTSG_BSDF_CONDUCTOR || b.type == MTSG_BSDF_PLASTIC || b.twosided) s->extBsdfs = true;
+        if (b.twosided && (b.back < 0 || (uint32_t)b.back >= d->n_bsdfs)) {
+            g_err = "bsdf " + std::to_string(i) + ": twosided back record out of range";
+            return fail(MTSG_ERR_INVALID);
+        }
+    }
     ds.env = DevEnv{nullptr, nullptr, nullptr, nullptr, nullptr};
     if (d->has_envmap) {
         const mtsg_envmap &E = d->envmap;

@@ -678,6 +678,51 @@ struct Loader {
         }
     }
 
+    // util.cpp:651-681 (double precision, for the quadrature below)
+    static double fresnelDielectricD(double cosThetaI, double eta) {
+        if (eta == 1) return 0.0;
+        double scale = cosThetaI > 0 ? 1 / eta : eta;
+        double cosThetaTSqr = 1 - (1 - cosThetaI * cosThetaI) * (scale * scale);
+        if (cosThetaTSqr <= 0.0) return 1.0;
+        double ci = std::abs(cosThetaI), ct = std::sqrt(cosThetaTSqr);
+        double Rs = (ci - eta * ct) / (ci + eta * ct), Rp = (eta * ci - ct) / (eta * ci + ct);
+        return 0.5 * (Rs * Rs + Rp * Rp);
+    }
+    // fresnelDiffuseReflectance(eta, fast = false) (util.cpp:814-860): the
+    // integral over xi in [0, 1] of F(sqrt(xi)); Mitsuba uses adaptive
+    // Gauss-Lobatto with relative error 1e-5, restated here as adaptive
+    // Simpson in double precision to 1e-10 (identical to float precision)
+    static double simpson(double eta, double a, double b, double fa, double fm, double fb, double whole, int depth) {
+        const double m = 0.5 * (a + b), lm = 0.5 * (a + m), rm = 0.5 * (m + b);
+        const double flm = fresnelDielectricD(std::sqrt(lm), eta), frm = fresnelDielectricD(std::sqrt(rm), eta);
+        const double left = (m - a) / 6 * (fa + 4 * flm + fm), right = (b - m) / 6 * (fm + 4 * frm + fb);
+        if (depth <= 0 || std::abs(left + right - whole) <= 1e-10) return left + right + (left + right - whole) / 15;
+        return simpson(eta, a, m, fa, flm, fm, left, depth - 1) + simpson(eta, m, b, fm, frm, fb, right, depth - 1);
+    }
+    static float fresnelDiffuseReflectance(float eta) {
+        const double fa = fresnelDielectricD(0.0, eta), fm = fresnelDielectricD(std::sqrt(0.5), eta), fb = fresnelDielectricD(1.0, eta);
+        return (float)simpson(eta, 0.0, 1.0, fa, fm, fb, (fa + 4 * fm + fb) / 6, 40);
+    }
+    // BSDF::ensureEnergyConservation(texture, name, 1) (bsdf.cpp:88-113): a
+    // constant whose largest component exceeds 1 is scaled by 0.99 / max
+    static V3 energyConserving(Properties &props, V3 v) {
+        if (!props.getBool("ensureEnergyConservation", true)) return v;
+        float mx = std::max(v.x, std::max(v.y, v.z));
+        return mx > 1.0f ? v * (0.99f * (1.0f / mx)) : v;
+    }
+    static float luminance(V3 v) { return v.x * 0.212671f + v.y * 0.715160f + v.z * 0.072169f; }   // spectrum.h:638-640
+    // conductor material: the data/ior/<name>.{eta,k}.spd lookup (RGB), eta/k overrides, / extEta
+    void conductorIOR(Properties &props, mtsg_bsdf &d, const char *who) {
+        std::string material = props.getString("material", "Cu");
+        V3 intEta, intK;
+        if (lower(material) == "none") { intEta = V3(0.0f); intK = V3(1.0f); }
+        else if (!lookupConductor(material, intEta, intK)) throw err(std::string(who) + ": unknown material \"" + material + "\"");
+        float extEta = lookupIORProp(props, "extEta", "air");
+        V3 eta = props.getSpectrum("eta", intEta) / extEta;
+        V3 k = props.getSpectrum("k", intK) / extEta;
+        for (int i = 0; i < 3; ++i) { d.eta[i] = eta[i]; d.k[i] = k[i]; }
+    }
+
     int parseBsdf(XNode &n) {
         substAll(n);
         Properties props;
@@ -690,22 +735,16 @@ struct Loader {
         if (type == "diffuse") {
             // diffuse.cpp:77-84, configure() keeps the component iff max > 0
             V3 r = props.getSpectrum(props.has("reflectance") ? "reflectance" : "diffuseReflectance", V3(0.5f));
+            r = energyConserving(props, r);
             float mx = std::max(r.x, std::max(r.y, r.z));
-            if (mx > 1.0f) r = r * (1.0f / mx);   // ensureEnergyConservation (bsdf.cpp)
             d.type = MTSG_BSDF_DIFFUSE;
             d.reflectance[0] = r.x; d.reflectance[1] = r.y; d.reflectance[2] = r.z;
             d.smooth = mx > 0;
             d.ref_n_zero = 0;
         } else if (type == "roughconductor") {
             // roughconductor.cpp:168-203
-            V3 spec = props.getSpectrum("specularReflectance", V3(1.0f));
-            std::string material = props.getString("material", "Cu");
-            V3 intEta, intK;
-            if (lower(material) == "none") { intEta = V3(0.0f); intK = V3(1.0f); }
-            else if (!lookupConductor(material, intEta, intK)) throw err("roughconductor: unknown material \"" + material + "\"");
-            float extEta = lookupIORProp(props, "extEta", "air");
-            V3 eta = props.getSpectrum("eta", intEta) / extEta;
-            V3 k = props.getSpectrum("k", intK) / extEta;
+            V3 spec = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
+            conductorIOR(props, d, "roughconductor");
             // MicrofacetDistribution(props) (microfacet.h:99-146)
             int distr = MTSG_MF_BECKMANN;
             if (props.strings.count("distribution")) {
@@ -729,7 +768,7 @@ struct Loader {
             // visible-normal sampling is not supported for Phong (microfacet.h:140-144)
             d.sample_visible = (props.getBool("sampleVisible", true) && distr != MTSG_MF_PHONG) ? 1 : 0;
             d.alpha_u = au; d.alpha_v = av;
-            for (int i = 0; i < 3; ++i) { d.eta[i] = eta[i]; d.k[i] = k[i]; d.spec_refl[i] = spec[i]; }
+            for (int i = 0; i < 3; ++i) d.spec_refl[i] = spec[i];
             d.smooth = 1;
             d.ref_n_zero = 0;
         } else if (type == "dielectric") {
@@ -737,14 +776,66 @@ struct Loader {
             float intIOR = lookupIORProp(props, "intIOR", "bk7");
             float extIOR = lookupIORProp(props, "extIOR", "air");
             if (intIOR < 0 || extIOR < 0) throw err("The interior and exterior indices of refraction must be positive!");
-            V3 sr = props.getSpectrum("specularReflectance", V3(1.0f));
-            V3 st = props.getSpectrum("specularTransmittance", V3(1.0f));
+            V3 sr = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
+            V3 st = energyConserving(props, props.getSpectrum("specularTransmittance", V3(1.0f)));
             d.type = MTSG_BSDF_DIELECTRIC;
             d.ior_eta = intIOR / extIOR;
             d.ior_inv_eta = 1 / d.ior_eta;
             for (int i = 0; i < 3; ++i) { d.spec_refl[i] = sr[i]; d.spec_trans[i] = st[i]; }
             d.smooth = 0;        // delta components only
             d.ref_n_zero = 1;    // ETransmission | EBackSide
+        } else if (type == "conductor") {
+            // conductor.cpp:98-130: ideal mirror with the exact conductor Fresnel term
+            V3 spec = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
+            conductorIOR(props, d, "conductor");
+            d.type = MTSG_BSDF_CONDUCTOR;
+            for (int i = 0; i < 3; ++i) d.spec_refl[i] = spec[i];
+            d.smooth = 0;        // delta reflection only: no direct sampling (path.cpp:174)
+            d.ref_n_zero = 0;
+        } else if (type == "plastic") {
+            // plastic.cpp:93-140: smooth dielectric coating over a diffuse base
+            float intIOR = lookupIORProp(props, "intIOR", "polypropylene");
+            float extIOR = lookupIORProp(props, "extIOR", "air");
+            if (intIOR < 0 || extIOR < 0) throw err("The interior and exterior indices of refraction must be positive!");
+            V3 sr = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
+            V3 dr = energyConserving(props, props.getSpectrum("diffuseReflectance", V3(0.5f)));
+            d.type = MTSG_BSDF_PLASTIC;
+            d.ior_eta = intIOR / extIOR;
+            d.ior_inv_eta = 1 / d.ior_eta;
+            d.nonlinear = props.getBool("nonlinear", false) ? 1 : 0;
+            d.fdr_int = fresnelDiffuseReflectance(1 / d.ior_eta);
+            const float dAvg = luminance(dr), sAvg = luminance(sr);
+            d.spec_sampling_weight = sAvg / (dAvg + sAvg);
+            for (int i = 0; i < 3; ++i) { d.spec_refl[i] = sr[i]; d.reflectance[i] = dr[i]; }
+            d.smooth = 1;        // diffuse component
+            d.ref_n_zero = 0;
+        } else if (type == "twosided") {
+            // twosided.cpp:52-80: one or two nested BRDFs, front and back
+            std::vector<int> kids;
+            for (XNode *c : nested) {
+                substAll(*c);
+                if (c->tag == "bsdf") kids.push_back(parseBsdf(*c));
+                else if (c->tag == "ref") {
+                    std::string id = c->attr("id");
+                    if (!bsdfIds.count(id)) throw err("Referenced object '" + id + "' not found!");
+                    kids.push_back(bsdfIds[id]);
+                } else {
+                    throw err("line " + std::to_string(c->line) + ": unsupported element <" + c->tag + "> inside twosided");
+                }
+            }
+            if (kids.empty()) throw err("A nested one-sided material is required!");
+            if (kids.size() > 2) throw err("No more than two nested BRDFs can be added!");
+            for (int k : kids) {
+                const mtsg_bsdf &kd = scene.bsdfs[k].d;
+                if (kd.type == MTSG_BSDF_DIELECTRIC) throw err("Only materials without a transmission component can be nested!");
+                if (kd.twosided) throw err("twosided: a nested twosided material is not supported by this build");
+            }
+            const int backIdx = kids.size() == 2 ? kids[1] : kids[0];
+            d = scene.bsdfs[kids[0]].d;
+            d.twosided = 1;
+            d.back = backIdx;
+            d.smooth = scene.bsdfs[kids[0]].d.smooth || scene.bsdfs[backIdx].d.smooth;
+            d.ref_n_zero = 1;    // EBackSide component (records.inl:160-164)
         } else {
             throw err("line " + std::to_string(n.line) + ": BSDF plugin \"" + type + "\" is outside this build's scope");
         }

@@ -1416,6 +1416,22 @@ Spec fresnelConductorExact(float cosThetaI, const Spec &eta, const Spec &k) {
 
 inline Vec reflectM(const Vec &wi, const Vec &m) { return m * (2 * dot(wi, m)) - wi; }
 
+float fresnelDielectricExt1(float cosThetaI, float eta) {
+    float cosThetaT;
+    return fresnelDielectricExt(cosThetaI, cosThetaT, eta);
+}
+// SmoothPlastic (plastic.cpp:93-140): m_invEta2, the internal-reflection
+// renormalised diffuse base and the Fresnel-steered specular probability
+inline float plasticInvEta2(const mtsg_bsdf &b) { return 1 / (b.ior_eta * b.ior_eta); }
+Spec plasticDiffuse(const mtsg_bsdf &b) {
+    Spec diff = Spec::of(b.reflectance);
+    if (b.nonlinear) return diff / (Spec(1.0f) - diff * b.fdr_int);
+    return diff / (1 - b.fdr_int);
+}
+float plasticProbSpecular(const mtsg_bsdf &b, float Fi) {
+    return (Fi * b.spec_sampling_weight) / (Fi * b.spec_sampling_weight + (1 - Fi) * (1 - b.spec_sampling_weight));
+}
+
 // BSDF::eval (measure = ESolidAngle for smooth BSDFs; dielectric only
 // evaluates EDiscrete, so it returns 0 here: dielectric.cpp:228-250)
 Spec bsdfEval(const mtsg_bsdf &b, const BRec &r) {
@@ -1434,7 +1450,13 @@ Spec bsdfEval(const mtsg_bsdf &b, const BRec &r) {
         float model = D * G / (4.0f * cosTheta(r.wi));
         return F * model;
     }
-    return Spec(0.0f);
+    if (b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:190-233 (ESolidAngle: the diffuse part)
+        if (cosTheta(r.wo) <= 0 || cosTheta(r.wi) <= 0) return Spec(0.0f);
+        float Fi = fresnelDielectricExt1(cosTheta(r.wi), b.ior_eta);
+        float Fo = fresnelDielectricExt1(cosTheta(r.wo), b.ior_eta);
+        return plasticDiffuse(b) * (kInvPi * cosTheta(r.wo) * plasticInvEta2(b) * (1 - Fi) * (1 - Fo));
+    }
+    return Spec(0.0f);   // dielectric / conductor: delta components only (EDiscrete)
 }
 
 float bsdfPdf(const mtsg_bsdf &b, const BRec &r) {
@@ -1448,6 +1470,11 @@ float bsdfPdf(const mtsg_bsdf &b, const BRec &r) {
         Microfacet distr = mfOf(b);
         if (distr.sampleVisible) return distr.eval(H) * distr.smithG1(r.wi, H) / (4.0f * cosTheta(r.wi));
         return distr.pdf(r.wi, H) / (4 * absDot(r.wo, H));
+    }
+    if (b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:235-263
+        if (cosTheta(r.wo) <= 0 || cosTheta(r.wi) <= 0) return 0.0f;
+        float Fi = fresnelDielectricExt1(cosTheta(r.wi), b.ior_eta);
+        return kInvPi * cosTheta(r.wo) * (1 - plasticProbSpecular(b, Fi));
     }
     return 0.0f;
 }
@@ -1496,7 +1523,60 @@ Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy) {
         float factor = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;   // ERadiance
         return Spec::of(b.spec_trans) * (factor * factor);
     }
+    if (b.type == MTSG_BSDF_CONDUCTOR) {   // conductor.cpp:220-236
+        if (cosTheta(r.wi) <= 0) return Spec(0.0f);
+        r.sampledType = EDeltaReflection;
+        r.wo = Vec(-r.wi.x, -r.wi.y, r.wi.z);
+        r.eta = 1.0f;
+        pdf = 1;
+        return Spec::of(b.spec_refl) * fresnelConductorExact(cosTheta(r.wi), Spec::of(b.eta), Spec::of(b.k));
+    }
+    if (b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:344-390 (both components)
+        if (cosTheta(r.wi) <= 0) return Spec(0.0f);
+        float Fi = fresnelDielectricExt1(cosTheta(r.wi), b.ior_eta);
+        r.eta = 1.0f;
+        float probSpecular = plasticProbSpecular(b, Fi);
+        if (sx < probSpecular) {
+            r.sampledType = EDeltaReflection;
+            r.wo = Vec(-r.wi.x, -r.wi.y, r.wi.z);
+            pdf = probSpecular;
+            return Spec::of(b.spec_refl) * Fi / probSpecular;
+        }
+        r.sampledType = EDiffuseReflection;
+        r.wo = squareToCosineHemisphere((sx - probSpecular) / (1 - probSpecular), sy);
+        float Fo = fresnelDielectricExt1(cosTheta(r.wo), b.ior_eta);
+        pdf = (1 - probSpecular) * (kInvPi * cosTheta(r.wo));
+        return plasticDiffuse(b) * (plasticInvEta2(b) * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
+    }
     return Spec(0.0f);
+}
+
+// TwoSidedBRDF (twosided.cpp:103-170): a twosided front record hands
+// back-side queries to bsdfs[back] with the z components negated
+const mtsg_bsdf &bsdfSide(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec &r, bool sampling, bool &flipped) {
+    flipped = b.twosided && (sampling ? cosTheta(r.wi) < 0 : !(cosTheta(r.wi) > 0));
+    if (!flipped) return b;
+    r.wi.z *= -1;
+    if (!sampling) r.wo.z *= -1;
+    return all[b.back];
+}
+Spec bsdfEvalTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec r) {
+    bool f;
+    return bsdfEval(bsdfSide(all, b, r, false, f), r);
+}
+float bsdfPdfTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec r) {
+    bool f;
+    return bsdfPdf(bsdfSide(all, b, r, false, f), r);
+}
+Spec bsdfSampleTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy) {
+    bool flipped;
+    const mtsg_bsdf &nb = bsdfSide(all, b, r, true, flipped);
+    Spec result = bsdfSample(nb, r, pdf, sx, sy);
+    if (flipped) {
+        r.wi.z *= -1;
+        if (!result.isZero() && pdf != 0) r.wo.z *= -1;
+    }
+    return result;
 }
 
 inline float miWeight(float pdfA, float pdfB) {   // path.cpp:296-300
@@ -1572,9 +1652,9 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
                 BRec bRec;
                 bRec.wi = its.wi;
                 bRec.wo = its.toLocal(dRec.d);
-                const Spec bsdfVal = bsdfEval(bsdf, bRec);
+                const Spec bsdfVal = bsdfEvalTS(scene.d.bsdfs, bsdf, bRec);
                 if (!bsdfVal.isZero() && (!I.strictNormals || dot(its.geoFrame.n, dRec.d) * cosTheta(bRec.wo) > 0)) {
-                    float bsdfPdfV = bsdfPdf(bsdf, bRec);   // area emitter: on surface, solid angle
+                    float bsdfPdfV = bsdfPdfTS(scene.d.bsdfs, bsdf, bRec);   // area emitter: on surface, solid angle
                     float weight = miWeight(dRec.pdf, bsdfPdfV);
                     Li += throughput * value * bsdfVal * weight;
                 }
@@ -1586,7 +1666,7 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
         bRec.wi = its.wi;
         float s0, s1;
         sampler.next2D(s0, s1);
-        Spec bsdfWeight = bsdfSample(bsdf, bRec, bsdfPdfS, s0, s1);
+        Spec bsdfWeight = bsdfSampleTS(scene.d.bsdfs, bsdf, bRec, bsdfPdfS, s0, s1);
         DBG("  depth %d bsdf type=%d s=(%g %g) wi=(%g %g %g) wo=(%g %g %g) w=(%g %g %g) pdf=%g sampled=%d\n", depth, bsdf.type, s0, s1, bRec.wi.x, bRec.wi.y, bRec.wi.z, bRec.wo.x, bRec.wo.y, bRec.wo.z, bsdfWeight.s[0], bsdfWeight.s[1], bsdfWeight.s[2], bsdfPdfS, bRec.sampledType);
         if (bsdfWeight.isZero()) break;
         scattered |= bRec.sampledType != 0;

@@ -28,26 +28,32 @@ THETA_BINS, PHI_BINS = 10, 20
 N_SAMPLES = THETA_BINS * PHI_BINS * 1000
 WI_PER_BSDF = 5
 
-DIFFUSE, ROUGHCONDUCTOR, DIELECTRIC = 1, 2, 3
+DIFFUSE, ROUGHCONDUCTOR, DIELECTRIC, CONDUCTOR, PLASTIC = 1, 2, 3, 4, 5
+DELTA = 4 | 16   # EDeltaReflection | EDeltaTransmission
 BECKMANN, GGX, PHONG = 0, 1, 2
 
 
 class Bsdf(C.Structure):
     """mtsg_bsdf (include/mtsg.h)."""
     _fields_ = [("type", C.c_int32), ("distribution", C.c_int32), ("sample_visible", C.c_int32),
-                ("smooth", C.c_int32), ("ref_n_zero", C.c_int32), ("pad", C.c_int32 * 3),
+                ("smooth", C.c_int32), ("ref_n_zero", C.c_int32), ("twosided", C.c_int32),
+                ("back", C.c_int32), ("nonlinear", C.c_int32),
                 ("reflectance", C.c_float * 3), ("eta", C.c_float * 3), ("k", C.c_float * 3),
                 ("spec_refl", C.c_float * 3), ("spec_trans", C.c_float * 3),
                 ("alpha_u", C.c_float), ("alpha_v", C.c_float),
-                ("ior_eta", C.c_float), ("ior_inv_eta", C.c_float)]
+                ("ior_eta", C.c_float), ("ior_inv_eta", C.c_float),
+                ("fdr_int", C.c_float), ("spec_sampling_weight", C.c_float)]
 
 
-def make_bsdf(kind, dist=GGX, alpha=0.2, visible=1, eta=1.5046, alpha_v=None):
+def make_bsdf(kind, dist=GGX, alpha=0.2, visible=1, eta=1.5046, alpha_v=None, nonlinear=0, fdr_int=0.6, spec_weight=0.6):
     b = Bsdf()
     b.type = kind
     b.distribution = dist
     b.sample_visible = visible
-    b.smooth = 1 if kind != DIELECTRIC else 0
+    b.smooth = 1 if kind not in (DIELECTRIC, CONDUCTOR) else 0
+    b.nonlinear = nonlinear
+    b.fdr_int = fdr_int
+    b.spec_sampling_weight = spec_weight
     b.reflectance[:] = (0.5, 0.3, 0.8)
     b.eta[:] = (0.200438, 0.924033, 1.10221)      # Cu (ior.h lookup), RGB
     b.k[:] = (3.91295, 2.45285, 2.14219)
@@ -166,6 +172,10 @@ CASES = [
     ("beckmann_aniso_classic", dict(kind=ROUGHCONDUCTOR, dist=BECKMANN, alpha=0.15, alpha_v=0.4, visible=0)),
     ("phong_0.3", dict(kind=ROUGHCONDUCTOR, dist=PHONG, alpha=0.3, visible=0)),
     ("phong_aniso", dict(kind=ROUGHCONDUCTOR, dist=PHONG, alpha=0.2, alpha_v=0.5, visible=0)),
+    # smooth plastic: only its diffuse lobe has a density (the specular
+    # samples are delta and excluded, as chisquare.cpp does for discrete ones)
+    ("plastic", dict(kind=PLASTIC, eta=1.49, fdr_int=0.595, spec_weight=0.6)),
+    ("plastic_nonlinear", dict(kind=PLASTIC, eta=1.8, nonlinear=1, fdr_int=0.7, spec_weight=0.3)),
 ]
 
 
@@ -176,8 +186,8 @@ def test_bsdf_sampling_matches_pdf(name, kw):
     alpha = 1 - (1 - SIGNIFICANCE) ** (1.0 / WI_PER_BSDF)   # Sidak (chisquare.cpp:255)
     for wi in random_wi(rng, WI_PER_BSDF):
         u2 = rng.random((N_SAMPLES, 2), dtype=np.float32)
-        wo, pdf, w, _ = sample(b, wi, u2)
-        ok = (pdf > 0) & (w.max(1) > 0)
+        wo, pdf, w, t = sample(b, wi, u2)
+        ok = (pdf > 0) & (w.max(1) > 0) & ((t & DELTA) == 0)
         p = chi2_pvalue(observed_counts(wo[ok]), expected_counts(b, wi, N_SAMPLES))
         assert p >= alpha, f"{name} wi={wi}: chi-square p-value {p:.3e} < {alpha:.3e}"
         # weight == f / pdf for the sampled directions (non-delta lobes)
@@ -224,3 +234,49 @@ def test_dielectric_split_follows_fresnel(cos_i):
         np.testing.assert_allclose(np.abs(wo[tr, 2]), cos_t, rtol=1e-4)
         np.testing.assert_allclose(w[tr], 1.0 / eta_rel ** 2, rtol=1e-4)
     np.testing.assert_allclose(w[refl], 1.0, rtol=1e-6)
+
+
+def fresnel_conductor(cos_i, eta, k):
+    """Exact unpolarised conductor Fresnel reflectance (independent complex
+    closed form)."""
+    n = eta + 1j * k
+    sin2 = 1 - cos_i ** 2
+    cos_t = np.sqrt(1 - sin2 / n ** 2)
+    rs = (cos_i - n * cos_t) / (cos_i + n * cos_t)
+    rp = (n * cos_i - cos_t) / (n * cos_i + cos_t)
+    return 0.5 * (np.abs(rs) ** 2 + np.abs(rp) ** 2)
+
+
+def test_smooth_conductor_is_a_fresnel_mirror():
+    # conductor.cpp:220-236: delta reflection, pdf 1, weight = specularReflectance * F
+    b = make_bsdf(CONDUCTOR)
+    for cos_i in (0.99, 0.7, 0.3, 0.05):
+        s = math.sqrt(1 - cos_i ** 2)
+        wi = np.array([s * 0.6, s * 0.8, cos_i], np.float32)
+        wo, pdf, w, t = sample(b, wi, np.full((4, 2), 0.37, np.float32))
+        assert np.all(t == 4) and np.all(pdf == 1)
+        np.testing.assert_allclose(wo, np.tile([-wi[0], -wi[1], wi[2]], (4, 1)), atol=1e-7)
+        F = [fresnel_conductor(cos_i, e, k) for e, k in zip(b.eta, b.k)]
+        np.testing.assert_allclose(w[0], F, rtol=2e-4)
+    # from below: no scattering
+    _, _, w, _ = sample(b, np.array([0.0, 0.6, -0.8], np.float32), np.full((1, 2), 0.5, np.float32))
+    assert np.all(w == 0)
+
+
+def test_plastic_specular_split_follows_fresnel():
+    # plastic.cpp:344-375: specular chosen with probability
+    # F w_s / (F w_s + (1 - F)(1 - w_s)), weight spec * F / p
+    eta, ws = 1.49, 0.6
+    b = make_bsdf(PLASTIC, eta=eta, spec_weight=ws)
+    for cos_i in (0.9, 0.4, 0.1):
+        s = math.sqrt(1 - cos_i ** 2)
+        wi = np.array([s, 0.0, cos_i], np.float32)
+        n = 100000
+        u2 = np.random.default_rng(3).random((n, 2), dtype=np.float32)
+        wo, pdf, w, t = sample(b, wi, u2)
+        F, _ = fresnel_dielectric(cos_i, eta)
+        p = F * ws / (F * ws + (1 - F) * (1 - ws))
+        spec = (t & 4) != 0
+        assert abs(spec.mean() - p) < 5 * math.sqrt(p * (1 - p) / n) + 1e-6
+        np.testing.assert_allclose(pdf[spec], p, rtol=1e-5)
+        np.testing.assert_allclose(w[spec], F / p, rtol=1e-4)

@@ -230,3 +230,15 @@ def test_rough_conductor_variants_parity(defs):
     _, c, gi = render_pair(scene, g)
     check_render(c, gi)
     g.close()
+
+
+def test_smooth_materials_scene_parity():
+    # plastic (linear and nonlinear), smooth conductor, twosided with one and
+    # with two nested BRDFs (back side seen by the camera)
+    scene = mtsg.Scene(os.path.join(SCENES, "cbox_materials.xml"), {"width": 48, "height": 48, "spp": 8})
+    g = mtsg.GPUScene(scene, 0)
+    _, c, gi = render_pair(scene, g)
+    check_render(c, gi)
+    _, c, gi = render_pair(scene, g, max_depth=3, strict_normals=1)
+    check_render(c, gi)
+    g.close()

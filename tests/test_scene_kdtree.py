@@ -122,3 +122,52 @@ def test_microfacet_distribution_parsing(tmp_path):
             assert msg in str(e), str(e)
         else:
             raise AssertionError("expected an error for " + body)
+
+
+def _bsdfs(scene):
+    """The scene descriptor's BSDF records (include/mtsg.h mtsg_bsdf)."""
+    import ctypes as C
+    from test_bsdf_chisquare import Bsdf
+    P, U = C.c_void_p, C.c_uint32
+
+    class Head(C.Structure):
+        _fields_ = [("abi", U), ("nv", U), ("pos", P), ("nrm", P), ("ntri", U), ("tri_idx", P), ("dpdu", P),
+                    ("nrects", U), ("rects", P), ("nshapes", U), ("shapes", P), ("nbsdfs", U), ("bsdfs", P)]
+    h = C.cast(scene.desc, C.POINTER(Head)).contents
+    return list(C.cast(h.bsdfs, C.POINTER(Bsdf))[:h.nbsdfs])
+
+
+def test_smooth_material_records():
+    s = mtsg.Scene(os.path.join(SCENES, "cbox_materials.xml"), {"width": 16, "height": 16, "spp": 1})
+    b = _bsdfs(s)
+    plastic = [x for x in b if x.type == 5]
+    assert len(plastic) == 2
+    for p in plastic:
+        eta = p.ior_eta
+        # fresnelDiffuseReflectance(1 / eta): the reference's own fit for
+        # eta < 1 (Egan & Hilgeman, util.cpp:822-833) to its stated accuracy
+        e = 1 / eta
+        fit = -1.4399 * e * e + 0.7099 * e + 0.6681 + 0.0636 / e
+        assert abs(p.fdr_int - fit) < 6e-3 * fit, (p.fdr_int, fit)
+        lum = lambda v: v[0] * 0.212671 + v[1] * 0.715160 + v[2] * 0.072169
+        assert abs(p.spec_sampling_weight - lum(p.spec_refl) / (lum(p.reflectance) + lum(p.spec_refl))) < 1e-6
+    assert plastic[0].ior_eta == np.float32(1.49) / np.float32(1.000277) and plastic[1].nonlinear == 1
+    cond = [x for x in b if x.type == 4]
+    assert len(cond) == 1 and cond[0].smooth == 0
+    two = [x for x in b if x.twosided]
+    assert len(two) == 2 and all(t.ref_n_zero == 1 and t.smooth == 1 for t in two)
+    # the two-BRDF panel: front red, back green
+    panel = [t for t in two if b[t.back].reflectance[1] > 0.4][0]
+    assert panel.reflectance[0] > 0.6
+
+
+def test_energy_conservation_scaling(tmp_path):
+    # BSDF::ensureEnergyConservation (bsdf.cpp:88-113): scale by 0.99 / max
+    p = tmp_path / "e.xml"
+    p.write_text('<scene version="0.5.0"><sensor type="perspective"><film type="hdrfilm">'
+                 '<integer name="width" value="8"/><integer name="height" value="8"/></film></sensor>'
+                 '<shape type="cube"><bsdf type="diffuse">'
+                 '<rgb name="reflectance" value="2, 1, 0.5"/></bsdf></shape>'
+                 '<shape type="rectangle"><emitter type="area"/></shape></scene>')
+    r = list(_bsdfs(mtsg.Scene(str(p)))[0].reflectance)
+    np.testing.assert_allclose(r, [0.99, 0.495, 0.2475], rtol=1e-6)

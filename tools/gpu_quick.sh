@@ -1,9 +1,6 @@
 #!/bin/bash
-# GPU parity tests + default benches (no CPU leg)
-mkdir -p gpurun_out/quick
-timeout -k 10 400 python -m pytest tests -q -m gpu -x > gpurun_out/quick/pytest_gpu.log 2>&1; rc=$?; tail -n 2 gpurun_out/quick/pytest_gpu.log
-if [ $rc -ne 0 ]; then exit $rc; fi
-for w in bunny15 cbox; do
-  timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu --workload $w > gpurun_out/quick/bench_$w.log 2>&1 || exit $?
-  echo "$w $(python tools/summarize_bench.py gpurun_out/quick/bench_$w.log)"
-done
+# GPU parity tests, then the C3 bench (whole frame and the emulated 8-rank share)
+O=gpurun_out/quick; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -q -m gpu -x --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }; tail -3 $O/pytest.log
+timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu > $O/e1.log 2>&1 || { tail $O/e1.log; exit 1; }; python tools/summarize_bench.py $O/e1.log
+timeout -k 10 200 python bench.py --steps 6 --warmup 1 --no-cpu --emulate-ranks 8 > $O/e8.log 2>&1 || { tail $O/e8.log; exit 1; }; python tools/summarize_bench.py $O/e8.log
