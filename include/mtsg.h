@@ -96,7 +96,8 @@ enum {
     MTSG_BSDF_ROUGHCONDUCTOR = 2,   /* src/bsdfs/roughconductor.cpp */
     MTSG_BSDF_DIELECTRIC     = 3,   /* src/bsdfs/dielectric.cpp     */
     MTSG_BSDF_CONDUCTOR      = 4,   /* src/bsdfs/conductor.cpp      */
-    MTSG_BSDF_PLASTIC        = 5    /* src/bsdfs/plastic.cpp        */
+    MTSG_BSDF_PLASTIC        = 5,   /* src/bsdfs/plastic.cpp        */
+    MTSG_BSDF_ROUGHDIELECTRIC = 6   /* src/bsdfs/roughdielectric.cpp */
 };
 enum { MTSG_MF_BECKMANN = 0, MTSG_MF_GGX = 1, MTSG_MF_PHONG = 2 };   /* microfacet.h:49-57 */
 
@@ -116,9 +117,9 @@ typedef struct mtsg_bsdf {
     float reflectance[3];    /* diffuse; plastic diffuseReflectance         */
     float eta[3], k[3];      /* (rough)conductor, already divided by extEta */
     float spec_refl[3];      /* (rough)conductor / dielectric / plastic     */
-    float spec_trans[3];     /* dielectric                                  */
+    float spec_trans[3];     /* (rough)dielectric                           */
     float alpha_u, alpha_v;  /* already clamped to >= 1e-4                  */
-    float ior_eta, ior_inv_eta; /* dielectric / plastic intIOR/extIOR and inverse */
+    float ior_eta, ior_inv_eta; /* (rough)dielectric / plastic intIOR/extIOR and inverse */
     float fdr_int;           /* plastic: fresnelDiffuseReflectance(1 / eta) */
     float spec_sampling_weight; /* plastic: sAvg / (dAvg + sAvg) luminances */
 } mtsg_bsdf;

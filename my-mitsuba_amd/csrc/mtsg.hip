@@ -1051,6 +1051,20 @@ struct MF {
         float sinThetaM = sqrtf(fmaxf(0.0f, 1 - cosThetaM * cosThetaM));
         return mk3(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
     }
+    // scaleAlpha (microfacet.h:178-183)
+    DEV void scale_alpha(float v) {
+        au *= v;
+        av *= v;
+        if (type == MTSG_MF_PHONG) {
+            eu = fmaxf(2.0f / (au * au) - 2.0f, 0.0f);
+            ev = fmaxf(2.0f / (av * av) - 2.0f, 0.0f);
+        }
+    }
+    // pdf (microfacet.h:253-262): pdfVisible (:462-466) or pdfAll = D cos
+    DEV float pdf(float3 wi, float3 m) const {
+        if (visible) return wi.z == 0 ? 0.0f : G1(wi, m) * fabsf(dot(wi, m)) * D(m) / fabsf(wi.z);
+        return D(m) * m.z;
+    }
     // sampleFirstQuadrant (microfacet.h:707-715)
     DEV void phong_quadrant(float u1, float &phi, float &exponent) const {
         phi = atanf(sqrtf((eu + 2.0f) / (ev + 2.0f)) * tanf(kPi * u1 * 0.5f));
@@ -1140,6 +1154,38 @@ DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
         float model = Dv * G / (4.0f * wi.z);
         return F * model;
     }
+    if (EXT && b.type == MTSG_BSDF_ROUGHDIELECTRIC) {   // roughdielectric.cpp:265-400
+        if (wi.z == 0) return mk3(0, 0, 0);
+        const bool reflect = wi.z * wo.z > 0;
+        const float eta = wi.z > 0 ? b.ior_eta : b.ior_inv_eta;
+        float3 H = reflect ? normalize(wo + wi) : normalize(wi + wo * eta);
+        H = H * copysignf(1.0f, H.z);
+        float dwh_dwo;
+        if (reflect) {
+            dwh_dwo = 1.0f / (4.0f * dot(wo, H));
+        } else {
+            const float sqrtDenom = dot(wi, H) + eta * dot(wo, H);
+            dwh_dwo = (eta * eta * dot(wo, H)) / (sqrtDenom * sqrtDenom);
+        }
+        const MF distr = make_mf(b);
+        MF sampleDistr = distr;
+        if (!distr.visible) sampleDistr.scale_alpha(1.2f - 0.2f * sqrtf(fabsf(wi.z)));
+        float prob = sampleDistr.pdf(wi * copysignf(1.0f, wi.z), H);
+        const float F = fresnel_dielectric1(dot(wi, H), b.ior_eta);
+        prob *= reflect ? F : (1 - F);
+        pdf = fabsf(prob * dwh_dwo);
+        const float D = distr.D(H);
+        if (D == 0) return mk3(0, 0, 0);
+        const float G = distr.G1(wi, H) * distr.G1(wo, H);
+        if (reflect) {
+            const float value = F * D * G / (4.0f * fabsf(wi.z));
+            return ld3(b.spec_refl) * value;
+        }
+        const float sqrtDenom = dot(wi, H) + eta * dot(wo, H);
+        const float value = ((1 - F) * D * G * eta * eta * dot(wi, H) * dot(wo, H)) / (wi.z * sqrtDenom * sqrtDenom);
+        const float factor = wi.z > 0 ? b.ior_inv_eta : b.ior_eta;   // ERadiance
+        return ld3(b.spec_trans) * fabsf(value * factor * factor);
+    }
     if (EXT && b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:190-263, the diffuse (ESolidAngle) part
         if (wo.z <= 0 || wi.z <= 0) return mk3(0, 0, 0);
         const float Fi = fresnel_dielectric1(wi.z, b.ior_eta), Fo = fresnel_dielectric1(wo.z, b.ior_eta);
@@ -1150,8 +1196,10 @@ DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
     return mk3(0, 0, 0);   // dielectric / conductor: delta components only
 }
 
-template <bool EXT>
-DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r) {
+// next1d: the sampler's next1D, drawn only where Mitsuba draws it
+// (roughdielectric's reflect/refract choice: roughdielectric.cpp:531-539)
+template <bool EXT, class Next1D>
+DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r, Next1D &&next1d) {
     r.eta = 1.0f;
     r.delta = 0;
     if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
@@ -1203,6 +1251,48 @@ DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSam
         r.weight = ld3(b.spec_refl) * fresnel_conductor(wi.z, ld3(b.eta), ld3(b.k));
         return !isZero(r.weight);
     }
+    if (EXT && b.type == MTSG_BSDF_ROUGHDIELECTRIC) {   // roughdielectric.cpp:508-590
+        const MF distr = make_mf(b);
+        MF sampleDistr = distr;
+        if (!distr.visible) sampleDistr.scale_alpha(1.2f - 0.2f * sqrtf(fabsf(wi.z)));
+        float microfacetPDF;
+        const float3 m = sampleDistr.sample(wi * copysignf(1.0f, wi.z), sx, sy, microfacetPDF);
+        if (microfacetPDF == 0) return false;
+        r.pdf = microfacetPDF;
+        float cosThetaT;
+        const float F = fresnel_dielectric(dot(wi, m), cosThetaT, b.ior_eta);
+        bool sampleReflection = true;
+        if (next1d() > F) {
+            sampleReflection = false;
+            r.pdf *= 1 - F;
+        } else {
+            r.pdf *= F;
+        }
+        float3 weight;
+        float dwh_dwo;
+        if (sampleReflection) {
+            r.wo = m * (2 * dot(wi, m)) - wi;
+            r.eta = 1.0f;
+            if (wi.z * r.wo.z <= 0) return false;
+            weight = ld3(b.spec_refl);
+            dwh_dwo = 1.0f / (4.0f * dot(r.wo, m));
+        } else {
+            if (cosThetaT == 0) return false;
+            const float e = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;   // refract (util.cpp:767-772)
+            r.wo = m * (dot(wi, m) * e + cosThetaT) - wi * e;
+            r.eta = cosThetaT < 0 ? b.ior_eta : b.ior_inv_eta;
+            if (wi.z * r.wo.z >= 0) return false;
+            const float factor = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;
+            weight = ld3(b.spec_trans) * (factor * factor);
+            const float sqrtDenom = dot(wi, m) + r.eta * dot(r.wo, m);
+            dwh_dwo = (r.eta * r.eta * dot(r.wo, m)) / (sqrtDenom * sqrtDenom);
+        }
+        if (distr.visible) weight = weight * distr.G1(r.wo, m);
+        else weight = weight * fabsf(distr.D(m) * (distr.G1(wi, m) * distr.G1(r.wo, m)) * dot(wi, m) / (microfacetPDF * wi.z));
+        r.pdf *= fabsf(dwh_dwo);
+        r.weight = weight;
+        return !isZero(r.weight);
+    }
     if (EXT && b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:344-375 (both components)
         if (wi.z <= 0) return false;
         const float Fi = fresnel_dielectric1(wi.z, b.ior_eta);
@@ -1235,15 +1325,15 @@ DEV float3 bsdf_eval(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float3
     }
     return bsdf_eval1<EXT>(b, wi, wo, pdf);
 }
-template <bool EXT>
-DEV bool bsdf_sample(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r) {
+template <bool EXT, class Next1D>
+DEV bool bsdf_sample(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r, Next1D &&next1d) {
     if (EXT && b.twosided && wi.z < 0) {
         wi.z = -wi.z;
-        if (!bsdf_sample1<EXT>(all[b.back], wi, sx, sy, r)) return false;
+        if (!bsdf_sample1<EXT>(all[b.back], wi, sx, sy, r, next1d)) return false;
         r.wo.z = -r.wo.z;
         return true;
     }
-    return bsdf_sample1<EXT>(b, wi, sx, sy, r);
+    return bsdf_sample1<EXT>(b, wi, sx, sy, r, next1d);
 }
 
 DEV float mis(float pdfA, float pdfB) {   // path.cpp:296-300
@@ -1541,7 +1631,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                     float sx, sy;
                     next2D<SMP>(I, smp, sx, sy);
                     BsdfSample bs;
-                    if (!bsdf_sample<EXT>(S.bsdfs, bsdf, wi, sx, sy, bs)) {
+                    if (!bsdf_sample<EXT>(S.bsdfs, bsdf, wi, sx, sy, bs, [&]() { return next1D<SMP>(I, smp); })) {
                         done = true;
                     } else {
                         flags |= F_SCATTERED;
@@ -2346,7 +2436,8 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     ds.has_env = d->has_envmap ? 1 : 0;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
         const mtsg_bsdf &b = d->bsdfs[i];
-        if (b.type == MTSG_BSDF_CONDUCTOR || b.type == MTSG_BSDF_PLASTIC || b.twosided) s->extBsdfs = true;
+        if (b.type == MTSG_BSDF_CONDUCTOR || b.type == MTSG_BSDF_PLASTIC || b.type == MTSG_BSDF_ROUGHDIELECTRIC || b.twosided)
+            s->extBsdfs = true;
         if (b.twosided && (b.back < 0 || (uint32_t)b.back >= d->n_bsdfs)) {
             g_err = "bsdf " + std::to_string(i) + ": twosided back record out of range";
             return fail(MTSG_ERR_INVALID);

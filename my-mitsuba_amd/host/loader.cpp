@@ -723,6 +723,31 @@ struct Loader {
         for (int i = 0; i < 3; ++i) { d.eta[i] = eta[i]; d.k[i] = k[i]; }
     }
 
+    // MicrofacetDistribution(props) (microfacet.h:99-146)
+    void microfacetProps(Properties &props, mtsg_bsdf &d) {
+        int distr = MTSG_MF_BECKMANN;
+        if (props.strings.count("distribution")) {
+            std::string dn = lower(props.strings["distribution"]);
+            if (dn == "beckmann") distr = MTSG_MF_BECKMANN;
+            else if (dn == "ggx") distr = MTSG_MF_GGX;
+            else if (dn == "phong" || dn == "as") distr = MTSG_MF_PHONG;
+            else throw err("Specified an invalid microfacet distribution \"" + dn + "\", must be \"beckmann\", \"ggx\", or \"phong\"/\"as\"!");
+        }
+        float au = 0.1f, av = 0.1f;
+        if (props.has("alpha")) {
+            if (props.has("alphaU") || props.has("alphaV")) throw err("Microfacet model: please specify either 'alpha' or 'alphaU'/'alphaV'.");
+            au = av = props.getFloat("alpha");
+        } else if (props.has("alphaU") || props.has("alphaV")) {
+            if (!props.has("alphaU") || !props.has("alphaV")) throw err("Microfacet model: both 'alphaU' and 'alphaV' must be specified.");
+            au = props.getFloat("alphaU"); av = props.getFloat("alphaV");
+        }
+        au = std::max(au, 1e-4f); av = std::max(av, 1e-4f);
+        d.distribution = distr;
+        // visible-normal sampling is not supported for Phong (microfacet.h:140-144)
+        d.sample_visible = (props.getBool("sampleVisible", true) && distr != MTSG_MF_PHONG) ? 1 : 0;
+        d.alpha_u = au; d.alpha_v = av;
+    }
+
     int parseBsdf(XNode &n) {
         substAll(n);
         Properties props;
@@ -745,29 +770,8 @@ struct Loader {
             // roughconductor.cpp:168-203
             V3 spec = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
             conductorIOR(props, d, "roughconductor");
-            // MicrofacetDistribution(props) (microfacet.h:99-146)
-            int distr = MTSG_MF_BECKMANN;
-            if (props.strings.count("distribution")) {
-                std::string dn = lower(props.strings["distribution"]);
-                if (dn == "beckmann") distr = MTSG_MF_BECKMANN;
-                else if (dn == "ggx") distr = MTSG_MF_GGX;
-                else if (dn == "phong" || dn == "as") distr = MTSG_MF_PHONG;
-                else throw err("Specified an invalid microfacet distribution \"" + dn + "\", must be \"beckmann\", \"ggx\", or \"phong\"/\"as\"!");
-            }
-            float au = 0.1f, av = 0.1f;
-            if (props.has("alpha")) {
-                if (props.has("alphaU") || props.has("alphaV")) throw err("Microfacet model: please specify either 'alpha' or 'alphaU'/'alphaV'.");
-                au = av = props.getFloat("alpha");
-            } else if (props.has("alphaU") || props.has("alphaV")) {
-                if (!props.has("alphaU") || !props.has("alphaV")) throw err("Microfacet model: both 'alphaU' and 'alphaV' must be specified.");
-                au = props.getFloat("alphaU"); av = props.getFloat("alphaV");
-            }
-            au = std::max(au, 1e-4f); av = std::max(av, 1e-4f);
+            microfacetProps(props, d);
             d.type = MTSG_BSDF_ROUGHCONDUCTOR;
-            d.distribution = distr;
-            // visible-normal sampling is not supported for Phong (microfacet.h:140-144)
-            d.sample_visible = (props.getBool("sampleVisible", true) && distr != MTSG_MF_PHONG) ? 1 : 0;
-            d.alpha_u = au; d.alpha_v = av;
             for (int i = 0; i < 3; ++i) d.spec_refl[i] = spec[i];
             d.smooth = 1;
             d.ref_n_zero = 0;
@@ -783,6 +787,21 @@ struct Loader {
             d.ior_inv_eta = 1 / d.ior_eta;
             for (int i = 0; i < 3; ++i) { d.spec_refl[i] = sr[i]; d.spec_trans[i] = st[i]; }
             d.smooth = 0;        // delta components only
+            d.ref_n_zero = 1;    // ETransmission | EBackSide
+        } else if (type == "roughdielectric") {
+            // roughdielectric.cpp:160-205: microfacet reflection + transmission
+            float intIOR = lookupIORProp(props, "intIOR", "bk7");
+            float extIOR = lookupIORProp(props, "extIOR", "air");
+            if (intIOR < 0 || extIOR < 0 || intIOR == extIOR)
+                throw err("The interior and exterior indices of refraction must be positive and differ!");
+            V3 sr = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
+            V3 st = energyConserving(props, props.getSpectrum("specularTransmittance", V3(1.0f)));
+            microfacetProps(props, d);
+            d.type = MTSG_BSDF_ROUGHDIELECTRIC;
+            d.ior_eta = intIOR / extIOR;
+            d.ior_inv_eta = 1 / d.ior_eta;
+            for (int i = 0; i < 3; ++i) { d.spec_refl[i] = sr[i]; d.spec_trans[i] = st[i]; }
+            d.smooth = 1;        // glossy components: direct sampling
             d.ref_n_zero = 1;    // ETransmission | EBackSide
         } else if (type == "conductor") {
             // conductor.cpp:98-130: ideal mirror with the exact conductor Fresnel term
@@ -827,7 +846,8 @@ struct Loader {
             if (kids.size() > 2) throw err("No more than two nested BRDFs can be added!");
             for (int k : kids) {
                 const mtsg_bsdf &kd = scene.bsdfs[k].d;
-                if (kd.type == MTSG_BSDF_DIELECTRIC) throw err("Only materials without a transmission component can be nested!");
+                if (kd.type == MTSG_BSDF_DIELECTRIC || kd.type == MTSG_BSDF_ROUGHDIELECTRIC)
+                    throw err("Only materials without a transmission component can be nested!");
                 if (kd.twosided) throw err("twosided: a nested twosided material is not supported by this build");
             }
             const int backIdx = kids.size() == 2 ? kids[1] : kids[0];

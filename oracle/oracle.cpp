@@ -1170,7 +1170,7 @@ struct SceneView {
 // ---------------------------------------------------------------------------
 // BSDFs
 // ---------------------------------------------------------------------------
-enum { EDeltaReflection = 4, EDeltaTransmission = 16, EGlossyReflection = 2, EDiffuseReflection = 1 };
+enum { EDeltaReflection = 4, EDeltaTransmission = 16, EGlossyReflection = 2, EDiffuseReflection = 1, EGlossyTransmission = 32 };   // own bit numbering of the bsdf.h:224-285 lobe types
 
 struct BRec {   // BSDFSamplingRecord (bsdf.h:40-193)
     Vec wi, wo;
@@ -1207,6 +1207,14 @@ struct Microfacet {
         }
     }
     bool isotropic() const { return au == av; }
+    void scaleAlpha(float v) {   // microfacet.h:178-183
+        au *= v;
+        av *= v;
+        if (type == MTSG_MF_PHONG) {
+            eu = std::max(2.0f / (au * au) - 2.0f, 0.0f);
+            ev = std::max(2.0f / (av * av) - 2.0f, 0.0f);
+        }
+    }
     float phongExponent(const Vec &v) const {   // interpolatePhongExponent :554-565
         const float st2 = sinTheta2(v);
         if (isotropic() || st2 <= 2.93873587705571876e-39f) return eu;
@@ -1450,6 +1458,32 @@ Spec bsdfEval(const mtsg_bsdf &b, const BRec &r) {
         float model = D * G / (4.0f * cosTheta(r.wi));
         return F * model;
     }
+    if (b.type == MTSG_BSDF_ROUGHDIELECTRIC) {   // roughdielectric.cpp:265-335
+        if (cosTheta(r.wi) == 0) return Spec(0.0f);
+        bool reflect = cosTheta(r.wi) * cosTheta(r.wo) > 0;
+        Vec H;
+        if (reflect) {
+            H = normalize(r.wo + r.wi);
+        } else {
+            float eta = cosTheta(r.wi) > 0 ? b.ior_eta : b.ior_inv_eta;
+            H = normalize(r.wi + r.wo * eta);
+        }
+        H = H * signum(cosTheta(H));
+        Microfacet distr = mfOf(b);
+        const float D = distr.eval(H);
+        if (D == 0) return Spec(0.0f);
+        const float F = fresnelDielectricExt1(dot(r.wi, H), b.ior_eta);
+        const float G = distr.G(r.wi, r.wo, H);
+        if (reflect) {
+            float value = F * D * G / (4.0f * std::abs(cosTheta(r.wi)));
+            return Spec::of(b.spec_refl) * value;
+        }
+        float eta = cosTheta(r.wi) > 0.0f ? b.ior_eta : b.ior_inv_eta;
+        float sqrtDenom = dot(r.wi, H) + eta * dot(r.wo, H);
+        float value = ((1 - F) * D * G * eta * eta * dot(r.wi, H) * dot(r.wo, H)) / (cosTheta(r.wi) * sqrtDenom * sqrtDenom);
+        float factor = cosTheta(r.wi) > 0 ? b.ior_inv_eta : b.ior_eta;   // ERadiance
+        return Spec::of(b.spec_trans) * std::abs(value * factor * factor);
+    }
     if (b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:190-233 (ESolidAngle: the diffuse part)
         if (cosTheta(r.wo) <= 0 || cosTheta(r.wi) <= 0) return Spec(0.0f);
         float Fi = fresnelDielectricExt1(cosTheta(r.wi), b.ior_eta);
@@ -1471,6 +1505,27 @@ float bsdfPdf(const mtsg_bsdf &b, const BRec &r) {
         if (distr.sampleVisible) return distr.eval(H) * distr.smithG1(r.wi, H) / (4.0f * cosTheta(r.wi));
         return distr.pdf(r.wi, H) / (4 * absDot(r.wo, H));
     }
+    if (b.type == MTSG_BSDF_ROUGHDIELECTRIC) {   // roughdielectric.cpp:337-400
+        bool reflect = cosTheta(r.wi) * cosTheta(r.wo) > 0;
+        Vec H;
+        float dwh_dwo;
+        if (reflect) {
+            H = normalize(r.wo + r.wi);
+            dwh_dwo = 1.0f / (4.0f * dot(r.wo, H));
+        } else {
+            float eta = cosTheta(r.wi) > 0 ? b.ior_eta : b.ior_inv_eta;
+            H = normalize(r.wi + r.wo * eta);
+            float sqrtDenom = dot(r.wi, H) + eta * dot(r.wo, H);
+            dwh_dwo = (eta * eta * dot(r.wo, H)) / (sqrtDenom * sqrtDenom);
+        }
+        H = H * signum(cosTheta(H));
+        Microfacet sampleDistr = mfOf(b);
+        if (!sampleDistr.sampleVisible) sampleDistr.scaleAlpha(1.2f - 0.2f * std::sqrt(std::abs(cosTheta(r.wi))));
+        float prob = sampleDistr.pdf(r.wi * signum(cosTheta(r.wi)), H);
+        float F = fresnelDielectricExt1(dot(r.wi, H), b.ior_eta);
+        prob *= reflect ? F : (1 - F);
+        return std::abs(prob * dwh_dwo);
+    }
     if (b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:235-263
         if (cosTheta(r.wo) <= 0 || cosTheta(r.wi) <= 0) return 0.0f;
         float Fi = fresnelDielectricExt1(cosTheta(r.wi), b.ior_eta);
@@ -1479,8 +1534,10 @@ float bsdfPdf(const mtsg_bsdf &b, const BRec &r) {
     return 0.0f;
 }
 
-// BSDF::sample(bRec, pdf, sample)
-Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy) {
+// BSDF::sample(bRec, pdf, sample); next1d: bRec.sampler->next1D(), drawn
+// only where the reference draws it (roughdielectric.cpp:531-539)
+template <class Next1D>
+Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy, Next1D &&next1d) {
     if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
         if (cosTheta(r.wi) <= 0) return Spec(0.0f);
         r.wo = squareToCosineHemisphere(sx, sy);
@@ -1531,6 +1588,49 @@ Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy) {
         pdf = 1;
         return Spec::of(b.spec_refl) * fresnelConductorExact(cosTheta(r.wi), Spec::of(b.eta), Spec::of(b.k));
     }
+    if (b.type == MTSG_BSDF_ROUGHDIELECTRIC) {   // roughdielectric.cpp:508-590 (both components)
+        Microfacet distr = mfOf(b);
+        Microfacet sampleDistr = distr;
+        if (!distr.sampleVisible) sampleDistr.scaleAlpha(1.2f - 0.2f * std::sqrt(std::abs(cosTheta(r.wi))));
+        float microfacetPDF;
+        const Vec m = sampleDistr.sample(r.wi * signum(cosTheta(r.wi)), sx, sy, microfacetPDF);
+        if (microfacetPDF == 0) return Spec(0.0f);
+        pdf = microfacetPDF;
+        float cosThetaT;
+        float F = fresnelDielectricExt(dot(r.wi, m), cosThetaT, b.ior_eta);
+        Spec weight(1.0f);
+        bool sampleReflection = true;
+        if (next1d() > F) {
+            sampleReflection = false;
+            pdf *= 1 - F;
+        } else {
+            pdf *= F;
+        }
+        float dwh_dwo;
+        if (sampleReflection) {
+            r.wo = reflectM(r.wi, m);
+            r.eta = 1.0f;
+            r.sampledType = EGlossyReflection;
+            if (cosTheta(r.wi) * cosTheta(r.wo) <= 0) return Spec(0.0f);
+            weight = weight * Spec::of(b.spec_refl);
+            dwh_dwo = 1.0f / (4.0f * dot(r.wo, m));
+        } else {
+            if (cosThetaT == 0) return Spec(0.0f);
+            float e = cosThetaT < 0 ? 1 / b.ior_eta : b.ior_eta;   // refract (util.cpp:767-772)
+            r.wo = m * (dot(r.wi, m) * e + cosThetaT) - r.wi * e;
+            r.eta = cosThetaT < 0 ? b.ior_eta : b.ior_inv_eta;
+            r.sampledType = EGlossyTransmission;
+            if (cosTheta(r.wi) * cosTheta(r.wo) >= 0) return Spec(0.0f);
+            float factor = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;   // ERadiance
+            weight = weight * (Spec::of(b.spec_trans) * (factor * factor));
+            float sqrtDenom = dot(r.wi, m) + r.eta * dot(r.wo, m);
+            dwh_dwo = (r.eta * r.eta * dot(r.wo, m)) / (sqrtDenom * sqrtDenom);
+        }
+        if (distr.sampleVisible) weight = weight * distr.smithG1(r.wo, m);
+        else weight = weight * std::abs(distr.eval(m) * distr.G(r.wi, r.wo, m) * dot(r.wi, m) / (microfacetPDF * cosTheta(r.wi)));
+        pdf *= std::abs(dwh_dwo);
+        return weight;
+    }
     if (b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:344-390 (both components)
         if (cosTheta(r.wi) <= 0) return Spec(0.0f);
         float Fi = fresnelDielectricExt1(cosTheta(r.wi), b.ior_eta);
@@ -1568,10 +1668,11 @@ float bsdfPdfTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec r) {
     bool f;
     return bsdfPdf(bsdfSide(all, b, r, false, f), r);
 }
-Spec bsdfSampleTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy) {
+template <class Next1D>
+Spec bsdfSampleTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy, Next1D &&next1d) {
     bool flipped;
     const mtsg_bsdf &nb = bsdfSide(all, b, r, true, flipped);
-    Spec result = bsdfSample(nb, r, pdf, sx, sy);
+    Spec result = bsdfSample(nb, r, pdf, sx, sy, next1d);
     if (flipped) {
         r.wi.z *= -1;
         if (!result.isZero() && pdf != 0) r.wo.z *= -1;
@@ -1666,7 +1767,7 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
         bRec.wi = its.wi;
         float s0, s1;
         sampler.next2D(s0, s1);
-        Spec bsdfWeight = bsdfSampleTS(scene.d.bsdfs, bsdf, bRec, bsdfPdfS, s0, s1);
+        Spec bsdfWeight = bsdfSampleTS(scene.d.bsdfs, bsdf, bRec, bsdfPdfS, s0, s1, [&]() { return sampler.next1D(); });
         DBG("  depth %d bsdf type=%d s=(%g %g) wi=(%g %g %g) wo=(%g %g %g) w=(%g %g %g) pdf=%g sampled=%d\n", depth, bsdf.type, s0, s1, bRec.wi.x, bRec.wi.y, bRec.wi.z, bRec.wo.x, bRec.wo.y, bRec.wo.z, bsdfWeight.s[0], bsdfWeight.s[1], bsdfWeight.s[2], bsdfPdfS, bRec.sampledType);
         if (bsdfWeight.isZero()) break;
         scattered |= bRec.sampledType != 0;
@@ -2131,10 +2232,15 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
 }
 
 int oracle_bsdf_sample(const mtsg_bsdf *b, const float wi[3], float s0, float s1, float wo[3], float *pdf, float weight[3]) {
+    return oracle_bsdf_sample3(b, wi, s0, s1, 0.5f, wo, pdf, weight);
+}
+
+int oracle_bsdf_sample3(const mtsg_bsdf *b, const float wi[3], float s0, float s1, float s2, float wo[3], float *pdf,
+                        float weight[3]) {
     BRec r;
     r.wi = Vec(wi[0], wi[1], wi[2]);
     float p = 0;
-    Spec w = bsdfSample(*b, r, p, s0, s1);
+    Spec w = bsdfSample(*b, r, p, s0, s1, [&]() { return s2; });
     wo[0] = r.wo.x; wo[1] = r.wo.y; wo[2] = r.wo.z;
     *pdf = p;
     weight[0] = w.s[0]; weight[1] = w.s[1]; weight[2] = w.s[2];
@@ -2155,6 +2261,13 @@ int oracle_bsdf_sample_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, cons
                          float *weight, int32_t *type) {
     for (uint32_t i = 0; i < n; ++i)
         type[i] = oracle_bsdf_sample(b, wi, u2[2 * i], u2[2 * i + 1], wo + 3 * i, pdf + i, weight + 3 * i);
+    return 0;
+}
+
+int oracle_bsdf_sample3_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *u3, float *wo, float *pdf,
+                          float *weight, int32_t *type) {
+    for (uint32_t i = 0; i < n; ++i)
+        type[i] = oracle_bsdf_sample3(b, wi, u3[3 * i], u3[3 * i + 1], u3[3 * i + 2], wo + 3 * i, pdf + i, weight + 3 * i);
     return 0;
 }
 

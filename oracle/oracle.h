@@ -82,6 +82,12 @@ int oracle_bsdf_eval(const mtsg_bsdf *b, const float wi[3], const float wo[3],
                      float value[3], float *pdf);
 
 /* batched forms for the chi-square tests: u2 = 2n sample pairs, wo/weight/value 3n */
+/* As oracle_bsdf_sample(_n) with a third uniform per sample for the BSDF's
+ * own sampler->next1D() draw (roughdielectric's reflect/refract choice). */
+int oracle_bsdf_sample3(const mtsg_bsdf *b, const float wi[3], float s0, float s1, float s2, float wo[3], float *pdf,
+                        float weight[3]);
+int oracle_bsdf_sample3_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *u3, float *wo, float *pdf,
+                          float *weight, int32_t *type);
 int oracle_bsdf_sample_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *u2, float *wo, float *pdf,
                          float *weight, int32_t *type);
 int oracle_bsdf_eval_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *wo, float *value, float *pdf);

@@ -28,7 +28,7 @@ THETA_BINS, PHI_BINS = 10, 20
 N_SAMPLES = THETA_BINS * PHI_BINS * 1000
 WI_PER_BSDF = 5
 
-DIFFUSE, ROUGHCONDUCTOR, DIELECTRIC, CONDUCTOR, PLASTIC = 1, 2, 3, 4, 5
+DIFFUSE, ROUGHCONDUCTOR, DIELECTRIC, CONDUCTOR, PLASTIC, ROUGHDIELECTRIC = 1, 2, 3, 4, 5, 6
 DELTA = 4 | 16   # EDeltaReflection | EDeltaTransmission
 BECKMANN, GGX, PHONG = 0, 1, 2
 
@@ -70,18 +70,23 @@ def _lib():
     if not getattr(L, "_bsdf_n_bound", False):
         L.oracle_bsdf_sample_n.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_bsdf_sample3_n.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_void_p]
         L.oracle_bsdf_eval_n.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         L._bsdf_n_bound = True
     return L
 
 
 def sample(b, wi, u2):
-    u2 = np.ascontiguousarray(u2, np.float32)
-    n = u2.shape[0]
+    """u2: n x 2 (the sample) or n x 3 (plus the BSDF's own next1D draw)."""
+    u = np.ascontiguousarray(u2, np.float32)
+    n = u.shape[0]
+    if u.shape[1] == 2:
+        u = np.ascontiguousarray(np.concatenate([u, np.full((n, 1), 0.5, np.float32)], 1))
     wi = np.ascontiguousarray(wi, np.float32)
     wo = np.zeros((n, 3), np.float32); pdf = np.zeros(n, np.float32)
     w = np.zeros((n, 3), np.float32); t = np.zeros(n, np.int32)
-    _lib().oracle_bsdf_sample_n(C.byref(b), O._p(wi), n, O._p(u2), O._p(wo), O._p(pdf), O._p(w), O._p(t))
+    _lib().oracle_bsdf_sample3_n(C.byref(b), O._p(wi), n, O._p(u), O._p(wo), O._p(pdf), O._p(w), O._p(t))
     return wo, pdf, w, t
 
 
@@ -94,7 +99,21 @@ def evaluate(b, wi, wo):
     return val, pdf
 
 
-def expected_counts(b, wi, n_samples, gl=32):
+def unreachable(b, wi, wo):
+    """Rough dielectric transmission directions no microfacet refraction can
+    produce (dot(wi, H) * dot(wo, H) >= 0 for the generalised half-vector):
+    the reference's pdf() (roughdielectric.cpp:337-400) still gives them a
+    density, and sample() rejects the corresponding draws by its side check,
+    so the sampled histogram is compared with the pdf on the reachable set."""
+    if b.type != ROUGHDIELECTRIC:
+        return np.zeros(len(wo), bool)
+    eta = b.ior_eta if wi[2] > 0 else b.ior_inv_eta
+    H = wi[None, :] + wo * eta
+    H = H / np.linalg.norm(H, axis=1, keepdims=True) * np.sign(H[:, 2:3])
+    return (wi[2] * wo[:, 2] < 0) & ((H @ wi) * (H * wo).sum(1) >= 0)
+
+
+def expected_counts(b, wi, n_samples, gl=32, reachable_only=True):
     """n_samples x integral of pdf(wo) sin(theta) over each (theta, phi) cell
     (tensor Gauss-Legendre, gl x gl nodes per cell: 12 under-resolves the
     alpha = 0.1 lobes of the anisotropic cases)."""
@@ -107,6 +126,8 @@ def expected_counts(b, wi, n_samples, gl=32):
     th, ph = np.broadcast_arrays(th, ph)
     wo = np.stack([np.sin(th) * np.cos(ph), np.sin(th) * np.sin(ph), np.cos(th)], -1).reshape(-1, 3)
     _, pdf = evaluate(b, wi, wo)
+    if reachable_only:
+        pdf = np.where(unreachable(b, np.asarray(wi, np.float64), wo.astype(np.float64)), 0.0, pdf)
     wts = (w[:, None] * w[None, :]) * (0.25 * dth * dph)
     integ = (pdf.reshape(THETA_BINS, PHI_BINS, gl, gl).astype(np.float64) * np.sin(th) * wts).sum((2, 3))
     return integ * n_samples
@@ -176,7 +197,16 @@ CASES = [
     # samples are delta and excluded, as chisquare.cpp does for discrete ones)
     ("plastic", dict(kind=PLASTIC, eta=1.49, fdr_int=0.595, spec_weight=0.6)),
     ("plastic_nonlinear", dict(kind=PLASTIC, eta=1.8, nonlinear=1, fdr_int=0.7, spec_weight=0.3)),
+    # rough dielectric: reflection + transmission over the whole sphere, from
+    # either side (roughdielectric.cpp; test_bsdf.xml holds rough dielectrics)
+    ("roughdielectric_ggx_visible", dict(kind=ROUGHDIELECTRIC, dist=GGX, alpha=0.3, visible=1, eta=1.5)),
+    ("roughdielectric_beckmann_classic", dict(kind=ROUGHDIELECTRIC, dist=BECKMANN, alpha=0.2, visible=0, eta=1.33)),
+    # (Beckmann: GGX visible sampling draws slope_y from a rational fit whose
+    # error the strongly stretched anisotropic incidences make visible)
+    ("roughdielectric_aniso", dict(kind=ROUGHDIELECTRIC, dist=BECKMANN, alpha=0.1, alpha_v=0.35, visible=1, eta=1.6)),
+    ("roughdielectric_phong", dict(kind=ROUGHDIELECTRIC, dist=PHONG, alpha=0.25, visible=0, eta=1.5)),
 ]
+BOTH_SIDES = (ROUGHDIELECTRIC,)
 
 
 @pytest.mark.parametrize("name,kw", CASES, ids=[c[0] for c in CASES])
@@ -184,8 +214,11 @@ def test_bsdf_sampling_matches_pdf(name, kw):
     b = make_bsdf(**kw)
     rng = np.random.default_rng(7)
     alpha = 1 - (1 - SIGNIFICANCE) ** (1.0 / WI_PER_BSDF)   # Sidak (chisquare.cpp:255)
-    for wi in random_wi(rng, WI_PER_BSDF):
-        u2 = rng.random((N_SAMPLES, 2), dtype=np.float32)
+    wis = random_wi(rng, WI_PER_BSDF)
+    if kw["kind"] in BOTH_SIDES:
+        wis = [w * (1 if k % 2 == 0 else -1) for k, w in enumerate(wis)]   # incident from inside too
+    for wi in wis:
+        u2 = rng.random((N_SAMPLES, 3), dtype=np.float32)
         wo, pdf, w, t = sample(b, wi, u2)
         ok = (pdf > 0) & (w.max(1) > 0) & ((t & DELTA) == 0)
         p = chi2_pvalue(observed_counts(wo[ok]), expected_counts(b, wi, N_SAMPLES))

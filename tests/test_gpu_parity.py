@@ -242,3 +242,15 @@ def test_smooth_materials_scene_parity():
     _, c, gi = render_pair(scene, g, max_depth=3, strict_normals=1)
     check_render(c, gi)
     g.close()
+
+
+@pytest.mark.parametrize("defs", [dict(dist="ggx", alpha=0.2), dict(dist="beckmann", alpha=0.35, sampleVisible="false")],
+                         ids=["ggx-visible", "beckmann-classic"])
+def test_rough_dielectric_parity(defs):
+    # roughdielectric: glossy reflection + transmission, the extra next1D draw
+    # of the reflect/refract choice, eta tracked through Russian roulette
+    scene = mtsg.Scene(os.path.join(SCENES, "cbox_roughglass.xml"), dict(defs, width=48, height=48, spp=8))
+    g = mtsg.GPUScene(scene, 0)
+    _, c, gi = render_pair(scene, g)
+    check_render(c, gi)
+    g.close()
