@@ -221,7 +221,8 @@ def main():
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         tj, tsrc = pmc_traffic(a.workload)
         traffic = None
-        if tj and avg_launch_s > 0 and a.workload == "bunny15" and params.spp == 256 and world == 1:
+        if (tj and avg_launch_s > 0 and a.workload == "bunny15" and params.spp == 256 and world == 1
+                and a.emulate_ranks <= 1):
             traffic = round(tj["traffic_bytes_per_launch"] / avg_launch_s / 1e9, 1)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

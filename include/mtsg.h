@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MTSG_ABI_VERSION 4
+#define MTSG_ABI_VERSION 5
 
 /* ---- error codes (mtsg_last_error() gives the message) ------------------ */
 enum {
@@ -97,7 +97,8 @@ enum {
     MTSG_BSDF_DIELECTRIC     = 3,   /* src/bsdfs/dielectric.cpp     */
     MTSG_BSDF_CONDUCTOR      = 4,   /* src/bsdfs/conductor.cpp      */
     MTSG_BSDF_PLASTIC        = 5,   /* src/bsdfs/plastic.cpp        */
-    MTSG_BSDF_ROUGHDIELECTRIC = 6   /* src/bsdfs/roughdielectric.cpp */
+    MTSG_BSDF_ROUGHDIELECTRIC = 6,  /* src/bsdfs/roughdielectric.cpp */
+    MTSG_BSDF_ROUGHPLASTIC   = 7    /* src/bsdfs/roughplastic.cpp   */
 };
 enum { MTSG_MF_BECKMANN = 0, MTSG_MF_GGX = 1, MTSG_MF_PHONG = 2 };   /* microfacet.h:49-57 */
 
@@ -105,6 +106,8 @@ enum { MTSG_MF_BECKMANN = 0, MTSG_MF_GGX = 1, MTSG_MF_PHONG = 2 };   /* microfac
  * of a twosided wrapper's front material: when the incident direction is on
  * the back (cosTheta(wi) <= 0 for eval/pdf, < 0 for sampling) the record
  * bsdfs[back] is used with wi.z and wo.z negated. */
+#define MTSG_RTRANS_SAMPLES 100     /* m_thetaSamples of the data/microfacet tables */
+
 typedef struct mtsg_bsdf {
     int32_t type;
     int32_t distribution;    /* MTSG_MF_*                                   */
@@ -122,6 +125,12 @@ typedef struct mtsg_bsdf {
     float ior_eta, ior_inv_eta; /* (rough)dielectric / plastic intIOR/extIOR and inverse */
     float fdr_int;           /* plastic: fresnelDiffuseReflectance(1 / eta) */
     float spec_sampling_weight; /* plastic: sAvg / (dAvg + sAvg) luminances */
+    /* roughplastic: the external RoughTransmittance reduced to the material's
+     * (eta, alpha) (rtrans.h:169-207, m_alphaFixed && m_etaFixed): samples at
+     * warped cos(theta) nodes k/(n-1) = cos^(1/4), evaluated by
+     * evalCubicInterp1D (spline.cpp:23-60); fdr_int holds
+     * 1 - internal.evalDiffuse(alpha) (roughplastic.cpp:349-351) */
+    float rtrans[MTSG_RTRANS_SAMPLES];
 } mtsg_bsdf;
 
 enum { MTSG_EMITTER_AREA = 1, MTSG_EMITTER_ENVMAP = 2 };

@@ -50,6 +50,13 @@ void mtsh_develop(const float *rgbaw, int w, int h, float *rgb_out);
 /* Write an RGB float image as PFM (bitmap.cpp:347-398). Returns 0 on success. */
 int mtsh_write_pfm(const char *path, int w, int h, const float *rgb);
 
+/* roughplastic's rough dielectric transmittance (src/bsdfs/rtrans.h,
+ * RoughTransmittance::eval / evalDiffuse at fixed eta and alpha): T at the
+ * n warped nodes cos(theta_k) = (k/(n-1))^4, and optionally the diffuse
+ * transmittance \int 2 mu T(mu) dmu.  distribution is MTSG_MF_*.
+ * Returns 0, or -1 on invalid arguments. */
+int mtsh_rough_transmittance(int distribution, float alpha, float eta, int n, float *trans, float *diffuse);
+
 void mtsh_last_error(char *buf, size_t size);
 
 #ifdef __cplusplus

@@ -1129,6 +1129,25 @@ DEV float plastic_prob_specular(const mtsg_bsdf &b, float Fi) {
     return (Fi * b.spec_sampling_weight) / (Fi * b.spec_sampling_weight + (1 - Fi) * (1 - b.spec_sampling_weight));
 }
 
+// evalCubicInterp1D over [0, 1] (spline.cpp:23-60)
+DEV float cubic_interp1d(float x, const float *v, int n) {
+    if (!(x >= 0.0f && x <= 1.0f)) return 0.0f;
+    float t = x * (float)(n - 1);
+    const int k = min((int)t, n - 2);
+    const float f0 = v[k], f1 = v[k + 1];
+    const float d0 = k > 0 ? 0.5f * (v[k + 1] - v[k - 1]) : v[k + 1] - v[k];
+    const float d1 = k + 2 < n ? 0.5f * (v[k + 2] - v[k]) : v[k + 1] - v[k];
+    t = t - (float)k;
+    const float t2 = t * t, t3 = t2 * t;
+    return (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
+}
+// RoughTransmittance::eval with eta and alpha fixed (rtrans.h:169-181, 205-206)
+DEV float rough_trans(const mtsg_bsdf &b, float cosTheta) {
+    if (!(cosTheta >= 0)) return 0.0f;
+    const float r = cubic_interp1d(powf(fabsf(cosTheta), 0.25f), b.rtrans, MTSG_RTRANS_SAMPLES);
+    return fminf(1.0f, fmaxf(0.0f, r));
+}
+
 // BSDF::eval * cos (ESolidAngle) and pdf for the smooth BSDFs.  EXT: the
 // scene has conductor / plastic / twosided records (the shade kernel is
 // instantiated without them otherwise: their code costs the common
@@ -1192,6 +1211,21 @@ DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
         const float invEta2 = 1 / (b.ior_eta * b.ior_eta);
         pdf = kInvPi * wo.z * (1 - plastic_prob_specular(b, Fi));
         return plastic_diffuse(b) * (kInvPi * wo.z * invEta2 * (1 - Fi) * (1 - Fo));
+    }
+    if (EXT && b.type == MTSG_BSDF_ROUGHPLASTIC) {   // roughplastic.cpp:302-345 (eval), 347-385 (pdf)
+        if (wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
+        const MF mf = make_mf(b);
+        const float3 H = normalize(wo + wi);
+        const float D = mf.D(H);
+        const float F = fresnel_dielectric1(dot(wi, H), b.ior_eta);
+        const float G = mf.G1(wi, H) * mf.G1(wo, H);
+        const float value = F * D * G / (4.0f * wi.z);
+        const float T12 = rough_trans(b, wi.z), T21 = rough_trans(b, wo.z);
+        const float invEta2 = 1.0f / (b.ior_eta * b.ior_eta);
+        float probSpecular = plastic_prob_specular(b, 1 - T12);
+        const float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
+        pdf = mf.pdf(wi, H) * dwh_dwo * probSpecular + (1 - probSpecular) * (kInvPi * wo.z);
+        return ld3(b.spec_refl) * value + plastic_diffuse(b) * (kInvPi * wo.z * T12 * T21 * invEta2);
     }
     return mk3(0, 0, 0);   // dielectric / conductor: delta components only
 }
@@ -1291,6 +1325,27 @@ DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSam
         else weight = weight * fabsf(distr.D(m) * (distr.G1(wi, m) * distr.G1(r.wo, m)) * dot(wi, m) / (microfacetPDF * wi.z));
         r.pdf *= fabsf(dwh_dwo);
         r.weight = weight;
+        return !isZero(r.weight);
+    }
+    if (EXT && b.type == MTSG_BSDF_ROUGHPLASTIC) {   // roughplastic.cpp:387-455: component chosen by sample.y
+        if (wi.z <= 0) return false;
+        const float probSpecular = plastic_prob_specular(b, 1 - rough_trans(b, wi.z));
+        if (sy < probSpecular) {
+            sy /= probSpecular;
+            const MF mf = make_mf(b);
+            float mpdf;
+            const float3 m = mf.sample(wi, sx, sy, mpdf);
+            r.wo = m * (2 * dot(wi, m)) - wi;
+            if (r.wo.z <= 0) return false;
+        } else {
+            sy = (sy - probSpecular) / (1 - probSpecular);
+            r.wo = cosine_hemisphere(sx, sy);
+        }
+        float pdf;
+        const float3 val = bsdf_eval1<EXT>(b, wi, r.wo, pdf);
+        if (pdf == 0) return false;
+        r.pdf = pdf;
+        r.weight = val / pdf;
         return !isZero(r.weight);
     }
     if (EXT && b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:344-375 (both components)
@@ -2436,7 +2491,8 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     ds.has_env = d->has_envmap ? 1 : 0;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
         const mtsg_bsdf &b = d->bsdfs[i];
-        if (b.type == MTSG_BSDF_CONDUCTOR || b.type == MTSG_BSDF_PLASTIC || b.type == MTSG_BSDF_ROUGHDIELECTRIC || b.twosided)
+        if (b.type == MTSG_BSDF_CONDUCTOR || b.type == MTSG_BSDF_PLASTIC || b.type == MTSG_BSDF_ROUGHDIELECTRIC ||
+            b.type == MTSG_BSDF_ROUGHPLASTIC || b.twosided)
             s->extBsdfs = true;
         if (b.twosided && (b.back < 0 || (uint32_t)b.back >= d->n_bsdfs)) {
             g_err = "bsdf " + std::to_string(i) + ": twosided back record out of range";

@@ -96,6 +96,16 @@ int mtsh_write_pfm(const char *path, int w, int h, const float *rgb) {
     }
 }
 
+int mtsh_rough_transmittance(int distribution, float alpha, float eta, int n, float *trans, float *diffuse) {
+    if (n < 2 || !trans || distribution < MTSG_MF_BECKMANN || distribution > MTSG_MF_PHONG || !(alpha > 0) || !(eta > 0)) {
+        g_err = "mtsh_rough_transmittance: invalid arguments";
+        return -1;
+    }
+    mtsh::roughTransmittanceSlice(distribution, alpha, eta, n, trans);
+    if (diffuse) *diffuse = mtsh::roughDiffuseTransmittance(distribution, alpha, eta);
+    return 0;
+}
+
 void mtsh_last_error(char *buf, size_t size) {
     if (!size) return;
     strncpy(buf, g_err.c_str(), size - 1);

@@ -25,6 +25,8 @@
 #include <functional>
 #include <sstream>
 
+#include <zlib.h>
+
 #include "scene.h"
 
 namespace mtsh {
@@ -439,6 +441,119 @@ void loadOBJ(const std::string &path, Mesh &mesh, bool flipTexCoords) {
     mesh.idx = std::move(idx);
 }
 
+// Mitsuba's `serialized` mesh container (src/shapes/serialized.cpp:64-145,
+// TriMesh::loadCompressed / readHeader / readOffset in
+// src/librender/trimesh.cpp:175-300): per mesh an uncompressed header
+// (uint16 0x041C, uint16 version 3 or 4) followed by a zlib (DEFLATE) stream
+// holding uint32 flags, [v4: a null-terminated name], uint64 vertex and
+// triangle counts, positions, optional normals / texcoords / colors (float32,
+// or float64 with flag 0x2000), and uint32 triangle indices.  The file ends
+// with a dictionary of the meshes' start offsets (v4: uint64, v3: uint32) and
+// a uint32 mesh count.  Vertex colors are read and dropped (no texture
+// plugins in this build).
+namespace {
+enum { kSerHasNormals = 0x0001, kSerHasTexcoords = 0x0002, kSerHasColors = 0x0008, kSerDouble = 0x2000 };
+
+class Inflater {
+public:
+    Inflater(const std::string &data, size_t offset, const std::string &path) : path_(path) {
+        memset(&z_, 0, sizeof(z_));
+        if (inflateInit(&z_) != Z_OK) throw err("\"" + path + "\": inflateInit failed");
+        z_.next_in = (Bytef *)data.data() + offset;
+        z_.avail_in = (uInt)(data.size() - offset);
+    }
+    ~Inflater() { inflateEnd(&z_); }
+    void read(void *dst, size_t n) {
+        z_.next_out = (Bytef *)dst;
+        z_.avail_out = (uInt)n;
+        while (z_.avail_out > 0) {
+            int rc = inflate(&z_, Z_SYNC_FLUSH);
+            if (rc == Z_STREAM_END && z_.avail_out > 0)
+                throw err("\"" + path_ + "\": unexpected end of the compressed mesh stream");
+            if (rc != Z_OK && rc != Z_STREAM_END)
+                throw err("\"" + path_ + "\": corrupt compressed mesh stream (zlib error " + std::to_string(rc) + ")");
+        }
+    }
+    template <class T> T get() { T v; read(&v, sizeof(T)); return v; }
+    std::string cstring() {
+        std::string s;
+        for (char c; (c = get<char>()) != 0;) s += c;
+        return s;
+    }
+    // readHelper (trimesh.cpp:150-172): single or double precision to float
+    void floats(std::vector<float> &out, size_t n, bool dbl) {
+        out.resize(n);
+        if (!dbl) { read(out.data(), n * sizeof(float)); return; }
+        std::vector<double> tmp(n);
+        read(tmp.data(), n * sizeof(double));
+        for (size_t i = 0; i < n; ++i) out[i] = (float)tmp[i];
+    }
+private:
+    z_stream z_;
+    std::string path_;
+};
+
+template <class T> T leAt(const std::string &d, size_t off) { T v; memcpy(&v, d.data() + off, sizeof(T)); return v; }
+}  // namespace
+
+void loadSerialized(const std::string &path, int shapeIndex, Mesh &mesh) {
+    const std::string data = readFile(path);
+    auto header = [&](size_t off) -> int {
+        if (off + 4 > data.size()) throw err("\"" + path + "\": truncated file");
+        const uint16_t format = leAt<uint16_t>(data, off), version = leAt<uint16_t>(data, off + 2);
+        if (format == 0x1C04)
+            throw err("Encountered a geometry file generated by an old version of Mitsuba. Please re-import the scene to update this file to the current format.");
+        if (format != 0x041C) throw err("\"" + path + "\": Encountered an invalid file format!");
+        if (version != 3 && version != 4) throw err("\"" + path + "\": Encountered an incompatible file version!");
+        return version;
+    };
+    if (shapeIndex < 0) throw err("Shape index must be nonnegative!");
+    const int version = header(0);
+    size_t offset = 0;
+    if (shapeIndex != 0) {
+        // readOffset (trimesh.cpp:272-291); the dictionary sits at the end
+        if (data.size() < 8) throw err("\"" + path + "\": truncated file");
+        const uint32_t count = leAt<uint32_t>(data, data.size() - 4);
+        if (shapeIndex >= (int)count)
+            throw err("Unable to unserialize mesh, shape index is out of range! (requested " + std::to_string(shapeIndex) +
+                      " out of 0.." + std::to_string((int)count - 1) + ")");
+        if (version == 4) {
+            const size_t at = data.size() - 8 * (size_t)(count - shapeIndex) - 4;
+            if (at > data.size()) throw err("\"" + path + "\": corrupt offset dictionary");
+            offset = (size_t)leAt<uint64_t>(data, at);
+        } else {
+            const size_t at = data.size() - 4 * (size_t)(count - shapeIndex + 1);
+            if (at > data.size()) throw err("\"" + path + "\": corrupt offset dictionary");
+            offset = leAt<uint32_t>(data, at);
+        }
+        if (offset + 4 > data.size()) throw err("\"" + path + "\": corrupt offset dictionary");
+        header(offset);
+    }
+    Inflater z(data, offset + 4, path);
+    const uint32_t flags = z.get<uint32_t>();
+    if (version == 4) mesh.name = z.cstring();
+    const uint64_t nv = z.get<uint64_t>(), nt = z.get<uint64_t>();
+    if (nv > 0xFFFFFFFFull || nt > 0x7FFFFFFFull) throw err("\"" + path + "\": mesh too large for 32-bit indices");
+    const bool dbl = (flags & kSerDouble) != 0;
+    std::vector<float> buf;
+    z.floats(buf, 3 * nv, dbl);
+    mesh.p.resize(nv);
+    for (size_t i = 0; i < nv; ++i) mesh.p[i] = V3(buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]);
+    mesh.n.clear();
+    if (flags & kSerHasNormals) {
+        z.floats(buf, 3 * nv, dbl);
+        mesh.n.resize(nv);
+        for (size_t i = 0; i < nv; ++i) mesh.n[i] = V3(buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]);
+    }
+    mesh.uv.clear();
+    if (flags & kSerHasTexcoords) z.floats(mesh.uv, 2 * nv, dbl);
+    if (flags & kSerHasColors) z.floats(buf, 3 * nv, dbl);
+    mesh.idx.resize(3 * nt);
+    z.read(mesh.idx.data(), mesh.idx.size() * sizeof(uint32_t));
+    for (uint32_t i : mesh.idx)
+        if (i >= nv) throw err("\"" + path + "\": triangle index out of range");
+}
+
 // trimesh.cpp:608-681
 static float unitAngle(const V3 &u, const V3 &v) {
     if (dot(u, v) < 0) return (float)M_PI - 2.0f * std::asin(0.5f * length(v + u));
@@ -828,6 +943,39 @@ struct Loader {
             for (int i = 0; i < 3; ++i) { d.spec_refl[i] = sr[i]; d.reflectance[i] = dr[i]; }
             d.smooth = 1;        // diffuse component
             d.ref_n_zero = 0;
+        } else if (type == "roughplastic") {
+            // roughplastic.cpp:198-300: microfacet dielectric coating over a
+            // diffuse base; rough transmittance through the interface
+            float intIOR = lookupIORProp(props, "intIOR", "polypropylene");
+            float extIOR = lookupIORProp(props, "extIOR", "air");
+            if (intIOR < 0 || extIOR < 0 || intIOR == extIOR)
+                throw err("The interior and exterior indices of refraction must be positive and differ!");
+            microfacetProps(props, d);
+            if (d.alpha_u != d.alpha_v)
+                throw err("The 'roughplastic' plugin currently does not support anisotropic microfacet distributions!");
+            // RoughTransmittance::checkEta/checkAlpha (rtrans.h:222-258): the
+            // range the reference's tables cover (eta in [1.0001, 4] after
+            // inverting eta < 1, alpha in [0, 4], [0, 0.5] for Phong)
+            const float etaChk = intIOR / extIOR < 1 ? extIOR / intIOR : intIOR / extIOR;
+            if (etaChk < 1.0001f || etaChk > 4.0f)
+                throw err("Error: the requested relative index of refraction is out of the supported range [1.0001, 4]");
+            const float alphaMax = d.distribution == MTSG_MF_PHONG ? 0.5f : 4.0f;   // phong.dat covers [0, 0.5]
+            if (d.alpha_u > alphaMax)
+                throw err("Error: the requested roughness value is out of the supported range");
+            V3 sr = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
+            V3 dr = energyConserving(props, props.getSpectrum("diffuseReflectance", V3(0.5f)));
+            d.type = MTSG_BSDF_ROUGHPLASTIC;
+            d.ior_eta = intIOR / extIOR;
+            d.ior_inv_eta = 1 / d.ior_eta;
+            d.nonlinear = props.getBool("nonlinear", false) ? 1 : 0;
+            const float dAvg = luminance(dr), sAvg = luminance(sr);
+            d.spec_sampling_weight = sAvg / (dAvg + sAvg);
+            for (int i = 0; i < 3; ++i) { d.spec_refl[i] = sr[i]; d.reflectance[i] = dr[i]; }
+            // external slice at (eta, alpha); internal diffuse transmittance at 1/eta
+            roughTransmittanceSlice(d.distribution, d.alpha_u, d.ior_eta, MTSG_RTRANS_SAMPLES, d.rtrans);
+            d.fdr_int = 1 - roughDiffuseTransmittance(d.distribution, d.alpha_u, d.ior_inv_eta);
+            d.smooth = 1;        // glossy + diffuse components
+            d.ref_n_zero = 0;
         } else if (type == "twosided") {
             // twosided.cpp:52-80: one or two nested BRDFs, front and back
             std::vector<int> kids;
@@ -993,6 +1141,19 @@ struct Loader {
             loadOBJ(resolve(props.getString("filename", "")), m, props.getBool("flipTexCoords", true));
         } else if (type == "cube") {
             buildCube(m);
+        } else if (type == "serialized") {
+            // serialized.cpp:146-196: the file's face-normal flag is overridden
+            // by the property; an orientation-reversing toWorld swaps the
+            // first two indices of every triangle
+            if (props.has("maxSmoothAngle"))
+                throw err("serialized: 'maxSmoothAngle' (TriMesh::rebuildTopology) is outside this build's scope");
+            loadSerialized(resolve(props.getString("filename", "")), props.getInt("shapeIndex", 0), m);
+            const auto &M = toWorld.m;
+            const double det = (double)M[0][0] * ((double)M[1][1] * M[2][2] - (double)M[1][2] * M[2][1]) -
+                               (double)M[0][1] * ((double)M[1][0] * M[2][2] - (double)M[1][2] * M[2][0]) +
+                               (double)M[0][2] * ((double)M[1][0] * M[2][1] - (double)M[1][1] * M[2][0]);
+            if (det < 0)
+                for (size_t t = 0; t + 2 < m.idx.size(); t += 3) std::swap(m.idx[t], m.idx[t + 1]);
         } else {
             throw err("line " + std::to_string(n.line) + ": shape plugin \"" + type + "\" is outside this build's scope");
         }

@@ -172,6 +172,7 @@ std::unique_ptr<Scene> loadScene(const std::string &path,
 // Mesh loaders
 void loadPLY(const std::string &path, Mesh &mesh);   // src/shapes/ply.cpp
 void loadOBJ(const std::string &path, Mesh &mesh, bool flipTexCoords);  // src/shapes/obj.cpp
+void loadSerialized(const std::string &path, int shapeIndex, Mesh &mesh);  // src/shapes/serialized.cpp
 
 // TriMesh::computeNormals (src/librender/trimesh.cpp:608-681)
 void computeNormals(Mesh &mesh, bool flipNormals);
@@ -188,6 +189,12 @@ void buildKDTree(const PrimSource &src, const KDBuildParams &params, KDTree &out
 // Conductor IOR lookup (generated from data/ior/*.spd), dielectric lookupIOR
 bool lookupConductor(const std::string &name, V3 &eta, V3 &k);
 float lookupIOR(const std::string &name);
+
+// roughplastic: the material's slice of RoughTransmittance (rtrans.h),
+// computed by quadrature (host/rtrans.cpp): T at cos(theta_k) = (k/(n-1))^4,
+// and the diffuse (cosine-weighted hemispherical) transmittance
+void roughTransmittanceSlice(int type, float alpha, float eta, int n, float *trans);
+float roughDiffuseTransmittance(int type, float alpha, float eta);
 
 // Film developing (hdrfilm.cpp:481-492, fmtconv.cpp:962-974) and PFM output
 void writePFM(const std::string &path, int w, int h, const std::vector<float> &rgb);

@@ -92,7 +92,8 @@ DEVICE_SYMBOLS = [
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_scene_desc", "mtsh_scene_render_params",
-    "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_last_error",
+    "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
+    "mtsh_last_error",
 ]
 
 

@@ -1440,6 +1440,56 @@ float plasticProbSpecular(const mtsg_bsdf &b, float Fi) {
     return (Fi * b.spec_sampling_weight) / (Fi * b.spec_sampling_weight + (1 - Fi) * (1 - b.spec_sampling_weight));
 }
 
+// evalCubicInterp1D (spline.cpp:23-60) on [0, 1]
+float evalCubicInterp1D(float x, const float *values, size_t size) {
+    if (!(x >= 0.0f && x <= 1.0f)) return 0.0f;
+    float t = (x * (size - 1)) / 1.0f;
+    size_t k = std::max((size_t)0, std::min((size_t)t, size - 2));
+    float f0 = values[k], f1 = values[k + 1], d0, d1;
+    if (k > 0) d0 = 0.5f * (values[k + 1] - values[k - 1]);
+    else d0 = values[k + 1] - values[k];
+    if (k + 2 < size) d1 = 0.5f * (values[k + 2] - values[k]);
+    else d1 = values[k + 1] - values[k];
+    t = t - (float)k;
+    float t2 = t * t, t3 = t2 * t;
+    return (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
+}
+// RoughTransmittance::eval, m_alphaFixed && m_etaFixed (rtrans.h:169-181,205-206)
+float roughTransmittance(const mtsg_bsdf &b, float cosTheta) {
+    float warpedCosTheta = std::pow(std::abs(cosTheta), 0.25f);
+    if (!(cosTheta >= 0)) return 0.0f;
+    float result = evalCubicInterp1D(warpedCosTheta, b.rtrans, MTSG_RTRANS_SAMPLES);
+    return std::min(1.0f, std::max(0.0f, result));
+}
+// RoughPlastic::eval / pdf (roughplastic.cpp:302-385), both components
+Spec roughPlasticEval(const mtsg_bsdf &b, const BRec &r) {
+    if (cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return Spec(0.0f);
+    Microfacet distr = mfOf(b);
+    Spec result(0.0f);
+    Vec H = normalize(r.wo + r.wi);
+    float D = distr.eval(H);
+    float F = fresnelDielectricExt1(dot(r.wi, H), b.ior_eta);
+    float G = distr.G(r.wi, r.wo, H);
+    float value = F * D * G / (4.0f * cosTheta(r.wi));
+    result += Spec::of(b.spec_refl) * value;
+    float T12 = roughTransmittance(b, cosTheta(r.wi)), T21 = roughTransmittance(b, cosTheta(r.wo));
+    result += plasticDiffuse(b) * (kInvPi * cosTheta(r.wo) * T12 * T21 * plasticInvEta2(b));
+    return result;
+}
+float roughPlasticPdf(const mtsg_bsdf &b, const BRec &r) {
+    if (cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return 0.0f;
+    Microfacet distr = mfOf(b);
+    Vec H = normalize(r.wo + r.wi);
+    float probSpecular = 1 - roughTransmittance(b, cosTheta(r.wi));
+    probSpecular = plasticProbSpecular(b, probSpecular);
+    float probDiffuse = 1 - probSpecular;
+    float dwh_dwo = 1.0f / (4.0f * dot(r.wo, H));
+    float prob = distr.pdf(r.wi, H);
+    float result = prob * dwh_dwo * probSpecular;
+    result += probDiffuse * (kInvPi * cosTheta(r.wo));
+    return result;
+}
+
 // BSDF::eval (measure = ESolidAngle for smooth BSDFs; dielectric only
 // evaluates EDiscrete, so it returns 0 here: dielectric.cpp:228-250)
 Spec bsdfEval(const mtsg_bsdf &b, const BRec &r) {
@@ -1490,6 +1540,7 @@ Spec bsdfEval(const mtsg_bsdf &b, const BRec &r) {
         float Fo = fresnelDielectricExt1(cosTheta(r.wo), b.ior_eta);
         return plasticDiffuse(b) * (kInvPi * cosTheta(r.wo) * plasticInvEta2(b) * (1 - Fi) * (1 - Fo));
     }
+    if (b.type == MTSG_BSDF_ROUGHPLASTIC) return roughPlasticEval(b, r);
     return Spec(0.0f);   // dielectric / conductor: delta components only (EDiscrete)
 }
 
@@ -1531,6 +1582,7 @@ float bsdfPdf(const mtsg_bsdf &b, const BRec &r) {
         float Fi = fresnelDielectricExt1(cosTheta(r.wi), b.ior_eta);
         return kInvPi * cosTheta(r.wo) * (1 - plasticProbSpecular(b, Fi));
     }
+    if (b.type == MTSG_BSDF_ROUGHPLASTIC) return roughPlasticPdf(b, r);
     return 0.0f;
 }
 
@@ -1630,6 +1682,32 @@ Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy, Nex
         else weight = weight * std::abs(distr.eval(m) * distr.G(r.wi, r.wo, m) * dot(r.wi, m) / (microfacetPDF * cosTheta(r.wi)));
         pdf *= std::abs(dwh_dwo);
         return weight;
+    }
+    if (b.type == MTSG_BSDF_ROUGHPLASTIC) {   // roughplastic.cpp:387-455
+        if (cosTheta(r.wi) <= 0) return Spec(0.0f);
+        bool choseSpecular = true;
+        float probSpecular = plasticProbSpecular(b, 1 - roughTransmittance(b, cosTheta(r.wi)));
+        if (sy < probSpecular) {
+            sy /= probSpecular;
+        } else {
+            sy = (sy - probSpecular) / (1 - probSpecular);
+            choseSpecular = false;
+        }
+        if (choseSpecular) {
+            Microfacet distr = mfOf(b);
+            float mpdf;
+            Vec m = distr.sample(r.wi, sx, sy, mpdf);
+            r.wo = reflectM(r.wi, m);
+            r.sampledType = EGlossyReflection;
+            if (cosTheta(r.wo) <= 0) return Spec(0.0f);
+        } else {
+            r.sampledType = EDiffuseReflection;
+            r.wo = squareToCosineHemisphere(sx, sy);
+        }
+        r.eta = 1.0f;
+        pdf = roughPlasticPdf(b, r);
+        if (pdf == 0) return Spec(0.0f);
+        return roughPlasticEval(b, r) / pdf;
     }
     if (b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:344-390 (both components)
         if (cosTheta(r.wi) <= 0) return Spec(0.0f);

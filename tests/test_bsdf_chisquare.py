@@ -28,9 +28,10 @@ THETA_BINS, PHI_BINS = 10, 20
 N_SAMPLES = THETA_BINS * PHI_BINS * 1000
 WI_PER_BSDF = 5
 
-DIFFUSE, ROUGHCONDUCTOR, DIELECTRIC, CONDUCTOR, PLASTIC, ROUGHDIELECTRIC = 1, 2, 3, 4, 5, 6
+DIFFUSE, ROUGHCONDUCTOR, DIELECTRIC, CONDUCTOR, PLASTIC, ROUGHDIELECTRIC, ROUGHPLASTIC = 1, 2, 3, 4, 5, 6, 7
 DELTA = 4 | 16   # EDeltaReflection | EDeltaTransmission
 BECKMANN, GGX, PHONG = 0, 1, 2
+RTRANS_SAMPLES = 100   # MTSG_RTRANS_SAMPLES
 
 
 class Bsdf(C.Structure):
@@ -42,7 +43,8 @@ class Bsdf(C.Structure):
                 ("spec_refl", C.c_float * 3), ("spec_trans", C.c_float * 3),
                 ("alpha_u", C.c_float), ("alpha_v", C.c_float),
                 ("ior_eta", C.c_float), ("ior_inv_eta", C.c_float),
-                ("fdr_int", C.c_float), ("spec_sampling_weight", C.c_float)]
+                ("fdr_int", C.c_float), ("spec_sampling_weight", C.c_float),
+                ("rtrans", C.c_float * RTRANS_SAMPLES)]
 
 
 def make_bsdf(kind, dist=GGX, alpha=0.2, visible=1, eta=1.5046, alpha_v=None, nonlinear=0, fdr_int=0.6, spec_weight=0.6):
@@ -62,7 +64,22 @@ def make_bsdf(kind, dist=GGX, alpha=0.2, visible=1, eta=1.5046, alpha_v=None, no
     b.alpha_u = alpha
     b.alpha_v = alpha if alpha_v is None else alpha_v
     b.ior_eta, b.ior_inv_eta = eta, 1.0 / eta
+    if kind == ROUGHPLASTIC:
+        # the host library's RoughTransmittance slice, as the scene loader builds it
+        H = host_lib()
+        diff = C.c_float()
+        assert H.mtsh_rough_transmittance(dist, C.c_float(alpha), C.c_float(eta), RTRANS_SAMPLES, b.rtrans, None) == 0
+        assert H.mtsh_rough_transmittance(dist, C.c_float(alpha), C.c_float(1.0 / eta), RTRANS_SAMPLES,
+                                          (C.c_float * RTRANS_SAMPLES)(), C.byref(diff)) == 0
+        b.fdr_int = 1 - diff.value
     return b
+
+
+def host_lib():
+    import mtsg
+    L = mtsg.host_lib()
+    L.mtsh_rough_transmittance.argtypes = [C.c_int, C.c_float, C.c_float, C.c_int, C.c_void_p, C.c_void_p]
+    return L
 
 
 def _lib():
@@ -205,6 +222,12 @@ CASES = [
     # error the strongly stretched anisotropic incidences make visible)
     ("roughdielectric_aniso", dict(kind=ROUGHDIELECTRIC, dist=BECKMANN, alpha=0.1, alpha_v=0.35, visible=1, eta=1.6)),
     ("roughdielectric_phong", dict(kind=ROUGHDIELECTRIC, dist=PHONG, alpha=0.25, visible=0, eta=1.5)),
+    # rough plastic: microfacet coating + diffuse base, component chosen by
+    # the rough transmittance (test_bsdf.xml holds roughplastic instances)
+    ("roughplastic_beckmann", dict(kind=ROUGHPLASTIC, dist=BECKMANN, alpha=0.1, visible=1, eta=1.49, spec_weight=0.6)),
+    ("roughplastic_ggx_classic", dict(kind=ROUGHPLASTIC, dist=GGX, alpha=0.3, visible=0, eta=1.9, spec_weight=0.3)),
+    ("roughplastic_phong_nonlinear", dict(kind=ROUGHPLASTIC, dist=PHONG, alpha=0.2, visible=0, eta=1.5, nonlinear=1,
+                                          spec_weight=0.5)),
 ]
 BOTH_SIDES = (ROUGHDIELECTRIC,)
 

@@ -244,6 +244,19 @@ def test_smooth_materials_scene_parity():
     g.close()
 
 
+def test_roughplastic_scene_parity():
+    # roughplastic: Beckmann / GGX (visible and classic) / Phong coatings,
+    # nonlinear, twosided front and back; rough transmittance slices and the
+    # sample.y component split (roughplastic.cpp:387-455)
+    scene = mtsg.Scene(os.path.join(SCENES, "cbox_roughplastic.xml"), {"width": 48, "height": 48, "spp": 8})
+    g = mtsg.GPUScene(scene, 0)
+    _, c, gi = render_pair(scene, g)
+    check_render(c, gi)
+    _, c, gi = render_pair(scene, g, max_depth=3, strict_normals=1)
+    check_render(c, gi)
+    g.close()
+
+
 @pytest.mark.parametrize("defs", [dict(dist="ggx", alpha=0.2), dict(dist="beckmann", alpha=0.35, sampleVisible="false")],
                          ids=["ggx-visible", "beckmann-classic"])
 def test_rough_dielectric_parity(defs):
