@@ -2217,7 +2217,9 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             for (uint32_t l = 0; l < nb; ++l) {
                 LaneRun &L = lr[l];
                 // lagged check: if bounce b-1 produced nothing, bounce b was empty
-                if (L.open && b >= 1) {
+                // (also for a lane that launched its last bounce b just now, so
+                // every bounce is booked once: b-1 here, the last one below)
+                if (b >= 1 && L.last == b) {
                     HIP_TRY(hipEventSynchronize(L.cntEv[(b - 1) & 1]));
                     if (account(l, b - 1) == 0) L.open = false;
                 }
