@@ -203,7 +203,7 @@ constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traver
 // large as the frame -- measured on the 1M-triangle scene (Msamples/s):
 // 4M paths 421, 16M 672, 32M 803, 64M 884, 128M 934, whole frame 960.
 constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 28;
-#define MTSG_MAX_LANES 2
+#define MTSG_MAX_LANES 4
 #ifndef MTSG_LANES
 #define MTSG_LANES 1
 #endif
@@ -1887,6 +1887,7 @@ struct mtsg_scene {
     uint32_t capacity = 0;         // paths per batch (per lane)
     uint32_t requestedBatch = 0;   // paths in flight over all lanes
     int lanes = MTSG_LANES;        // concurrent batches (streams) of a render
+    int stagger = 0;               // bounces between the starts of consecutive lanes
     int lanesAlloc = 0;            // lanes with path state allocated
     hipStream_t lstream[MTSG_MAX_LANES] = {};   // lstream[0] == stream
     DevPaths LP[MTSG_MAX_LANES]{};
@@ -2160,6 +2161,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     struct LaneRun {
         DevBatch B;
         int last = -1;
+        int start = 0;
         bool open = false;
         hipEvent_t cntEv[2] = {nullptr, nullptr};
     } lr[MTSG_MAX_LANES];
@@ -2189,20 +2191,26 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             L.B = batches[k0 + l];
             L.last = -1;
             L.open = true;
-            DevPaths &P = s->LP[l];
-            hipStream_t st = s->lstream[l];
-            HIP_TRY(hipMemsetAsync(P.cnt, 0, CNT_WORDS * sizeof(uint32_t), st));
-            timed_launch(s, K_CAMERA, st, [&]() {
-                hipLaunchKernelGGL(k_camera, dim3((L.B.nslots + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, s->cam, I, L.B, P);
-            });
+            // staggered lanes: lane l starts `stagger` bounces after lane
+            // l-1, so its early, full launches overlap the other lanes'
+            // late, tail-bound ones
+            L.start = (int)l * s->stagger;
         }
-        for (int b = 0;; ++b) {
+        for (int gb = 0;; ++gb) {
             bool any = false;
             for (uint32_t l = 0; l < nb; ++l) {
                 LaneRun &L = lr[l];
                 if (!L.open) continue;
+                const int b = gb - L.start;
+                if (b < 0) continue;
                 DevPaths &P = s->LP[l];
                 hipStream_t st = s->lstream[l];
+                if (b == 0) {
+                    HIP_TRY(hipMemsetAsync(P.cnt, 0, CNT_WORDS * sizeof(uint32_t), st));
+                    timed_launch(s, K_CAMERA, st, [&]() {
+                        hipLaunchKernelGGL(k_camera, dim3((L.B.nslots + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, s->cam, I, L.B, P);
+                    });
+                }
                 const int qin = b == 0 ? -1 : (b & 1);
                 const int qout = (b & 1) ^ 1;
                 hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, P.cnt, qout, b & 1);
@@ -2216,6 +2224,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             }
             for (uint32_t l = 0; l < nb; ++l) {
                 LaneRun &L = lr[l];
+                const int b = gb - L.start;
                 // lagged check: if bounce b-1 produced nothing, bounce b was empty
                 // (also for a lane that launched its last bounce b just now, so
                 // every bounce is booked once: b-1 here, the last one below)
@@ -2570,6 +2579,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     s->traceGrid = s->cuCount * perCU;
     s->shadeGrid = s->cuCount * 8 * 256 / SHADE_BLOCK;
     if (const char *l = getenv("MTSG_LANES")) s->lanes = std::max(1, std::min(MTSG_MAX_LANES, atoi(l)));
+    if (const char *g = getenv("MTSG_STAGGER")) s->stagger = std::max(0, std::min(16, atoi(g)));
     s->lstream[0] = s->stream;
     for (int l = 1; l < MTSG_MAX_LANES; ++l)
         if (hipStreamCreateWithFlags(&s->lstream[l], hipStreamNonBlocking) != hipSuccess) { g_err = "stream"; return fail(MTSG_ERR_DEVICE); }

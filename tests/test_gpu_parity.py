@@ -151,6 +151,26 @@ def test_tiling_is_additive(cbox_small, gpu_cbox):
     np.testing.assert_allclose(merged, full, rtol=2e-5, atol=2e-5)
 
 
+def test_staggered_lanes_are_bit_identical(cbox_small):
+    # the multi-lane render path (MTSG_LANES batches on their own streams,
+    # MTSG_STAGGER bounces apart) renders the same samples as one lane
+    import os as _os
+    p = cbox_small.params()
+    b = cbox_small.border
+    g1 = mtsg.GPUScene(cbox_small, 0)
+    ref = g1.render(p, b)
+    g1.close()
+    _os.environ["MTSG_LANES"], _os.environ["MTSG_STAGGER"] = "3", "2"
+    try:
+        g3 = mtsg.GPUScene(cbox_small, 0)
+        g3.set_batch_paths(16 * 16 * 4 * 4)
+        img = g3.render(p, b)
+        g3.close()
+    finally:
+        del _os.environ["MTSG_LANES"], _os.environ["MTSG_STAGGER"]
+    np.testing.assert_allclose(img, ref, rtol=2e-5, atol=2e-5)
+
+
 def test_dielectric_scene_parity():
     # smooth dielectric: delta BSDF, no NEE, MIS weight 1 on emitter hits, eta in RR
     scene = mtsg.Scene(os.path.join(SCENES, "cbox_glass.xml"), {"width": 48, "height": 48, "spp": 8})
