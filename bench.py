@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--batch-paths", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-parity", action="store_true", help="skip the headline parity leg")
+    ap.add_argument("--parity-stride", type=int, default=8,
+                    help="parity leg: compare the 16x16 tiles t %% N == 0 (1/N of the frame) at full spp")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="single process: render only rank 0's tile share of an N-GPU run (scaling rehearsal)")
@@ -108,31 +111,107 @@ def scene_args(a):
     return path, defs
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cgroup_cpus():
+    """CPU quota of this process's cgroup (cpu.max), or None when unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(scene, params, border, target_s):
     """Oracle (faithful C++ restatement, Mitsuba SSE2 flags, SFMT sampler,
     32x32 spiral blocks, one worker per core) timed on a bounded sample of
-    the same frame: all pixels at a reduced spp chosen to take ~target_s."""
+    the same frame: all pixels at a reduced spp chosen to take ~target_s.
+    SURVEY §8(d): all host cores, best of 3 (kdbench.cpp:213-242 style); the
+    box's per-GPU share of 16 cores is timed once beside it."""
     from oracle import pyoracle as O
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))   # the box's CPU share per GPU
     p = params.copy()
     p.spp = 1
     _, st = O.render(scene.desc, p, border, rng=O.RNG_SFMT, threads=cores, fast=True)
     rate1 = st.samples / max(st.seconds, 1e-9)
     spp = int(max(1, min(params.spp, round(target_s * rate1 / (params.tile_w * params.tile_h)))))
     p.spp = spp
-    best = None
-    _, st = O.render(scene.desc, p, border, rng=O.RNG_SFMT, threads=cores, fast=True)
-    best = st.samples / st.seconds
+    runs = []
+    for _ in range(3):
+        _, st = O.render(scene.desc, p, border, rng=O.RNG_SFMT, threads=cores, fast=True)
+        runs.append(st.samples / st.seconds)
+    best = max(runs)
+    r16 = None
+    if cores != 16:
+        _, st16 = O.render(scene.desc, p, border, rng=O.RNG_SFMT, threads=16, fast=True)
+        r16 = st16.samples / st16.seconds
     return {
         "value": round(best / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+        "cpu_model": cpu_model(), "nproc": os.cpu_count(), "cgroup_cpus": cgroup_cpus(),
+        "runs_msamples_s": [round(r / 1e6, 4) for r in runs],
+        "value_16_threads": round(r16 / 1e6, 4) if r16 else round(best / 1e6, 4),
         "sample": f"{params.tile_w}x{params.tile_h}x{spp}spp of the same scene/frame "
-                  f"({st.samples} samples, {st.seconds:.1f} s; oracle/liboracle_fast.so, "
-                  f"-O3 -msse2 -march=nocona -funsafe-math-optimizations, SFMT independent sampler)",
+                  f"({st.samples} samples per run, best of 3 on {cores} threads; oracle/liboracle_fast.so, "
+                  f"-O3 -msse2 -march=nocona -funsafe-math-optimizations, SFMT independent sampler, "
+                  f"32x32 spiral blocks)",
     }
+
+
+def parity_at_headline(scene, gpu, params, border, stride):
+    """Per-pixel L1 of the GPU frame vs the CPU oracle at the full spp: the
+    tile share t % stride == 0 (1/stride of the 16x16 tiles, every pixel of
+    them, all samples) rendered by both in counter mode (identical random
+    numbers per pixel / sample / dimension), developed (sum w L / sum w) and
+    compared on the pixels of those tiles.  Runs after the timed region."""
+    import mtsg
+    from oracle import pyoracle as O
+    p = params.copy()
+    p.tile_stride, p.tile_offset = stride, 0
+    t0 = time.time()
+    img_g = gpu.render(p, border)
+    t_gpu = time.time() - t0
+    t0 = time.time()
+    img_c, st = O.render(scene.desc, p, border, rng=O.RNG_COUNTER)
+    t_cpu = time.time() - t0
+    b = border
+    rgb_g = mtsg.develop(img_g[b:b + p.tile_h, b:b + p.tile_w])
+    rgb_c = mtsg.develop(img_c[b:b + p.tile_h, b:b + p.tile_w])
+    ty, tx = np.meshgrid(np.arange(p.tile_h) // 16, np.arange(p.tile_w) // 16, indexing="ij")
+    tiles_x = (p.tile_w + 15) // 16
+    own = ((ty * tiles_x + tx) % stride) == 0
+    d = np.abs(rgb_g - rgb_c)[own]
+    l1 = float(d.mean())
+    mean = float(rgb_c[own].mean())
+    return {"l1": l1, "mean": round(mean, 6), "l1_rel_mean": l1 / max(mean, 1e-12),
+            "max_abs": float(d.max()), "pixels": int(own.sum()), "spp": int(p.spp),
+            "samples": int(st.samples), "tiles": f"16x16 tiles t % {stride} == 0 of {p.tile_w}x{p.tile_h}",
+            "bar": "l1 < 1e-3 (and l1_rel_mean < 1e-3)", "pass": bool(l1 < 1e-3 and l1 < 1e-3 * max(mean, 1e-12)),
+            "rng": "counter mode on both sides", "oracle_seconds": round(t_cpu, 1), "gpu_seconds": round(t_gpu, 2)}
+
+
+def pmc_tcc(workload):
+    """L2 hit rate of the traversal kernel from the newest committed
+    TCC_HIT/TCC_MISS pass (profiles/rNN_tcc.json), if any."""
+    import glob
+    for f in reversed(sorted(glob.glob(os.path.join(REPO, "profiles", "r*_tcc.json")))):
+        try:
+            j = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if j.get("workload") == workload and j.get("kernel") == TRAFFIC_KERNEL:
+            return j, os.path.relpath(f, REPO)
+    return None, None
 
 
 def main():
@@ -206,33 +285,46 @@ def main():
         per = lambda v, n: v / max(1, n)  # noqa: E731
         nodes_c, tests_c = per(cs.nodes_visited, cs.rays_closest), per(cs.tri_tests, cs.rays_closest)
         nodes_s, tests_s = per(cs.shadow_nodes_visited, cs.rays_shadow), per(cs.shadow_tri_tests, cs.rays_shadow)
-        # Algorithmic bytes per ray in the device layout (DESIGN.md "Roofline"):
-        # 16 B of node pair per inner node descended, one 48-B TriAccel record
-        # per primitive test (leaf-ordered, no index indirection), the 32-B ray
-        # record in, and 16 B out (closest: the hit record; shadow: the 16-B
-        # contribution record read when unoccluded, counted for every ray).
-        b_c = 16 * nodes_c + 48 * tests_c + 48
-        b_s = 16 * nodes_s + 48 * tests_s + 48
+        # SURVEY §8(d) algorithmic bytes per ray: 8 B per KDNode visited, 4 B
+        # per leaf reference, 48 B per TriAccel test (gkdtree.h:452-480,
+        # triaccel.h:37-51), counted by the instrumented pass.  The device
+        # layout's own bytes (16 B node pairs, leaf-ordered 48-B records, no
+        # index indirection, plus 48 B of ray I/O) are reported beside it.
+        refs_c, refs_s = per(cs.leaf_refs, cs.rays_closest), per(cs.shadow_leaf_refs, cs.rays_shadow)
+        b_c = 8 * nodes_c + 4 * refs_c + 48 * tests_c
+        b_s = 8 * nodes_s + 4 * refs_s + 48 * tests_s
+        d_c = 16 * nodes_c + 48 * tests_c + 48
+        d_s = 16 * nodes_s + 48 * tests_s + 48
         launches = max(1, acc["launches_trace_closest"] + acc["launches_trace_shadow"])
         trace_s = (acc["ms_trace_closest"] + acc["ms_trace_shadow"]) / 1e3
-        bytes_total = b_c * acc["rays_closest"] + b_s * acc["rays_shadow"]
-        bytes_per_launch = bytes_total / launches
+        bytes_per_launch = (b_c * acc["rays_closest"] + b_s * acc["rays_shadow"]) / launches
+        dev_bytes_per_launch = (d_c * acc["rays_closest"] + d_s * acc["rays_shadow"]) / launches
         avg_launch_s = trace_s / launches
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        dev_achieved = dev_bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         tj, tsrc = pmc_traffic(a.workload)
         traffic = None
         if (tj and avg_launch_s > 0 and a.workload == "bunny15" and params.spp == 256 and world == 1
                 and a.emulate_ranks <= 1):
             traffic = round(tj["traffic_bytes_per_launch"] / avg_launch_s / 1e9, 1)
+        hj, hsrc = pmc_tcc(a.workload)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_frac": round(traffic / HBM_PEAK_GBS, 4) if traffic else None,
                     "traffic_source": (f"{tsrc}: FETCH_SIZE x2 + WRITE_SIZE per launch "
-                                       f"({tj['traffic_bytes_per_launch'] / 1e9:.2f} GB) / this run's avg launch time"
+                                       f"({tj['traffic_bytes_per_launch'] / 1e9:.2f} GB) / this run's avg launch time; "
+                                       "memory-side requests, Infinity-Cache hits included"
                                        if traffic is not None else None),
+                    "tcc_hit_rate": hj["tcc_hit_rate"] if hj else None,
+                    "tcc_source": hsrc,
                     "kernel": "k_trace_s (closest + shadow rays)",
+                    "bytes_model": "SURVEY 8(d): 8 B/KDNode + 4 B/leaf ref + 48 B/TriAccel test",
                     "algorithmic_bytes_per_launch": round(bytes_per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                     "launches_per_frame": launches // a.steps,
                     "bytes_per_closest_ray": round(b_c, 1), "bytes_per_shadow_ray": round(b_s, 1),
+                    "device_layout": {"achieved": round(dev_achieved, 1), "frac": round(dev_achieved / HBM_PEAK_GBS, 4),
+                                      "bytes_per_closest_ray": round(d_c, 1), "bytes_per_shadow_ray": round(d_s, 1),
+                                      "model": "16 B node pair per inner node + 48 B leaf-ordered TriAccel per test + 48 B ray I/O"},
                     "nodes_per_closest_ray": round(nodes_c, 2), "tests_per_closest_ray": round(tests_c, 2),
                     "nodes_per_shadow_ray": round(nodes_s, 2), "tests_per_shadow_ray": round(tests_s, 2),
                     # SIMD efficiency of the traversal waves (instrumented pass)
@@ -243,6 +335,9 @@ def main():
             img = mtsg.develop(host_block[border:H - border, border:W - border])
             np.save(a.save, img)
 
+    parity = None
+    if rank == 0 and world == 1 and not a.no_parity and a.emulate_ranks <= 1:
+        parity = parity_at_headline(scene, gpu, params, border, a.parity_stride)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(scene, params, border, a.cpu_seconds)
@@ -255,7 +350,7 @@ def main():
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": {"bunny15": "C3 instanced bunny x15 (1,041,765 tris), roughconductor Cu GGX 0.2",
+            "config": {"workload": {"bunny15": "C3 bunny x15, 15 instances flattened to 1,041,765 world-space triangles, roughconductor Cu GGX 0.2",
                                     "cbox": "C2 Cornell box, diffuse + area emitter",
                                     "c5": "C5 dielectric + roughconductor bunnies, HDR envmap, maxDepth 64"}[a.workload],
                        "resolution": f"{params.tile_w}x{params.tile_h}", "spp": params.spp,
@@ -266,7 +361,7 @@ def main():
             **({"emulated_ranks": a.emulate_ranks,
                 "note": "one GPU rendering rank 0's 1/N tile share; value = frame samples / that time"}
                if a.emulate_ranks > 1 and world == 1 else {}),
-            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "kernels": kernels,
         }
         print(json.dumps(out))
     if pg is not None:

@@ -361,7 +361,11 @@ int  mtsg_device_free(mtsg_scene *scene, void *ptr);
 int  mtsg_device_memset(mtsg_scene *scene, void *ptr, size_t bytes);
 int  mtsg_device_to_host(mtsg_scene *scene, void *dst, const void *src, size_t bytes);
 
-/* Cancel a running render on this handle (async-safe flag). */
+/* Cancel the render running on this handle (async-safe flag, checked
+ * between bounces; SamplingIntegrator::cancel, integrator.cpp:94-97): it
+ * returns MTSG_ERR_CANCELLED once the lanes have drained.  The flag is
+ * consumed when a render returns; set while no render runs, it cancels the
+ * next one. */
 void mtsg_cancel(mtsg_scene *scene);
 
 int  mtsg_set_flags(mtsg_scene *scene, uint32_t flags);

@@ -1,15 +1,24 @@
 /*
- * mtsg_path.h -- the `path` integrator's render() on N GPUs (libmtsg_path.so).
+ * mtsg_path.h -- the `path` integrator's preprocess() / render() / cancel()
+ * on N GPUs (libmtsg_path.so).
  *
  * Replaces SamplingIntegrator::render (reference src/librender/integrator.cpp:99-133)
  * together with BlockedRenderProcess (src/librender/renderproc.cpp:26-186):
  * instead of 32x32 blocks handed to CPU workers, the film's 16x16 tiles are
  * dealt round-robin to one host thread per GPU (tile t -> GPU t % N), each
- * GPU renders its tiles into an ImageBlock of the full film plus filter
+ * GPU renders its tiles into an ImageBlock of the full rectangle plus filter
  * border, and the blocks are merged by addition as ImageBlock::put(const
  * ImageBlock *) does (include/mitsuba/render/imageblock.h:103-107).  No
  * collectives; the RNG is keyed by (pixel, sample), so the image does not
  * depend on N.
+ *
+ * A job mirrors the integrator object's life cycle:
+ *   mtsh_path_job_create   Integrator::preprocess (integrator.h:61-63):
+ *                          the scene is uploaded to every GPU once
+ *   mtsh_path_job_render   SamplingIntegrator::render (integrator.cpp:99-133)
+ *   mtsh_path_job_cancel   SamplingIntegrator::cancel (integrator.cpp:94-97):
+ *                          async-safe, from any thread; the running render
+ *                          returns MTSG_ERR_CANCELLED (render() == false)
  */
 #ifndef MTSG_PATH_H
 #define MTSG_PATH_H
@@ -20,12 +29,37 @@
 extern "C" {
 #endif
 
-/* Render params->tile_* of `scene` with n_gpus devices (<= 0: all visible)
- * into rgbaw_out ((tile_h + 2b) x (tile_w + 2b) x 5 floats, b = border).
- * seconds_out (optional) receives the render time, upload excluded
- * (renderjob.cpp:102).  Returns an mtsg error code. */
+typedef struct mtsh_path_job mtsh_path_job;
+
+/* Upload `scene` to n_gpus devices (<= 0: all visible gfx950 devices).
+ * The host scene may be freed once this call returns. */
+int mtsh_path_job_create(const mtsh_scene *scene, int n_gpus, mtsh_path_job **out);
+
+/* Number of GPUs of the job. */
+int mtsh_path_job_gpus(const mtsh_path_job *job);
+
+/* Render params->tile_* into rgbaw_out ((tile_h + 2b) x (tile_w + 2b) x 5
+ * floats, b = border).  The rectangle's 16x16 tiles selected by
+ * params->tile_stride / tile_offset (all tiles when stride <= 1) are dealt
+ * over the job's N GPUs: GPU g renders tiles offset + (g + k N) stride.
+ * seconds_out (optional) receives the render time.  Blocking; returns an mtsg
+ * error code (MTSG_ERR_CANCELLED after mtsh_path_job_cancel). */
+int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, float *rgbaw_out,
+                         double *seconds_out);
+
+/* Cancel the job's running render (async-safe; no effect when idle). */
+void mtsh_path_job_cancel(mtsh_path_job *job);
+
+void mtsh_path_job_destroy(mtsh_path_job *job);
+
+/* One-shot: create a job, render, destroy.  seconds_out excludes the upload
+ * (renderjob.cpp:102). */
 int mtsh_path_render(const mtsh_scene *scene, const mtsg_render_params *params, int n_gpus,
                      float *rgbaw_out, double *seconds_out);
+
+/* Last error of this library on the calling thread: names the GPU whose
+ * render failed and carries the device error of that worker thread. */
+void mtsh_path_last_error(char *buf, size_t size);
 
 #ifdef __cplusplus
 }

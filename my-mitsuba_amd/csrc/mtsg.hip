@@ -2139,7 +2139,8 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
         HIP_TRY(hipMalloc((void **)&s->waveTimes, (size_t)WT_WORDS * s->traceGrid * WT_MAX_LAUNCHES * sizeof(unsigned long long)));
     s->evUsed = 0;
     s->timed.clear();
-    s->cancel.store(0);
+    // the cancel flag is consumed (cleared) when a render returns, so a
+    // cancel that races with the start of a render is not lost
     if (count) HIP_TRY(hipMemsetAsync(s->LP[0].ctr, 0, CTR_WORDS * sizeof(unsigned long long), s->stream));
     // the batches of this call, tile-major
     std::vector<DevBatch> batches;
@@ -2169,6 +2170,17 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     for (uint32_t l = 0; l < nl && result == MTSG_OK; ++l)
         for (int k = 0; k < 2; ++k)
             if (hipEventCreateWithFlags(&lr[l].cntEv[k], hipEventDisableTiming) != hipSuccess) { g_err = "event"; result = MTSG_ERR_DEVICE; }
+    // work the caller queued on s->stream (the film memset of mtsg_render)
+    // precedes every lane's first kernel
+    hipEvent_t startEv = nullptr;
+    if (result == MTSG_OK && nl > 1) {
+        if (hipEventCreateWithFlags(&startEv, hipEventDisableTiming) != hipSuccess || hipEventRecord(startEv, s->stream) != hipSuccess) {
+            g_err = "event";
+            result = MTSG_ERR_DEVICE;
+        }
+        for (uint32_t l = 1; l < nl && result == MTSG_OK; ++l)
+            if (hipStreamWaitEvent(s->lstream[l], startEv, 0) != hipSuccess) { g_err = "stream wait"; result = MTSG_ERR_DEVICE; }
+    }
     const int maxBounces = p->max_depth > 0 ? p->max_depth : 1 << 30;
     // bounce b of a lane: one trace launch over this bounce's closest rays
     // (work list qin(b), identity for b = 0) and bounce b-1's shadow rays
@@ -2183,8 +2195,11 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
         s->stats.launches_trace_closest++;
         return hc[((bb & 1) ^ 1) ? CNT_Q1 : CNT_Q0];
     };
-    for (size_t k0 = 0; k0 < batches.size() && result == MTSG_OK; k0 += nl) {
-        if (s->cancel.load()) { result = MTSG_ERR_CANCELLED; g_err = "cancelled"; break; }
+    // every error inside the batch loop returns from `run`; the lanes are then
+    // drained and the per-render events destroyed below, whatever happened
+    auto run = [&]() -> int {
+    for (size_t k0 = 0; k0 < batches.size(); k0 += nl) {
+        if (s->cancel.load()) { g_err = "cancelled"; return MTSG_ERR_CANCELLED; }
         const uint32_t nb = (uint32_t)std::min<size_t>(nl, batches.size() - k0);
         for (uint32_t l = 0; l < nb; ++l) {
             LaneRun &L = lr[l];
@@ -2197,6 +2212,8 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             L.start = (int)l * s->stagger;
         }
         for (int gb = 0;; ++gb) {
+            // cancel() between bounces (the whole frame is usually one batch)
+            if (s->cancel.load()) { g_err = "cancelled"; return MTSG_ERR_CANCELLED; }
             bool any = false;
             for (uint32_t l = 0; l < nb; ++l) {
                 LaneRun &L = lr[l];
@@ -2268,7 +2285,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             if (hostCnt(l, L.last)[CNT_ERR]) {
                 g_err = "Lookup dimension exceeds the prime number table size! "
                         "You may have to reduce the 'maxDepth' parameter of your integrator.";
-                result = MTSG_ERR_INVALID;
+                return MTSG_ERR_INVALID;
             }
         }
         if (s->dumpL) {
@@ -2288,6 +2305,11 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             }
         }
     }
+    return MTSG_OK;
+    };
+    if (result == MTSG_OK) result = run();
+    // drain every lane (also after an error or a cancel: the caller may free
+    // the film as soon as this returns) and release the per-render events
     hipError_t e = hipSuccess;
     for (uint32_t l = 0; l < nl; ++l) {
         const hipError_t el = hipStreamSynchronize(s->lstream[l]);
@@ -2295,6 +2317,8 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
         for (int k = 0; k < 2; ++k)
             if (lr[l].cntEv[k]) hipEventDestroy(lr[l].cntEv[k]);
     }
+    if (startEv) hipEventDestroy(startEv);
+    s->cancel.store(0);
     if (e != hipSuccess) { g_err = std::string("render: ") + hipGetErrorString(e); return MTSG_ERR_DEVICE; }
     e = hipGetLastError();
     if (e != hipSuccess) { g_err = std::string("kernel launch: ") + hipGetErrorString(e); return MTSG_ERR_DEVICE; }

@@ -9,6 +9,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -17,47 +18,141 @@
 #include "../../include/mtsh.h"
 #include "../../include/mtsg_path.h"
 
+namespace {
+thread_local std::string g_perr;
+
+std::string device_error() {
+    char buf[1024];
+    mtsg_last_error(buf, sizeof(buf));
+    return buf;
+}
+}  // namespace
+
+struct mtsh_path_job {
+    std::vector<mtsg_scene *> handles;
+    int border = 0;
+    // cancel(): the job's flag is checked by each worker before its render
+    // starts; the handles' flags stop renders already running (per bounce)
+    std::atomic<int> cancel{0};
+    std::vector<std::atomic<int>> rendering;   // per GPU: its mtsg_render is running
+    std::mutex renderLock;   // one render at a time per job
+    explicit mtsh_path_job(int n) : rendering(n) {}
+};
+
 extern "C" {
 
-// Render the whole film of `scene` with `n_gpus` devices into rgbaw_out
-// ((film_h + 2b) x (film_w + 2b) x 5 floats).  Returns an mtsg error code.
-int mtsh_path_render(const mtsh_scene *scene, const mtsg_render_params *params, int n_gpus, float *rgbaw_out,
-                     double *seconds_out) {
+int mtsh_path_job_create(const mtsh_scene *scene, int n_gpus, mtsh_path_job **out) {
+    if (!scene || !out) { g_perr = "null argument"; return MTSG_ERR_INVALID; }
+    *out = nullptr;
+    const int avail = mtsg_device_count();
+    if (n_gpus <= 0) n_gpus = avail;
+    if (n_gpus > avail || n_gpus <= 0) {
+        g_perr = "requested " + std::to_string(n_gpus) + " GPU(s), " + std::to_string(avail) + " gfx950 device(s) visible";
+        return MTSG_ERR_NODEVICE;
+    }
     const mtsg_scene_desc *desc = mtsh_scene_desc(scene);
     mtsh_scene_info info;
     mtsh_scene_get_info(scene, &info);
-    const int b = info.border;
-    const size_t W = (size_t)params->tile_w + 2 * b, H = (size_t)params->tile_h + 2 * b;
-    const int avail = mtsg_device_count();
-    if (n_gpus <= 0) n_gpus = avail;
-    if (n_gpus > avail || n_gpus <= 0) return MTSG_ERR_NODEVICE;
-    std::vector<std::vector<float>> blocks(n_gpus, std::vector<float>(W * H * 5));
-    std::vector<int> rcs(n_gpus, MTSG_OK);
-    std::vector<mtsg_scene *> handles(n_gpus, nullptr);
+    auto *job = new mtsh_path_job(n_gpus);
+    job->border = info.border;
+    job->handles.assign(n_gpus, nullptr);
     // upload (preprocessing; excluded from the render time like renderjob.cpp:102)
-    for (int g = 0; g < n_gpus; ++g)
-        if ((rcs[g] = mtsg_scene_create(desc, g, &handles[g])) != MTSG_OK) {
-            for (auto *h : handles) mtsg_scene_destroy(h);
-            return rcs[g];
+    for (int g = 0; g < n_gpus; ++g) {
+        const int rc = mtsg_scene_create(desc, g, &job->handles[g]);
+        if (rc != MTSG_OK) {
+            g_perr = "GPU " + std::to_string(g) + ": " + device_error();
+            mtsh_path_job_destroy(job);
+            return rc;
         }
+    }
+    *out = job;
+    return MTSG_OK;
+}
+
+int mtsh_path_job_gpus(const mtsh_path_job *job) { return job ? (int)job->handles.size() : 0; }
+
+int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, float *rgbaw_out,
+                         double *seconds_out) {
+    if (!job || !params || !rgbaw_out) { g_perr = "null argument"; return MTSG_ERR_INVALID; }
+    std::lock_guard<std::mutex> lock(job->renderLock);
+    const int n = (int)job->handles.size();
+    const int b = job->border;
+    if (params->tile_w <= 0 || params->tile_h <= 0) { g_perr = "tile rectangle outside the film"; return MTSG_ERR_INVALID; }
+    if (params->tile_stride < 0 || (params->tile_stride > 1 && (params->tile_offset < 0 || params->tile_offset >= params->tile_stride))) {
+        g_perr = "invalid tile_stride / tile_offset";
+        return MTSG_ERR_INVALID;
+    }
+    const size_t W = (size_t)params->tile_w + 2 * b, H = (size_t)params->tile_h + 2 * b;
+    // compose the caller's tile subset with the deal over GPUs: of the
+    // caller's tiles off + k * S, GPU g takes every n-th one
+    const int S = params->tile_stride > 1 ? params->tile_stride : 1;
+    const int off = params->tile_stride > 1 ? params->tile_offset : 0;
+    std::vector<std::vector<float>> blocks(n, std::vector<float>(W * H * 5));
+    std::vector<int> rcs(n, MTSG_OK);
+    std::vector<std::string> errs(n);
+    job->cancel.store(0);   // a cancel() while idle has no effect
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> threads;
-    for (int g = 0; g < n_gpus; ++g)
+    for (int g = 0; g < n; ++g)
         threads.emplace_back([&, g]() {
             mtsg_render_params p = *params;
-            p.tile_stride = n_gpus;
-            p.tile_offset = g;
-            rcs[g] = mtsg_render(handles[g], &p, blocks[g].data());
+            p.tile_stride = S * n;
+            p.tile_offset = p.tile_stride > 1 ? off + g * S : 0;
+            job->rendering[g].store(1);
+            if (job->cancel.load()) rcs[g] = MTSG_ERR_CANCELLED;
+            else rcs[g] = mtsg_render(job->handles[g], &p, blocks[g].data());
+            job->rendering[g].store(0);
+            // the device library's error is thread-local: capture it here
+            if (rcs[g] != MTSG_OK) errs[g] = device_error();
         });
     for (auto &t : threads) t.join();
-    std::memset(rgbaw_out, 0, W * H * 5 * sizeof(float));
-    for (int g = 0; g < n_gpus; ++g)
-        for (size_t i = 0; i < W * H * 5; ++i) rgbaw_out[i] += blocks[g][i];
     if (seconds_out) *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    for (auto *h : handles) mtsg_scene_destroy(h);
-    for (int rc : rcs)
-        if (rc != MTSG_OK) return rc;
+    const bool cancelled = job->cancel.exchange(0) != 0;
+    for (int g = 0; g < n; ++g)
+        if (rcs[g] != MTSG_OK && rcs[g] != MTSG_ERR_CANCELLED) {
+            g_perr = "GPU " + std::to_string(g) + ": " + errs[g];
+            return rcs[g];
+        }
+    for (int g = 0; g < n; ++g)
+        if (rcs[g] == MTSG_ERR_CANCELLED || cancelled) {
+            g_perr = "cancelled";
+            return MTSG_ERR_CANCELLED;
+        }
+    std::memset(rgbaw_out, 0, W * H * 5 * sizeof(float));
+    for (int g = 0; g < n; ++g)
+        for (size_t i = 0; i < W * H * 5; ++i) rgbaw_out[i] += blocks[g][i];
     return MTSG_OK;
+}
+
+void mtsh_path_job_cancel(mtsh_path_job *job) {
+    if (!job) return;
+    job->cancel.store(1);
+    // only renders still running are told: a handle's flag set after its
+    // render returned would cancel the job's next render
+    for (size_t g = 0; g < job->handles.size(); ++g)
+        if (job->rendering[g].load()) mtsg_cancel(job->handles[g]);
+}
+
+void mtsh_path_job_destroy(mtsh_path_job *job) {
+    if (!job) return;
+    for (auto *h : job->handles) mtsg_scene_destroy(h);
+    delete job;
+}
+
+int mtsh_path_render(const mtsh_scene *scene, const mtsg_render_params *params, int n_gpus, float *rgbaw_out,
+                     double *seconds_out) {
+    mtsh_path_job *job = nullptr;
+    int rc = mtsh_path_job_create(scene, n_gpus, &job);
+    if (rc != MTSG_OK) return rc;
+    rc = mtsh_path_job_render(job, params, rgbaw_out, seconds_out);
+    mtsh_path_job_destroy(job);
+    return rc;
+}
+
+void mtsh_path_last_error(char *buf, size_t size) {
+    if (!buf || !size) return;
+    strncpy(buf, g_perr.c_str(), size - 1);
+    buf[size - 1] = 0;
 }
 
 }  // extern "C"

@@ -95,6 +95,33 @@ HOST_SYMBOLS = [
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
     "mtsh_last_error",
 ]
+PATH_SYMBOLS = [
+    "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
+    "mtsh_path_job_destroy", "mtsh_path_render", "mtsh_path_last_error",
+]
+_path = None
+
+
+def path_lib() -> C.CDLL:
+    """libmtsg_path.so: the multi-GPU render() / cancel() (include/mtsg_path.h)."""
+    global _path
+    if _path is None:
+        device_lib()   # raises when the HIP library is missing
+        path = os.path.join(PKG_DIR, "libmtsg_path.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: run `make` (or __graft_entry__.build())")
+        lib = C.CDLL(path)
+        lib.mtsh_path_job_create.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+        lib.mtsh_path_job_gpus.argtypes = [C.c_void_p]
+        lib.mtsh_path_job_render.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p,
+                                             C.POINTER(C.c_double)]
+        lib.mtsh_path_job_cancel.argtypes = [C.c_void_p]
+        lib.mtsh_path_job_destroy.argtypes = [C.c_void_p]
+        lib.mtsh_path_render.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p,
+                                         C.POINTER(C.c_double)]
+        lib.mtsh_path_last_error.argtypes = [C.c_char_p, C.c_size_t]
+        _path = lib
+    return _path
 
 
 def host_lib() -> C.CDLL:
@@ -310,6 +337,9 @@ class GPUScene:
         self._check(device_lib().mtsg_device_to_host(self._h, _ptr(out), film, out.nbytes), "mtsg_device_to_host")
         return out
 
+    def cancel(self) -> None:
+        device_lib().mtsg_cancel(self._h)
+
     def close(self):
         if getattr(self, "_h", None):
             device_lib().mtsg_scene_destroy(self._h)
@@ -317,3 +347,42 @@ class GPUScene:
 
     def __del__(self):
         self.close()
+
+
+class PathJob:
+    """The `path` integrator's preprocess() / render() / cancel() over N GPUs
+    (include/mtsg_path.h; SamplingIntegrator::render, integrator.cpp:99-133)."""
+
+    def __init__(self, scene: Scene, n_gpus: int = 0):
+        lib = path_lib()
+        h = C.c_void_p()
+        rc = lib.mtsh_path_job_create(C.c_void_p(scene._h), n_gpus, C.byref(h))
+        if rc != MTSG_OK:
+            raise RuntimeError(f"mtsh_path_job_create failed ({rc}): " + _err(lib, "mtsh_path_last_error"))
+        self._h = h
+        self.scene = scene
+        self.gpus = lib.mtsh_path_job_gpus(h)
+
+    def render(self, params: RenderParams, border: int) -> tuple[int, np.ndarray, float]:
+        """Returns (error code, ImageBlock of the rectangle + border, seconds)."""
+        out = np.zeros((params.tile_h + 2 * border, params.tile_w + 2 * border, 5), dtype=np.float32)
+        secs = C.c_double(0.0)
+        rc = path_lib().mtsh_path_job_render(self._h, C.byref(params), _ptr(out), C.byref(secs))
+        return rc, out, secs.value
+
+    def last_error(self) -> str:
+        return _err(path_lib(), "mtsh_path_last_error")
+
+    def cancel(self) -> None:
+        path_lib().mtsh_path_job_cancel(self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            path_lib().mtsh_path_job_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+MTSG_ERR_CANCELLED = -4

@@ -18,13 +18,16 @@ def pytest_configure(config):
 
 
 def _ensure_built():
+    """Every library the tests load must match its sources: `make -q` checks
+    the in-tree .so files against csrc/, host/ and oracle/ (a no-op when they
+    are current) and anything stale is rebuilt here, loudly, before any test
+    runs -- a prebuilt library that no longer matches the sources is never
+    tested silently."""
     import subprocess
-    need = [os.path.join(REPO, p) for p in ("my-mitsuba_amd/libmtsg_host.so", "oracle/liboracle.so",
-                                             "oracle/liboracle_fast.so")]
-    if not all(os.path.exists(p) for p in need):
-        subprocess.check_call(["make", "-C", REPO, "-j4", "host", "oracle"])
-    if not os.path.exists(os.path.join(REPO, "scenes", "sky512.pfm")):
-        subprocess.check_call(["make", "-C", REPO, "scenes/sky512.pfm"])
+    targets = ["host", "device", "oracle", "my-mitsuba_amd/libmtsg_path.so", "scenes/sky512.pfm"]
+    if subprocess.call(["make", "-C", REPO, "-q"] + targets, stdout=subprocess.DEVNULL) != 0:
+        print(f"conftest: rebuilding stale native libraries ({' '.join(targets)})", flush=True)
+        subprocess.check_call(["make", "-C", REPO, "-j8"] + targets)
 
 
 _ensure_built()

@@ -287,3 +287,16 @@ def test_rough_dielectric_parity(defs):
     _, c, gi = render_pair(scene, g)
     check_render(c, gi)
     g.close()
+
+
+def test_c3_full_frame_parity():
+    # the headline frame (C3: 15 bunnies, 1,041,765 triangles, roughconductor,
+    # 1280x720, maxDepth 8) at 2 spp through the production render entry,
+    # every pixel against the oracle (counter-mode RNG => identical samples)
+    scene = mtsg.Scene(os.path.join(SCENES, "bunny15.xml"), {"width": 1280, "height": 720, "spp": 2})
+    g = mtsg.GPUScene(scene, 0)
+    p, c, gi = render_pair(scene, g)
+    g.close()
+    assert (p.tile_w, p.tile_h, p.max_depth) == (1280, 720, 8)
+    l1, mean = check_render(c, gi)
+    print(f"C3 1280x720x2spp: per-pixel L1 {l1:.3e}, mean {mean:.4f}, L1/mean {l1 / mean:.2e}")
