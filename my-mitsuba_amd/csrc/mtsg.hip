@@ -1776,6 +1776,13 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
     const bool inside = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
     // block (tile rect + border) bounds relative to the window origin (x - R, y - R)
     const int bx0 = (B.rect_x - bord) - (x - R), by0 = (B.rect_y - bord) - (y - R);
+    // Mitsuba computes a sample's filter offsets relative to the origin of the
+    // 32x32 render block that holds its pixel (ImageBlock::put,
+    // imageblock.h:158-160; blocks of BlockedImageProcess, imageproc.cpp:28-78,
+    // scene.cpp:27), and `pos - 0.5 - origin` can round when it crosses a power
+    // of two: the same origin is used here so the weights are bit-identical
+    const int mbx = B.rect_x + ((x - B.rect_x) & ~31) - bord, mby = B.rect_y + ((y - B.rect_y) & ~31) - bord;
+    const int wxo = (x - R) - mbx, wyo = (y - R) - mby;   // window origin in that block
     float win[K][K][CH];
 #pragma unroll
     for (int r = 0; r < K; ++r)
@@ -1792,17 +1799,17 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
             camera_jitter(I, x, y, B.s0 + sl, ja, jb);
             // invalid samples are rejected (imageblock.h:147-151)
             if (!(isfinite(L.x) && isfinite(L.y) && isfinite(L.z) && L.x >= 0 && L.y >= 0 && L.z >= 0)) continue;
-            // sample position relative to the window origin, as ImageBlock::put
-            // computes it relative to the block origin (imageblock.h:158-160)
-            const float px = ((float)x + ja) - 0.5f - (float)(x - R);
-            const float py = ((float)y + jb) - 0.5f - (float)(y - R);
+            // sample position relative to the Mitsuba block origin
+            // (imageblock.h:158-160)
+            const float px = ((float)x + ja) - 0.5f - (float)mbx;
+            const float py = ((float)y + jb) - 0.5f - (float)mby;
             float wx[K], wy[K];
 #pragma unroll
             for (int c = 0; c < K; ++c) {
                 const bool okx = c >= bx0 && c < bx0 + blockW;
                 const bool oky = c >= by0 && c < by0 + blockH;
-                wx[c] = okx ? C.filter_values[min((int)fabsf(((float)c - px) * C.filter_scale), 31)] : 0.0f;
-                wy[c] = oky ? C.filter_values[min((int)fabsf(((float)c - py) * C.filter_scale), 31)] : 0.0f;
+                wx[c] = okx ? C.filter_values[min((int)fabsf(((float)(wxo + c) - px) * C.filter_scale), 31)] : 0.0f;
+                wy[c] = oky ? C.filter_values[min((int)fabsf(((float)(wyo + c) - py) * C.filter_scale), 31)] : 0.0f;
             }
             const float v[5] = {L.x, L.y, L.z, L.w, 1.0f};
 #pragma unroll
