@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MTSG_ABI_VERSION 5
+#define MTSG_ABI_VERSION 6
 
 /* ---- error codes (mtsg_last_error() gives the message) ------------------ */
 enum {
@@ -78,7 +78,10 @@ typedef struct mtsg_rect {
     uint32_t shape_index;
 } mtsg_rect;
 
-enum { MTSG_SHAPE_MESH = 0, MTSG_SHAPE_RECT = 1 };
+/* MTSG_SHAPE_INSTANCE: a two-level `instance` of a `shapegroup`
+ * (src/shapes/instance.cpp:107-160); its TriAccel record in the top-level
+ * tree has k == MTSG_TRIACCEL_SHAPE and prim_index == the instance index. */
+enum { MTSG_SHAPE_MESH = 0, MTSG_SHAPE_RECT = 1, MTSG_SHAPE_INSTANCE = 2 };
 
 typedef struct mtsg_shape {
     int32_t type;          /* MTSG_SHAPE_*                                 */
@@ -88,8 +91,34 @@ typedef struct mtsg_shape {
     uint32_t tri_begin;    /* mesh: first global triangle                  */
     uint32_t tri_count;
     uint32_t rect;         /* rectangle index                              */
-    uint32_t pad;
+    uint32_t instance;     /* instance index (MTSG_SHAPE_INSTANCE)         */
 } mtsg_shape;
+
+/* Two-level instancing (src/shapes/instance.cpp:115-160,
+ * src/shapes/shapegroup.cpp:94-101).  A shape group owns a kd-tree over its
+ * own triangles, in group space: its nodes are group_nodes[node_offset ..],
+ * KDNode offsets relative to that root, and its leaves reference
+ * group_indices[index_offset ..], which index the scene's `triaccel` array
+ * (the group triangles' TriAccel records, built from group-space vertices;
+ * the top-level tree never references them).  Instance::rayIntersect
+ * transforms the ray by to_local (Transform::inverse(); the direction is not
+ * renormalized, so t is preserved) and traverses the group tree;
+ * fillIntersectionRecord maps p, dpdu and the normals back with to_world
+ * (normals by the inverse transpose, i.e. to_local transposed). */
+typedef struct mtsg_instance {
+    float to_world[12];    /* row-major 3x4 of the instance's toWorld       */
+    float to_local[12];    /* row-major 3x4 of its inverse                  */
+    uint32_t group;        /* index into groups                             */
+    uint32_t shape_index;  /* the instance's entry in shapes                */
+    uint32_t pad[2];
+} mtsg_instance;
+
+typedef struct mtsg_group {
+    uint32_t node_offset, n_nodes;      /* its KDNode[] in group_nodes     */
+    uint32_t index_offset, n_indices;   /* its leaf references             */
+    float aabb_min[3], aabb_max[3];     /* enlarged tree AABB, group space */
+    uint32_t max_depth, pad;
+} mtsg_group;
 
 enum {
     MTSG_BSDF_DIFFUSE        = 1,   /* src/bsdfs/diffuse.cpp        */
@@ -242,7 +271,7 @@ typedef struct mtsg_scene_desc {
     const mtsg_kdnode *nodes;
     uint32_t n_indices;
     const uint32_t *indices;
-    uint32_t n_prims;             /* == n_triangles + n_rects              */
+    uint32_t n_prims;             /* == n_triangles + n_rects + n_instances */
     const mtsg_triaccel *triaccel;
     float aabb_min[3], aabb_max[3];  /* enlarged tree AABB (gkdtree.h:1213-1220) */
     uint32_t max_depth;           /* deepest leaf (traversal stack bound)  */
@@ -262,6 +291,15 @@ typedef struct mtsg_scene_desc {
     const uint16_t *qmc_perm;     /* digit permutation of base primes[i] at
                                      qmc_perm + qmc_perm_offset[i]; NULL when
                                      unscrambled (scramble 0) or unused     */
+    /* two-level instancing (n_instances = 0: none) */
+    uint32_t n_instances;
+    const mtsg_instance *instances;
+    uint32_t n_groups;
+    const mtsg_group *groups;
+    uint32_t n_group_nodes;
+    const mtsg_kdnode *group_nodes;
+    uint32_t n_group_indices;
+    const uint32_t *group_indices;
 } mtsg_scene_desc;
 
 /* ---- render ------------------------------------------------------------- */
@@ -325,6 +363,8 @@ typedef struct mtsg_stats {
      * histogram of floor(log2(iterations)), bins 0-15                      */
     uint64_t iter_max_closest, iter_max_shadow;
     uint64_t iter_hist_closest[16], iter_hist_shadow[16];
+    /* instance transform visits (MTSG_FLAG_COUNT; two-level scenes)      */
+    uint64_t instance_visits, shadow_instance_visits;
 } mtsg_stats;
 
 enum {

@@ -35,6 +35,18 @@ mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_
 /* Override kd-tree build parameters before loading (0 = default). */
 void mtsh_set_kd_threads(int threads);
 
+/* How `instance` shapes of a `shapegroup` are handed to the device, for the
+ * loads that follow:
+ *   MTSH_INSTANCING_FLATTEN    each instance's triangles are transformed to
+ *                              world space and join the one scene kd-tree
+ *                              (the default);
+ *   MTSH_INSTANCING_TWO_LEVEL  Mitsuba's own structure (instance.cpp:115-160,
+ *                              shapegroup.cpp:94-101): one group-space kd-tree
+ *                              per shape group, instances in the top-level
+ *                              tree, rays transformed per instance visit. */
+enum { MTSH_INSTANCING_FLATTEN = 0, MTSH_INSTANCING_TWO_LEVEL = 1 };
+void mtsh_set_instancing(int mode);
+
 const mtsg_scene_desc *mtsh_scene_desc(const mtsh_scene *scene);
 
 /* Integrator properties + sampleCount of the scene; tile = full film. */

@@ -55,16 +55,17 @@ AABB clipTriangle(const V3 &a, const V3 &b, const V3 &c, const AABB &box) {
 
 struct ScenePrims : PrimSource {
     const Scene &s;
-    explicit ScenePrims(const Scene &sc) : s(sc) {}
-    size_t count() const override { return s.triIdx.size() / 3 + s.rectDesc.size(); }
+    const std::vector<uint8_t> &grouped;   // triangle belongs to a shape group (two-level)
+    ScenePrims(const Scene &sc, const std::vector<uint8_t> &g) : s(sc), grouped(g) {}
+    size_t count() const override { return s.triIdx.size() / 3 + s.rectDesc.size() + s.instanceDesc.size(); }
     V3 vtx(uint32_t i) const { return V3(s.vtxPos[3 * i], s.vtxPos[3 * i + 1], s.vtxPos[3 * i + 2]); }
     AABB bounds(size_t i) const override {
         AABB b;
-        size_t nt = s.triIdx.size() / 3;
+        size_t nt = s.triIdx.size() / 3, nr = s.rectDesc.size();
         if (i < nt) {
-            if (s.triaccel[i].k == 3) return AABB();   // degenerate: never intersected
+            if (s.triaccel[i].k == 3 || grouped[i]) return AABB();   // degenerate, or in a group's own tree
             for (int k = 0; k < 3; ++k) b.expand(vtx(s.triIdx[3 * i + k]));
-        } else {
+        } else if (i < nt + nr) {
             const mtsg_rect &r = s.rectDesc[i - nt];
             for (int cx = -1; cx <= 1; cx += 2)
                 for (int cy = -1; cy <= 1; cy += 2) {
@@ -72,6 +73,15 @@ struct ScenePrims : PrimSource {
                     V3 p(m[0] * cx + m[1] * cy + m[3], m[4] * cx + m[5] * cy + m[7], m[8] * cx + m[9] * cy + m[11]);
                     b.expand(p);
                 }
+        } else {
+            // Instance::getAABB (instance.cpp:78-96): the group tree's AABB
+            // corners through the instance transform
+            const InstanceDef &in = s.instances[i - nt - nr];
+            const AABB &ga = s.groupTrees[in.group].aabb;
+            if (!ga.valid()) return AABB();
+            for (int c = 0; c < 8; ++c)
+                b.expand(in.toWorld.point(V3((c & 1) ? ga.mx.x : ga.mn.x, (c & 2) ? ga.mx.y : ga.mn.y,
+                                             (c & 4) ? ga.mx.z : ga.mn.z)));
         }
         return b;
     }
@@ -81,6 +91,26 @@ struct ScenePrims : PrimSource {
         AABB b = bounds(i);
         b.clip(box);
         return b;
+    }
+};
+
+// the triangles of one shape group, in group space (ShapeGroup's ShapeKDTree)
+struct GroupPrims : PrimSource {
+    const Scene &s;
+    const std::vector<uint32_t> &tris;   // global triangle indices
+    GroupPrims(const Scene &sc, const std::vector<uint32_t> &t) : s(sc), tris(t) {}
+    size_t count() const override { return tris.size(); }
+    V3 vtx(uint32_t i) const { return V3(s.vtxPos[3 * i], s.vtxPos[3 * i + 1], s.vtxPos[3 * i + 2]); }
+    AABB bounds(size_t i) const override {
+        AABB b;
+        const uint32_t t = tris[i];
+        if (s.triaccel[t].k == 3) return AABB();
+        for (int k = 0; k < 3; ++k) b.expand(vtx(s.triIdx[3 * t + k]));
+        return b;
+    }
+    AABB clippedBounds(size_t i, const AABB &box) const override {
+        const uint32_t t = tris[i];
+        return clipTriangle(vtx(s.triIdx[3 * t]), vtx(s.triIdx[3 * t + 1]), vtx(s.triIdx[3 * t + 2]), box);
     }
 };
 
@@ -168,6 +198,10 @@ void Scene::finalize() {
             sd.tri_begin = tbase;
             sd.tri_count = (uint32_t)(m.idx.size() / 3);
             sd.emitter = m.emitter;
+        } else if (sr.type == MTSG_SHAPE_INSTANCE) {
+            sd.bsdf = -1;
+            sd.emitter = -1;
+            sd.instance = (uint32_t)sr.index;
         } else {
             Rect &r = rects[sr.index];
             // rectangle.cpp:78-94 configure()
@@ -248,10 +282,14 @@ void Scene::finalize() {
     }
 
     // ---------------- TriAccel + kd-tree ----------------
-    triaccel.assign(nTri + rectDesc.size(), mtsg_triaccel{});
+    const size_t nInst = instances.size();
+    triaccel.assign(nTri + rectDesc.size() + nInst, mtsg_triaccel{});
+    std::vector<uint8_t> grouped(nTri, 0);
+    std::vector<std::vector<uint32_t>> groupTris(groups.size());
     for (size_t si = 0; si < shapeDesc.size(); ++si) {
         const mtsg_shape &sd = shapeDesc[si];
         if (sd.type == MTSG_SHAPE_MESH) {
+            const int grp = meshes[shapes[si].index].group;
             for (uint32_t t = 0; t < sd.tri_count; ++t) {
                 uint32_t g = sd.tri_begin + t;
                 auto P = [&](int k) { uint32_t vi = triIdx[3 * g + k]; return V3(vtxPos[3 * vi], vtxPos[3 * vi + 1], vtxPos[3 * vi + 2]); };
@@ -259,16 +297,53 @@ void Scene::finalize() {
                 loadTriAccel(ta, P(0), P(1), P(2));
                 ta.shape_index = (uint32_t)si;
                 ta.prim_index = g;
+                if (grp >= 0) { grouped[g] = 1; groupTris[grp].push_back(g); }
             }
-        } else {
+        } else if (sd.type == MTSG_SHAPE_RECT) {
             mtsg_triaccel &ta = triaccel[nTri + sd.rect];
             memset(&ta, 0, sizeof(ta));
             ta.k = MTSG_TRIACCEL_SHAPE;
             ta.shape_index = (uint32_t)si;
             ta.prim_index = sd.rect;
+        } else {
+            mtsg_triaccel &ta = triaccel[nTri + rectDesc.size() + sd.instance];
+            memset(&ta, 0, sizeof(ta));
+            ta.k = MTSG_TRIACCEL_SHAPE;
+            ta.shape_index = (uint32_t)si;
+            ta.prim_index = sd.instance;
         }
     }
-    ScenePrims src(*this);
+    // one kd-tree per shape group, in group space (ShapeGroup::configure,
+    // shapegroup.cpp:94-101); leaf references index `triaccel`
+    groupTrees.assign(groups.size(), KDTree());
+    groupDesc.clear(); groupNodes.clear(); groupIndices.clear(); instanceDesc.clear();
+    for (size_t g = 0; g < groups.size(); ++g) {
+        if (groupTris[g].empty()) throw std::runtime_error("shapegroup \"" + groups[g].id + "\" holds no triangles");
+        GroupPrims gp(*this, groupTris[g]);
+        buildKDTree(gp, kd, groupTrees[g]);
+        const KDTree &T = groupTrees[g];
+        mtsg_group gd{};
+        gd.node_offset = (uint32_t)groupNodes.size();
+        gd.n_nodes = (uint32_t)T.nodes.size();
+        gd.index_offset = (uint32_t)groupIndices.size();
+        gd.n_indices = (uint32_t)T.indices.size();
+        for (int k = 0; k < 3; ++k) { gd.aabb_min[k] = T.aabb.mn[k]; gd.aabb_max[k] = T.aabb.mx[k]; }
+        gd.max_depth = T.maxDepth;
+        // leaf ranges stay relative to the group's own index block
+        groupNodes.insert(groupNodes.end(), T.nodes.begin(), T.nodes.end());
+        for (uint32_t i : T.indices) groupIndices.push_back(groupTris[g][i]);
+        groupDesc.push_back(gd);
+    }
+    for (const InstanceDef &in : instances) {
+        mtsg_instance id{};
+        setRow34(id.to_world, in.toWorld, false);
+        setRow34(id.to_local, in.toWorld, true);
+        id.group = (uint32_t)in.group;
+        instanceDesc.push_back(id);
+    }
+    for (size_t si = 0; si < shapeDesc.size(); ++si)
+        if (shapeDesc[si].type == MTSG_SHAPE_INSTANCE) instanceDesc[shapeDesc[si].instance].shape_index = (uint32_t)si;
+    ScenePrims src(*this, grouped);
     buildKDTree(src, kd, tree);
 
     // ---------------- sensor / film ----------------
@@ -383,6 +458,14 @@ void Scene::finalize() {
     d.triaccel = triaccel.data();
     for (int k = 0; k < 3; ++k) { d.aabb_min[k] = tree.aabb.mn[k]; d.aabb_max[k] = tree.aabb.mx[k]; }
     d.max_depth = tree.maxDepth;
+    d.n_instances = (uint32_t)instanceDesc.size();
+    d.instances = instanceDesc.empty() ? nullptr : instanceDesc.data();
+    d.n_groups = (uint32_t)groupDesc.size();
+    d.groups = groupDesc.empty() ? nullptr : groupDesc.data();
+    d.n_group_nodes = (uint32_t)groupNodes.size();
+    d.group_nodes = groupNodes.empty() ? nullptr : groupNodes.data();
+    d.n_group_indices = (uint32_t)groupIndices.size();
+    d.group_indices = groupIndices.empty() ? nullptr : groupIndices.data();
     d.camera = cam;
     // ---------------- sampler ----------------
     d.sampler = sampler;

@@ -16,6 +16,7 @@ thread_local std::string g_err;
 extern "C" {
 
 void mtsh_set_kd_threads(int threads) { mtsh::g_defaultKDThreads = threads; }
+void mtsh_set_instancing(int mode) { mtsh::g_instancing = mode == MTSH_INSTANCING_TWO_LEVEL ? 1 : 0; }
 
 mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_defines) {
     try {

@@ -647,8 +647,9 @@ void writePFM(const std::string &path, int w, int h, const std::vector<float> &r
 namespace {
 
 struct ShapeGroup {
-    std::vector<Mesh> meshes;   // object space
+    std::vector<Mesh> meshes;   // object space (flattening)
     std::vector<Rect> rects;
+    int index = -1;             // two-level: Scene::groups entry
 };
 
 struct Loader {
@@ -1075,6 +1076,7 @@ struct Loader {
         substAll(n);
         std::string type = lower(n.attr("type"));
         if (type == "shapegroup") {
+            if (inGroup) throw err("Nested instancing is not permitted");
             ShapeGroup g;
             for (auto &cp : n.children) {
                 substAll(*cp);
@@ -1083,6 +1085,24 @@ struct Loader {
             }
             std::string id = n.attr("id");
             if (id.empty()) throw err("shapegroup needs an id");
+            if (scene.twoLevel) {
+                // ShapeGroup::addChild / configure (shapegroup.cpp:94-138): the
+                // group's shapes get their own kd-tree in group space
+                if (!g.rects.empty())
+                    throw err("shapegroup \"" + id + "\": rectangles inside shape groups are outside the two-level "
+                              "variant of this build (use the flattening mode)");
+                GroupDef gd;
+                gd.id = id;
+                g.index = (int)scene.groups.size();
+                for (auto &m : g.meshes) {
+                    m.group = g.index;
+                    scene.meshes.push_back(std::move(m));
+                    gd.shapes.push_back((int)scene.shapes.size());
+                    scene.shapes.push_back({MTSG_SHAPE_MESH, (int)scene.meshes.size() - 1});
+                }
+                g.meshes.clear();
+                scene.groups.push_back(std::move(gd));
+            }
             groups[id] = std::move(g);
             return;
         }
@@ -1109,8 +1129,19 @@ struct Loader {
         Transform toWorld = props.getTransform("toWorld", Transform());
         bool flip = props.getBool("flipNormals", false);
         if (type == "instance") {
-            if (instRef.empty()) throw err("instance: missing <ref> to a shapegroup");
+            if (instRef.empty()) throw err("A reference to a 'shapegroup' must be specified!");
+            if (inGroup) throw err("Nested instancing is not permitted");
             const ShapeGroup &g = groups[instRef];
+            if (scene.twoLevel) {
+                // Instance (instance.cpp:57-130): a top-level primitive that
+                // transforms rays into the group's space
+                InstanceDef idf;
+                idf.group = g.index;
+                idf.toWorld = toWorld;
+                scene.instances.push_back(idf);
+                scene.shapes.push_back({MTSG_SHAPE_INSTANCE, (int)scene.instances.size() - 1});
+                return;
+            }
             for (const Mesh &m0 : g.meshes) {
                 Mesh m = m0;
                 for (auto &p : m.p) p = toWorld.point(p);
@@ -1380,10 +1411,12 @@ bool readPFM(const std::string &path, int &w, int &h, std::vector<float> &rgb, s
 }
 
 int g_defaultKDThreads = 0;
+int g_instancing = 0;
 
 std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::string, std::string> &defines) {
     auto scene = std::make_unique<Scene>();
     scene->kd.threads = g_defaultKDThreads;
+    scene->twoLevel = g_instancing == 1;
     // build-parameter overrides (tree-quality experiments; defaults follow gkdtree.h:734-744)
     if (const char *v = getenv("MTSH_KD_TRAVERSAL")) scene->kd.traversalCost = (float)atof(v);
     if (const char *v = getenv("MTSH_KD_QUERY")) scene->kd.queryCost = (float)atof(v);

@@ -44,6 +44,7 @@ struct Mesh {
     std::vector<uint32_t> idx;       // 3 per triangle
     bool faceNormals = false;
     int bsdf = -1, emitter = -1;
+    int group = -1;                  // two-level: the shape group it belongs to (group space)
 };
 
 struct Rect {
@@ -70,7 +71,17 @@ struct Emitter {
 
 struct ShapeRef {                    // m_shapes order in the kd-tree
     int type;                        // MTSG_SHAPE_*
-    int index;                       // into meshes / rects
+    int index;                       // into meshes / rects / instances
+};
+
+// Two-level instancing (src/shapes/shapegroup.cpp, instance.cpp)
+struct GroupDef {
+    std::string id;
+    std::vector<int> shapes;         // its meshes' entries in Scene::shapes
+};
+struct InstanceDef {
+    int group = -1;
+    Transform toWorld;
 };
 
 struct Sensor {
@@ -121,12 +132,15 @@ struct Scene {
     std::vector<Mesh> meshes;
     std::vector<Rect> rects;
     std::vector<ShapeRef> shapes;     // in kd-tree order
+    std::vector<GroupDef> groups;     // two-level instancing only
+    std::vector<InstanceDef> instances;
     std::vector<Bsdf> bsdfs;
     std::vector<Emitter> emitters;
     Sensor sensor;
     Film film;
     IntegratorProps integrator;
     int sampleCount = 4;
+    bool twoLevel = false;            // MTSH_INSTANCING_TWO_LEVEL
     std::string samplerType = "independent";
     mtsg_sampler sampler{MTSG_SAMPLER_INDEPENDENT, -1, 4, 0};
     KDBuildParams kd;
@@ -143,6 +157,11 @@ struct Scene {
     std::vector<uint32_t> qmcPrimes, qmcOffsets;
     std::vector<uint16_t> qmcPerm;
     KDTree tree;
+    std::vector<KDTree> groupTrees;
+    std::vector<mtsg_instance> instanceDesc;
+    std::vector<mtsg_group> groupDesc;
+    std::vector<mtsg_kdnode> groupNodes;
+    std::vector<uint32_t> groupIndices;
     mtsg_camera camera{};
     mtsg_scene_desc desc{};
 
@@ -150,6 +169,7 @@ struct Scene {
 };
 
 extern int g_defaultKDThreads;   // 0 = hardware concurrency
+extern int g_instancing;         // MTSH_INSTANCING_* of the next load
 
 // Environment emitter tables (envmap.cpp in this directory)
 void buildEnvmap(const Emitter &e, const float aabbMin[3], const float aabbMax[3], const float camPos[3],

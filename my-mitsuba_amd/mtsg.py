@@ -22,6 +22,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 
 MTSG_OK = 0
+MTSH_INSTANCING_FLATTEN = 0
+MTSH_INSTANCING_TWO_LEVEL = 1
 MTSG_FLAG_TIMING = 1
 MTSG_FLAG_COUNT = 2
 MTSG_FLAG_WAVETIME = 4
@@ -64,6 +66,7 @@ class Stats(C.Structure):
         ("launches_trace_shadow", C.c_uint64),
         ("iter_max_closest", C.c_uint64), ("iter_max_shadow", C.c_uint64),
         ("iter_hist_closest", C.c_uint64 * 16), ("iter_hist_shadow", C.c_uint64 * 16),
+        ("instance_visits", C.c_uint64), ("shadow_instance_visits", C.c_uint64),
     ]
 
 
@@ -91,7 +94,7 @@ DEVICE_SYMBOLS = [
     "mtsg_last_error", "mtsg_env_eval", "mtsg_sampler_draws", "mtsg_debug_wavetimes", "mtsg_debug_stragglers",
 ]
 HOST_SYMBOLS = [
-    "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_scene_desc", "mtsh_scene_render_params",
+    "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
     "mtsh_last_error",
 ]
@@ -142,6 +145,7 @@ def host_lib() -> C.CDLL:
         lib.mtsh_write_pfm.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_void_p]
         lib.mtsh_last_error.argtypes = [C.c_char_p, C.c_size_t]
         lib.mtsh_set_kd_threads.argtypes = [C.c_int]
+        lib.mtsh_set_instancing.argtypes = [C.c_int]
         _host = lib
     return _host
 
@@ -196,9 +200,15 @@ def _ptr(a: np.ndarray) -> C.c_void_p:
 class Scene:
     """A loaded Mitsuba XML scene (host side; owns the flat descriptor)."""
 
-    def __init__(self, path: str, defines: dict | None = None, kd_threads: int = 0):
+    def __init__(self, path: str, defines: dict | None = None, kd_threads: int = 0, instancing: str = "flatten"):
+        """instancing: "flatten" (instances become world-space triangles of the
+        one scene tree) or "two-level" (Mitsuba's instance / shapegroup
+        structure: per-group trees, rays transformed per instance visit)."""
         lib = host_lib()
         lib.mtsh_set_kd_threads(kd_threads)
+        if instancing not in ("flatten", "two-level"):
+            raise ValueError(f"instancing must be 'flatten' or 'two-level', not {instancing!r}")
+        lib.mtsh_set_instancing(MTSH_INSTANCING_TWO_LEVEL if instancing == "two-level" else MTSH_INSTANCING_FLATTEN)
         defs = [f"{k}={v}".encode() for k, v in (defines or {}).items()]
         arr = (C.c_char_p * max(1, len(defs)))(*defs)
         self._h = lib.mtsh_scene_load(path.encode(), arr, len(defs))

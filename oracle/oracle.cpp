@@ -586,7 +586,7 @@ struct Ray {
 };
 
 struct Counters {
-    uint64_t nodes = 0, refs = 0, tests = 0, closest = 0, shadow = 0;
+    uint64_t nodes = 0, refs = 0, tests = 0, closest = 0, shadow = 0, inst = 0;
 };
 
 // ---------------------------------------------------------------------------
@@ -603,7 +603,10 @@ struct Its {
     Vec toWorld(const Vec &v) const { return shFrame.toWorld(v); }
 };
 
-struct Cache { uint32_t shapeIndex, primIndex; float u, v, rx, ry; };
+// IntersectionCache (skdtree.h:236-241); for a hit inside an instance the
+// group tree's cache, and the instance (Instance::rayIntersect passes its
+// temp space down to the group's ShapeKDTree, instance.cpp:115-122)
+struct Cache { uint32_t shapeIndex, primIndex; float u, v, rx, ry; uint32_t inst = 0xFFFFFFFFu; };
 
 struct SceneView {
     const mtsg_scene_desc &d;
@@ -614,10 +617,13 @@ struct SceneView {
 
     // AABB::rayIntersect (aabb.h:308-338)
     bool aabbIntersect(const Ray &ray, float &nearT, float &farT) const {
+        return aabbIntersect(ray, d.aabb_min, d.aabb_max, nearT, farT);
+    }
+    static bool aabbIntersect(const Ray &ray, const float *bmin, const float *bmax, float &nearT, float &farT) {
         nearT = -std::numeric_limits<float>::infinity();
         farT = std::numeric_limits<float>::infinity();
         for (int i = 0; i < 3; i++) {
-            const float origin = ray.o[i], minVal = d.aabb_min[i], maxVal = d.aabb_max[i];
+            const float origin = ray.o[i], minVal = bmin[i], maxVal = bmax[i];
             if (ray.d[i] == 0) {
                 if (origin < minVal || origin > maxVal) return false;
             } else {
@@ -670,7 +676,8 @@ struct SceneView {
     }
 
     // ShapeKDTree::intersect (skdtree.h:248-337)
-    bool primIntersect(const Ray &ray, uint32_t idx, float mint, float maxt, float &t, Cache *cache) const {
+    bool primIntersect(const Ray &ray, uint32_t idx, float mint, float maxt, float &t, Cache *cache,
+                       Counters *ctr = nullptr) const {
         const mtsg_triaccel &ta = d.triaccel[idx];
         if (ta.k != MTSG_TRIACCEL_SHAPE) {
             float u, v, tt;
@@ -681,6 +688,8 @@ struct SceneView {
             }
             return false;
         }
+        if (d.shapes[ta.shape_index].type == MTSG_SHAPE_INSTANCE)
+            return instanceIntersect<false>(ray, ta.prim_index, mint, maxt, t, cache, ctr);
         float tt, lx, ly;
         if (rectIntersect(d.rects[ta.prim_index], ray, mint, maxt, tt, lx, ly)) {
             t = tt;
@@ -690,10 +699,64 @@ struct SceneView {
         return false;
     }
 
+    // ShapeKDTree::intersect(ray, idx, mint, maxt) (skdtree.h:310-337): shadow
+    // rays; an instance runs Instance::rayIntersect(ray, mint, maxt)
+    bool primIntersectShadow(const Ray &ray, uint32_t idx, float mint, float maxt, float &t, Counters *ctr) const {
+        const mtsg_triaccel &ta = d.triaccel[idx];
+        if (ta.k == MTSG_TRIACCEL_SHAPE && d.shapes[ta.shape_index].type == MTSG_SHAPE_INSTANCE)
+            return instanceIntersect<true>(ray, ta.prim_index, mint, maxt, t, nullptr, ctr);
+        return primIntersect(ray, idx, mint, maxt, t, nullptr);
+    }
+
     // SAHKDTree3D::rayIntersectHavran (sahkdtree3.h:178-308), with the
     // 8-entry hashed mailbox (sahkdtree3.h:30-32,138-152)
+    // Transform::operator()(Ray) (transform.h:262-278) with the instance's
+    // inverse: o and d transformed, the reciprocal recomputed, mint / maxt kept
+    Ray toInstance(const Ray &r, const mtsg_instance &in) const {
+        const float *m = in.to_local;
+        Ray l;
+        l.o = Vec(m[0] * r.o.x + m[1] * r.o.y + m[2] * r.o.z + m[3], m[4] * r.o.x + m[5] * r.o.y + m[6] * r.o.z + m[7],
+                  m[8] * r.o.x + m[9] * r.o.y + m[10] * r.o.z + m[11]);
+        l.setDirection(Vec(m[0] * r.d.x + m[1] * r.d.y + m[2] * r.d.z, m[4] * r.d.x + m[5] * r.d.y + m[6] * r.d.z,
+                           m[8] * r.d.x + m[9] * r.d.y + m[10] * r.d.z));
+        l.mint = r.mint;
+        l.maxt = r.maxt;
+        return l;
+    }
+    // Instance::rayIntersect (instance.cpp:115-130) -> the group's
+    // ShapeKDTree::rayIntersect(ray, mint, maxt, t, temp) (skdtree.h:431-458)
+    template <bool shadowRay>
+    bool instanceIntersect(const Ray &wr, uint32_t inst, float mint, float maxt, float &t, Cache *cache,
+                           Counters *ctr) const {
+        const mtsg_instance &in = d.instances[inst];
+        const mtsg_group &G = d.groups[in.group];
+        const Ray r = toInstance(wr, in);
+        if (ctr) ctr->inst++;
+        float nearT, farT;
+        if (!aabbIntersect(r, G.aabb_min, G.aabb_max, nearT, farT)) return false;
+        if (mint > nearT) nearT = mint;
+        if (maxt < farT) farT = maxt;
+        if (!(farT > nearT)) return false;
+        const mtsg_kdnode *nodes = d.group_nodes + G.node_offset;
+        const uint32_t *idx = d.group_indices + G.index_offset;
+        float tt = std::numeric_limits<float>::infinity();
+        Cache c;
+        const bool hit = ctr ? havranTree<shadowRay, true>(nodes, idx, r, nearT, farT, tt, shadowRay ? nullptr : &c, ctr)
+                             : havranTree<shadowRay, false>(nodes, idx, r, nearT, farT, tt, shadowRay ? nullptr : &c, nullptr);
+        if (!hit) return false;
+        t = tt;
+        if (cache) { *cache = c; cache->inst = inst; }
+        return true;
+    }
+
     template <bool shadowRay, bool count>
     bool havran(const Ray &ray, float mint, float maxt, float &t, Cache *cache, Counters *ctr) const {
+        return havranTree<shadowRay, count>(d.nodes, d.indices, ray, mint, maxt, t, cache, ctr);
+    }
+
+    template <bool shadowRay, bool count>
+    bool havranTree(const mtsg_kdnode *nodes, const uint32_t *indices, const Ray &ray, float mint, float maxt, float &t,
+                    Cache *cache, Counters *ctr) const {
         struct Entry { uint32_t node; float t; uint32_t prev; Vec p; };
         Entry stack[48];
         uint32_t mailbox[8];
@@ -711,7 +774,7 @@ struct SceneView {
         while (cur != 0xFFFFFFFFu) {
             for (;;) {
                 if (count) ctr->nodes++;
-                const mtsg_kdnode &node = d.nodes[cur];
+                const mtsg_kdnode &node = nodes[cur];
                 if (node.combined & 0x80000000u) break;
                 float splitVal;
                 memcpy(&splitVal, &node.data, 4);
@@ -738,15 +801,15 @@ struct SceneView {
                 stack[exPt].p = ray(distToSplit);
                 stack[exPt].p[axis] = splitVal;
             }
-            const mtsg_kdnode &leaf = d.nodes[cur];
+            const mtsg_kdnode &leaf = nodes[cur];
             for (uint32_t entry = leaf.combined & 0x7FFFFFFFu, last = leaf.data; entry != last; entry++) {
-                const uint32_t primIdx = d.indices[entry];
+                const uint32_t primIdx = indices[entry];
                 if (count) ctr->refs++;
                 if (mailbox[primIdx & 7] == primIdx) continue;
                 if (count) ctr->tests++;
                 bool result;
-                if (!shadowRay) result = primIntersect(ray, primIdx, mint, maxt, t, &tmp);
-                else { float tt; result = primIntersect(ray, primIdx, mint, maxt, tt, nullptr); }
+                if (!shadowRay) result = primIntersect(ray, primIdx, mint, maxt, t, &tmp, count ? ctr : nullptr);
+                else { float tt; result = primIntersectShadow(ray, primIdx, mint, maxt, tt, count ? ctr : nullptr); }
                 if (result) {
                     if (shadowRay) return true;
                     maxt = t;
@@ -763,8 +826,9 @@ struct SceneView {
         return found;
     }
 
-    // ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428)
-    void fill(const Ray &ray, const Cache &c, Its &its) const {
+    // ShapeKDTree::fillIntersectionRecord<BarycentricPos> (skdtree.h:343-428),
+    // without the final computeShadingFrame / wi
+    void fillShape(const Ray &ray, const Cache &c, Its &its, bool barycentricPos) const {
         its.shape = (int)c.shapeIndex;
         const mtsg_shape &sh = d.shapes[c.shapeIndex];
         if (c.primIndex != 0xFFFFFFFFu) {
@@ -772,7 +836,7 @@ struct SceneView {
             const uint32_t i0 = d.tri_idx[3 * g], i1 = d.tri_idx[3 * g + 1], i2 = d.tri_idx[3 * g + 2];
             const float bx = 1 - c.u - c.v, by = c.u, bz = c.v;
             const Vec p0 = vtx(i0), p1 = vtx(i1), p2 = vtx(i2);
-            its.p = p0 * bx + p1 * by + p2 * bz;
+            its.p = barycentricPos ? p0 * bx + p1 * by + p2 * bz : ray(its.t);
             Vec side1 = p1 - p0, side2 = p2 - p0;
             Vec faceNormal = cross(side1, side2);
             float len = length(faceNormal);
@@ -795,6 +859,34 @@ struct SceneView {
             its.shFrame.n = its.geoFrame.n;
             its.dpdu = Vec(r.dpdu[0], r.dpdu[1], r.dpdu[2]);
             its.p = ray(its.t);
+        }
+    }
+
+    // ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428)
+    void fill(const Ray &ray, const Cache &c, Its &its) const {
+        if (c.inst == 0xFFFFFFFFu) {
+            fillShape(ray, c, its, true);
+        } else {
+            // Instance::fillIntersectionRecord (instance.cpp:146-160): the
+            // group tree fills the record from the group-space ray
+            // (BarycentricPos = false), then it is mapped back with toWorld;
+            // normals by the inverse transpose (transform.h:203-211)
+            const mtsg_instance &in = d.instances[c.inst];
+            const Ray lr = toInstance(ray, in);
+            fillShape(lr, c, its, false);
+            const float *W = in.to_world, *L = in.to_local;
+            auto normalT = [&](const Vec &v) {
+                return Vec(L[0] * v.x + L[4] * v.y + L[8] * v.z, L[1] * v.x + L[5] * v.y + L[9] * v.z,
+                           L[2] * v.x + L[6] * v.y + L[10] * v.z);
+            };
+            its.shFrame.n = normalize(normalT(its.shFrame.n));
+            its.geoFrame = Frame(normalize(normalT(its.geoFrame.n)));
+            its.dpdu = Vec(W[0] * its.dpdu.x + W[1] * its.dpdu.y + W[2] * its.dpdu.z,
+                           W[4] * its.dpdu.x + W[5] * its.dpdu.y + W[6] * its.dpdu.z,
+                           W[8] * its.dpdu.x + W[9] * its.dpdu.y + W[10] * its.dpdu.z);
+            its.p = Vec(W[0] * its.p.x + W[1] * its.p.y + W[2] * its.p.z + W[3],
+                        W[4] * its.p.x + W[5] * its.p.y + W[6] * its.p.z + W[7],
+                        W[8] * its.p.x + W[9] * its.p.y + W[10] * its.p.z + W[11]);
         }
         computeShadingFrame(its.shFrame.n, its.dpdu, its.shFrame);
         its.wi = its.toLocal(-ray.d);
@@ -2064,6 +2156,17 @@ int oracle_trace_shadow(const mtsg_scene_desc *d, uint32_t n, const float *rays,
 
 int oracle_trace_closest_brute(const mtsg_scene_desc *d, uint32_t n, const float *rays, float *t, uint32_t *prim) {
     SceneView sv(*d);
+    // triangles of shape groups are only reachable through their instances
+    std::vector<uint8_t> grouped(d->n_prims, 0);
+    std::vector<std::vector<uint32_t>> groupPrims(d->n_groups);
+    for (uint32_t g = 0; g < d->n_groups; ++g) {
+        const mtsg_group &G = d->groups[g];
+        for (uint32_t i = 0; i < G.n_indices; ++i) {
+            const uint32_t p = d->group_indices[G.index_offset + i];
+            if (!grouped[p]) groupPrims[g].push_back(p);
+            grouped[p] = 1;
+        }
+    }
     parallelFor(n, 0, [&](uint32_t i) {
         Ray ray = rayFrom(rays + 8 * i);
         float mint, maxt;
@@ -2077,6 +2180,22 @@ int oracle_trace_closest_brute(const mtsg_scene_desc *d, uint32_t n, const float
         if (ray.maxt < maxt) maxt = ray.maxt;
         if (!(maxt > mint)) return;
         for (uint32_t p = 0; p < d->n_prims; ++p) {
+            if (grouped[p]) continue;
+            const mtsg_triaccel &ta = d->triaccel[p];
+            if (ta.k == MTSG_TRIACCEL_SHAPE && d->shapes[ta.shape_index].type == MTSG_SHAPE_INSTANCE) {
+                // every primitive of the group with the instance-space ray
+                const Ray lr = sv.toInstance(ray, d->instances[ta.prim_index]);
+                for (uint32_t q : groupPrims[d->instances[ta.prim_index].group]) {
+                    float tt;
+                    Cache c;
+                    if (sv.primIntersect(lr, q, mint, maxt, tt, &c)) {
+                        maxt = tt;
+                        t[i] = tt;
+                        prim[i] = c.primIndex;
+                    }
+                }
+                continue;
+            }
             float tt;
             Cache c;
             if (sv.primIntersect(ray, p, mint, maxt, tt, &c)) {
