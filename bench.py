@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="bunny15", choices=["bunny15", "cbox", "c5"])
     ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--instancing", default="flatten", choices=["flatten", "two-level"],
+                    help="C3's 15 bunny instances: world-space copies in one tree, or Mitsuba's two-level structure")
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--batch-paths", type=int, default=0)
@@ -227,7 +229,7 @@ def main():
 
     path, defs = scene_args(a)
     t_load = time.time()
-    scene = mtsg.Scene(path, defs)
+    scene = mtsg.Scene(path, defs, instancing=a.instancing)
     load_s = time.time() - t_load
     border = scene.border
     params = scene.params()

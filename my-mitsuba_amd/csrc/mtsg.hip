@@ -72,7 +72,13 @@ struct DevScene {
     // halton / hammersley tables (sampler.h); nullptr for the other samplers
     const uint32_t *qmcPrimes, *qmcOff;
     const uint16_t *qmcPerm;
+    // two-level instancing (instance.cpp:115-160): per instance 8 float4 =
+    // to_local rows 0-2, to_world rows 0-2, {group AABB min, root word 0},
+    // {group AABB max, root word 1}; the group trees live in `blocks` / `triL`
+    // beside the top-level tree.  nullptr: no instances.
+    const float4 *__restrict__ inst;
 };
+constexpr uint32_t KINST = 4u;   // leaf-ordered TriAccel copy of an instance primitive: k = 4
 
 struct DevCamera {
     float s2c[16];
@@ -152,6 +158,7 @@ struct DevPaths {
     float4 *n_ray_o, *n_ray_d, *n_T, *n_aux, *n_Lp;   // next bounce (compacted)
     uint4 *n_meta;
     float4 *hit;      // t, u, v, prim (bits) of ray i
+    uint32_t *hitInst;   // instance of hit i (0xFFFFFFFF: none); two-level scenes only
     float4 *L;        // per sample slot: final radiance, alpha (k_splat input)
     float4 *sh_o;     // shadow ray i: origin, maxt
     float4 *sh_d;     // direction, mint
@@ -314,7 +321,7 @@ DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float m
 // Algorithmic work (per lane) and, for the SIMD-efficiency figures, the
 // wave-level iteration counts (accumulated by lane 0 only): a wave pays
 // max-over-lanes of the inner-node and primitive iterations of every step.
-struct TraceCounts { uint32_t nodes, refs, tests, wnodes, wtests, wsteps, wactive, restarts; };   // restarts: not flushed
+struct TraceCounts { uint32_t nodes, refs, tests, wnodes, wtests, wsteps, wactive, restarts, inst; };   // restarts: not flushed
 
 template <bool COUNT>
 DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
@@ -629,6 +636,221 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
 }
 
+// ---------------------------------------------------------------------------
+// Two-level traversal (Instance::rayIntersect, instance.cpp:115-130, over the
+// group's ShapeKDTree::rayIntersect, skdtree.h:431-458): the same speculative
+// iterations, with a per-lane level.  An instance primitive met in a
+// top-level leaf saves the top-level state (node, interval, held leaf range,
+// stack counters) to LDS, transforms the ray by the instance's to_local and
+// traverses the group tree on the clipped interval [max(mint, near),
+// min(best, far)]; when the group traversal ends (or Havran's exit fires
+// inside it) the top-level state is restored and the world-space ray is
+// reloaded from the work list.  The two levels keep separate LDS stacks
+// (top level: OUTER_STACK entries, group: SHORT_STACK), so a group visit
+// never evicts top-level entries.  Hits are written through with the
+// instance they were found in.
+// ---------------------------------------------------------------------------
+constexpr int OUTER_STACK = 2;
+constexpr int SAVE_WORDS = 11;   // cur.x, cur.y, tmin, tmax, lfE, lfEnd, lfTmax, bits, instance, root.x, root.y
+__shared__ uint2 s_outNode[OUTER_STACK * TRACE_BLOCK];
+__shared__ float s_outT[OUTER_STACK * TRACE_BLOCK];
+__shared__ uint32_t s_save[SAVE_WORDS * TRACE_BLOCK];
+enum : uint32_t { SB_INST = 1u << 22 };
+
+DEV uint32_t &save_word(uint32_t k) { return s_save[k * TRACE_BLOCK + lane_here()]; }
+
+// push the far child onto the stack of the lane's level (circular, drops
+// the oldest entry when full)
+DEV uint2 spec_take_i(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push) {
+    const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
+    if (push) {
+        const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
+        const uint32_t b = r.bits, top = b & SB_TOP;
+        const bool inner = (b & SB_INST) != 0;
+        const uint32_t cap = inner ? (uint32_t)SHORT_STACK : (uint32_t)OUTER_STACK;
+        const uint32_t i = top * TRACE_BLOCK + lane_here();
+        if (inner) { s_specNode[i] = other; s_specT[i] = r.tmax; }
+        else { s_outNode[i] = other; s_outT[i] = r.tmax; }
+        const bool full = (b & SB_N) == cap * SB_N1;
+        r.bits = ((b & ~SB_TOP) | (top == cap - 1 ? 0u : top + 1u)) + (full ? SB_DROPPED - (b & SB_DROPPED) : SB_N1);
+        r.tmax = tsplit;
+    }
+    return c;
+}
+
+// back to the top level after a group traversal: restore the saved state,
+// keep the hit flag, reload the world-space ray
+DEV void inst_exit(SpecRay &r, const float4 *wo, const float4 *wd) {
+    const uint32_t found = r.bits & SB_FOUND;
+    r.cur = make_uint2(save_word(0), save_word(1));
+    r.tmin = __uint_as_float(save_word(2));
+    r.tmax = __uint_as_float(save_word(3));
+    r.lfE = save_word(4);
+    r.lfEnd = save_word(5);
+    r.lfTmax = __uint_as_float(save_word(6));
+    r.bits = save_word(7) | found;
+    float4 ro = ldS(wo), rd = ldS(wd);
+    r.o = xyz(ro);
+    r.d = xyz(rd);
+    r.inv = mk3(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
+}
+
+template <bool COUNT>
+DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hitOut, uint32_t *instOut,
+                     const float4 *wo, const float4 *wd) {
+    const uint2 n = r.cur;
+    const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
+    const bool prim = r.lfE < r.lfEnd;
+    const bool rootKind = inner && !(n.x & 4u);
+    float tsplit;
+    bool goLeft, push;
+    spec_plan(r, n, tsplit, goLeft, push);
+    const uint32_t base = inner ? (n.x >> 3) << ((~n.x >> 1) & 2u) : 0u;
+    const uint32_t off = rootKind ? 2u - (uint32_t)goLeft : 0u;
+    const uint32_t pi = prim ? r.lfE : 0u;
+    const uint4 p0 = S.blocks[base], pc = S.blocks[base + off];
+    const float4 *rec = S.triL + (size_t)(3u * pi);
+    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
+    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
+                 "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
+                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
+    bool enter = false;
+    if (prim) {
+        if (COUNT) cnt.refs++;
+        const uint32_t k = __float_as_uint(f0.x);
+        enter = k == KINST;
+        if (!enter) {
+            if (COUNT) cnt.tests++;
+            float t, u, v;
+            bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+            const bool isRect = k == MTSG_TRIACCEL_SHAPE;
+            if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+            if (h) {
+                r.bits |= SB_FOUND;
+                if (r.bits & SB_SHADOW) return true;   // any hit occludes
+                r.best = t;
+                stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
+                *instOut = (r.bits & SB_INST) ? save_word(8) : 0xFFFFFFFFu;
+            }
+        }
+        ++r.lfE;
+    }
+    if (inner) {
+        if (COUNT) cnt.nodes++;
+        const uint2 c = spec_take_i(r, p0, tsplit, goLeft, push);
+        r.cur = c;
+        if (rootKind && !(c.x & 0x80000000u)) {
+            if (COUNT) cnt.nodes++;
+            float ts2;
+            bool gl2, push2;
+            spec_plan(r, c, ts2, gl2, push2);
+            r.cur = spec_take_i(r, pc, ts2, gl2, push2);
+        }
+    }
+    if (enter) {
+        // Instance::rayIntersect: the ray in group space (Transform::operator()
+        // (Ray), transform.h:262-278), clipped to the group tree's AABB
+        if (COUNT) cnt.inst++;
+        const uint32_t ii = __float_as_uint(f2.w);
+        const float4 *I = S.inst + 8 * (size_t)ii;
+        const float4 L0 = I[0], L1 = I[1], L2 = I[2], A0 = I[6], A1 = I[7];
+        const float3 o = r.o, d = r.d;   // (the library is built with -ffp-contract=off)
+        const float3 lo = mk3(L0.x * o.x + L0.y * o.y + L0.z * o.z + L0.w, L1.x * o.x + L1.y * o.y + L1.z * o.z + L1.w,
+                              L2.x * o.x + L2.y * o.y + L2.z * o.z + L2.w);
+        const float3 ld = mk3(L0.x * d.x + L0.y * d.y + L0.z * d.z, L1.x * d.x + L1.y * d.y + L1.z * d.z,
+                              L2.x * d.x + L2.y * d.y + L2.z * d.z);
+        const float3 li = mk3(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
+        float nearT = -INFINITY, farT = INFINITY;
+        bool ok = true;
+        const float bmn[3] = {A0.x, A0.y, A0.z}, bmx[3] = {A1.x, A1.y, A1.z};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const float oi = comp(lo, i), di = comp(ld, i), iv = comp(li, i);
+            if (di == 0.0f) {
+                if (oi < bmn[i] || oi > bmx[i]) ok = false;
+            } else {
+                const float t1 = (bmn[i] - oi) * iv, t2 = (bmx[i] - oi) * iv;
+                nearT = fmaxf(fminf(t1, t2), nearT);
+                farT = fminf(fmaxf(t1, t2), farT);
+            }
+        }
+        const float t0 = fmaxf(r.mint, nearT), t1 = fminf(r.best, farT);
+        if (ok & (nearT <= farT) & (t1 > t0)) {
+            save_word(0) = r.cur.x;
+            save_word(1) = r.cur.y;
+            save_word(2) = __float_as_uint(r.tmin);
+            save_word(3) = __float_as_uint(r.tmax);
+            save_word(4) = r.lfE;
+            save_word(5) = r.lfEnd;
+            save_word(6) = __float_as_uint(r.lfTmax);
+            save_word(7) = r.bits & ~SB_FOUND;
+            save_word(8) = ii;
+            const uint2 root = make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w));
+            save_word(9) = root.x;
+            save_word(10) = root.y;
+            r.o = lo;
+            r.d = ld;
+            r.inv = li;
+            r.tmin = t0;
+            r.tmax = t1;
+            r.cur = root;
+            r.lfE = r.lfEnd = 0;
+            r.lfTmax = -1.0f;
+            const uint32_t dneg = (ld.x <= 0.0f ? 1u : 0u) | (ld.y <= 0.0f ? 2u : 0u) | (ld.z <= 0.0f ? 4u : 0u);
+            r.bits = (r.bits & (SB_FOUND | SB_SHADOW)) | SB_INST | dneg << SB_DNEG;
+            return false;
+        }
+    }
+    const bool found = (r.bits & SB_FOUND) != 0;
+    const bool inInst = (r.bits & SB_INST) != 0;
+    const bool leafDone = (r.lfTmax >= 0.0f) & (r.lfE >= r.lfEnd);
+    if (leafDone & found & (r.best < r.lfTmax)) {
+        if (!inInst) return true;
+        inst_exit(r, wo, wd);
+        return false;
+    }
+    r.lfTmax = leafDone ? -1.0f : r.lfTmax;
+    const uint2 c = r.cur;
+    if ((r.lfTmax < 0.0f) & !(r.bits & SB_TRAVDONE) & (bool)(c.x >> 31)) {
+        const uint32_t st = c.x & 0x7FFFFFFFu;
+        const bool nonEmpty = st < c.y;
+        if (!nonEmpty & found & (r.best < r.tmax)) {
+            if (!inInst) return true;
+            inst_exit(r, wo, wd);
+            return false;
+        }
+        r.lfE = nonEmpty ? st : r.lfE;
+        r.lfEnd = nonEmpty ? c.y : r.lfEnd;
+        r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
+        const uint32_t b = r.bits;
+        const uint32_t cap = inInst ? (uint32_t)SHORT_STACK : (uint32_t)OUTER_STACK;
+        if (b & SB_N) {
+            const uint32_t top = b & SB_TOP, k = top == 0 ? cap - 1 : top - 1u;
+            const uint32_t i = k * TRACE_BLOCK + lane_here();
+            r.cur = inInst ? s_specNode[i] : s_outNode[i];
+            const float t = inInst ? s_specT[i] : s_outT[i];
+            r.bits = ((b & ~SB_TOP) | k) - SB_N1;
+            r.tmin = r.tmax;
+            r.tmax = fminf(t, r.best);
+        } else {
+            const bool restart = (b & SB_DROPPED) != 0;
+            const float t0 = r.tmax;
+            r.tmin = restart ? t0 : r.tmin;
+            r.tmax = restart ? r.best : r.tmax;
+            const uint2 root = inInst ? make_uint2(save_word(9), save_word(10)) : S.root2;
+            r.cur = restart ? root : c;
+            if (COUNT && restart) cnt.restarts++;
+            r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
+        }
+    }
+    const bool done = (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
+    if (done && inInst) {
+        inst_exit(r, wo, wd);
+        return false;
+    }
+    return done;
+}
+
 // Persistent traversal kernel with lane-level refill (the "while-while +
 // dynamic fetch" structure of Aila & Laine 2009, re-tiled for 64-lane waves):
 // a wave reserves FETCH work-list entries with ONE atomic into a wave-uniform
@@ -642,14 +864,14 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
 //   cIn: -1 = nIdentity closest rays (bounce 0), 0/1 = count in cnt_q(cIn), -2 = none
 //   sIn: 0/1 = count in CNT_S0/CNT_S1, -1 = none
 
-template <bool COUNT, int MIN_IDLE>
+template <bool COUNT, int MIN_IDLE, bool INST = false>
 __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
     const SpecStack stk{};
     const unsigned long long tStart = wt ? wall_clock64() : 0ull;
     const uint32_t nC = cIn == -1 ? nIdentity : (cIn >= 0 ? __atomic_load_n(&P.cnt[cnt_q(cIn)], __ATOMIC_RELAXED) : 0u);
     const uint32_t nS = sIn >= 0 ? __atomic_load_n(&P.cnt[cnt_s(sIn)], __ATOMIC_RELAXED) : 0u;
     Fetch F{&P.cnt[CNT_FETCH], nC + nS, blockIdx.x % XGROUPS, 0, max(1u, gridDim.x / XGROUPS * GUIDE_SPLIT), FETCH};
-    TraceCounts cc{0, 0, 0, 0, 0, 0, 0, 0}, cs{0, 0, 0, 0, 0, 0, 0, 0};
+    TraceCounts cc{0, 0, 0, 0, 0, 0, 0, 0, 0}, cs{0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
     bool exhausted = false;
     bool active = false;
@@ -689,6 +911,7 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
                 } else if (!(rd.w < 0.0f)) {   // maxt < 0: dead slot outside the render rectangle
                     stS(&P.hit[idx], miss_record());
                 }
+                if (INST && !shadow) P.hitInst[idx] = 0xFFFFFFFFu;
             }
             poolBase += take;
             poolLeft -= take;
@@ -711,8 +934,15 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
         if (WT_DRAIN && wt && exhausted) ++drainIters;
         bool done = false;
         if (active) {
-            if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx);
-            else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx);
+            if (INST) {
+                const bool sh = (r.bits & SB_SHADOW) != 0;
+                const float4 *wo = (sh ? P.sh_o : P.ray_o) + idx, *wd = (sh ? P.sh_d : P.ray_d) + idx;
+                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P.hit + idx, P.hitInst + idx, wo, wd);
+                else done = spec_iter_i<COUNT>(S, r, cc, P.hit + idx, P.hitInst + idx, wo, wd);
+            } else {
+                if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx);
+                else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx);
+            }
         }
         if (COUNT && active) ++iters;
         if (done) {
@@ -742,6 +972,13 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
     }
     flush_counts<COUNT>(P.ctr, cc);
     flush_counts<COUNT>(P.ctr + 8, cs);
+    if (COUNT && INST) {
+        unsigned long long vi[2] = {cc.inst, cs.inst};
+        for (int k = 0; k < 2; ++k) {
+            for (int o2 = 32; o2 > 0; o2 >>= 1) vi[k] += __shfl_down(vi[k], o2);
+            if (lane_id() == 0) atomicAdd(P.ctr + 49 + k, vi[k]);
+        }
+    }
     if (wt && __lane_id() == 0) {
         wt[WT_WORDS * blockIdx.x] = tStart;
         wt[WT_WORDS * blockIdx.x + 1] = wall_clock64();
@@ -1423,8 +1660,13 @@ struct Its {
     int shape, bsdf, emitter;
 };
 
-// ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428) + computeShadingFrame (util.cpp:603-608)
-DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, Its &its) {
+// ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428) + computeShadingFrame (util.cpp:603-608).
+// inst != ~0: the hit was found inside that instance; the group tree fills
+// the record from the group-space ray (BarycentricPos = false, so p = ray(t))
+// and Instance::fillIntersectionRecord (instance.cpp:146-160) maps it back
+// with toWorld, normals by the inverse transpose (transform.h:203-211)
+DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, uint32_t inst, Its &its) {
+#pragma clang fp contract(off)
     const uint32_t p = __float_as_uint(h.w);   // triangle, or 0x80000000 | rectangle
     float3 dpdu, n;
     if (!(p & 0x80000000u)) {
@@ -1438,7 +1680,6 @@ DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, Its &its) {
         its.bsdf = (int)(bw & 0x7FFFFFFFu);
         its.emitter = (int)__float_as_uint(r5.w);
         const float bx = 1 - h.y - h.z, by = h.y, bz = h.z;
-        its.p = p0 * bx + p1 * by + p2 * bz;
         float3 fn = cross(p1 - p0, p2 - p0);
         if (!isZero(fn)) fn = fn / length(fn);
         if (!(bw & 0x80000000u)) {
@@ -1447,7 +1688,28 @@ DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, Its &its) {
         } else {
             n = fn;
         }
-        its.geoN = fn;
+        if (inst == 0xFFFFFFFFu) {
+            its.p = p0 * bx + p1 * by + p2 * bz;
+            its.geoN = fn;
+        } else {
+            const float4 *I = S.inst + 8 * (size_t)inst;
+            const float4 L0 = I[0], L1 = I[1], L2 = I[2], W0 = I[3], W1 = I[4], W2 = I[5];
+            const float3 lo = mk3(L0.x * ro.x + L0.y * ro.y + L0.z * ro.z + L0.w, L1.x * ro.x + L1.y * ro.y + L1.z * ro.z + L1.w,
+                                  L2.x * ro.x + L2.y * ro.y + L2.z * ro.z + L2.w);
+            const float3 ld = mk3(L0.x * rd.x + L0.y * rd.y + L0.z * rd.z, L1.x * rd.x + L1.y * rd.y + L1.z * rd.z,
+                                  L2.x * rd.x + L2.y * rd.y + L2.z * rd.z);
+            const float3 pl = lo + ld * h.x;
+            auto normalT = [&](float3 v) {
+                return mk3(L0.x * v.x + L1.x * v.y + L2.x * v.z, L0.y * v.x + L1.y * v.y + L2.y * v.z,
+                           L0.z * v.x + L1.z * v.y + L2.z * v.z);
+            };
+            n = normalize(normalT(n));
+            its.geoN = normalize(normalT(fn));
+            dpdu = mk3(W0.x * dpdu.x + W0.y * dpdu.y + W0.z * dpdu.z, W1.x * dpdu.x + W1.y * dpdu.y + W1.z * dpdu.z,
+                       W2.x * dpdu.x + W2.y * dpdu.y + W2.z * dpdu.z);
+            its.p = mk3(W0.x * pl.x + W0.y * pl.y + W0.z * pl.z + W0.w, W1.x * pl.x + W1.y * pl.y + W1.z * pl.z + W1.w,
+                        W2.x * pl.x + W2.y * pl.y + W2.z * pl.z + W2.w);
+        }
     } else {
         const mtsg_rect &r = S.rects[p & 0x7FFFFFFFu];
         its.shape = (int)r.shape_index;
@@ -1576,7 +1838,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
             const bool valid = __float_as_uint(h.w) != 0xFFFFFFFFu;
             bool done = false;
             Its its;
-            if (valid) fill_its(S, ro, rd, h, its);
+            if (valid) fill_its(S, ro, rd, h, S.inst ? P.hitInst[i] : 0xFFFFFFFFu, its);
             if (bounce == 0) {
                 // RadianceQueryRecord::rayIntersect (records.inl:117-143)
                 if (hasAlpha) L4.w = valid ? 1.0f : 0.0f;
@@ -1901,7 +2163,7 @@ struct mtsg_scene {
     std::vector<void *> batchAllocs;
     uint32_t *hostCnt = nullptr;   // pinned copy of the queue counters (2 per lane)
     int cuCount = 0;
-    int traceGrid = 0, shadeGrid = 0;
+    int traceGrid = 0, shadeGrid = 0, traceGridInst = 0;
     uint32_t flags = 0;
     int samplerType = MTSG_SAMPLER_INDEPENDENT, samplerDim = 4;
     int qmcInv[2][3] = {{0, 0, 0}, {0, 0, 0}};
@@ -1950,6 +2212,7 @@ int ensure_batch(mtsg_scene *s, uint32_t paths, int lanes) {
     A(ray_o, float4); A(ray_d, float4); A(T, float4); A(aux, float4); A(Lp, float4); A(meta, uint4);
     A(n_ray_o, float4); A(n_ray_d, float4); A(n_T, float4); A(n_aux, float4); A(n_Lp, float4); A(n_meta, uint4);
     A(hit, float4); A(L, float4); A(sh_o, float4); A(sh_d, float4); A(sh_c, float4);
+    if (s->ds.inst) { A(hitInst, uint32_t); } else P.hitInst = nullptr;
 #undef A
     if ((rc = alloc(CNT_WORDS * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
     if ((rc = alloc(CTR_WORDS * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
@@ -1999,9 +2262,10 @@ template <bool COUNT>
 void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t n, hipStream_t st) {
     dim3 g(s->traceGrid), blk(TRACE_BLOCK);
     unsigned long long *wt = nullptr;
-    if ((s->flags & MTSG_FLAG_WAVETIME) && s->waveTimes && s->wtLaunches < WT_MAX_LAUNCHES)
+    if ((s->flags & MTSG_FLAG_WAVETIME) && s->waveTimes && s->wtLaunches < WT_MAX_LAUNCHES && !s->ds.inst)
         wt = s->waveTimes + (size_t)WT_WORDS * s->traceGrid * s->wtLaunches++;
-    if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    if (s->ds.inst) hipLaunchKernelGGL((k_trace_s<COUNT, 16, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    else if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
 }
 void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn, uint32_t n, hipStream_t st) {
@@ -2369,6 +2633,8 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             s->stats.iter_hist_shadow[k] = c[32 + k];
         }
         s->stragglers.assign(c + 64, c + 64 + 8 * std::min<unsigned long long>(c[48], STRAGGLER_MAX));
+        s->stats.instance_visits = c[49];
+        s->stats.shadow_instance_visits = c[50];
     }
     s->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MTSG_OK;
@@ -2396,7 +2662,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     if (!d || !out) { g_err = "null argument"; return MTSG_ERR_INVALID; }
     *out = nullptr;
     if (d->abi_version != MTSG_ABI_VERSION) { g_err = "ABI version mismatch"; return MTSG_ERR_INVALID; }
-    if (d->n_prims != d->n_triangles + d->n_rects || d->n_nodes == 0 || d->n_emitters == 0) {
+    if (d->n_prims != d->n_triangles + d->n_rects + d->n_instances || d->n_nodes == 0 || d->n_emitters == 0) {
         g_err = "inconsistent scene description";
         return MTSG_ERR_INVALID;
     }
@@ -2457,21 +2723,31 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     };
     // ---- device kd-tree layout from Mitsuba's KDNode array (same splits and
     // leaves, re-laid out): sibling pairs (host only, the input of the
-    // two-level blocks) + leaf-ordered TriAccel copies
+    // two-level blocks) + leaf-ordered TriAccel copies.  The top-level tree
+    // and every shape group's tree (two-level instancing) share both arrays.
     std::vector<uint4> pairs;
     std::vector<float4> triL;
     pairs.reserve(d->n_nodes / 2 + 1);
     triL.reserve((size_t)d->n_indices * 3);
     bool layoutOk = true;
+    const mtsg_kdnode *tNodes = d->nodes;
+    const uint32_t *tIdx = d->indices;
+    uint32_t tNodeCount = d->n_nodes, tIdxCount = d->n_indices;
     std::function<uint2(uint32_t, int)> convert = [&](uint32_t ni, int depth) -> uint2 {
-        const mtsg_kdnode &N = d->nodes[ni];
-        if (depth > 64 || ni >= d->n_nodes) { layoutOk = false; return make_uint2(0x80000000u, 0u); }
+        if (depth > 64 || ni >= tNodeCount) { layoutOk = false; return make_uint2(0x80000000u, 0u); }
+        const mtsg_kdnode &N = tNodes[ni];
         if (N.combined & 0x80000000u) {
             const uint32_t start = (uint32_t)(triL.size() / 3);
             for (uint32_t e = N.combined & 0x7FFFFFFFu; e < N.data; ++e) {
-                const uint32_t p = e < d->n_indices ? d->indices[e] : 0xFFFFFFFFu;
+                const uint32_t p = e < tIdxCount ? tIdx[e] : 0xFFFFFFFFu;
                 if (p >= d->n_prims) { layoutOk = false; break; }
-                const float4 *t = (const float4 *)(d->triaccel + p);
+                mtsg_triaccel ta = d->triaccel[p];
+                if (ta.k == MTSG_TRIACCEL_SHAPE && ta.shape_index < d->n_shapes &&
+                    d->shapes[ta.shape_index].type == MTSG_SHAPE_INSTANCE) {
+                    if (ta.prim_index >= d->n_instances) { layoutOk = false; break; }
+                    ta.k = KINST;
+                }
+                const float4 *t = (const float4 *)&ta;
                 triL.push_back(t[0]); triL.push_back(t[1]); triL.push_back(t[2]);
             }
             return make_uint2(0x80000000u | start, (uint32_t)(triL.size() / 3));
@@ -2485,6 +2761,20 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         return make_uint2((N.combined & 3u) | (pi << 2), N.data);
     };
     const uint2 root = convert(0, 0);
+    std::vector<uint2> groupRoots(d->n_groups);
+    if (d->n_instances && (!d->instances || !d->groups || !d->group_nodes || !d->group_indices)) layoutOk = false;
+    for (uint32_t g = 0; g < d->n_groups && layoutOk; ++g) {
+        const mtsg_group &G = d->groups[g];
+        if ((uint64_t)G.node_offset + G.n_nodes > d->n_group_nodes || (uint64_t)G.index_offset + G.n_indices > d->n_group_indices ||
+            G.n_nodes == 0) { layoutOk = false; break; }
+        tNodes = d->group_nodes + G.node_offset;
+        tIdx = d->group_indices + G.index_offset;
+        tNodeCount = G.n_nodes;
+        tIdxCount = G.n_indices;
+        groupRoots[g] = convert(0, 0);
+    }
+    for (uint32_t i = 0; i < d->n_instances && layoutOk; ++i)
+        if (d->instances[i].group >= d->n_groups) layoutOk = false;
     if (!layoutOk || pairs.size() >= (1u << 29) || triL.size() / 3 >= (1u << 30)) {
         g_err = "malformed or oversized kd-tree";
         return fail(MTSG_ERR_INVALID);
@@ -2510,6 +2800,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         return make_uint2((w.x & 3u) | 4u | (slot << 3), w.y);
     };
     const uint2 root2 = conv2(root, true, 0);
+    for (auto &gr : groupRoots) gr = conv2(gr, true, 0);
     blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));   // slack for the 3-slot fetch of the last slot
     if (blocks.size() >= (1u << 29)) { g_err = "kd-tree too large for the two-level layout"; return fail(MTSG_ERR_INVALID); }
     if (triL.empty()) triL.resize(3, make_float4(0, 0, 0, 0));
@@ -2529,6 +2820,29 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     ds.triL = dtriL; ds.vpos = dvpos; ds.vnrm = dvnrm;
     ds.tidx = dtidx; ds.shrec = dshrec; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
+    ds.inst = nullptr;
+    if (d->n_instances) {
+        std::vector<float4> in((size_t)8 * d->n_instances);
+        for (uint32_t i = 0; i < d->n_instances; ++i) {
+            const mtsg_instance &I = d->instances[i];
+            const mtsg_group &G = d->groups[I.group];
+            const float *L = I.to_local, *W = I.to_world;
+            float4 *o = &in[8 * (size_t)i];
+            for (int r = 0; r < 3; ++r) {
+                o[r] = make_float4(L[4 * r], L[4 * r + 1], L[4 * r + 2], L[4 * r + 3]);
+                o[3 + r] = make_float4(W[4 * r], W[4 * r + 1], W[4 * r + 2], W[4 * r + 3]);
+            }
+            const uint2 gr = groupRoots[I.group];
+            float r0, r1;
+            memcpy(&r0, &gr.x, 4);
+            memcpy(&r1, &gr.y, 4);
+            o[6] = make_float4(G.aabb_min[0], G.aabb_min[1], G.aabb_min[2], r0);
+            o[7] = make_float4(G.aabb_max[0], G.aabb_max[1], G.aabb_max[2], r1);
+        }
+        float4 *dinst;
+        if ((rc = up(in.data(), in.size(), &dinst))) return fail(rc);
+        ds.inst = dinst;
+    }
     // environment emitter tables (envmap.h)
     ds.has_env = d->has_envmap ? 1 : 0;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
@@ -2608,6 +2922,11 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, occKernel, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;
+    perCU = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace_s<false, 16, true>, TRACE_BLOCK, 0) != hipSuccess ||
+        perCU <= 0)
+        perCU = 4;
+    s->traceGridInst = s->cuCount * perCU;
     s->shadeGrid = s->cuCount * 8 * 256 / SHADE_BLOCK;
     if (const char *l = getenv("MTSG_LANES")) s->lanes = std::max(1, std::min(MTSG_MAX_LANES, atoi(l)));
     if (const char *g = getenv("MTSG_STAGGER")) s->stagger = std::max(0, std::min(16, atoi(g)));
@@ -2779,6 +3098,7 @@ static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, fl
     if (e == hipSuccess) e = alloc((void **)pb, f4, b.data());
     if (e == hipSuccess) e = alloc((void **)po, f4, out.data());
     if (e == hipSuccess && shadow) e = alloc((void **)&D.sh_c, f4, c.data());
+    if (e == hipSuccess && s->ds.inst) e = alloc((void **)&D.hitInst, (size_t)n * sizeof(uint32_t), nullptr);
     if (e == hipSuccess) e = alloc((void **)&D.cnt, CNT_WORDS * sizeof(uint32_t), nullptr);
     if (e == hipSuccess) e = alloc((void **)&D.ctr, CTR_WORDS * sizeof(unsigned long long), nullptr);
     if (e == hipSuccess && shadow) e = hipMemcpy(D.cnt + CNT_S0, &n, sizeof(uint32_t), hipMemcpyHostToDevice);
