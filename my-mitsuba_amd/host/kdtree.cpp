@@ -5,10 +5,12 @@
 // (include/mitsuba/render/gkdtree.h:734-744 parameters, :1792-1950 min-max
 // binning, :1954-2400 exact sweep, :1797-1842 leaf/bad-refine criteria,
 // sahkdtree3.h:39-84 SurfaceAreaHeuristic3) with perfect-split clipping of
-// triangles (Triangle::getClippedAABB).  Retraction of bad refines and
-// indirection nodes are not implemented: any valid kd-tree yields the same
-// closest hits, so the traversal kernels only rely on the node encoding
-// (gkdtree.h:452-600), not on Mitsuba's exact split choices.
+// triangles (Triangle::getClippedAABB) and retraction of splits whose
+// subtree ends up costlier than a leaf (m_retract, gkdtree.h:739-742,
+// 1895-1922; createLeafAfterRetraction :1665-1699).  Indirection nodes are
+// not implemented: any valid kd-tree yields the same closest hits, so the
+// traversal kernels only rely on the node encoding (gkdtree.h:452-600), not
+// on Mitsuba's exact split choices.
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -30,7 +32,7 @@ struct Sub {                         // independently built subtree
     std::vector<mtsg_kdnode> nodes;
     std::vector<uint32_t> indices;
     uint32_t maxDepth = 0;
-    size_t leaves = 0, nonEmpty = 0;
+    size_t leaves = 0, nonEmpty = 0, retracted = 0;
 };
 
 struct Split {
@@ -52,6 +54,18 @@ struct Builder {
     static float areaOf(const float lo[3], const float hi[3]) {
         float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
         return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+
+    // SurfaceAreaHeuristic3 probabilities of the two children
+    // (sahkdtree3.h:39-84, TreeConstructionHeuristic::operator())
+    static void probs(const AABB &box, int axis, float pos, float &pL, float &pR) {
+        V3 ext = box.extents();
+        float tmp = ext.x * ext.y + ext.y * ext.z + ext.x * ext.z;
+        float inv = tmp > 0 ? 1.0f / tmp : 0.0f;
+        int a1 = (axis + 1) % 3, a2 = (axis + 2) % 3;
+        float t0 = ext[a1] * ext[a2] * inv, t1 = (ext[a1] + ext[a2]) * inv;
+        pL = t0 + t1 * (pos - box.mn[axis]);
+        pR = t0 + t1 * (box.mx[axis] - pos);
     }
 
     // SurfaceAreaHeuristic3 as a cost for split (axis, pos) of box
@@ -178,22 +192,27 @@ struct Builder {
     };
 
     // Build subtree rooted at s.nodes[slot]; large nodes become jobs when
-    // `jobs` is non-null.
-    void build(Sub &s, uint32_t slot, const AABB &box, std::vector<BPrim> &prims, int depth,
-               int badRefines, std::vector<std::unique_ptr<Job>> *jobs) {
+    // `jobs` is non-null.  Returns the subtree's SAH cost (buildTreeMinMax /
+    // buildTree return values, gkdtree.h:1792-1923); a split whose final cost
+    // is not below the leaf cost is retracted into a leaf of the node's
+    // primitives (gkdtree.h:1910-1922).  Subtrees deferred to parallel jobs
+    // report their split estimate and are never retracted (nodes of that size
+    // always pay for their split).
+    float build(Sub &s, uint32_t slot, const AABB &box, std::vector<BPrim> &prims, int depth,
+                int badRefines, std::vector<std::unique_ptr<Job>> *jobs) {
         size_t N = prims.size();
         float leafCost = (float)N * P.queryCost;
-        if ((int)N <= P.stopPrims || depth >= maxDepth) { makeLeaf(s, slot, prims, depth); return; }
+        if ((int)N <= P.stopPrims || depth >= maxDepth) { makeLeaf(s, slot, prims, depth); return leafCost; }
         if (jobs && N <= parallelCut) {
             auto j = std::make_unique<Job>();
             j->box = box; j->prims = std::move(prims); j->depth = depth; j->badRefines = badRefines; j->slot = slot;
             jobs->push_back(std::move(j));
-            return;
+            return leafCost;
         }
         Split sp = N <= (size_t)P.exactSweepLimit ? findExact(box, prims) : findBinned(box, prims);
-        if (sp.axis < 0) { makeLeaf(s, slot, prims, depth); return; }
+        if (sp.axis < 0) { makeLeaf(s, slot, prims, depth); return leafCost; }
         if (sp.cost >= leafCost) {
-            if ((sp.cost > 4 * leafCost && N < 16) || badRefines >= P.maxBadRefines) { makeLeaf(s, slot, prims, depth); return; }
+            if ((sp.cost > 4 * leafCost && N < 16) || badRefines >= P.maxBadRefines) { makeLeaf(s, slot, prims, depth); return leafCost; }
             ++badRefines;
         }
         AABB lb = box, rb = box;
@@ -214,7 +233,10 @@ struct Builder {
             }
         }
         std::vector<BPrim>().swap(prims);
-        uint32_t c = (uint32_t)s.nodes.size();
+        const size_t jobsBefore = jobs ? jobs->size() : 0;
+        const uint32_t c = (uint32_t)s.nodes.size();
+        const size_t indexStart = s.indices.size(), leavesBefore = s.leaves, nonEmptyBefore = s.nonEmpty;
+        const uint32_t depthBefore = s.maxDepth;
         s.nodes.push_back({0, 0});
         s.nodes.push_back({0, 0});
         uint32_t rel = c - slot;
@@ -222,8 +244,27 @@ struct Builder {
         memcpy(&split, &sp.pos, 4);
         s.nodes[slot].combined = (uint32_t)ax | (rel << 2);
         s.nodes[slot].data = split;
-        build(s, c, lb, L, depth + 1, badRefines, jobs);
-        build(s, c + 1, rb, R, depth + 1, badRefines, jobs);
+        const float leftCost = build(s, c, lb, L, depth + 1, badRefines, jobs);
+        const float rightCost = build(s, c + 1, rb, R, depth + 1, badRefines, jobs);
+        float pL, pR;
+        probs(box, ax, sp.pos, pL, pR);
+        const float finalCost = P.traversalCost + (pL * leftCost + pR * rightCost);
+        const bool deferred = jobs && jobs->size() != jobsBefore;
+        if (!P.retract || deferred || finalCost < leafCost) return finalCost;
+        // retraction: tear up the subtree, one leaf with its unique primitives
+        std::vector<uint32_t> ids(s.indices.begin() + indexStart, s.indices.end());
+        std::sort(ids.begin(), ids.end());
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+        s.nodes.resize(c);
+        s.indices.resize(indexStart);
+        s.leaves = leavesBefore;
+        s.nonEmpty = nonEmptyBefore;
+        s.maxDepth = depthBefore;
+        s.retracted++;
+        std::vector<BPrim> leaf(ids.size());
+        for (size_t i = 0; i < ids.size(); ++i) leaf[i].id = ids[i];
+        makeLeaf(s, slot, leaf, depth);
+        return leafCost;
     }
 };
 
@@ -290,6 +331,7 @@ void buildKDTree(const PrimSource &src, const KDBuildParams &params, KDTree &out
     out.maxDepth = top.maxDepth;
     out.leafCount = top.leaves;
     out.nonEmptyLeaves = top.nonEmpty;
+    out.retractedSplits = top.retracted;
     for (auto &jp : jobs) {
         Sub &s = jp->result;
         uint32_t base = (uint32_t)out.nodes.size();
@@ -316,6 +358,7 @@ void buildKDTree(const PrimSource &src, const KDBuildParams &params, KDTree &out
         out.maxDepth = std::max(out.maxDepth, s.maxDepth);
         out.leafCount += s.leaves;
         out.nonEmptyLeaves += s.nonEmpty;
+        out.retractedSplits += s.retracted;
     }
     if (out.nodes.size() >= (1u << 28)) throw std::runtime_error("kd-tree has too many nodes");
 

@@ -1424,6 +1424,7 @@ std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::st
     if (const char *v = getenv("MTSH_KD_STOP_PRIMS")) scene->kd.stopPrims = atoi(v);
     if (const char *v = getenv("MTSH_KD_EXACT_LIMIT")) scene->kd.exactSweepLimit = atoi(v);
     if (const char *v = getenv("MTSH_KD_MAX_DEPTH")) scene->kd.maxDepth = atoi(v);
+    if (const char *v = getenv("MTSH_KD_RETRACT")) scene->kd.retract = atoi(v) != 0;
     Loader L(*scene);
     L.defines = defines;
     L.dirStack.push_back(dirName(path));

@@ -113,6 +113,7 @@ struct KDBuildParams {                // gkdtree.h:734-744 defaults
     int exactPrimThreshold = 65536;
     int exactSweepLimit = 65536;      // exact O(n log n) sweep below exactPrimThreshold (gkdtree.h:980, 1510), binned above
     bool clip = true;
+    bool retract = true;              // m_retract (gkdtree.h:742)
     int maxDepth = 0;                 // 0 = 8 + 1.3 log2(N) (gkdtree.h:986-988)
     int threads = 0;                  // 0 = hardware concurrency
 };
@@ -125,7 +126,7 @@ struct KDTree {
     uint32_t maxDepth = 0;
     double buildSeconds = 0;
     double sahCost = 0;
-    size_t leafCount = 0, nonEmptyLeaves = 0;
+    size_t leafCount = 0, nonEmptyLeaves = 0, retractedSplits = 0;
 };
 
 struct Scene {
