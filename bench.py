@@ -358,9 +358,12 @@ def main():
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": {"bunny15": "C3 bunny x15, 15 instances flattened to 1,041,765 world-space triangles, roughconductor Cu GGX 0.2",
+            "config": {"workload": {"bunny15": ("C3 bunny x15, 1,041,765 triangles, roughconductor Cu GGX 0.2" + (
+                                        ", 15 instances flattened to world-space triangles" if a.instancing == "flatten" else "")),
                                     "cbox": "C2 Cornell box, diffuse + area emitter",
-                                    "c5": "C5 dielectric + roughconductor bunnies, HDR envmap, maxDepth 64"}[a.workload],
+                                    "c5": "C5 dielectric + roughconductor bunnies under data/tests/envmap.exr (HDR envmap), maxDepth 64"}[a.workload]
+                       + (" [two-level: 15 instances of one 69,451-triangle shapegroup, Mitsuba's instance.cpp structure]"
+                          if a.instancing == "two-level" and a.workload == "bunny15" else ""),
                        "resolution": f"{params.tile_w}x{params.tile_h}", "spp": params.spp,
                        "max_depth": 64 if a.workload == "c5" else 8,
                        "samples_per_step": params.tile_w * params.tile_h * params.spp,

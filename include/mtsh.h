@@ -69,6 +69,12 @@ int mtsh_write_pfm(const char *path, int w, int h, const float *rgb);
  * Returns 0, or -1 on invalid arguments. */
 int mtsh_rough_transmittance(int distribution, float alpha, float eta, int n, float *trans, float *diffuse);
 
+/* Read an OpenEXR (NO/RLE/ZIPS/ZIP/PIZ, HALF or FLOAT) or PFM image as RGB
+ * float, rows top-down, as the environment emitter loads it
+ * (Bitmap::readOpenEXR, bitmap.cpp:2780).  rgb == NULL: only the size.
+ * Returns 0, or -1 (see mtsh_last_error; -2: rgb_capacity too small). */
+int mtsh_read_image(const char *path, int *w, int *h, float *rgb, size_t rgb_capacity);
+
 void mtsh_last_error(char *buf, size_t size);
 
 #ifdef __cplusplus

@@ -1,4 +1,5 @@
 // extern "C" surface of the host-side scene library (include/mtsh.h).
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -104,6 +105,19 @@ int mtsh_rough_transmittance(int distribution, float alpha, float eta, int n, fl
     }
     mtsh::roughTransmittanceSlice(distribution, alpha, eta, n, trans);
     if (diffuse) *diffuse = mtsh::roughDiffuseTransmittance(distribution, alpha, eta);
+    return 0;
+}
+
+int mtsh_read_image(const char *path, int *w, int *h, float *rgb, size_t rgb_capacity) {
+    if (!path || !w || !h) { g_err = "mtsh_read_image: invalid arguments"; return -1; }
+    std::string p(path), e;
+    std::vector<float> img;
+    const bool exr = p.size() > 4 && (p.substr(p.size() - 4) == ".exr" || p.substr(p.size() - 4) == ".EXR");
+    if (!(exr ? mtsh::readEXR(p, *w, *h, img, e) : mtsh::readPFM(p, *w, *h, img, e))) { g_err = e; return -1; }
+    if (rgb) {
+        if (rgb_capacity < img.size()) { g_err = "mtsh_read_image: buffer too small"; return -2; }
+        std::copy(img.begin(), img.end(), rgb);
+    }
     return 0;
 }
 

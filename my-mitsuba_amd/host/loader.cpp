@@ -1063,10 +1063,14 @@ struct Loader {
         if (file.empty()) throw err("envmap: missing 'filename'");
         std::string path = resolve(file);
         std::string ext = lower(path.size() > 4 ? path.substr(path.size() - 4) : path);
-        if (ext != ".pfm")
-            throw err("envmap \"" + file + "\": only PFM images are supported (no OpenEXR decoder in this build; re-encode as PFM)");
         std::string e2;
-        if (!readPFM(path, e.width, e.height, e.rgb, e2)) throw err("envmap \"" + file + "\": " + e2);
+        if (ext == ".pfm") {
+            if (!readPFM(path, e.width, e.height, e.rgb, e2)) throw err("envmap \"" + file + "\": " + e2);
+        } else if (ext == ".exr") {
+            if (!readEXR(path, e.width, e.height, e.rgb, e2)) throw err("envmap \"" + file + "\": " + e2);
+        } else {
+            throw err("envmap \"" + file + "\": only OpenEXR and PFM images are supported by this build");
+        }
         if (std::max(e.width, e.height) > 0xFFFF) throw err("Environment maps images must be smaller than 65536 pixels in width and height");
         scene.emitters.push_back(std::move(e));
     }

@@ -185,6 +185,9 @@ void buildQmcTables(int scramble, std::vector<uint32_t> &primes, std::vector<uin
 
 // PFM image (src/libcore/bitmap.cpp:3764-3814): RGB float, rows top-down
 bool readPFM(const std::string &path, int &w, int &h, std::vector<float> &rgb, std::string &err);
+// OpenEXR scanline image (Bitmap::readOpenEXR, bitmap.cpp:2780; exr.cpp):
+// RGB float, rows top-down
+bool readEXR(const std::string &path, int &w, int &h, std::vector<float> &rgb, std::string &err);
 
 // XML loading (src/librender/scenehandler.cpp), `-D name=value` defines
 std::unique_ptr<Scene> loadScene(const std::string &path,

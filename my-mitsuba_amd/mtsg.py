@@ -96,7 +96,7 @@ DEVICE_SYMBOLS = [
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
-    "mtsh_last_error",
+    "mtsh_read_image", "mtsh_last_error",
 ]
 PATH_SYMBOLS = [
     "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
@@ -146,6 +146,7 @@ def host_lib() -> C.CDLL:
         lib.mtsh_last_error.argtypes = [C.c_char_p, C.c_size_t]
         lib.mtsh_set_kd_threads.argtypes = [C.c_int]
         lib.mtsh_set_instancing.argtypes = [C.c_int]
+        lib.mtsh_read_image.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p, C.c_size_t]
         _host = lib
     return _host
 
@@ -245,6 +246,18 @@ def develop(rgbaw: np.ndarray) -> np.ndarray:
     h, w = rgbaw.shape[:2]
     out = np.zeros((h, w, 3), dtype=np.float32)
     host_lib().mtsh_develop(_ptr(rgbaw), w, h, _ptr(out))
+    return out
+
+
+def read_image(path: str) -> np.ndarray:
+    """OpenEXR / PFM image as (h, w, 3) float32, rows top-down (the envmap loader's reader)."""
+    lib = host_lib()
+    w, h = C.c_int(), C.c_int()
+    if lib.mtsh_read_image(path.encode(), C.byref(w), C.byref(h), None, 0) != 0:
+        raise RuntimeError(_err(lib, "mtsh_last_error"))
+    out = np.zeros((h.value, w.value, 3), np.float32)
+    if lib.mtsh_read_image(path.encode(), C.byref(w), C.byref(h), _ptr(out), out.size) != 0:
+        raise RuntimeError(_err(lib, "mtsh_last_error"))
     return out
 
 

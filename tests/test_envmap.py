@@ -1,11 +1,13 @@
 """Environment emitter (src/emitters/envmap.cpp, mipmap.h) on the CPU side:
-PFM loading and the MIP pyramid, the sampling CDFs, and sample-vs-pdf
-consistency of EnvironmentMap::sampleDirect.  The χ² check mirrors the
-EmitterAdapter of the reference's src/tests/test_chisquare.cpp:342-388,580-615
-(envmap rotated 40 degrees about x, as in data/tests/test_emitter.xml).  The
-reference's own envmap.exr cannot be decoded here (PIZ-compressed OpenEXR, no
-decoder in the image), so a seeded random map stands in: parity unpinned at
-the EXR boundary."""
+PFM / OpenEXR loading and the MIP pyramid, the sampling CDFs, and
+sample-vs-pdf consistency of EnvironmentMap::sampleDirect.  The χ² check
+mirrors the EmitterAdapter of the reference's
+src/tests/test_chisquare.cpp:342-388,580-615 on the reference's own
+data/tests/envmap.exr (PIZ-compressed HALF RGB, decoded by host/exr.cpp)
+rotated 40 degrees about x, as data/tests/test_emitter.xml sets it up, and on
+a seeded random map.  No reference test pins the decoded texel values (the
+reference links OpenEXR): the decoder is checked by its own round trips
+(NO / ZIP writers below) and by the image's structure."""
 import ctypes as C
 import math
 import os
@@ -43,13 +45,17 @@ SCENE = """<scene version="0.5.0">
 """
 
 
-def make_scene(tmp_path, img, scale=1.0, angle=40.0):
+def make_scene(tmp_path, img, scale=1.0, angle=40.0, env=None):
     import mtsg
-    env = tmp_path / "env.pfm"
-    write_pfm(env, img)
+    if env is None:
+        env = tmp_path / "env.pfm"
+        write_pfm(env, img)
     xml = tmp_path / "scene.xml"
-    xml.write_text(SCENE.format(env=env.name, scale=scale, angle=angle))
+    xml.write_text(SCENE.format(env=str(env), scale=scale, angle=angle))
     return mtsg.Scene(str(xml))
+
+
+EXR = os.path.join(SCENES, "envmap.exr")   # the reference's data/tests/envmap.exr
 
 
 def bind():
@@ -96,13 +102,7 @@ def test_half_precision_texels(tmp_path):
     np.testing.assert_array_equal(v[0], np.float32(np.float16(1.0 / 3.0)))
 
 
-def test_envmap_sampling_matches_pdf(tmp_path):
-    rng = np.random.default_rng(11)
-    base = rng.gamma(2.0, 1.0, size=(32, 64, 3)).astype(np.float32)
-    # smooth it a little and add one bright region, like a sky with a sun
-    base = 0.5 * base + 0.5 * np.roll(base, 1, axis=1)
-    base[6:9, 40:44] *= 25.0
-    sc = make_scene(tmp_path, base)
+def check_sampling_matches_pdf(sc, rng):
     L, P = bind()
     n = THETA_BINS * PHI_BINS * 1000
     u2 = rng.random((n, 2), dtype=np.float32)
@@ -135,6 +135,92 @@ def test_envmap_sampling_matches_pdf(tmp_path):
     assert abs(exp.sum() / n - 1) < 0.02
     pval = chi2_pvalue(observed_counts(d), exp)
     assert pval >= SIGNIFICANCE, pval
+
+
+def test_envmap_sampling_matches_pdf(tmp_path):
+    rng = np.random.default_rng(11)
+    base = rng.gamma(2.0, 1.0, size=(32, 64, 3)).astype(np.float32)
+    # smooth it a little and add one bright region, like a sky with a sun
+    base = 0.5 * base + 0.5 * np.roll(base, 1, axis=1)
+    base[6:9, 40:44] *= 25.0
+    check_sampling_matches_pdf(make_scene(tmp_path, base), rng)
+
+
+def test_reference_envmap_sampling_matches_pdf(tmp_path):
+    # the EmitterAdapter instance of test_chisquare.cpp:575-620 on
+    # data/tests/test_emitter.xml's own map (envmap.exr, rotated 40 deg about x)
+    check_sampling_matches_pdf(make_scene(tmp_path, None, env=EXR), np.random.default_rng(12))
+
+
+def test_exr_decodes_the_reference_envmap():
+    import mtsg
+    img = mtsg.read_image(EXR)
+    assert img.shape == (256, 512, 3)            # dataWindow (0,0)-(511,255), B/G/R HALF, PIZ
+    assert np.isfinite(img).all() and img.min() > 0
+    # HALF source: every value is exactly a binary16
+    np.testing.assert_array_equal(img.astype(np.float16).astype(np.float32), img)
+    # an image, not noise: neighbouring texels are ~10x closer in log
+    # luminance than random pairs (a wrong Huffman / wavelet decode is noise)
+    lum = np.log(img.mean(axis=2))
+    d = np.abs(np.diff(lum, axis=1)).mean()
+    rnd = np.abs(lum - np.random.default_rng(0).permutation(lum.ravel()).reshape(lum.shape)).mean()
+    assert d < 0.15 * rnd
+    # the ceiling (top rows) is brighter than the floor (bottom rows):
+    # scanline order and the vertical orientation are right
+    assert img[:32].mean() > img[-32:].mean()
+    assert abs(float(img.mean()) - 0.3306) < 2e-3
+
+
+def _write_exr(path, img, compression, half):
+    """Minimal scanline OpenEXR writer (NO_COMPRESSION / ZIP), B/G/R."""
+    import struct
+    import zlib
+    h, w, _ = img.shape
+    def attr(name, typ, data):
+        return name.encode() + b"\0" + typ.encode() + b"\0" + struct.pack("<i", len(data)) + data
+    ptype = 1 if half else 2
+    chl = b"".join(c.encode() + b"\0" + struct.pack("<iB3xii", ptype, 0, 1, 1) for c in "BGR") + b"\0"
+    hdr = (struct.pack("<II", 20000630, 2) + attr("channels", "chlist", chl) +
+           attr("compression", "compression", bytes([compression])) +
+           attr("dataWindow", "box2i", struct.pack("<4i", 0, 0, w - 1, h - 1)) +
+           attr("displayWindow", "box2i", struct.pack("<4i", 0, 0, w - 1, h - 1)) +
+           attr("lineOrder", "lineOrder", b"\0") + attr("pixelAspectRatio", "float", struct.pack("<f", 1)) +
+           attr("screenWindowCenter", "v2f", struct.pack("<2f", 0, 0)) + attr("screenWindowWidth", "float", struct.pack("<f", 1)) + b"\0")
+    lpc = 16 if compression == 3 else 1
+    chunks = []
+    dt = "<f2" if half else "<f4"
+    for y0 in range(0, h, lpc):
+        raw = b"".join(np.ascontiguousarray(img[y, :, c]).astype(dt).tobytes() for y in range(y0, min(h, y0 + lpc)) for c in (2, 1, 0))
+        if compression == 3:
+            b = np.frombuffer(raw, np.uint8)
+            t = np.concatenate([b[0::2], b[1::2]])
+            p = t.astype(np.int32)
+            p[1:] = (t[1:].astype(np.int32) - t[:-1].astype(np.int32) + 128 + 256) & 255
+            data = zlib.compress(p.astype(np.uint8).tobytes())
+            if len(data) >= len(raw):   # the format stores a chunk raw when compression does not pay
+                data = raw
+        else:
+            data = raw
+        chunks.append(struct.pack("<ii", y0, len(data)) + data)
+    off = len(hdr) + 8 * len(chunks)
+    table = b""
+    for c in chunks:
+        table += struct.pack("<Q", off)
+        off += len(c)
+    open(path, "wb").write(hdr + table + b"".join(chunks))
+
+
+@pytest.mark.parametrize("compression,half", [(0, True), (0, False), (3, True), (3, False)],
+                         ids=["none-half", "none-float", "zip-half", "zip-float"])
+def test_exr_round_trip(tmp_path, compression, half):
+    import mtsg
+    rng = np.random.default_rng(3)
+    img = rng.gamma(2.0, 1.0, size=(37, 53, 3)).astype(np.float32)
+    if half:
+        img = img.astype(np.float16).astype(np.float32)
+    p = tmp_path / "t.exr"
+    _write_exr(str(p), img, compression, half)
+    np.testing.assert_array_equal(mtsg.read_image(str(p)), img)
 
 
 def test_env_glass_scene_loads():

@@ -300,3 +300,13 @@ def test_c3_full_frame_parity():
     assert (p.tile_w, p.tile_h, p.max_depth) == (1280, 720, 8)
     l1, mean = check_render(c, gi)
     print(f"C3 1280x720x2spp: per-pixel L1 {l1:.3e}, mean {mean:.4f}, L1/mean {l1 / mean:.2e}")
+
+
+def test_envmap_synthetic_sky_parity():
+    # round 1's synthetic sky (tools/gen_envmap.py) as a second environment map
+    scene = mtsg.Scene(os.path.join(SCENES, "env_glass.xml"),
+                       {"width": 48, "height": 27, "spp": 8, "maxDepth": 16, "envmap": "sky512.pfm"})
+    g = mtsg.GPUScene(scene, 0)
+    _, c, gi = render_pair(scene, g)
+    g.close()
+    check_render(c, gi)
