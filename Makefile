@@ -28,8 +28,9 @@ host: $(HOST_LIB)
 device: $(DEV_LIB)
 oracle: $(ORACLE) $(ORACLE_FAST)
 
-$(HOST_LIB): $(HOST_SRC) $(HOST_HDR)
-	$(CXX) -std=c++17 -O2 -g -fPIC -shared -Wall -o $@ $(HOST_SRC) -lz -lpthread
+SOBOL_BIN := $(PKG)/data/sobol_tables.bin
+$(HOST_LIB): $(HOST_SRC) $(HOST_HDR) $(SOBOL_BIN)
+	$(CXX) -std=c++17 -O2 -g -fPIC -shared -Wall -DMTSH_SOBOL_BIN='"$(SOBOL_BIN)"' -o $@ $(HOST_SRC) -lz -lpthread
 
 # gfx950 only: no dual CUDA/HIP paths, no hipify output.
 # -ffp-contract=off: no FMA contraction, like Mitsuba's SSE2 build

@@ -236,8 +236,17 @@ typedef struct mtsg_camera {
  * from sampleTEA seeded with the scramble value. */
 enum {
     MTSG_SAMPLER_INDEPENDENT = 0, MTSG_SAMPLER_HALTON = 1, MTSG_SAMPLER_HAMMERSLEY = 2,
-    MTSG_SAMPLER_LDSAMPLER = 3
+    MTSG_SAMPLER_LDSAMPLER = 3, MTSG_SAMPLER_SOBOL = 4
 };
+/* sobol (src/samplers/sobol.cpp:86-250): Gruenschloss's Sobol' enumeration
+ * with Joe & Kuo's direction numbers (sobolseq.cpp / sobolseq.h), single
+ * precision: value = min(XOR of the generator columns of the set bits of the
+ * index, scrambled) * 2^-32; the film is bucketed (setFilmResolution with
+ * bucketed = true), so the index of sample s of pixel (x, y) is
+ * look_up(log2 res, s, x, y, scramble) and the first 2D request returns the
+ * position inside the pixel. */
+#define MTSG_SOBOL_DIMS 1024
+#define MTSG_SOBOL_COLUMNS 52
 #define MTSG_QMC_PRIMES 1024          /* primeTableSize (qmc.h:38)            */
 
 typedef struct mtsg_sampler {
@@ -291,6 +300,12 @@ typedef struct mtsg_scene_desc {
     const uint16_t *qmc_perm;     /* digit permutation of base primes[i] at
                                      qmc_perm + qmc_perm_offset[i]; NULL when
                                      unscrambled (scramble 0) or unused     */
+    /* sobol sampler tables (NULL unless MTSG_SAMPLER_SOBOL) */
+    uint64_t sobol_scramble;      /* sampleTEA of 'scramble' (sobol.cpp:92-102), 0: none */
+    const uint32_t *sobol_matrices;  /* matrices32: MTSG_SOBOL_DIMS x MTSG_SOBOL_COLUMNS */
+    uint32_t sobol_vdc_rows, sobol_vdc_inv_rows;
+    const uint64_t *sobol_vdc;    /* vdc_sobol_matrices[rows][MTSG_SOBOL_COLUMNS]     */
+    const uint64_t *sobol_vdc_inv;   /* vdc_sobol_matrices_inv[inv rows][COLUMNS]  */
     /* two-level instancing (n_instances = 0: none) */
     uint32_t n_instances;
     const mtsg_instance *instances;

@@ -104,7 +104,9 @@ struct DevIntegrator {
 // `n2` 2D requests into the path
 DEV PathSampler path_sampler(const DevIntegrator &I, int x, int y, uint32_t s, uint32_t dim, uint32_t n2) {
     const uint64_t pix = (uint64_t)y * (uint64_t)I.film_w + (uint64_t)x;
-    return PathSampler{counterKey(I.seed, pix * I.spp + s), dim, n2, s, x, y, false};
+    PathSampler p{counterKey(I.seed, pix * I.spp + s), dim, n2, s, x, y, false, 0ull};
+    if (I.smp.type == MTSG_SAMPLER_SOBOL) p.qidx = sobol_index(I.smp, s, x, y);
+    return p;
 }
 DEV uint64_t pixel_index(const DevIntegrator &I, const PathSampler &p) {
     return (uint64_t)p.y * (uint64_t)I.film_w + (uint64_t)p.x;
@@ -125,6 +127,7 @@ DEV void camera_jitter(const DevIntegrator &I, int x, int y, uint32_t s, float &
         case MTSG_SAMPLER_HALTON: next2D<MTSG_SAMPLER_HALTON>(I, p, a, b); break;
         case MTSG_SAMPLER_HAMMERSLEY: next2D<MTSG_SAMPLER_HAMMERSLEY>(I, p, a, b); break;
         case MTSG_SAMPLER_LDSAMPLER: next2D<MTSG_SAMPLER_LDSAMPLER>(I, p, a, b); break;
+        case MTSG_SAMPLER_SOBOL: next2D<MTSG_SAMPLER_SOBOL>(I, p, a, b); break;
         default: next2D<MTSG_SAMPLER_INDEPENDENT>(I, p, a, b); break;
     }
 }
@@ -1967,7 +1970,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                     }
                 }
             }
-            if ((SMP == MTSG_SAMPLER_HALTON || SMP == MTSG_SAMPLER_HAMMERSLEY) && smp.dimError)
+            if ((SMP == MTSG_SAMPLER_HALTON || SMP == MTSG_SAMPLER_HAMMERSLEY || SMP == MTSG_SAMPLER_SOBOL) && smp.dimError)
                 atomicOr(&P.cnt[CNT_ERR], 1u);   // the render fails as Mitsuba's Log(EError) would
             const float4 finalL = make_float4(L.x, L.y, L.z, L4.w);
             if (cont) {
@@ -2178,6 +2181,9 @@ struct mtsg_scene {
     unsigned long long *waveTimes = nullptr;     // MTSG_FLAG_WAVETIME: [launch][wave][WT_WORDS]
     uint32_t wtLaunches = 0;
     bool extBsdfs = false;   // conductor / plastic / twosided records present (k_shade<..., true>)
+    const uint32_t *sobolM = nullptr;        // sobol sampler tables (device)
+    const uint64_t *sobolVdc = nullptr, *sobolVdcInv = nullptr;
+    uint64_t sobolScramble = 0;
 };
 
 namespace {
@@ -2286,6 +2292,9 @@ void launch_shade_env(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, 
         case MTSG_SAMPLER_LDSAMPLER:
             hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_LDSAMPLER, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
             break;
+        case MTSG_SAMPLER_SOBOL:
+            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_SOBOL, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
+            break;
         default:
             hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_INDEPENDENT, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
     }
@@ -2311,6 +2320,19 @@ DevSampler make_sampler(const mtsg_scene *s, uint32_t spp) {
     S.primes = s->ds.qmcPrimes;
     S.off = s->ds.qmcOff;
     S.perm = s->ds.qmcPerm;
+    S.sobolM = s->sobolM;
+    S.vdc = s->sobolVdc;
+    S.vdcInv = s->sobolVdcInv;
+    S.sobolScramble = s->sobolScramble;
+    S.logRes = 0;
+    S.sobolRes = 1.0f;
+    if (S.type == MTSG_SAMPLER_SOBOL) {
+        // setFilmResolution(crop size, bucketed = true) (sobol.cpp:147-158)
+        uint32_t r = 1;
+        while (r < (uint32_t)std::max(s->cam.crop_w, s->cam.crop_h)) r <<= 1;
+        S.sobolRes = (float)r;
+        while ((1u << (S.logRes + 1)) <= r) ++S.logRes;
+    }
     for (int b = 0; b < 2; ++b)
         for (int j = 0; j < 3; ++j) S.inv[b][j] = (uint16_t)s->qmcInv[b][j];
     const int crop[2] = {s->cam.crop_w, s->cam.crop_h};
@@ -2343,6 +2365,13 @@ DevSampler make_sampler(const mtsg_scene *s, uint32_t spp) {
         S.stride = S.res[1];
     }
     return S;
+}
+
+// Mitsuba's Log(EError) of Halton/Hammersley (halton.cpp:343-386) and sobol (sobol.cpp:223-239)
+const char *dim_error(int sampler) {
+    return sampler == MTSG_SAMPLER_SOBOL
+               ? "Lookup dimension exceeds the direction number table size! You may have to reduce the 'maxDepth' parameter of your integrator."
+               : "Lookup dimension exceeds the prime number table size! You may have to reduce the 'maxDepth' parameter of your integrator.";
 }
 
 int validate(const mtsg_render_params *p, const mtsg_scene *s) {
@@ -2554,8 +2583,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             account(l, L.last);
             // the error word is sticky within the batch: the last copy holds it
             if (hostCnt(l, L.last)[CNT_ERR]) {
-                g_err = "Lookup dimension exceeds the prime number table size! "
-                        "You may have to reduce the 'maxDepth' parameter of your integrator.";
+                g_err = dim_error(s->samplerType);
                 return MTSG_ERR_INVALID;
             }
         }
@@ -2894,7 +2922,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     // sampler and its quasi-Monte Carlo tables
     s->samplerType = d->sampler.type;
     s->samplerDim = d->sampler.dimension;
-    if (s->samplerType < MTSG_SAMPLER_INDEPENDENT || s->samplerType > MTSG_SAMPLER_LDSAMPLER) {
+    if (s->samplerType < MTSG_SAMPLER_INDEPENDENT || s->samplerType > MTSG_SAMPLER_SOBOL) {
         g_err = "unknown sampler type";
         return fail(MTSG_ERR_INVALID);
     }
@@ -2914,6 +2942,23 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
             for (int b = 0; b < 2; ++b)
                 for (uint32_t j = 0; j < d->qmc_primes[b]; ++j) s->qmcInv[b][d->qmc_perm[d->qmc_perm_offset[b] + j]] = (int)j;
         }
+    }
+    if (s->samplerType == MTSG_SAMPLER_SOBOL) {
+        if (!d->sobol_matrices || !d->sobol_vdc || !d->sobol_vdc_inv) { g_err = "sampler: missing sobol tables"; return fail(MTSG_ERR_INVALID); }
+        uint32_t r = 1, m = 0;
+        while (r < (uint32_t)std::max(d->camera.crop_w, d->camera.crop_h)) r <<= 1;
+        while ((1u << (m + 1)) <= r) ++m;
+        if (m > 1 && (m > d->sobol_vdc_inv_rows || m > d->sobol_vdc_rows + 1)) { g_err = "sobol: film too large for the look_up tables"; return fail(MTSG_ERR_INVALID); }
+        uint32_t *dm;
+        uint64_t *dv, *dvi;
+        if ((rc = up(d->sobol_matrices, (size_t)MTSG_SOBOL_DIMS * MTSG_SOBOL_COLUMNS, &dm)) ||
+            (rc = up(d->sobol_vdc, (size_t)d->sobol_vdc_rows * MTSG_SOBOL_COLUMNS + MTSG_SOBOL_COLUMNS, &dv)) ||
+            (rc = up(d->sobol_vdc_inv, (size_t)d->sobol_vdc_inv_rows * MTSG_SOBOL_COLUMNS, &dvi)))
+            return fail(rc);
+        s->sobolM = dm;
+        s->sobolVdc = dv;
+        s->sobolVdcInv = dvi;
+        s->sobolScramble = d->sobol_scramble;
     }
     // persistent grids from the occupancy query
     if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
@@ -3163,6 +3208,7 @@ __global__ void k_sampler_draws(DevIntegrator I, int x, int y, uint32_t s, uint3
             if (t == MTSG_SAMPLER_HALTON) next2D<MTSG_SAMPLER_HALTON>(I, p, a, b);
             else if (t == MTSG_SAMPLER_HAMMERSLEY) next2D<MTSG_SAMPLER_HAMMERSLEY>(I, p, a, b);
             else if (t == MTSG_SAMPLER_LDSAMPLER) next2D<MTSG_SAMPLER_LDSAMPLER>(I, p, a, b);
+            else if (t == MTSG_SAMPLER_SOBOL) next2D<MTSG_SAMPLER_SOBOL>(I, p, a, b);
             else next2D<MTSG_SAMPLER_INDEPENDENT>(I, p, a, b);
             *out++ = a;
             *out++ = b;
@@ -3171,6 +3217,7 @@ __global__ void k_sampler_draws(DevIntegrator I, int x, int y, uint32_t s, uint3
             if (t == MTSG_SAMPLER_HALTON) a = next1D<MTSG_SAMPLER_HALTON>(I, p);
             else if (t == MTSG_SAMPLER_HAMMERSLEY) a = next1D<MTSG_SAMPLER_HAMMERSLEY>(I, p);
             else if (t == MTSG_SAMPLER_LDSAMPLER) a = next1D<MTSG_SAMPLER_LDSAMPLER>(I, p);
+            else if (t == MTSG_SAMPLER_SOBOL) a = next1D<MTSG_SAMPLER_SOBOL>(I, p);
             else a = next1D<MTSG_SAMPLER_INDEPENDENT>(I, p);
             *out++ = a;
         }
@@ -3209,8 +3256,7 @@ int mtsg_sampler_draws(mtsg_scene *s, const mtsg_render_params *p, int x, int y,
     cleanup();
     if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
     if (err) {
-        g_err = "Lookup dimension exceeds the prime number table size! "
-                "You may have to reduce the 'maxDepth' parameter of your integrator.";
+        g_err = dim_error(s->samplerType);
         return MTSG_ERR_INVALID;
     }
     return MTSG_OK;

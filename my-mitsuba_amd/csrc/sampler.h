@@ -33,6 +33,13 @@ struct DevSampler {
     uint16_t inv[2][3];            // inverse digit permutations of bases 2, 3
     const uint32_t *primes, *off;  // MTSG_QMC_PRIMES each
     const uint16_t *perm;          // nullptr: unscrambled
+    // sobol (sobol.cpp, sobolseq.h): generator matrices, look_up tables,
+    // bucketed resolution 2^logRes, TEA'd scramble
+    const uint32_t *sobolM;
+    const uint64_t *vdc, *vdcInv;
+    uint32_t logRes;
+    float sobolRes;
+    uint64_t sobolScramble;
 };
 
 constexpr float kOneMinusEps = 0x1.fffffep-1f;   // ONE_MINUS_EPS_FLT (constants.h:56)
@@ -123,6 +130,31 @@ DEV uint64_t qmc_pixel_offset(const DevSampler &S, int x, int y, uint32_t spp) {
     return (uint64_t)px * S.res[1] * spp + inverse_scrambled_radical_inverse(2, py, S.logH, S.perm ? S.inv[0] : nullptr);
 }
 
+// sobolseq.h:43-58 sampleSingle
+DEV float sobol_sample(const DevSampler &S, uint64_t index, uint32_t dim) {
+    uint32_t result = (uint32_t)S.sobolScramble;
+    const uint32_t *col = S.sobolM + dim * MTSG_SOBOL_COLUMNS;
+    uint32_t lo = (uint32_t)index, hi = (uint32_t)(index >> 32);
+    for (uint32_t i = 0; lo; lo &= lo - 1u) result ^= col[__builtin_ctz(lo)];
+    for (; hi; hi &= hi - 1u) result ^= col[32 + __builtin_ctz(hi)];
+    return fminf((float)result * (1.0f / 4294967296.0f), kOneMinusEps);
+}
+
+// sobolseq.h:99-131 look_up (single precision), as SobolSampler::setSampleIndex
+// uses it when the film is bucketed (sobol.cpp:204-216)
+DEV uint64_t sobol_index(const DevSampler &S, uint32_t frame, int x, int y) {
+    if (!(S.logRes > 1 && x >= 0)) return (uint64_t)frame;
+    const uint32_t m = S.logRes;
+    uint64_t index = (uint64_t)frame << (2 * m);
+    uint64_t delta = 0;
+    const uint64_t *v = S.vdc + (size_t)(m - 1) * MTSG_SOBOL_COLUMNS, *vi = S.vdcInv + (size_t)(m - 1) * MTSG_SOBOL_COLUMNS;
+    for (uint32_t f = frame; f; f &= f - 1u) delta ^= v[__builtin_ctz(f)];
+    const uint64_t scramble = (S.sobolScramble & 0xFFFFFFFFull) >> (32 - m);
+    uint64_t b = ((((uint64_t)(uint32_t)x ^ scramble) << m) | ((uint64_t)(uint32_t)y ^ scramble)) ^ delta;
+    for (; b; b &= b - 1ull) index ^= vi[__builtin_ctzll(b)];
+    return index;
+}
+
 // One path's draws.  `dim` = dimensions consumed so far (next1D: 1,
 // next2D: 2), `n2` = next2D calls so far; both live in the path state.
 struct PathSampler {
@@ -130,6 +162,7 @@ struct PathSampler {
     uint32_t dim, n2, s;           // dimensions used, 2D requests, sample index
     int x, y;                      // film pixel
     bool dimError;                 // QMC dimension limit exceeded (Mitsuba: EError)
+    uint64_t qidx;                 // sobol: the sample's index in the sequence (sobol_index)
 };
 
 template <int KIND>
@@ -146,6 +179,10 @@ DEV float qmc_float(const DevSampler &S, PathSampler &p, uint64_t idx) {
 // carries only its sampler's code)
 template <int KIND>
 DEV float smp_next1D(const DevSampler &S, PathSampler &p, uint32_t seed, uint64_t pixelIndex, uint32_t spp) {
+    if (KIND == MTSG_SAMPLER_SOBOL) {   // sobol.cpp:218-228
+        if (p.dim >= MTSG_SOBOL_DIMS) { p.dimError = true; p.dim++; return 0.0f; }
+        return sobol_sample(S, p.qidx, p.dim++);
+    }
     if (KIND == MTSG_SAMPLER_HALTON || KIND == MTSG_SAMPLER_HAMMERSLEY) {
         if (p.dim >= MTSG_QMC_PRIMES) { p.dimError = true; p.dim++; return 0.0f; }
         return qmc_float<KIND>(S, p, qmc_pixel_offset(S, p.x, p.y, spp) + (uint64_t)S.stride * p.s);
@@ -163,6 +200,18 @@ DEV float smp_next1D(const DevSampler &S, PathSampler &p, uint32_t seed, uint64_
 
 template <int KIND>
 DEV void smp_next2D(const DevSampler &S, PathSampler &p, uint32_t seed, uint64_t pixelIndex, uint32_t spp, float &a, float &b) {
+    if (KIND == MTSG_SAMPLER_SOBOL) {   // sobol.cpp:230-250
+        if (p.dim + 1 >= MTSG_SOBOL_DIMS) { p.dimError = true; p.dim += 2; p.n2++; a = b = 0.0f; return; }
+        if (p.dim == 0 && p.qidx != (uint64_t)p.s) {
+            a = sobol_sample(S, p.qidx, p.dim++) * S.sobolRes - (float)p.x;
+            b = sobol_sample(S, p.qidx, p.dim++) * S.sobolRes - (float)p.y;
+        } else {
+            a = sobol_sample(S, p.qidx, p.dim++);
+            b = sobol_sample(S, p.qidx, p.dim++);
+        }
+        p.n2++;
+        return;
+    }
     if (KIND == MTSG_SAMPLER_HALTON || KIND == MTSG_SAMPLER_HAMMERSLEY) {
         if (p.dim + 1 >= MTSG_QMC_PRIMES) { p.dimError = true; p.dim += 2; p.n2++; a = b = 0.0f; return; }
         const uint64_t idx = qmc_pixel_offset(S, p.x, p.y, spp) + (uint64_t)S.stride * p.s;

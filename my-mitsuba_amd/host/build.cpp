@@ -475,6 +475,10 @@ void Scene::finalize() {
         d.qmc_perm_offset = qmcOffsets.data();
         d.qmc_perm = qmcPerm.empty() ? nullptr : qmcPerm.data();
     }
+    if (sampler.type == MTSG_SAMPLER_SOBOL) {
+        sobolTables(d.sobol_matrices, d.sobol_vdc, d.sobol_vdc_rows, d.sobol_vdc_inv, d.sobol_vdc_inv_rows);
+        d.sobol_scramble = sobolScramble(sobolScrambleProp);
+    }
     // ---------------- environment emitter ----------------
     d.has_envmap = 0;
     for (size_t i = 0; i < emitters.size(); ++i) {

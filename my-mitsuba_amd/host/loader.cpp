@@ -1333,9 +1333,13 @@ struct Loader {
                     uint32_t c = (uint32_t)std::max(1, scene.sampleCount), r = 1;
                     while (r < c) r <<= 1;
                     scene.sampleCount = (int)r;
+                } else if (st == "sobol") {
+                    // sobol.cpp:86-107
+                    smp.type = MTSG_SAMPLER_SOBOL;
+                    scene.sobolScrambleProp = (uint64_t)sp.getInt("scramble", 0);
                 } else {
                     throw err("sampler \"" + st + "\" is outside this build's scope "
-                              "(independent, halton, hammersley, ldsampler)");
+                              "(independent, halton, hammersley, ldsampler, sobol)");
                 }
                 if (scene.sampleCount <= 0) throw err("sampleCount must be > 0");
                 scene.samplerType = st;

@@ -144,6 +144,7 @@ struct Scene {
     bool twoLevel = false;            // MTSH_INSTANCING_TWO_LEVEL
     std::string samplerType = "independent";
     mtsg_sampler sampler{MTSG_SAMPLER_INDEPENDENT, -1, 4, 0};
+    uint64_t sobolScrambleProp = 0;   // sobol 'scramble' (before TEA)
     KDBuildParams kd;
 
     // ---- flattened (filled by finalize()) ----
@@ -182,6 +183,11 @@ void buildEnvmap(const Emitter &e, const float aabbMin[3], const float aabbMax[3
 // (empty for scramble 0)
 void buildQmcTables(int scramble, std::vector<uint32_t> &primes, std::vector<uint32_t> &offsets,
                     std::vector<uint16_t> &perm);
+
+// Sobol' tables (qmc.cpp, embedded data of sobolseq.cpp) and the TEA'd scramble
+uint64_t sobolScramble(uint64_t scramble);
+void sobolTables(const uint32_t *&matrices, const uint64_t *&vdc, uint32_t &vdcRows, const uint64_t *&vdcInv,
+                 uint32_t &vdcInvRows);
 
 // PFM image (src/libcore/bitmap.cpp:3764-3814): RGB float, rows top-down
 bool readPFM(const std::string &path, int &w, int &h, std::vector<float> &rgb, std::string &err);

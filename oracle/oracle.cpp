@@ -399,6 +399,8 @@ uint32_t ldShuffle(uint32_t s, uint32_t bits, uint64_t h) {
     return x;
 }
 constexpr uint32_t kLdSalt = 0x6C64736Du;   // "ldsm": pixel keys of the ldsampler
+constexpr const char *kSobolDimError = "Lookup dimension exceeds the direction number table size! "
+                                       "You may have to reduce the 'maxDepth' parameter of your integrator.";
 constexpr const char *kDimError = "Lookup dimension exceeds the prime number table size! "
                                   "You may have to reduce the 'maxDepth' parameter of your integrator.";
 
@@ -418,6 +420,33 @@ struct Qmc {
     float factor = 1.0f;
     int ldDim = 4;
     uint32_t ldBits = 0;
+    // sobol.cpp:147-158 (bucketed): resolution = roundToPowerOfTwo(max crop side)
+    const uint32_t *sobolM = nullptr;
+    const uint64_t *vdc = nullptr, *vdcInv = nullptr;
+    uint32_t logRes = 0;
+    float sobolRes = 1.0f;
+    uint64_t sobolScramble = 0;
+
+    // sobolseq.h:43-58 sampleSingle
+    float sobolSample(uint64_t index, uint32_t dim) const {
+        uint32_t result = (uint32_t)sobolScramble;
+        for (uint32_t i = dim * MTSG_SOBOL_COLUMNS; index; index >>= 1, ++i)
+            if (index & 1) result ^= sobolM[i];
+        return std::min(result * (1.0f / 4294967296.0f), kOneMinusEps);
+    }
+    // sobolseq.h:99-131 look_up (single precision)
+    uint64_t sobolLookUp(uint32_t m, uint32_t frame, uint32_t px, uint32_t py) const {
+        const uint32_t m2 = m << 1;
+        uint64_t index = (uint64_t)frame << m2;
+        uint64_t delta = 0;
+        for (uint32_t c = 0; frame; frame >>= 1, ++c)
+            if (frame & 1) delta ^= vdc[(size_t)(m - 1) * MTSG_SOBOL_COLUMNS + c];
+        const uint64_t scramble = (sobolScramble & 0xFFFFFFFFull) >> (32 - m);
+        uint64_t b = ((((uint64_t)px ^ scramble) << m) | ((uint64_t)py ^ scramble)) ^ delta;
+        for (uint32_t c = 0; b; b >>= 1, ++c)
+            if (b & 1) index ^= vdcInv[(size_t)(m - 1) * MTSG_SOBOL_COLUMNS + c];
+        return index;
+    }
 
     const uint16_t *permOf(uint32_t dim) const { return perm ? perm + off[dim] : nullptr; }
 
@@ -425,6 +454,20 @@ struct Qmc {
         type = d.sampler.type;
         ldDim = d.sampler.dimension;
         while ((1u << ldBits) < spp) ++ldBits;
+        if (type == MTSG_SAMPLER_SOBOL) {
+            sobolM = d.sobol_matrices;
+            vdc = d.sobol_vdc;
+            vdcInv = d.sobol_vdc_inv;
+            sobolScramble = d.sobol_scramble;
+            uint32_t r = 1;
+            const uint32_t mx = (uint32_t)std::max(d.camera.crop_w, d.camera.crop_h);
+            while (r < mx) r <<= 1;   // math::roundToPowerOfTwo
+            sobolRes = (float)r;
+            logRes = 0;
+            while ((1u << (logRes + 1)) <= r) ++logRes;   // math::log2i
+            if (logRes > d.sobol_vdc_inv_rows) throw std::runtime_error("sobol: film too large for the tables");
+            return;
+        }
         if (type != MTSG_SAMPLER_HALTON && type != MTSG_SAMPLER_HAMMERSLEY) return;
         primes = d.qmc_primes;
         off = d.qmc_perm_offset;
@@ -489,6 +532,7 @@ struct Sampler {
     int px = 0, py = 0;
     uint32_t s = 0;
     uint64_t offset = 0, ldKey = 0;
+    uint64_t sobolIndex = 0;      // m_sobolSampleIndex (sobol.cpp:204-216)
 
     // start sample s of pixel (x, y) (Sampler::generate + setSampleIndex)
     void begin(const Qmc *qmc, uint32_t seed, int film_w, uint32_t spp, int x, int y, uint32_t si) {
@@ -498,6 +542,8 @@ struct Sampler {
         key = counterKey(seed, ((uint64_t)y * film_w + x) * spp + si);
         offset = q ? q->pixelOffset(x, y, spp) : 0;
         if (q && q->type == MTSG_SAMPLER_LDSAMPLER) ldKey = counterKey(seed ^ kLdSalt, (uint64_t)y * film_w + x);
+        if (q && q->type == MTSG_SAMPLER_SOBOL)
+            sobolIndex = (q->logRes > 1 && x >= 0) ? q->sobolLookUp(q->logRes, si, (uint32_t)x, (uint32_t)y) : (uint64_t)si;
     }
     int kind() const { return q ? q->type : MTSG_SAMPLER_INDEPENDENT; }
     float indep() { return mode == ORACLE_RNG_SFMT ? sfmt->nextFloat() : counterFloat(key, dim); }
@@ -516,6 +562,9 @@ struct Sampler {
             case MTSG_SAMPLER_HAMMERSLEY:
                 if (dim >= MTSG_QMC_PRIMES) throw std::runtime_error(kDimError);
                 return qmcFloat(offset + q->stride * s);
+            case MTSG_SAMPLER_SOBOL:   // sobol.cpp:218-228 (no sample arrays: nothing to skip)
+                if (dim >= MTSG_SOBOL_DIMS) throw std::runtime_error(kSobolDimError);
+                return q->sobolSample(sobolIndex, dim++);
             case MTSG_SAMPLER_LDSAMPLER: {   // ldsampler.cpp:202-208
                 const uint32_t n1 = dim - 2 * n2;
                 if ((int)n1 < q->ldDim) {
@@ -549,6 +598,18 @@ struct Sampler {
                     a = qmcFloat(idx);
                     b = qmcFloat(idx);
                 }
+                break;
+            }
+            case MTSG_SAMPLER_SOBOL: {   // sobol.cpp:230-250
+                if (dim + 1 >= MTSG_SOBOL_DIMS) throw std::runtime_error(kSobolDimError);
+                if (dim == 0 && sobolIndex != (uint64_t)s) {
+                    a = q->sobolSample(sobolIndex, dim++) * q->sobolRes - (float)px;
+                    b = q->sobolSample(sobolIndex, dim++) * q->sobolRes - (float)py;
+                } else {
+                    a = q->sobolSample(sobolIndex, dim++);
+                    b = q->sobolSample(sobolIndex, dim++);
+                }
+                ++n2;
                 break;
             }
             case MTSG_SAMPLER_LDSAMPLER: {   // ldsampler.cpp:210-216

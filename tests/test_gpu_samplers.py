@@ -20,6 +20,9 @@ SAMPLERS = {
                      '<integer name="sampleCount" value="$spp"/></sampler>',
     "hammersley": '<sampler type="hammersley"><integer name="sampleCount" value="$spp"/></sampler>',
     "ldsampler": '<sampler type="ldsampler"><integer name="sampleCount" value="$spp"/></sampler>',
+    "sobol": '<sampler type="sobol"><integer name="sampleCount" value="$spp"/></sampler>',
+    "sobol_scrambled": '<sampler type="sobol"><integer name="scramble" value="9"/>'
+                       '<integer name="sampleCount" value="$spp"/></sampler>',
 }
 
 
@@ -37,16 +40,17 @@ def test_sampler_draws_match_oracle(tmp_path, name):
     g.close()
 
 
-def test_device_dimension_limit(tmp_path):
-    sc = sampler_scene(tmp_path, SAMPLERS["halton"], width=8, height=8, spp=4)
+@pytest.mark.parametrize("name,msg", [("halton", "prime number table"), ("sobol", "direction number table")])
+def test_device_dimension_limit(tmp_path, name, msg):
+    sc = sampler_scene(tmp_path, SAMPLERS[name], width=8, height=8, spp=4)
     g = mtsg.GPUScene(sc, 0)
     g.sampler_draws(sc.params(), 0, 0, 0, [1] * 1024)
-    with pytest.raises(RuntimeError):
+    with pytest.raises(RuntimeError, match=msg):
         g.sampler_draws(sc.params(), 0, 0, 0, [1] * 1025)
     g.close()
 
 
-@pytest.mark.parametrize("name", ["halton", "hammersley", "ldsampler"])
+@pytest.mark.parametrize("name", ["halton", "hammersley", "ldsampler", "sobol", "sobol_scrambled"])
 def test_render_parity_per_sampler(tmp_path, name):
     sc = sampler_scene(tmp_path, SAMPLERS[name], width=64, height=48, spp=8)
     g = mtsg.GPUScene(sc, 0)

@@ -131,4 +131,4 @@ def test_halton_dimension_limit(tmp_path):
 
 def test_unknown_sampler_is_rejected(tmp_path):
     with pytest.raises(RuntimeError):
-        sampler_scene(tmp_path, '<sampler type="sobol"/>')
+        sampler_scene(tmp_path, '<sampler type="stratified"/>')
