@@ -29,7 +29,7 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-TRAFFIC_KERNEL = "k_trace_s<false, 16>"
+TRAFFIC_KERNEL = "k_trace_s<false, 16, false>"
 
 
 def pmc_traffic(workload):

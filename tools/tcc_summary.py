@@ -7,7 +7,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_trace_s<false, 16>"
+KERNEL = "k_trace_s<false, 16, false>"
 
 d = sys.argv[1]
 hit = miss = 0.0

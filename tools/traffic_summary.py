@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_trace_s<false, 16>"
+KERNEL = "k_trace_s<false, 16, false>"
 
 
 def launches(path, counter):
