@@ -11,7 +11,7 @@ JOBS    ?= 8
 
 HOST_SRC := $(wildcard $(PKG)/host/*.cpp)
 HOST_HDR := $(wildcard $(PKG)/host/*.h) $(PKG)/host/ior_table.inc include/mtsg.h include/mtsh.h
-DEV_SRC  := $(PKG)/csrc/mtsg.hip
+DEV_SRC  := $(PKG)/csrc/mtsg.hip $(PKG)/csrc/smp_kernels.hip
 DEV_HDR  := $(wildcard $(PKG)/csrc/*.h) include/mtsg.h
 
 HOST_LIB := $(PKG)/libmtsg_host.so
@@ -37,9 +37,21 @@ $(HOST_LIB): $(HOST_SRC) $(HOST_HDR) $(SOBOL_BIN)
 # (build/config-linux-gcc.py:7); long specular paths otherwise diverge from
 # the oracle through ulp-level differences (measured: C5 parity 2.0e-3 ->
 # 1.8e-4 relative L1), at no measured cost (C3 1262 vs 1256 Msamples/s).
-DEV_FLAGS := -O3 -std=c++17 -fPIC -shared -Wall -ffp-contract=off -munsafe-fp-atomics -Wno-unused-value -Wno-unused-result
-$(DEV_LIB): $(DEV_SRC) $(DEV_HDR)
-	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) -o $@ $(DEV_SRC)
+# The device library is six translation units built in parallel: mtsg.hip
+# (host side, traversal, camera, splat) and smp_kernels.hip once per sampler
+# (k_shade / k_finish of MTSG_SAMPLER_* = 0..4; unit 0 also answers the
+# k_finish occupancy query).  DEV_EXTRA / DEV_OBJ: measurement variants.
+DEV_FLAGS := -O3 -std=c++17 -fPIC -Wall -ffp-contract=off -munsafe-fp-atomics -Wno-unused-value -Wno-unused-result
+DEV_OBJ   ?= build/dev
+DEV_OBJS  := $(DEV_OBJ)/mtsg.o $(foreach k,0 1 2 3 4,$(DEV_OBJ)/smp_$(k).o)
+$(DEV_OBJ)/mtsg.o: $(PKG)/csrc/mtsg.hip $(DEV_HDR)
+	@mkdir -p $(DEV_OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) $(DEV_EXTRA) -c -o $@ $<
+$(DEV_OBJ)/smp_%.o: $(PKG)/csrc/smp_kernels.hip $(DEV_HDR)
+	@mkdir -p $(DEV_OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) $(DEV_EXTRA) -DMTSG_TU_SAMPLER=$* $(if $(filter 0,$*),-DMTSG_TU_OCCUPANCY) -c -o $@ $<
+$(DEV_LIB): $(DEV_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(DEV_OBJS)
 
 # Host-side `path` integrator plugin mirror: tiles the film over GPUs
 $(PATH_LIB): $(PKG)/host/path_integrator.cc $(HOST_LIB) $(DEV_LIB) include/mtsg.h include/mtsh.h include/mtsg_path.h
@@ -72,5 +84,4 @@ VAR_LIBS := $(foreach v,$(VARIANTS),build/var/libmtsg_$(word 1,$(subst :, ,$(v))
 .PHONY: variants
 variants: $(VAR_LIBS)
 build/var/libmtsg_%.so: $(DEV_SRC) $(DEV_HDR)
-	@mkdir -p build/var
-	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) $(subst @, ,$(word 2,$(subst :, ,$(filter $*:%,$(VARIANTS))))) -o $@ $(DEV_SRC)
+	$(MAKE) DEV_OBJ=build/var/$* DEV_LIB=$@ DEV_EXTRA="$(subst @, ,$(word 2,$(subst :, ,$(filter $*:%,$(VARIANTS)))))" $@

@@ -262,7 +262,8 @@ def main():
         step()
         st = gpu.stats()
         for f in ("ms_trace_closest", "ms_trace_shadow", "ms_shade", "ms_camera", "ms_splat", "ms_total",
-                  "rays_closest", "rays_shadow", "launches_trace_closest", "launches_trace_shadow"):
+                  "rays_closest", "rays_shadow", "launches_trace_closest", "launches_trace_shadow",
+                  "ms_finish", "paths_finish", "launches_finish"):
             acc[f] = acc.get(f, 0) + getattr(st, f)
     barrier(pg)
     elapsed = max_over_ranks(pg, time.perf_counter() - t0)
@@ -281,7 +282,10 @@ def main():
                    "shade_ms": acc["ms_shade"] / k, "camera_ms": acc["ms_camera"] / k, "splat_ms": acc["ms_splat"] / k,
                    "frame_ms": acc["ms_total"] / k, "closest_rays": acc["rays_closest"] // k,
                    "shadow_rays": acc["rays_shadow"] // k,
-                   "trace_launches": (acc["launches_trace_closest"] + acc["launches_trace_shadow"]) // k}
+                   "trace_launches": (acc["launches_trace_closest"] + acc["launches_trace_shadow"]) // k,
+                   # tail mode: the paths left at the switch bounce, finished in one k_finish launch
+                   "finish_ms": acc["ms_finish"] / k, "finish_paths": acc["paths_finish"] // k,
+                   "finish_launches": acc["launches_finish"] // k}
         # instrumented pass at reduced spp (per-ray counts are spp-independent)
         pc = params.copy()
         pc.spp = max(1, min(params.spp, 16))

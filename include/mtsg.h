@@ -380,6 +380,11 @@ typedef struct mtsg_stats {
     uint64_t iter_hist_closest[16], iter_hist_shadow[16];
     /* instance transform visits (MTSG_FLAG_COUNT; two-level scenes)      */
     uint64_t instance_visits, shadow_instance_visits;
+    /* tail mode: once a bounce starts with few paths, one k_finish launch
+     * carries them through their remaining bounces (ms_finish; the paths it
+     * took over; its launches).  Their traversal is not in rays_* above.   */
+    double ms_finish;
+    uint64_t paths_finish, launches_finish;
 } mtsg_stats;
 
 enum {
@@ -441,6 +446,14 @@ int  mtsg_debug_stragglers(mtsg_scene *scene, float *out, uint32_t max_rays);
 
 /* Wavefront batch size in paths (default chosen from device memory). */
 int  mtsg_set_batch_paths(mtsg_scene *scene, uint32_t paths);
+
+/* Tail mode: once a bounce starts with fewer than `paths` paths, one
+ * persistent launch carries them through all their remaining bounces
+ * instead of a trace + shade launch per bounce (same arithmetic in the same
+ * order: the image is unchanged).  0 turns it off; the default is
+ * MTSG_DEFAULT_FINISH_PATHS (environment override MTSG_FINISH).            */
+#define MTSG_DEFAULT_FINISH_PATHS 524288u
+int  mtsg_set_finish_paths(mtsg_scene *scene, uint32_t paths);
 
 /* Debug/parity entry points over SoA rays (host buffers).  Semantics of
  * ShapeKDTree::rayIntersect (src/librender/skdtree.cpp:112-142) including

@@ -35,2094 +35,9 @@
 #include "envmap.h"
 #include "sampler.h"
 
-using namespace mtsg;
+#include "kernels.h"
 
 namespace {
-
-// ---------------------------------------------------------------------------
-// device-side scene and path state
-// ---------------------------------------------------------------------------
-struct DevScene {
-    // device kd-tree (built from Mitsuba's KDNode array at upload: same splits
-    // and leaves, re-laid out as two-level blocks).  A block root's 64-B block
-    // holds {children pair, left child's pair, right child's pair, pad}, so one
-    // fetch descends two levels.  Node words (8 B):
-    //   leaf            1 << 31 | start, end   (range of triL records)
-    //   block root      axis | block << 3, split
-    //   pair-only node  axis | 4 | slot << 3, split  (slot = 4 * block + 1|2, uint4 units)
-    const uint4 *__restrict__ blocks;
-    uint2 root2;
-    const float4 *__restrict__ triL;       // TriAccel records in leaf order (3 float4 each)
-    const float4 *__restrict__ vpos;       // xyz
-    const float4 *__restrict__ vnrm;       // xyz
-    const uint4 *__restrict__ tidx;        // i0, i1, i2, shape
-    // per-triangle shading record, 6 float4 (96 B, one contiguous fetch per hit):
-    //   p0 p1 p2 | n0 n1 n2 | dpdu | shape, bsdf | faceNormals << 31, emitter
-    const float4 *__restrict__ shrec;
-    const mtsg_rect *__restrict__ rects;
-    const mtsg_shape *__restrict__ shapes;
-    const mtsg_bsdf *__restrict__ bsdfs;
-    const mtsg_emitter *__restrict__ emitters;
-    const float *__restrict__ emitter_cdf;
-    const float *__restrict__ emitter_tri_cdf;
-    uint32_t n_emitters, n_tri;
-    float bmin[3], bmax[3];
-    int has_env;
-    DevEnv env;
-    // halton / hammersley tables (sampler.h); nullptr for the other samplers
-    const uint32_t *qmcPrimes, *qmcOff;
-    const uint16_t *qmcPerm;
-    // two-level instancing (instance.cpp:115-160): per instance 8 float4 =
-    // to_local rows 0-2, to_world rows 0-2, {group AABB min, root word 0},
-    // {group AABB max, root word 1}; the group trees live in `blocks` / `triL`
-    // beside the top-level tree.  nullptr: no instances.
-    const float4 *__restrict__ inst;
-};
-constexpr uint32_t KINST = 4u;   // leaf-ordered TriAccel copy of an instance primitive: k = 4
-
-struct DevCamera {
-    float s2c[16];
-    float c2w[12];
-    float near_clip, far_clip, inv_res_x, inv_res_y;
-    int film_w, film_h;
-    float filter_radius, filter_scale;
-    int border, has_alpha;
-    float filter_values[32];
-    float dx[3], dy[3];   // near-plane differentials (perspective.cpp:160-170)
-    int has_env;          // store primary-ray differentials for the environment lookup
-    int crop_w, crop_h;   // the sampler's space partition (setFilmResolution)
-};
-
-struct DevIntegrator {
-    int max_depth, rr_depth, strict_normals, hide_emitters;
-    uint32_t spp, seed;
-    uint32_t film_w;   // sample id = (y * film_w + x) * spp + s
-    DevSampler smp;
-};
-
-// a path's sampler at sample s of film pixel (x, y), `dim` dimensions and
-// `n2` 2D requests into the path
-DEV PathSampler path_sampler(const DevIntegrator &I, int x, int y, uint32_t s, uint32_t dim, uint32_t n2) {
-    const uint64_t pix = (uint64_t)y * (uint64_t)I.film_w + (uint64_t)x;
-    PathSampler p{counterKey(I.seed, pix * I.spp + s), dim, n2, s, x, y, false, 0ull};
-    if (I.smp.type == MTSG_SAMPLER_SOBOL) p.qidx = sobol_index(I.smp, s, x, y);
-    return p;
-}
-DEV uint64_t pixel_index(const DevIntegrator &I, const PathSampler &p) {
-    return (uint64_t)p.y * (uint64_t)I.film_w + (uint64_t)p.x;
-}
-template <int KIND>
-DEV float next1D(const DevIntegrator &I, PathSampler &p) {
-    return smp_next1D<KIND>(I.smp, p, I.seed, pixel_index(I, p), I.spp);
-}
-template <int KIND>
-DEV void next2D(const DevIntegrator &I, PathSampler &p, float &a, float &b) {
-    smp_next2D<KIND>(I.smp, p, I.seed, pixel_index(I, p), I.spp, a, b);
-}
-// the camera's pixel jitter: the first 2D request of a sample (the sampler is
-// a run-time choice here; k_shade is instantiated per sampler)
-DEV void camera_jitter(const DevIntegrator &I, int x, int y, uint32_t s, float &a, float &b) {
-    PathSampler p = path_sampler(I, x, y, s, 0, 0);
-    switch (I.smp.type) {
-        case MTSG_SAMPLER_HALTON: next2D<MTSG_SAMPLER_HALTON>(I, p, a, b); break;
-        case MTSG_SAMPLER_HAMMERSLEY: next2D<MTSG_SAMPLER_HAMMERSLEY>(I, p, a, b); break;
-        case MTSG_SAMPLER_LDSAMPLER: next2D<MTSG_SAMPLER_LDSAMPLER>(I, p, a, b); break;
-        case MTSG_SAMPLER_SOBOL: next2D<MTSG_SAMPLER_SOBOL>(I, p, a, b); break;
-        default: next2D<MTSG_SAMPLER_INDEPENDENT>(I, p, a, b); break;
-    }
-}
-
-// wavefront batch: tiles [tile0, tile0 + ntiles) x samples [s0, s0 + ns)
-struct DevBatch {
-    int rect_x, rect_y, rect_w, rect_h;   // render rectangle (film coords)
-    int tiles_x;                          // tiles per row of the rectangle
-    int tile0, ntiles;                    // virtual tile range of this batch
-    int tstride, toffset;                 // global tile = toffset + virtual * tstride
-    uint32_t s0, ns;
-    uint32_t nslots;
-};
-
-enum : uint32_t { F_SCATTERED = 1u << 16, F_DELTA = 1u << 17 };
-
-// Path state.  The paths of a bounce are stored densely by their position in
-// that bounce's work list (the camera's slot order at bounce 0, then the order
-// in which k_shade appended the surviving paths), so every kernel streams its
-// state with coalesced 16-B accesses instead of gathering it through a queue of
-// slot indices.  k_shade writes the survivors into the n_* arrays at their new
-// position; the host swaps the two sets after each bounce.  Only the final
-// radiance is kept per sample slot (L, written when a path terminates).
-struct DevPaths {
-    float4 *ray_o;    // o.xyz, mint
-    float4 *ray_d;    // d.xyz, maxt
-    float4 *T;        // throughput rgb, eta        (bounce 0: x-differential direction)
-    float4 *aux;      // refN.xyz of the previous vertex, bsdf pdf (bounce 0: y-differential)
-    float4 *Lp;       // radiance so far, alpha
-    uint4 *meta;      // depth | flags, next RNG dimension, sample slot, 0
-    float4 *n_ray_o, *n_ray_d, *n_T, *n_aux, *n_Lp;   // next bounce (compacted)
-    uint4 *n_meta;
-    float4 *hit;      // t, u, v, prim (bits) of ray i
-    uint32_t *hitInst;   // instance of hit i (0xFFFFFFFF: none); two-level scenes only
-    float4 *L;        // per sample slot: final radiance, alpha (k_splat input)
-    float4 *sh_o;     // shadow ray i: origin, maxt
-    float4 *sh_d;     // direction, mint
-    float4 *sh_c;     // NEE contribution, target (bits): next-bounce position, or 1 << 31 | slot
-    uint32_t *cnt;    // counters, each on its own 256-B line (see CNT_*)
-    unsigned long long *ctr;  // traversal counters (nodes, refs, tests)
-};
-
-// queue / fetch counters live on separate 256-byte lines: a single
-// contended address serialises at ~11 ns per atomic (MI355X_MICROARCH.md,
-// row "dequeue"), and counters sharing a line would serialise together
-constexpr int XGROUPS = 8;                  // XCDs: blocks b and b + 8 share one
-// Q0/Q1: paths of the next bounce (ping-pong); S0/S1: shadow rays of a bounce
-// (ping-pong: bounce b appends to S(b & 1) while its trace reads S((b-1) & 1))
-constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S0 = 128, CNT_S1 = 192;
-constexpr int CNT_ERR = 96;   // sticky error flags (1: QMC dimension limit)
-constexpr int CNT_FETCH = 256;                           // XGROUPS counters, 32 words apart
-constexpr int CNT_WORDS = CNT_FETCH + 32 * XGROUPS;
-constexpr int HOSTCNT_STRIDE = 256;
-// traversal counters (MTSG_FLAG_COUNT): [0,7) closest, [8,15) shadow (see
-// flush_counts), 7 / 15 the maximum iterations per ray, [16,32) / [32,48)
-// histograms of floor(log2(iterations per ray)); [48] the number of captured
-// stragglers (rays of >= STRAGGLER_ITERS iterations), [64, 64 + 8 * 64) their
-// records (o.xyz, d.xyz, iterations, shadow as float / integer bits)
-constexpr int CTR_WORDS = 64 + 8 * 64;
-constexpr uint32_t STRAGGLER_ITERS = 300, STRAGGLER_MAX = 64;
-constexpr uint32_t WT_MAX_LAUNCHES = 64;   // MTSG_FLAG_WAVETIME launches recorded per render
-// MTSG_FLAG_WAVETIME words per wave: start, exit, time the work list was found
-// empty, loop iterations after that
-constexpr uint32_t WT_WORDS = 4;
-#ifndef MTSG_WT_DRAIN
-#define MTSG_WT_DRAIN 0   // record words 2-3 (diagnostic builds: the bookkeeping costs ~4% in the hot loop)
-#endif
-constexpr bool WT_DRAIN = MTSG_WT_DRAIN;
-__host__ __device__ constexpr int cnt_s(int k) { return k ? CNT_S1 : CNT_S0; }
-DEV int cnt_q(int q) { return q ? CNT_Q1 : CNT_Q0; }
-
-constexpr int TILE = 16;                    // splat tile edge (256 pixels)
-constexpr int BLOCK = 256;
-#ifndef MTSG_SHADE_BLOCK
-#define MTSG_SHADE_BLOCK 256
-#endif
-constexpr int SHADE_BLOCK = MTSG_SHADE_BLOCK;   // k_shade workgroup size
-constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traversal
-// Paths per wavefront batch (272 B of state per path; 2^28 paths = 73 GB
-// of the 288 GB HBM, capped at 60% of free device memory at run time).
-// Every traversal launch ends with a tail of ~0.5-0.8 ms while its longest
-// rays finish, and late bounces hold few paths, so the batch should be as
-// large as the frame -- measured on the 1M-triangle scene (Msamples/s):
-// 4M paths 421, 16M 672, 32M 803, 64M 884, 128M 934, whole frame 960.
-constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 28;
-#define MTSG_MAX_LANES 4
-#ifndef MTSG_LANES
-#define MTSG_LANES 1
-#endif
-constexpr size_t PATH_STATE_BYTES = 272;    // bytes per path slot (DevPaths: 2 x 96 dense + hit, L, 3 x shadow)
-#ifndef MTSG_SHORT_STACK
-#define MTSG_SHORT_STACK 6   // 6 x 12 B x 64 lanes = 4.6 KB LDS/wave -> 8 waves/SIMD (8: 6.5, 12: 4.2)
-#endif
-constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per lane
-// the compact speculative traversal is sized for 8 waves per SIMD (64 VGPRs)
-#ifndef MTSG_SPEC_WAVES
-#define MTSG_SPEC_WAVES 8
-#endif
-#define SPEC_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SPEC_WAVES)))
-// streaming (non-temporal) access to the per-path SoA state: the state of a
-// 32M-path batch is GBs per bounce and would otherwise evict the kd-tree from
-// the 256 MB Infinity Cache (experiment switch MTSG_NT)
-#ifndef MTSG_NT
-#define MTSG_NT 1
-#endif
-typedef float nf4 __attribute__((ext_vector_type(4)));
-DEV float4 ldS(const float4 *p) {
-#if MTSG_NT
-    const nf4 v = __builtin_nontemporal_load((const nf4 *)p);
-    return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-DEV void stS(float4 *p, const float4 &v) {
-#if MTSG_NT
-    __builtin_nontemporal_store((nf4){v.x, v.y, v.z, v.w}, (nf4 *)p);
-#else
-    *p = v;
-#endif
-}
-typedef uint32_t nu4 __attribute__((ext_vector_type(4)));
-DEV uint4 ldS(const uint4 *p) {
-#if MTSG_NT
-    const nu4 v = __builtin_nontemporal_load((const nu4 *)p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-DEV void stS(uint4 *p, const uint4 &v) {
-#if MTSG_NT
-    __builtin_nontemporal_store((nu4){v.x, v.y, v.z, v.w}, (nu4 *)p);
-#else
-    *p = v;
-#endif
-}
-
-// ---------------------------------------------------------------------------
-// wave helpers (64 lanes)
-// ---------------------------------------------------------------------------
-DEV uint32_t lane_id() { return __lane_id(); }
-
-// ---------------------------------------------------------------------------
-// primitive tests
-// ---------------------------------------------------------------------------
-// TriAccel::rayIntersect (triaccel.h:96-158)
-DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, float3 d, float mint, float maxt,
-                  float &u, float &v, float &t) {
-    // no FMA contraction: bit-identical t, u, v to the oracle (and Mitsuba's SSE2 build)
-#pragma clang fp contract(off)
-    const uint32_t k = __float_as_uint(f0.x);
-    // (u, v, k) = (1,2,0) | (2,0,1) | (0,1,2): a rotation of (x, y, z) by k, so
-    // two compares and two selects per component (k >= 3 never hits)
-    const bool k0 = k == 0u, k1 = k == 1u;
-    const float o_k = k0 ? o.x : (k1 ? o.y : o.z), d_k = k0 ? d.x : (k1 ? d.y : d.z);
-    const float o_u = k0 ? o.y : (k1 ? o.z : o.x), d_u = k0 ? d.y : (k1 ? d.z : d.x);
-    const float o_v = k0 ? o.z : (k1 ? o.x : o.y), d_v = k0 ? d.z : (k1 ? d.x : d.y);
-    const float n_u = f0.y, n_v = f0.z, n_d = f0.w;
-    // branch-free on purpose: with an early `t` rejection the compiler sinks
-    // the loads of f1/f2 behind it, turning one 48-byte fetch into two or
-    // three dependent memory round trips per primitive
-    t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
-    const float hu = o_u + t * d_u - f1.x;
-    const float hv = o_v + t * d_v - f1.y;
-    u = hv * f1.z + hu * f1.w;
-    v = hu * f2.x + hv * f2.y;
-    return (t >= mint) & (t <= maxt) & (u >= 0) & (v >= 0) & (u + v <= 1.0f) & (k < 3);
-}
-
-// Rectangle::rayIntersect (rectangle.cpp:115-139)
-DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float maxt, float &t, float &lx, float &ly) {
-#pragma clang fp contract(off)
-    const float *m = r.to_object;
-    float3 o = mk3(m[0] * wo.x + m[1] * wo.y + m[2] * wo.z + m[3], m[4] * wo.x + m[5] * wo.y + m[6] * wo.z + m[7],
-                   m[8] * wo.x + m[9] * wo.y + m[10] * wo.z + m[11]);
-    float3 d = mk3(m[0] * wd.x + m[1] * wd.y + m[2] * wd.z, m[4] * wd.x + m[5] * wd.y + m[6] * wd.z,
-                   m[8] * wd.x + m[9] * wd.y + m[10] * wd.z);
-    float hit = -o.z / d.z;
-    if (!(hit >= mint && hit <= maxt)) return false;
-    float x = o.x + d.x * hit, y = o.y + d.y * hit;
-    if (fabsf(x) <= 1 && fabsf(y) <= 1) { t = hit; lx = x; ly = y; return true; }
-    return false;
-}
-
-// ---------------------------------------------------------------------------
-// kd-tree traversal (ShapeKDTree::rayIntersectHavran, sahkdtree3.h:246-358):
-// t-interval front-to-back order with an LDS short stack and kd-restart when
-// the short stack has overflowed (Horn et al. 2007).  Finds the same closest
-// primitive as the Havran loop: every leaf overlapping the ray segment is
-// visited until the best hit lies before the current leaf's exit distance
-// (sahkdtree3.h:299-300).
-// ---------------------------------------------------------------------------
-// Algorithmic work (per lane) and, for the SIMD-efficiency figures, the
-// wave-level iteration counts (accumulated by lane 0 only): a wave pays
-// max-over-lanes of the inner-node and primitive iterations of every step.
-struct TraceCounts { uint32_t nodes, refs, tests, wnodes, wtests, wsteps, wactive, restarts, inst; };   // restarts: not flushed
-
-template <bool COUNT>
-DEV void flush_counts(unsigned long long *ctr, TraceCounts c) {
-    if (!COUNT) return;
-    // wave reduction then one atomic per counter per wave
-    unsigned long long v[7] = {c.nodes, c.refs, c.tests, c.wnodes, c.wtests, c.wsteps, c.wactive};
-#pragma unroll
-    for (int k = 0; k < 7; ++k)
-        for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_down(v[k], off);
-    if (lane_id() == 0)
-#pragma unroll
-        for (int k = 0; k < 7; ++k) atomicAdd(ctr + k, v[k]);
-}
-
-#ifndef MTSG_FETCH
-#define MTSG_FETCH 128
-#endif
-constexpr uint32_t FETCH = MTSG_FETCH;
-#ifndef MTSG_GUIDE
-#define MTSG_GUIDE 0
-#endif
-#ifndef MTSG_FETCH_MIN
-#define MTSG_FETCH_MIN 64
-#endif
-#ifndef MTSG_GUIDE_SPLIT
-#define MTSG_GUIDE_SPLIT 2
-#endif
-constexpr bool GUIDE = MTSG_GUIDE;
-constexpr uint32_t FETCH_MIN = MTSG_FETCH_MIN, GUIDE_SPLIT = MTSG_GUIDE_SPLIT;
-
-// XCD-partitioned work fetch: the queue is cut into XGROUPS contiguous
-// ranges; workgroup b draws from range b % XGROUPS first (blocks b, b + 8
-// share an XCD, so coherent neighbouring rays share that XCD's L2) and then
-// steals from the other ranges.  Each range has its own fetch counter on its
-// own cache line (a contended word serialises at ~11 ns per atomic).
-struct Fetch {
-    uint32_t *ctr;
-    uint32_t count;
-    uint32_t group;    // range currently drained (wave-uniform)
-    uint32_t tried;
-    uint32_t guide;    // waves per range x GUIDE_SPLIT
-    uint32_t req;      // next request size (GUIDE)
-    DEV uint32_t lo(uint32_t g) const { return (uint32_t)(((uint64_t)count * g) / XGROUPS); }
-    // returns false when every range is exhausted; else [base, base + n)
-    DEV bool next(uint32_t want, uint32_t &base, uint32_t &n) {
-        while (tried < XGROUPS) {
-            const uint32_t beg = lo(group), end = lo(group + 1);
-            // called with the whole wave active: lane 0 draws for it
-            uint32_t off = 0;
-            if (GUIDE) want = req;
-            if (__lane_id() == 0) off = atomicAdd(&ctr[32 * group], want);
-            off = __builtin_amdgcn_readfirstlane(off);
-            if (beg + off < end) {
-                base = beg + off;
-                n = min(want, end - base);
-                // guided self-scheduling: size the next request by what this
-                // draw saw left of the range (no extra access to the
-                // contended counter), so the last pools are small and the
-                // waves run out of work together
-                if (GUIDE) req = max(FETCH_MIN, min(FETCH, (end - base - n) / guide));
-                return true;
-            }
-            group = (group + 1) % XGROUPS;
-            ++tried;
-        }
-        return false;
-    }
-};
-
-// unoccluded shadow ray i: its contribution goes to the path's radiance, at
-// the path's position in the current bounce (the trace runs after the swap)
-// or, if the path ended, to its sample's final slot
-DEV void shadow_unoccluded(const DevPaths &P, uint32_t i) {
-    const float4 con = ldS(&P.sh_c[i]);
-    const uint32_t tgt = __float_as_uint(con.w);
-    float4 *L = (tgt & 0x80000000u) ? &P.L[tgt & 0x7FFFFFFFu] : &P.Lp[tgt];
-    float4 v = ldS(L);
-    v.x += con.x; v.y += con.y; v.z += con.z;
-    stS(L, v);
-}
-
-// Debug entry point: environment radiance along directions (rx/ry null:
-// bilinear level-0 lookup; else EWA with those differential directions)
-__global__ void k_env_eval(DevScene S, const float *dirs, const float *rx, const float *ry, uint32_t n, float *out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float3 d = mk3(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
-    const bool diff = rx != nullptr;
-    const float3 x = diff ? mk3(rx[3 * i], rx[3 * i + 1], rx[3 * i + 2]) : d;
-    const float3 y = diff ? mk3(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]) : d;
-    const float3 v = env_eval(S.env, d, diff, x, y);
-    out[3 * i] = v.x; out[3 * i + 1] = v.y; out[3 * i + 2] = v.z;
-}
-
-// ---------------------------------------------------------------------------
-// Speculative traversal with compact per-lane state: each iteration issues
-// one node fetch and one primitive fetch per lane, testing the leaf it holds
-// while descending towards the next one.  Stack counters, direction signs and
-// flags are packed in one word and hit records are written through on every
-// hit (u, v and the primitive index are not kept live): 64 VGPRs, 8 waves/SIMD.
-// ---------------------------------------------------------------------------
-struct SpecRay {
-    float3 o, d, inv;
-    float mint, best;    // primitive-test interval (best shrinks with hits)
-    float tmin, tmax;    // traversal interval of r.cur
-    uint2 cur;           // traversal node (two-level encoding)
-    uint32_t lfE, lfEnd; // primitive range of the held leaf
-    float lfTmax;        // exit distance of the held leaf; < 0: none held
-    uint32_t bits;       // see SB_*
-};
-// bits: top slot of the circular short stack (0-2), entries held (3-5),
-// entries dropped since the last restart (6), ray direction signs (16-18),
-// traversal done (19), hit found (20), shadow ray (21)
-enum : uint32_t {
-    SB_TOP = 7u, SB_N = 7u << 3, SB_N1 = 1u << 3, SB_DROPPED = 1u << 6, SB_STACK = 0x7Fu,
-    SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20, SB_SHADOW = 1u << 21
-};
-
-// short stack of the compact traversal: entry k of lane i at [k * TRACE_BLOCK
-// + i].  A workgroup is one wave, so the lane index is recomputed at every use
-// (v_mbcnt) instead of holding a register through the traversal loop.
-static_assert(TRACE_BLOCK == 64, "one wave per traversal workgroup");
-__shared__ uint2 s_specNode[SHORT_STACK * TRACE_BLOCK];
-__shared__ float s_specT[SHORT_STACK * TRACE_BLOCK];
-// lane index, recomputed where it is used (volatile: not hoisted out of loops)
-DEV uint32_t lane_here() {
-    uint32_t l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-}
-// number of set bits of a wave mask below this lane
-DEV uint32_t rank_below(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-struct SpecStack {
-    DEV static uint32_t at(uint32_t k) { return k * TRACE_BLOCK + lane_here(); }
-    DEV void push(uint32_t k, uint2 node, float t) const {
-        const uint32_t i = at(k);
-        s_specNode[i] = node;
-        s_specT[i] = t;
-    }
-    DEV uint2 node(uint32_t k) const { return s_specNode[at(k)]; }
-    DEV float t(uint32_t k) const { return s_specT[at(k)]; }
-};
-
-// constant 4-vector built at its use (keeps the compiler from holding it in
-// registers across the traversal loop)
-DEV float4 miss_record() {
-    float4 m;
-    uint32_t inf = 0x7F800000u, z = 0u, ff = 0xFFFFFFFFu;
-    asm volatile("" : "+v"(inf), "+v"(z), "+v"(ff));
-    m.x = __uint_as_float(inf); m.y = __uint_as_float(z); m.z = __uint_as_float(z); m.w = __uint_as_float(ff);
-    return m;
-}
-
-// Ray setup: scene-AABB clip (AABB::rayIntersect, aabb.h:308-338) and the
-// adaptive epsilon of ShapeKDTree::rayIntersect / rayIntersect for shadow
-// rays (skdtree.cpp:112-142 / 207-226).  Returns false when the ray misses
-// the scene bounds or its interval is empty.
-DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, bool shadow, SpecRay &r) {
-    r.o = o;
-    r.d = d;
-    r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const uint32_t dneg = (d.x <= 0.0f ? 1u : 0u) | (d.y <= 0.0f ? 2u : 0u) | (d.z <= 0.0f ? 4u : 0u);
-    float nearT = -INFINITY, farT = INFINITY;
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const float oi = comp(o, i), di = comp(d, i), ii = comp(r.inv, i);
-        if (di == 0.0f) {
-            if (oi < S.bmin[i] || oi > S.bmax[i]) ok = false;
-        } else {
-            const float t1 = (S.bmin[i] - oi) * ii, t2 = (S.bmax[i] - oi) * ii;
-            nearT = fmaxf(fminf(t1, t2), nearT);
-            farT = fminf(fmaxf(t1, t2), farT);
-        }
-    }
-    if (!ok || !(nearT <= farT)) return false;
-    float rayMinT = rayMint;
-    if (rayMinT == kEpsilon) {
-        float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-        if (!shadow) m = fmaxf(m, kEpsilon);
-        rayMinT *= m;
-    }
-    r.mint = fmaxf(nearT, rayMinT);
-    r.best = fminf(farT, rayMaxt);
-    if (!(r.best > r.mint)) return false;
-    r.tmin = r.mint;
-    r.tmax = r.best;
-    r.cur = S.root2;
-    r.lfE = r.lfEnd = 0;
-    r.lfTmax = -1.0f;
-    r.bits = dneg << SB_DNEG | (shadow ? SB_SHADOW : 0u);
-    return true;
-}
-
-// inner-node step with the packed short-stack counters (as kd_descend), split
-// in two: spec_plan needs only the node word (axis, split), so the child to
-// visit is known before the node's children are fetched; spec_take applies it.
-DEV void spec_plan(const SpecRay &r, uint2 n, float &tsplit, bool &goLeft, bool &push) {
-    const uint32_t axis = n.x & 3u;
-    const float split = __uint_as_float(n.y);
-    const bool a0 = axis == 0u, a1 = axis == 1u;
-    const float ox = r.o.x, oy = r.o.y, oz = r.o.z, ix = r.inv.x, iy = r.inv.y, iz = r.inv.z;
-    const float oa = a0 ? ox : (a1 ? oy : oz);
-    const float ia = a0 ? ix : (a1 ? iy : iz);
-    tsplit = (split - oa) * ia;
-    if (tsplit != tsplit) tsplit = INFINITY;
-    // bitwise, not short-circuit: no exec-mask branches for these
-    const bool belowFirst = (oa < split) | ((oa == split) & (bool)((r.bits >> (SB_DNEG + axis)) & 1u));
-    const bool onlyFirst = (tsplit > r.tmax) | (tsplit <= 0.0f);
-    const bool goSecond = !onlyFirst & (tsplit < r.tmin);
-    push = !onlyFirst & !goSecond;
-    goLeft = belowFirst != goSecond;
-}
-
-DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push, SpecStack stk) {
-    const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
-    if (push) {
-        // circular short stack: a push onto a full stack drops the oldest entry
-        const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
-        const uint32_t b = r.bits, top = b & SB_TOP;
-        stk.push(top, other, r.tmax);
-        const bool full = (b & SB_N) == (uint32_t)SHORT_STACK * SB_N1;
-        r.bits = ((b & ~SB_TOP) | (top == SHORT_STACK - 1 ? 0u : top + 1u)) + (full ? SB_DROPPED - (b & SB_DROPPED) : SB_N1);
-        r.tmax = tsplit;
-    }
-    return c;
-}
-
-template <bool COUNT>
-DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cnt, float4 *hitOut) {
-    const uint2 n = r.cur;
-    const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
-    const bool prim = r.lfE < r.lfEnd;
-    const bool rootKind = inner && !(n.x & 4u);
-    // the first step is planned from the node word alone, so only the pair
-    // of the grandchildren on the side taken is fetched (block root: {children,
-    // left grandchildren, right grandchildren})
-    float tsplit;
-    bool goLeft, push;
-    spec_plan(r, n, tsplit, goLeft, push);
-    // block root: 64-B block n.x >> 3; pair-only node: 16-B pair n.x >> 3
-    const uint32_t base = inner ? (n.x >> 3) << ((~n.x >> 1) & 2u) : 0u;
-    const uint32_t off = rootKind ? 2u - (uint32_t)goLeft : 0u;
-    const uint32_t pi = prim ? r.lfE : 0u;
-    const uint4 p0 = S.blocks[base], pc = S.blocks[base + off];
-    const float4 *rec = S.triL + (size_t)(3u * pi);   // < 2^32: checked at upload
-    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
-                 "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
-                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
-    if (prim) {
-        if (COUNT) { cnt.refs++; cnt.tests++; }
-        float t, u, v;
-        bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-        const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
-        if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
-        if (h) {
-            r.bits |= SB_FOUND;
-            if (r.bits & SB_SHADOW) return true;   // any hit occludes
-            r.best = t;
-            stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
-        }
-        ++r.lfE;
-    }
-    if (inner) {
-        if (COUNT) cnt.nodes++;
-        const uint2 c = spec_take(r, p0, tsplit, goLeft, push, stk);
-        r.cur = c;
-        if (rootKind && !(c.x & 0x80000000u)) {
-            if (COUNT) cnt.nodes++;
-            float ts2;
-            bool gl2, push2;
-            spec_plan(r, c, ts2, gl2, push2);
-            r.cur = spec_take(r, pc, ts2, gl2, push2, stk);
-        }
-    }
-    const bool found = (r.bits & SB_FOUND) != 0;
-    // the held leaf is finished: Havran's exit, or let the descent take over
-    const bool leafDone = (r.lfTmax >= 0.0f) & (r.lfE >= r.lfEnd);
-    if (leafDone & found & (r.best < r.lfTmax)) return true;
-    r.lfTmax = leafDone ? -1.0f : r.lfTmax;
-    const uint2 c = r.cur;
-    if ((r.lfTmax < 0.0f) & !(r.bits & SB_TRAVDONE) & (bool)(c.x >> 31)) {
-        // the descent reached a leaf: adopt it, then continue from the stack
-        const uint32_t st = c.x & 0x7FFFFFFFu;
-        const bool nonEmpty = st < c.y;
-        if (!nonEmpty & found & (r.best < r.tmax)) return true;
-        r.lfE = nonEmpty ? st : r.lfE;
-        r.lfEnd = nonEmpty ? c.y : r.lfEnd;
-        r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
-        const uint32_t b = r.bits;
-        if (b & SB_N) {
-            const uint32_t top = b & SB_TOP, k = top == 0 ? SHORT_STACK - 1 : top - 1u;
-            r.cur = stk.node(k);
-            const float t = stk.t(k);
-            r.bits = ((b & ~SB_TOP) | k) - SB_N1;
-            r.tmin = r.tmax;
-            r.tmax = fminf(t, r.best);
-        } else {
-            // empty: done, or a kd-restart behind this leaf if entries were dropped
-            const bool restart = (b & SB_DROPPED) != 0;
-            const float t0 = r.tmax;
-            r.tmin = restart ? t0 : r.tmin;
-            r.tmax = restart ? r.best : r.tmax;
-            r.cur = restart ? S.root2 : c;
-            if (COUNT && restart) cnt.restarts++;
-            r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
-        }
-    }
-    return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
-}
-
-// ---------------------------------------------------------------------------
-// Two-level traversal (Instance::rayIntersect, instance.cpp:115-130, over the
-// group's ShapeKDTree::rayIntersect, skdtree.h:431-458): the same speculative
-// iterations, with a per-lane level.  An instance primitive met in a
-// top-level leaf saves the top-level state (node, interval, held leaf range,
-// stack counters) to LDS, transforms the ray by the instance's to_local and
-// traverses the group tree on the clipped interval [max(mint, near),
-// min(best, far)]; when the group traversal ends (or Havran's exit fires
-// inside it) the top-level state is restored and the world-space ray is
-// reloaded from the work list.  The two levels keep separate LDS stacks
-// (top level: OUTER_STACK entries, group: SHORT_STACK), so a group visit
-// never evicts top-level entries.  Hits are written through with the
-// instance they were found in.
-// ---------------------------------------------------------------------------
-constexpr int OUTER_STACK = 2;
-constexpr int SAVE_WORDS = 11;   // cur.x, cur.y, tmin, tmax, lfE, lfEnd, lfTmax, bits, instance, root.x, root.y
-__shared__ uint2 s_outNode[OUTER_STACK * TRACE_BLOCK];
-__shared__ float s_outT[OUTER_STACK * TRACE_BLOCK];
-__shared__ uint32_t s_save[SAVE_WORDS * TRACE_BLOCK];
-enum : uint32_t { SB_INST = 1u << 22 };
-
-DEV uint32_t &save_word(uint32_t k) { return s_save[k * TRACE_BLOCK + lane_here()]; }
-
-// push the far child onto the stack of the lane's level (circular, drops
-// the oldest entry when full)
-DEV uint2 spec_take_i(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push) {
-    const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
-    if (push) {
-        const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
-        const uint32_t b = r.bits, top = b & SB_TOP;
-        const bool inner = (b & SB_INST) != 0;
-        const uint32_t cap = inner ? (uint32_t)SHORT_STACK : (uint32_t)OUTER_STACK;
-        const uint32_t i = top * TRACE_BLOCK + lane_here();
-        if (inner) { s_specNode[i] = other; s_specT[i] = r.tmax; }
-        else { s_outNode[i] = other; s_outT[i] = r.tmax; }
-        const bool full = (b & SB_N) == cap * SB_N1;
-        r.bits = ((b & ~SB_TOP) | (top == cap - 1 ? 0u : top + 1u)) + (full ? SB_DROPPED - (b & SB_DROPPED) : SB_N1);
-        r.tmax = tsplit;
-    }
-    return c;
-}
-
-// back to the top level after a group traversal: restore the saved state,
-// keep the hit flag, reload the world-space ray
-DEV void inst_exit(SpecRay &r, const float4 *wo, const float4 *wd) {
-    const uint32_t found = r.bits & SB_FOUND;
-    r.cur = make_uint2(save_word(0), save_word(1));
-    r.tmin = __uint_as_float(save_word(2));
-    r.tmax = __uint_as_float(save_word(3));
-    r.lfE = save_word(4);
-    r.lfEnd = save_word(5);
-    r.lfTmax = __uint_as_float(save_word(6));
-    r.bits = save_word(7) | found;
-    float4 ro = ldS(wo), rd = ldS(wd);
-    r.o = xyz(ro);
-    r.d = xyz(rd);
-    r.inv = mk3(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
-}
-
-template <bool COUNT>
-DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hitOut, uint32_t *instOut,
-                     const float4 *wo, const float4 *wd) {
-    const uint2 n = r.cur;
-    const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
-    const bool prim = r.lfE < r.lfEnd;
-    const bool rootKind = inner && !(n.x & 4u);
-    float tsplit;
-    bool goLeft, push;
-    spec_plan(r, n, tsplit, goLeft, push);
-    const uint32_t base = inner ? (n.x >> 3) << ((~n.x >> 1) & 2u) : 0u;
-    const uint32_t off = rootKind ? 2u - (uint32_t)goLeft : 0u;
-    const uint32_t pi = prim ? r.lfE : 0u;
-    const uint4 p0 = S.blocks[base], pc = S.blocks[base + off];
-    const float4 *rec = S.triL + (size_t)(3u * pi);
-    const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
-    asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
-                 "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
-                 "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
-    bool enter = false;
-    if (prim) {
-        if (COUNT) cnt.refs++;
-        const uint32_t k = __float_as_uint(f0.x);
-        enter = k == KINST;
-        if (!enter) {
-            if (COUNT) cnt.tests++;
-            float t, u, v;
-            bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-            const bool isRect = k == MTSG_TRIACCEL_SHAPE;
-            if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
-            if (h) {
-                r.bits |= SB_FOUND;
-                if (r.bits & SB_SHADOW) return true;   // any hit occludes
-                r.best = t;
-                stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
-                *instOut = (r.bits & SB_INST) ? save_word(8) : 0xFFFFFFFFu;
-            }
-        }
-        ++r.lfE;
-    }
-    if (inner) {
-        if (COUNT) cnt.nodes++;
-        const uint2 c = spec_take_i(r, p0, tsplit, goLeft, push);
-        r.cur = c;
-        if (rootKind && !(c.x & 0x80000000u)) {
-            if (COUNT) cnt.nodes++;
-            float ts2;
-            bool gl2, push2;
-            spec_plan(r, c, ts2, gl2, push2);
-            r.cur = spec_take_i(r, pc, ts2, gl2, push2);
-        }
-    }
-    if (enter) {
-        // Instance::rayIntersect: the ray in group space (Transform::operator()
-        // (Ray), transform.h:262-278), clipped to the group tree's AABB
-        if (COUNT) cnt.inst++;
-        const uint32_t ii = __float_as_uint(f2.w);
-        const float4 *I = S.inst + 8 * (size_t)ii;
-        const float4 L0 = I[0], L1 = I[1], L2 = I[2], A0 = I[6], A1 = I[7];
-        const float3 o = r.o, d = r.d;   // (the library is built with -ffp-contract=off)
-        const float3 lo = mk3(L0.x * o.x + L0.y * o.y + L0.z * o.z + L0.w, L1.x * o.x + L1.y * o.y + L1.z * o.z + L1.w,
-                              L2.x * o.x + L2.y * o.y + L2.z * o.z + L2.w);
-        const float3 ld = mk3(L0.x * d.x + L0.y * d.y + L0.z * d.z, L1.x * d.x + L1.y * d.y + L1.z * d.z,
-                              L2.x * d.x + L2.y * d.y + L2.z * d.z);
-        const float3 li = mk3(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
-        float nearT = -INFINITY, farT = INFINITY;
-        bool ok = true;
-        const float bmn[3] = {A0.x, A0.y, A0.z}, bmx[3] = {A1.x, A1.y, A1.z};
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const float oi = comp(lo, i), di = comp(ld, i), iv = comp(li, i);
-            if (di == 0.0f) {
-                if (oi < bmn[i] || oi > bmx[i]) ok = false;
-            } else {
-                const float t1 = (bmn[i] - oi) * iv, t2 = (bmx[i] - oi) * iv;
-                nearT = fmaxf(fminf(t1, t2), nearT);
-                farT = fminf(fmaxf(t1, t2), farT);
-            }
-        }
-        const float t0 = fmaxf(r.mint, nearT), t1 = fminf(r.best, farT);
-        if (ok & (nearT <= farT) & (t1 > t0)) {
-            save_word(0) = r.cur.x;
-            save_word(1) = r.cur.y;
-            save_word(2) = __float_as_uint(r.tmin);
-            save_word(3) = __float_as_uint(r.tmax);
-            save_word(4) = r.lfE;
-            save_word(5) = r.lfEnd;
-            save_word(6) = __float_as_uint(r.lfTmax);
-            save_word(7) = r.bits & ~SB_FOUND;
-            save_word(8) = ii;
-            const uint2 root = make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w));
-            save_word(9) = root.x;
-            save_word(10) = root.y;
-            r.o = lo;
-            r.d = ld;
-            r.inv = li;
-            r.tmin = t0;
-            r.tmax = t1;
-            r.cur = root;
-            r.lfE = r.lfEnd = 0;
-            r.lfTmax = -1.0f;
-            const uint32_t dneg = (ld.x <= 0.0f ? 1u : 0u) | (ld.y <= 0.0f ? 2u : 0u) | (ld.z <= 0.0f ? 4u : 0u);
-            r.bits = (r.bits & (SB_FOUND | SB_SHADOW)) | SB_INST | dneg << SB_DNEG;
-            return false;
-        }
-    }
-    const bool found = (r.bits & SB_FOUND) != 0;
-    const bool inInst = (r.bits & SB_INST) != 0;
-    const bool leafDone = (r.lfTmax >= 0.0f) & (r.lfE >= r.lfEnd);
-    if (leafDone & found & (r.best < r.lfTmax)) {
-        if (!inInst) return true;
-        inst_exit(r, wo, wd);
-        return false;
-    }
-    r.lfTmax = leafDone ? -1.0f : r.lfTmax;
-    const uint2 c = r.cur;
-    if ((r.lfTmax < 0.0f) & !(r.bits & SB_TRAVDONE) & (bool)(c.x >> 31)) {
-        const uint32_t st = c.x & 0x7FFFFFFFu;
-        const bool nonEmpty = st < c.y;
-        if (!nonEmpty & found & (r.best < r.tmax)) {
-            if (!inInst) return true;
-            inst_exit(r, wo, wd);
-            return false;
-        }
-        r.lfE = nonEmpty ? st : r.lfE;
-        r.lfEnd = nonEmpty ? c.y : r.lfEnd;
-        r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
-        const uint32_t b = r.bits;
-        const uint32_t cap = inInst ? (uint32_t)SHORT_STACK : (uint32_t)OUTER_STACK;
-        if (b & SB_N) {
-            const uint32_t top = b & SB_TOP, k = top == 0 ? cap - 1 : top - 1u;
-            const uint32_t i = k * TRACE_BLOCK + lane_here();
-            r.cur = inInst ? s_specNode[i] : s_outNode[i];
-            const float t = inInst ? s_specT[i] : s_outT[i];
-            r.bits = ((b & ~SB_TOP) | k) - SB_N1;
-            r.tmin = r.tmax;
-            r.tmax = fminf(t, r.best);
-        } else {
-            const bool restart = (b & SB_DROPPED) != 0;
-            const float t0 = r.tmax;
-            r.tmin = restart ? t0 : r.tmin;
-            r.tmax = restart ? r.best : r.tmax;
-            const uint2 root = inInst ? make_uint2(save_word(9), save_word(10)) : S.root2;
-            r.cur = restart ? root : c;
-            if (COUNT && restart) cnt.restarts++;
-            r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
-        }
-    }
-    const bool done = (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
-    if (done && inInst) {
-        inst_exit(r, wo, wd);
-        return false;
-    }
-    return done;
-}
-
-// Persistent traversal kernel with lane-level refill (the "while-while +
-// dynamic fetch" structure of Aila & Laine 2009, re-tiled for 64-lane waves):
-// a wave reserves FETCH work-list entries with ONE atomic into a wave-uniform
-// pool (SGPRs), and once MIN_IDLE lanes have finished their rays they take the
-// next pool entries.  One launch traces this bounce's closest-hit rays and the
-// previous bounce's shadow rays as one work list (both only depend on the
-// previous k_shade), so lanes of either kind share waves and the launch has
-// one tail instead of two:
-//   [0, nC):       closest hit of P.ray_o/ray_d[i]   -> P.hit[i]
-//   [nC, nC + nS): any hit of P.sh_o/sh_d[i - nC]    -> unoccluded: L += sh_c
-//   cIn: -1 = nIdentity closest rays (bounce 0), 0/1 = count in cnt_q(cIn), -2 = none
-//   sIn: 0/1 = count in CNT_S0/CNT_S1, -1 = none
-
-template <bool COUNT, int MIN_IDLE, bool INST = false>
-__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
-    const SpecStack stk{};
-    const unsigned long long tStart = wt ? wall_clock64() : 0ull;
-    const uint32_t nC = cIn == -1 ? nIdentity : (cIn >= 0 ? __atomic_load_n(&P.cnt[cnt_q(cIn)], __ATOMIC_RELAXED) : 0u);
-    const uint32_t nS = sIn >= 0 ? __atomic_load_n(&P.cnt[cnt_s(sIn)], __ATOMIC_RELAXED) : 0u;
-    Fetch F{&P.cnt[CNT_FETCH], nC + nS, blockIdx.x % XGROUPS, 0, max(1u, gridDim.x / XGROUPS * GUIDE_SPLIT), FETCH};
-    TraceCounts cc{0, 0, 0, 0, 0, 0, 0, 0, 0}, cs{0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t poolBase = 0, poolLeft = 0;   // wave-uniform
-    bool exhausted = false;
-    bool active = false;
-    uint32_t idx = 0;                      // index into the ray's own list
-    uint32_t iters = 0;                    // COUNT: iterations of this ray
-    uint32_t n0 = 0, t0c = 0, r0 = 0;      // COUNT: the lane's node / test / restart totals at its start
-    unsigned long long tExh = 0;           // wt: when the work list was found empty
-    uint32_t drainIters = 0;               // wt: loop iterations after that
-    SpecRay r;
-    for (;;) {
-        unsigned long long idle = __ballot(!active);
-        if ((uint32_t)__popcll(idle) < (uint32_t)MIN_IDLE && __any(active)) idle = 0;
-        while (idle && !exhausted) {
-            if (poolLeft == 0 && !F.next(FETCH, poolBase, poolLeft)) {
-                exhausted = true;
-                if (WT_DRAIN && wt) tExh = wall_clock64();
-                break;
-            }
-            const uint32_t nIdle = (uint32_t)__popcll(idle);
-            const uint32_t take = min(nIdle, poolLeft);
-            const uint32_t rank = rank_below(idle);
-            if (!active && rank < take) {
-                const uint32_t i = poolBase + rank;
-                const bool shadow = i >= nC;
-                idx = shadow ? i - nC : i;
-                float4 ro = ldS((shadow ? P.sh_o : P.ray_o) + idx), rd = ldS((shadow ? P.sh_d : P.ray_d) + idx);
-                if (shadow) { const float mint = rd.w; rd.w = ro.w; ro.w = mint; }   // sh_o.w = maxt, sh_d.w = mint
-                if (spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, shadow, r)) {
-                    active = true;
-                    if (COUNT) {
-                        iters = 0;
-                        const TraceCounts &k = shadow ? cs : cc;
-                        n0 = k.nodes; t0c = k.tests; r0 = k.restarts;
-                    }
-                } else if (shadow) {
-                    shadow_unoccluded(P, idx);
-                } else if (!(rd.w < 0.0f)) {   // maxt < 0: dead slot outside the render rectangle
-                    stS(&P.hit[idx], miss_record());
-                }
-                if (INST && !shadow) P.hitInst[idx] = 0xFFFFFFFFu;
-            }
-            poolBase += take;
-            poolLeft -= take;
-            idle = __ballot(!active);
-            if (take == nIdle) break;
-        }
-        if (!__any(active)) {
-            if (exhausted) break;
-            continue;
-        }
-        if (COUNT) {
-            // wave-level figures are booked with the closest-hit counters
-            const uint2 n = r.cur;
-            const bool inner = active && !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
-            const bool prim = active && r.lfE < r.lfEnd;
-            const bool anyInner = __any(inner), anyPrim = __any(prim);
-            const uint32_t nActive = (uint32_t)__popcll(__ballot(active));
-            if (__lane_id() == 0) { cc.wsteps += 1; cc.wnodes += anyInner; cc.wtests += anyPrim; cc.wactive += nActive; }
-        }
-        if (WT_DRAIN && wt && exhausted) ++drainIters;
-        bool done = false;
-        if (active) {
-            if (INST) {
-                const bool sh = (r.bits & SB_SHADOW) != 0;
-                const float4 *wo = (sh ? P.sh_o : P.ray_o) + idx, *wd = (sh ? P.sh_d : P.ray_d) + idx;
-                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P.hit + idx, P.hitInst + idx, wo, wd);
-                else done = spec_iter_i<COUNT>(S, r, cc, P.hit + idx, P.hitInst + idx, wo, wd);
-            } else {
-                if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx);
-                else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx);
-            }
-        }
-        if (COUNT && active) ++iters;
-        if (done) {
-            active = false;
-            if (COUNT) {
-                const bool sh = (r.bits & SB_SHADOW) != 0;
-                atomicMax(&P.ctr[sh ? 15 : 7], (unsigned long long)iters);
-                atomicAdd(&P.ctr[(sh ? 32 : 16) + min(15, 31 - __clz(max(iters, 1u)))], 1ull);
-                if (iters >= STRAGGLER_ITERS) {
-                    const unsigned long long k = atomicAdd(&P.ctr[48], 1ull);
-                    if (k < STRAGGLER_MAX) {
-                        unsigned long long *o = P.ctr + 64 + 8 * k;
-                        o[0] = __float_as_uint(r.o.x); o[1] = __float_as_uint(r.o.y); o[2] = __float_as_uint(r.o.z);
-                        o[3] = __float_as_uint(r.d.x); o[4] = __float_as_uint(r.d.y); o[5] = __float_as_uint(r.d.z);
-                        const TraceCounts &kk = sh ? cs : cc;
-                        o[6] = iters | (sh ? 0x80000000u : 0u);
-                        o[7] = min(kk.nodes - n0, 4095u) | min(kk.tests - t0c, 4095u) << 12 | min(kk.restarts - r0, 255u) << 24;
-                    }
-                }
-            }
-            // closest: hits were written through, only a miss needs a record
-            if (!(r.bits & SB_FOUND)) {
-                if (r.bits & SB_SHADOW) shadow_unoccluded(P, idx);
-                else stS(&P.hit[idx], miss_record());
-            }
-        }
-    }
-    flush_counts<COUNT>(P.ctr, cc);
-    flush_counts<COUNT>(P.ctr + 8, cs);
-    if (COUNT && INST) {
-        unsigned long long vi[2] = {cc.inst, cs.inst};
-        for (int k = 0; k < 2; ++k) {
-            for (int o2 = 32; o2 > 0; o2 >>= 1) vi[k] += __shfl_down(vi[k], o2);
-            if (lane_id() == 0) atomicAdd(P.ctr + 49 + k, vi[k]);
-        }
-    }
-    if (wt && __lane_id() == 0) {
-        wt[WT_WORDS * blockIdx.x] = tStart;
-        wt[WT_WORDS * blockIdx.x + 1] = wall_clock64();
-        wt[WT_WORDS * blockIdx.x + 2] = tExh;
-        wt[WT_WORDS * blockIdx.x + 3] = drainIters;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// camera rays (PerspectiveCamera::sampleRayDifferential, perspective.cpp:271-298)
-// ---------------------------------------------------------------------------
-DEV void slot_pixel(const DevBatch &B, uint32_t slot, int &x, int &y, uint32_t &s) {
-    const uint32_t pix = slot & (TILE * TILE - 1);
-    const uint32_t rest = slot >> 8;
-    const uint32_t sl = rest % B.ns;
-    const uint32_t tl = rest / B.ns;
-    const int tile = B.toffset + (B.tile0 + (int)tl) * B.tstride;
-    const int tx = tile % B.tiles_x, ty = tile / B.tiles_x;
-    x = B.rect_x + tx * TILE + (int)(pix % TILE);
-    y = B.rect_y + ty * TILE + (int)(pix / TILE);
-    s = B.s0 + sl;
-}
-
-__global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P) {
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    bool alive = false;
-    if (slot < B.nslots) {
-        int x, y;
-        uint32_t s;
-        slot_pixel(B, slot, x, y, s);
-        alive = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
-        if (alive) {
-            float a, b;
-            camera_jitter(I, x, y, s, a, b);
-            const float sx = ((float)x + a) * C.inv_res_x, sy = ((float)y + b) * C.inv_res_y;
-            const float *m = C.s2c;
-            float px = m[0] * sx + m[1] * sy + m[3], py = m[4] * sx + m[5] * sy + m[7];
-            float pz = m[8] * sx + m[9] * sy + m[11], pw = m[12] * sx + m[13] * sy + m[15];
-            float3 nearP = pw == 1.0f ? mk3(px, py, pz) : mk3(px, py, pz) / pw;
-            float3 d = normalize(nearP);
-            float invZ = 1.0f / d.z;
-            const float *t = C.c2w;
-            float3 wd = mk3(t[0] * d.x + t[1] * d.y + t[2] * d.z, t[4] * d.x + t[5] * d.y + t[6] * d.z,
-                            t[8] * d.x + t[9] * d.y + t[10] * d.z);
-            stS(&P.ray_o[slot], make_float4(t[3], t[7], t[11], C.near_clip * invZ));
-            stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
-            if (C.has_env) {
-                // rx/ryDirection scaled by 1/sqrt(spp) (integrator.cpp:148-149, ray.h:163-168),
-                const float3 rxc = normalize(nearP + ld3(C.dx)), ryc = normalize(nearP + ld3(C.dy));
-                const float3 rx = mk3(t[0] * rxc.x + t[1] * rxc.y + t[2] * rxc.z, t[4] * rxc.x + t[5] * rxc.y + t[6] * rxc.z,
-                                      t[8] * rxc.x + t[9] * rxc.y + t[10] * rxc.z);
-                const float3 ry = mk3(t[0] * ryc.x + t[1] * ryc.y + t[2] * ryc.z, t[4] * ryc.x + t[5] * ryc.y + t[6] * ryc.z,
-                                      t[8] * ryc.x + t[9] * ryc.y + t[10] * ryc.z);
-                const float scale = 1.0f / sqrtf((float)I.spp);
-                const float3 rxs = wd + (rx - wd) * scale, rys = wd + (ry - wd) * scale;
-                // parked in T and aux (throughput 1, no previous vertex) until
-                // bounce 0 is shaded
-                stS(&P.T[slot], make_float4(rxs.x, rxs.y, rxs.z, 1.f));
-                stS(&P.aux[slot], make_float4(rys.x, rys.y, rys.z, 0.f));
-            } else {
-                stS(&P.T[slot], make_float4(1.f, 1.f, 1.f, 1.f));
-            }
-            stS(&P.Lp[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
-            stS(&P.meta[slot], make_uint4(1u, 2u, slot, 1u));   // depth 1, 2 dimensions in one 2D request
-        } else {
-            // dead slot: bounce 0 runs over all slots and skips it
-            stS(&P.ray_d[slot], make_float4(0.f, 0.f, 1.f, -1.0f));
-            stS(&P.meta[slot], make_uint4(0u, 0u, slot, 0u));
-            stS(&P.L[slot], make_float4(0.f, 0.f, 0.f, 0.f));
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// BSDFs (local shading frame)
-// ---------------------------------------------------------------------------
-struct BsdfSample {
-    float3 wo, weight;
-    float pdf, eta;
-    uint32_t delta;
-};
-
-// warp.cpp:43-52,81-102
-DEV float3 cosine_hemisphere(float sx, float sy) {
-    float r1 = 2.0f * sx - 1.0f, r2 = 2.0f * sy - 1.0f;
-    float phi, r;
-    if (r1 == 0 && r2 == 0) { r = phi = 0; }
-    else if (r1 * r1 > r2 * r2) { r = r1; phi = (kPi / 4.0f) * (r2 / r1); }
-    else { r = r2; phi = (kPi / 2.0f) - (r1 / r2) * (kPi / 4.0f); }
-    float sinPhi, cosPhi;
-    sincosf(phi, &sinPhi, &cosPhi);
-    float px = r * cosPhi, py = r * sinPhi;
-    float z = sqrtf(fmaxf(0.0f, 1.0f - px * px - py * py));
-    if (z == 0) z = 1e-10f;
-    return mk3(px, py, z);
-}
-
-// math.cpp:25-70
-DEV float erfinv_m(float x) {
-    float w = -logf((1.0f - x) * (1.0f + x));
-    float p;
-    if (w < 5.0f) {
-        w = w - 2.5f;
-        p = 2.81022636e-08f;
-        p = 3.43273939e-07f + p * w;
-        p = -3.5233877e-06f + p * w;
-        p = -4.39150654e-06f + p * w;
-        p = 0.00021858087f + p * w;
-        p = -0.00125372503f + p * w;
-        p = -0.00417768164f + p * w;
-        p = 0.246640727f + p * w;
-        p = 1.50140941f + p * w;
-    } else {
-        w = sqrtf(w) - 3.0f;
-        p = -0.000200214257f;
-        p = 0.000100950558f + p * w;
-        p = 0.00134934322f + p * w;
-        p = -0.00367342844f + p * w;
-        p = 0.00573950773f + p * w;
-        p = -0.0076224613f + p * w;
-        p = 0.00943887047f + p * w;
-        p = 1.00167406f + p * w;
-        p = 2.83297682f + p * w;
-    }
-    return p * x;
-}
-DEV float erf_m(float x) {
-    const float a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f;
-    const float a4 = -1.453152027f, a5 = 1.061405429f, p = 0.3275911f;
-    float sign = copysignf(1.0f, x);
-    x = fabsf(x);
-    float t = 1.0f / (1.0f + p * x);
-    float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * expf(-x * x);
-    return sign * y;
-}
-DEV float hypot2_m(float a, float b) {   // math.cpp:74-86
-    float r;
-    if (fabsf(a) > fabsf(b)) { r = b / a; r = fabsf(a) * sqrtf(1.0f + r * r); }
-    else if (b != 0.0f) { r = a / b; r = fabsf(b) * sqrtf(1.0f + r * r); }
-    else r = 0.0f;
-    return r;
-}
-
-// MicrofacetDistribution, isotropic (microfacet.h:191-697)
-struct MF {
-    int type;
-    float au, av;        // roughness along the shading tangent / bitangent
-    bool visible;
-    float eu, ev;        // Phong exponents (computePhongExponent, microfacet.h:701-704)
-    DEV bool iso() const { return au == av; }
-    // microfacet.h:545-552
-    DEV float project(float3 v) const {
-        const float invSinTheta2 = 1 / (1.0f - v.z * v.z);
-        if (iso() || invSinTheta2 <= 0) return au;
-        const float cosPhi2 = v.x * v.x * invSinTheta2, sinPhi2 = v.y * v.y * invSinTheta2;
-        return sqrtf(cosPhi2 * au * au + sinPhi2 * av * av);
-    }
-    // microfacet.h:554-565 (RCPOVERFLOW_FLT = 2^-128)
-    DEV float phong_exponent(float3 v) const {
-        const float sinTheta2 = 1.0f - v.z * v.z;
-        if (iso() || sinTheta2 <= 2.93873587705571876e-39f) return eu;
-        const float invSinTheta2 = 1 / sinTheta2;
-        return eu * (v.x * v.x * invSinTheta2) + ev * (v.y * v.y * invSinTheta2);
-    }
-    // microfacet.h:191-234
-    DEV float D(float3 m) const {
-        if (m.z <= 0) return 0.0f;
-        float ct2 = m.z * m.z;
-        float be = ((m.x * m.x) / (au * au) + (m.y * m.y) / (av * av)) / ct2;
-        float result;
-        if (type == MTSG_MF_BECKMANN) result = expf(-be) / (kPi * au * av * ct2 * ct2);
-        else if (type == MTSG_MF_GGX) { float root = (1.0f + be) * ct2; result = 1.0f / (kPi * au * av * root * root); }
-        else result = sqrtf((eu + 2) * (ev + 2)) * (0.5f * kInvPi) * powf(m.z, phong_exponent(m));
-        if (result * m.z < 1e-20f) result = 0;
-        return result;
-    }
-    // microfacet.h:477-514 (Phong uses the Beckmann approximation)
-    DEV float G1(float3 v, float3 m) const {
-        if (dot(v, m) * v.z <= 0) return 0.0f;
-        float temp = 1 - v.z * v.z;
-        float tt = temp <= 0.0f ? 0.0f : fabsf(sqrtf(temp) / v.z);
-        if (tt == 0.0f) return 1.0f;
-        const float a = project(v);
-        if (type != MTSG_MF_GGX) {
-            float aa = 1.0f / (a * tt);
-            if (aa >= 1.6f) return 1.0f;
-            float aSqr = aa * aa;
-            return (3.535f * aa + 2.181f * aSqr) / (1.0f + 2.276f * aa + 2.577f * aSqr);
-        }
-        return 2.0f / (1.0f + hypot2_m(1.0f, a * tt));
-    }
-    DEV void visible11(float thetaI, float sx, float sy, float &slx, float &sly) const {
-        if (type == MTSG_MF_BECKMANN) {
-            const float SQRT_PI_INV = 0.56418958354775628695f;
-            if (thetaI < 1e-4f) {
-                float r = sqrtf(-logf(1.0f - sx));
-                float sp, cp;
-                sincosf(2 * kPi * sy, &sp, &cp);
-                slx = r * cp; sly = r * sp;
-                return;
-            }
-            float tanThetaI = tanf(thetaI), cotThetaI = 1 / tanThetaI;
-            float aa = -1, c = erf_m(cotThetaI);
-            float sample_x = fmaxf(sx, 1e-6f);
-            float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
-            float b = c - (1 + c) * powf(1 - sample_x, fit);
-            float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * expf(-cotThetaI * cotThetaI));
-            int it = 0;
-            while (++it < 10) {
-                if (!(b >= aa && b <= c)) b = 0.5f * (aa + c);
-                float invErf = erfinv_m(b);
-                float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * expf(-invErf * invErf)) - sample_x;
-                float derivative = normalization * (1 - invErf * tanThetaI);
-                if (fabsf(value) < 1e-5f) break;
-                if (value > 0) c = b; else aa = b;
-                b -= value / derivative;
-            }
-            slx = erfinv_m(b);
-            sly = erfinv_m(2.0f * fmaxf(sy, 1e-6f) - 1.0f);
-            return;
-        }
-        if (thetaI < 1e-4f) {
-            float r = sqrtf(fmaxf(0.0f, sx / (1 - sx)));
-            float sp, cp;
-            sincosf(2 * kPi * sy, &sp, &cp);
-            slx = r * cp; sly = r * sp;
-            return;
-        }
-        float tanThetaI = tanf(thetaI);
-        float aa = 1 / tanThetaI;
-        float G1v = 2.0f / (1.0f + sqrtf(fmaxf(0.0f, 1.0f + 1.0f / (aa * aa))));
-        float A = 2.0f * sx / G1v - 1.0f;
-        if (fabsf(A) == 1) A -= copysignf(1.0f, A) * kEpsilon;
-        float tmp = 1.0f / (A * A - 1.0f);
-        float B = tanThetaI;
-        float D = sqrtf(fmaxf(0.0f, B * B * tmp * tmp - (A * A - B * B) * tmp));
-        float s1 = B * tmp - D, s2 = B * tmp + D;
-        slx = (A < 0.0f || s2 > 1.0f / tanThetaI) ? s1 : s2;
-        float S;
-        if (sy > 0.5f) { S = 1.0f; sy = 2.0f * (sy - 0.5f); }
-        else { S = -1.0f; sy = 2.0f * (0.5f - sy); }
-        float z = (sy * (sy * (sy * (-0.365728915865723f) + 0.790235037209296f) - 0.424965825137544f) + 0.000152998850436920f) /
-                  (sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) - 0.539825872510702f);
-        sly = S * z * sqrtf(1.0f + slx * slx);
-    }
-    // sampleVisible (microfacet.h:421-459) or sampleAll (:287-397)
-    DEV float3 sample(float3 wi_, float sx, float sy, float &pdf) const {
-        if (visible) {
-            float3 wi = normalize(mk3(au * wi_.x, av * wi_.y, wi_.z));
-            float theta = 0, phi = 0;
-            if (wi.z < 0.99999f) { theta = acosf(wi.z); phi = atan2f(wi.y, wi.x); }
-            float sinPhi, cosPhi;
-            sincosf(phi, &sinPhi, &cosPhi);
-            float slx, sly;
-            visible11(theta, sx, sy, slx, sly);
-            float rx = cosPhi * slx - sinPhi * sly, ry = sinPhi * slx + cosPhi * sly;
-            rx *= au; ry *= av;
-            float normalization = 1.0f / sqrtf(rx * rx + ry * ry + 1.0f);
-            float3 m = mk3(-rx * normalization, -ry * normalization, normalization);
-            pdf = wi_.z == 0 ? 0.0f : G1(wi_, m) * fabsf(dot(wi_, m)) * D(m) / fabsf(wi_.z);
-            return m;
-        }
-        float sinPhiM, cosPhiM, cosThetaM;
-        if (type == MTSG_MF_PHONG) {
-            float phiM, exponent;
-            if (iso()) {
-                phiM = (2.0f * kPi) * sy;
-                exponent = eu;
-            } else if (sy < 0.25f) {
-                phong_quadrant(4 * sy, phiM, exponent);
-            } else if (sy < 0.5f) {
-                phong_quadrant(4 * (0.5f - sy), phiM, exponent);
-                phiM = kPi - phiM;
-            } else if (sy < 0.75f) {
-                phong_quadrant(4 * (sy - 0.5f), phiM, exponent);
-                phiM += kPi;
-            } else {
-                phong_quadrant(4 * (1 - sy), phiM, exponent);
-                phiM = 2 * kPi - phiM;
-            }
-            sincosf(phiM, &sinPhiM, &cosPhiM);
-            cosThetaM = powf(sx, 1.0f / (exponent + 2.0f));
-            pdf = sqrtf((eu + 2.0f) * (ev + 2.0f)) * (0.5f * kInvPi) * powf(cosThetaM, exponent + 1.0f);
-        } else {
-            float alphaSqr;
-            if (iso()) {
-                sincosf((2.0f * kPi) * sy, &sinPhiM, &cosPhiM);
-                alphaSqr = au * au;
-            } else {
-                const float phiM = atanf(av / au * tanf(kPi + 2 * kPi * sy)) + kPi * floorf(2 * sy + 0.5f);
-                sincosf(phiM, &sinPhiM, &cosPhiM);
-                const float cosSc = cosPhiM / au, sinSc = sinPhiM / av;
-                alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
-            }
-            if (type == MTSG_MF_BECKMANN) {
-                float t2 = alphaSqr * -logf(1.0f - sx);
-                cosThetaM = 1.0f / sqrtf(1.0f + t2);
-                pdf = (1.0f - sx) / (kPi * au * av * cosThetaM * cosThetaM * cosThetaM);
-            } else {
-                float t2 = alphaSqr * sx / (1.0f - sx);
-                cosThetaM = 1.0f / sqrtf(1.0f + t2);
-                float temp = 1 + t2 / alphaSqr;
-                pdf = kInvPi / (au * av * cosThetaM * cosThetaM * cosThetaM * temp * temp);
-            }
-        }
-        if (pdf < 1e-20f) pdf = 0;
-        float sinThetaM = sqrtf(fmaxf(0.0f, 1 - cosThetaM * cosThetaM));
-        return mk3(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
-    }
-    // scaleAlpha (microfacet.h:178-183)
-    DEV void scale_alpha(float v) {
-        au *= v;
-        av *= v;
-        if (type == MTSG_MF_PHONG) {
-            eu = fmaxf(2.0f / (au * au) - 2.0f, 0.0f);
-            ev = fmaxf(2.0f / (av * av) - 2.0f, 0.0f);
-        }
-    }
-    // pdf (microfacet.h:253-262): pdfVisible (:462-466) or pdfAll = D cos
-    DEV float pdf(float3 wi, float3 m) const {
-        if (visible) return wi.z == 0 ? 0.0f : G1(wi, m) * fabsf(dot(wi, m)) * D(m) / fabsf(wi.z);
-        return D(m) * m.z;
-    }
-    // sampleFirstQuadrant (microfacet.h:707-715)
-    DEV void phong_quadrant(float u1, float &phi, float &exponent) const {
-        phi = atanf(sqrtf((eu + 2.0f) / (ev + 2.0f)) * tanf(kPi * u1 * 0.5f));
-        float sinPhi, cosPhi;
-        sincosf(phi, &sinPhi, &cosPhi);
-        exponent = eu * cosPhi * cosPhi + ev * sinPhi * sinPhi;
-    }
-};
-
-// MicrofacetDistribution(props) after the loader's clamping (microfacet.h:96-144):
-// Phong never samples visible normals
-DEV MF make_mf(const mtsg_bsdf &b) {
-    MF m;
-    m.type = b.distribution;
-    m.au = b.alpha_u;
-    m.av = b.alpha_v;
-    m.visible = b.sample_visible != 0 && b.distribution != MTSG_MF_PHONG;
-    const bool phong = b.distribution == MTSG_MF_PHONG;
-    m.eu = phong ? fmaxf(2.0f / (m.au * m.au) - 2.0f, 0.0f) : 0.0f;
-    m.ev = phong ? fmaxf(2.0f / (m.av * m.av) - 2.0f, 0.0f) : 0.0f;
-    return m;
-}
-
-// util.cpp:739-761
-DEV float3 fresnel_conductor(float cosThetaI, float3 eta, float3 k) {
-    float c2 = cosThetaI * cosThetaI, s2 = 1 - c2, s4 = s2 * s2;
-    float3 temp1 = eta * eta - k * k - mk3(s2, s2, s2);
-    float3 a2pb2 = sqrtSafe3(temp1 * temp1 + k * k * eta * eta * 4);
-    float3 aa = sqrtSafe3((a2pb2 + temp1) * 0.5f);
-    float3 term1 = a2pb2 + mk3(c2, c2, c2), term2 = aa * (2 * cosThetaI);
-    float3 Rs2 = (term1 - term2) / (term1 + term2);
-    float3 term3 = a2pb2 * c2 + mk3(s4, s4, s4), term4 = term2 * s2;
-    float3 Rp2 = Rs2 * (term3 - term4) / (term3 + term4);
-    return (Rp2 + Rs2) * 0.5f;
-}
-
-// util.cpp:651-681
-DEV float fresnel_dielectric(float cosThetaI_, float &cosThetaT_, float eta) {
-    if (eta == 1) { cosThetaT_ = -cosThetaI_; return 0.0f; }
-    float scale = (cosThetaI_ > 0) ? 1 / eta : eta, c2 = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
-    if (c2 <= 0.0f) { cosThetaT_ = 0.0f; return 1.0f; }
-    float ci = fabsf(cosThetaI_), ct = sqrtf(c2);
-    float Rs = (ci - eta * ct) / (ci + eta * ct), Rp = (eta * ci - ct) / (eta * ci + ct);
-    cosThetaT_ = (cosThetaI_ > 0) ? -ct : ct;
-    return 0.5f * (Rs * Rs + Rp * Rp);
-}
-
-// fresnelDielectricExt without the transmitted cosine (util.cpp:651-681)
-DEV float fresnel_dielectric1(float cosThetaI, float eta) {
-    float cosThetaT;
-    return fresnel_dielectric(cosThetaI, cosThetaT, eta);
-}
-
-// plastic.cpp:216-222: the diffuse base renormalised for internal reflection
-DEV float3 plastic_diffuse(const mtsg_bsdf &b) {
-    float3 diff = ld3(b.reflectance);
-    if (b.nonlinear) diff = diff / (mk3(1.0f, 1.0f, 1.0f) - diff * b.fdr_int);
-    else diff = diff / (1 - b.fdr_int);
-    return diff;
-}
-DEV float plastic_prob_specular(const mtsg_bsdf &b, float Fi) {
-    return (Fi * b.spec_sampling_weight) / (Fi * b.spec_sampling_weight + (1 - Fi) * (1 - b.spec_sampling_weight));
-}
-
-// evalCubicInterp1D over [0, 1] (spline.cpp:23-60)
-DEV float cubic_interp1d(float x, const float *v, int n) {
-    if (!(x >= 0.0f && x <= 1.0f)) return 0.0f;
-    float t = x * (float)(n - 1);
-    const int k = min((int)t, n - 2);
-    const float f0 = v[k], f1 = v[k + 1];
-    const float d0 = k > 0 ? 0.5f * (v[k + 1] - v[k - 1]) : v[k + 1] - v[k];
-    const float d1 = k + 2 < n ? 0.5f * (v[k + 2] - v[k]) : v[k + 1] - v[k];
-    t = t - (float)k;
-    const float t2 = t * t, t3 = t2 * t;
-    return (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
-}
-// RoughTransmittance::eval with eta and alpha fixed (rtrans.h:169-181, 205-206)
-DEV float rough_trans(const mtsg_bsdf &b, float cosTheta) {
-    if (!(cosTheta >= 0)) return 0.0f;
-    const float r = cubic_interp1d(powf(fabsf(cosTheta), 0.25f), b.rtrans, MTSG_RTRANS_SAMPLES);
-    return fminf(1.0f, fmaxf(0.0f, r));
-}
-
-// BSDF::eval * cos (ESolidAngle) and pdf for the smooth BSDFs.  EXT: the
-// scene has conductor / plastic / twosided records (the shade kernel is
-// instantiated without them otherwise: their code costs the common
-// diffuse + roughconductor + dielectric kernel its register budget)
-template <bool EXT>
-DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
-    pdf = 0.0f;
-    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:107-126
-        if (!b.smooth || wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
-        pdf = kInvPi * wo.z;
-        return ld3(b.reflectance) * (kInvPi * wo.z);
-    }
-    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:235-293
-        if (wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
-        float3 H = normalize(wo + wi);
-        const MF mf = make_mf(b);
-        const float Dv = mf.D(H);
-        if (mf.visible) pdf = Dv * mf.G1(wi, H) / (4.0f * wi.z);
-        else pdf = Dv * H.z / (4 * fabsf(dot(wo, H)));
-        if (Dv == 0) return mk3(0, 0, 0);
-        float3 F = fresnel_conductor(dot(wi, H), ld3(b.eta), ld3(b.k)) * ld3(b.spec_refl);
-        const float G = mf.G1(wi, H) * mf.G1(wo, H);
-        float model = Dv * G / (4.0f * wi.z);
-        return F * model;
-    }
-    if (EXT && b.type == MTSG_BSDF_ROUGHDIELECTRIC) {   // roughdielectric.cpp:265-400
-        if (wi.z == 0) return mk3(0, 0, 0);
-        const bool reflect = wi.z * wo.z > 0;
-        const float eta = wi.z > 0 ? b.ior_eta : b.ior_inv_eta;
-        float3 H = reflect ? normalize(wo + wi) : normalize(wi + wo * eta);
-        H = H * copysignf(1.0f, H.z);
-        float dwh_dwo;
-        if (reflect) {
-            dwh_dwo = 1.0f / (4.0f * dot(wo, H));
-        } else {
-            const float sqrtDenom = dot(wi, H) + eta * dot(wo, H);
-            dwh_dwo = (eta * eta * dot(wo, H)) / (sqrtDenom * sqrtDenom);
-        }
-        const MF distr = make_mf(b);
-        MF sampleDistr = distr;
-        if (!distr.visible) sampleDistr.scale_alpha(1.2f - 0.2f * sqrtf(fabsf(wi.z)));
-        float prob = sampleDistr.pdf(wi * copysignf(1.0f, wi.z), H);
-        const float F = fresnel_dielectric1(dot(wi, H), b.ior_eta);
-        prob *= reflect ? F : (1 - F);
-        pdf = fabsf(prob * dwh_dwo);
-        const float D = distr.D(H);
-        if (D == 0) return mk3(0, 0, 0);
-        const float G = distr.G1(wi, H) * distr.G1(wo, H);
-        if (reflect) {
-            const float value = F * D * G / (4.0f * fabsf(wi.z));
-            return ld3(b.spec_refl) * value;
-        }
-        const float sqrtDenom = dot(wi, H) + eta * dot(wo, H);
-        const float value = ((1 - F) * D * G * eta * eta * dot(wi, H) * dot(wo, H)) / (wi.z * sqrtDenom * sqrtDenom);
-        const float factor = wi.z > 0 ? b.ior_inv_eta : b.ior_eta;   // ERadiance
-        return ld3(b.spec_trans) * fabsf(value * factor * factor);
-    }
-    if (EXT && b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:190-263, the diffuse (ESolidAngle) part
-        if (wo.z <= 0 || wi.z <= 0) return mk3(0, 0, 0);
-        const float Fi = fresnel_dielectric1(wi.z, b.ior_eta), Fo = fresnel_dielectric1(wo.z, b.ior_eta);
-        const float invEta2 = 1 / (b.ior_eta * b.ior_eta);
-        pdf = kInvPi * wo.z * (1 - plastic_prob_specular(b, Fi));
-        return plastic_diffuse(b) * (kInvPi * wo.z * invEta2 * (1 - Fi) * (1 - Fo));
-    }
-    if (EXT && b.type == MTSG_BSDF_ROUGHPLASTIC) {   // roughplastic.cpp:302-345 (eval), 347-385 (pdf)
-        if (wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
-        const MF mf = make_mf(b);
-        const float3 H = normalize(wo + wi);
-        const float D = mf.D(H);
-        const float F = fresnel_dielectric1(dot(wi, H), b.ior_eta);
-        const float G = mf.G1(wi, H) * mf.G1(wo, H);
-        const float value = F * D * G / (4.0f * wi.z);
-        const float T12 = rough_trans(b, wi.z), T21 = rough_trans(b, wo.z);
-        const float invEta2 = 1.0f / (b.ior_eta * b.ior_eta);
-        float probSpecular = plastic_prob_specular(b, 1 - T12);
-        const float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
-        pdf = mf.pdf(wi, H) * dwh_dwo * probSpecular + (1 - probSpecular) * (kInvPi * wo.z);
-        return ld3(b.spec_refl) * value + plastic_diffuse(b) * (kInvPi * wo.z * T12 * T21 * invEta2);
-    }
-    return mk3(0, 0, 0);   // dielectric / conductor: delta components only
-}
-
-// next1d: the sampler's next1D, drawn only where Mitsuba draws it
-// (roughdielectric's reflect/refract choice: roughdielectric.cpp:531-539)
-template <bool EXT, class Next1D>
-DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r, Next1D &&next1d) {
-    r.eta = 1.0f;
-    r.delta = 0;
-    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
-        if (wi.z <= 0) return false;
-        r.wo = cosine_hemisphere(sx, sy);
-        r.pdf = kInvPi * r.wo.z;
-        r.weight = ld3(b.reflectance);
-        return !isZero(r.weight);
-    }
-    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:345-394
-        if (wi.z < 0) return false;
-        const MF mf = make_mf(b);
-        float pdf;
-        float3 m = mf.sample(wi, sx, sy, pdf);
-        if (pdf == 0) return false;
-        r.wo = m * (2 * dot(wi, m)) - wi;
-        if (r.wo.z <= 0) return false;
-        float3 F = fresnel_conductor(dot(wi, m), ld3(b.eta), ld3(b.k)) * ld3(b.spec_refl);
-        float weight;
-        if (mf.visible) weight = mf.G1(r.wo, m);
-        else weight = mf.D(m) * mf.G1(wi, m) * mf.G1(r.wo, m) * dot(wi, m) / (pdf * wi.z);
-        r.pdf = pdf / (4.0f * dot(r.wo, m));
-        r.weight = F * weight;
-        return !isZero(r.weight);
-    }
-    if (b.type == MTSG_BSDF_DIELECTRIC) {   // dielectric.cpp:277-333
-        float cosThetaT;
-        float F = fresnel_dielectric(wi.z, cosThetaT, b.ior_eta);
-        r.delta = 1;
-        if (sx <= F) {
-            r.wo = mk3(-wi.x, -wi.y, wi.z);
-            r.pdf = F;
-            r.weight = ld3(b.spec_refl);
-        } else {
-            float scale = -(cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta);
-            r.wo = mk3(scale * wi.x, scale * wi.y, cosThetaT);
-            r.eta = cosThetaT < 0 ? b.ior_eta : b.ior_inv_eta;
-            r.pdf = 1 - F;
-            float factor = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;
-            r.weight = ld3(b.spec_trans) * (factor * factor);
-        }
-        return !isZero(r.weight);
-    }
-    if (EXT && b.type == MTSG_BSDF_CONDUCTOR) {   // conductor.cpp:220-236
-        if (wi.z <= 0) return false;
-        r.delta = 1;
-        r.wo = mk3(-wi.x, -wi.y, wi.z);
-        r.pdf = 1.0f;
-        r.weight = ld3(b.spec_refl) * fresnel_conductor(wi.z, ld3(b.eta), ld3(b.k));
-        return !isZero(r.weight);
-    }
-    if (EXT && b.type == MTSG_BSDF_ROUGHDIELECTRIC) {   // roughdielectric.cpp:508-590
-        const MF distr = make_mf(b);
-        MF sampleDistr = distr;
-        if (!distr.visible) sampleDistr.scale_alpha(1.2f - 0.2f * sqrtf(fabsf(wi.z)));
-        float microfacetPDF;
-        const float3 m = sampleDistr.sample(wi * copysignf(1.0f, wi.z), sx, sy, microfacetPDF);
-        if (microfacetPDF == 0) return false;
-        r.pdf = microfacetPDF;
-        float cosThetaT;
-        const float F = fresnel_dielectric(dot(wi, m), cosThetaT, b.ior_eta);
-        bool sampleReflection = true;
-        if (next1d() > F) {
-            sampleReflection = false;
-            r.pdf *= 1 - F;
-        } else {
-            r.pdf *= F;
-        }
-        float3 weight;
-        float dwh_dwo;
-        if (sampleReflection) {
-            r.wo = m * (2 * dot(wi, m)) - wi;
-            r.eta = 1.0f;
-            if (wi.z * r.wo.z <= 0) return false;
-            weight = ld3(b.spec_refl);
-            dwh_dwo = 1.0f / (4.0f * dot(r.wo, m));
-        } else {
-            if (cosThetaT == 0) return false;
-            const float e = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;   // refract (util.cpp:767-772)
-            r.wo = m * (dot(wi, m) * e + cosThetaT) - wi * e;
-            r.eta = cosThetaT < 0 ? b.ior_eta : b.ior_inv_eta;
-            if (wi.z * r.wo.z >= 0) return false;
-            const float factor = cosThetaT < 0 ? b.ior_inv_eta : b.ior_eta;
-            weight = ld3(b.spec_trans) * (factor * factor);
-            const float sqrtDenom = dot(wi, m) + r.eta * dot(r.wo, m);
-            dwh_dwo = (r.eta * r.eta * dot(r.wo, m)) / (sqrtDenom * sqrtDenom);
-        }
-        if (distr.visible) weight = weight * distr.G1(r.wo, m);
-        else weight = weight * fabsf(distr.D(m) * (distr.G1(wi, m) * distr.G1(r.wo, m)) * dot(wi, m) / (microfacetPDF * wi.z));
-        r.pdf *= fabsf(dwh_dwo);
-        r.weight = weight;
-        return !isZero(r.weight);
-    }
-    if (EXT && b.type == MTSG_BSDF_ROUGHPLASTIC) {   // roughplastic.cpp:387-455: component chosen by sample.y
-        if (wi.z <= 0) return false;
-        const float probSpecular = plastic_prob_specular(b, 1 - rough_trans(b, wi.z));
-        if (sy < probSpecular) {
-            sy /= probSpecular;
-            const MF mf = make_mf(b);
-            float mpdf;
-            const float3 m = mf.sample(wi, sx, sy, mpdf);
-            r.wo = m * (2 * dot(wi, m)) - wi;
-            if (r.wo.z <= 0) return false;
-        } else {
-            sy = (sy - probSpecular) / (1 - probSpecular);
-            r.wo = cosine_hemisphere(sx, sy);
-        }
-        float pdf;
-        const float3 val = bsdf_eval1<EXT>(b, wi, r.wo, pdf);
-        if (pdf == 0) return false;
-        r.pdf = pdf;
-        r.weight = val / pdf;
-        return !isZero(r.weight);
-    }
-    if (EXT && b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:344-375 (both components)
-        if (wi.z <= 0) return false;
-        const float Fi = fresnel_dielectric1(wi.z, b.ior_eta);
-        const float probSpecular = plastic_prob_specular(b, Fi);
-        if (sx < probSpecular) {
-            r.delta = 1;
-            r.wo = mk3(-wi.x, -wi.y, wi.z);
-            r.pdf = probSpecular;
-            r.weight = ld3(b.spec_refl) * Fi / probSpecular;
-        } else {
-            r.wo = cosine_hemisphere((sx - probSpecular) / (1 - probSpecular), sy);
-            const float Fo = fresnel_dielectric1(r.wo.z, b.ior_eta);
-            const float invEta2 = 1 / (b.ior_eta * b.ior_eta);
-            r.pdf = (1 - probSpecular) * (kInvPi * r.wo.z);
-            r.weight = plastic_diffuse(b) * (invEta2 * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
-        }
-        return !isZero(r.weight);
-    }
-    return false;
-}
-
-// twosided.cpp:103-170: a twosided front record hands back-side queries to
-// bsdfs[back] with the z components negated
-template <bool EXT>
-DEV float3 bsdf_eval(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
-    if (EXT && b.twosided && !(wi.z > 0)) {
-        wi.z = -wi.z;
-        wo.z = -wo.z;
-        return bsdf_eval1<EXT>(all[b.back], wi, wo, pdf);
-    }
-    return bsdf_eval1<EXT>(b, wi, wo, pdf);
-}
-template <bool EXT, class Next1D>
-DEV bool bsdf_sample(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r, Next1D &&next1d) {
-    if (EXT && b.twosided && wi.z < 0) {
-        wi.z = -wi.z;
-        if (!bsdf_sample1<EXT>(all[b.back], wi, sx, sy, r, next1d)) return false;
-        r.wo.z = -r.wo.z;
-        return true;
-    }
-    return bsdf_sample1<EXT>(b, wi, sx, sy, r, next1d);
-}
-
-DEV float mis(float pdfA, float pdfB) {   // path.cpp:296-300
-    pdfA *= pdfA;
-    pdfB *= pdfB;
-    return pdfA / (pdfA + pdfB);
-}
-
-// DiscreteDistribution::sampleReuse (pmf.h:128-188): lower_bound over cdf[0..n]
-DEV uint32_t pmf_sample_reuse(const float *cdf, uint32_t n, float &x, float &pdf) {
-    uint32_t lo = 0, len = n + 1;
-    while (len > 0) {   // std::lower_bound
-        uint32_t half = len >> 1;
-        if (cdf[lo + half] < x) { lo += half + 1; len -= half + 1; }
-        else len = half;
-    }
-    int idx = (int)lo - 1;
-    uint32_t index = (uint32_t)min((int)n - 1, max(0, idx));
-    while ((cdf[index + 1] - cdf[index]) == 0 && index < n) ++index;
-    float c0 = cdf[index], c1 = cdf[index + 1];
-    pdf = c1 - c0;
-    x = (x - c0) / (c1 - c0);
-    return index;
-}
-
-// ---------------------------------------------------------------------------
-// shading
-// ---------------------------------------------------------------------------
-struct Its {
-    float3 p, geoN;
-    Frame3 sh;
-    int shape, bsdf, emitter;
-};
-
-// ShapeKDTree::fillIntersectionRecord<true> (skdtree.h:343-428) + computeShadingFrame (util.cpp:603-608).
-// inst != ~0: the hit was found inside that instance; the group tree fills
-// the record from the group-space ray (BarycentricPos = false, so p = ray(t))
-// and Instance::fillIntersectionRecord (instance.cpp:146-160) maps it back
-// with toWorld, normals by the inverse transpose (transform.h:203-211)
-DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, uint32_t inst, Its &its) {
-#pragma clang fp contract(off)
-    const uint32_t p = __float_as_uint(h.w);   // triangle, or 0x80000000 | rectangle
-    float3 dpdu, n;
-    if (!(p & 0x80000000u)) {
-        const float4 *rec = S.shrec + 6 * (size_t)p;
-        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3], r4 = rec[4], r5 = rec[5];
-        const float3 p0 = mk3(r0.x, r0.y, r0.z), p1 = mk3(r0.w, r1.x, r1.y), p2 = mk3(r1.z, r1.w, r2.x);
-        const float3 n0 = mk3(r2.y, r2.z, r2.w), n1 = mk3(r3.x, r3.y, r3.z), n2 = mk3(r3.w, r4.x, r4.y);
-        dpdu = mk3(r4.z, r4.w, r5.x);
-        its.shape = (int)__float_as_uint(r5.y);
-        const uint32_t bw = __float_as_uint(r5.z);
-        its.bsdf = (int)(bw & 0x7FFFFFFFu);
-        its.emitter = (int)__float_as_uint(r5.w);
-        const float bx = 1 - h.y - h.z, by = h.y, bz = h.z;
-        float3 fn = cross(p1 - p0, p2 - p0);
-        if (!isZero(fn)) fn = fn / length(fn);
-        if (!(bw & 0x80000000u)) {
-            n = normalize(n0 * bx + n1 * by + n2 * bz);
-            if (dot(fn, n) < 0) fn = -fn;
-        } else {
-            n = fn;
-        }
-        if (inst == 0xFFFFFFFFu) {
-            its.p = p0 * bx + p1 * by + p2 * bz;
-            its.geoN = fn;
-        } else {
-            const float4 *I = S.inst + 8 * (size_t)inst;
-            const float4 L0 = I[0], L1 = I[1], L2 = I[2], W0 = I[3], W1 = I[4], W2 = I[5];
-            const float3 lo = mk3(L0.x * ro.x + L0.y * ro.y + L0.z * ro.z + L0.w, L1.x * ro.x + L1.y * ro.y + L1.z * ro.z + L1.w,
-                                  L2.x * ro.x + L2.y * ro.y + L2.z * ro.z + L2.w);
-            const float3 ld = mk3(L0.x * rd.x + L0.y * rd.y + L0.z * rd.z, L1.x * rd.x + L1.y * rd.y + L1.z * rd.z,
-                                  L2.x * rd.x + L2.y * rd.y + L2.z * rd.z);
-            const float3 pl = lo + ld * h.x;
-            auto normalT = [&](float3 v) {
-                return mk3(L0.x * v.x + L1.x * v.y + L2.x * v.z, L0.y * v.x + L1.y * v.y + L2.y * v.z,
-                           L0.z * v.x + L1.z * v.y + L2.z * v.z);
-            };
-            n = normalize(normalT(n));
-            its.geoN = normalize(normalT(fn));
-            dpdu = mk3(W0.x * dpdu.x + W0.y * dpdu.y + W0.z * dpdu.z, W1.x * dpdu.x + W1.y * dpdu.y + W1.z * dpdu.z,
-                       W2.x * dpdu.x + W2.y * dpdu.y + W2.z * dpdu.z);
-            its.p = mk3(W0.x * pl.x + W0.y * pl.y + W0.z * pl.z + W0.w, W1.x * pl.x + W1.y * pl.y + W1.z * pl.z + W1.w,
-                        W2.x * pl.x + W2.y * pl.y + W2.z * pl.z + W2.w);
-        }
-    } else {
-        const mtsg_rect &r = S.rects[p & 0x7FFFFFFFu];
-        its.shape = (int)r.shape_index;
-        its.bsdf = S.shapes[its.shape].bsdf;
-        its.emitter = S.shapes[its.shape].emitter;
-        its.geoN = ld3(r.frame_n);
-        n = its.geoN;
-        dpdu = ld3(r.dpdu);
-        its.p = ro + rd * h.x;
-    }
-    its.sh.n = n;
-    its.sh.s = normalize(dpdu - n * dot(n, dpdu));
-    its.sh.t = cross(n, its.sh.s);
-}
-
-// Shape::sampleDirect over TriMesh / Rectangle samplePosition (shape.cpp:102-115,
-// trimesh.cpp:412-423, triangle.cpp:24-60, rectangle.cpp:200-207)
-DEV void emitter_sample_position(const DevScene &S, const mtsg_emitter &em, float sx, float sy, float3 &p, float3 &n) {
-    const mtsg_shape &sh = S.shapes[em.shape];
-    if (sh.type == MTSG_SHAPE_MESH) {
-        float pdfDummy;
-        uint32_t index = pmf_sample_reuse(S.emitter_tri_cdf + em.cdf_offset, sh.tri_count, sy, pdfDummy);
-        const uint4 ti = S.tidx[sh.tri_begin + index];
-        const float3 p0 = xyz(S.vpos[ti.x]), p1 = xyz(S.vpos[ti.y]), p2 = xyz(S.vpos[ti.z]);
-        float a = sqrtf(fmaxf(0.0f, 1.0f - sx));
-        float bx = 1 - a, by = a * sy;
-        float3 sideA = p1 - p0, sideB = p2 - p0;
-        p = p0 + (sideA * bx) + (sideB * by);
-        if (!sh.face_normals)
-            n = normalize(xyz(S.vnrm[ti.x]) * (1.0f - bx - by) + xyz(S.vnrm[ti.y]) * bx + xyz(S.vnrm[ti.z]) * by);
-        else
-            n = normalize(cross(sideA, sideB));
-    } else {
-        const mtsg_rect &r = S.rects[sh.rect];
-        const float *m = r.to_world;
-        float x = sx * 2 - 1, y = sy * 2 - 1;
-        p = mk3(m[0] * x + m[1] * y + m[3], m[4] * x + m[5] * y + m[7], m[8] * x + m[9] * y + m[11]);
-        n = ld3(r.frame_n);
-    }
-}
-
-// Block-aggregated queue append: one LDS atomic per wave, one global atomic
-// per workgroup and queue (a contended global word costs ~11 ns per atomic).
-struct BlockAppend {
-    uint32_t cnt[2];
-    uint32_t base[2];
-};
-
-DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p0, bool p1, uint32_t &i0, uint32_t &i1) {
-    if (threadIdx.x == 0) { ba.cnt[0] = 0; ba.cnt[1] = 0; }
-    __syncthreads();
-    const unsigned long long m0 = __ballot(p0), m1 = __ballot(p1);
-    const unsigned long long below = (1ull << lane_id()) - 1ull;
-    uint32_t w0 = 0, w1 = 0;
-    if (lane_id() == 0) {
-        if (m0) w0 = atomicAdd(&ba.cnt[0], (uint32_t)__popcll(m0));
-        if (m1) w1 = atomicAdd(&ba.cnt[1], (uint32_t)__popcll(m1));
-    }
-    w0 = __shfl(w0, 0);
-    w1 = __shfl(w1, 0);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        ba.base[0] = ba.cnt[0] ? atomicAdd(gcnt0, ba.cnt[0]) : 0u;
-        ba.base[1] = ba.cnt[1] ? atomicAdd(gcnt1, ba.cnt[1]) : 0u;
-    }
-    __syncthreads();
-    i0 = ba.base[0] + w0 + (uint32_t)__popcll(m0 & below);
-    i1 = ba.base[1] + w1 + (uint32_t)__popcll(m1 & below);
-}
-
-// outgoing records of one workgroup (36 KB: 4 workgroups per CU at 4 waves/SIMD)
-struct ShadeStage {
-    float4 o[SHADE_BLOCK], d[SHADE_BLOCK], T[SHADE_BLOCK], aux[SHADE_BLOCK], L[SHADE_BLOCK];
-    uint4 meta[SHADE_BLOCK];
-    float4 sho[SHADE_BLOCK], shd[SHADE_BLOCK], shc[SHADE_BLOCK];
-};
-
-// qin < 0: bounce 0 over the identity queue of nIdentity slots
-#ifndef MTSG_SHADE_WAVES
-#define MTSG_SHADE_WAVES 4   // 127 VGPRs: 4 waves/SIMD (3 at 144; 5+ spill heavily)
-#endif
-#if MTSG_SHADE_WAVES > 0
-#define SHADE_ATTR __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SHADE_WAVES)))
-#else
-#define SHADE_ATTR __launch_bounds__(SHADE_BLOCK)
-#endif
-// ENV: the scene has an environment emitter (the variant without it keeps
-// the environment code, and its registers, out of the common case)
-// SMP: the render's sampler (MTSG_SAMPLER_*)
-template <bool ENV, int SMP, bool EXT>
-__global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int bounce, int qin,
-                                                 uint32_t nIdentity, int hasAlpha) {
-    __shared__ BlockAppend ba;
-    __shared__ ShadeStage stage;
-    uint32_t count = nIdentity;
-    if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
-    const uint32_t nIter = (count + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
-    const int qout = qin < 0 ? 1 : (qin ^ 1);
-    for (uint32_t it = 0; it < nIter; ++it) {
-        const uint32_t i = (it * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
-        bool alive = i < count;
-        bool cont = false, shadow = false;
-        uint4 meta = make_uint4(0u, 0u, 0u, 0u);
-        if (alive) {
-            meta = ldS(&P.meta[i]);
-            if (meta.x == 0u) alive = false;   // dead slot (bounce 0)
-        }
-        const uint32_t slot = meta.z;
-        if (alive) {
-            const float4 h = ldS(&P.hit[i]);
-            const float4 ro4 = ldS(&P.ray_o[i]), rd4 = ldS(&P.ray_d[i]);
-            const float3 ro = xyz(ro4), rd = xyz(rd4);
-            float4 L4 = ldS(&P.Lp[i]);
-            float4 T4 = ldS(&P.T[i]);
-            PathSampler smp;
-            {
-                int x, y;
-                uint32_t sIdx;
-                slot_pixel(B, slot, x, y, sIdx);
-                smp = path_sampler(I, x, y, sIdx, meta.y, meta.w);
-            }
-            float3 L = xyz(L4), T = xyz(T4);
-            float eta = T4.w;
-            uint32_t depth = meta.x & 0xFFFFu;
-            uint32_t flags = meta.x & 0xFFFF0000u;
-            const bool valid = __float_as_uint(h.w) != 0xFFFFFFFFu;
-            bool done = false;
-            Its its;
-            if (valid) fill_its(S, ro, rd, h, S.inst ? P.hitInst[i] : 0xFFFFFFFFu, its);
-            if (bounce == 0) {
-                // RadianceQueryRecord::rayIntersect (records.inl:117-143)
-                if (hasAlpha) L4.w = valid ? 1.0f : 0.0f;
-                if (!valid) {
-                    // Scene::evalEnvironment of the differential camera ray (path.cpp:136-143)
-                    if (ENV && !I.hide_emitters) {
-                        const float3 rxd = T, ryd = xyz(ldS(&P.aux[i]));
-                        L += env_eval(S.env, rd, true, rxd, ryd);   // throughput 1
-                    }
-                    done = true;
-                }
-                if (ENV) T = mk3(1.f, 1.f, 1.f);   // T held the x-differential
-            } else {
-                // tail of the previous iteration after scene->rayIntersect (path.cpp:226-286)
-                if (!valid) {
-                    // environment hit by the BSDF sample (path.cpp:236-246, 257-265)
-                    if (ENV && !(I.hide_emitters && !(flags & F_SCATTERED))) {
-                        const float3 value = env_eval(S.env, rd, false, rd, rd);
-                        float nearT, farT;
-                        if (env_sphere(S.env, ro, rd, nearT, farT) && !(nearT > 0) && !(farT < 0)) {
-                            float lumPdf = 0.0f;
-                            if (!(flags & F_DELTA))   // Scene::pdfEmitterDirect -> EnvironmentMap::pdfDirect
-                                lumPdf = env_internal_pdf(S.env, env_rot(S.env.E->to_local, rd)) *
-                                         S.emitters[S.env.E->emitter].pdf_discrete;
-                            L += T * value * mis(ldS(&P.aux[i]).w, lumPdf);
-                        }
-                    }
-                    done = true;
-                } else {
-                    const int em = its.emitter;
-                    if (em >= 0) {
-                        const mtsg_emitter &E = S.emitters[em];
-                        const float3 value = dot(its.sh.n, -rd) > 0 ? ld3(E.radiance) : mk3(0, 0, 0);
-                        float lumPdf = 0.0f;
-                        if (!(flags & F_DELTA)) {
-                            // Scene::pdfEmitterDirect with dRec.setQuery(ray, its)
-                            const float4 ax = ldS(&P.aux[i]);
-                            const float3 refN = xyz(ax);
-                            if (dot(rd, refN) >= 0 && dot(rd, its.sh.n) < 0)
-                                lumPdf = E.inv_area * (h.x * h.x) / fabsf(dot(rd, its.sh.n));
-                            lumPdf *= E.pdf_discrete;
-                        }
-                        L += T * value * mis(ldS(&P.aux[i]).w, lumPdf);
-                    }
-                    if (depth++ >= (uint32_t)I.rr_depth) {
-                        float q = fminf(maxc(T) * eta * eta, 0.95f);
-                        if (next1D<SMP>(I, smp) >= q) done = true;
-                        else T = T / q;
-                    }
-                }
-            }
-            if (!done && !((int)depth <= I.max_depth || I.max_depth < 0)) done = true;
-            if (!done) {
-                const mtsg_bsdf &bsdf = S.bsdfs[its.bsdf];
-                const float3 wi = its.sh.toLocal(-rd);
-                if (bounce == 0 && its.emitter >= 0 && !I.hide_emitters) {
-                    if (dot(its.sh.n, -rd) > 0) L += T * ld3(S.emitters[its.emitter].radiance);
-                }
-                if (((int)depth >= I.max_depth && I.max_depth > 0) ||
-                    (I.strict_normals && dot(rd, its.geoN) * wi.z >= 0)) {
-                    done = true;
-                } else {
-                    const float3 refN = bsdf.ref_n_zero ? mk3(0, 0, 0) : its.sh.n;
-                    // ---- direct illumination (path.cpp:172-200)
-                    if (bsdf.smooth) {
-                        float sx, sy;
-                        next2D<SMP>(I, smp, sx, sy);
-                        float emPdf;
-                        const uint32_t ei = pmf_sample_reuse(S.emitter_cdf, S.n_emitters, sx, emPdf);
-                        const mtsg_emitter &E = S.emitters[ei];
-                        float3 dd, value;
-                        float dist, pdf;
-                        bool accepted;
-                        if (ENV && E.type == MTSG_EMITTER_ENVMAP) {
-                            accepted = env_sample_direct(S.env, its.p, sx, sy, dd, dist, value, pdf);
-                        } else {
-                            float3 ep, en;
-                            emitter_sample_position(S, E, sx, sy, ep, en);
-                            dd = ep - its.p;
-                            const float distSquared = dot(dd, dd);
-                            dist = sqrtf(distSquared);
-                            dd = dd / dist;
-                            const float dp = fabsf(dot(dd, en));
-                            pdf = E.inv_area * (dp != 0 ? (distSquared / dp) : 0.0f);
-                            accepted = dot(dd, refN) >= 0 && dot(dd, en) < 0 && pdf != 0;
-                            if (accepted) value = ld3(E.radiance) / pdf;
-                        }
-                        if (accepted) {
-                            pdf *= emPdf;
-                            value = value / emPdf;
-                            const float3 wo = its.sh.toLocal(dd);
-                            float bpdf;
-                            const float3 bval = bsdf_eval<EXT>(S.bsdfs, bsdf, wi, wo, bpdf);
-                            if (!isZero(bval) && (!I.strict_normals || dot(its.geoN, dd) * wo.z > 0)) {
-                                const float weight = mis(pdf, bpdf);
-                                const float3 c = T * value * bval * weight;
-                                if (!isZero(c)) {
-                                    shadow = true;
-                                    stage.sho[threadIdx.x] = make_float4(its.p.x, its.p.y, its.p.z, dist * (1 - kShadowEpsilon));
-                                    stage.shd[threadIdx.x] = make_float4(dd.x, dd.y, dd.z, kEpsilon);
-                                    stage.shc[threadIdx.x] = make_float4(c.x, c.y, c.z, 0.f);
-                                }
-                            }
-                        }
-                    }
-                    // ---- BSDF sampling (path.cpp:206-221)
-                    float sx, sy;
-                    next2D<SMP>(I, smp, sx, sy);
-                    BsdfSample bs;
-                    if (!bsdf_sample<EXT>(S.bsdfs, bsdf, wi, sx, sy, bs, [&]() { return next1D<SMP>(I, smp); })) {
-                        done = true;
-                    } else {
-                        flags |= F_SCATTERED;
-                        const float3 wo = its.sh.toWorld(bs.wo);
-                        if (I.strict_normals && dot(its.geoN, wo) * bs.wo.z <= 0) {
-                            done = true;
-                        } else {
-                            T = T * bs.weight;
-                            eta *= bs.eta;
-                            flags = bs.delta ? (flags | F_DELTA) : (flags & ~F_DELTA);
-                            stage.o[threadIdx.x] = make_float4(its.p.x, its.p.y, its.p.z, kEpsilon);
-                            stage.d[threadIdx.x] = make_float4(wo.x, wo.y, wo.z, INFINITY);
-                            stage.aux[threadIdx.x] = make_float4(refN.x, refN.y, refN.z, bs.pdf);
-                            cont = true;
-                        }
-                    }
-                }
-            }
-            if ((SMP == MTSG_SAMPLER_HALTON || SMP == MTSG_SAMPLER_HAMMERSLEY || SMP == MTSG_SAMPLER_SOBOL) && smp.dimError)
-                atomicOr(&P.cnt[CNT_ERR], 1u);   // the render fails as Mitsuba's Log(EError) would
-            const float4 finalL = make_float4(L.x, L.y, L.z, L4.w);
-            if (cont) {
-                stage.T[threadIdx.x] = make_float4(T.x, T.y, T.z, eta);
-                stage.L[threadIdx.x] = finalL;
-                stage.meta[threadIdx.x] = make_uint4(depth | flags, smp.dim, slot, smp.n2);
-            } else {
-                stS(&P.L[slot], finalL);   // path ended: its sample's final radiance
-            }
-        }
-        // The output positions come from the workgroup-aggregated append; the
-        // outgoing records wait for it in LDS (lane-private rows) rather than
-        // in registers live across its barriers.
-        const int tid = threadIdx.x;
-        uint32_t is, ic;
-        block_append2(ba, &P.cnt[cnt_s(bounce & 1)], &P.cnt[cnt_q(qout)], shadow, cont, is, ic);
-        if (cont) {
-            // survivor: compacted into the next bounce's arrays
-            stS(&P.n_ray_o[ic], stage.o[tid]);
-            stS(&P.n_ray_d[ic], stage.d[tid]);
-            stS(&P.n_T[ic], stage.T[tid]);
-            stS(&P.n_aux[ic], stage.aux[tid]);
-            stS(&P.n_Lp[ic], stage.L[tid]);
-            stS(&P.n_meta[ic], stage.meta[tid]);
-        }
-        if (shadow) {
-            float4 c = stage.shc[tid];
-            c.w = __uint_as_float(cont ? ic : (0x80000000u | slot));
-            stS(&P.sh_o[is], stage.sho[tid]);
-            stS(&P.sh_d[is], stage.shd[tid]);
-            stS(&P.sh_c[is], c);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// film splat: one workgroup per 16x16 tile, LDS accumulation of the
-// discretized reconstruction filter (imageblock.h:124-204), then one float
-// atomic per texel into the tile+border block in HBM.
-// ---------------------------------------------------------------------------
-constexpr int MAX_BORDER = 4;
-constexpr int LT = TILE + 2 * MAX_BORDER;   // LDS tile edge
-constexpr int SPLAT_CHUNK = 16;             // samples per pixel per workgroup
-
-// One workgroup = one 16x16 tile x one chunk of SPLAT_CHUNK samples per pixel.
-// Each thread owns one pixel: all its samples fall in [x, x+1) x [y, y+1), so
-// their filter footprints lie in the K x K window centred on the pixel
-// (K = 2 * border + 1).  The thread accumulates that window in registers
-// (weights of texels outside a sample's [ceil, floor] range are exactly 0,
-// as evalDiscretized returns m_values[31] = 0 there), then the workgroup
-// reduces the windows into an LDS tile in K*K conflict-free phases (each
-// phase shifts every window by the same offset, so no two threads touch the
-// same texel: no atomics, fixed order) and flushes the tile with one float
-// atomic per texel and channel into the HBM ImageBlock.
-template <int K, int CH>
-__global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P, float *film, int blockW, int blockH) {
-    __shared__ float acc[CH][LT * LT];
-    constexpr int R = K / 2;
-    for (int k = threadIdx.x; k < CH * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
-    const int tl = blockIdx.x;
-    const int tile = B.toffset + (B.tile0 + tl) * B.tstride;
-    const int tx = tile % B.tiles_x, ty = tile / B.tiles_x;
-    const int x0 = B.rect_x + tx * TILE, y0 = B.rect_y + ty * TILE;   // tile origin (film coords)
-    const int bord = C.border;
-    const int pix = threadIdx.x;
-    const int lx = pix % TILE, ly = pix / TILE;
-    const int x = x0 + lx, y = y0 + ly;
-    const bool inside = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
-    // block (tile rect + border) bounds relative to the window origin (x - R, y - R)
-    const int bx0 = (B.rect_x - bord) - (x - R), by0 = (B.rect_y - bord) - (y - R);
-    // Mitsuba computes a sample's filter offsets relative to the origin of the
-    // 32x32 render block that holds its pixel (ImageBlock::put,
-    // imageblock.h:158-160; blocks of BlockedImageProcess, imageproc.cpp:28-78,
-    // scene.cpp:27), and `pos - 0.5 - origin` can round when it crosses a power
-    // of two: the same origin is used here so the weights are bit-identical
-    const int mbx = B.rect_x + ((x - B.rect_x) & ~31) - bord, mby = B.rect_y + ((y - B.rect_y) & ~31) - bord;
-    const int wxo = (x - R) - mbx, wyo = (y - R) - mby;   // window origin in that block
-    float win[K][K][CH];
-#pragma unroll
-    for (int r = 0; r < K; ++r)
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-#pragma unroll
-            for (int h = 0; h < CH; ++h) win[r][c][h] = 0.0f;
-    const uint32_t sBeg = blockIdx.y * SPLAT_CHUNK, sEnd = min(B.ns, sBeg + SPLAT_CHUNK);
-    if (inside) {
-        for (uint32_t sl = sBeg; sl < sEnd; ++sl) {
-            const uint32_t slot = ((uint32_t)tl * B.ns + sl) * (TILE * TILE) + pix;
-            const float4 L = ldS(&P.L[slot]);
-            float ja, jb;
-            camera_jitter(I, x, y, B.s0 + sl, ja, jb);
-            // invalid samples are rejected (imageblock.h:147-151)
-            if (!(isfinite(L.x) && isfinite(L.y) && isfinite(L.z) && L.x >= 0 && L.y >= 0 && L.z >= 0)) continue;
-            // sample position relative to the Mitsuba block origin
-            // (imageblock.h:158-160)
-            const float px = ((float)x + ja) - 0.5f - (float)mbx;
-            const float py = ((float)y + jb) - 0.5f - (float)mby;
-            float wx[K], wy[K];
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                const bool okx = c >= bx0 && c < bx0 + blockW;
-                const bool oky = c >= by0 && c < by0 + blockH;
-                wx[c] = okx ? C.filter_values[min((int)fabsf(((float)(wxo + c) - px) * C.filter_scale), 31)] : 0.0f;
-                wy[c] = oky ? C.filter_values[min((int)fabsf(((float)(wyo + c) - py) * C.filter_scale), 31)] : 0.0f;
-            }
-            const float v[5] = {L.x, L.y, L.z, L.w, 1.0f};
-#pragma unroll
-            for (int r = 0; r < K; ++r)
-#pragma unroll
-                for (int c = 0; c < K; ++c) {
-                    const float w = wx[c] * wy[r];
-#pragma unroll
-                    for (int h = 0; h < CH; ++h) win[r][c][h] += w * v[CH == 5 ? h : (h == 3 ? 4 : h)];
-                }
-        }
-    }
-    __syncthreads();
-    // K*K shifted phases: texel (ly + r + MAX_BORDER - R, lx + c + MAX_BORDER - R)
-#pragma unroll
-    for (int r = 0; r < K; ++r)
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const int o = (ly + r + MAX_BORDER - R) * LT + (lx + c + MAX_BORDER - R);
-#pragma unroll
-            for (int h = 0; h < CH; ++h) acc[h][o] += win[r][c][h];
-            __syncthreads();
-        }
-    // flush into the HBM block (blockW x blockH x 5, origin = rect - border)
-    for (int k = threadIdx.x; k < LT * LT; k += BLOCK) {
-        const int ty2 = k / LT, tx2 = k % LT;
-        const int fx = x0 - MAX_BORDER + tx2 - (B.rect_x - bord), fy = y0 - MAX_BORDER + ty2 - (B.rect_y - bord);
-        if (fx < 0 || fy < 0 || fx >= blockW || fy >= blockH) continue;
-        const float w = acc[CH - 1][k];
-        if (w == 0.0f) continue;
-        float *dst = film + ((size_t)fy * blockW + fx) * 5;
-        unsafeAtomicAdd(dst + 0, acc[0][k]);
-        unsafeAtomicAdd(dst + 1, acc[1][k]);
-        unsafeAtomicAdd(dst + 2, acc[2][k]);
-        unsafeAtomicAdd(dst + 3, CH == 5 ? acc[3][k] : w);   // no alpha channel: alpha == 1 per sample
-        unsafeAtomicAdd(dst + 4, w);
-    }
-}
-
-// zero the counters bounce b appends to (next-bounce paths qout, shadow rays
-// S(sOut); sOut < 0: none) and the work-fetch counters of its trace launch
-__global__ void k_reset(uint32_t *cnt, int qout, int sOut) {
-    if (threadIdx.x == 0) {
-        if (qout >= 0) cnt[qout ? CNT_Q1 : CNT_Q0] = 0;
-        if (sOut >= 0) cnt[sOut ? CNT_S1 : CNT_S0] = 0;
-    }
-    if (threadIdx.x < XGROUPS) cnt[CNT_FETCH + 32 * threadIdx.x] = 0;
-}
 
 // ---------------------------------------------------------------------------
 // host side
@@ -2166,7 +81,11 @@ struct mtsg_scene {
     std::vector<void *> batchAllocs;
     uint32_t *hostCnt = nullptr;   // pinned copy of the queue counters (2 per lane)
     int cuCount = 0;
-    int traceGrid = 0, shadeGrid = 0, traceGridInst = 0;
+    int traceGrid = 0, shadeGrid = 0, traceGridInst = 0, finishGrid = 0;
+    // tail mode: once a bounce starts with fewer than finishPaths paths, k_finish
+    // carries them through their remaining bounces in one launch (0: off)
+    uint32_t finishPaths = 0;
+    uint32_t finishShadeMin = 1;
     uint32_t flags = 0;
     int samplerType = MTSG_SAMPLER_INDEPENDENT, samplerDim = 4;
     int qmcInv[2][3] = {{0, 0, 0}, {0, 0, 0}};
@@ -2229,7 +148,7 @@ int ensure_batch(mtsg_scene *s, uint32_t paths, int lanes) {
     return MTSG_OK;
 }
 
-enum { K_CAMERA = 0, K_CLOSEST, K_SHADOW, K_SHADE, K_SPLAT };
+enum { K_CAMERA = 0, K_CLOSEST, K_SHADOW, K_SHADE, K_SPLAT, K_FINISH };
 
 // the survivors k_shade compacted into n_* are the next bounce's paths
 void swap_bounce(DevPaths &P) {
@@ -2279,33 +198,44 @@ void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn
     else launch_trace_c<false>(s, P, cIn, sIn, n, st);
 }
 
-template <bool ENV, bool EXT>
-void launch_shade_env(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {
-    dim3 g(s->shadeGrid), blk(SHADE_BLOCK);
-    switch (I.smp.type) {
-        case MTSG_SAMPLER_HALTON:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HALTON, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
-            break;
-        case MTSG_SAMPLER_HAMMERSLEY:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_HAMMERSLEY, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
-            break;
-        case MTSG_SAMPLER_LDSAMPLER:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_LDSAMPLER, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
-            break;
-        case MTSG_SAMPLER_SOBOL:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_SOBOL, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
-            break;
-        default:
-            hipLaunchKernelGGL((k_shade<ENV, MTSG_SAMPLER_INDEPENDENT, EXT>), g, blk, 0, st, s->ds, I, B, P, b, qin, B.nslots, s->cam.has_alpha);
-    }
+// k_shade / k_finish are instantiated per sampler in smp_kernels.hip
+ShadeLaunch shade_args(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st,
+                       dim3 grid, dim3 block) {
+    ShadeLaunch a;
+    a.grid = grid;
+    a.block = block;
+    a.stream = st;
+    a.S = &s->ds;
+    a.I = &I;
+    a.B = &B;
+    a.P = &P;
+    a.bounce = b;
+    a.qin = qin;
+    a.nIdentity = B.nslots;
+    a.hasAlpha = s->cam.has_alpha;
+    a.shadeMin = s->finishShadeMin;
+    a.env = s->ds.has_env != 0;
+    a.ext = s->extBsdfs;
+    return a;
 }
 void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {
-    if (s->extBsdfs) {
-        if (s->ds.has_env) launch_shade_env<true, true>(s, I, B, P, b, qin, st);
-        else launch_shade_env<false, true>(s, I, B, P, b, qin, st);
-    } else {
-        if (s->ds.has_env) launch_shade_env<true, false>(s, I, B, P, b, qin, st);
-        else launch_shade_env<false, false>(s, I, B, P, b, qin, st);
+    const ShadeLaunch a = shade_args(s, I, B, P, b, qin, st, dim3(s->shadeGrid), dim3(SHADE_BLOCK));
+    switch (I.smp.type) {
+        case MTSG_SAMPLER_HALTON: launch_shade_smp<MTSG_SAMPLER_HALTON>(a); break;
+        case MTSG_SAMPLER_HAMMERSLEY: launch_shade_smp<MTSG_SAMPLER_HAMMERSLEY>(a); break;
+        case MTSG_SAMPLER_LDSAMPLER: launch_shade_smp<MTSG_SAMPLER_LDSAMPLER>(a); break;
+        case MTSG_SAMPLER_SOBOL: launch_shade_smp<MTSG_SAMPLER_SOBOL>(a); break;
+        default: launch_shade_smp<MTSG_SAMPLER_INDEPENDENT>(a);
+    }
+}
+void launch_finish(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int qin, hipStream_t st) {
+    const ShadeLaunch a = shade_args(s, I, B, P, 1, qin, st, dim3(s->finishGrid), dim3(TRACE_BLOCK));
+    switch (I.smp.type) {
+        case MTSG_SAMPLER_HALTON: launch_finish_smp<MTSG_SAMPLER_HALTON>(a); break;
+        case MTSG_SAMPLER_HAMMERSLEY: launch_finish_smp<MTSG_SAMPLER_HAMMERSLEY>(a); break;
+        case MTSG_SAMPLER_LDSAMPLER: launch_finish_smp<MTSG_SAMPLER_LDSAMPLER>(a); break;
+        case MTSG_SAMPLER_SOBOL: launch_finish_smp<MTSG_SAMPLER_SOBOL>(a); break;
+        default: launch_finish_smp<MTSG_SAMPLER_INDEPENDENT>(a);
     }
 }
 
@@ -2464,6 +394,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
         int last = -1;
         int start = 0;
         bool open = false;
+        bool finished = false;   // the tail kernel took over the batch's remaining bounces
         hipEvent_t cntEv[2] = {nullptr, nullptr};
     } lr[MTSG_MAX_LANES];
     int result = MTSG_OK;
@@ -2482,6 +413,8 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             if (hipStreamWaitEvent(s->lstream[l], startEv, 0) != hipSuccess) { g_err = "stream wait"; result = MTSG_ERR_DEVICE; }
     }
     const int maxBounces = p->max_depth > 0 ? p->max_depth : 1 << 30;
+    // tail mode (k_finish): one lane, not in the instrumented or two-level modes
+    const bool useFinish = s->finishPaths > 0 && nl == 1 && !count && !s->ds.inst;
     // bounce b of a lane: one trace launch over this bounce's closest rays
     // (work list qin(b), identity for b = 0) and bounce b-1's shadow rays
     // (S((b-1) & 1)), then k_shade appends the next bounce's paths to
@@ -2506,6 +439,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             L.B = batches[k0 + l];
             L.last = -1;
             L.open = true;
+            L.finished = false;
             // staggered lanes: lane l starts `stagger` bounces after lane
             // l-1, so its early, full launches overlap the other lanes'
             // late, tail-bound ones
@@ -2532,6 +466,25 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 const int qout = (b & 1) ^ 1;
                 hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, P.cnt, qout, b & 1);
                 timed_launch(s, K_CLOSEST, st, [&]() { launch_trace(s, count, P, qin, b == 0 ? -1 : ((b - 1) & 1), L.B.nslots, st); });
+                if (useFinish && b >= 1) {
+                    // the count of this bounce's paths is known once bounce b-1 is
+                    // done (the GPU meanwhile runs this bounce's trace): few left ->
+                    // k_finish carries them to their ends in one launch
+                    HIP_TRY(hipEventSynchronize(L.cntEv[(b - 1) & 1]));
+                    const uint32_t nb = account(l, b - 1);
+                    if (nb < s->finishPaths) {
+                        hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, P.cnt, -1, -1);
+                        timed_launch(s, K_FINISH, st, [&]() { launch_finish(s, I, L.B, P, qin, st); });
+                        s->stats.launches_finish++;
+                        s->stats.paths_finish += nb;
+                        HIP_TRY(hipMemcpyAsync(hostCnt(l, b), P.cnt, (CNT_S1 + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                        HIP_TRY(hipEventRecord(L.cntEv[b & 1], st));
+                        L.last = b;
+                        L.open = false;
+                        L.finished = true;
+                        continue;
+                    }
+                }
                 timed_launch(s, K_SHADE, st, [&]() { launch_shade(s, I, L.B, P, b, qin, st); });
                 swap_bounce(P);
                 HIP_TRY(hipMemcpyAsync(hostCnt(l, b), P.cnt, (CNT_S1 + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -2545,7 +498,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 // lagged check: if bounce b-1 produced nothing, bounce b was empty
                 // (also for a lane that launched its last bounce b just now, so
                 // every bounce is booked once: b-1 here, the last one below)
-                if (b >= 1 && L.last == b) {
+                if (b >= 1 && L.last == b && !useFinish) {
                     HIP_TRY(hipEventSynchronize(L.cntEv[(b - 1) & 1]));
                     if (account(l, b - 1) == 0) L.open = false;
                 }
@@ -2558,7 +511,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             DevPaths &P = s->LP[l];
             hipStream_t st = s->lstream[l];
             const DevBatch &B = L.B;
-            if (L.last >= 0) {
+            if (L.last >= 0 && !L.finished) {
                 // the last bounce's shadow rays
                 hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, P.cnt, -1, -1);
                 timed_launch(s, K_SHADOW, st, [&]() { launch_trace(s, count, P, -2, L.last & 1, 0u, st); });
@@ -2634,6 +587,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
                 case K_SHADOW: s->stats.ms_trace_shadow += ms; break;
                 case K_SHADE: s->stats.ms_shade += ms; break;
                 case K_SPLAT: s->stats.ms_splat += ms; break;
+                case K_FINISH: s->stats.ms_finish += ms; break;
             }
         }
     }
@@ -2973,6 +927,12 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         perCU = 4;
     s->traceGridInst = s->cuCount * perCU;
     s->shadeGrid = s->cuCount * 8 * 256 / SHADE_BLOCK;
+    perCU = 0;
+    if ((perCU = finish_blocks_per_cu()) <= 0) perCU = 4;
+    s->finishGrid = s->cuCount * perCU;
+    s->finishPaths = MTSG_DEFAULT_FINISH_PATHS;
+    if (const char *f = getenv("MTSG_FINISH")) s->finishPaths = (uint32_t)strtoul(f, nullptr, 0);
+    if (const char *f = getenv("MTSG_FINISH_SHADE_MIN")) s->finishShadeMin = std::max(1, atoi(f));
     if (const char *l = getenv("MTSG_LANES")) s->lanes = std::max(1, std::min(MTSG_MAX_LANES, atoi(l)));
     if (const char *g = getenv("MTSG_STAGGER")) s->stagger = std::max(0, std::min(16, atoi(g)));
     s->lstream[0] = s->stream;
@@ -2986,6 +946,12 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
 int mtsg_set_batch_paths(mtsg_scene *s, uint32_t paths) {
     if (!s || paths < TILE * TILE) { g_err = "batch must hold at least 256 paths"; return MTSG_ERR_INVALID; }
     s->requestedBatch = paths;
+    return MTSG_OK;
+}
+
+int mtsg_set_finish_paths(mtsg_scene *s, uint32_t paths) {
+    if (!s) return MTSG_ERR_INVALID;
+    s->finishPaths = paths;
     return MTSG_OK;
 }
 

@@ -1,0 +1,48 @@
+// smp_kernels.hip -- the shading kernels (k_shade, k_finish) of one sampler.
+// Compiled once per sampler with -DMTSG_TU_SAMPLER=<MTSG_SAMPLER_* value>, so the
+// four ENV x EXT variants of both kernels of each sampler build in their own
+// translation unit, in parallel (see kernels.h and the Makefile).
+#include "kernels.h"
+
+#ifndef MTSG_TU_SAMPLER
+#error "MTSG_TU_SAMPLER must name the sampler this unit instantiates"
+#endif
+
+namespace mtsg {
+
+template <>
+void launch_shade_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
+    constexpr int SMP = MTSG_TU_SAMPLER;
+    if (a.ext) {
+        if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+        else hipLaunchKernelGGL((k_shade<false, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+    } else {
+        if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+        else hipLaunchKernelGGL((k_shade<false, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+    }
+}
+
+template <>
+void launch_finish_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
+    constexpr int SMP = MTSG_TU_SAMPLER;
+    if (a.ext) {
+        if (a.env) hipLaunchKernelGGL((k_finish<true, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
+        else hipLaunchKernelGGL((k_finish<false, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
+    } else {
+        if (a.env) hipLaunchKernelGGL((k_finish<true, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
+        else hipLaunchKernelGGL((k_finish<false, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
+    }
+}
+
+#ifdef MTSG_TU_OCCUPANCY
+// persistent grid of k_finish (the register-heaviest variant bounds them all)
+int finish_blocks_per_cu() {
+    int perCU = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_finish<true, MTSG_SAMPLER_INDEPENDENT, true>, TRACE_BLOCK, 0) !=
+        hipSuccess)
+        return 0;
+    return perCU;
+}
+#endif
+
+}  // namespace mtsg

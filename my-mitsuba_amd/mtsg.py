@@ -67,6 +67,7 @@ class Stats(C.Structure):
         ("iter_max_closest", C.c_uint64), ("iter_max_shadow", C.c_uint64),
         ("iter_hist_closest", C.c_uint64 * 16), ("iter_hist_shadow", C.c_uint64 * 16),
         ("instance_visits", C.c_uint64), ("shadow_instance_visits", C.c_uint64),
+        ("ms_finish", C.c_double), ("paths_finish", C.c_uint64), ("launches_finish", C.c_uint64),
     ]
 
 
@@ -89,7 +90,7 @@ _dev = None
 DEVICE_SYMBOLS = [
     "mtsg_device_count", "mtsg_scene_create", "mtsg_render", "mtsg_render_device",
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
-    "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths",
+    "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
     "mtsg_last_error", "mtsg_env_eval", "mtsg_sampler_draws", "mtsg_debug_wavetimes", "mtsg_debug_stragglers",
 ]
@@ -175,6 +176,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_set_flags.argtypes = [C.c_void_p, C.c_uint32]
         lib.mtsg_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
         lib.mtsg_set_batch_paths.argtypes = [C.c_void_p, C.c_uint32]
+        lib.mtsg_set_finish_paths.argtypes = [C.c_void_p, C.c_uint32]
         lib.mtsg_trace_closest.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_trace_shadow.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
@@ -300,6 +302,10 @@ class GPUScene:
 
     def set_batch_paths(self, n: int) -> None:
         self._check(device_lib().mtsg_set_batch_paths(self._h, n), "mtsg_set_batch_paths")
+
+    def set_finish_paths(self, n: int) -> None:
+        """Tail-mode threshold (paths; 0: off), see mtsg_set_finish_paths."""
+        self._check(device_lib().mtsg_set_finish_paths(self._h, n), "mtsg_set_finish_paths")
 
     def stats(self) -> Stats:
         s = Stats()

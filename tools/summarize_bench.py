@@ -17,4 +17,5 @@ for path in sys.argv[1:]:
     tr = k.get("trace_ms", k.get("trace_closest_ms", 0) + k.get("trace_shadow_ms", 0))
     print(f"{j['value']:.1f} Ms/s  trace {tr:.1f} "
           f"shade {k.get('shade_ms', 0):.1f} splat {k.get('splat_ms', 0):.1f} cam {k.get('camera_ms', 0):.1f} "
+          f"fin {k.get('finish_ms', 0):.2f}/{k.get('finish_paths', 0)} "
           f"frame {k.get('frame_ms', 0):.1f}  GB/s {r.get('achieved', 0)}")
