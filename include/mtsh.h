@@ -75,6 +75,13 @@ int mtsh_rough_transmittance(int distribution, float alpha, float eta, int n, fl
  * Returns 0, or -1 (see mtsh_last_error; -2: rgb_capacity too small). */
 int mtsh_read_image(const char *path, int *w, int *h, float *rgb, size_t rgb_capacity);
 
+/* Triangle::getClippedAABB (src/libcore/triangle.cpp) as the kd build's
+ * perfect splits use it: the bounds of triangle v[0..8] clipped to the box
+ * box[0..5] = (min xyz, max xyz) go to out[0..5].  Returns 1 if the clipped
+ * box is valid, 0 if the triangle lies outside (the reference's KAT:
+ * src/tests/test_kd.cpp:34-84). */
+int mtsh_clip_triangle(const float *v, const float *box, float *out);
+
 void mtsh_last_error(char *buf, size_t size);
 
 #ifdef __cplusplus

@@ -16,9 +16,8 @@
 
 namespace mtsh {
 
-namespace {
-
-// Triangle::getClippedAABB (Sutherland-Hodgman against the 6 box planes)
+// Triangle::getClippedAABB (src/libcore/triangle.cpp; Sutherland-Hodgman
+// against the 6 box planes), used by the kd build's perfect splits
 AABB clipTriangle(const V3 &a, const V3 &b, const V3 &c, const AABB &box) {
     double poly[16][3], tmp[16][3];
     int n = 3;
@@ -52,6 +51,8 @@ AABB clipTriangle(const V3 &a, const V3 &b, const V3 &c, const AABB &box) {
     r.clip(box);
     return r;
 }
+
+namespace {
 
 struct ScenePrims : PrimSource {
     const Scene &s;

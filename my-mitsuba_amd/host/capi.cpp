@@ -17,6 +17,15 @@ thread_local std::string g_err;
 extern "C" {
 
 void mtsh_set_kd_threads(int threads) { mtsh::g_defaultKDThreads = threads; }
+
+int mtsh_clip_triangle(const float *v, const float *box, float *out) {
+    mtsh::AABB b;
+    b.mn = mtsh::V3(box[0], box[1], box[2]);
+    b.mx = mtsh::V3(box[3], box[4], box[5]);
+    const mtsh::AABB r = mtsh::clipTriangle(mtsh::V3(v[0], v[1], v[2]), mtsh::V3(v[3], v[4], v[5]), mtsh::V3(v[6], v[7], v[8]), b);
+    for (int k = 0; k < 3; ++k) { out[k] = r.mn[k]; out[3 + k] = r.mx[k]; }
+    return r.valid() ? 1 : 0;
+}
 void mtsh_set_instancing(int mode) { mtsh::g_instancing = mode == MTSH_INSTANCING_TWO_LEVEL ? 1 : 0; }
 
 mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_defines) {

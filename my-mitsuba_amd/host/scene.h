@@ -215,6 +215,7 @@ struct PrimSource {
     virtual AABB clippedBounds(size_t i, const AABB &box) const = 0;
 };
 void buildKDTree(const PrimSource &src, const KDBuildParams &params, KDTree &out);
+AABB clipTriangle(const V3 &a, const V3 &b, const V3 &c, const AABB &box);   // build.cpp
 
 // Conductor IOR lookup (generated from data/ior/*.spd), dielectric lookupIOR
 bool lookupConductor(const std::string &name, V3 &eta, V3 &k);

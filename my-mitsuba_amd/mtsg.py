@@ -97,7 +97,7 @@ DEVICE_SYMBOLS = [
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
-    "mtsh_read_image", "mtsh_last_error",
+    "mtsh_read_image", "mtsh_clip_triangle", "mtsh_last_error",
 ]
 PATH_SYMBOLS = [
     "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
@@ -148,6 +148,7 @@ def host_lib() -> C.CDLL:
         lib.mtsh_set_kd_threads.argtypes = [C.c_int]
         lib.mtsh_set_instancing.argtypes = [C.c_int]
         lib.mtsh_read_image.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p, C.c_size_t]
+        lib.mtsh_clip_triangle.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         _host = lib
     return _host
 
