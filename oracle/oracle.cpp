@@ -2575,4 +2575,29 @@ int oracle_env_eval_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, co
     return 0;
 }
 
+/* MicrofacetDistribution sampling and densities for the reference's own
+ * microfacet chi-square test (src/tests/test_microfacet.cpp:53-94,
+ * MicrofacetAdapter): wi == NULL: sampleAll with its pdf, and pdfAll(m) =
+ * D(m) cos(theta_m); else sampleVisible(wi) and pdfVisible(wi, m). */
+int oracle_mf_sample_n(int type, float au, float av, const float *wi, uint32_t n, const float *u2, float *m, float *pdf) {
+    const Microfacet mf(type, au, av, wi != nullptr);
+    for (uint32_t i = 0; i < n; ++i) {
+        float p = 0;
+        const Vec v = wi ? mf.sampleVisibleN(Vec(wi[0], wi[1], wi[2]), u2[2 * i], u2[2 * i + 1])
+                         : mf.sampleAll(u2[2 * i], u2[2 * i + 1], p);
+        m[3 * i] = v.x; m[3 * i + 1] = v.y; m[3 * i + 2] = v.z;
+        pdf[i] = wi ? mf.pdfVisible(Vec(wi[0], wi[1], wi[2]), v) : p;
+    }
+    return 0;
+}
+
+int oracle_mf_pdf_n(int type, float au, float av, const float *wi, uint32_t n, const float *m, float *pdf) {
+    const Microfacet mf(type, au, av, wi != nullptr);
+    for (uint32_t i = 0; i < n; ++i) {
+        const Vec v(m[3 * i], m[3 * i + 1], m[3 * i + 2]);
+        pdf[i] = wi ? mf.pdfVisible(Vec(wi[0], wi[1], wi[2]), v) : mf.eval(v) * cosTheta(v);
+    }
+    return 0;
+}
+
 }  // extern "C"

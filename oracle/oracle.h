@@ -91,6 +91,10 @@ int oracle_bsdf_sample3_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, con
 int oracle_bsdf_sample_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *u2, float *wo, float *pdf,
                          float *weight, int32_t *type);
 int oracle_bsdf_eval_n(const mtsg_bsdf *b, const float wi[3], uint32_t n, const float *wo, float *value, float *pdf);
+/* MicrofacetDistribution (MTSG_MF_*) sampleAll / sampleVisible and pdfAll /
+ * pdfVisible (wi == NULL: the "all normals" variant) */
+int oracle_mf_sample_n(int type, float au, float av, const float *wi, uint32_t n, const float *u2, float *m, float *pdf);
+int oracle_mf_pdf_n(int type, float au, float av, const float *wi, uint32_t n, const float *m, float *pdf);
 
 /* environment emitter (EmitterAdapter of test_chisquare.cpp:342-388) */
 int oracle_env_sample_direct_n(const mtsg_scene_desc *d, uint32_t n, const float *u2, const float ref[3], float *dir,
