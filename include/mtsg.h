@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MTSG_ABI_VERSION 6
+#define MTSG_ABI_VERSION 7
 
 /* ---- error codes (mtsg_last_error() gives the message) ------------------ */
 enum {
@@ -160,33 +160,71 @@ typedef struct mtsg_bsdf {
      * evalCubicInterp1D (spline.cpp:23-60); fdr_int holds
      * 1 - internal.evalDiffuse(alpha) (roughplastic.cpp:349-351) */
     float rtrans[MTSG_RTRANS_SAMPLES];
+    /* 1 + index into textures when `reflectance` is a bitmap texture
+     * (evaluated per hit instead of the constant above), 0 otherwise */
+    int32_t texture;
+    int32_t pad_tex[3];
 } mtsg_bsdf;
 
 enum { MTSG_EMITTER_AREA = 1, MTSG_EMITTER_ENVMAP = 2 };
 
 #define MTSG_ENVMAP_MAX_LEVELS 24
+#define MTSG_MIPMAP_MAX_LEVELS 24
 #define MTSG_MIPMAP_LUT_SIZE 64      /* MTS_MIPMAP_LUT_SIZE (mipmap.h:37) */
 
-/* Environment emitter (src/emitters/envmap.cpp:99-660): lat-long RGB MIP
- * pyramid (texel values already rounded to half precision, as Mitsuba's
- * TMIPMap<Spectrum, SpectrumHalf> stores them), row/column CDFs for
- * importance sampling, and the scene bounding sphere the shadow rays end on.
- * Boundary conditions: u repeats, v clamps (envmap.cpp:160-161). */
-typedef struct mtsg_envmap {
+/* Boundary conditions (ReconstructionFilter::EBoundaryCondition,
+ * include/mitsuba/core/rfilter.h:52-64) and MIP filter types
+ * (EMIPFilterType, include/mitsuba/render/mipmap.h:43-55). */
+enum { MTSG_WRAP_CLAMP = 0, MTSG_WRAP_REPEAT = 1, MTSG_WRAP_MIRROR = 2, MTSG_WRAP_ZERO = 3, MTSG_WRAP_ONE = 4 };
+enum { MTSG_MIP_NEAREST = 0, MTSG_MIP_BILINEAR = 1, MTSG_MIP_TRILINEAR = 2, MTSG_MIP_EWA = 3 };
+
+/* One RGB MIP pyramid, TMIPMap<Color3, Color3h> (mipmap.h:61-860): the
+ * texels of level l are 3 floats per texel, row-major, at level_offset[l]
+ * of the owner's texel buffer, already rounded to half precision as the
+ * reference stores them.  Nearest / bilinear pyramids have one level. */
+typedef struct mtsg_mipmap {
     int32_t levels;
-    int32_t level_w[MTSG_ENVMAP_MAX_LEVELS], level_h[MTSG_ENVMAP_MAX_LEVELS];
-    uint32_t level_offset[MTSG_ENVMAP_MAX_LEVELS];   /* float offset of each level in texels (RGB) */
-    float size_ratio_x[MTSG_ENVMAP_MAX_LEVELS], size_ratio_y[MTSG_ENVMAP_MAX_LEVELS];
+    int32_t filter;               /* MTSG_MIP_*                               */
+    int32_t wrap_u, wrap_v;       /* MTSG_WRAP_*                              */
+    int32_t level_w[MTSG_MIPMAP_MAX_LEVELS], level_h[MTSG_MIPMAP_MAX_LEVELS];
+    uint32_t level_offset[MTSG_MIPMAP_MAX_LEVELS];   /* float offset of each level */
+    float size_ratio_x[MTSG_MIPMAP_MAX_LEVELS], size_ratio_y[MTSG_MIPMAP_MAX_LEVELS];
+    float max_anisotropy;         /* EWA only (1 otherwise, bitmap.cpp:234-235) */
+    int32_t pad[3];
+    float weight_lut[MTSG_MIPMAP_LUT_SIZE];   /* EWA Gaussian (mipmap.h:296-301) */
+} mtsg_mipmap;
+
+/* Environment emitter (src/emitters/envmap.cpp:99-660): lat-long RGB MIP
+ * pyramid (EWA; u repeats, v clamps, envmap.cpp:160-161), row/column CDFs
+ * for importance sampling, and the scene bounding sphere the shadow rays
+ * end on. */
+typedef struct mtsg_envmap {
+    mtsg_mipmap mip;
     float scale;                  /* 'scale' property                        */
     float to_world[9], to_local[9];  /* rotation part of toWorld and its inverse (row-major) */
     float bsphere_center[3], bsphere_radius;   /* scene bsphere x 1.5 (envmap.cpp:321-325) */
     float normalization;          /* envmap.cpp:300-301                      */
     float pixel_size[2];          /* (2 pi / w, pi / h)                      */
-    float max_anisotropy;         /* 10 (envmap.cpp:144)                     */
-    float weight_lut[MTSG_MIPMAP_LUT_SIZE];   /* EWA Gaussian (mipmap.h:296-301) */
     int32_t emitter;              /* index into emitters                     */
     int32_t pad[3];
 } mtsg_envmap;
+
+/* `bitmap` texture (src/textures/bitmap.cpp:167-591) bound to a BSDF's
+ * reflectance parameter (diffuse `reflectance`, (rough)plastic
+ * `diffuseReflectance`).  Texture2D::eval (src/librender/texture.cpp:112-121)
+ * maps uv -> uv * uv_scale + uv_offset; with UV partials (the first hit of a
+ * camera ray, records.inl:69-75) the lookup is TMIPMap::eval (filtered),
+ * otherwise evalBilinear(0) (evalBox(0) for `nearest`).  `scale` is the
+ * ScaleTexture that BSDF::ensureEnergyConservation wraps around a texture
+ * whose maximum exceeds 1 (src/librender/bsdf.cpp:88-113), else 1. */
+typedef struct mtsg_texture {
+    mtsg_mipmap mip;
+    float uv_offset[2], uv_scale[2];
+    float scale;
+    float average[3];             /* getAverage() (level 0, before the scale) */
+    float maximum[3];             /* getMaximum()                            */
+    int32_t pad[3];
+} mtsg_texture;
 
 typedef struct mtsg_emitter {
     int32_t type;
@@ -315,6 +353,17 @@ typedef struct mtsg_scene_desc {
     const mtsg_kdnode *group_nodes;
     uint32_t n_group_indices;
     const uint32_t *group_indices;
+    /* bitmap textures (n_textures = 0: none) and the per-triangle data their
+     * lookups need (NULL without textures): tri_uv = the three vertices'
+     * texture coordinates, (0,0) (1,0) (0,1) for meshes without UVs so that
+     * the interpolation gives Point2(b.y, b.z) bit for bit (skdtree.h:398-405);
+     * tri_dpdv = the UV tangent dpdv (trimesh.cpp:701-735) or p2 - p0 */
+    uint32_t n_textures;
+    const mtsg_texture *textures;
+    uint32_t n_tex_texels;        /* floats: 3 per texel over all textures' levels */
+    const float *tex_texels;
+    const float *tri_uv;          /* 6 * n_triangles                          */
+    const float *tri_dpdv;        /* 3 * n_triangles                          */
 } mtsg_scene_desc;
 
 /* ---- render ------------------------------------------------------------- */
@@ -464,6 +513,12 @@ int  mtsg_set_finish_paths(mtsg_scene *scene, uint32_t paths);
  * EWA lookup with those differential directions (camera rays).
  * EnvironmentMap::evalEnvironment, src/emitters/envmap.cpp:380-410. */
 int  mtsg_env_eval(mtsg_scene *scene, uint32_t n, const float *dirs, const float *rx, const float *ry, float *out);
+
+/* Debug / parity entry: BitmapTexture::eval (src/textures/bitmap.cpp:431-499)
+ * of texture `tex` at n uv points (2 floats each): the filtered TMIPMap::eval
+ * with the uv partials duv = (d0.x, d0.y, d1.x, d1.y) per point, or the
+ * unfiltered evalBilinear(0) / evalBox(0) when duv is NULL.  RGB out. */
+int  mtsg_tex_eval(mtsg_scene *scene, int tex, uint32_t n, const float *uv, const float *duv, float *out);
 
 /* Debug: the scene sampler's draws for sample s of film pixel (x, y): kinds[i]
  * = 1 (next1D, one float out) or 2 (next2D, two floats), in call order, as

@@ -56,6 +56,10 @@ void mtsh_scene_get_info(const mtsh_scene *scene, mtsh_scene_info *out);
 
 void mtsh_scene_free(mtsh_scene *scene);
 
+/* The scene's bitmap textures (headers as in its mtsg_scene_desc): copies
+ * up to `capacity` of them to out (may be NULL) and returns their count. */
+int mtsh_scene_textures(const mtsh_scene *scene, mtsg_texture *out, int capacity);
+
 /* hdrfilm develop (fmtconv.cpp:962-974): rgb = (sum w*L) / (sum w). */
 void mtsh_develop(const float *rgbaw, int w, int h, float *rgb_out);
 
@@ -81,6 +85,20 @@ int mtsh_read_image(const char *path, int *w, int *h, float *rgb, size_t rgb_cap
  * box is valid, 0 if the triangle lies outside (the reference's KAT:
  * src/tests/test_kd.cpp:34-84). */
 int mtsh_clip_triangle(const float *v, const float *box, float *out);
+
+/* The `bitmap` texture's input (src/textures/bitmap.cpp:246-278): PNG
+ * (8/16-bit, palette, sRGB / gAMA), OpenEXR or PFM converted to linear
+ * float RGB (fmtconv.cpp:1093-1160), rows top-down; gamma != 0 overrides
+ * the file's gamma.  Same return convention as mtsh_read_image. */
+int mtsh_texture_image(const char *path, float gamma, int *w, int *h, float *rgb, size_t rgb_capacity);
+
+/* TMIPMap construction (include/mitsuba/render/mipmap.h:155-302) over a
+ * linear RGB level 0: fills *mip, the half-rounded texels of every level
+ * (*n_texels floats; texels may be NULL to query the size) and the level-0
+ * average / maximum (may be NULL). */
+int mtsh_build_mipmap(const float *rgb, int w, int h, int filter, int wrap_u, int wrap_v, float max_value,
+                      float max_anisotropy, mtsg_mipmap *mip, float *texels, size_t texel_capacity, size_t *n_texels,
+                      float *average, float *maximum);
 
 void mtsh_last_error(char *buf, size_t size);
 

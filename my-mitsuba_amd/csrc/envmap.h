@@ -5,6 +5,7 @@
 // scene bounding sphere.
 #pragma once
 #include "device_math.h"
+#include "mipmap.h"
 #include "../../include/mtsg.h"
 
 namespace mtsg {
@@ -17,113 +18,7 @@ struct DevEnv {
     const float *cdfRows, *cdfCols, *rowWeights;
 };
 
-DEV int env_modulo(int a, int b) { int r = a % b; return r < 0 ? r + b : r; }
-
-// evalTexel: u repeats, v clamps (mipmap.h:503-562)
-DEV float3 env_texel(const DevEnv &V, int level, int x, int y) {
-    const int w = V.E->level_w[level], h = V.E->level_h[level];
-    if (x < 0 || x >= w) x = env_modulo(x, w);
-    if (y < 0 || y >= h) y = min(max(y, 0), h - 1);
-    const float *t = V.texels + V.E->level_offset[level] + 3 * ((size_t)y * w + x);
-    return mk3(t[0], t[1], t[2]);
-}
-
-DEV float3 env_box(const DevEnv &V, int level, float u, float v) {   // mipmap.h:566-569
-    return env_texel(V, level, (int)floorf(u * V.E->level_w[level]), (int)floorf(v * V.E->level_h[level]));
-}
-
-// evalBilinear (mipmap.h:575-596)
-DEV float3 env_bilinear(const DevEnv &V, int level, float ux, float uy) {
-    if (!isfinite(ux) || !isfinite(uy)) return mk3(0, 0, 0);
-    if (level >= V.E->levels) return env_box(V, V.E->levels - 1, ux, uy);
-    const float u = ux * V.E->level_w[level] - 0.5f, v = uy * V.E->level_h[level] - 0.5f;
-    const int xPos = (int)floorf(u), yPos = (int)floorf(v);
-    const float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
-    return env_texel(V, level, xPos, yPos) * dx2 * dy2 + env_texel(V, level, xPos, yPos + 1) * dx2 * dy1 +
-           env_texel(V, level, xPos + 1, yPos) * dx1 * dy2 + env_texel(V, level, xPos + 1, yPos + 1) * dx1 * dy1;
-}
-
-// evalEWA (mipmap.h:775-840)
-DEV float3 env_ewa(const DevEnv &V, int level, float ux, float uy, float A, float B, float C) {
-    if (!isfinite(A + B + C + ux + uy)) return mk3(0, 0, 0);
-    if (level >= V.E->levels) return env_box(V, V.E->levels - 1, ux, uy);
-    const float u = ux * V.E->level_w[level] - 0.5f, v = uy * V.E->level_h[level] - 0.5f;
-    const float rx = V.E->size_ratio_x[level], ry = V.E->size_ratio_y[level];
-    A /= rx * rx;
-    B /= rx * ry;
-    C /= ry * ry;
-    const float invDet = 1.0f / (-B * B + 4.0f * A * C), deltaU = 2.0f * sqrtf(C * invDet), deltaV = 2.0f * sqrtf(A * invDet);
-    const int u0 = (int)ceilf(u - deltaU), u1 = (int)floorf(u + deltaU);
-    const int v0 = (int)ceilf(v - deltaV), v1 = (int)floorf(v + deltaV);
-    const float As = A * MTSG_MIPMAP_LUT_SIZE, Bs = B * MTSG_MIPMAP_LUT_SIZE, Cs = C * MTSG_MIPMAP_LUT_SIZE;
-    float3 result = mk3(0, 0, 0);
-    float denominator = 0.0f;
-    const float ddq = 2 * As, uu0 = (float)u0 - u;
-    for (int vt = v0; vt <= v1; ++vt) {
-        const float vv = (float)vt - v;
-        float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
-        float dq = As * (2 * uu0 + 1) + Bs * vv;
-        for (int ut = u0; ut <= u1; ++ut) {
-            if (q < (float)MTSG_MIPMAP_LUT_SIZE) {
-                const uint32_t qi = (uint32_t)q;
-                if (qi < MTSG_MIPMAP_LUT_SIZE) {
-                    const float weight = V.E->weight_lut[(int)q];
-                    result += env_texel(V, level, ut, vt) * weight;
-                    denominator += weight;
-                }
-            }
-            q += dq;
-            dq += ddq;
-        }
-    }
-    if (denominator == 0) return env_bilinear(V, level, ux, uy);
-    return result / denominator;
-}
-
-DEV float hypot2_env(float a, float b) {   // math.cpp:74-86
-    float r;
-    if (fabsf(a) > fabsf(b)) { r = b / a; r = fabsf(a) * sqrtf(1.0f + r * r); }
-    else if (b != 0.0f) { r = a / b; r = fabsf(b) * sqrtf(1.0f + r * r); }
-    else r = 0.0f;
-    return r;
-}
-
-DEV float log2_m(float v) { return logf(v) * (1.0f / 0.69314718055994530942f); }   // math.cpp:103-106
-
-// TMIPMap::eval with EEWA (mipmap.h:633-722)
-DEV float3 env_filtered(const DevEnv &V, float ux, float uy, float d0x, float d0y, float d1x, float d1y) {
-    const float w0 = (float)V.E->level_w[0], h0 = (float)V.E->level_h[0];
-    const float du0 = d0x * w0, dv0 = d0y * h0, du1 = d1x * w0, dv1 = d1y * h0;
-    float A = dv0 * dv0 + dv1 * dv1, B = -2.0f * (du0 * dv0 + du1 * dv1), C = du0 * du0 + du1 * du1, F = A * C - B * B * 0.25f;
-    const float root = hypot2_env(A - C, B), Aprime = 0.5f * (A + C - root), Cprime = 0.5f * (A + C + root);
-    float majorRadius = Aprime != 0 ? sqrtf(F / Aprime) : 0, minorRadius = Cprime != 0 ? sqrtf(F / Cprime) : 0;
-    if (!(minorRadius > 0) || !(majorRadius > 0) || F < 0) {
-        const float level = log2_m(fmaxf(majorRadius, kEpsilon));
-        const int ilevel = (int)floorf(level);
-        if (ilevel < 0) return env_bilinear(V, 0, ux, uy);
-        const float a = level - ilevel;
-        return env_bilinear(V, ilevel, ux, uy) * (1.0f - a) + env_bilinear(V, ilevel + 1, ux, uy) * a;
-    }
-    if (minorRadius * V.E->max_anisotropy < majorRadius) {
-        minorRadius = majorRadius / V.E->max_anisotropy;
-        const float theta = 0.5f * atanf(B / (A - C));
-        float sinTheta, cosTheta;
-        sincosf(theta, &sinTheta, &cosTheta);
-        const float a2 = majorRadius * majorRadius, b2 = minorRadius * minorRadius, sinTheta2 = sinTheta * sinTheta,
-                    cosTheta2 = cosTheta * cosTheta, sin2Theta = 2 * sinTheta * cosTheta;
-        A = a2 * cosTheta2 + b2 * sinTheta2;
-        B = (a2 - b2) * sin2Theta;
-        C = a2 * sinTheta2 + b2 * cosTheta2;
-        F = a2 * b2;
-    }
-    const float scale = 1.0f / F;
-    A *= scale; B *= scale; C *= scale;
-    const float level = fmaxf(0.0f, log2_m(minorRadius));
-    const int ilevel = (int)level;
-    const float a = level - ilevel;
-    if (majorRadius < 1 || !(A > 0 && C > 0)) return env_bilinear(V, ilevel, ux, uy);
-    return env_ewa(V, ilevel, ux, uy, A, B, C) * (1.0f - a) + env_ewa(V, ilevel + 1, ux, uy, A, B, C) * a;
-}
+DEV DevMip env_mip(const DevEnv &V) { return DevMip{&V.E->mip, V.texels}; }   // u repeats, v clamps
 
 DEV float3 env_rot(const float *m, float3 v) {
     return mk3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z, m[6] * v.x + m[7] * v.y + m[8] * v.z);
@@ -136,11 +31,11 @@ DEV float3 env_eval(const DevEnv &V, float3 dWorld, bool hasDiff, float3 rxD, fl
     const float ux = atan2f(v.x, -v.z) * kInvTwoPi, uy = acosf(fminf(1.0f, fmaxf(-1.0f, v.y))) * kInvPi;
     float3 value;
     if (!hasDiff) {
-        value = env_bilinear(V, 0, ux, uy);
+        value = mip_bilinear(env_mip(V), 0, ux, uy);
     } else {
         const float3 dvdx = env_rot(V.E->to_local, rxD) - v, dvdy = env_rot(V.E->to_local, ryD) - v;
         const float t1 = kInvTwoPi / (v.x * v.x + v.z * v.z), t2 = -kInvPi / fmaxf(sqrtf(fmaxf(0.0f, 1.0f - v.y * v.y)), kEpsilon);
-        value = env_filtered(V, ux, uy, t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y, t1 * (dvdy.z * v.x - dvdy.x * v.z),
+        value = mip_filtered(env_mip(V), ux, uy, t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y, t1 * (dvdy.z * v.x - dvdy.x * v.z),
                              t2 * dvdy.y);
     }
     return value * V.E->scale;
@@ -170,14 +65,15 @@ DEV float env_tent(float sample) {   // warp.cpp:143-155
 
 // internalSampleDirection (envmap.cpp:574-600): local direction, value, pdf
 DEV void env_internal_sample(const DevEnv &V, float sx, float sy, float3 &d, float3 &value, float &pdf) {
-    const int W = V.E->level_w[0], H = V.E->level_h[0];
+    const int W = V.E->mip.level_w[0], H = V.E->mip.level_h[0];
+    const DevMip M = env_mip(V);
     const uint32_t row = env_sample_reuse(V.cdfRows, (uint32_t)H, sy);
     const uint32_t col = env_sample_reuse(V.cdfCols + row * (uint32_t)(W + 1), (uint32_t)W, sx);
     const float px = (float)col + env_tent(sx), py = (float)row + env_tent(sy);
     const int xPos = (int)floorf(px), yPos = (int)floorf(py);
     const float dx1 = px - xPos, dx2 = 1.0f - dx1, dy1 = py - yPos, dy2 = 1.0f - dy1;
-    const float3 value1 = env_texel(V, 0, xPos, yPos) * dx2 * dy2 + env_texel(V, 0, xPos + 1, yPos) * dx1 * dy2;
-    const float3 value2 = env_texel(V, 0, xPos, yPos + 1) * dx2 * dy1 + env_texel(V, 0, xPos + 1, yPos + 1) * dx1 * dy1;
+    const float3 value1 = mip_texel(M, 0, xPos, yPos) * dx2 * dy2 + mip_texel(M, 0, xPos + 1, yPos) * dx1 * dy2;
+    const float3 value2 = mip_texel(M, 0, xPos, yPos + 1) * dx2 * dy1 + mip_texel(M, 0, xPos + 1, yPos + 1) * dx1 * dy1;
     value = (value1 + value2) * V.E->scale;
     pdf = (env_lum(value1) * V.rowWeights[min(max(yPos, 0), H - 1)] +
            env_lum(value2) * V.rowWeights[min(max(yPos + 1, 0), H - 1)]) * V.E->normalization;
@@ -190,14 +86,15 @@ DEV void env_internal_sample(const DevEnv &V, float sx, float sy, float3 &d, flo
 
 // internalPdfDirection (envmap.cpp:603-633), local direction
 DEV float env_internal_pdf(const DevEnv &V, float3 d) {
-    const int W = V.E->level_w[0], H = V.E->level_h[0];
+    const int W = V.E->mip.level_w[0], H = V.E->mip.level_h[0];
+    const DevMip M = env_mip(V);
     const float ux = atan2f(d.x, -d.z) * kInvTwoPi, uy = acosf(fminf(1.0f, fmaxf(-1.0f, d.y))) * kInvPi;
     if (!isfinite(ux) || !isfinite(uy)) return 0.0f;
     const float u = ux * W - 0.5f, v = uy * H - 0.5f;
     const int xPos = (int)floorf(u), yPos = (int)floorf(v);
     const float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
-    const float3 value1 = env_texel(V, 0, xPos, yPos) * dx2 * dy2 + env_texel(V, 0, xPos + 1, yPos) * dx1 * dy2;
-    const float3 value2 = env_texel(V, 0, xPos, yPos + 1) * dx2 * dy1 + env_texel(V, 0, xPos + 1, yPos + 1) * dx1 * dy1;
+    const float3 value1 = mip_texel(M, 0, xPos, yPos) * dx2 * dy2 + mip_texel(M, 0, xPos + 1, yPos) * dx1 * dy2;
+    const float3 value2 = mip_texel(M, 0, xPos, yPos + 1) * dx2 * dy1 + mip_texel(M, 0, xPos + 1, yPos + 1) * dx1 * dy1;
     const float sinTheta = sqrtf(fmaxf(0.0f, 1 - d.y * d.y));
     return (env_lum(value1) * V.rowWeights[min(max(yPos, 0), H - 1)] +
             env_lum(value2) * V.rowWeights[min(max(yPos + 1, 0), H - 1)]) *

@@ -58,6 +58,12 @@ struct DevScene {
     // {group AABB max, root word 1}; the group trees live in `blocks` / `triL`
     // beside the top-level tree.  nullptr: no instances.
     const float4 *__restrict__ inst;
+    // bitmap textures (mipmap.h): headers, texels, and per triangle 3 float4
+    // {uv0, uv1 | uv2, dpdv.xy | dpdv.z} for the lookups; nullptr: none
+    const mtsg_texture *__restrict__ textures;
+    const float *__restrict__ tex_texels;
+    const float4 *__restrict__ ttex;
+    int cam_diffs;        // bounce 0 carries the camera's ray differentials in T / aux
 };
 
 struct DevCamera {
@@ -69,7 +75,7 @@ struct DevCamera {
     int border, has_alpha;
     float filter_values[32];
     float dx[3], dy[3];   // near-plane differentials (perspective.cpp:160-170)
-    int has_env;          // store primary-ray differentials for the environment lookup
+    int diffs;            // store primary-ray differentials (environment / filtered texture lookups)
     int crop_w, crop_h;   // the sampler's space partition (setFilmResolution)
 };
 
@@ -434,6 +440,19 @@ __global__ void k_env_eval(DevScene S, const float *dirs, const float *rx, const
     const float3 y = diff ? mk3(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]) : d;
     const float3 v = env_eval(S.env, d, diff, x, y);
     out[3 * i] = v.x; out[3 * i + 1] = v.y; out[3 * i + 2] = v.z;
+}
+
+// BitmapTexture::eval(uv) / eval(uv, d0, d1) (bitmap.cpp:431-499) of texture
+// `tex`, for the parity tests (mtsg_tex_eval)
+__global__ void k_tex_eval(DevScene S, int tex, const float *uv, const float *duv, uint32_t n, float *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const DevMip M{&S.textures[tex].mip, S.tex_texels};
+    const float u = uv[2 * i], v = uv[2 * i + 1];
+    float3 r;
+    if (duv) r = mip_filtered(M, u, v, duv[4 * i], duv[4 * i + 1], duv[4 * i + 2], duv[4 * i + 3]);
+    else r = M.M->filter == MTSG_MIP_NEAREST ? mip_box(M, 0, u, v) : mip_bilinear(M, 0, u, v);
+    out[3 * i] = r.x; out[3 * i + 1] = r.y; out[3 * i + 2] = r.z;
 }
 
 // ---------------------------------------------------------------------------
@@ -1045,7 +1064,7 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
                             t[8] * d.x + t[9] * d.y + t[10] * d.z);
             stS(&P.ray_o[slot], make_float4(t[3], t[7], t[11], C.near_clip * invZ));
             stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
-            if (C.has_env) {
+            if (C.diffs) {
                 // rx/ryDirection scaled by 1/sqrt(spp) (integrator.cpp:148-149, ray.h:163-168),
                 const float3 rxc = normalize(nearP + ld3(C.dx)), ryc = normalize(nearP + ld3(C.dy));
                 const float3 rx = mk3(t[0] * rxc.x + t[1] * rxc.y + t[2] * rxc.z, t[4] * rxc.x + t[5] * rxc.y + t[6] * rxc.z,
@@ -1376,8 +1395,7 @@ DEV float fresnel_dielectric1(float cosThetaI, float eta) {
 }
 
 // plastic.cpp:216-222: the diffuse base renormalised for internal reflection
-DEV float3 plastic_diffuse(const mtsg_bsdf &b) {
-    float3 diff = ld3(b.reflectance);
+DEV float3 plastic_diffuse(const mtsg_bsdf &b, float3 diff) {
     if (b.nonlinear) diff = diff / (mk3(1.0f, 1.0f, 1.0f) - diff * b.fdr_int);
     else diff = diff / (1 - b.fdr_int);
     return diff;
@@ -1409,13 +1427,15 @@ DEV float rough_trans(const mtsg_bsdf &b, float cosTheta) {
 // scene has conductor / plastic / twosided records (the shade kernel is
 // instantiated without them otherwise: their code costs the common
 // diffuse + roughconductor + dielectric kernel its register budget)
+// alb: the record's reflectance (`reflectance` / `diffuseReflectance`), the
+// constant or its texture's value at the hit (texture_eval)
 template <bool EXT>
-DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
+DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 alb, float3 wi, float3 wo, float &pdf) {
     pdf = 0.0f;
     if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:107-126
         if (!b.smooth || wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
         pdf = kInvPi * wo.z;
-        return ld3(b.reflectance) * (kInvPi * wo.z);
+        return alb * (kInvPi * wo.z);
     }
     if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:235-293
         if (wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
@@ -1467,7 +1487,7 @@ DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
         const float Fi = fresnel_dielectric1(wi.z, b.ior_eta), Fo = fresnel_dielectric1(wo.z, b.ior_eta);
         const float invEta2 = 1 / (b.ior_eta * b.ior_eta);
         pdf = kInvPi * wo.z * (1 - plastic_prob_specular(b, Fi));
-        return plastic_diffuse(b) * (kInvPi * wo.z * invEta2 * (1 - Fi) * (1 - Fo));
+        return plastic_diffuse(b, alb) * (kInvPi * wo.z * invEta2 * (1 - Fi) * (1 - Fo));
     }
     if (EXT && b.type == MTSG_BSDF_ROUGHPLASTIC) {   // roughplastic.cpp:302-345 (eval), 347-385 (pdf)
         if (wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
@@ -1482,7 +1502,7 @@ DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
         float probSpecular = plastic_prob_specular(b, 1 - T12);
         const float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
         pdf = mf.pdf(wi, H) * dwh_dwo * probSpecular + (1 - probSpecular) * (kInvPi * wo.z);
-        return ld3(b.spec_refl) * value + plastic_diffuse(b) * (kInvPi * wo.z * T12 * T21 * invEta2);
+        return ld3(b.spec_refl) * value + plastic_diffuse(b, alb) * (kInvPi * wo.z * T12 * T21 * invEta2);
     }
     return mk3(0, 0, 0);   // dielectric / conductor: delta components only
 }
@@ -1490,14 +1510,14 @@ DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
 // next1d: the sampler's next1D, drawn only where Mitsuba draws it
 // (roughdielectric's reflect/refract choice: roughdielectric.cpp:531-539)
 template <bool EXT, class Next1D>
-DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r, Next1D &&next1d) {
+DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 alb, float3 wi, float sx, float sy, BsdfSample &r, Next1D &&next1d) {
     r.eta = 1.0f;
     r.delta = 0;
     if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
         if (wi.z <= 0) return false;
         r.wo = cosine_hemisphere(sx, sy);
         r.pdf = kInvPi * r.wo.z;
-        r.weight = ld3(b.reflectance);
+        r.weight = alb;
         return !isZero(r.weight);
     }
     if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:345-394
@@ -1599,7 +1619,7 @@ DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSam
             r.wo = cosine_hemisphere(sx, sy);
         }
         float pdf;
-        const float3 val = bsdf_eval1<EXT>(b, wi, r.wo, pdf);
+        const float3 val = bsdf_eval1<EXT>(b, alb, wi, r.wo, pdf);
         if (pdf == 0) return false;
         r.pdf = pdf;
         r.weight = val / pdf;
@@ -1619,7 +1639,7 @@ DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSam
             const float Fo = fresnel_dielectric1(r.wo.z, b.ior_eta);
             const float invEta2 = 1 / (b.ior_eta * b.ior_eta);
             r.pdf = (1 - probSpecular) * (kInvPi * r.wo.z);
-            r.weight = plastic_diffuse(b) * (invEta2 * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
+            r.weight = plastic_diffuse(b, alb) * (invEta2 * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
         }
         return !isZero(r.weight);
     }
@@ -1628,24 +1648,27 @@ DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSam
 
 // twosided.cpp:103-170: a twosided front record hands back-side queries to
 // bsdfs[back] with the z components negated
+// alb belongs to the record that answers (the back record for back-side
+// queries of a twosided front record)
 template <bool EXT>
-DEV float3 bsdf_eval(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float3 wo, float &pdf) {
+DEV float3 bsdf_eval(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 alb, float3 wi, float3 wo, float &pdf) {
     if (EXT && b.twosided && !(wi.z > 0)) {
         wi.z = -wi.z;
         wo.z = -wo.z;
-        return bsdf_eval1<EXT>(all[b.back], wi, wo, pdf);
+        return bsdf_eval1<EXT>(all[b.back], alb, wi, wo, pdf);
     }
-    return bsdf_eval1<EXT>(b, wi, wo, pdf);
+    return bsdf_eval1<EXT>(b, alb, wi, wo, pdf);
 }
 template <bool EXT, class Next1D>
-DEV bool bsdf_sample(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 wi, float sx, float sy, BsdfSample &r, Next1D &&next1d) {
+DEV bool bsdf_sample(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 alb, float3 wi, float sx, float sy, BsdfSample &r,
+                     Next1D &&next1d) {
     if (EXT && b.twosided && wi.z < 0) {
         wi.z = -wi.z;
-        if (!bsdf_sample1<EXT>(all[b.back], wi, sx, sy, r, next1d)) return false;
+        if (!bsdf_sample1<EXT>(all[b.back], alb, wi, sx, sy, r, next1d)) return false;
         r.wo.z = -r.wo.z;
         return true;
     }
-    return bsdf_sample1<EXT>(b, wi, sx, sy, r, next1d);
+    return bsdf_sample1<EXT>(b, alb, wi, sx, sy, r, next1d);
 }
 
 DEV float mis(float pdfA, float pdfB) {   // path.cpp:296-300
@@ -1745,6 +1768,85 @@ DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, uint32_t in
     its.sh.t = cross(n, its.sh.s);
 }
 
+// `bitmap` texture value of a hit (Texture2D::eval(its, filter),
+// texture.cpp:112-121, over BitmapTexture::eval, bitmap.cpp:431-499, times
+// the ScaleTexture of ensureEnergyConservation).  The hit's uv and dpdv come
+// from the triangle's texture record (skdtree.h:369-405; rectangles:
+// rectangle.cpp:155-164), dpdu from its shading record; instances map both
+// tangents with toWorld (instance.cpp:146-160).  diffs: the camera ray's
+// scaled differentials rxD / ryD exist (bounce 0), so the lookup is filtered
+// with the UV partials of Intersection::computePartials (intersection.cpp:5-80)
+DEV float3 texture_eval(const DevScene &S, int tex, float4 h, uint32_t inst, const Its &its, float3 ro, bool diffs, float3 rxD,
+                        float3 ryD) {
+#pragma clang fp contract(off)
+    const mtsg_texture &T = S.textures[tex];
+    const DevMip M{&T.mip, S.tex_texels};
+    const uint32_t p = __float_as_uint(h.w);
+    float2 uv;
+    float3 dpdu, dpdv;
+    if (!(p & 0x80000000u)) {
+        const float4 *t = S.ttex + 3 * (size_t)p;
+        const float4 t0 = t[0], t1 = t[1], t2 = t[2];
+        const float bx = 1 - h.y - h.z, by = h.y, bz = h.z;
+        uv = make_float2(t0.x * bx + t0.z * by + t1.x * bz, t0.y * bx + t0.w * by + t1.y * bz);
+        dpdv = mk3(t1.z, t1.w, t2.x);
+        const float4 *rec = S.shrec + 6 * (size_t)p;
+        const float4 r4 = rec[4], r5 = rec[5];
+        dpdu = mk3(r4.z, r4.w, r5.x);
+        if (inst != 0xFFFFFFFFu) {
+            const float4 *I = S.inst + 8 * (size_t)inst;
+            const float4 W0 = I[3], W1 = I[4], W2 = I[5];
+            dpdu = mk3(W0.x * dpdu.x + W0.y * dpdu.y + W0.z * dpdu.z, W1.x * dpdu.x + W1.y * dpdu.y + W1.z * dpdu.z,
+                       W2.x * dpdu.x + W2.y * dpdu.y + W2.z * dpdu.z);
+            dpdv = mk3(W0.x * dpdv.x + W0.y * dpdv.y + W0.z * dpdv.z, W1.x * dpdv.x + W1.y * dpdv.y + W1.z * dpdv.z,
+                       W2.x * dpdv.x + W2.y * dpdv.y + W2.z * dpdv.z);
+        }
+    } else {
+        const mtsg_rect &r = S.rects[p & 0x7FFFFFFFu];
+        uv = make_float2(0.5f * (h.y + 1), 0.5f * (h.z + 1));
+        dpdu = ld3(r.dpdu);
+        dpdv = ld3(r.dpdv);
+    }
+    const float2 uvs = make_float2(uv.x * T.uv_scale[0] + T.uv_offset[0], uv.y * T.uv_scale[1] + T.uv_offset[1]);
+    float3 value;
+    if (diffs && T.mip.filter >= MTSG_MIP_TRILINEAR) {
+        float dudx = 0, dvdx = 0, dudy = 0, dvdy = 0;
+        const float3 n = its.geoN;
+        if (!(isZero(dpdu) && isZero(dpdv))) {
+            const float pp = dot(n, its.p), po = dot(n, ro), prx = dot(n, rxD), pry = dot(n, ryD);
+            if (!(prx == 0 || pry == 0)) {
+                const float tx = (pp - po) / prx, ty = (pp - po) / pry;
+                const float ax = fabsf(n.x), ay = fabsf(n.y), az = fabsf(n.z);
+                int a0, a1;
+                if (ax > ay && ax > az) { a0 = 1; a1 = 2; }
+                else if (ay > az) { a0 = 0; a1 = 2; }
+                else { a0 = 0; a1 = 1; }
+                auto c = [](float3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); };
+                const float A00 = c(dpdu, a0), A01 = c(dpdv, a0), A10 = c(dpdu, a1), A11 = c(dpdv, a1);
+                const float3 px = ro + rxD * tx, py = ro + ryD * ty;
+                const float Bx0 = c(px, a0) - c(its.p, a0), Bx1 = c(px, a1) - c(its.p, a1);
+                const float By0 = c(py, a0) - c(its.p, a0), By1 = c(py, a1) - c(its.p, a1);
+                // solveLinearSystem2x2 (util.cpp:527-539); on failure dudx = 1,
+                // dvdx = 0, dudy = 1 (the reference leaves dvdy unset: 0 here)
+                const float det = A00 * A11 - A01 * A10;
+                if (fabsf(det) <= 0x1p-128f) {
+                    dudx = 1; dvdx = 0; dudy = 1; dvdy = 0;
+                } else {
+                    const float inv = 1.0f / det;
+                    dudx = (A11 * Bx0 - A01 * Bx1) * inv;
+                    dvdx = (A00 * Bx1 - A10 * Bx0) * inv;
+                    dudy = (A11 * By0 - A01 * By1) * inv;
+                    dvdy = (A00 * By1 - A10 * By0) * inv;
+                }
+            }
+        }
+        value = mip_filtered(M, uvs.x, uvs.y, dudx * T.uv_scale[0], dvdx * T.uv_scale[1], dudy * T.uv_scale[0], dvdy * T.uv_scale[1]);
+    } else {
+        value = T.mip.filter == MTSG_MIP_NEAREST ? mip_box(M, 0, uvs.x, uvs.y) : mip_bilinear(M, 0, uvs.x, uvs.y);
+    }
+    return value * T.scale;
+}
+
 // Shape::sampleDirect over TriMesh / Rectangle samplePosition (shape.cpp:102-115,
 // trimesh.cpp:412-423, triangle.cpp:24-60, rectangle.cpp:200-207)
 DEV void emitter_sample_position(const DevScene &S, const mtsg_emitter &em, float sx, float sy, float3 &p, float3 &n) {
@@ -1836,7 +1938,9 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
     const bool valid = __float_as_uint(h.w) != 0xFFFFFFFFu;
     bool done = false;
     Its its;
-    if (valid) fill_its(S, ro, rd, h, S.inst ? P.hitInst[i] : 0xFFFFFFFFu, its);
+    const uint32_t inst = (valid && S.inst) ? P.hitInst[i] : 0xFFFFFFFFu;
+    if (valid) fill_its(S, ro, rd, h, inst, its);
+    float3 rxd = mk3(0, 0, 0), ryd = mk3(0, 0, 0);   // camera differentials (textured EXT scenes)
     if (first) {
         // RadianceQueryRecord::rayIntersect (records.inl:117-143)
         if (hasAlpha) L4.w = valid ? 1.0f : 0.0f;
@@ -1848,7 +1952,10 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
             }
             done = true;
         }
-        if (ENV) T = mk3(1.f, 1.f, 1.f);   // T held the x-differential
+        if (S.cam_diffs) {   // T / aux held the camera's scaled differentials
+            if (EXT && S.textures) { rxd = T; ryd = xyz(ldS(&P.aux[i])); }
+            T = mk3(1.f, 1.f, 1.f);
+        }
     } else {
         // tail of the previous iteration after scene->rayIntersect (path.cpp:226-286)
         if (!valid) {
@@ -1892,6 +1999,14 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
     if (!done) {
         const mtsg_bsdf &bsdf = S.bsdfs[its.bsdf];
         const float3 wi = its.sh.toLocal(-rd);
+        float3 alb;
+        if (EXT) {
+            const mtsg_bsdf &eff = (bsdf.twosided && !(wi.z > 0)) ? S.bsdfs[bsdf.back] : bsdf;
+            alb = eff.texture ? texture_eval(S, eff.texture - 1, h, inst, its, ro, first && S.cam_diffs, rxd, ryd)
+                              : ld3(eff.reflectance);
+        } else {
+            alb = ld3(bsdf.reflectance);
+        }
         if (first && its.emitter >= 0 && !I.hide_emitters) {
             if (dot(its.sh.n, -rd) > 0) L += T * ld3(S.emitters[its.emitter].radiance);
         }
@@ -1929,7 +2044,7 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
                     value = value / emPdf;
                     const float3 wo = its.sh.toLocal(dd);
                     float bpdf;
-                    const float3 bval = bsdf_eval<EXT>(S.bsdfs, bsdf, wi, wo, bpdf);
+                    const float3 bval = bsdf_eval<EXT>(S.bsdfs, bsdf, alb, wi, wo, bpdf);
                     if (!isZero(bval) && (!I.strict_normals || dot(its.geoN, dd) * wo.z > 0)) {
                         const float weight = mis(pdf, bpdf);
                         const float3 c = T * value * bval * weight;
@@ -1945,7 +2060,7 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
             float sx, sy;
             next2D<SMP>(I, smp, sx, sy);
             BsdfSample bs;
-            if (!bsdf_sample<EXT>(S.bsdfs, bsdf, wi, sx, sy, bs, [&]() { return next1D<SMP>(I, smp); })) {
+            if (!bsdf_sample<EXT>(S.bsdfs, bsdf, alb, wi, sx, sy, bs, [&]() { return next1D<SMP>(I, smp); })) {
                 done = true;
             } else {
                 flags |= F_SCATTERED;

@@ -99,7 +99,8 @@ struct mtsg_scene {
     std::vector<unsigned long long> stragglers;  // MTSG_FLAG_COUNT: slow-ray records
     unsigned long long *waveTimes = nullptr;     // MTSG_FLAG_WAVETIME: [launch][wave][WT_WORDS]
     uint32_t wtLaunches = 0;
-    bool extBsdfs = false;   // conductor / plastic / twosided records present (k_shade<..., true>)
+    bool extBsdfs = false;   // conductor / plastic / twosided records or textures present (k_shade<..., true>)
+    uint32_t nTextures = 0;
     const uint32_t *sobolM = nullptr;        // sobol sampler tables (device)
     const uint64_t *sobolVdc = nullptr, *sobolVdcInv = nullptr;
     uint64_t sobolScramble = 0;
@@ -840,23 +841,63 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     ds.env = DevEnv{nullptr, nullptr, nullptr, nullptr, nullptr};
     if (d->has_envmap) {
         const mtsg_envmap &E = d->envmap;
-        if (E.levels <= 0 || E.levels > MTSG_ENVMAP_MAX_LEVELS || !d->env_texels || !d->env_cdf_rows || !d->env_cdf_cols ||
+        const mtsg_mipmap &EM = E.mip;
+        if (EM.levels <= 0 || EM.levels > MTSG_ENVMAP_MAX_LEVELS || !d->env_texels || !d->env_cdf_rows || !d->env_cdf_cols ||
             !d->env_row_weights || E.emitter < 0 || (uint32_t)E.emitter >= d->n_emitters) {
             g_err = "inconsistent environment map description";
             return fail(MTSG_ERR_INVALID);
         }
         size_t need = 0;
-        for (int l = 0; l < E.levels; ++l)
-            need = std::max(need, (size_t)E.level_offset[l] + 3 * (size_t)E.level_w[l] * E.level_h[l]);
+        for (int l = 0; l < EM.levels; ++l)
+            need = std::max(need, (size_t)EM.level_offset[l] + 3 * (size_t)EM.level_w[l] * EM.level_h[l]);
         if (need > d->n_env_texels) { g_err = "environment map texel array too small"; return fail(MTSG_ERR_INVALID); }
         mtsg_envmap *dE; float *dt, *dr, *dc, *dw;
-        const int W = E.level_w[0], H = E.level_h[0];
+        const int W = EM.level_w[0], H = EM.level_h[0];
         if ((rc = up(&E, 1, &dE)) || (rc = up(d->env_texels, d->n_env_texels, &dt)) ||
             (rc = up(d->env_cdf_rows, (size_t)H + 1, &dr)) || (rc = up(d->env_cdf_cols, (size_t)(W + 1) * H, &dc)) ||
             (rc = up(d->env_row_weights, (size_t)H, &dw)))
             return fail(rc);
         ds.env = DevEnv{dE, dt, dr, dc, dw};
     }
+    // bitmap textures (mipmap.h) and the per-triangle records of their lookups
+    ds.textures = nullptr; ds.tex_texels = nullptr; ds.ttex = nullptr;
+    bool texDiffs = false;
+    for (uint32_t i = 0; i < d->n_bsdfs; ++i)
+        if (d->bsdfs[i].texture < 0 || (uint32_t)d->bsdfs[i].texture > d->n_textures) {
+            g_err = "bsdf " + std::to_string(i) + ": texture index out of range";
+            return fail(MTSG_ERR_INVALID);
+        }
+    if (d->n_textures) {
+        if (!d->textures || !d->tex_texels || (d->n_triangles && (!d->tri_uv || !d->tri_dpdv))) {
+            g_err = "inconsistent texture description";
+            return fail(MTSG_ERR_INVALID);
+        }
+        for (uint32_t i = 0; i < d->n_textures; ++i) {
+            const mtsg_mipmap &M = d->textures[i].mip;
+            bool ok = M.levels > 0 && M.levels <= MTSG_MIPMAP_MAX_LEVELS && M.filter >= MTSG_MIP_NEAREST && M.filter <= MTSG_MIP_EWA &&
+                      M.wrap_u >= MTSG_WRAP_CLAMP && M.wrap_u <= MTSG_WRAP_ONE && M.wrap_v >= MTSG_WRAP_CLAMP && M.wrap_v <= MTSG_WRAP_ONE;
+            for (int l = 0; ok && l < M.levels; ++l)
+                ok = M.level_w[l] > 0 && M.level_h[l] > 0 &&
+                     (size_t)M.level_offset[l] + 3 * (size_t)M.level_w[l] * M.level_h[l] <= d->n_tex_texels;
+            if (!ok) { g_err = "texture " + std::to_string(i) + ": malformed MIP map"; return fail(MTSG_ERR_INVALID); }
+            texDiffs |= M.filter == MTSG_MIP_TRILINEAR || M.filter == MTSG_MIP_EWA;
+        }
+        std::vector<float4> tt((size_t)3 * std::max(1u, d->n_triangles), make_float4(0, 0, 0, 0));
+        for (uint32_t t = 0; t < d->n_triangles; ++t) {
+            const float *uv = d->tri_uv + 6 * (size_t)t, *dv = d->tri_dpdv + 3 * (size_t)t;
+            tt[3 * t] = make_float4(uv[0], uv[1], uv[2], uv[3]);
+            tt[3 * t + 1] = make_float4(uv[4], uv[5], dv[0], dv[1]);
+            tt[3 * t + 2] = make_float4(dv[2], 0.f, 0.f, 0.f);
+        }
+        mtsg_texture *dtex; float *dtt; float4 *dttex;
+        if ((rc = up(d->textures, d->n_textures, &dtex)) || (rc = up(d->tex_texels, d->n_tex_texels, &dtt)) ||
+            (rc = up(tt.data(), tt.size(), &dttex)))
+            return fail(rc);
+        ds.textures = dtex; ds.tex_texels = dtt; ds.ttex = dttex;
+        s->nTextures = d->n_textures;
+        s->extBsdfs = true;   // texture lookups live in the extended shade kernel
+    }
+    ds.cam_diffs = (d->has_envmap || texDiffs) ? 1 : 0;
     ds.n_emitters = d->n_emitters;
     ds.n_tri = d->n_triangles;
     for (int k = 0; k < 3; ++k) { ds.bmin[k] = d->aabb_min[k]; ds.bmax[k] = d->aabb_max[k]; }
@@ -871,7 +912,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     memcpy(c.filter_values, hc.filter_values, sizeof(c.filter_values));
     memcpy(c.dx, hc.dx, sizeof(c.dx));
     memcpy(c.dy, hc.dy, sizeof(c.dy));
-    c.has_env = d->has_envmap ? 1 : 0;
+    c.diffs = ds.cam_diffs;
     c.crop_w = hc.crop_w; c.crop_h = hc.crop_h;
     // sampler and its quasi-Monte Carlo tables
     s->samplerType = d->sampler.type;
@@ -1155,6 +1196,29 @@ int mtsg_env_eval(mtsg_scene *s, uint32_t n, const float *dirs, const float *rx,
         e = hipStreamSynchronize(s->stream);
     }
     if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+    cleanup();
+    if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    return MTSG_OK;
+}
+
+int mtsg_tex_eval(mtsg_scene *s, int tex, uint32_t n, const float *uv, const float *duv, float *out) {
+    if (!s || (!uv && n) || (!out && n)) { g_err = "invalid arguments"; return MTSG_ERR_INVALID; }
+    if (tex < 0 || (uint32_t)tex >= s->nTextures) { g_err = "texture index out of range"; return MTSG_ERR_INVALID; }
+    if (n == 0) return MTSG_OK;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    float *duv_d = nullptr, *dd = nullptr, *dout = nullptr;
+    auto cleanup = [&]() { hipFree(duv_d); hipFree(dd); hipFree(dout); };
+    hipError_t e = hipMalloc((void **)&dd, (size_t)n * 2 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc((void **)&dout, (size_t)n * 3 * sizeof(float));
+    if (e == hipSuccess && duv) e = hipMalloc((void **)&duv_d, (size_t)n * 4 * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(dd, uv, (size_t)n * 2 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess && duv) e = hipMemcpy(duv_d, duv, (size_t)n * 4 * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_tex_eval, dim3((n + 255) / 256), dim3(256), 0, s->stream, s->ds, tex, dd, duv_d, n, dout);
+        e = hipStreamSynchronize(s->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost);
     cleanup();
     if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
     return MTSG_OK;

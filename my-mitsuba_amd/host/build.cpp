@@ -147,7 +147,8 @@ void setRow34(float *dst, const Transform &t, bool inverse) {
 
 void Scene::finalize() {
     // ---------------- geometry ----------------
-    vtxPos.clear(); vtxNrm.clear(); triIdx.clear(); triDpdu.clear();
+    vtxPos.clear(); vtxNrm.clear(); triIdx.clear(); triDpdu.clear(); triUv.clear(); triDpdv.clear();
+    const bool texData = !textures.empty();
     shapeDesc.clear(); rectDesc.clear();
     std::vector<uint32_t> meshTriBegin(meshes.size());
     for (size_t si = 0; si < shapes.size(); ++si) {
@@ -171,26 +172,34 @@ void Scene::finalize() {
                 uint32_t i0 = m.idx[t], i1 = m.idx[t + 1], i2 = m.idx[t + 2];
                 triIdx.insert(triIdx.end(), {vbase + i0, vbase + i1, vbase + i2});
                 V3 dP1 = m.p[i1] - m.p[i0], dP2 = m.p[i2] - m.p[i0];
-                V3 dpdu = dP1;   // no UV tangents: its.dpdu = side1 (skdtree.h:373-380)
+                V3 dpdu = dP1, dpdv = dP2;   // no UV tangents: side1, side2 (skdtree.h:373-380)
                 if (hasUV) {
-                    // computeUVTangents (trimesh.cpp:701-735)
+                    // computeUVTangents (trimesh.cpp:701-735); degenerate
+                    // triangles keep the zeroed tangents
                     V3 n = cross(dP1, dP2);
                     float len = length(n);
                     if (len == 0) {
-                        dpdu = V3(0.0f);
+                        dpdu = dpdv = V3(0.0f);
                     } else {
                         float du1 = m.uv[2 * i1] - m.uv[2 * i0], dv1 = m.uv[2 * i1 + 1] - m.uv[2 * i0 + 1];
                         float du2 = m.uv[2 * i2] - m.uv[2 * i0], dv2 = m.uv[2 * i2 + 1] - m.uv[2 * i0 + 1];
                         float det = du1 * dv2 - dv1 * du2;
                         if (det == 0) {
-                            V3 s, tt;
-                            coordinateSystem(n / len, s, tt);
-                            dpdu = s;
+                            coordinateSystem(n / len, dpdu, dpdv);
                         } else {
                             float invDet = 1.0f / det;
                             dpdu = (dP1 * dv2 - dP2 * dv1) * invDet;
+                            dpdv = (dP1 * (-du2) + dP2 * du1) * invDet;
                         }
                     }
+                }
+                if (texData) {
+                    if (hasUV) {
+                        for (uint32_t vi : {i0, i1, i2}) triUv.insert(triUv.end(), {m.uv[2 * vi], m.uv[2 * vi + 1]});
+                    } else {
+                        triUv.insert(triUv.end(), {0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 1.0f});   // -> Point2(b.y, b.z)
+                    }
+                    triDpdv.insert(triDpdv.end(), {dpdv.x, dpdv.y, dpdv.z});
                 }
                 triDpdu.insert(triDpdu.end(), {dpdu.x, dpdu.y, dpdu.z});
             }
@@ -440,6 +449,14 @@ void Scene::finalize() {
     d.n_triangles = (uint32_t)nTri;
     d.tri_idx = triIdx.data();
     d.tri_dpdu = triDpdu.data();
+    d.n_textures = (uint32_t)textures.size();
+    textureDesc.clear();
+    for (auto &t : textures) textureDesc.push_back(t.d);
+    d.textures = textureDesc.empty() ? nullptr : textureDesc.data();
+    d.n_tex_texels = (uint32_t)texTexels.size();
+    d.tex_texels = texTexels.empty() ? nullptr : texTexels.data();
+    d.tri_uv = triUv.empty() ? nullptr : triUv.data();
+    d.tri_dpdv = triDpdv.empty() ? nullptr : triDpdv.data();
     d.n_rects = (uint32_t)rectDesc.size();
     d.rects = rectDesc.data();
     d.n_shapes = (uint32_t)shapeDesc.size();

@@ -65,6 +65,13 @@ void mtsh_scene_render_params(const mtsh_scene *s, mtsg_render_params *p) {
     p->tile_offset = 0;
 }
 
+int mtsh_scene_textures(const mtsh_scene *s, mtsg_texture *out, int capacity) {
+    const mtsh::Scene &sc = *s->scene;
+    const int n = (int)sc.textureDesc.size();
+    for (int i = 0; out && i < n && i < capacity; ++i) out[i] = sc.textureDesc[i];
+    return n;
+}
+
 void mtsh_scene_get_info(const mtsh_scene *s, mtsh_scene_info *out) {
     const mtsh::Scene &sc = *s->scene;
     memset(out, 0, sizeof(*out));
@@ -128,6 +135,42 @@ int mtsh_read_image(const char *path, int *w, int *h, float *rgb, size_t rgb_cap
         std::copy(img.begin(), img.end(), rgb);
     }
     return 0;
+}
+
+int mtsh_texture_image(const char *path, float gamma, int *w, int *h, float *rgb, size_t rgb_capacity) {
+    if (!path || !w || !h) { g_err = "mtsh_texture_image: invalid arguments"; return -1; }
+    try {
+        std::vector<float> img;
+        mtsh::loadTextureImage(path, gamma, *w, *h, img);
+        if (rgb) {
+            if (rgb_capacity < img.size()) { g_err = "mtsh_texture_image: buffer too small"; return -2; }
+            std::copy(img.begin(), img.end(), rgb);
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+int mtsh_build_mipmap(const float *rgb, int w, int h, int filter, int wrap_u, int wrap_v, float max_value,
+                      float max_anisotropy, mtsg_mipmap *mip, float *texels, size_t texel_capacity, size_t *n_texels,
+                      float *average, float *maximum) {
+    if (!rgb || w <= 0 || h <= 0 || !mip || !n_texels) { g_err = "mtsh_build_mipmap: invalid arguments"; return -1; }
+    try {
+        std::vector<float> out;
+        mtsh::buildMipmap(std::vector<float>(rgb, rgb + (size_t)w * h * 3), w, h, filter, wrap_u, wrap_v, max_value,
+                          max_anisotropy, out, *mip, average, maximum);
+        *n_texels = out.size();
+        if (texels) {
+            if (texel_capacity < out.size()) { g_err = "mtsh_build_mipmap: buffer too small"; return -2; }
+            std::copy(out.begin(), out.end(), texels);
+        }
+        return 0;
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
 }
 
 void mtsh_last_error(char *buf, size_t size) {

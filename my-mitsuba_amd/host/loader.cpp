@@ -656,6 +656,7 @@ struct Loader {
     Scene &scene;
     std::map<std::string, std::string> defines;
     std::map<std::string, int> bsdfIds;
+    std::map<std::string, int> textureIds;
     std::map<std::string, ShapeGroup> groups;
     std::map<std::string, int> namedEmitters;
     std::vector<std::string> dirStack;
@@ -864,6 +865,113 @@ struct Loader {
         d.alpha_u = au; d.alpha_v = av;
     }
 
+    // `bitmap` texture (src/textures/bitmap.cpp:179-302, Texture2D(props),
+    // src/librender/texture.cpp:84-98); returns its index in scene.textures
+    int parseTexture(XNode &n) {
+        substAll(n);
+        Properties props;
+        std::vector<XNode *> nested;
+        parseProps(n, props, nested);
+        const std::string type = lower(n.attr("type"));
+        if (type != "bitmap")
+            throw err("line " + std::to_string(n.line) + ": texture plugin \"" + type + "\" is outside this build's scope (only 'bitmap')");
+        if (lower(props.getString("coordinates", "uv")) != "uv") throw err("Only UV coordinates are supported at the moment!");
+        if (!props.getString("channel", "").empty()) throw err("bitmap: the 'channel' parameter is not supported by this build");
+        const std::string file = props.getString("filename", "");
+        if (file.empty()) throw err("bitmap: missing 'filename'");
+        const std::string path = resolve(file);
+        const std::string filterType = lower(props.getString("filterType", "ewa"));
+        int filter;
+        if (filterType == "ewa") filter = MTSG_MIP_EWA;
+        else if (filterType == "bilinear") filter = MTSG_MIP_BILINEAR;
+        else if (filterType == "trilinear") filter = MTSG_MIP_TRILINEAR;
+        else if (filterType == "nearest") filter = MTSG_MIP_NEAREST;
+        else throw err("Unknown filter type '" + filterType + "' -- must be 'ewa', 'trilinear', or 'nearest'!");
+        auto wrap = [&](const std::string &w) {   // bitmap.cpp:324-339
+            if (w == "repeat") return (int)MTSG_WRAP_REPEAT;
+            if (w == "clamp") return (int)MTSG_WRAP_CLAMP;
+            if (w == "mirror") return (int)MTSG_WRAP_MIRROR;
+            if (w == "zero" || w == "black") return (int)MTSG_WRAP_ZERO;
+            if (w == "one" || w == "white") return (int)MTSG_WRAP_ONE;
+            throw err("Unknown wrap mode '" + w + "' -- must be 'repeat', 'clamp', 'black', or 'white'!");
+        };
+        const std::string wrapMode = props.getString("wrapMode", "repeat");
+        const int wrapU = wrap(props.getString("wrapModeU", wrapMode)), wrapV = wrap(props.getString("wrapModeV", wrapMode));
+        const float gamma = props.getFloat("gamma", 0.0f);
+        const float maxAniso = props.getFloat("maxAnisotropy", 20.0f);
+        Texture t;
+        t.id = n.attr("id");
+        mtsg_texture &d = t.d;
+        const float uvscale = props.getFloat("uvscale", 1.0f);
+        d.uv_offset[0] = props.getFloat("uoffset", 0.0f);
+        d.uv_offset[1] = props.getFloat("voffset", 0.0f);
+        d.uv_scale[0] = props.getFloat("uscale", uvscale);
+        d.uv_scale[1] = props.getFloat("vscale", uvscale);
+        d.scale = 1.0f;
+        int w = 0, h = 0;
+        std::vector<float> rgb;
+        loadTextureImage(path, gamma, w, h, rgb);
+        // TMIPMap(bitmap, ..., maxValue = 1) (mipmap.h:155-170)
+        buildMipmap(std::move(rgb), w, h, filter, wrapU, wrapV, 1.0f, maxAniso, scene.texTexels, d.mip, d.average, d.maximum);
+        scene.textures.push_back(t);
+        const int idx = (int)scene.textures.size() - 1;
+        if (!t.id.empty()) textureIds[t.id] = idx;
+        return idx;
+    }
+
+    // A BSDF's spectrum parameter given as a nested texture or a reference
+    // to one: the texture index, or -1 (constant).  Only the parameters the
+    // device evaluates per hit may be textured.
+    int textureParam(std::vector<XNode *> &nested, const std::vector<std::string> &names, const std::string &bsdfType) {
+        int found = -1;
+        for (XNode *c : nested) {
+            substAll(*c);
+            const std::string name = c->attr("name");
+            if (c->tag == "texture" || (c->tag == "ref" && textureIds.count(c->attr("id")))) {
+                bool ok = false;
+                for (auto &nm : names) ok |= nm == name;
+                if (!ok)
+                    throw err("line " + std::to_string(c->line) + ": " + bsdfType + ": a texture for parameter \"" + name +
+                              "\" is outside this build's scope");
+                found = c->tag == "texture" ? parseTexture(*c) : textureIds[c->attr("id")];
+            } else if (c->tag != "bsdf" && c->tag != "ref") {
+                throw err("line " + std::to_string(c->line) + ": unsupported element <" + c->tag + "> inside a BSDF");
+            }
+        }
+        return found;
+    }
+    // Constant or textured reflectance of diffuse / plastic / roughplastic:
+    // ensureEnergyConservation scales a texture by 0.99 / max through a
+    // ScaleTexture (bsdf.cpp:88-113); returns the value used for
+    // getAverage() (the texture's average x scale) and sets d.texture
+    V3 reflectanceParam(Properties &props, std::vector<XNode *> &nested, const std::vector<std::string> &names,
+                        const V3 &constant, const std::string &bsdfType, mtsg_bsdf &d, float &maxOut) {
+        const int tex = textureParam(nested, names, bsdfType);
+        if (tex < 0) {
+            const V3 r = energyConserving(props, constant);
+            maxOut = std::max(r.x, std::max(r.y, r.z));
+            d.texture = 0;
+            return r;
+        }
+        mtsg_texture &t = scene.textures[tex].d;
+        float mx = std::max(t.maximum[0], std::max(t.maximum[1], t.maximum[2]));
+        if (props.getBool("ensureEnergyConservation", true) && mx * t.scale > 1.0f) {
+            // a second BSDF sharing the texture by reference gets its own scaled copy
+            Texture copy = scene.textures[tex];
+            copy.id.clear();
+            copy.d.scale = t.scale * (0.99f * (1.0f / (mx * t.scale)));
+            scene.textures.push_back(copy);
+            return reflectanceTex((int)scene.textures.size() - 1, d, maxOut);
+        }
+        return reflectanceTex(tex, d, maxOut);
+    }
+    V3 reflectanceTex(int tex, mtsg_bsdf &d, float &maxOut) {
+        const mtsg_texture &t = scene.textures[tex].d;
+        d.texture = tex + 1;
+        maxOut = std::max(t.maximum[0], std::max(t.maximum[1], t.maximum[2])) * t.scale;
+        return V3(t.average[0], t.average[1], t.average[2]) * t.scale;
+    }
+
     int parseBsdf(XNode &n) {
         substAll(n);
         Properties props;
@@ -875,15 +983,17 @@ struct Loader {
         mtsg_bsdf &d = b.d;
         if (type == "diffuse") {
             // diffuse.cpp:77-84, configure() keeps the component iff max > 0
-            V3 r = props.getSpectrum(props.has("reflectance") ? "reflectance" : "diffuseReflectance", V3(0.5f));
-            r = energyConserving(props, r);
-            float mx = std::max(r.x, std::max(r.y, r.z));
+            float mx;
+            V3 r = reflectanceParam(props, nested, {"reflectance", "diffuseReflectance"},
+                                    props.getSpectrum(props.has("reflectance") ? "reflectance" : "diffuseReflectance", V3(0.5f)),
+                                    "diffuse", d, mx);
             d.type = MTSG_BSDF_DIFFUSE;
             d.reflectance[0] = r.x; d.reflectance[1] = r.y; d.reflectance[2] = r.z;
             d.smooth = mx > 0;
             d.ref_n_zero = 0;
         } else if (type == "roughconductor") {
             // roughconductor.cpp:168-203
+            textureParam(nested, {}, type);
             V3 spec = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
             conductorIOR(props, d, "roughconductor");
             microfacetProps(props, d);
@@ -893,6 +1003,7 @@ struct Loader {
             d.ref_n_zero = 0;
         } else if (type == "dielectric") {
             // dielectric.cpp:148-170
+            textureParam(nested, {}, type);
             float intIOR = lookupIORProp(props, "intIOR", "bk7");
             float extIOR = lookupIORProp(props, "extIOR", "air");
             if (intIOR < 0 || extIOR < 0) throw err("The interior and exterior indices of refraction must be positive!");
@@ -906,6 +1017,7 @@ struct Loader {
             d.ref_n_zero = 1;    // ETransmission | EBackSide
         } else if (type == "roughdielectric") {
             // roughdielectric.cpp:160-205: microfacet reflection + transmission
+            textureParam(nested, {}, type);
             float intIOR = lookupIORProp(props, "intIOR", "bk7");
             float extIOR = lookupIORProp(props, "extIOR", "air");
             if (intIOR < 0 || extIOR < 0 || intIOR == extIOR)
@@ -921,6 +1033,7 @@ struct Loader {
             d.ref_n_zero = 1;    // ETransmission | EBackSide
         } else if (type == "conductor") {
             // conductor.cpp:98-130: ideal mirror with the exact conductor Fresnel term
+            textureParam(nested, {}, type);
             V3 spec = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
             conductorIOR(props, d, "conductor");
             d.type = MTSG_BSDF_CONDUCTOR;
@@ -933,7 +1046,9 @@ struct Loader {
             float extIOR = lookupIORProp(props, "extIOR", "air");
             if (intIOR < 0 || extIOR < 0) throw err("The interior and exterior indices of refraction must be positive!");
             V3 sr = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
-            V3 dr = energyConserving(props, props.getSpectrum("diffuseReflectance", V3(0.5f)));
+            float dmx;
+            V3 dr = reflectanceParam(props, nested, {"diffuseReflectance"}, props.getSpectrum("diffuseReflectance", V3(0.5f)),
+                                     "plastic", d, dmx);
             d.type = MTSG_BSDF_PLASTIC;
             d.ior_eta = intIOR / extIOR;
             d.ior_inv_eta = 1 / d.ior_eta;
@@ -964,7 +1079,9 @@ struct Loader {
             if (d.alpha_u > alphaMax)
                 throw err("Error: the requested roughness value is out of the supported range");
             V3 sr = energyConserving(props, props.getSpectrum("specularReflectance", V3(1.0f)));
-            V3 dr = energyConserving(props, props.getSpectrum("diffuseReflectance", V3(0.5f)));
+            float dmx;
+            V3 dr = reflectanceParam(props, nested, {"diffuseReflectance"}, props.getSpectrum("diffuseReflectance", V3(0.5f)),
+                                     "roughplastic", d, dmx);
             d.type = MTSG_BSDF_ROUGHPLASTIC;
             d.ior_eta = intIOR / extIOR;
             d.ior_inv_eta = 1 / d.ior_eta;
@@ -1262,6 +1379,8 @@ struct Loader {
                 parseSensor(c);
             } else if (tag == "bsdf") {
                 parseBsdf(c);
+            } else if (tag == "texture") {
+                parseTexture(c);
             } else if (tag == "shape") {
                 std::vector<Mesh> meshes;
                 std::vector<Rect> rects;

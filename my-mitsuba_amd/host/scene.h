@@ -69,6 +69,13 @@ struct Emitter {
     Transform toWorld;
 };
 
+// `bitmap` texture (src/textures/bitmap.cpp): its pyramid lives in
+// Scene::texTexels, the header in desc
+struct Texture {
+    std::string id;
+    mtsg_texture d{};
+};
+
 struct ShapeRef {                    // m_shapes order in the kd-tree
     int type;                        // MTSG_SHAPE_*
     int index;                       // into meshes / rects / instances
@@ -137,6 +144,8 @@ struct Scene {
     std::vector<InstanceDef> instances;
     std::vector<Bsdf> bsdfs;
     std::vector<Emitter> emitters;
+    std::vector<Texture> textures;
+    std::vector<float> texTexels;     // all textures' MIP levels (half-rounded RGB)
     Sensor sensor;
     Film film;
     IntegratorProps integrator;
@@ -149,6 +158,8 @@ struct Scene {
 
     // ---- flattened (filled by finalize()) ----
     std::vector<float> vtxPos, vtxNrm, triDpdu, emitterCdf, emitterTriCdf;
+    std::vector<float> triUv, triDpdv;   // only with textures
+    std::vector<mtsg_texture> textureDesc;
     std::vector<uint32_t> triIdx;
     std::vector<mtsg_rect> rectDesc;
     std::vector<mtsg_shape> shapeDesc;
@@ -177,6 +188,24 @@ extern int g_instancing;         // MTSH_INSTANCING_* of the next load
 void buildEnvmap(const Emitter &e, const float aabbMin[3], const float aabbMax[3], const float camPos[3],
                  std::vector<float> &texels, std::vector<float> &cdfRows, std::vector<float> &cdfCols,
                  std::vector<float> &rowWeights, mtsg_envmap &env);
+
+// MIP pyramids (mipmap.cpp): TMIPMap over a linear float RGB level 0
+// (3 floats per texel, rows top-down); levels are appended to `texels` with
+// offsets relative to its start.  average / maximum: level-0 statistics
+// after clamping negative values (may be null).
+void buildMipmap(std::vector<float> level0, int w, int h, int filter, int wrapU, int wrapV, float maxValue,
+                 float maxAnisotropy, std::vector<float> &texels, mtsg_mipmap &mip, float average[3], float maximum[3]);
+float toHalfAndBack(float f);
+// PNG image: samples (8- or 16-bit) per channel, palette expanded, gamma as
+// Bitmap::readPNG sets it (-1 = sRGB)
+struct PngImage {
+    int width = 0, height = 0, channels = 0, depth = 8;
+    float gamma = -1.0f;
+    std::vector<uint16_t> samples;
+};
+bool readPNG(const std::string &path, PngImage &img, std::string &err);
+// the bitmap plugin's input: linear float RGB, rows top-down
+void loadTextureImage(const std::string &path, float gammaOverride, int &w, int &h, std::vector<float> &rgb);
 
 // Halton / Hammersley tables (qmc.cpp in this directory): the first 1024
 // primes, offsets of each base's digit permutation, and the permutations

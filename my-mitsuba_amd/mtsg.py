@@ -71,6 +71,22 @@ class Stats(C.Structure):
     ]
 
 
+class MipMapHeader(C.Structure):
+    """mtsg_mipmap (include/mtsg.h)."""
+    _fields_ = [
+        ("levels", C.c_int32), ("filter", C.c_int32), ("wrap_u", C.c_int32), ("wrap_v", C.c_int32),
+        ("level_w", C.c_int32 * 24), ("level_h", C.c_int32 * 24), ("level_offset", C.c_uint32 * 24),
+        ("size_ratio_x", C.c_float * 24), ("size_ratio_y", C.c_float * 24),
+        ("max_anisotropy", C.c_float), ("pad", C.c_int32 * 3), ("weight_lut", C.c_float * 64),
+    ]
+
+
+class TextureHeader(C.Structure):
+    """mtsg_texture (include/mtsg.h)."""
+    _fields_ = [("mip", MipMapHeader), ("uv_offset", C.c_float * 2), ("uv_scale", C.c_float * 2), ("scale", C.c_float),
+                ("average", C.c_float * 3), ("maximum", C.c_float * 3), ("pad", C.c_int32 * 3)]
+
+
 class SceneInfo(C.Structure):
     """mtsh_scene_info."""
     _fields_ = [
@@ -92,12 +108,13 @@ DEVICE_SYMBOLS = [
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
-    "mtsg_last_error", "mtsg_env_eval", "mtsg_sampler_draws", "mtsg_debug_wavetimes", "mtsg_debug_stragglers",
+    "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_sampler_draws", "mtsg_debug_wavetimes",
+    "mtsg_debug_stragglers",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
-    "mtsh_read_image", "mtsh_clip_triangle", "mtsh_last_error",
+    "mtsh_read_image", "mtsh_clip_triangle", "mtsh_texture_image", "mtsh_build_mipmap", "mtsh_scene_textures", "mtsh_last_error",
 ]
 PATH_SYMBOLS = [
     "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
@@ -149,6 +166,12 @@ def host_lib() -> C.CDLL:
         lib.mtsh_set_instancing.argtypes = [C.c_int]
         lib.mtsh_read_image.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p, C.c_size_t]
         lib.mtsh_clip_triangle.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.mtsh_scene_textures.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        lib.mtsh_texture_image.argtypes = [C.c_char_p, C.c_float, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p,
+                                           C.c_size_t]
+        lib.mtsh_build_mipmap.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                          C.POINTER(MipMapHeader), C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                          C.c_void_p, C.c_void_p]
         _host = lib
     return _host
 
@@ -183,6 +206,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_trace_shadow.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
         lib.mtsg_render_samples.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
         lib.mtsg_env_eval.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.mtsg_tex_eval.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_sampler_draws.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int, C.c_uint32,
                                            C.c_uint32, C.c_void_p, C.c_void_p]
         lib.mtsg_scene_destroy.argtypes = [C.c_void_p]
@@ -237,6 +261,14 @@ class Scene:
     def border(self) -> int:
         return self.info.border
 
+    def textures(self) -> list:
+        """The scene's bitmap texture headers (TextureHeader)."""
+        lib = host_lib()
+        n = lib.mtsh_scene_textures(self._h, None, 0)
+        arr = (TextureHeader * max(n, 1))()
+        lib.mtsh_scene_textures(self._h, arr, n)
+        return list(arr[:n])
+
     def __del__(self):
         if getattr(self, "_h", None):
             host_lib().mtsh_scene_free(self._h)
@@ -262,6 +294,47 @@ def read_image(path: str) -> np.ndarray:
     if lib.mtsh_read_image(path.encode(), C.byref(w), C.byref(h), _ptr(out), out.size) != 0:
         raise RuntimeError(_err(lib, "mtsh_last_error"))
     return out
+
+
+def texture_image(path: str, gamma: float = 0.0) -> np.ndarray:
+    """The bitmap texture's input as linear float RGB (h, w, 3), rows top-down
+    (PNG / OpenEXR / PFM; gamma != 0 overrides the file's)."""
+    lib = host_lib()
+    w, h = C.c_int(), C.c_int()
+    if lib.mtsh_texture_image(path.encode(), gamma, C.byref(w), C.byref(h), None, 0) != 0:
+        raise RuntimeError(_err(lib, "mtsh_last_error"))
+    out = np.zeros((h.value, w.value, 3), np.float32)
+    if lib.mtsh_texture_image(path.encode(), gamma, C.byref(w), C.byref(h), _ptr(out), out.size) != 0:
+        raise RuntimeError(_err(lib, "mtsh_last_error"))
+    return out
+
+
+MIP_NEAREST, MIP_BILINEAR, MIP_TRILINEAR, MIP_EWA = 0, 1, 2, 3
+WRAP_CLAMP, WRAP_REPEAT, WRAP_MIRROR, WRAP_ZERO, WRAP_ONE = 0, 1, 2, 3, 4
+
+
+def build_mipmap(rgb: np.ndarray, filter: int = MIP_EWA, wrap_u: int = WRAP_REPEAT, wrap_v: int = WRAP_REPEAT,
+                 max_value: float = 1.0, max_anisotropy: float = 20.0):
+    """TMIPMap of a linear RGB image (h, w, 3): (list of (h_l, w_l, 3) levels,
+    header, level-0 average, level-0 maximum)."""
+    lib = host_lib()
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = rgb.shape[:2]
+    hdr = MipMapHeader()
+    n = C.c_size_t()
+    avg = np.zeros(3, np.float32)
+    mx = np.zeros(3, np.float32)
+    args = (_ptr(rgb), w, h, filter, wrap_u, wrap_v, max_value, max_anisotropy, C.byref(hdr))
+    if lib.mtsh_build_mipmap(*args, None, 0, C.byref(n), None, None) != 0:
+        raise RuntimeError(_err(lib, "mtsh_last_error"))
+    tex = np.zeros(n.value, np.float32)
+    if lib.mtsh_build_mipmap(*args, _ptr(tex), tex.size, C.byref(n), _ptr(avg), _ptr(mx)) != 0:
+        raise RuntimeError(_err(lib, "mtsh_last_error"))
+    levels = []
+    for l in range(hdr.levels):
+        lw, lh, off = hdr.level_w[l], hdr.level_h[l], hdr.level_offset[l]
+        levels.append(tex[off:off + lw * lh * 3].reshape(lh, lw, 3))
+    return levels, hdr, avg, mx
 
 
 def write_pfm(path: str, rgb: np.ndarray) -> None:
@@ -332,6 +405,18 @@ class GPUScene:
             ry = np.ascontiguousarray(ry, dtype=np.float32)
             px, py = _ptr(rx), _ptr(ry)
         self._check(device_lib().mtsg_env_eval(self._h, dirs.shape[0], _ptr(dirs), px, py, _ptr(out)), "mtsg_env_eval")
+        return out
+
+    def tex_eval(self, tex: int, uv: np.ndarray, duv: np.ndarray | None = None) -> np.ndarray:
+        """BitmapTexture::eval of texture `tex` at uv (n, 2), filtered with the
+        uv partials duv (n, 4) when given (debug entry point)."""
+        uv = np.ascontiguousarray(uv, dtype=np.float32)
+        out = np.empty((uv.shape[0], 3), np.float32)
+        pd = None
+        if duv is not None:
+            duv = np.ascontiguousarray(duv, dtype=np.float32)
+            pd = _ptr(duv)
+        self._check(device_lib().mtsg_tex_eval(self._h, tex, uv.shape[0], _ptr(uv), pd, _ptr(out)), "mtsg_tex_eval")
         return out
 
     def sampler_draws(self, params: RenderParams, x: int, y: int, s: int, kinds) -> np.ndarray:

@@ -651,13 +651,138 @@ struct Counters {
 };
 
 // ---------------------------------------------------------------------------
+// TMIPMap lookups (include/mitsuba/render/mipmap.h:498-840) over a pyramid
+// built by the host library (mtsg_mipmap + half-rounded RGB texels): the
+// environment map and the bitmap textures
+// ---------------------------------------------------------------------------
+struct MipMap {
+    const mtsg_mipmap &M;
+    const float *texels;
+    static int modulo(int a, int b) { int r = a % b; return r < 0 ? r + b : r; }   // math::modulo
+    static float log2f_m(float v) {   // math.cpp:103-106
+        const float invLn2 = 1.0f / std::log(2.0f);
+        return (float)std::log((double)v) * invLn2;
+    }
+    // one boundary condition of evalTexel (mipmap.h:503-562); false: the
+    // constant `c` (EZero / EOne) replaces the texel
+    static bool wrap(int mode, int &x, int n, float &c) {
+        if (x >= 0 && x < n) return true;
+        switch (mode) {
+            case MTSG_WRAP_REPEAT: x = modulo(x, n); return true;
+            case MTSG_WRAP_CLAMP: x = std::min(std::max(x, 0), n - 1); return true;
+            case MTSG_WRAP_MIRROR:
+                x = modulo(x, 2 * n);
+                if (x >= n) x = 2 * n - x - 1;
+                return true;
+            case MTSG_WRAP_ZERO: c = 0.0f; return false;
+            default: c = 1.0f; return false;
+        }
+    }
+    Spec texel(int level, int x, int y) const {
+        const int w = M.level_w[level], h = M.level_h[level];
+        float c;
+        if (!wrap(M.wrap_u, x, w, c)) return Spec(c);
+        if (!wrap(M.wrap_v, y, h, c)) return Spec(c);
+        return Spec::of(texels + M.level_offset[level] + 3 * ((size_t)y * w + x));
+    }
+    Spec box(int level, float u, float v) const {   // mipmap.h:566-569
+        return texel(level, (int)std::floor(u * M.level_w[level]), (int)std::floor(v * M.level_h[level]));
+    }
+    Spec bilinear(int level, float ux, float uy) const {   // mipmap.h:575-596
+        if (!std::isfinite(ux) || !std::isfinite(uy)) return Spec(0.0f);
+        if (level >= M.levels) return box(M.levels - 1, ux, uy);
+        const float u = ux * M.level_w[level] - 0.5f, v = uy * M.level_h[level] - 0.5f;
+        const int xPos = (int)std::floor(u), yPos = (int)std::floor(v);
+        const float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
+        return texel(level, xPos, yPos) * dx2 * dy2 + texel(level, xPos, yPos + 1) * dx2 * dy1 +
+               texel(level, xPos + 1, yPos) * dx1 * dy2 + texel(level, xPos + 1, yPos + 1) * dx1 * dy1;
+    }
+    Spec ewa(int level, float ux, float uy, float A, float B, float C) const {   // mipmap.h:775-840
+        if (!std::isfinite(A + B + C + ux + uy)) return Spec(0.0f);
+        if (level >= M.levels) return box(M.levels - 1, ux, uy);
+        const float u = ux * M.level_w[level] - 0.5f, v = uy * M.level_h[level] - 0.5f;
+        const float rx = M.size_ratio_x[level], ry = M.size_ratio_y[level];
+        A /= rx * rx;
+        B /= rx * ry;
+        C /= ry * ry;
+        const float invDet = 1.0f / (-B * B + 4.0f * A * C), deltaU = 2.0f * std::sqrt(C * invDet),
+                    deltaV = 2.0f * std::sqrt(A * invDet);
+        const int u0 = (int)std::ceil(u - deltaU), u1 = (int)std::floor(u + deltaU);
+        const int v0 = (int)std::ceil(v - deltaV), v1 = (int)std::floor(v + deltaV);
+        const float As = A * MTSG_MIPMAP_LUT_SIZE, Bs = B * MTSG_MIPMAP_LUT_SIZE, Cs = C * MTSG_MIPMAP_LUT_SIZE;
+        Spec result(0.0f);
+        float denominator = 0.0f;
+        const float ddq = 2 * As, uu0 = (float)u0 - u;
+        for (int vt = v0; vt <= v1; ++vt) {
+            const float vv = (float)vt - v;
+            float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
+            float dq = As * (2 * uu0 + 1) + Bs * vv;
+            for (int ut = u0; ut <= u1; ++ut) {
+                if (q < (float)MTSG_MIPMAP_LUT_SIZE) {
+                    const uint32_t qi = (uint32_t)q;
+                    if (qi < MTSG_MIPMAP_LUT_SIZE) {
+                        const float weight = M.weight_lut[(int)q];
+                        result += texel(level, ut, vt) * weight;
+                        denominator += weight;
+                    }
+                }
+                q += dq;
+                dq += ddq;
+            }
+        }
+        if (denominator == 0) return bilinear(level, ux, uy);
+        return result / denominator;
+    }
+    // TMIPMap::eval(uv, d0, d1) (mipmap.h:633-722)
+    Spec filtered(float ux, float uy, float d0x, float d0y, float d1x, float d1y) const {
+        if (M.filter == MTSG_MIP_NEAREST) return box(0, ux, uy);
+        if (M.filter == MTSG_MIP_BILINEAR) return bilinear(0, ux, uy);
+        const float du0 = d0x * M.level_w[0], dv0 = d0y * M.level_h[0], du1 = d1x * M.level_w[0], dv1 = d1y * M.level_h[0];
+        float A = dv0 * dv0 + dv1 * dv1, B = -2.0f * (du0 * dv0 + du1 * dv1), C = du0 * du0 + du1 * du1,
+              F = A * C - B * B * 0.25f;
+        const float root = hypot2(A - C, B), Aprime = 0.5f * (A + C - root), Cprime = 0.5f * (A + C + root);
+        float majorRadius = Aprime != 0 ? std::sqrt(F / Aprime) : 0, minorRadius = Cprime != 0 ? std::sqrt(F / Cprime) : 0;
+        if (M.filter == MTSG_MIP_TRILINEAR || !(minorRadius > 0) || !(majorRadius > 0) || F < 0) {
+            const float level = log2f_m(std::max(majorRadius, kEpsilon));
+            const int ilevel = (int)std::floor(level);
+            if (ilevel < 0) return bilinear(0, ux, uy);
+            const float a = level - ilevel;
+            return bilinear(ilevel, ux, uy) * (1.0f - a) + bilinear(ilevel + 1, ux, uy) * a;
+        }
+        if (minorRadius * M.max_anisotropy < majorRadius) {
+            minorRadius = majorRadius / M.max_anisotropy;
+            const float theta = 0.5f * std::atan(B / (A - C));
+            const float sinTheta = std::sin(theta), cosTheta = std::cos(theta);
+            const float a2 = majorRadius * majorRadius, b2 = minorRadius * minorRadius, sinTheta2 = sinTheta * sinTheta,
+                        cosTheta2 = cosTheta * cosTheta, sin2Theta = 2 * sinTheta * cosTheta;
+            A = a2 * cosTheta2 + b2 * sinTheta2;
+            B = (a2 - b2) * sin2Theta;
+            C = a2 * sinTheta2 + b2 * cosTheta2;
+            F = a2 * b2;
+        }
+        const float scale = 1.0f / F;
+        A *= scale; B *= scale; C *= scale;
+        const float level = std::max(0.0f, log2f_m(minorRadius));
+        const int ilevel = (int)level;
+        const float a = level - ilevel;
+        if (majorRadius < 1 || !(A > 0 && C > 0)) return bilinear(ilevel, ux, uy);
+        return ewa(ilevel, ux, uy, A, B, C) * (1.0f - a) + ewa(ilevel + 1, ux, uy, A, B, C) * a;
+    }
+    // BitmapTexture::eval(uv) (bitmap.cpp:431-454): no partials
+    Spec unfiltered(float ux, float uy) const {
+        return M.filter == MTSG_MIP_NEAREST ? box(0, ux, uy) : bilinear(0, ux, uy);
+    }
+};
+
+// ---------------------------------------------------------------------------
 // Scene view over the flat descriptor
 // ---------------------------------------------------------------------------
 struct Its {
     float t = std::numeric_limits<float>::infinity();
     Vec p;
     Frame geoFrame, shFrame;
-    Vec dpdu, wi;
+    Vec dpdu, dpdv, wi;
+    float u = 0, v = 0;              // its.uv
     int shape = -1;
     bool valid() const { return t != std::numeric_limits<float>::infinity(); }
     Vec toLocal(const Vec &v) const { return shFrame.toLocal(v); }
@@ -903,6 +1028,17 @@ struct SceneView {
             float len = length(faceNormal);
             if (!(faceNormal.x == 0 && faceNormal.y == 0 && faceNormal.z == 0)) faceNormal = faceNormal / len;
             its.dpdu = Vec(d.tri_dpdu[3 * g], d.tri_dpdu[3 * g + 1], d.tri_dpdu[3 * g + 2]);
+            // UV tangent dpdv or side2; uv interpolated from the vertices' texture
+            // coordinates, Point2(b.y, b.z) without them (skdtree.h:373-405)
+            its.dpdv = d.tri_dpdv ? Vec(d.tri_dpdv[3 * g], d.tri_dpdv[3 * g + 1], d.tri_dpdv[3 * g + 2]) : side2;
+            if (d.tri_uv) {
+                const float *t = d.tri_uv + 6 * (size_t)g;
+                its.u = t[0] * bx + t[2] * by + t[4] * bz;
+                its.v = t[1] * bx + t[3] * by + t[5] * bz;
+            } else {
+                its.u = by;
+                its.v = bz;
+            }
             if (!sh.face_normals) {
                 const Vec n0 = nrm(i0), n1 = nrm(i1), n2 = nrm(i2);
                 its.shFrame.n = normalize(n0 * bx + n1 * by + n2 * bz);
@@ -919,6 +1055,9 @@ struct SceneView {
             its.geoFrame.n = Vec(r.frame_n[0], r.frame_n[1], r.frame_n[2]);
             its.shFrame.n = its.geoFrame.n;
             its.dpdu = Vec(r.dpdu[0], r.dpdu[1], r.dpdu[2]);
+            its.dpdv = Vec(r.dpdv[0], r.dpdv[1], r.dpdv[2]);
+            its.u = 0.5f * (c.rx + 1);
+            its.v = 0.5f * (c.ry + 1);
             its.p = ray(its.t);
         }
     }
@@ -945,6 +1084,9 @@ struct SceneView {
             its.dpdu = Vec(W[0] * its.dpdu.x + W[1] * its.dpdu.y + W[2] * its.dpdu.z,
                            W[4] * its.dpdu.x + W[5] * its.dpdu.y + W[6] * its.dpdu.z,
                            W[8] * its.dpdu.x + W[9] * its.dpdu.y + W[10] * its.dpdu.z);
+            its.dpdv = Vec(W[0] * its.dpdv.x + W[1] * its.dpdv.y + W[2] * its.dpdv.z,
+                           W[4] * its.dpdv.x + W[5] * its.dpdv.y + W[6] * its.dpdv.z,
+                           W[8] * its.dpdv.x + W[9] * its.dpdv.y + W[10] * its.dpdv.z);
             its.p = Vec(W[0] * its.p.x + W[1] * its.p.y + W[2] * its.p.z + W[3],
                         W[4] * its.p.x + W[5] * its.p.y + W[6] * its.p.z + W[7],
                         W[8] * its.p.x + W[9] * its.p.y + W[10] * its.p.z + W[11]);
@@ -1061,105 +1203,52 @@ struct SceneView {
     // ------------------------------------------------------------------
     // EnvironmentMap (src/emitters/envmap.cpp) over TMIPMap (mipmap.h)
     // ------------------------------------------------------------------
-    static int modulo(int a, int b) { int r = a % b; return r < 0 ? r + b : r; }
-    static float log2f_m(float v) {   // math.cpp:103-106
-        const float invLn2 = 1.0f / std::log(2.0f);
-        return (float)std::log((double)v) * invLn2;
+    MipMap envMip() const { return MipMap{d.envmap.mip, d.env_texels}; }   // u repeats, v clamps
+
+    // Intersection::computePartials (src/librender/intersection.cpp:5-80) for
+    // a camera ray with (scaled) differentials rxD / ryD from origin o
+    // (rxOrigin = ryOrigin = o for the perspective camera)
+    static void computePartials(const Its &its, const Vec &o, const Vec &rxD, const Vec &ryD, float &dudx, float &dvdx,
+                                float &dudy, float &dvdy) {
+        dudx = dvdx = dudy = dvdy = 0.0f;
+        const auto isZero = [](const Vec &v) { return v.x == 0 && v.y == 0 && v.z == 0; };
+        if (isZero(its.dpdu) && isZero(its.dpdv)) return;
+        const Vec &n = its.geoFrame.n;
+        const float pp = dot(n, its.p), pox = dot(n, o), poy = dot(n, o), prx = dot(n, rxD), pry = dot(n, ryD);
+        if (prx == 0 || pry == 0) return;
+        const float tx = (pp - pox) / prx, ty = (pp - poy) / pry;
+        const float absX = std::abs(n.x), absY = std::abs(n.y), absZ = std::abs(n.z);
+        int axes[2];
+        if (absX > absY && absX > absZ) { axes[0] = 1; axes[1] = 2; }
+        else if (absY > absZ) { axes[0] = 0; axes[1] = 2; }
+        else { axes[0] = 0; axes[1] = 1; }
+        float A[2][2], Bx[2], By[2], x[2];
+        A[0][0] = its.dpdu[axes[0]]; A[0][1] = its.dpdv[axes[0]];
+        A[1][0] = its.dpdu[axes[1]]; A[1][1] = its.dpdv[axes[1]];
+        const Vec px = o + rxD * tx, py = o + ryD * ty;
+        Bx[0] = px[axes[0]] - its.p[axes[0]]; Bx[1] = px[axes[1]] - its.p[axes[1]];
+        By[0] = py[axes[0]] - its.p[axes[0]]; By[1] = py[axes[1]] - its.p[axes[1]];
+        // solveLinearSystem2x2 (src/libcore/util.cpp:527-539)
+        auto solve = [&](const float b[2]) {
+            const float det = A[0][0] * A[1][1] - A[0][1] * A[1][0];
+            if (std::abs(det) <= 0x1p-128f) return false;   // RCPOVERFLOW
+            const float inverse = 1.0f / det;
+            x[0] = (A[1][1] * b[0] - A[0][1] * b[1]) * inverse;
+            x[1] = (A[0][0] * b[1] - A[1][0] * b[0]) * inverse;
+            return true;
+        };
+        if (solve(Bx)) { dudx = x[0]; dvdx = x[1]; }
+        else { dudx = 1; dvdx = 0; }
+        if (solve(By)) { dudy = x[0]; dvdy = x[1]; }
+        else { dudy = 1; dvdy = 0; }   // the reference sets dudy twice and leaves dvdy unset
     }
-    // TMIPMap::evalTexel (mipmap.h:503-562): u repeats, v clamps
-    Spec envTexel(int level, int x, int y) const {
-        const mtsg_envmap &E = d.envmap;
-        const int w = E.level_w[level], h = E.level_h[level];
-        if (x < 0 || x >= w) x = modulo(x, w);
-        if (y < 0 || y >= h) y = std::min(std::max(y, 0), h - 1);
-        const float *t = d.env_texels + E.level_offset[level] + 3 * ((size_t)y * w + x);
-        return Spec::of(t);
-    }
-    Spec envBox(int level, float u, float v) const {   // mipmap.h:566-569
-        const mtsg_envmap &E = d.envmap;
-        return envTexel(level, (int)std::floor(u * E.level_w[level]), (int)std::floor(v * E.level_h[level]));
-    }
-    Spec envBilinear(int level, float ux, float uy) const {   // mipmap.h:575-596
-        const mtsg_envmap &E = d.envmap;
-        if (!std::isfinite(ux) || !std::isfinite(uy)) return Spec(0.0f);
-        if (level >= E.levels) return envBox(E.levels - 1, ux, uy);
-        const float u = ux * E.level_w[level] - 0.5f, v = uy * E.level_h[level] - 0.5f;
-        const int xPos = (int)std::floor(u), yPos = (int)std::floor(v);
-        const float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
-        return envTexel(level, xPos, yPos) * dx2 * dy2 + envTexel(level, xPos, yPos + 1) * dx2 * dy1 +
-               envTexel(level, xPos + 1, yPos) * dx1 * dy2 + envTexel(level, xPos + 1, yPos + 1) * dx1 * dy1;
-    }
-    Spec envEWA(int level, float ux, float uy, float A, float B, float C) const {   // mipmap.h:775-840
-        const mtsg_envmap &E = d.envmap;
-        if (!std::isfinite(A + B + C + ux + uy)) return Spec(0.0f);
-        if (level >= E.levels) return envBox(E.levels - 1, ux, uy);
-        const float u = ux * E.level_w[level] - 0.5f, v = uy * E.level_h[level] - 0.5f;
-        const float rx = E.size_ratio_x[level], ry = E.size_ratio_y[level];
-        A /= rx * rx;
-        B /= rx * ry;
-        C /= ry * ry;
-        const float invDet = 1.0f / (-B * B + 4.0f * A * C), deltaU = 2.0f * std::sqrt(C * invDet),
-                    deltaV = 2.0f * std::sqrt(A * invDet);
-        const int u0 = (int)std::ceil(u - deltaU), u1 = (int)std::floor(u + deltaU);
-        const int v0 = (int)std::ceil(v - deltaV), v1 = (int)std::floor(v + deltaV);
-        const float As = A * MTSG_MIPMAP_LUT_SIZE, Bs = B * MTSG_MIPMAP_LUT_SIZE, Cs = C * MTSG_MIPMAP_LUT_SIZE;
-        Spec result(0.0f);
-        float denominator = 0.0f;
-        const float ddq = 2 * As, uu0 = (float)u0 - u;
-        for (int vt = v0; vt <= v1; ++vt) {
-            const float vv = (float)vt - v;
-            float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
-            float dq = As * (2 * uu0 + 1) + Bs * vv;
-            for (int ut = u0; ut <= u1; ++ut) {
-                if (q < (float)MTSG_MIPMAP_LUT_SIZE) {
-                    const uint32_t qi = (uint32_t)q;
-                    if (qi < MTSG_MIPMAP_LUT_SIZE) {
-                        const float weight = E.weight_lut[(int)q];
-                        result += envTexel(level, ut, vt) * weight;
-                        denominator += weight;
-                    }
-                }
-                q += dq;
-                dq += ddq;
-            }
-        }
-        if (denominator == 0) return envBilinear(level, ux, uy);
-        return result / denominator;
-    }
-    // TMIPMap::eval (mipmap.h:633-722), filter type EWA
-    Spec envFiltered(float ux, float uy, float d0x, float d0y, float d1x, float d1y) const {
-        const mtsg_envmap &E = d.envmap;
-        const float du0 = d0x * E.level_w[0], dv0 = d0y * E.level_h[0], du1 = d1x * E.level_w[0], dv1 = d1y * E.level_h[0];
-        float A = dv0 * dv0 + dv1 * dv1, B = -2.0f * (du0 * dv0 + du1 * dv1), C = du0 * du0 + du1 * du1,
-              F = A * C - B * B * 0.25f;
-        const float root = hypot2(A - C, B), Aprime = 0.5f * (A + C - root), Cprime = 0.5f * (A + C + root);
-        float majorRadius = Aprime != 0 ? std::sqrt(F / Aprime) : 0, minorRadius = Cprime != 0 ? std::sqrt(F / Cprime) : 0;
-        if (!(minorRadius > 0) || !(majorRadius > 0) || F < 0) {
-            const float level = log2f_m(std::max(majorRadius, kEpsilon));
-            const int ilevel = (int)std::floor(level);
-            if (ilevel < 0) return envBilinear(0, ux, uy);
-            const float a = level - ilevel;
-            return envBilinear(ilevel, ux, uy) * (1.0f - a) + envBilinear(ilevel + 1, ux, uy) * a;
-        }
-        if (minorRadius * E.max_anisotropy < majorRadius) {
-            minorRadius = majorRadius / E.max_anisotropy;
-            const float theta = 0.5f * std::atan(B / (A - C));
-            const float sinTheta = std::sin(theta), cosTheta = std::cos(theta);
-            const float a2 = majorRadius * majorRadius, b2 = minorRadius * minorRadius, sinTheta2 = sinTheta * sinTheta,
-                        cosTheta2 = cosTheta * cosTheta, sin2Theta = 2 * sinTheta * cosTheta;
-            A = a2 * cosTheta2 + b2 * sinTheta2;
-            B = (a2 - b2) * sin2Theta;
-            C = a2 * sinTheta2 + b2 * cosTheta2;
-            F = a2 * b2;
-        }
-        const float scale = 1.0f / F;
-        A *= scale; B *= scale; C *= scale;
-        const float level = std::max(0.0f, log2f_m(minorRadius));
-        const int ilevel = (int)level;
-        const float a = level - ilevel;
-        if (majorRadius < 1 || !(A > 0 && C > 0)) return envBilinear(ilevel, ux, uy);
-        return envEWA(ilevel, ux, uy, A, B, C) * (1.0f - a) + envEWA(ilevel + 1, ux, uy, A, B, C) * a;
-    }
+
+    // The reflectance a BSDF record sees at a hit: its constant, or its bitmap
+    // texture through Texture2D::eval(its) (texture.cpp:112-121) -> the
+    // filtered lookup with UV partials when the ray carries differentials (the
+    // camera ray, records.inl:69-75), BitmapTexture::eval(uv) otherwise
+    // (bitmap.cpp:431-499) -> times the ScaleTexture of ensureEnergyConservation
+    Spec reflectance(const mtsg_bsdf &b, const Its &its, const Vec &rayO, const struct RayDiff *diff) const;
     Vec envToLocal(const Vec &v) const {
         const float *m = d.envmap.to_local;
         return Vec(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z, m[6] * v.x + m[7] * v.y + m[8] * v.z);
@@ -1174,12 +1263,12 @@ struct SceneView {
         const float ux = std::atan2(v.x, -v.z) * kInvTwoPi, uy = std::acos(std::min(1.0f, std::max(-1.0f, v.y))) * kInvPi;
         Spec value;
         if (!hasDiff) {
-            value = envBilinear(0, ux, uy);
+            value = envMip().bilinear(0, ux, uy);
         } else {
             const Vec dvdx = envToLocal(rxD) - v, dvdy = envToLocal(ryD) - v;
             const float t1 = kInvTwoPi / (v.x * v.x + v.z * v.z),
                         t2 = -kInvPi / std::max(safe_sqrt(1.0f - v.y * v.y), kEpsilon);
-            value = envFiltered(ux, uy, t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y, t1 * (dvdy.z * v.x - dvdy.x * v.z),
+            value = envMip().filtered(ux, uy, t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y, t1 * (dvdy.z * v.x - dvdy.x * v.z),
                                 t2 * dvdy.y);
         }
         return value * d.envmap.scale;
@@ -1200,14 +1289,15 @@ struct SceneView {
     // envmap.cpp:574-600
     void envInternalSample(float sx, float sy, Vec &dOut, Spec &value, float &pdf) const {
         const mtsg_envmap &E = d.envmap;
-        const int W = E.level_w[0], H = E.level_h[0];
+        const int W = E.mip.level_w[0], H = E.mip.level_h[0];
+        const MipMap M = envMip();
         const uint32_t row = envSampleReuse(d.env_cdf_rows, H, sy);
         const uint32_t col = envSampleReuse(d.env_cdf_cols + row * (W + 1), W, sx);
         const float px = (float)col + intervalToTent(sx), py = (float)row + intervalToTent(sy);
         const int xPos = (int)std::floor(px), yPos = (int)std::floor(py);
         const float dx1 = px - xPos, dx2 = 1.0f - dx1, dy1 = py - yPos, dy2 = 1.0f - dy1;
-        const Spec value1 = envTexel(0, xPos, yPos) * dx2 * dy2 + envTexel(0, xPos + 1, yPos) * dx1 * dy2;
-        const Spec value2 = envTexel(0, xPos, yPos + 1) * dx2 * dy1 + envTexel(0, xPos + 1, yPos + 1) * dx1 * dy1;
+        const Spec value1 = M.texel(0, xPos, yPos) * dx2 * dy2 + M.texel(0, xPos + 1, yPos) * dx1 * dy2;
+        const Spec value2 = M.texel(0, xPos, yPos + 1) * dx2 * dy1 + M.texel(0, xPos + 1, yPos + 1) * dx1 * dy1;
         value = (value1 + value2) * E.scale;
         pdf = (value1.luminance() * d.env_row_weights[std::min(std::max(yPos, 0), H - 1)] +
                value2.luminance() * d.env_row_weights[std::min(std::max(yPos + 1, 0), H - 1)]) * E.normalization;
@@ -1219,14 +1309,15 @@ struct SceneView {
     // envmap.cpp:603-633
     float envInternalPdf(const Vec &dl) const {
         const mtsg_envmap &E = d.envmap;
-        const int W = E.level_w[0], H = E.level_h[0];
+        const int W = E.mip.level_w[0], H = E.mip.level_h[0];
+        const MipMap M = envMip();
         const float ux = std::atan2(dl.x, -dl.z) * kInvTwoPi, uy = std::acos(std::min(1.0f, std::max(-1.0f, dl.y))) * kInvPi;
         if (!std::isfinite(ux) || !std::isfinite(uy)) return 0.0f;
         const float u = ux * W - 0.5f, v = uy * H - 0.5f;
         const int xPos = (int)std::floor(u), yPos = (int)std::floor(v);
         const float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
-        const Spec value1 = envTexel(0, xPos, yPos) * dx2 * dy2 + envTexel(0, xPos + 1, yPos) * dx1 * dy2;
-        const Spec value2 = envTexel(0, xPos, yPos + 1) * dx2 * dy1 + envTexel(0, xPos + 1, yPos + 1) * dx1 * dy1;
+        const Spec value1 = M.texel(0, xPos, yPos) * dx2 * dy2 + M.texel(0, xPos + 1, yPos) * dx1 * dy2;
+        const Spec value2 = M.texel(0, xPos, yPos + 1) * dx2 * dy1 + M.texel(0, xPos + 1, yPos + 1) * dx1 * dy1;
         const float sinTheta = safe_sqrt(1 - dl.y * dl.y);
         return (value1.luminance() * d.env_row_weights[std::min(std::max(yPos, 0), H - 1)] +
                 value2.luminance() * d.env_row_weights[std::min(std::max(yPos + 1, 0), H - 1)]) *
@@ -1584,8 +1675,7 @@ float fresnelDielectricExt1(float cosThetaI, float eta) {
 // SmoothPlastic (plastic.cpp:93-140): m_invEta2, the internal-reflection
 // renormalised diffuse base and the Fresnel-steered specular probability
 inline float plasticInvEta2(const mtsg_bsdf &b) { return 1 / (b.ior_eta * b.ior_eta); }
-Spec plasticDiffuse(const mtsg_bsdf &b) {
-    Spec diff = Spec::of(b.reflectance);
+Spec plasticDiffuse(const mtsg_bsdf &b, Spec diff) {
     if (b.nonlinear) return diff / (Spec(1.0f) - diff * b.fdr_int);
     return diff / (1 - b.fdr_int);
 }
@@ -1615,7 +1705,7 @@ float roughTransmittance(const mtsg_bsdf &b, float cosTheta) {
     return std::min(1.0f, std::max(0.0f, result));
 }
 // RoughPlastic::eval / pdf (roughplastic.cpp:302-385), both components
-Spec roughPlasticEval(const mtsg_bsdf &b, const BRec &r) {
+Spec roughPlasticEval(const mtsg_bsdf &b, const Spec &alb, const BRec &r) {
     if (cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return Spec(0.0f);
     Microfacet distr = mfOf(b);
     Spec result(0.0f);
@@ -1626,7 +1716,7 @@ Spec roughPlasticEval(const mtsg_bsdf &b, const BRec &r) {
     float value = F * D * G / (4.0f * cosTheta(r.wi));
     result += Spec::of(b.spec_refl) * value;
     float T12 = roughTransmittance(b, cosTheta(r.wi)), T21 = roughTransmittance(b, cosTheta(r.wo));
-    result += plasticDiffuse(b) * (kInvPi * cosTheta(r.wo) * T12 * T21 * plasticInvEta2(b));
+    result += plasticDiffuse(b, alb) * (kInvPi * cosTheta(r.wo) * T12 * T21 * plasticInvEta2(b));
     return result;
 }
 float roughPlasticPdf(const mtsg_bsdf &b, const BRec &r) {
@@ -1645,10 +1735,12 @@ float roughPlasticPdf(const mtsg_bsdf &b, const BRec &r) {
 
 // BSDF::eval (measure = ESolidAngle for smooth BSDFs; dielectric only
 // evaluates EDiscrete, so it returns 0 here: dielectric.cpp:228-250)
-Spec bsdfEval(const mtsg_bsdf &b, const BRec &r) {
+// alb: the record's `reflectance` / `diffuseReflectance` at the hit (the
+// constant, or its texture's value: SceneView::reflectance)
+Spec bsdfEval(const mtsg_bsdf &b, const Spec &alb, const BRec &r) {
     if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:107-116
         if (!b.smooth || cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return Spec(0.0f);
-        return Spec::of(b.reflectance) * (kInvPi * cosTheta(r.wo));
+        return alb * (kInvPi * cosTheta(r.wo));
     }
     if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:235-268
         if (cosTheta(r.wi) <= 0 || cosTheta(r.wo) <= 0) return Spec(0.0f);
@@ -1691,9 +1783,9 @@ Spec bsdfEval(const mtsg_bsdf &b, const BRec &r) {
         if (cosTheta(r.wo) <= 0 || cosTheta(r.wi) <= 0) return Spec(0.0f);
         float Fi = fresnelDielectricExt1(cosTheta(r.wi), b.ior_eta);
         float Fo = fresnelDielectricExt1(cosTheta(r.wo), b.ior_eta);
-        return plasticDiffuse(b) * (kInvPi * cosTheta(r.wo) * plasticInvEta2(b) * (1 - Fi) * (1 - Fo));
+        return plasticDiffuse(b, alb) * (kInvPi * cosTheta(r.wo) * plasticInvEta2(b) * (1 - Fi) * (1 - Fo));
     }
-    if (b.type == MTSG_BSDF_ROUGHPLASTIC) return roughPlasticEval(b, r);
+    if (b.type == MTSG_BSDF_ROUGHPLASTIC) return roughPlasticEval(b, alb, r);
     return Spec(0.0f);   // dielectric / conductor: delta components only (EDiscrete)
 }
 
@@ -1742,14 +1834,14 @@ float bsdfPdf(const mtsg_bsdf &b, const BRec &r) {
 // BSDF::sample(bRec, pdf, sample); next1d: bRec.sampler->next1D(), drawn
 // only where the reference draws it (roughdielectric.cpp:531-539)
 template <class Next1D>
-Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy, Next1D &&next1d) {
+Spec bsdfSample(const mtsg_bsdf &b, const Spec &alb, BRec &r, float &pdf, float sx, float sy, Next1D &&next1d) {
     if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
         if (cosTheta(r.wi) <= 0) return Spec(0.0f);
         r.wo = squareToCosineHemisphere(sx, sy);
         r.eta = 1.0f;
         r.sampledType = EDiffuseReflection;
         pdf = kInvPi * cosTheta(r.wo);
-        return Spec::of(b.reflectance);
+        return alb;
     }
     if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:345-394
         if (cosTheta(r.wi) < 0) return Spec(0.0f);
@@ -1860,7 +1952,7 @@ Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy, Nex
         r.eta = 1.0f;
         pdf = roughPlasticPdf(b, r);
         if (pdf == 0) return Spec(0.0f);
-        return roughPlasticEval(b, r) / pdf;
+        return roughPlasticEval(b, alb, r) / pdf;
     }
     if (b.type == MTSG_BSDF_PLASTIC) {   // plastic.cpp:344-390 (both components)
         if (cosTheta(r.wi) <= 0) return Spec(0.0f);
@@ -1877,7 +1969,7 @@ Spec bsdfSample(const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy, Nex
         r.wo = squareToCosineHemisphere((sx - probSpecular) / (1 - probSpecular), sy);
         float Fo = fresnelDielectricExt1(cosTheta(r.wo), b.ior_eta);
         pdf = (1 - probSpecular) * (kInvPi * cosTheta(r.wo));
-        return plasticDiffuse(b) * (plasticInvEta2(b) * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
+        return plasticDiffuse(b, alb) * (plasticInvEta2(b) * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
     }
     return Spec(0.0f);
 }
@@ -1891,19 +1983,21 @@ const mtsg_bsdf &bsdfSide(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec &r, boo
     if (!sampling) r.wo.z *= -1;
     return all[b.back];
 }
-Spec bsdfEvalTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec r) {
+template <class Alb>
+Spec bsdfEvalTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec r, Alb &&alb) {
     bool f;
-    return bsdfEval(bsdfSide(all, b, r, false, f), r);
+    const mtsg_bsdf &nb = bsdfSide(all, b, r, false, f);
+    return bsdfEval(nb, alb(nb), r);
 }
 float bsdfPdfTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec r) {
     bool f;
     return bsdfPdf(bsdfSide(all, b, r, false, f), r);
 }
-template <class Next1D>
-Spec bsdfSampleTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy, Next1D &&next1d) {
+template <class Next1D, class Alb>
+Spec bsdfSampleTS(const mtsg_bsdf *all, const mtsg_bsdf &b, BRec &r, float &pdf, float sx, float sy, Next1D &&next1d, Alb &&alb) {
     bool flipped;
     const mtsg_bsdf &nb = bsdfSide(all, b, r, true, flipped);
-    Spec result = bsdfSample(nb, r, pdf, sx, sy, next1d);
+    Spec result = bsdfSample(nb, alb(nb), r, pdf, sx, sy, next1d);
     if (flipped) {
         r.wi.z *= -1;
         if (!result.isZero() && pdf != 0) r.wo.z *= -1;
@@ -1938,6 +2032,22 @@ struct RayDiff {
     Vec rx, ry;
 };
 
+Spec SceneView::reflectance(const mtsg_bsdf &b, const Its &its, const Vec &rayO, const RayDiff *diff) const {
+    if (!b.texture) return Spec::of(b.reflectance);
+    const mtsg_texture &T = d.textures[b.texture - 1];
+    const MipMap M{T.mip, d.tex_texels};
+    const float u = its.u * T.uv_scale[0] + T.uv_offset[0], v = its.v * T.uv_scale[1] + T.uv_offset[1];
+    Spec value;
+    if (diff && diff->has) {
+        float dudx, dvdx, dudy, dvdy;
+        computePartials(its, rayO, diff->rx, diff->ry, dudx, dvdx, dudy, dvdy);
+        value = M.filtered(u, v, dudx * T.uv_scale[0], dvdx * T.uv_scale[1], dudy * T.uv_scale[0], dvdy * T.uv_scale[1]);
+    } else {
+        value = M.unfiltered(u, v);
+    }
+    return value * T.scale;
+}
+
 template <bool count>
 Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, float &alpha, int &depthOut, Counters *ctr,
         bool hasAlpha, const RayDiff &diff = RayDiff()) {
@@ -1971,6 +2081,11 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
             (I.strictNormals && dot(ray.d, its.geoFrame.n) * cosTheta(its.wi) >= 0))
             break;
 
+        // the hit's reflectance, with UV partials at the camera ray's hit only
+        // (later rays are built without differentials, path.cpp:217)
+        // (alb is used before the next rayIntersect overwrites its / ray)
+        const RayDiff *hitDiff = depth == 1 ? &diff : nullptr;
+        auto alb = [&](const mtsg_bsdf &rec) { return scene.reflectance(rec, its, ray.o, hitDiff); };
         // DirectSamplingRecord dRec(its) (records.inl:160-164)
         SceneView::DRec dRec;
         dRec.ref = its.p;
@@ -1984,7 +2099,7 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
                 BRec bRec;
                 bRec.wi = its.wi;
                 bRec.wo = its.toLocal(dRec.d);
-                const Spec bsdfVal = bsdfEvalTS(scene.d.bsdfs, bsdf, bRec);
+                const Spec bsdfVal = bsdfEvalTS(scene.d.bsdfs, bsdf, bRec, alb);
                 if (!bsdfVal.isZero() && (!I.strictNormals || dot(its.geoFrame.n, dRec.d) * cosTheta(bRec.wo) > 0)) {
                     float bsdfPdfV = bsdfPdfTS(scene.d.bsdfs, bsdf, bRec);   // area emitter: on surface, solid angle
                     float weight = miWeight(dRec.pdf, bsdfPdfV);
@@ -1998,7 +2113,7 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
         bRec.wi = its.wi;
         float s0, s1;
         sampler.next2D(s0, s1);
-        Spec bsdfWeight = bsdfSampleTS(scene.d.bsdfs, bsdf, bRec, bsdfPdfS, s0, s1, [&]() { return sampler.next1D(); });
+        Spec bsdfWeight = bsdfSampleTS(scene.d.bsdfs, bsdf, bRec, bsdfPdfS, s0, s1, [&]() { return sampler.next1D(); }, alb);
         DBG("  depth %d bsdf type=%d s=(%g %g) wi=(%g %g %g) wo=(%g %g %g) w=(%g %g %g) pdf=%g sampled=%d\n", depth, bsdf.type, s0, s1, bRec.wi.x, bRec.wi.y, bRec.wi.z, bRec.wo.x, bRec.wo.y, bRec.wo.z, bsdfWeight.s[0], bsdfWeight.s[1], bsdfWeight.s[2], bsdfPdfS, bRec.sampledType);
         if (bsdfWeight.isZero()) break;
         scattered |= bRec.sampledType != 0;
@@ -2498,7 +2613,7 @@ int oracle_bsdf_sample3(const mtsg_bsdf *b, const float wi[3], float s0, float s
     BRec r;
     r.wi = Vec(wi[0], wi[1], wi[2]);
     float p = 0;
-    Spec w = bsdfSample(*b, r, p, s0, s1, [&]() { return s2; });
+    Spec w = bsdfSample(*b, Spec::of(b->reflectance), r, p, s0, s1, [&]() { return s2; });
     wo[0] = r.wo.x; wo[1] = r.wo.y; wo[2] = r.wo.z;
     *pdf = p;
     weight[0] = w.s[0]; weight[1] = w.s[1]; weight[2] = w.s[2];
@@ -2509,7 +2624,7 @@ int oracle_bsdf_eval(const mtsg_bsdf *b, const float wi[3], const float wo[3], f
     BRec r;
     r.wi = Vec(wi[0], wi[1], wi[2]);
     r.wo = Vec(wo[0], wo[1], wo[2]);
-    Spec v = bsdfEval(*b, r);
+    Spec v = bsdfEval(*b, Spec::of(b->reflectance), r);
     value[0] = v.s[0]; value[1] = v.s[1]; value[2] = v.s[2];
     *pdf = bsdfPdf(*b, r);
     return 0;
@@ -2570,6 +2685,19 @@ int oracle_env_eval_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, co
         const bool diff = rx && ry;
         const Spec v = sv.envEvalEnvironment(r, diff, diff ? Vec(rx[3 * i], rx[3 * i + 1], rx[3 * i + 2]) : Vec(0.0f),
                                              diff ? Vec(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]) : Vec(0.0f));
+        out[3 * i] = v.s[0]; out[3 * i + 1] = v.s[1]; out[3 * i + 2] = v.s[2];
+    }
+    return 0;
+}
+
+/* BitmapTexture::eval(uv) / eval(uv, d0, d1) (bitmap.cpp:431-499) of texture
+ * `tex`: the MIP-level lookup the device's mtsg_tex_eval answers */
+int oracle_tex_eval_n(const mtsg_scene_desc *d, int tex, uint32_t n, const float *uv, const float *duv, float *out) {
+    if (!d || tex < 0 || (uint32_t)tex >= d->n_textures) { g_err = "texture index out of range"; return -1; }
+    const MipMap M{d->textures[tex].mip, d->tex_texels};
+    for (uint32_t i = 0; i < n; ++i) {
+        const Spec v = duv ? M.filtered(uv[2 * i], uv[2 * i + 1], duv[4 * i], duv[4 * i + 1], duv[4 * i + 2], duv[4 * i + 3])
+                           : M.unfiltered(uv[2 * i], uv[2 * i + 1]);
         out[3 * i] = v.s[0]; out[3 * i + 1] = v.s[1]; out[3 * i + 2] = v.s[2];
     }
     return 0;

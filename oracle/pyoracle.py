@@ -123,3 +123,19 @@ def sampler_draws(desc, params, x: int, y: int, s: int, kinds) -> np.ndarray:
     if L.oracle_sampler_draws(desc, C.byref(params), x, y, s, kinds.size, _p(kinds), _p(out)) != 0:
         raise RuntimeError("oracle_sampler_draws: " + L.oracle_last_error().decode())
     return out
+
+
+def tex_eval(desc, tex: int, uv: np.ndarray, duv: np.ndarray | None = None) -> np.ndarray:
+    """BitmapTexture::eval of texture `tex` at uv (n, 2), filtered with the uv
+    partials duv (n, 4) when given (oracle_tex_eval_n)."""
+    L = lib()
+    uv = np.ascontiguousarray(uv, dtype=np.float32)
+    out = np.empty((uv.shape[0], 3), np.float32)
+    pd = None
+    if duv is not None:
+        duv = np.ascontiguousarray(duv, dtype=np.float32)
+        pd = _p(duv)
+    L.oracle_tex_eval_n.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+    if L.oracle_tex_eval_n(desc, tex, uv.shape[0], _p(uv), pd, _p(out)) != 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return out

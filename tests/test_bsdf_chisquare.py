@@ -44,7 +44,7 @@ class Bsdf(C.Structure):
                 ("alpha_u", C.c_float), ("alpha_v", C.c_float),
                 ("ior_eta", C.c_float), ("ior_inv_eta", C.c_float),
                 ("fdr_int", C.c_float), ("spec_sampling_weight", C.c_float),
-                ("rtrans", C.c_float * RTRANS_SAMPLES)]
+                ("rtrans", C.c_float * RTRANS_SAMPLES), ("texture", C.c_int32), ("pad_tex", C.c_int32 * 3)]
 
 
 def make_bsdf(kind, dist=GGX, alpha=0.2, visible=1, eta=1.5046, alpha_v=None, nonlinear=0, fdr_int=0.6, spec_weight=0.6):
