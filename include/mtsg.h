@@ -294,6 +294,24 @@ typedef struct mtsg_sampler {
     int32_t pad;
 } mtsg_sampler;
 
+/* Occupancy maps of the fork's `myPath2_OM` integrator
+ * (src/integrators/testOM/myOM.h, myPath2_OM.cpp:137-172): MTSG_OM_COUNT
+ * bit-voxel grids of MTSG_OM_SIZE^3 over the cube around the scene's
+ * triangle meshes, each the base occupancy resampled along one rotated
+ * direction (generateROMA).  A shadow connection o1 -> o2 is answered by
+ * the map nearest to its direction: one column's z bits (Visible). */
+#define MTSG_OM_SIZE 256               /* OMSIZE                              */
+#define MTSG_OM_SQRT 4                 /* OMNUMSQRT                           */
+#define MTSG_OM_COUNT 16               /* OMNUM                               */
+typedef struct mtsg_om {
+    float aabb_min[3];            /* m_AABB.min                             */
+    float grid_size_recp;         /* m_gridSizeRecp                         */
+    float center[3];              /* m_center                               */
+    float pad;
+    float dir[MTSG_OM_COUNT][3];  /* m_dir of each rotated map              */
+    float rotate[MTSG_OM_COUNT][9];  /* m_rotate (row-major 3x3)            */
+} mtsg_om;
+
 typedef struct mtsg_scene_desc {
     uint32_t abi_version;         /* = MTSG_ABI_VERSION                     */
     uint32_t n_vertices;
@@ -364,6 +382,10 @@ typedef struct mtsg_scene_desc {
     const float *tex_texels;
     const float *tri_uv;          /* 6 * n_triangles                          */
     const float *tri_dpdv;        /* 3 * n_triangles                          */
+    /* myPath2_OM occupancy maps (NULL unless the scene's integrator is it):
+     * om_bits[((id * SIZE + x) * SIZE + y) * (SIZE / 32) + z / 32] bit z % 32 */
+    const mtsg_om *om;
+    const uint32_t *om_bits;
 } mtsg_scene_desc;
 
 /* ---- render ------------------------------------------------------------- */
@@ -389,7 +411,22 @@ typedef struct mtsg_render_params {
      * output block always covers the whole rectangle + border; blocks of
      * different offsets are merged by addition (imageblock.h:103-107). */
     int32_t tile_stride, tile_offset;
+    /* integrator: MTSG_INTEGRATOR_PATH = MIPathTracer (path.cpp);
+     * MTSG_INTEGRATOR_PATH2_OM = the fork's myPath2_OM (myPath2_OM.cpp:
+     * 317-485): max_depth is its maxDepthEye, next-event estimation sees
+     * occupancy-map visibility instead of a shadow ray, om_strategy /
+     * om_mis its `strategy` (bsdf / nee / mis) and `MISmode` (uniform /
+     * balance / power), om_jitter its `jitterSample`; the film is its
+     * per-pixel running mean (a 1-pixel box) */
+    int32_t integrator;
+    int32_t om_strategy;
+    int32_t om_mis;
+    int32_t om_jitter;
 } mtsg_render_params;
+
+enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_PATH2_OM = 1 };
+enum { MTSG_OM_STRATEGY_BSDF = 0, MTSG_OM_STRATEGY_NEE = 1, MTSG_OM_STRATEGY_MIS = 2 };
+enum { MTSG_OM_MIS_UNIFORM = 0, MTSG_OM_MIS_BALANCE = 1, MTSG_OM_MIS_POWER = 2 };
 
 /* Statistics of the last render call on a handle. */
 typedef struct mtsg_stats {
@@ -519,6 +556,12 @@ int  mtsg_env_eval(mtsg_scene *scene, uint32_t n, const float *dirs, const float
  * with the uv partials duv = (d0.x, d0.y, d1.x, d1.y) per point, or the
  * unfiltered evalBilinear(0) / evalBox(0) when duv is NULL.  RGB out. */
 int  mtsg_tex_eval(mtsg_scene *scene, int tex, uint32_t n, const float *uv, const float *duv, float *out);
+
+/* Debug / parity entry: myPath2_OM's visibility query for n connections:
+ * ids[i] = OccupancyMap::nearestOMindex(dirs[i]) (myOM.h:603-615) and
+ * vis[i] = roma[ids[i]].Visible(o1[i], o2[i]) (myOM.h:383-503), 0 or 1. */
+int  mtsg_om_query(mtsg_scene *scene, uint32_t n, const float *dirs, const float *o1, const float *o2, int32_t *ids,
+                   int32_t *vis);
 
 /* Debug: the scene sampler's draws for sample s of film pixel (x, y): kinds[i]
  * = 1 (next1D, one float out) or 2 (next2D, two floats), in call order, as

@@ -60,6 +60,11 @@ void mtsh_scene_free(mtsh_scene *scene);
  * up to `capacity` of them to out (may be NULL) and returns their count. */
 int mtsh_scene_textures(const mtsh_scene *scene, mtsg_texture *out, int capacity);
 
+/* The myPath2_OM occupancy maps of the scene (om.cpp): the header and the
+ * MTSG_OM_COUNT * 256 * 256 * 8 words of bits (either may be NULL).
+ * Returns 0, -1 without maps, -2 when capacity is too small. */
+int mtsh_scene_om(const mtsh_scene *scene, mtsg_om *om, uint32_t *bits, size_t capacity);
+
 /* hdrfilm develop (fmtconv.cpp:962-974): rgb = (sum w*L) / (sum w). */
 void mtsh_develop(const float *rgbaw, int w, int h, float *rgb_out);
 

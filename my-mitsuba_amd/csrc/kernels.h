@@ -64,6 +64,9 @@ struct DevScene {
     const float *__restrict__ tex_texels;
     const float4 *__restrict__ ttex;
     int cam_diffs;        // bounce 0 carries the camera's ray differentials in T / aux
+    // myPath2_OM occupancy maps (om.cpp; nullptr unless that integrator)
+    const mtsg_om *__restrict__ om;
+    const uint32_t *__restrict__ om_bits;
 };
 
 struct DevCamera {
@@ -84,6 +87,7 @@ struct DevIntegrator {
     uint32_t spp, seed;
     uint32_t film_w;   // sample id = (y * film_w + x) * spp + s
     DevSampler smp;
+    int om, om_strategy, om_mis, om_jitter;   // myPath2_OM (mtsg_render_params)
 };
 
 // wavefront batch: tiles [tile0, tile0 + ntiles) x samples [s0, s0 + ns)
@@ -1050,8 +1054,9 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
         slot_pixel(B, slot, x, y, s);
         alive = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
         if (alive) {
-            float a, b;
-            camera_jitter(I, x, y, s, a, b);
+            float a = 0.5f, b = 0.5f;   // myPath2_OM without jitterSample: the pixel centre, no draw
+            const bool jitter = !I.om || I.om_jitter;
+            if (jitter) camera_jitter(I, x, y, s, a, b);
             const float sx = ((float)x + a) * C.inv_res_x, sy = ((float)y + b) * C.inv_res_y;
             const float *m = C.s2c;
             float px = m[0] * sx + m[1] * sy + m[3], py = m[4] * sx + m[5] * sy + m[7];
@@ -1064,7 +1069,7 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
                             t[8] * d.x + t[9] * d.y + t[10] * d.z);
             stS(&P.ray_o[slot], make_float4(t[3], t[7], t[11], C.near_clip * invZ));
             stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
-            if (C.diffs) {
+            if (C.diffs && !I.om) {   // myPath2_OM uses sensor->sampleRay: no differentials
                 // rx/ryDirection scaled by 1/sqrt(spp) (integrator.cpp:148-149, ray.h:163-168),
                 const float3 rxc = normalize(nearP + ld3(C.dx)), ryc = normalize(nearP + ld3(C.dy));
                 const float3 rx = mk3(t[0] * rxc.x + t[1] * rxc.y + t[2] * rxc.z, t[4] * rxc.x + t[5] * rxc.y + t[6] * rxc.z,
@@ -1081,7 +1086,8 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
                 stS(&P.T[slot], make_float4(1.f, 1.f, 1.f, 1.f));
             }
             stS(&P.Lp[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
-            stS(&P.meta[slot], make_uint4(1u, 2u, slot, 1u));   // depth 1, 2 dimensions in one 2D request
+            // depth 1; the jitter used 2 dimensions in one 2D request
+            stS(&P.meta[slot], jitter ? make_uint4(1u, 2u, slot, 1u) : make_uint4(1u, 0u, slot, 0u));
         } else {
             // dead slot: bounce 0 runs over all slots and skips it
             stS(&P.ray_d[slot], make_float4(0.f, 0.f, 1.f, -1.0f));
@@ -2088,6 +2094,241 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
     }
 }
 
+// ---------------------------------------------------------------------------
+// myPath2_OM: the fork's path tracer with occupancy-map visibility
+// (src/integrators/testOM/myPath2_OM.cpp:317-485, myOM.h)
+// ---------------------------------------------------------------------------
+// OccupancyMap::nearestOMindex over direct2uv (myOM.h:603-615,
+// testOM/helpers.h:6-44).  Like the reference, it flips d in place when
+// d.z < 0 (the caller's direction stays flipped).  The mixed float / double
+// arithmetic follows the reference's expressions (M_PI is a double).
+DEV int om_index(float3 &d) {
+#pragma clang fp contract(off)
+    if (d.z < 0) d = -d;
+    const double PI = 3.14159265358979323846;
+    const float r = sqrtf(1 - d.z);
+    float phi = atan2f(d.y, d.x);
+    float u = 0, v = 0;
+    if (r != 0) {
+        float a, b;
+        if ((double)phi < -PI / 4) phi = (float)((double)phi + 2 * PI);
+        if ((double)phi < PI / 4) {
+            a = r;
+            b = (float)((double)(phi * a) / (PI / 4));
+        } else if ((double)phi < PI * 3 / 4) {
+            b = r;
+            a = (float)(-((double)phi - PI / 2) * (double)b / (PI / 4));
+        } else if ((double)phi < PI * 5 / 4) {
+            a = -r;
+            b = (float)(((double)phi - PI) * (double)a / (PI / 4));
+        } else {
+            b = -r;
+            a = (float)(-((double)phi - PI * 3 / 2) * (double)b / (PI / 4));
+        }
+        u = (a + 1) / 2;
+        v = (b + 1) / 2;
+    }
+    if ((double)u > 0.999999) u = (float)0.999999;
+    if ((double)v > 0.999999) v = (float)0.999999;
+    return (int)floorf(u * MTSG_OM_SQRT) * MTSG_OM_SQRT + (int)floorf(v * MTSG_OM_SQRT);
+}
+
+// OccupancyMap::Visible(o1, o2) of rotated map `id` (myOM.h:383-503, the
+// 32-bit column path): o1 rotated into the map's frame, o2 placed `length`
+// along m_dir from it, and the z cells strictly between theirs tested in
+// the (x, y) column.  The reference accepts x == 256 / y == 256 and reads
+// past the column array there; this build answers "visible".
+DEV bool om_visible(const DevScene &S, int id, float3 o1, float3 o2) {
+#pragma clang fp contract(off)
+    const mtsg_om &O = *S.om;
+    const float3 dir = mk3(O.dir[id][0], O.dir[id][1], O.dir[id][2]);
+    const float3 o21 = o2 - o1;
+    float len = sqrtf(o21.x * o21.x + o21.y * o21.y + o21.z * o21.z);
+    if (dot(dir, o21) < 0) len = -len;
+    const float *m = O.rotate[id];
+    const float3 c = mk3(O.center[0], O.center[1], O.center[2]);
+    const float3 q = o1 - c;   // Point - Vector
+    const float3 a1 = mk3(m[0] * q.x + m[1] * q.y + m[2] * q.z + 0.0f, m[3] * q.x + m[4] * q.y + m[5] * q.z + 0.0f,
+                          m[6] * q.x + m[7] * q.y + m[8] * q.z + 0.0f) + c;
+    const float3 a2 = a1 + dir * len;
+    const float rc = O.grid_size_recp;
+    const int x = (int)floorf((a1.x - O.aabb_min[0]) * rc + kEpsilon), y = (int)floorf((a1.y - O.aabb_min[1]) * rc + kEpsilon);
+    if (x < 0 || x >= MTSG_OM_SIZE || y < 0 || y >= MTSG_OM_SIZE) return true;
+    int z1 = (int)floorf((a1.z - O.aabb_min[2]) * rc + kEpsilon), z2 = (int)floorf((a2.z - O.aabb_min[2]) * rc + kEpsilon);
+    if (z1 > z2) { const int t = z1; z1 = z2; z2 = t; }
+    if (z2 - z1 < 2) return true;
+    z1 = min(max(z1 + 1, 0), MTSG_OM_SIZE - 1);
+    z2 = min(max(z2 - 1, 0), MTSG_OM_SIZE - 1);
+    const uint32_t *col = S.om_bits + (((size_t)id * MTSG_OM_SIZE + x) * MTSG_OM_SIZE + y) * (MTSG_OM_SIZE / 32);
+    const int p1 = z1 >> 5, p2 = z2 >> 5, r1 = z1 & 31, r2 = (31 - z2) & 31;
+    if (p1 == p2) return ((col[p1] >> r1) << (r1 + r2)) == 0u;
+    if ((col[p1] >> r1) != 0u) return false;
+    for (int k = p1 + 1; k < p2; ++k)
+        if (col[k] != 0u) return false;
+    return (col[p2] << r2) == 0u;
+}
+
+// nearestOMindex + Visible for the parity tests (mtsg_om_query)
+__global__ void k_om_query(DevScene S, const float *dirs, const float *o1, const float *o2, uint32_t n, int32_t *ids, int32_t *vis) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float3 d = mk3(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+    const int id = om_index(d);
+    ids[i] = id;
+    vis[i] = om_visible(S, id, mk3(o1[3 * i], o1[3 * i + 1], o1[3 * i + 2]), mk3(o2[3 * i], o2[3 * i + 1], o2[3 * i + 2])) ? 1 : 0;
+}
+
+// myPath2OMIntegrator::mis / misWeight (myPath2_OM.cpp:276-314)
+DEV float om_mis(const DevIntegrator &I, float p1, float p2) {
+    if (I.om_mis == MTSG_OM_MIS_UNIFORM) return 0.5f;
+    if (I.om_mis == MTSG_OM_MIS_BALANCE) return p1 / (p1 + p2);
+    return (p1 * p1) / ((p1 * p1) + (p2 * p2));
+}
+DEV float om_weight_nee(const DevIntegrator &I, float pdfBSDF, float pdfDirect) {
+    if (I.om_strategy == MTSG_OM_STRATEGY_BSDF) return 0.0f;
+    if (I.om_strategy == MTSG_OM_STRATEGY_NEE) return 1.0f;
+    return om_mis(I, pdfDirect, pdfBSDF);
+}
+DEV float om_weight_bsdf(const DevIntegrator &I, float pdfBSDF, float pdfDirect) {
+    if (I.om_strategy == MTSG_OM_STRATEGY_BSDF) return 1.0f;
+    if (I.om_strategy == MTSG_OM_STRATEGY_NEE) return 0.0f;
+    return om_mis(I, pdfBSDF, pdfDirect);
+}
+
+// One iteration of myPath2OMIntegrator::Li (myPath2_OM.cpp:386-485) for the
+// path at position i; the independent sampler only (see build.cpp).
+// Bounce 0: a camera ray that hits an emitter returns its radiance (:396-397).
+// Later bounces first finish the previous iteration: a BSDF ray that found
+// an emitter adds its MIS-weighted emission and ends the path (:462-472),
+// otherwise Russian roulette (:475-479) and ++depth.  Then next-event
+// estimation against occupancy-map visibility and the BSDF sample.
+template <bool EXT, class Out>
+DEV void shade_path_om(const DevScene &S, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, bool first, uint32_t i,
+                       const uint4 meta, Out &out, bool &cont) {
+    constexpr int SMP = MTSG_SAMPLER_INDEPENDENT;
+    const uint32_t slot = meta.z;
+    const float4 h = ldS(&P.hit[i]);
+    const float3 ro = xyz(ldS(&P.ray_o[i])), rd = xyz(ldS(&P.ray_d[i]));
+    const float4 L4 = ldS(&P.Lp[i]);
+    const float4 T4 = ldS(&P.T[i]);
+    PathSampler smp;
+    {
+        int x, y;
+        uint32_t sIdx;
+        slot_pixel(B, slot, x, y, sIdx);
+        smp = path_sampler(I, x, y, sIdx, meta.y, meta.w);
+    }
+    float3 L = xyz(L4), T = xyz(T4);
+    float eta = T4.w;
+    uint32_t depth = meta.x & 0xFFFFu;
+    uint32_t flags = meta.x & 0xFFFF0000u;
+    const bool valid = __float_as_uint(h.w) != 0xFFFFFFFFu;
+    bool done = false;
+    Its its;
+    const uint32_t inst = (valid && S.inst) ? P.hitInst[i] : 0xFFFFFFFFu;
+    if (valid) fill_its(S, ro, rd, h, inst, its);
+    if (first) {
+        if (valid && its.emitter >= 0) {   // its.Le(-ray.d) (area.cpp:104-109)
+            if (dot(its.sh.n, -rd) > 0) L = ld3(S.emitters[its.emitter].radiance);
+            done = true;
+        }
+    } else {
+        if (valid && its.emitter >= 0) {
+            const mtsg_emitter &E = S.emitters[its.emitter];
+            const float3 value = dot(its.sh.n, -rd) > 0 ? ld3(E.radiance) : mk3(0, 0, 0);
+            float lumPdf = 0.0f;
+            const float4 ax = ldS(&P.aux[i]);
+            if (!(flags & F_DELTA)) {   // Scene::pdfEmitterDirect after dRec.setQuery(ray, its)
+                if (dot(rd, xyz(ax)) >= 0 && dot(rd, its.sh.n) < 0) lumPdf = E.inv_area * (h.x * h.x) / fabsf(dot(rd, its.sh.n));
+                lumPdf *= E.pdf_discrete;
+            }
+            L += T * value * om_weight_bsdf(I, ax.w, lumPdf);
+            done = true;   // return Li
+        } else {
+            const float q = fminf(maxc(T) * eta * eta, 0.95f);
+            if (next1D<SMP>(I, smp) >= q) done = true;
+            else T = T / q;
+            ++depth;
+        }
+    }
+    if (!done && ((int)depth > I.max_depth || !valid)) done = true;
+    if (!done) {
+        const mtsg_bsdf &bsdf = S.bsdfs[its.bsdf];
+        const float3 wi = its.sh.toLocal(-rd);
+        float3 alb;
+        if (EXT) {   // rays from sensor->sampleRay carry no differentials: unfiltered lookups
+            const mtsg_bsdf &eff = (bsdf.twosided && !(wi.z > 0)) ? S.bsdfs[bsdf.back] : bsdf;
+            alb = eff.texture ? texture_eval(S, eff.texture - 1, h, inst, its, ro, false, ro, ro) : ld3(eff.reflectance);
+        } else {
+            alb = ld3(bsdf.reflectance);
+        }
+        const float3 refN = bsdf.ref_n_zero ? mk3(0, 0, 0) : its.sh.n;
+        if (bsdf.smooth) {
+            // scene->sampleEmitterDirect(dRec, next2D, testVisibility = false)
+            float sx, sy;
+            next2D<SMP>(I, smp, sx, sy);
+            float emPdf;
+            const uint32_t ei = pmf_sample_reuse(S.emitter_cdf, S.n_emitters, sx, emPdf);
+            const mtsg_emitter &E = S.emitters[ei];
+            float3 dd, value, ep = mk3(0, 0, 0);
+            float dist, pdf;
+            bool accepted, onSurface = true;
+            if (S.has_env && E.type == MTSG_EMITTER_ENVMAP) {
+                accepted = env_sample_direct(S.env, its.p, sx, sy, dd, dist, value, pdf);
+                if (accepted) ep = its.p + dd * dist;   // ray(farT)
+                onSurface = false;
+            } else {
+                float3 en;
+                emitter_sample_position(S, E, sx, sy, ep, en);
+                dd = ep - its.p;
+                const float distSquared = dot(dd, dd);
+                dist = sqrtf(distSquared);
+                dd = dd / dist;
+                const float dp = fabsf(dot(dd, en));
+                pdf = E.inv_area * (dp != 0 ? (distSquared / dp) : 0.0f);
+                accepted = dot(dd, refN) >= 0 && dot(dd, en) < 0 && pdf != 0;
+                if (accepted) value = ld3(E.radiance) / pdf;
+            }
+            if (accepted) {
+                pdf *= emPdf;
+                value = value / emPdf;
+            } else {
+                value = mk3(0, 0, 0);
+            }
+            // roma[nearestOMindex(dRec.d)].Visible(its.p + its.shFrame.n * 0.5, dRec.p)
+            // (the reference evaluates it twice, for its timing, with the same answer)
+            const int id = om_index(dd);
+            const bool vis = om_visible(S, id, its.p + its.sh.n * 0.5f, ep);
+            if (vis && !isZero(value)) {
+                const float3 wo = its.sh.toLocal(dd);   // the possibly flipped dRec.d, as in the reference
+                float bpdf;
+                const float3 bval = bsdf_eval<EXT>(S.bsdfs, bsdf, alb, wi, wo, bpdf);
+                if (!isZero(bval)) {
+                    const float bsdfPdf = onSurface ? bpdf : 0.0f;   // isOnSurface && ESolidAngle
+                    L += T * value * bval * om_weight_nee(I, bsdfPdf, pdf);
+                }
+            }
+        }
+        float sx, sy;
+        next2D<SMP>(I, smp, sx, sy);
+        BsdfSample bs;
+        if (!bsdf_sample<EXT>(S.bsdfs, bsdf, alb, wi, sx, sy, bs, [&]() { return next1D<SMP>(I, smp); })) {
+            done = true;
+        } else {
+            const float3 wo = its.sh.toWorld(bs.wo);
+            T = T * bs.weight;
+            eta *= bs.eta;
+            flags = bs.delta ? (flags | F_DELTA) : (flags & ~F_DELTA);
+            out.next(make_float4(its.p.x, its.p.y, its.p.z, kEpsilon), make_float4(wo.x, wo.y, wo.z, INFINITY),
+                     make_float4(refN.x, refN.y, refN.z, bs.pdf));
+            cont = true;
+        }
+    }
+    const float4 finalL = make_float4(L.x, L.y, L.z, L4.w);
+    if (cont) out.state(make_float4(T.x, T.y, T.z, eta), finalL, make_uint4(depth | flags, smp.dim, slot, smp.n2));
+    else stS(&P.L[slot], finalL);
+}
+
 // k_shade's outgoing records: lane-private LDS rows until the block append
 struct StageOut {
     ShadeStage &st;
@@ -2095,6 +2336,44 @@ struct StageOut {
     DEV void next(float4 o, float4 d, float4 aux) { st.o[threadIdx.x] = o; st.d[threadIdx.x] = d; st.aux[threadIdx.x] = aux; }
     DEV void state(float4 T, float4 L, uint4 meta) { st.T[threadIdx.x] = T; st.L[threadIdx.x] = L; st.meta[threadIdx.x] = meta; }
 };
+
+// myPath2_OM's shading launch: one iteration of its Li per path (no shadow
+// rays: visibility comes from the occupancy maps inside the kernel)
+template <bool EXT>
+__global__ void __launch_bounds__(SHADE_BLOCK) k_shade_om(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int bounce, int qin,
+                                                        uint32_t nIdentity) {
+    __shared__ BlockAppend ba;
+    __shared__ ShadeStage stage;
+    uint32_t count = nIdentity;
+    if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
+    const uint32_t nIter = (count + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
+    const int qout = qin < 0 ? 1 : (qin ^ 1);
+    for (uint32_t it = 0; it < nIter; ++it) {
+        const uint32_t i = (it * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+        bool alive = i < count;
+        bool cont = false;
+        uint4 meta = make_uint4(0u, 0u, 0u, 0u);
+        if (alive) {
+            meta = ldS(&P.meta[i]);
+            if (meta.x == 0u) alive = false;   // dead slot (bounce 0)
+        }
+        if (alive) {
+            StageOut out{stage};
+            shade_path_om<EXT>(S, I, B, P, bounce == 0, i, meta, out, cont);
+        }
+        const int tid = threadIdx.x;
+        uint32_t is, ic;
+        block_append2(ba, &P.cnt[cnt_s(bounce & 1)], &P.cnt[cnt_q(qout)], false, cont, is, ic);
+        if (cont) {
+            stS(&P.n_ray_o[ic], stage.o[tid]);
+            stS(&P.n_ray_d[ic], stage.d[tid]);
+            stS(&P.n_T[ic], stage.T[tid]);
+            stS(&P.n_aux[ic], stage.aux[tid]);
+            stS(&P.n_Lp[ic], stage.L[tid]);
+            stS(&P.n_meta[ic], stage.meta[tid]);
+        }
+    }
+}
 
 // qin < 0: bounce 0 over the identity queue of nIdentity slots
 #ifndef MTSG_SHADE_WAVES

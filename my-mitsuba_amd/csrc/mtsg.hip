@@ -323,6 +323,17 @@ int validate(const mtsg_render_params *p, const mtsg_scene *s) {
         g_err = "invalid tile_stride / tile_offset";
         return MTSG_ERR_INVALID;
     }
+    if (p->integrator != MTSG_INTEGRATOR_PATH && p->integrator != MTSG_INTEGRATOR_PATH2_OM) { g_err = "unknown integrator"; return MTSG_ERR_INVALID; }
+    if (p->integrator == MTSG_INTEGRATOR_PATH2_OM) {
+        if (!s->ds.om) { g_err = "myPath2_OM: the scene has no occupancy maps"; return MTSG_ERR_INVALID; }
+        if (s->samplerType != MTSG_SAMPLER_INDEPENDENT) { g_err = "myPath2_OM: only the independent sampler is supported"; return MTSG_ERR_INVALID; }
+        if (p->max_depth < 1) { g_err = "myPath2_OM: 'maxDepthEye' must be at least 1"; return MTSG_ERR_INVALID; }
+        if (p->om_strategy < MTSG_OM_STRATEGY_BSDF || p->om_strategy > MTSG_OM_STRATEGY_MIS || p->om_mis < MTSG_OM_MIS_UNIFORM ||
+            p->om_mis > MTSG_OM_MIS_POWER) {
+            g_err = "myPath2_OM: unknown strategy or MIS mode";
+            return MTSG_ERR_INVALID;
+        }
+    }
     return MTSG_OK;
 }
 
@@ -364,6 +375,10 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     const int blockW = p->tile_w + 2 * s->cam.border, blockH = p->tile_h + 2 * s->cam.border;
     DevIntegrator I{p->max_depth, p->rr_depth, p->strict_normals, p->hide_emitters, p->spp, p->seed, (uint32_t)s->cam.film_w,
                     make_sampler(s, p->spp)};
+    I.om = p->integrator == MTSG_INTEGRATOR_PATH2_OM ? 1 : 0;
+    I.om_strategy = p->om_strategy;
+    I.om_mis = p->om_mis;
+    I.om_jitter = p->om_jitter;
     memset(&s->stats, 0, sizeof(s->stats));
     s->wtLaunches = 0;
     if ((s->flags & MTSG_FLAG_WAVETIME) && !s->waveTimes)
@@ -413,9 +428,11 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
         for (uint32_t l = 1; l < nl && result == MTSG_OK; ++l)
             if (hipStreamWaitEvent(s->lstream[l], startEv, 0) != hipSuccess) { g_err = "stream wait"; result = MTSG_ERR_DEVICE; }
     }
-    const int maxBounces = p->max_depth > 0 ? p->max_depth : 1 << 30;
-    // tail mode (k_finish): one lane, not in the instrumented or two-level modes
-    const bool useFinish = s->finishPaths > 0 && nl == 1 && !count && !s->ds.inst;
+    // myPath2_OM shades depths 1..maxDepthEye and one more launch books the
+    // emitters its last BSDF rays found
+    const int maxBounces = I.om ? p->max_depth + 1 : (p->max_depth > 0 ? p->max_depth : 1 << 30);
+    // tail mode (k_finish): one lane, not in the instrumented, two-level or myPath2_OM modes
+    const bool useFinish = s->finishPaths > 0 && nl == 1 && !count && !s->ds.inst && !I.om;
     // bounce b of a lane: one trace launch over this bounce's closest rays
     // (work list qin(b), identity for b = 0) and bounce b-1's shadow rays
     // (S((b-1) & 1)), then k_shade appends the next bounce's paths to
@@ -898,6 +915,16 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         s->extBsdfs = true;   // texture lookups live in the extended shade kernel
     }
     ds.cam_diffs = (d->has_envmap || texDiffs) ? 1 : 0;
+    // myPath2_OM occupancy maps (om.cpp)
+    ds.om = nullptr; ds.om_bits = nullptr;
+    if (d->om) {
+        if (!d->om_bits) { g_err = "occupancy maps without their bits"; return fail(MTSG_ERR_INVALID); }
+        mtsg_om *dom; uint32_t *dbits;
+        if ((rc = up(d->om, 1, &dom)) ||
+            (rc = up(d->om_bits, (size_t)MTSG_OM_COUNT * MTSG_OM_SIZE * MTSG_OM_SIZE * (MTSG_OM_SIZE / 32), &dbits)))
+            return fail(rc);
+        ds.om = dom; ds.om_bits = dbits;
+    }
     ds.n_emitters = d->n_emitters;
     ds.n_tri = d->n_triangles;
     for (int k = 0; k < 3; ++k) { ds.bmin[k] = d->aabb_min[k]; ds.bmax[k] = d->aabb_max[k]; }
@@ -1219,6 +1246,35 @@ int mtsg_tex_eval(mtsg_scene *s, int tex, uint32_t n, const float *uv, const flo
         e = hipStreamSynchronize(s->stream);
     }
     if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost);
+    cleanup();
+    if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    return MTSG_OK;
+}
+
+int mtsg_om_query(mtsg_scene *s, uint32_t n, const float *dirs, const float *o1, const float *o2, int32_t *ids, int32_t *vis) {
+    if (!s || (n && (!dirs || !o1 || !o2 || !ids || !vis))) { g_err = "invalid arguments"; return MTSG_ERR_INVALID; }
+    if (!s->ds.om) { g_err = "scene has no occupancy maps"; return MTSG_ERR_INVALID; }
+    if (n == 0) return MTSG_OK;
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    const size_t fb = (size_t)n * 3 * sizeof(float), ib = (size_t)n * sizeof(int32_t);
+    float *dd = nullptr, *d1 = nullptr, *d2 = nullptr;
+    int32_t *di = nullptr, *dv = nullptr;
+    auto cleanup = [&]() { hipFree(dd); hipFree(d1); hipFree(d2); hipFree(di); hipFree(dv); };
+    hipError_t e = hipMalloc((void **)&dd, fb);
+    if (e == hipSuccess) e = hipMalloc((void **)&d1, fb);
+    if (e == hipSuccess) e = hipMalloc((void **)&d2, fb);
+    if (e == hipSuccess) e = hipMalloc((void **)&di, ib);
+    if (e == hipSuccess) e = hipMalloc((void **)&dv, ib);
+    if (e == hipSuccess) e = hipMemcpy(dd, dirs, fb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d1, o1, fb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d2, o2, fb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_om_query, dim3((n + 255) / 256), dim3(256), 0, s->stream, s->ds, dd, d1, d2, n, di, dv);
+        e = hipStreamSynchronize(s->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpy(ids, di, ib, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(vis, dv, ib, hipMemcpyDeviceToHost);
     cleanup();
     if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
     return MTSG_OK;

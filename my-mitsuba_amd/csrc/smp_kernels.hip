@@ -13,6 +13,13 @@ namespace mtsg {
 template <>
 void launch_shade_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
     constexpr int SMP = MTSG_TU_SAMPLER;
+#if MTSG_TU_SAMPLER == MTSG_SAMPLER_INDEPENDENT
+    if (a.I->om) {   // myPath2_OM (independent sampler only)
+        if (a.ext) hipLaunchKernelGGL((k_shade_om<true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity);
+        else hipLaunchKernelGGL((k_shade_om<false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity);
+        return;
+    }
+#endif
     if (a.ext) {
         if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
         else hipLaunchKernelGGL((k_shade<false, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);

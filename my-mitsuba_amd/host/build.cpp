@@ -407,12 +407,17 @@ void Scene::finalize() {
     cam.film_h = f.height;
     cam.crop_x = f.cropX; cam.crop_y = f.cropY; cam.crop_w = f.cropW; cam.crop_h = f.cropH;
     cam.has_alpha = f.hasAlpha ? 1 : 0;
+    // myPath2_OM accumulates each pixel's running mean of its own samples
+    // and hands the film a finished bitmap (myPath2_OM.cpp:229-281): a box of
+    // exactly one pixel, no alpha
+    const bool om = integrator.type == "myPath2_OM";
+    if (om) cam.has_alpha = 0;
 
     // rfilter.cpp:37-57 with MTS_FILTER_RESOLUTION = 31
     const int RES = 31;
     float radius;
     std::function<float(float)> eval;
-    if (f.filter == "gaussian") {
+    if (f.filter == "gaussian" && !om) {
         float stddev = f.stddev;
         radius = 4 * stddev;
         eval = [stddev, radius](float x) {
@@ -421,7 +426,7 @@ void Scene::finalize() {
         };
         cam.filter_type = MTSG_FILTER_GAUSSIAN;
     } else {
-        radius = f.boxRadius + 1e-5f;
+        radius = om ? 0.5f : f.boxRadius + 1e-5f;
         eval = [radius](float x) { return std::abs(x) <= radius ? 1.0f : 0.0f; };
         cam.filter_type = MTSG_FILTER_BOX;
     }
@@ -457,6 +462,16 @@ void Scene::finalize() {
     d.tex_texels = texTexels.empty() ? nullptr : texTexels.data();
     d.tri_uv = triUv.empty() ? nullptr : triUv.data();
     d.tri_dpdv = triDpdv.empty() ? nullptr : triDpdv.data();
+    if (om) {
+        // the fork's integrator draws from one sampler per core without
+        // generate()/advance() (myPath2_OM.cpp:198-265): only the independent
+        // sampler has a defined sequence there
+        if (samplerType != "independent")
+            throw std::runtime_error("myPath2_OM: only the independent sampler is supported by this build");
+        buildOccupancyMaps(*this);
+        d.om = &omDesc;
+        d.om_bits = omBits.data();
+    }
     d.n_rects = (uint32_t)rectDesc.size();
     d.rects = rectDesc.data();
     d.n_shapes = (uint32_t)shapeDesc.size();

@@ -63,6 +63,10 @@ void mtsh_scene_render_params(const mtsh_scene *s, mtsg_render_params *p) {
     p->tile_h = sc.film.cropH;
     p->tile_stride = 1;
     p->tile_offset = 0;
+    p->integrator = sc.integrator.type == "myPath2_OM" ? MTSG_INTEGRATOR_PATH2_OM : MTSG_INTEGRATOR_PATH;
+    p->om_strategy = sc.integrator.omStrategy;
+    p->om_mis = sc.integrator.omMis;
+    p->om_jitter = sc.integrator.omJitter ? 1 : 0;
 }
 
 int mtsh_scene_textures(const mtsh_scene *s, mtsg_texture *out, int capacity) {
@@ -70,6 +74,17 @@ int mtsh_scene_textures(const mtsh_scene *s, mtsg_texture *out, int capacity) {
     const int n = (int)sc.textureDesc.size();
     for (int i = 0; out && i < n && i < capacity; ++i) out[i] = sc.textureDesc[i];
     return n;
+}
+
+int mtsh_scene_om(const mtsh_scene *s, mtsg_om *om, uint32_t *bits, size_t capacity) {
+    const mtsh::Scene &sc = *s->scene;
+    if (sc.omBits.empty()) { g_err = "the scene has no occupancy maps"; return -1; }
+    if (om) *om = sc.omDesc;
+    if (bits) {
+        if (capacity < sc.omBits.size()) { g_err = "mtsh_scene_om: buffer too small"; return -2; }
+        std::copy(sc.omBits.begin(), sc.omBits.end(), bits);
+    }
+    return 0;
 }
 
 void mtsh_scene_get_info(const mtsh_scene *s, mtsh_scene_info *out) {

@@ -1265,6 +1265,7 @@ struct Loader {
             }
             for (const Mesh &m0 : g.meshes) {
                 Mesh m = m0;
+                m.instanced = true;   // an Instance in the reference: not one of Scene::getMeshes()
                 for (auto &p : m.p) p = toWorld.point(p);
                 for (auto &nn : m.n) nn = normalize(toWorld.normal(nn));
                 meshes.push_back(std::move(m));
@@ -1365,9 +1366,28 @@ struct Loader {
                 Properties props;
                 std::vector<XNode *> nested;
                 parseProps(c, props, nested);
-                std::string type = lower(c.attr("type"));
-                if (type != "path") throw err("line " + std::to_string(c.line) + ": integrator \"" + type + "\" is outside this build's scope (only 'path')");
+                std::string type = c.attr("type");
                 IntegratorProps &ip = scene.integrator;
+                if (type == "myPath2_OM") {
+                    // myPath2OMIntegrator(props) (myPath2_OM.cpp:61-85)
+                    ip.type = type;
+                    ip.maxDepth = (int)props.getInt("maxDepthEye", 50);
+                    ip.rrDepth = 1;
+                    const std::string st = props.getString("strategy", "mis"), mm = props.getString("MISmode", "balance");
+                    if (st == "bsdf") ip.omStrategy = MTSG_OM_STRATEGY_BSDF;
+                    else if (st == "nee") ip.omStrategy = MTSG_OM_STRATEGY_NEE;
+                    else if (st == "mis") ip.omStrategy = MTSG_OM_STRATEGY_MIS;
+                    else throw err("Unknown strategy: " + st);
+                    if (mm == "uniform") ip.omMis = MTSG_OM_MIS_UNIFORM;
+                    else if (mm == "balance") ip.omMis = MTSG_OM_MIS_BALANCE;
+                    else if (mm == "power") ip.omMis = MTSG_OM_MIS_POWER;
+                    else throw err("Unknown MIS mode: " + mm);
+                    ip.omJitter = props.getBool("jitterSample", true);
+                    if (ip.maxDepth < 1) throw err("myPath2_OM: 'maxDepthEye' must be at least 1");
+                    continue;
+                }
+                type = lower(type);
+                if (type != "path") throw err("line " + std::to_string(c.line) + ": integrator \"" + type + "\" is outside this build's scope (only 'path' and 'myPath2_OM')");
                 ip.type = type;
                 ip.rrDepth = (int)props.getInt("rrDepth", 5);
                 ip.maxDepth = (int)props.getInt("maxDepth", -1);

@@ -45,6 +45,7 @@ struct Mesh {
     bool faceNormals = false;
     int bsdf = -1, emitter = -1;
     int group = -1;                  // two-level: the shape group it belongs to (group space)
+    bool instanced = false;          // flattened from an instance (not a Scene::getMeshes() TriMesh)
 };
 
 struct Rect {
@@ -112,6 +113,9 @@ struct IntegratorProps {
     std::string type = "path";
     int maxDepth = -1, rrDepth = 5;
     bool strictNormals = false, hideEmitters = false;
+    // myPath2_OM (myPath2_OM.cpp:61-85)
+    int omStrategy = MTSG_OM_STRATEGY_MIS, omMis = MTSG_OM_MIS_BALANCE;
+    bool omJitter = true;
 };
 
 struct KDBuildParams {                // gkdtree.h:734-744 defaults
@@ -160,6 +164,8 @@ struct Scene {
     std::vector<float> vtxPos, vtxNrm, triDpdu, emitterCdf, emitterTriCdf;
     std::vector<float> triUv, triDpdv;   // only with textures
     std::vector<mtsg_texture> textureDesc;
+    mtsg_om omDesc{};                 // myPath2_OM only
+    std::vector<uint32_t> omBits;
     std::vector<uint32_t> triIdx;
     std::vector<mtsg_rect> rectDesc;
     std::vector<mtsg_shape> shapeDesc;
@@ -206,6 +212,9 @@ struct PngImage {
 bool readPNG(const std::string &path, PngImage &img, std::string &err);
 // the bitmap plugin's input: linear float RGB, rows top-down
 void loadTextureImage(const std::string &path, float gammaOverride, int &w, int &h, std::vector<float> &rgb);
+
+// myPath2_OM's occupancy maps (om.cpp): fills omDesc / omBits
+void buildOccupancyMaps(Scene &scene);
 
 // Halton / Hammersley tables (qmc.cpp in this directory): the first 1024
 // primes, offsets of each base's digit permutation, and the permutations

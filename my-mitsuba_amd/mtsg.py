@@ -38,6 +38,7 @@ class RenderParams(C.Structure):
         ("tile_x", C.c_int32), ("tile_y", C.c_int32),
         ("tile_w", C.c_int32), ("tile_h", C.c_int32),
         ("tile_stride", C.c_int32), ("tile_offset", C.c_int32),
+        ("integrator", C.c_int32), ("om_strategy", C.c_int32), ("om_mis", C.c_int32), ("om_jitter", C.c_int32),
     ]
 
     def copy(self) -> "RenderParams":
@@ -81,6 +82,12 @@ class MipMapHeader(C.Structure):
     ]
 
 
+class OMHeader(C.Structure):
+    """mtsg_om (include/mtsg.h)."""
+    _fields_ = [("aabb_min", C.c_float * 3), ("grid_size_recp", C.c_float), ("center", C.c_float * 3), ("pad", C.c_float),
+                ("dir", (C.c_float * 3) * 16), ("rotate", (C.c_float * 9) * 16)]
+
+
 class TextureHeader(C.Structure):
     """mtsg_texture (include/mtsg.h)."""
     _fields_ = [("mip", MipMapHeader), ("uv_offset", C.c_float * 2), ("uv_scale", C.c_float * 2), ("scale", C.c_float),
@@ -108,13 +115,13 @@ DEVICE_SYMBOLS = [
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
-    "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_sampler_draws", "mtsg_debug_wavetimes",
+    "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_sampler_draws", "mtsg_debug_wavetimes",
     "mtsg_debug_stragglers",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
-    "mtsh_read_image", "mtsh_clip_triangle", "mtsh_texture_image", "mtsh_build_mipmap", "mtsh_scene_textures", "mtsh_last_error",
+    "mtsh_read_image", "mtsh_clip_triangle", "mtsh_texture_image", "mtsh_build_mipmap", "mtsh_scene_textures", "mtsh_scene_om", "mtsh_last_error",
 ]
 PATH_SYMBOLS = [
     "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
@@ -167,6 +174,7 @@ def host_lib() -> C.CDLL:
         lib.mtsh_read_image.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p, C.c_size_t]
         lib.mtsh_clip_triangle.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsh_scene_textures.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        lib.mtsh_scene_om.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
         lib.mtsh_texture_image.argtypes = [C.c_char_p, C.c_float, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p,
                                            C.c_size_t]
         lib.mtsh_build_mipmap.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
@@ -207,6 +215,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_render_samples.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
         lib.mtsg_env_eval.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_tex_eval.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.mtsg_om_query.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_sampler_draws.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int, C.c_uint32,
                                            C.c_uint32, C.c_void_p, C.c_void_p]
         lib.mtsg_scene_destroy.argtypes = [C.c_void_p]
@@ -260,6 +269,15 @@ class Scene:
     @property
     def border(self) -> int:
         return self.info.border
+
+    def occupancy_maps(self):
+        """myPath2_OM's maps: (header OMHeader, bits (16, 256, 256, 8) uint32)."""
+        lib = host_lib()
+        hdr = OMHeader()
+        bits = np.zeros((16, 256, 256, 8), np.uint32)
+        if lib.mtsh_scene_om(self._h, C.byref(hdr), _ptr(bits), bits.size) != 0:
+            raise RuntimeError(_err(lib, "mtsh_last_error"))
+        return hdr, bits
 
     def textures(self) -> list:
         """The scene's bitmap texture headers (TextureHeader)."""
@@ -418,6 +436,16 @@ class GPUScene:
             pd = _ptr(duv)
         self._check(device_lib().mtsg_tex_eval(self._h, tex, uv.shape[0], _ptr(uv), pd, _ptr(out)), "mtsg_tex_eval")
         return out
+
+    def om_query(self, dirs: np.ndarray, o1: np.ndarray, o2: np.ndarray):
+        """myPath2_OM visibility (debug entry point): (map ids, visible flags)."""
+        dirs, o1, o2 = (np.ascontiguousarray(a, dtype=np.float32) for a in (dirs, o1, o2))
+        n = dirs.shape[0]
+        ids = np.empty(n, np.int32)
+        vis = np.empty(n, np.int32)
+        self._check(device_lib().mtsg_om_query(self._h, n, _ptr(dirs), _ptr(o1), _ptr(o2), _ptr(ids), _ptr(vis)),
+                    "mtsg_om_query")
+        return ids, vis
 
     def sampler_draws(self, params: RenderParams, x: int, y: int, s: int, kinds) -> np.ndarray:
         """The scene sampler's next1D (kind 1) / next2D (kind 2) draws of one

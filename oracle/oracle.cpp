@@ -1365,7 +1365,7 @@ struct SceneView {
 
     // Scene::sampleEmitterDirect (scene.cpp:910-947) + AreaLight::sampleDirect (area.cpp:150-165)
     template <bool count>
-    Spec sampleEmitterDirect(DRec &dRec, float sx, float sy, Counters *ctr) const {
+    Spec sampleEmitterDirect(DRec &dRec, float sx, float sy, Counters *ctr, bool testVisibility = true) const {
         float emPdf;
         size_t index = pmfSampleReuse(d.emitter_cdf, d.n_emitters, sx, emPdf);
         const mtsg_emitter &em = d.emitters[index];
@@ -1387,7 +1387,7 @@ struct SceneView {
             ray.setDirection(dRec.d);
             ray.mint = kEpsilon;
             ray.maxt = dRec.dist * (1 - kShadowEpsilon);
-            if (rayIntersectShadow<count>(ray, ctr)) return Spec(0.0f);
+            if (testVisibility && rayIntersectShadow<count>(ray, ctr)) return Spec(0.0f);
             dRec.emitter = (int)index;
             dRec.pdf *= emPdf;
             value = value / emPdf;
@@ -2180,6 +2180,172 @@ Spec Li(const SceneView &scene, const Integrator &I, Ray ray, Sampler &sampler, 
     return Li;
 }
 
+
+// ---------------------------------------------------------------------------
+// myPath2_OM (src/integrators/testOM/myPath2_OM.cpp:317-485) and the
+// occupancy-map visibility it uses instead of shadow rays (myOM.h)
+// ---------------------------------------------------------------------------
+// OccupancyMap::nearestOMindex / direct2uv (myOM.h:603-615, helpers.h:6-44):
+// flips d in place when d.z < 0, as the reference does
+int omNearestIndex(Vec &d) {
+    if (d.z < 0) d = -d;
+    const float r = std::sqrt(1 - d.z);
+    float phi = std::atan2(d.y, d.x);
+    float u, v;
+    if (r == 0) {
+        u = 0;
+        v = 0;
+    } else {
+        float a, b;
+        if (phi < -M_PI / 4) phi += 2 * M_PI;
+        if (phi < M_PI / 4) {
+            a = r;
+            b = phi * a / (M_PI / 4);
+        } else if (phi < M_PI * 3 / 4) {
+            b = r;
+            a = -(phi - M_PI / 2) * b / (M_PI / 4);
+        } else if (phi < M_PI * 5 / 4) {
+            a = -r;
+            b = (phi - M_PI) * a / (M_PI / 4);
+        } else {
+            b = -r;
+            a = -(phi - M_PI * 3 / 2) * b / (M_PI / 4);
+        }
+        u = (a + 1) / 2;
+        v = (b + 1) / 2;
+    }
+    if (u > 0.999999) u = 0.999999;
+    if (v > 0.999999) v = 0.999999;
+    return int(std::floor(u * MTSG_OM_SQRT)) * MTSG_OM_SQRT + int(std::floor(v * MTSG_OM_SQRT));
+}
+
+// OccupancyMap::Visible (myOM.h:383-503, 32-bit column path); x or y == 256
+// (an out-of-range read in the reference) counts as visible
+bool omVisible(const mtsg_scene_desc &d, int id, const Vec &o1, const Vec &o2) {
+    const mtsg_om &O = *d.om;
+    const Vec dir(O.dir[id][0], O.dir[id][1], O.dir[id][2]);
+    const Vec o21 = o2 - o1;
+    float length = std::sqrt(o21.x * o21.x + o21.y * o21.y + o21.z * o21.z);
+    if (dot(dir, o21) < 0) length = -length;
+    const float *m = O.rotate[id];
+    const Vec c(O.center[0], O.center[1], O.center[2]);
+    const Vec q = o1 - c;
+    const Vec a1 = Vec(m[0] * q.x + m[1] * q.y + m[2] * q.z + 0.0f, m[3] * q.x + m[4] * q.y + m[5] * q.z + 0.0f,
+                       m[6] * q.x + m[7] * q.y + m[8] * q.z + 0.0f) + c;
+    const Vec a2 = a1 + dir * length;
+    const float rc = O.grid_size_recp;
+    const int x = (int)std::floor((a1.x - O.aabb_min[0]) * rc + kEpsilon), y = (int)std::floor((a1.y - O.aabb_min[1]) * rc + kEpsilon);
+    if (x < 0 || x >= MTSG_OM_SIZE || y < 0 || y >= MTSG_OM_SIZE) return true;
+    int z1 = (int)std::floor((a1.z - O.aabb_min[2]) * rc + kEpsilon), z2 = (int)std::floor((a2.z - O.aabb_min[2]) * rc + kEpsilon);
+    if (z1 > z2) std::swap(z1, z2);
+    if (z2 - z1 < 2) return true;
+    z1 += 1;
+    z2 -= 1;
+    z1 = std::min(std::max(z1, 0), MTSG_OM_SIZE - 1);
+    z2 = std::min(std::max(z2, 0), MTSG_OM_SIZE - 1);
+    const uint32_t *col = d.om_bits + (((size_t)id * MTSG_OM_SIZE + x) * MTSG_OM_SIZE + y) * (MTSG_OM_SIZE / 32);
+    const int p1 = z1 >> 5, p2 = z2 >> 5, r1 = z1 & 31, r2 = (31 - z2) & 31;
+    if (p1 == p2) return ((col[p1] >> r1) << (r1 + r2)) == 0;
+    if (col[p1] >> r1) return false;
+    for (int i = p1 + 1; i < p2; ++i)
+        if (col[i]) return false;
+    return (col[p2] << r2) == 0;
+}
+
+struct OMParams { int maxDepthEye, strategy, mis; };
+
+float omMis(const OMParams &P, float p1, float p2) {   // myPath2_OM.cpp:301-314
+    if (P.mis == MTSG_OM_MIS_UNIFORM) return 0.5f;
+    if (P.mis == MTSG_OM_MIS_BALANCE) return p1 / (p1 + p2);
+    return (p1 * p1) / ((p1 * p1) + (p2 * p2));
+}
+// misWeight (myPath2_OM.cpp:270-299): which = 0 for the BSDF strategy, 1 for NEE
+float omMisWeight(const OMParams &P, float pdfBSDF, float pdfDirect, int which) {
+    if (which == 0) {
+        if (P.strategy == MTSG_OM_STRATEGY_BSDF) return 1;
+        if (P.strategy == MTSG_OM_STRATEGY_NEE) return 0;
+        return omMis(P, pdfBSDF, pdfDirect);
+    }
+    if (P.strategy == MTSG_OM_STRATEGY_BSDF) return 0;
+    if (P.strategy == MTSG_OM_STRATEGY_NEE) return 1;
+    return omMis(P, pdfDirect, pdfBSDF);
+}
+
+// myPath2OMIntegrator::Li (myPath2_OM.cpp:386-485)
+Spec LiOM(const SceneView &scene, const OMParams &P, Ray ray, Sampler &sampler) {
+    Its its;
+    Spec Li(0.0f), throughput(1.0f);
+    float eta = 1.0f;
+    scene.rayIntersect<false>(ray, its, nullptr, nullptr);
+    ray.mint = kEpsilon;
+    if (its.valid() && scene.d.shapes[its.shape].emitter >= 0) {   // its.Le(-ray.d)
+        if (dot(its.shFrame.n, -ray.d) > 0) return Spec::of(scene.d.emitters[scene.d.shapes[its.shape].emitter].radiance);
+        return Spec(0.0f);
+    }
+    int depth = 1;
+    while (depth <= P.maxDepthEye) {
+        if (!its.valid()) break;
+        const mtsg_bsdf &bsdf = scene.d.bsdfs[scene.d.shapes[its.shape].bsdf];
+        auto alb = [&](const mtsg_bsdf &rec) { return scene.reflectance(rec, its, ray.o, nullptr); };   // sampleRay: no differentials
+        SceneView::DRec dRec;
+        dRec.ref = its.p;
+        dRec.refN = bsdf.ref_n_zero ? Vec(0.0f) : its.shFrame.n;
+        if (bsdf.smooth) {
+            float s0, s1;
+            sampler.next2D(s0, s1);
+            const Spec value = scene.sampleEmitterDirect<false>(dRec, s0, s1, nullptr, false);
+            const int id = omNearestIndex(dRec.d);   // (twice in the reference, same answer)
+            const bool vis = omVisible(scene.d, id, its.p + its.shFrame.n * 0.5f, dRec.p);
+            if (vis && !value.isZero()) {
+                BRec bRec;
+                bRec.wi = its.wi;
+                bRec.wo = its.toLocal(dRec.d);   // the possibly flipped direction
+                const Spec bsdfVal = bsdfEvalTS(scene.d.bsdfs, bsdf, bRec, alb);
+                if (!bsdfVal.isZero()) {
+                    const bool onSurface = scene.d.emitters[dRec.emitter].type != MTSG_EMITTER_ENVMAP;
+                    const float bsdfPdf = onSurface ? bsdfPdfTS(scene.d.bsdfs, bsdf, bRec) : 0.0f;
+                    Li += throughput * value * bsdfVal * omMisWeight(P, bsdfPdf, dRec.pdf, 1);
+                }
+            }
+        }
+        float bsdfPdf;
+        BRec bRec;
+        bRec.wi = its.wi;
+        float s0, s1;
+        sampler.next2D(s0, s1);
+        const Spec bsdfWeight = bsdfSampleTS(scene.d.bsdfs, bsdf, bRec, bsdfPdf, s0, s1, [&]() { return sampler.next1D(); }, alb);
+        if (bsdfWeight.isZero()) break;
+        const Vec wo = its.toWorld(bRec.wo);
+        throughput *= bsdfWeight;
+        eta *= bRec.eta;
+        Ray next;
+        next.o = its.p;
+        next.setDirection(wo);
+        next.mint = kEpsilon;
+        next.maxt = std::numeric_limits<float>::infinity();
+        ray = next;
+        if (scene.rayIntersect<false>(ray, its, nullptr, nullptr)) {
+            const int em = scene.d.shapes[its.shape].emitter;
+            if (em >= 0) {
+                const Spec value = dot(its.shFrame.n, -ray.d) > 0 ? Spec::of(scene.d.emitters[em].radiance) : Spec(0.0f);
+                dRec.p = its.p;   // dRec.setQuery(ray, its) (records.inl:170-176)
+                dRec.n = its.shFrame.n;
+                dRec.emitter = em;
+                dRec.d = ray.d;
+                dRec.dist = its.t;
+                const float lumPdf = !(bRec.sampledType & (EDeltaReflection | EDeltaTransmission)) ? scene.pdfEmitterDirect(dRec) : 0;
+                Li += throughput * value * omMisWeight(P, bsdfPdf, lumPdf, 0);
+                return Li;
+            }
+        }
+        const float q = std::min(throughput.max() * eta * eta, 0.95f);
+        if (sampler.next1D() >= q) break;
+        throughput = throughput / q;
+        ++depth;
+    }
+    return Li;
+}
+
 // PerspectiveCamera::sampleRayDifferential (perspective.cpp:271-298)
 Ray cameraRay(const mtsg_camera &c, float px, float py, RayDiff *diff = nullptr, uint32_t spp = 1) {
     const float *m = c.sample_to_camera;
@@ -2484,6 +2650,8 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
         std::fill(rgbaw, rgbaw + (size_t)W * H * 5, 0.0f);
         SceneView sv(*d);
         Integrator I{p->max_depth, p->rr_depth, p->strict_normals != 0, p->hide_emitters != 0};
+        const OMParams omp{p->max_depth, p->om_strategy, p->om_mis};
+        if (p->integrator == MTSG_INTEGRATOR_PATH2_OM && !d->om) throw std::runtime_error("myPath2_OM: the scene has no occupancy maps");
         int T = hwThreads(threads);
         const int BS = 32;   // scene.cpp:27 block size
         int nbx = (p->tile_w + BS - 1) / BS, nby = (p->tile_h + BS - 1) / BS;
@@ -2538,6 +2706,16 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
                         }
                         for (uint32_t s = 0; s < p->spp; ++s) {
                             smp.begin(&qmc, p->seed, cam.film_w, p->spp, x, y, s);
+                            if (p->integrator == MTSG_INTEGRATOR_PATH2_OM) {
+                                // myPath2_OM.cpp:243-256: jittered (or centred) sample, sensor->sampleRay
+                                float a = 0.5f, b = 0.5f;
+                                if (p->om_jitter) smp.next2D(a, b);
+                                const float spx = x + a, spy = y + b;
+                                const Spec L = LiOM(sv, omp, cameraRay(cam, spx, spy), smp);
+                                samples[tid]++;
+                                blk.put(spx, spy, L, 1.0f);
+                                continue;
+                            }
                             float a, b;
                             smp.next2D(a, b);
                             float spx = x + a, spy = y + b;
@@ -2686,6 +2864,18 @@ int oracle_env_eval_n(const mtsg_scene_desc *d, uint32_t n, const float *dir, co
         const Spec v = sv.envEvalEnvironment(r, diff, diff ? Vec(rx[3 * i], rx[3 * i + 1], rx[3 * i + 2]) : Vec(0.0f),
                                              diff ? Vec(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]) : Vec(0.0f));
         out[3 * i] = v.s[0]; out[3 * i + 1] = v.s[1]; out[3 * i + 2] = v.s[2];
+    }
+    return 0;
+}
+
+/* myPath2_OM's visibility query (nearestOMindex + Visible), as mtsg_om_query */
+int oracle_om_query_n(const mtsg_scene_desc *d, uint32_t n, const float *dirs, const float *o1, const float *o2, int32_t *ids,
+                      int32_t *vis) {
+    if (!d || !d->om) { g_err = "scene has no occupancy maps"; return -1; }
+    for (uint32_t i = 0; i < n; ++i) {
+        Vec dd(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+        ids[i] = omNearestIndex(dd);
+        vis[i] = omVisible(*d, ids[i], Vec(o1[3 * i], o1[3 * i + 1], o1[3 * i + 2]), Vec(o2[3 * i], o2[3 * i + 1], o2[3 * i + 2])) ? 1 : 0;
     }
     return 0;
 }

@@ -139,3 +139,16 @@ def tex_eval(desc, tex: int, uv: np.ndarray, duv: np.ndarray | None = None) -> n
     if L.oracle_tex_eval_n(desc, tex, uv.shape[0], _p(uv), pd, _p(out)) != 0:
         raise RuntimeError(L.oracle_last_error().decode())
     return out
+
+
+def om_query(desc, dirs: np.ndarray, o1: np.ndarray, o2: np.ndarray):
+    """myPath2_OM's nearestOMindex + Visible (oracle_om_query_n): (ids, vis)."""
+    L = lib()
+    dirs, o1, o2 = (np.ascontiguousarray(a, dtype=np.float32) for a in (dirs, o1, o2))
+    n = dirs.shape[0]
+    ids = np.empty(n, np.int32)
+    vis = np.empty(n, np.int32)
+    L.oracle_om_query_n.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    if L.oracle_om_query_n(desc, n, _p(dirs), _p(o1), _p(o2), _p(ids), _p(vis)) != 0:
+        raise RuntimeError(L.oracle_last_error().decode())
+    return ids, vis
