@@ -11,7 +11,7 @@ JOBS    ?= 8
 
 HOST_SRC := $(wildcard $(PKG)/host/*.cpp)
 HOST_HDR := $(wildcard $(PKG)/host/*.h) $(PKG)/host/ior_table.inc include/mtsg.h include/mtsh.h
-DEV_SRC  := $(PKG)/csrc/mtsg.hip $(PKG)/csrc/smp_kernels.hip
+DEV_SRC  := $(PKG)/csrc/mtsg.hip $(PKG)/csrc/smp_kernels.hip $(PKG)/csrc/kdbuild.hip
 DEV_HDR  := $(wildcard $(PKG)/csrc/*.h) include/mtsg.h
 
 HOST_LIB := $(PKG)/libmtsg_host.so
@@ -43,8 +43,11 @@ $(HOST_LIB): $(HOST_SRC) $(HOST_HDR) $(SOBOL_BIN)
 # k_finish occupancy query).  DEV_EXTRA / DEV_OBJ: measurement variants.
 DEV_FLAGS := -O3 -std=c++17 -fPIC -Wall -ffp-contract=off -munsafe-fp-atomics -Wno-unused-value -Wno-unused-result
 DEV_OBJ   ?= build/dev
-DEV_OBJS  := $(DEV_OBJ)/mtsg.o $(foreach k,0 1 2 3 4,$(DEV_OBJ)/smp_$(k).o)
+DEV_OBJS  := $(DEV_OBJ)/mtsg.o $(DEV_OBJ)/kdbuild.o $(foreach k,0 1 2 3 4,$(DEV_OBJ)/smp_$(k).o)
 $(DEV_OBJ)/mtsg.o: $(PKG)/csrc/mtsg.hip $(DEV_HDR)
+	@mkdir -p $(DEV_OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) $(DEV_EXTRA) -c -o $@ $<
+$(DEV_OBJ)/kdbuild.o: $(PKG)/csrc/kdbuild.hip include/mtsg.h
 	@mkdir -p $(DEV_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) $(DEV_EXTRA) -c -o $@ $<
 $(DEV_OBJ)/smp_%.o: $(PKG)/csrc/smp_kernels.hip $(DEV_HDR)

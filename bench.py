@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="bunny15", choices=["bunny15", "cbox", "c5"])
     ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--kd-build", default="host", choices=["host", "device"],
+                    help="top-level kd-tree: the host SAH build (default) or the GPU build (mtsg_kd_build)")
     ap.add_argument("--instancing", default="flatten", choices=["flatten", "two-level"],
                     help="C3's 15 bunny instances: world-space copies in one tree, or Mitsuba's two-level structure")
     ap.add_argument("--width", type=int, default=1280)
@@ -231,6 +233,13 @@ def main():
     t_load = time.time()
     scene = mtsg.Scene(path, defs, instancing=a.instancing)
     load_s = time.time() - t_load
+    kd_info = {"kd_build": "host", "kd_build_ms": round(scene.info.kd_build_seconds * 1e3, 1), "kd_refs": scene.info.kd_indices}
+    if a.kd_build == "device":
+        mtsg.kd_build(scene, device=local if world > 1 else 0)   # warm-up
+        tree = mtsg.kd_build(scene, device=local if world > 1 else 0)
+        scene.set_kdtree(tree)
+        kd_info = {"kd_build": "device", "kd_build_ms": round(tree["ms"], 1), "kd_refs": int(tree["indices"].size),
+                   "host_kd_build_ms": round(scene.info.kd_build_seconds * 1e3, 1)}
     border = scene.border
     params = scene.params()
     params.tile_stride = world
@@ -372,7 +381,7 @@ def main():
                        "max_depth": 64 if a.workload == "c5" else 8,
                        "samples_per_step": params.tile_w * params.tile_h * params.spp,
                        "parallelism": f"film tiles round-robin over {world} GPU(s)",
-                       "scene_load_s": round(load_s, 2)},
+                       "scene_load_s": round(load_s, 2), **kd_info},
             **({"emulated_ranks": a.emulate_ranks,
                 "note": "one GPU rendering rank 0's 1/N tile share; value = frame samples / that time"}
                if a.emulate_ranks > 1 and world == 1 else {}),

@@ -563,6 +563,39 @@ int  mtsg_tex_eval(mtsg_scene *scene, int tex, uint32_t n, const float *uv, cons
 int  mtsg_om_query(mtsg_scene *scene, uint32_t n, const float *dirs, const float *o1, const float *o2, int32_t *ids,
                    int32_t *vis);
 
+/* ---- device-side SAH kd-tree build ----------------------
+ * GenericKDTree::build (include/mitsuba/render/gkdtree.h:958-1240) on the
+ * GPU: breadth-first min-max binned SAH (32 bins per axis) with Mitsuba's
+ * costs, straddling triangles clipped to the children (perfect splits).
+ * Input: the scene's n_prims primitives as 6 floats each (min xyz, max xyz;
+ * an empty box leaves the primitive out), in the order of scene->triaccel,
+ * and its triangles (vtx_pos / tri_idx) for the clipping.
+ * Output: host arrays in the mtsg_kdnode / index encoding of the scene
+ * descriptor, the enlarged tree AABB, the deepest leaf and the build time
+ * (ms, uploads and downloads included).  Free with mtsg_kd_free. */
+typedef struct mtsg_kd_build_params {
+    float traversal_cost;         /* 15 (gkdtree.h:734-744)                  */
+    float query_cost;             /* 20                                      */
+    float empty_space_bonus;      /* 0.9                                     */
+    int32_t stop_prims;           /* 6                                       */
+    int32_t max_depth;            /* 0: 8 + 1.3 log2i(N)                     */
+    int32_t pad;
+} mtsg_kd_build_params;
+
+typedef struct mtsg_kd_tree {
+    mtsg_kdnode *nodes;
+    uint32_t n_nodes;
+    uint32_t *indices;
+    uint32_t n_indices;
+    float aabb_min[3], aabb_max[3];
+    uint32_t max_depth, leaves;
+    double ms_build;
+} mtsg_kd_tree;
+
+int  mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bounds, const mtsg_kd_build_params *params,
+                   mtsg_kd_tree *out);
+void mtsg_kd_free(mtsg_kd_tree *tree);
+
 /* Debug: the scene sampler's draws for sample s of film pixel (x, y): kinds[i]
  * = 1 (next1D, one float out) or 2 (next2D, two floats), in call order, as
  * Sampler::next1D / next2D after Sampler::generate(pos) + setSampleIndex(s)

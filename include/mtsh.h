@@ -65,6 +65,17 @@ int mtsh_scene_textures(const mtsh_scene *scene, mtsg_texture *out, int capacity
  * Returns 0, -1 without maps, -2 when capacity is too small. */
 int mtsh_scene_om(const mtsh_scene *scene, mtsg_om *om, uint32_t *bits, size_t capacity);
 
+/* The top-level kd-tree's primitive boxes, 6 floats each (min xyz, max xyz;
+ * an empty box for primitives it leaves out: degenerate triangles, shape
+ * group triangles): the input of mtsg_kd_build.  Returns the primitive
+ * count (out may be NULL), -2 when capacity is too small. */
+int64_t mtsh_scene_prim_bounds(const mtsh_scene *scene, float *out, size_t capacity);
+
+/* Replace the scene's top-level kd-tree (e.g. by mtsg_kd_build's) in its
+ * descriptor; the arrays are copied.  Returns 0 or -1. */
+int mtsh_scene_set_kdtree(mtsh_scene *scene, const mtsg_kdnode *nodes, uint32_t n_nodes, const uint32_t *indices,
+                          uint32_t n_indices, const float *aabb_min, const float *aabb_max, uint32_t max_depth);
+
 /* hdrfilm develop (fmtconv.cpp:962-974): rgb = (sum w*L) / (sum w). */
 void mtsh_develop(const float *rgbaw, int w, int h, float *rgb_out);
 

@@ -1282,6 +1282,10 @@ int mtsg_om_query(mtsg_scene *s, uint32_t n, const float *dirs, const float *o1,
 
 }  // extern "C"
 
+namespace mtsg {
+void set_last_error(const std::string &e) { g_err = e; }   // kdbuild.hip
+}
+
 namespace {
 __global__ void k_sampler_draws(DevIntegrator I, int x, int y, uint32_t s, uint32_t n, const int32_t *kinds, float *out,
                                 int *err) {

@@ -145,6 +145,34 @@ void setRow34(float *dst, const Transform &t, bool inverse) {
 
 }  // namespace
 
+// The top-level tree's primitive boxes (6 floats each; empty for primitives
+// it leaves out): the input of the device build (mtsg_kd_build)
+void Scene::primBounds(std::vector<float> &out) const {
+    ScenePrims src(*this, triGrouped);
+    out.assign(src.count() * 6, 0.0f);
+    for (size_t i = 0; i < src.count(); ++i) {
+        const AABB b = src.bounds(i);
+        float *o = &out[6 * i];
+        if (!b.valid()) { o[0] = 1; o[3] = -1; continue; }
+        for (int k = 0; k < 3; ++k) { o[k] = b.mn[k]; o[3 + k] = b.mx[k]; }
+    }
+}
+
+// Replace the top-level tree (a device-built one) and point the descriptor at it
+void Scene::setTree(const mtsg_kdnode *nodes, uint32_t nNodes, const uint32_t *indices, uint32_t nIndices, const float *aabbMin,
+                    const float *aabbMax, uint32_t maxDepth) {
+    tree.nodes.assign(nodes, nodes + nNodes);
+    tree.indices.assign(indices, indices + nIndices);
+    for (int k = 0; k < 3; ++k) { tree.aabb.mn[k] = aabbMin[k]; tree.aabb.mx[k] = aabbMax[k]; }
+    tree.maxDepth = maxDepth;
+    desc.n_nodes = nNodes;
+    desc.nodes = tree.nodes.data();
+    desc.n_indices = nIndices;
+    desc.indices = tree.indices.data();
+    for (int k = 0; k < 3; ++k) { desc.aabb_min[k] = aabbMin[k]; desc.aabb_max[k] = aabbMax[k]; }
+    desc.max_depth = maxDepth;
+}
+
 void Scene::finalize() {
     // ---------------- geometry ----------------
     vtxPos.clear(); vtxNrm.clear(); triIdx.clear(); triDpdu.clear(); triUv.clear(); triDpdv.clear();
@@ -294,7 +322,8 @@ void Scene::finalize() {
     // ---------------- TriAccel + kd-tree ----------------
     const size_t nInst = instances.size();
     triaccel.assign(nTri + rectDesc.size() + nInst, mtsg_triaccel{});
-    std::vector<uint8_t> grouped(nTri, 0);
+    triGrouped.assign(nTri, 0);
+    std::vector<uint8_t> &grouped = triGrouped;
     std::vector<std::vector<uint32_t>> groupTris(groups.size());
     for (size_t si = 0; si < shapeDesc.size(); ++si) {
         const mtsg_shape &sd = shapeDesc[si];

@@ -76,6 +76,29 @@ int mtsh_scene_textures(const mtsh_scene *s, mtsg_texture *out, int capacity) {
     return n;
 }
 
+int64_t mtsh_scene_prim_bounds(const mtsh_scene *s, float *out, size_t capacity) {
+    std::vector<float> b;
+    s->scene->primBounds(b);
+    if (out) {
+        if (capacity < b.size()) { g_err = "mtsh_scene_prim_bounds: buffer too small"; return -2; }
+        std::copy(b.begin(), b.end(), out);
+    }
+    return (int64_t)(b.size() / 6);
+}
+
+int mtsh_scene_set_kdtree(mtsh_scene *s, const mtsg_kdnode *nodes, uint32_t n_nodes, const uint32_t *indices, uint32_t n_indices,
+                          const float *aabb_min, const float *aabb_max, uint32_t max_depth) {
+    if (!s || !nodes || !n_nodes || (n_indices && !indices) || !aabb_min || !aabb_max) {
+        g_err = "mtsh_scene_set_kdtree: invalid arguments";
+        return -1;
+    }
+    const uint32_t nPrims = s->scene->desc.n_prims;
+    for (uint32_t i = 0; i < n_indices; ++i)
+        if (indices[i] >= nPrims) { g_err = "mtsh_scene_set_kdtree: index out of range"; return -1; }
+    s->scene->setTree(nodes, n_nodes, indices, n_indices, aabb_min, aabb_max, max_depth);
+    return 0;
+}
+
 int mtsh_scene_om(const mtsh_scene *s, mtsg_om *om, uint32_t *bits, size_t capacity) {
     const mtsh::Scene &sc = *s->scene;
     if (sc.omBits.empty()) { g_err = "the scene has no occupancy maps"; return -1; }

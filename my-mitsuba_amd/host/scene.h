@@ -184,7 +184,12 @@ struct Scene {
     mtsg_camera camera{};
     mtsg_scene_desc desc{};
 
+    std::vector<uint8_t> triGrouped;  // triangle lives in a shape group's own tree (two-level)
+
     void finalize();                  // normals, tangents, CDFs, kd-tree, desc
+    void primBounds(std::vector<float> &out) const;
+    void setTree(const mtsg_kdnode *nodes, uint32_t nNodes, const uint32_t *indices, uint32_t nIndices, const float *aabbMin,
+                 const float *aabbMax, uint32_t maxDepth);
 };
 
 extern int g_defaultKDThreads;   // 0 = hardware concurrency

@@ -82,6 +82,40 @@ class MipMapHeader(C.Structure):
     ]
 
 
+class KDBuildParams(C.Structure):
+    """mtsg_kd_build_params (include/mtsg.h)."""
+    _fields_ = [("traversal_cost", C.c_float), ("query_cost", C.c_float), ("empty_space_bonus", C.c_float),
+                ("stop_prims", C.c_int32), ("max_depth", C.c_int32), ("pad", C.c_int32)]
+
+
+class KDTree(C.Structure):
+    """mtsg_kd_tree (include/mtsg.h)."""
+    _fields_ = [("nodes", C.POINTER(C.c_uint32)), ("n_nodes", C.c_uint32), ("indices", C.POINTER(C.c_uint32)),
+                ("n_indices", C.c_uint32), ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3),
+                ("max_depth", C.c_uint32), ("leaves", C.c_uint32), ("ms_build", C.c_double)]
+
+
+def kd_build(scene: "Scene", bounds: np.ndarray | None = None, device: int = 0, **params) -> dict:
+    """SAH kd-tree over the scene's primitives built on the GPU (mtsg_kd_build);
+    bounds: their boxes (n, 6), by default scene.prim_bounds()."""
+    lib = device_lib()
+    b = np.ascontiguousarray(scene.prim_bounds() if bounds is None else bounds, dtype=np.float32)
+    p = KDBuildParams(15.0, 20.0, 0.9, 6, 0, 0)
+    for k, v in params.items():
+        setattr(p, k, v)
+    t = KDTree()
+    if lib.mtsg_kd_build(device, scene.desc, _ptr(b), C.byref(p), C.byref(t)) != 0:
+        raise RuntimeError(_err(lib, "mtsg_last_error"))
+    try:
+        out = dict(nodes=np.ctypeslib.as_array(t.nodes, (t.n_nodes * 2,)).reshape(-1, 2).copy(),
+                   indices=np.ctypeslib.as_array(t.indices, (max(t.n_indices, 1),))[:t.n_indices].copy(),
+                   aabb_min=np.array(t.aabb_min[:], np.float32), aabb_max=np.array(t.aabb_max[:], np.float32),
+                   max_depth=t.max_depth, leaves=t.leaves, ms=t.ms_build)
+    finally:
+        lib.mtsg_kd_free(C.byref(t))
+    return out
+
+
 class OMHeader(C.Structure):
     """mtsg_om (include/mtsg.h)."""
     _fields_ = [("aabb_min", C.c_float * 3), ("grid_size_recp", C.c_float), ("center", C.c_float * 3), ("pad", C.c_float),
@@ -115,13 +149,15 @@ DEVICE_SYMBOLS = [
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
-    "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_sampler_draws", "mtsg_debug_wavetimes",
+    "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_kd_build", "mtsg_kd_free",
+    "mtsg_sampler_draws", "mtsg_debug_wavetimes",
     "mtsg_debug_stragglers",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
-    "mtsh_read_image", "mtsh_clip_triangle", "mtsh_texture_image", "mtsh_build_mipmap", "mtsh_scene_textures", "mtsh_scene_om", "mtsh_last_error",
+    "mtsh_read_image", "mtsh_clip_triangle", "mtsh_texture_image", "mtsh_build_mipmap", "mtsh_scene_textures", "mtsh_scene_om", "mtsh_scene_prim_bounds", "mtsh_scene_set_kdtree",
+    "mtsh_last_error",
 ]
 PATH_SYMBOLS = [
     "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
@@ -175,6 +211,10 @@ def host_lib() -> C.CDLL:
         lib.mtsh_clip_triangle.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsh_scene_textures.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         lib.mtsh_scene_om.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.mtsh_scene_prim_bounds.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.mtsh_scene_prim_bounds.restype = C.c_int64
+        lib.mtsh_scene_set_kdtree.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p,
+                                              C.c_void_p, C.c_uint32]
         lib.mtsh_texture_image.argtypes = [C.c_char_p, C.c_float, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_void_p,
                                            C.c_size_t]
         lib.mtsh_build_mipmap.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
@@ -215,6 +255,8 @@ def device_lib() -> C.CDLL:
         lib.mtsg_render_samples.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
         lib.mtsg_env_eval.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_tex_eval.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.mtsg_kd_build.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.POINTER(KDBuildParams), C.POINTER(KDTree)]
+        lib.mtsg_kd_free.argtypes = [C.POINTER(KDTree)]
         lib.mtsg_om_query.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_sampler_draws.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int, C.c_uint32,
                                            C.c_uint32, C.c_void_p, C.c_void_p]
@@ -269,6 +311,27 @@ class Scene:
     @property
     def border(self) -> int:
         return self.info.border
+
+    def prim_bounds(self) -> np.ndarray:
+        """The top-level kd-tree's primitive boxes (n, 6); empty boxes mark
+        primitives the tree leaves out."""
+        lib = host_lib()
+        n = lib.mtsh_scene_prim_bounds(self._h, None, 0)
+        out = np.zeros((n, 6), np.float32)
+        if lib.mtsh_scene_prim_bounds(self._h, _ptr(out), out.size) != n:
+            raise RuntimeError(_err(lib, "mtsh_last_error"))
+        return out
+
+    def set_kdtree(self, tree: dict) -> None:
+        """Install a kd-tree (kd_build's dict) as the scene's top-level tree."""
+        lib = host_lib()
+        nodes = np.ascontiguousarray(tree["nodes"], dtype=np.uint32)
+        idx = np.ascontiguousarray(tree["indices"], dtype=np.uint32)
+        lo = np.ascontiguousarray(tree["aabb_min"], dtype=np.float32)
+        hi = np.ascontiguousarray(tree["aabb_max"], dtype=np.float32)
+        if lib.mtsh_scene_set_kdtree(self._h, _ptr(nodes), nodes.shape[0], _ptr(idx), idx.size, _ptr(lo), _ptr(hi),
+                                     int(tree["max_depth"])) != 0:
+            raise RuntimeError(_err(lib, "mtsh_last_error"))
 
     def occupancy_maps(self):
         """myPath2_OM's maps: (header OMHeader, bits (16, 256, 256, 8) uint32)."""
