@@ -64,6 +64,9 @@ struct DevScene {
     const float *__restrict__ tex_texels;
     const float4 *__restrict__ ttex;
     int cam_diffs;        // bounce 0 carries the camera's ray differentials in T / aux
+    // two-level traversal: per-lane save slots of the top-level state
+    // (SAVE_WORDS words per lane of the traversal grid); nullptr: no instances
+    uint32_t *__restrict__ instSave;
     // myPath2_OM occupancy maps (om.cpp; nullptr unless that integrator)
     const mtsg_om *__restrict__ om;
     const uint32_t *__restrict__ om_bits;
@@ -694,13 +697,24 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
 // instance they were found in.
 // ---------------------------------------------------------------------------
 constexpr int OUTER_STACK = 2;
-constexpr int SAVE_WORDS = 11;   // cur.x, cur.y, tmin, tmax, lfE, lfEnd, lfTmax, bits, instance, root.x, root.y
+// the top-level state saved while a lane is inside an instance: cur.x, cur.y,
+// tmin, tmax, lfE, lfEnd, lfTmax, bits, instance.  It lives in a per-lane
+// global slot (S.instSave, word k of lane g at k * lanes + g), not in LDS:
+// written on entry, read on exit, and the LDS then holds only the two stacks
+// (6 KB per wave instead of 8.8 KB: 6 waves per SIMD instead of 4)
+constexpr int SAVE_WORDS = 9;
 __shared__ uint2 s_outNode[OUTER_STACK * TRACE_BLOCK];
 __shared__ float s_outT[OUTER_STACK * TRACE_BLOCK];
-__shared__ uint32_t s_save[SAVE_WORDS * TRACE_BLOCK];
 enum : uint32_t { SB_INST = 1u << 22 };
 
-DEV uint32_t &save_word(uint32_t k) { return s_save[k * TRACE_BLOCK + lane_here()]; }
+DEV uint32_t &save_word(const DevScene &S, uint32_t k) {
+    return S.instSave[(size_t)k * (gridDim.x * TRACE_BLOCK) + blockIdx.x * TRACE_BLOCK + lane_here()];
+}
+// the group tree's root words of instance ii (its 8-float4 record, words 6.w / 7.w)
+DEV uint2 inst_root(const DevScene &S, uint32_t ii) {
+    const float4 *I = S.inst + 8 * (size_t)ii;
+    return make_uint2(__float_as_uint(I[6].w), __float_as_uint(I[7].w));
+}
 
 // push the far child onto the stack of the lane's level (circular, drops
 // the oldest entry when full)
@@ -723,15 +737,15 @@ DEV uint2 spec_take_i(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bo
 
 // back to the top level after a group traversal: restore the saved state,
 // keep the hit flag, reload the world-space ray
-DEV void inst_exit(SpecRay &r, const float4 *wo, const float4 *wd) {
+DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4 *wd) {
     const uint32_t found = r.bits & SB_FOUND;
-    r.cur = make_uint2(save_word(0), save_word(1));
-    r.tmin = __uint_as_float(save_word(2));
-    r.tmax = __uint_as_float(save_word(3));
-    r.lfE = save_word(4);
-    r.lfEnd = save_word(5);
-    r.lfTmax = __uint_as_float(save_word(6));
-    r.bits = save_word(7) | found;
+    r.cur = make_uint2(save_word(S, 0), save_word(S, 1));
+    r.tmin = __uint_as_float(save_word(S, 2));
+    r.tmax = __uint_as_float(save_word(S, 3));
+    r.lfE = save_word(S, 4);
+    r.lfEnd = save_word(S, 5);
+    r.lfTmax = __uint_as_float(save_word(S, 6));
+    r.bits = save_word(S, 7) | found;
     float4 ro = ldS(wo), rd = ldS(wd);
     r.o = xyz(ro);
     r.d = xyz(rd);
@@ -773,7 +787,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
                 if (r.bits & SB_SHADOW) return true;   // any hit occludes
                 r.best = t;
                 stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
-                *instOut = (r.bits & SB_INST) ? save_word(8) : 0xFFFFFFFFu;
+                *instOut = (r.bits & SB_INST) ? save_word(S, 8) : 0xFFFFFFFFu;
             }
         }
         ++r.lfE;
@@ -819,18 +833,16 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
         }
         const float t0 = fmaxf(r.mint, nearT), t1 = fminf(r.best, farT);
         if (ok & (nearT <= farT) & (t1 > t0)) {
-            save_word(0) = r.cur.x;
-            save_word(1) = r.cur.y;
-            save_word(2) = __float_as_uint(r.tmin);
-            save_word(3) = __float_as_uint(r.tmax);
-            save_word(4) = r.lfE;
-            save_word(5) = r.lfEnd;
-            save_word(6) = __float_as_uint(r.lfTmax);
-            save_word(7) = r.bits & ~SB_FOUND;
-            save_word(8) = ii;
+            save_word(S, 0) = r.cur.x;
+            save_word(S, 1) = r.cur.y;
+            save_word(S, 2) = __float_as_uint(r.tmin);
+            save_word(S, 3) = __float_as_uint(r.tmax);
+            save_word(S, 4) = r.lfE;
+            save_word(S, 5) = r.lfEnd;
+            save_word(S, 6) = __float_as_uint(r.lfTmax);
+            save_word(S, 7) = r.bits & ~SB_FOUND;
+            save_word(S, 8) = ii;
             const uint2 root = make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w));
-            save_word(9) = root.x;
-            save_word(10) = root.y;
             r.o = lo;
             r.d = ld;
             r.inv = li;
@@ -849,7 +861,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
     const bool leafDone = (r.lfTmax >= 0.0f) & (r.lfE >= r.lfEnd);
     if (leafDone & found & (r.best < r.lfTmax)) {
         if (!inInst) return true;
-        inst_exit(r, wo, wd);
+        inst_exit(S, r, wo, wd);
         return false;
     }
     r.lfTmax = leafDone ? -1.0f : r.lfTmax;
@@ -859,7 +871,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
         const bool nonEmpty = st < c.y;
         if (!nonEmpty & found & (r.best < r.tmax)) {
             if (!inInst) return true;
-            inst_exit(r, wo, wd);
+            inst_exit(S, r, wo, wd);
             return false;
         }
         r.lfE = nonEmpty ? st : r.lfE;
@@ -880,7 +892,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
             const float t0 = r.tmax;
             r.tmin = restart ? t0 : r.tmin;
             r.tmax = restart ? r.best : r.tmax;
-            const uint2 root = inInst ? make_uint2(save_word(9), save_word(10)) : S.root2;
+            const uint2 root = inInst ? inst_root(S, save_word(S, 8)) : S.root2;
             r.cur = restart ? root : c;
             if (COUNT && restart) cnt.restarts++;
             r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
@@ -888,7 +900,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
     }
     const bool done = (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
     if (done && inInst) {
-        inst_exit(r, wo, wd);
+        inst_exit(S, r, wo, wd);
         return false;
     }
     return done;

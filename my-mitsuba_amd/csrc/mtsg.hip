@@ -998,6 +998,17 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     perCU = 0;
     if ((perCU = finish_blocks_per_cu()) <= 0) perCU = 4;
     s->finishGrid = s->cuCount * perCU;
+    // two-level traversal: the per-lane save slots of its grid (kernels.h save_word)
+    s->ds.instSave = nullptr;
+    if (s->ds.inst) {
+        uint32_t *save = nullptr;
+        if (hipMalloc((void **)&save, (size_t)SAVE_WORDS * s->traceGridInst * TRACE_BLOCK * sizeof(uint32_t)) != hipSuccess) {
+            g_err = "out of device memory (instance save slots)";
+            return fail(MTSG_ERR_OOM);
+        }
+        s->allocs.push_back(save);
+        s->ds.instSave = save;
+    }
     s->finishPaths = MTSG_DEFAULT_FINISH_PATHS;
     if (const char *f = getenv("MTSG_FINISH")) s->finishPaths = (uint32_t)strtoul(f, nullptr, 0);
     if (const char *f = getenv("MTSG_FINISH_SHADE_MIN")) s->finishShadeMin = std::max(1, atoi(f));
