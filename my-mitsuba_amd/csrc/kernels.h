@@ -1094,10 +1094,10 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
                 // bounce 0 is shaded
                 stS(&P.T[slot], make_float4(rxs.x, rxs.y, rxs.z, 1.f));
                 stS(&P.aux[slot], make_float4(rys.x, rys.y, rys.z, 0.f));
-            } else {
-                stS(&P.T[slot], make_float4(1.f, 1.f, 1.f, 1.f));
+                stS(&P.Lp[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
             }
-            stS(&P.Lp[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
+            // otherwise T = 1 and Lp = (0, 0, 0, 1) are implied at bounce 0
+            // (shade_path `fresh`): 32 B per camera path neither written nor read
             // depth 1; the jitter used 2 dimensions in one 2D request
             stS(&P.meta[slot], jitter ? make_uint4(1u, 2u, slot, 1u) : make_uint4(1u, 0u, slot, 0u));
         } else {
@@ -1940,8 +1940,11 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
     const float4 h = ldS(&P.hit[i]);
     const float4 ro4 = ldS(&P.ray_o[i]), rd4 = ldS(&P.ray_d[i]);
     const float3 ro = xyz(ro4), rd = xyz(rd4);
-    float4 L4 = ldS(&P.Lp[i]);
-    float4 T4 = ldS(&P.T[i]);
+    // a camera path starts with L = 0, alpha 1, T = 1, eta = 1: k_camera writes
+    // neither array then (T holds the ray differentials when cam_diffs)
+    const bool fresh = first && !S.cam_diffs;
+    float4 L4 = fresh ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
+    float4 T4 = fresh ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
     PathSampler smp;
     {
         int x, y;
@@ -2221,8 +2224,8 @@ DEV void shade_path_om(const DevScene &S, const DevIntegrator &I, const DevBatch
     const uint32_t slot = meta.z;
     const float4 h = ldS(&P.hit[i]);
     const float3 ro = xyz(ldS(&P.ray_o[i])), rd = xyz(ldS(&P.ray_d[i]));
-    const float4 L4 = ldS(&P.Lp[i]);
-    const float4 T4 = ldS(&P.T[i]);
+    const float4 L4 = first ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);   // camera paths: see shade_path
+    const float4 T4 = first ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
     PathSampler smp;
     {
         int x, y;
