@@ -257,6 +257,11 @@ constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per l
 #define MTSG_SPEC_WAVES 8
 #endif
 #define SPEC_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SPEC_WAVES)))
+// the two-level kernel: its LDS (group stack + top-level stack, 5.25 KB/wave)
+// allows 7 waves/SIMD, so it is given the registers of 7 (72)
+#ifndef MTSG_INST_WAVES
+#define MTSG_INST_WAVES 7
+#endif
 // streaming (non-temporal) access to the per-path SoA state: the state of a
 // 32M-path batch is GBs per bounce and would otherwise evict the kd-tree from
 // the 256 MB Infinity Cache (experiment switch MTSG_NT)
@@ -703,8 +708,16 @@ constexpr int OUTER_STACK = 2;
 // written on entry, read on exit, and the LDS then holds only the two stacks
 // (6 KB per wave instead of 8.8 KB: 6 waves per SIMD instead of 4)
 constexpr int SAVE_WORDS = 9;
+// the group level's own stack, one entry shorter than the flat traversal's:
+// 5 x 12 B + 2 x 12 B per lane = 5.25 KB per wave, 7 waves/SIMD
+#ifndef MTSG_INNER_STACK
+#define MTSG_INNER_STACK 5
+#endif
+constexpr int INNER_STACK = MTSG_INNER_STACK;
 __shared__ uint2 s_outNode[OUTER_STACK * TRACE_BLOCK];
 __shared__ float s_outT[OUTER_STACK * TRACE_BLOCK];
+__shared__ uint2 s_grpNode[INNER_STACK * TRACE_BLOCK];
+__shared__ float s_grpT[INNER_STACK * TRACE_BLOCK];
 enum : uint32_t { SB_INST = 1u << 22 };
 
 DEV uint32_t &save_word(const DevScene &S, uint32_t k) {
@@ -724,9 +737,9 @@ DEV uint2 spec_take_i(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bo
         const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
         const uint32_t b = r.bits, top = b & SB_TOP;
         const bool inner = (b & SB_INST) != 0;
-        const uint32_t cap = inner ? (uint32_t)SHORT_STACK : (uint32_t)OUTER_STACK;
+        const uint32_t cap = inner ? (uint32_t)INNER_STACK : (uint32_t)OUTER_STACK;
         const uint32_t i = top * TRACE_BLOCK + lane_here();
-        if (inner) { s_specNode[i] = other; s_specT[i] = r.tmax; }
+        if (inner) { s_grpNode[i] = other; s_grpT[i] = r.tmax; }
         else { s_outNode[i] = other; s_outT[i] = r.tmax; }
         const bool full = (b & SB_N) == cap * SB_N1;
         r.bits = ((b & ~SB_TOP) | (top == cap - 1 ? 0u : top + 1u)) + (full ? SB_DROPPED - (b & SB_DROPPED) : SB_N1);
@@ -753,8 +766,7 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
 }
 
 template <bool COUNT>
-DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hitOut, uint32_t *instOut,
-                     const float4 *wo, const float4 *wd) {
+DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevPaths &P, uint32_t idx) {
     const uint2 n = r.cur;
     const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
     const bool prim = r.lfE < r.lfEnd;
@@ -786,8 +798,8 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
                 r.bits |= SB_FOUND;
                 if (r.bits & SB_SHADOW) return true;   // any hit occludes
                 r.best = t;
-                stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
-                *instOut = (r.bits & SB_INST) ? save_word(S, 8) : 0xFFFFFFFFu;
+                stS(P.hit + idx, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
+                P.hitInst[idx] = (r.bits & SB_INST) ? save_word(S, 8) : 0xFFFFFFFFu;
             }
         }
         ++r.lfE;
@@ -859,31 +871,30 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
     const bool found = (r.bits & SB_FOUND) != 0;
     const bool inInst = (r.bits & SB_INST) != 0;
     const bool leafDone = (r.lfTmax >= 0.0f) & (r.lfE >= r.lfEnd);
-    if (leafDone & found & (r.best < r.lfTmax)) {
-        if (!inInst) return true;
-        inst_exit(S, r, wo, wd);
-        return false;
-    }
+    // Havran's exit (held leaf finished, or an empty leaf reached, beyond the
+    // best hit) and the end of the traversal: the ray is done at the top level,
+    // or leaves its instance (one exit point, so inst_exit is inlined once)
+    bool leave = leafDone & found & (r.best < r.lfTmax);
     r.lfTmax = leafDone ? -1.0f : r.lfTmax;
     const uint2 c = r.cur;
-    if ((r.lfTmax < 0.0f) & !(r.bits & SB_TRAVDONE) & (bool)(c.x >> 31)) {
+    if (!leave & (r.lfTmax < 0.0f) & !(r.bits & SB_TRAVDONE) & (bool)(c.x >> 31)) {
         const uint32_t st = c.x & 0x7FFFFFFFu;
         const bool nonEmpty = st < c.y;
-        if (!nonEmpty & found & (r.best < r.tmax)) {
-            if (!inInst) return true;
-            inst_exit(S, r, wo, wd);
-            return false;
-        }
+        leave = !nonEmpty & found & (r.best < r.tmax);
+    }
+    if (!leave & (r.lfTmax < 0.0f) & !(r.bits & SB_TRAVDONE) & (bool)(c.x >> 31)) {
+        const uint32_t st = c.x & 0x7FFFFFFFu;
+        const bool nonEmpty = st < c.y;
         r.lfE = nonEmpty ? st : r.lfE;
         r.lfEnd = nonEmpty ? c.y : r.lfEnd;
         r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
         const uint32_t b = r.bits;
-        const uint32_t cap = inInst ? (uint32_t)SHORT_STACK : (uint32_t)OUTER_STACK;
+        const uint32_t cap = inInst ? (uint32_t)INNER_STACK : (uint32_t)OUTER_STACK;
         if (b & SB_N) {
             const uint32_t top = b & SB_TOP, k = top == 0 ? cap - 1 : top - 1u;
             const uint32_t i = k * TRACE_BLOCK + lane_here();
-            r.cur = inInst ? s_specNode[i] : s_outNode[i];
-            const float t = inInst ? s_specT[i] : s_outT[i];
+            r.cur = inInst ? s_grpNode[i] : s_outNode[i];
+            const float t = inInst ? s_grpT[i] : s_outT[i];
             r.bits = ((b & ~SB_TOP) | k) - SB_N1;
             r.tmin = r.tmax;
             r.tmax = fminf(t, r.best);
@@ -898,9 +909,10 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
             r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
         }
     }
-    const bool done = (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
+    const bool done = leave || ((r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f);
     if (done && inInst) {
-        inst_exit(S, r, wo, wd);
+        const bool sh = (r.bits & SB_SHADOW) != 0;
+        inst_exit(S, r, (sh ? P.sh_o : P.ray_o) + idx, (sh ? P.sh_d : P.ray_d) + idx);
         return false;
     }
     return done;
@@ -920,7 +932,8 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, float4 *hi
 //   sIn: 0/1 = count in CNT_S0/CNT_S1, -1 = none
 
 template <bool COUNT, int MIN_IDLE, bool INST = false>
-__global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
+__global__ void __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(INST ? (COUNT ? 1 : MTSG_INST_WAVES) : MTSG_SPEC_WAVES)))
+k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
     const SpecStack stk{};
     const unsigned long long tStart = wt ? wall_clock64() : 0ull;
     const uint32_t nC = cIn == -1 ? nIdentity : (cIn >= 0 ? __atomic_load_n(&P.cnt[cnt_q(cIn)], __ATOMIC_RELAXED) : 0u);
@@ -991,9 +1004,8 @@ __global__ void SPEC_ATTR k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, ui
         if (active) {
             if (INST) {
                 const bool sh = (r.bits & SB_SHADOW) != 0;
-                const float4 *wo = (sh ? P.sh_o : P.ray_o) + idx, *wd = (sh ? P.sh_d : P.ray_d) + idx;
-                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P.hit + idx, P.hitInst + idx, wo, wd);
-                else done = spec_iter_i<COUNT>(S, r, cc, P.hit + idx, P.hitInst + idx, wo, wd);
+                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P, idx);
+                else done = spec_iter_i<COUNT>(S, r, cc, P, idx);
             } else {
                 if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx);
                 else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx);
