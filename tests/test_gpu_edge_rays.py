@@ -1,0 +1,113 @@
+"""Degenerate ray queries through the device traversal (mtsg_trace_closest /
+mtsg_trace_shadow -> k_trace_s) against the oracle's Havran restatement:
+- axis-aligned directions and directions with one zero component (the
+  scene-AABB slab test of spec_init takes its `d == 0` branch, aabb.h:308-338;
+  the split-plane distance is +-inf or NaN, sahkdtree3.h:214-228);
+- origins exactly on the scene bounds' faces, moving along the face (grazing)
+  or inward;
+- origins on primitive-bound planes, the candidate planes of the SAH build
+  (gkdtree.h), so many lie exactly on split planes of the tree;
+- empty and reversed intervals (mint >= maxt), which must miss;
+over the flattened C3 scene, the Cornell box and the two-level C3 scene.
+Same primitive => bit-identical t, u, v (compare_closest); occlusion equal."""
+import os
+
+import numpy as np
+import pytest
+
+import mtsg
+from conftest import SCENES
+from oracle import pyoracle as O
+from test_gpu_parity import compare_closest
+
+pytestmark = pytest.mark.gpu
+
+
+def bounds(scene):
+    b = scene.prim_bounds()
+    live = (b[:, :3] <= b[:, 3:]).all(1)
+    return b[live, :3].min(0).astype(np.float32), b[live, 3:].max(0).astype(np.float32)
+
+
+def degenerate_rays(lo, hi, n, seed, planes=None):
+    rng = np.random.default_rng(seed)
+    rays = np.zeros((n, 8), np.float32)
+    ext = hi - lo
+    o = rng.uniform(lo + 0.05 * ext, hi - 0.05 * ext, (n, 3)).astype(np.float32)
+    d = np.zeros((n, 3), np.float32)
+    kind = rng.integers(0, 4, n)
+    # 0: +-axis; 1: one zero component; 2: face origin moving along the face;
+    # 3: face origin moving inward along the axis
+    ax = rng.integers(0, 3, n)
+    sgn = np.where(rng.random(n) < 0.5, -1.0, 1.0).astype(np.float32)
+    idx = np.arange(n)
+    m = kind == 0
+    d[idx[m], ax[m]] = sgn[m]
+    m = (kind == 1) | (kind == 2)
+    v = rng.normal(size=(n, 3)).astype(np.float32)
+    v[idx, ax] = 0.0
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    d[m] = v[m]
+    m = (kind == 2) | (kind == 3)
+    face = np.where(sgn > 0, lo[ax], hi[ax])   # the face the inward axis ray starts on
+    o[idx[m], ax[m]] = face[m]
+    m = kind == 3
+    d[idx[m], ax[m]] = sgn[m]
+    if planes is not None:   # a quarter of the origins on primitive-bound planes
+        m = np.flatnonzero(rng.random(n) < 0.25)
+        k = rng.integers(0, planes.shape[0], m.size)
+        c = rng.integers(0, 6, m.size)
+        o[m, c % 3] = planes[k, c]
+    rays[:, 0:3] = o
+    rays[:, 3:6] = d
+    rays[:, 6] = 1e-4
+    rays[:, 7] = np.inf
+    return rays
+
+
+def planes(scene):
+    b = scene.prim_bounds()
+    return b[(b[:, :3] <= b[:, 3:]).all(1)].astype(np.float32)
+
+
+@pytest.fixture(scope="module", params=["cbox", "bunny15", "bunny15-two-level"])
+def scene_pair(request):
+    name = request.param
+    inst = "two-level" if name.endswith("two-level") else "flatten"
+    xml = "cbox.xml" if name == "cbox" else "bunny15.xml"
+    s = mtsg.Scene(os.path.join(SCENES, xml), {"width": 32, "height": 24, "spp": 1}, instancing=inst)
+    g = mtsg.GPUScene(s, 0)
+    yield s, g
+    g.close()
+
+
+def test_degenerate_closest(scene_pair):
+    s, g = scene_pair
+    lo, hi = bounds(s)
+    rays = degenerate_rays(lo, hi, 60000, 41, planes(s))
+    assert compare_closest(s, g, rays) > 0.1
+
+
+def test_degenerate_shadow(scene_pair):
+    s, g = scene_pair
+    lo, hi = bounds(s)
+    rays = degenerate_rays(lo, hi, 60000, 43, planes(s))
+    rays[:, 7] = np.random.default_rng(44).uniform(0.01, float((hi - lo).max()), len(rays))
+    o0 = O.trace_shadow(s.desc, rays)
+    o1 = g.trace_shadow(rays)
+    assert (o0 != o1).mean() < 1e-4
+    assert 0.01 < o1.mean() < 0.99
+
+
+def test_empty_intervals_miss(scene_pair):
+    s, g = scene_pair
+    lo, hi = bounds(s)
+    rays = degenerate_rays(lo, hi, 4096, 45)
+    rays[:2048, 7] = rays[:2048, 6]          # mint == maxt
+    rays[2048:, 6] = 5.0
+    rays[2048:, 7] = 1.0                     # mint > maxt
+    _, _, _, p = g.trace_closest(rays)
+    assert (p == 0xFFFFFFFF).all()
+    assert not g.trace_shadow(rays).any()
+    _, _, _, p0 = O.trace_closest(s.desc, rays)
+    assert (p0 == 0xFFFFFFFF).all()
