@@ -134,6 +134,22 @@ def cgroup_cpus():
         return None
 
 
+def mitsuba_tree_scene(scene):
+    """The same scene with Mitsuba's own kd-tree parameters (gkdtree.h:734-744:
+    stopPrims 6; this build's GPU-tuned default is 4), so the CPU baseline
+    traverses the tree Mitsuba would build."""
+    import mtsg
+    old = os.environ.get("MTSH_KD_STOP_PRIMS")
+    os.environ["MTSH_KD_STOP_PRIMS"] = "6"
+    try:
+        return mtsg.Scene(scene.path, scene.defines, instancing=scene.instancing)
+    finally:
+        if old is None:
+            del os.environ["MTSH_KD_STOP_PRIMS"]
+        else:
+            os.environ["MTSH_KD_STOP_PRIMS"] = old
+
+
 def cpu_baseline(scene, params, border, target_s):
     """Oracle (faithful C++ restatement, Mitsuba SSE2 flags, SFMT sampler,
     32x32 spiral blocks, one worker per core) timed on a bounded sample of
@@ -150,6 +166,7 @@ def cpu_baseline(scene, params, border, target_s):
     # more threads than the quota only time-slice)
     quota = cgroup_cpus()
     cores = max(1, min(visible, int(quota + 0.999))) if quota else visible
+    scene = mitsuba_tree_scene(scene)
     p = params.copy()
     p.spp = 1
     _, st = O.render(scene.desc, p, border, rng=O.RNG_SFMT, threads=cores, fast=True)

@@ -118,9 +118,15 @@ struct IntegratorProps {
     bool omJitter = true;
 };
 
-struct KDBuildParams {                // gkdtree.h:734-744 defaults
+struct KDBuildParams {                // gkdtree.h:734-744 defaults, except stopPrims
     float traversalCost = 15, queryCost = 20, emptySpaceBonus = 0.9f;
-    int stopPrims = 6, maxBadRefines = 3, minMaxBins = 128;
+    // stopPrims: 4 instead of Mitsuba's 6 (gkdtree.h:738).  The GPU traversal
+    // tests one primitive per iteration while it descends, so a primitive test
+    // costs it more, relative to a node step, than Mitsuba's cost model
+    // assumes: C3 1501 -> 1538 Msamples/s (5.99 instead of 7.24 tests per ray,
+    // DESIGN §3).  Hits do not depend on the tree; MTSH_KD_STOP_PRIMS=6 gives
+    // Mitsuba's tree (the CPU baseline in bench.py is timed on that one).
+    int stopPrims = 4, maxBadRefines = 3, minMaxBins = 128;
     int exactPrimThreshold = 65536;
     int exactSweepLimit = 65536;      // exact O(n log n) sweep below exactPrimThreshold (gkdtree.h:980, 1510), binned above
     bool clip = true;

@@ -294,6 +294,8 @@ class Scene:
         if not self._h:
             raise RuntimeError("scene load failed: " + _err(lib, "mtsh_last_error"))
         self.path = path
+        self.defines = dict(defines or {})
+        self.instancing = instancing
         self.info = SceneInfo()
         lib.mtsh_scene_get_info(self._h, C.byref(self.info))
 

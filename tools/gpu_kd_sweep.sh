@@ -17,6 +17,7 @@ print(f"{sys.argv[2]:>14s} e{sys.argv[3]}: {j['value']:9.1f} Msamples/s  {j['ms_
 PY
   done
 }
+if [ -n "$KD_SWEEP" ]; then eval "$KD_SWEEP"; exit 0; fi
 run default X=1
 run stop3 MTSH_KD_STOP_PRIMS=3
 run stop4 MTSH_KD_STOP_PRIMS=4
@@ -27,3 +28,5 @@ run trav40 MTSH_KD_TRAVERSAL=40
 run empty08 MTSH_KD_EMPTY_BONUS=0.8
 run empty10 MTSH_KD_EMPTY_BONUS=1.0
 run noretract MTSH_KD_RETRACT=0
+run trav60 MTSH_KD_TRAVERSAL=60
+run trav40s3 MTSH_KD_TRAVERSAL=40 MTSH_KD_STOP_PRIMS=3
