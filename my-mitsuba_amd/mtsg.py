@@ -97,10 +97,12 @@ class KDTree(C.Structure):
 
 def kd_build(scene: "Scene", bounds: np.ndarray | None = None, device: int = 0, **params) -> dict:
     """SAH kd-tree over the scene's primitives built on the GPU (mtsg_kd_build);
-    bounds: their boxes (n, 6), by default scene.prim_bounds()."""
+    bounds: their boxes (n, 6), by default scene.prim_bounds().  Costs are
+    Mitsuba's (gkdtree.h:734-744); leaves stop at 4 primitives like the host
+    build's GPU-tuned default (MTSH_KD_STOP_PRIMS overrides both)."""
     lib = device_lib()
     b = np.ascontiguousarray(scene.prim_bounds() if bounds is None else bounds, dtype=np.float32)
-    p = KDBuildParams(15.0, 20.0, 0.9, 6, 0, 0)
+    p = KDBuildParams(15.0, 20.0, 0.9, int(os.environ.get("MTSH_KD_STOP_PRIMS", "4")), 0, 0)
     for k, v in params.items():
         setattr(p, k, v)
     t = KDTree()
