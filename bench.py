@@ -245,6 +245,10 @@ def main():
     a = parse()
     rank, world, local, pg = dist_setup(a.gpus)
     import mtsg
+    # one GPU per rank (LOCAL_RANK); more ranks than visible GPUs share them
+    # round-robin (a rehearsal of the multi-process path on a smaller box)
+    ndev = max(1, mtsg.device_lib().mtsg_device_count())
+    dev = local % ndev if world > 1 else 0
 
     path, defs = scene_args(a)
     t_load = time.time()
@@ -252,8 +256,8 @@ def main():
     load_s = time.time() - t_load
     kd_info = {"kd_build": "host", "kd_build_ms": round(scene.info.kd_build_seconds * 1e3, 1), "kd_refs": scene.info.kd_indices}
     if a.kd_build == "device":
-        mtsg.kd_build(scene, device=local if world > 1 else 0)   # warm-up
-        tree = mtsg.kd_build(scene, device=local if world > 1 else 0)
+        mtsg.kd_build(scene, device=dev)   # warm-up
+        tree = mtsg.kd_build(scene, device=dev)
         scene.set_kdtree(tree)
         kd_info = {"kd_build": "device", "kd_build_ms": round(tree["ms"], 1), "kd_refs": int(tree["indices"].size),
                    "host_kd_build_ms": round(scene.info.kd_build_seconds * 1e3, 1)}
@@ -263,7 +267,7 @@ def main():
     params.tile_offset = rank
     if a.emulate_ranks > 1 and world == 1:
         params.tile_stride = a.emulate_ranks
-    gpu = mtsg.GPUScene(scene, local if world > 1 else 0)
+    gpu = mtsg.GPUScene(scene, dev)
     if a.batch_paths:
         gpu.set_batch_paths(a.batch_paths)
     W, H = params.tile_w + 2 * border, params.tile_h + 2 * border
