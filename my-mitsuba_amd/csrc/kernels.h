@@ -2514,6 +2514,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
     // misses the scene bounds gets its miss record and is shaded next
     auto startClosest = [&]() {
         const float4 ro = ldS(&P.ray_o[idx]), rd = ldS(&P.ray_d[idx]);
+        if (S.inst) P.hitInst[idx] = 0xFFFFFFFFu;   // two-level: no instance until a hit in one
         if (spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, false, r)) {
             state = FS_TRACE;
         } else {
@@ -2569,7 +2570,12 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
             }
         }
         bool done = false;
-        if (state == FS_TRACE) done = spec_iter<false>(S, r, stk, tc, P.hit + idx);
+        if (state == FS_TRACE) {
+            // two-level scenes: the per-lane level switch of k_trace_s<.., true>
+            // (its save slots are sized for this grid too)
+            if (S.inst) done = spec_iter_i<false>(S, r, tc, P, idx);
+            else done = spec_iter<false>(S, r, stk, tc, P.hit + idx);
+        }
         if (done) {
             if (r.bits & SB_SHADOW) {
                 if (!(r.bits & SB_FOUND)) shadow_unoccluded(P, idx);

@@ -432,7 +432,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     // emitters its last BSDF rays found
     const int maxBounces = I.om ? p->max_depth + 1 : (p->max_depth > 0 ? p->max_depth : 1 << 30);
     // tail mode (k_finish): one lane, not in the instrumented, two-level or myPath2_OM modes
-    const bool useFinish = s->finishPaths > 0 && nl == 1 && !count && !s->ds.inst && !I.om;
+    const bool useFinish = s->finishPaths > 0 && nl == 1 && !count && !I.om;
     // bounce b of a lane: one trace launch over this bounce's closest rays
     // (work list qin(b), identity for b = 0) and bounce b-1's shadow rays
     // (S((b-1) & 1)), then k_shade appends the next bounce's paths to
@@ -1002,7 +1002,9 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     s->ds.instSave = nullptr;
     if (s->ds.inst) {
         uint32_t *save = nullptr;
-        if (hipMalloc((void **)&save, (size_t)SAVE_WORDS * s->traceGridInst * TRACE_BLOCK * sizeof(uint32_t)) != hipSuccess) {
+        // slots for the larger of the two grids that switch levels (k_trace_s, k_finish)
+        const size_t lanes = (size_t)std::max(s->traceGridInst, s->finishGrid) * TRACE_BLOCK;
+        if (hipMalloc((void **)&save, (size_t)SAVE_WORDS * lanes * sizeof(uint32_t)) != hipSuccess) {
             g_err = "out of device memory (instance save slots)";
             return fail(MTSG_ERR_OOM);
         }

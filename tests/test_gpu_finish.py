@@ -61,3 +61,18 @@ def test_tail_mode_threshold_switches_late():
     out, st = samples(scene, 20000)
     assert st.launches_finish == 1 and 0 < st.paths_finish < 20000
     assert np.array_equal(ref, out)
+
+
+@pytest.mark.parametrize("name,defs", [
+    ("bunny15.xml", {"width": 160, "height": 90, "spp": 4}),
+    ("bunny15.xml", {"width": 96, "height": 54, "spp": 4, "maxDepth": 16}),
+])
+def test_tail_mode_two_level_is_bit_identical(name, defs):
+    # two-level instancing: the tail kernel switches levels per lane like
+    # k_trace_s<.., true>, with the instance of each hit for the shading
+    scene = mtsg.Scene(os.path.join(SCENES, name), defs, instancing="two-level")
+    ref, st0 = samples(scene, 0)
+    out, st1 = samples(scene, ALWAYS)
+    assert st0.launches_finish == 0
+    assert st1.launches_finish == 1 and st1.paths_finish > 0
+    assert np.array_equal(ref, out), f"{np.count_nonzero((ref != out).any(-1))} samples differ"
