@@ -2660,14 +2660,21 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
                 wy[c] = oky ? C.filter_values[min((int)fabsf(((float)(wyo + c) - py) * C.filter_scale), 31)] : 0.0f;
             }
             const float v[5] = {L.x, L.y, L.z, L.w, 1.0f};
+            {
+                // the K*K*CH window update is the kernel's VALU bound: one FMA
+                // per term instead of a multiply and an add (the film sums
+                // differ from the oracle's by rounding only; the weights and
+                // their lookup above stay uncontracted, so no sample moves)
+#pragma clang fp contract(fast)
 #pragma unroll
-            for (int r = 0; r < K; ++r)
+                for (int r = 0; r < K; ++r)
 #pragma unroll
-                for (int c = 0; c < K; ++c) {
-                    const float w = wx[c] * wy[r];
+                    for (int c = 0; c < K; ++c) {
+                        const float w = wx[c] * wy[r];
 #pragma unroll
-                    for (int h = 0; h < CH; ++h) win[r][c][h] += w * v[CH == 5 ? h : (h == 3 ? 4 : h)];
-                }
+                        for (int h = 0; h < CH; ++h) win[r][c][h] += w * v[CH == 5 ? h : (h == 3 ? 4 : h)];
+                    }
+            }
         }
     }
     __syncthreads();
