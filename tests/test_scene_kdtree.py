@@ -171,3 +171,23 @@ def test_energy_conservation_scaling(tmp_path):
                  '<shape type="rectangle"><emitter type="area"/></shape></scene>')
     r = list(_bsdfs(mtsg.Scene(str(p)))[0].reflectance)
     np.testing.assert_allclose(r, [0.99, 0.495, 0.2475], rtol=1e-6)
+
+
+def test_leaf_size_default_and_mitsuba_tree(monkeypatch):
+    """The build stops at 4 primitives per leaf (GPU-tuned, host/scene.h);
+    MTSH_KD_STOP_PRIMS=6 gives Mitsuba's tree (gkdtree.h:738), which bench.py's
+    CPU baseline traverses.  Both trees answer the same closest hits."""
+    path = os.path.join(SCENES, "bunny15.xml")
+    defs = {"width": 16, "height": 16, "spp": 1}
+    tuned = mtsg.Scene(path, defs)
+    monkeypatch.setenv("MTSH_KD_STOP_PRIMS", "6")
+    mitsuba = mtsg.Scene(path, defs)
+    monkeypatch.delenv("MTSH_KD_STOP_PRIMS")
+    assert mitsuba.info.kd_leaves < tuned.info.kd_leaves
+    assert mitsuba.info.kd_indices < tuned.info.kd_indices
+    rays = chords(20000, np.array([0.0, 0.45, 0.0]), 3.2, 5)
+    t0, _, _, p0 = O.trace_closest(tuned.desc, rays)
+    t1, _, _, p1 = O.trace_closest(mitsuba.desc, rays)
+    same = p0 == p1
+    assert same.mean() > 0.999
+    np.testing.assert_array_equal(t0[same], t1[same])
