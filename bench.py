@@ -254,7 +254,8 @@ def main():
     t_load = time.time()
     scene = mtsg.Scene(path, defs, instancing=a.instancing)
     load_s = time.time() - t_load
-    kd_info = {"kd_build": "host", "kd_build_ms": round(scene.info.kd_build_seconds * 1e3, 1), "kd_refs": scene.info.kd_indices}
+    kd_info = {"kd_build": "host", "kd_build_ms": round(scene.info.kd_build_seconds * 1e3, 1), "kd_refs": scene.info.kd_indices,
+               "kd_stop_prims": int(os.environ.get("MTSH_KD_STOP_PRIMS", "4"))}   # Mitsuba: 6
     if a.kd_build == "device":
         mtsg.kd_build(scene, device=dev)   # warm-up
         tree = mtsg.kd_build(scene, device=dev)
