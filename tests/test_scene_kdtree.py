@@ -191,3 +191,14 @@ def test_leaf_size_default_and_mitsuba_tree(monkeypatch):
     same = p0 == p1
     assert same.mean() > 0.999
     np.testing.assert_array_equal(t0[same], t1[same])
+
+
+def test_bench_cpu_baseline_uses_mitsubas_tree(bunny_small):
+    """bench.py times its CPU baseline on the tree Mitsuba would build
+    (stopPrims 6), not on the GPU-tuned one, and restores the environment."""
+    import bench
+    before = os.environ.get("MTSH_KD_STOP_PRIMS")
+    m = bench.mitsuba_tree_scene(bunny_small)
+    assert os.environ.get("MTSH_KD_STOP_PRIMS") == before
+    assert m.info.n_triangles == bunny_small.info.n_triangles
+    assert m.info.kd_indices < bunny_small.info.kd_indices
