@@ -577,7 +577,8 @@ typedef struct mtsg_kd_build_params {
     float traversal_cost;         /* 15 (gkdtree.h:734-744)                  */
     float query_cost;             /* 20                                      */
     float empty_space_bonus;      /* 0.9                                     */
-    int32_t stop_prims;           /* 6 in Mitsuba; 4 measured best here      */
+    int32_t stop_prims;           /* 6 in Mitsuba; 4 measured best here and  */
+                                  /* the default when params is NULL         */
     int32_t max_depth;            /* 0: 8 + 1.3 log2i(N)                     */
     int32_t pad;
 } mtsg_kd_build_params;

@@ -23,7 +23,7 @@
 //   k_sort_leaves  each leaf's indices ascending (the scatter's atomics
 //              order them arbitrarily; sorting makes the tree deterministic)
 // The host loop keeps the node list of the level (a few MB at most), makes
-// the leaf decisions (stopPrims 6, maxDepth 8 + 1.3 log2 N, SAH cost not
+// the leaf decisions (stopPrims 4 by default, maxDepth 8 + 1.3 log2 N, SAH cost not
 // below the leaf's) and writes the nodes in Mitsuba's KDNode encoding, so the
 // result plugs into mtsg_scene_desc like the host-built tree.
 #include <hip/hip_runtime.h>
@@ -95,6 +95,9 @@ __device__ bool clip_triangle(const float4 &a, const float4 &b, const float4 &c,
     poly[2][0] = c.x; poly[2][1] = c.y; poly[2][2] = c.z;
     for (int axis = 0; axis < 3; ++axis)
         for (int side = 0; side < 2; ++side) {
+            // sutherlandHodgman (triangle.cpp:70-73) gives up on fewer than
+            // three vertices: the triangle only touches the box there
+            if (n < 3) return false;
             const double plane = side == 0 ? lo[axis] : hi[axis];
             int m = 0;
             for (int i = 0; i < n; ++i) {
@@ -110,12 +113,18 @@ __device__ bool clip_triangle(const float4 &a, const float4 &b, const float4 &c,
                 }
             }
             n = m;
-            if (n == 0) return false;
             for (int i = 0; i < n; ++i) { poly[i][0] = tmp[i][0]; poly[i][1] = tmp[i][1]; poly[i][2] = tmp[i][2]; }
         }
+    if (n == 0) return false;
+    // rounded outwards (math::castflt_down / castflt_up, triangle.cpp:134-141):
+    // a clipped bound rounded to nearest can land on the far side of a later
+    // split plane and drop the triangle from a child it overlaps
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int i = 0; i < n; ++i)
-        for (int k = 0; k < 3; ++k) { mn[k] = fminf(mn[k], (float)poly[i][k]); mx[k] = fmaxf(mx[k], (float)poly[i][k]); }
+        for (int k = 0; k < 3; ++k) {
+            mn[k] = fminf(mn[k], __double2float_rd(poly[i][k]));
+            mx[k] = fmaxf(mx[k], __double2float_ru(poly[i][k]));
+        }
     for (int k = 0; k < 3; ++k) { mn[k] = fmaxf(mn[k], lo[k]); mx[k] = fminf(mx[k], hi[k]); }
     cmn = make_float3(mn[0], mn[1], mn[2]);
     cmx = make_float3(mx[0], mx[1], mx[2]);
@@ -319,7 +328,7 @@ int mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bo
     }
     if (hipSetDevice(device) != hipSuccess) { mtsg::set_last_error("hipSetDevice failed"); return MTSG_ERR_DEVICE; }
     const auto t0 = clock::now();
-    mtsg_kd_build_params P{15.0f, 20.0f, 0.9f, 6, 0, 0};
+    mtsg_kd_build_params P{15.0f, 20.0f, 0.9f, 4, 0, 0};   // NULL: the host build's defaults
     if (params) P = *params;
     // live primitives (an empty box marks one the tree leaves out) and the root box
     std::vector<Ref> refs0;

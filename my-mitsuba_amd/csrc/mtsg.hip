@@ -431,7 +431,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     // myPath2_OM shades depths 1..maxDepthEye and one more launch books the
     // emitters its last BSDF rays found
     const int maxBounces = I.om ? p->max_depth + 1 : (p->max_depth > 0 ? p->max_depth : 1 << 30);
-    // tail mode (k_finish): one lane, not in the instrumented, two-level or myPath2_OM modes
+    // tail mode (k_finish): one lane, not in the instrumented or myPath2_OM modes
     const bool useFinish = s->finishPaths > 0 && nl == 1 && !count && !I.om;
     // bounce b of a lane: one trace launch over this bounce's closest rays
     // (work list qin(b), identity for b = 0) and bounce b-1's shadow rays

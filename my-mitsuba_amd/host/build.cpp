@@ -26,6 +26,9 @@ AABB clipTriangle(const V3 &a, const V3 &b, const V3 &c, const AABB &box) {
         for (int k = 0; k < 3; ++k) poly[i][k] = (*v[i])[k];
     for (int axis = 0; axis < 3; ++axis) {
         for (int side = 0; side < 2; ++side) {
+            // sutherlandHodgman (triangle.cpp:70-73) gives up on fewer than
+            // three vertices: the triangle only touches the box there
+            if (n < 3) return AABB();
             double plane = side == 0 ? box.mn[axis] : box.mx[axis];
             int m = 0;
             for (int i = 0; i < n; ++i) {
@@ -43,11 +46,21 @@ AABB clipTriangle(const V3 &a, const V3 &b, const V3 &c, const AABB &box) {
             n = m;
             for (int i = 0; i < n; ++i)
                 for (int k = 0; k < 3; ++k) poly[i][k] = tmp[i][k];
-            if (n == 0) return AABB();
         }
     }
+    if (n == 0) return AABB();
+    // rounded outwards (math::castflt_down / castflt_up, triangle.cpp:134-141):
+    // a clipped bound rounded to nearest can land on the far side of a later
+    // split plane and drop the triangle from a child it overlaps
     AABB r;
-    for (int i = 0; i < n; ++i) r.expand(V3((float)poly[i][0], (float)poly[i][1], (float)poly[i][2]));
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            float lo = (float)poly[i][k], hi = lo;
+            if ((double)lo > poly[i][k]) lo = std::nextafter(lo, -INFINITY);
+            if ((double)hi < poly[i][k]) hi = std::nextafter(hi, INFINITY);
+            r.mn[k] = std::min(r.mn[k], lo);
+            r.mx[k] = std::max(r.mx[k], hi);
+        }
     r.clip(box);
     return r;
 }

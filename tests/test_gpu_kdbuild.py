@@ -61,7 +61,9 @@ def test_structure_and_brute_force_hits(name, defs):
     t0, p0 = O.trace_closest_brute(s.desc, rays)
     t1, _, _, p1 = O.trace_closest(s.desc, rays)
     hit0, hit1 = p0 != 0xFFFFFFFF, p1 != 0xFFFFFFFF
-    assert (hit0 == hit1).mean() > 0.9999
+    # exact: a reference lost by the build (e.g. a clipped bound rounded
+    # across a split plane) shows up here as a miss
+    np.testing.assert_array_equal(hit1, hit0)
     both = hit0 & hit1
     same = both & (p0 == p1)
     assert same.sum() >= 0.999 * both.sum()
@@ -92,7 +94,7 @@ def test_c3_device_tree(c3):
     th, _, _, ph = gh.trace_closest(rays)
     td, _, _, pd = gd.trace_closest(rays)
     hh, hd = ph != 0xFFFFFFFF, pd != 0xFFFFFFFF
-    assert (hh == hd).mean() > 0.9999
+    np.testing.assert_array_equal(hd, hh)
     both = hh & hd
     same = both & (ph == pd)
     assert same.sum() >= 0.999 * both.sum()
