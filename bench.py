@@ -29,22 +29,34 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-TRAFFIC_KERNEL = "k_trace_s<false, 16, false>"
 
 
-def pmc_traffic(workload):
-    """Memory-side bytes per launch of the closest-hit traversal from the
-    newest committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-    (profiles/rNN_traffic.json, written by tools/traffic_summary.py; PMC
-    counters need their own profiler runs, so they cannot be read live)."""
+def trace_kernel(a):
+    """rocprofv3's name of the timed traversal instantiation this run launches
+    (the instrumented COUNT pass runs k_trace_s<true, ...>)."""
+    return "k_trace_s<false, 16, true>" if a.instancing == "two-level" else "k_trace_s<false, 16, false>"
+
+
+def pmc_key(a, world=1):
+    """The configuration a committed PMC set must have been collected on for
+    this run to quote it (tools/gpu_pmc_config.sh, tools/pmc_kernels.py)."""
+    return {"workload": a.workload, "instancing": a.instancing, "kd_build": a.kd_build, "width": a.width,
+            "height": a.height, "spp": a.spp, "share": max(world, a.emulate_ranks, 1)}
+
+
+def pmc_lookup(key, directory=None):
+    """The newest committed per-kernel PMC set (profiles/rNN_pmc_*.json) whose
+    key equals this run's configuration, or (None, None).  PMC counters need
+    their own profiler runs (MI355X_MICROARCH.md), so they cannot be read
+    live; a set of another configuration is never used."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_traffic.json")))
+    files = sorted(glob.glob(os.path.join(directory or os.path.join(REPO, "profiles"), "r*_pmc_*.json")))
     for f in reversed(files):
         try:
             j = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if j.get("workload") == workload and j.get("kernel") == TRAFFIC_KERNEL:
+        if j.get("key") == key:
             return j, os.path.relpath(f, REPO)
     return None, None
 
@@ -71,6 +83,9 @@ def parse():
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="single process: render only rank 0's tile share of an N-GPU run (scaling rehearsal)")
     ap.add_argument("--save", default="", help="write the developed image (.npy) here (rank 0)")
+    ap.add_argument("--no-count", action="store_true",
+                    help="skip the instrumented (untimed) pass of per-ray counts (profiler runs)")
+    ap.add_argument("--print-pmc-key", action="store_true", help="print this configuration's PMC key and exit")
     return ap.parse_args()
 
 
@@ -220,29 +235,23 @@ def parity_at_headline(scene, gpu, params, border, stride):
     d = np.abs(rgb_g - rgb_c)[own]
     l1 = float(d.mean())
     mean = float(rgb_c[own].mean())
+    # per-pixel L1 (mean over RGB of |GPU - CPU|) and its distribution
+    px = d.mean(-1)
+    dist = {"p50": float(np.percentile(px, 50)), "p90": float(np.percentile(px, 90)),
+            "p99": float(np.percentile(px, 99)), "p999": float(np.percentile(px, 99.9)), "max": float(px.max()),
+            "frac_over_1e-3": float((px > 1e-3).mean()), "frac_over_1e-3_of_mean": float((px > 1e-3 * mean).mean())}
     return {"l1": l1, "mean": round(mean, 6), "l1_rel_mean": l1 / max(mean, 1e-12),
-            "max_abs": float(d.max()), "pixels": int(own.sum()), "spp": int(p.spp),
+            "max_abs": float(d.max()), "per_pixel": dist, "pixels": int(own.sum()), "spp": int(p.spp),
             "samples": int(st.samples), "tiles": f"16x16 tiles t % {stride} == 0 of {p.tile_w}x{p.tile_h}",
             "bar": "l1 < 1e-3 (and l1_rel_mean < 1e-3)", "pass": bool(l1 < 1e-3 and l1 < 1e-3 * max(mean, 1e-12)),
             "rng": "counter mode on both sides", "oracle_seconds": round(t_cpu, 1), "gpu_seconds": round(t_gpu, 2)}
 
 
-def pmc_tcc(workload):
-    """L2 hit rate of the traversal kernel from the newest committed
-    TCC_HIT/TCC_MISS pass (profiles/rNN_tcc.json), if any."""
-    import glob
-    for f in reversed(sorted(glob.glob(os.path.join(REPO, "profiles", "r*_tcc.json")))):
-        try:
-            j = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        if j.get("workload") == workload and j.get("kernel") == TRAFFIC_KERNEL:
-            return j, os.path.relpath(f, REPO)
-    return None, None
-
-
 def main():
     a = parse()
+    if a.print_pmc_key:
+        print(json.dumps(pmc_key(a, int(os.environ.get("WORLD_SIZE", "1")))))
+        return
     rank, world, local, pg = dist_setup(a.gpus)
     import mtsg
     # one GPU per rank (LOCAL_RANK); more ranks than visible GPUs share them
@@ -281,24 +290,45 @@ def main():
         gpu.render_device(params, film)
         mtsg.device_lib().mtsg_device_to_host(gpu._h, host_block.ctypes.data, film, nbytes)
 
-    for _ in range(a.warmup):
-        step()
-    # per-kernel HIP events on the library's stream stay on through the timed
-    # steps (two event records per launch); the per-frame figures are summed
-    gpu.set_flags(mtsg.MTSG_FLAG_TIMING)
+    # --emulate-ranks N: every rank's tile share in turn on this one GPU, each
+    # timed like a rank of an N-GPU run (max over the shares = the frame time)
+    shares = list(range(a.emulate_ranks)) if (a.emulate_ranks > 1 and world == 1) else [params.tile_offset]
+    share_s = []
     acc = {}
-    barrier(pg)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-        st = gpu.stats()
-        for f in ("ms_trace_closest", "ms_trace_shadow", "ms_shade", "ms_camera", "ms_splat", "ms_total",
-                  "rays_closest", "rays_shadow", "launches_trace_closest", "launches_trace_shadow",
-                  "ms_finish", "paths_finish", "launches_finish"):
-            acc[f] = acc.get(f, 0) + getattr(st, f)
-    barrier(pg)
-    elapsed = max_over_ranks(pg, time.perf_counter() - t0)
-    gpu.set_flags(0)
+    for off in shares:
+        params.tile_offset = off
+        for _ in range(a.warmup):
+            step()
+        # per-kernel HIP events on the library's stream stay on through the
+        # timed steps (two event records per launch); the per-frame figures
+        # are summed (rank 0's share only when shares are emulated)
+        gpu.set_flags(mtsg.MTSG_FLAG_TIMING)
+        barrier(pg)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+            st = gpu.stats()
+            if off == shares[0]:
+                for f in ("ms_trace_closest", "ms_trace_shadow", "ms_shade", "ms_camera", "ms_splat", "ms_total",
+                          "rays_closest", "rays_shadow", "launches_trace_closest", "launches_trace_shadow",
+                          "ms_finish", "paths_finish", "launches_finish"):
+                    acc[f] = acc.get(f, 0) + getattr(st, f)
+        barrier(pg)
+        share_s.append(time.perf_counter() - t0)
+        gpu.set_flags(0)
+    params.tile_offset = shares[0]
+    elapsed = max_over_ranks(pg, max(share_s))
+    whole_s = None
+    if len(shares) > 1:
+        # the whole frame on this GPU, for the per-share speedups
+        params.tile_stride, params.tile_offset = 1, 0
+        for _ in range(a.warmup):
+            step()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        whole_s = time.perf_counter() - t0
+        params.tile_stride, params.tile_offset = a.emulate_ranks, shares[0]
     samples_total = params.tile_w * params.tile_h * params.spp * a.steps
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
@@ -317,6 +347,25 @@ def main():
                    # tail mode: the paths left at the switch bounce, finished in one k_finish launch
                    "finish_ms": acc["ms_finish"] / k, "finish_paths": acc["paths_finish"] // k,
                    "finish_launches": acc["launches_finish"] // k}
+        # counter-backed bandwidth of the other kernels: memory-side bytes of
+        # one frame (the committed PMC set of this configuration) / this
+        # run's HIP-event time of that kernel per frame
+        pj, psrc = pmc_lookup(pmc_key(a, world))
+        if pj:
+            fam_ms = {"k_shade": kernels["shade_ms"], "k_finish": kernels["finish_ms"],
+                      "k_camera": kernels["camera_ms"], "k_splat": kernels["splat_ms"]}
+            pmc = {}
+            for fam, ms in fam_ms.items():
+                ks = [v for n, v in pj["kernels"].items() if n.startswith(fam + "<") or n.startswith(fam + "(")]
+                b = sum(v.get("traffic_bytes_per_step", 0.0) for v in ks)
+                if b > 0 and ms > 0:
+                    hits = [v["tcc_hit_rate"] for v in ks if "tcc_hit_rate" in v]
+                    pmc[fam] = {"bytes_per_frame": round(b), "GBps": round(b / (ms / 1e3) / 1e9, 1),
+                                "frac_of_hbm_peak": round(b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "tcc_hit_rate": hits[0] if len(hits) == 1 else None}
+            kernels["pmc"] = pmc
+            kernels["pmc_source"] = psrc
+    if rank == 0 and not a.no_count:
         # instrumented pass at reduced spp (per-ray counts are spp-independent)
         pc = params.copy()
         pc.spp = max(1, min(params.spp, 16))
@@ -345,22 +394,24 @@ def main():
         avg_launch_s = trace_s / launches
         achieved = bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
         dev_achieved = dev_bytes_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-        tj, tsrc = pmc_traffic(a.workload)
+        # counters of the same kernel instantiation on the same configuration
+        # only (profiles/rNN_pmc_*.json); otherwise null
+        tkern = trace_kernel(a)
+        pj, psrc = pmc_lookup(pmc_key(a, world))
+        tk = (pj or {}).get("kernels", {}).get(tkern, {})
         traffic = None
-        if (tj and avg_launch_s > 0 and a.workload == "bunny15" and params.spp == 256 and world == 1
-                and a.emulate_ranks <= 1):
-            traffic = round(tj["traffic_bytes_per_launch"] / avg_launch_s / 1e9, 1)
-        hj, hsrc = pmc_tcc(a.workload)
+        if "traffic_bytes_per_launch" in tk and avg_launch_s > 0:
+            traffic = round(tk["traffic_bytes_per_launch"] / avg_launch_s / 1e9, 1)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_frac": round(traffic / HBM_PEAK_GBS, 4) if traffic else None,
-                    "traffic_source": (f"{tsrc}: FETCH_SIZE x2 + WRITE_SIZE per launch "
-                                       f"({tj['traffic_bytes_per_launch'] / 1e9:.2f} GB) / this run's avg launch time; "
+                    "traffic_source": (f"{psrc} [{tkern}]: FETCH_SIZE x2 + WRITE_SIZE per launch "
+                                       f"({tk['traffic_bytes_per_launch'] / 1e9:.2f} GB) / this run's avg launch time; "
                                        "memory-side requests, Infinity-Cache hits included"
                                        if traffic is not None else None),
-                    "tcc_hit_rate": hj["tcc_hit_rate"] if hj else None,
-                    "tcc_source": hsrc,
-                    "kernel": "k_trace_s (closest + shadow rays)",
+                    "tcc_hit_rate": tk.get("tcc_hit_rate"),
+                    "tcc_source": f"{psrc} [{tkern}]" if "tcc_hit_rate" in tk else None,
+                    "kernel": f"{tkern} (closest + shadow rays)",
                     "bytes_model": "SURVEY 8(d): 8 B/KDNode + 4 B/leaf ref + 48 B/TriAccel test",
                     "algorithmic_bytes_per_launch": round(bytes_per_launch), "avg_launch_ms": round(avg_launch_s * 1e3, 3),
                     "launches_per_frame": launches // a.steps,
@@ -405,7 +456,12 @@ def main():
                        "parallelism": f"film tiles round-robin over {world} GPU(s)",
                        "scene_load_s": round(load_s, 2), **kd_info},
             **({"emulated_ranks": a.emulate_ranks,
-                "note": "one GPU rendering rank 0's 1/N tile share; value = frame samples / that time"}
+                "share_ms_per_step": [round(t / a.steps * 1e3, 3) for t in share_s],
+                "whole_frame_ms_per_step": round(whole_s / a.steps * 1e3, 3) if whole_s else None,
+                "share_speedups": [round(whole_s / t, 3) for t in share_s] if whole_s else None,
+                "share_speedup_min": round(whole_s / max(share_s), 3) if whole_s else None,
+                "note": "one GPU rendering each rank's 1/N tile share in turn; value = frame samples / the slowest "
+                        "share's time (the N-GPU frame time without launch and gather overheads); kernels = share 0"}
                if a.emulate_ranks > 1 and world == 1 else {}),
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "kernels": kernels,
         }

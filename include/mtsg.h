@@ -38,7 +38,9 @@ enum {
     MTSG_ERR_DEVICE     = -2,  /* HIP runtime error                        */
     MTSG_ERR_OOM        = -3,  /* device allocation failed                 */
     MTSG_ERR_CANCELLED  = -4,  /* mtsg_cancel() was called (render() == false) */
-    MTSG_ERR_NODEVICE   = -5   /* no gfx950 device / bad device index      */
+    MTSG_ERR_NODEVICE   = -5,  /* no gfx950 device / bad device index      */
+    MTSG_ERR_TRAVERSAL  = -6   /* a ray hit the kd-restart limit (a guard  */
+                               /* against non-terminating traversal)       */
 };
 
 /* ---- scene description: flat arrays, all world space -------------------- */
@@ -513,6 +515,11 @@ int  mtsg_device_to_host(mtsg_scene *scene, void *dst, const void *src, size_t b
  * consumed when a render returns; set while no render runs, it cancels the
  * next one. */
 void mtsg_cancel(mtsg_scene *scene);
+
+/* Withdraw a pending cancel flag (one that was set after the render it was
+ * meant for had returned).  For callers that serialise their cancel() with
+ * the end of their renders, as libmtsg_path's job does. */
+void mtsg_cancel_clear(mtsg_scene *scene);
 
 int  mtsg_set_flags(mtsg_scene *scene, uint32_t flags);
 int  mtsg_get_stats(mtsg_scene *scene, mtsg_stats *out);

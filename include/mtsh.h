@@ -32,6 +32,28 @@ typedef struct mtsh_scene_info {
  * Returns NULL on error (see mtsh_last_error). */
 mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_defines);
 
+/* The values a Mitsuba plugin holds in memory after the reference loaded the
+ * scene with its own -D parameter map (mitsuba.cpp:168-174,
+ * scenehandler.cpp:211): they replace the XML's values before the scene is
+ * finalised, so the device renders the film, sample count and integrator
+ * parameters the user asked for.  `mask` selects the groups that apply. */
+enum {
+    MTSH_OVERRIDE_FILM_SIZE    = 1,   /* Film::getSize (crop = the full film)       */
+    MTSH_OVERRIDE_SAMPLE_COUNT = 2,   /* Sampler::getSampleCount                    */
+    MTSH_OVERRIDE_INTEGRATOR   = 4    /* MonteCarloIntegrator m_maxDepth, m_rrDepth, */
+                                      /* m_strictNormals, m_hideEmitters            */
+};
+typedef struct mtsh_scene_overrides {
+    uint32_t mask;
+    int32_t film_width, film_height;
+    int32_t sample_count;
+    int32_t max_depth, rr_depth, strict_normals, hide_emitters;
+} mtsh_scene_overrides;
+
+/* mtsh_scene_load, then the overrides (may be NULL) before finalisation. */
+mtsh_scene *mtsh_scene_load_overrides(const char *path, const char *const *defines, int n_defines,
+                                      const mtsh_scene_overrides *overrides);
+
 /* Override kd-tree build parameters before loading (0 = default). */
 void mtsh_set_kd_threads(int threads);
 

@@ -70,6 +70,11 @@ struct DevScene {
     // myPath2_OM occupancy maps (om.cpp; nullptr unless that integrator)
     const mtsg_om *__restrict__ om;
     const uint32_t *__restrict__ om_bits;
+    // traversal stacks in use (<= SHORT_STACK / INNER_STACK / OUTER_STACK;
+    // smaller only to exercise the restart guard) and the restart guard:
+    // from restart rstGuard of a ray (per level) on, a restart starts one ulp
+    // beyond its exit distance; restart rstMax ends the ray with SB_ERR
+    uint32_t capFlat, capGrp, capTop, rstGuard, rstMax;
 };
 
 struct DevCamera {
@@ -207,7 +212,8 @@ constexpr int XGROUPS = 8;                  // XCDs: blocks b and b + 8 share on
 // Q0/Q1: paths of the next bounce (ping-pong); S0/S1: shadow rays of a bounce
 // (ping-pong: bounce b appends to S(b & 1) while its trace reads S((b-1) & 1))
 constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S0 = 128, CNT_S1 = 192;
-constexpr int CNT_ERR = 96;   // sticky error flags (1: QMC dimension limit)
+constexpr int CNT_ERR = 96;   // sticky error flags (CNT_ERR_*)
+constexpr uint32_t CNT_ERR_QMC_DIM = 1u, CNT_ERR_TRAVERSAL = 2u;
 constexpr int CNT_FETCH = 256;                           // XGROUPS counters, 32 words apart
 constexpr int CNT_WORDS = CNT_FETCH + 32 * XGROUPS;
 constexpr int HOSTCNT_STRIDE = 256;
@@ -484,12 +490,38 @@ struct SpecRay {
     uint32_t bits;       // see SB_*
 };
 // bits: top slot of the circular short stack (0-2), entries held (3-5),
-// entries dropped since the last restart (6), ray direction signs (16-18),
-// traversal done (19), hit found (20), shadow ray (21)
+// entries dropped since the last restart (6), kd-restarts of the ray at this
+// level (7-15), ray direction signs (16-18), traversal done (19), hit found
+// (20), shadow ray (21), inside an instance (22), restart limit hit (31)
 enum : uint32_t {
     SB_TOP = 7u, SB_N = 7u << 3, SB_N1 = 1u << 3, SB_DROPPED = 1u << 6, SB_STACK = 0x7Fu,
-    SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20, SB_SHADOW = 1u << 21
+    SB_RST_SHIFT = 7, SB_RST1 = 1u << 7, SB_RST_MASK = 0x1FFu,
+    SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20, SB_SHADOW = 1u << 21, SB_ERR = 1u << 31
 };
+// the restart guard's defaults (DevScene::rstGuard / rstMax): rays of the
+// scenes at hand restart 0-3 times (tools/iter_hist.py)
+constexpr uint32_t RST_GUARD = 8, RST_MAX = SB_RST_MASK;
+
+// kd-restart after the stack ran empty with entries dropped (Foley &
+// Sugerman's restart, at the exit distance t0 of the leaf just finished).
+// It can only return to t0 when more far children are pushed at split
+// planes crossed exactly at t0 than the stack holds; from the rstGuard-th
+// restart of the ray on it starts one ulp beyond t0 instead (hits exactly at
+// t0 in leaves not yet visited are the only thing that can be skipped), so
+// t0 strictly increases, and the rstMax-th restart ends the ray with SB_ERR
+// (the render then fails with MTSG_ERR_TRAVERSAL) instead of spinning.
+DEV void kd_restart(const DevScene &S, SpecRay &r, uint32_t b, uint2 root, uint2 c) {
+    const bool restart = (b & SB_DROPPED) != 0;
+    const uint32_t nr = (b >> SB_RST_SHIFT) & SB_RST_MASK;
+    float t0 = r.tmax;
+    t0 = (restart & (nr >= S.rstGuard)) ? nextafterf(t0, INFINITY) : t0;
+    const bool fail = restart & (nr >= S.rstMax);
+    r.tmin = restart ? t0 : r.tmin;
+    r.tmax = restart ? r.best : r.tmax;
+    r.cur = restart ? root : c;
+    r.bits = ((b & ~SB_STACK) + (restart ? SB_RST1 : 0u)) |
+             ((!restart | fail | !(t0 < r.best)) ? SB_TRAVDONE : 0u) | (fail ? SB_ERR : 0u);
+}
 
 // short stack of the compact traversal: entry k of lane i at [k * TRACE_BLOCK
 // + i].  A workgroup is one wave, so the lane index is recomputed at every use
@@ -589,15 +621,15 @@ DEV void spec_plan(const SpecRay &r, uint2 n, float &tsplit, bool &goLeft, bool 
     goLeft = belowFirst != goSecond;
 }
 
-DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push, SpecStack stk) {
+DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push, SpecStack stk, uint32_t cap) {
     const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
     if (push) {
         // circular short stack: a push onto a full stack drops the oldest entry
         const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
         const uint32_t b = r.bits, top = b & SB_TOP;
         stk.push(top, other, r.tmax);
-        const bool full = (b & SB_N) == (uint32_t)SHORT_STACK * SB_N1;
-        r.bits = ((b & ~SB_TOP) | (top == SHORT_STACK - 1 ? 0u : top + 1u)) + (full ? SB_DROPPED - (b & SB_DROPPED) : SB_N1);
+        const bool full = (b & SB_N) == cap * SB_N1;
+        r.bits = ((b & ~SB_TOP) | (top == cap - 1 ? 0u : top + 1u)) + (full ? SB_DROPPED - (b & SB_DROPPED) : SB_N1);
         r.tmax = tsplit;
     }
     return c;
@@ -641,14 +673,14 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     }
     if (inner) {
         if (COUNT) cnt.nodes++;
-        const uint2 c = spec_take(r, p0, tsplit, goLeft, push, stk);
+        const uint2 c = spec_take(r, p0, tsplit, goLeft, push, stk, S.capFlat);
         r.cur = c;
         if (rootKind && !(c.x & 0x80000000u)) {
             if (COUNT) cnt.nodes++;
             float ts2;
             bool gl2, push2;
             spec_plan(r, c, ts2, gl2, push2);
-            r.cur = spec_take(r, pc, ts2, gl2, push2, stk);
+            r.cur = spec_take(r, pc, ts2, gl2, push2, stk, S.capFlat);
         }
     }
     const bool found = (r.bits & SB_FOUND) != 0;
@@ -667,7 +699,7 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
         const uint32_t b = r.bits;
         if (b & SB_N) {
-            const uint32_t top = b & SB_TOP, k = top == 0 ? SHORT_STACK - 1 : top - 1u;
+            const uint32_t top = b & SB_TOP, k = top == 0 ? S.capFlat - 1 : top - 1u;
             r.cur = stk.node(k);
             const float t = stk.t(k);
             r.bits = ((b & ~SB_TOP) | k) - SB_N1;
@@ -675,13 +707,8 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
             r.tmax = fminf(t, r.best);
         } else {
             // empty: done, or a kd-restart behind this leaf if entries were dropped
-            const bool restart = (b & SB_DROPPED) != 0;
-            const float t0 = r.tmax;
-            r.tmin = restart ? t0 : r.tmin;
-            r.tmax = restart ? r.best : r.tmax;
-            r.cur = restart ? S.root2 : c;
-            if (COUNT && restart) cnt.restarts++;
-            r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
+            if (COUNT && (b & SB_DROPPED)) cnt.restarts++;
+            kd_restart(S, r, b, S.root2, c);
         }
     }
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
@@ -731,13 +758,13 @@ DEV uint2 inst_root(const DevScene &S, uint32_t ii) {
 
 // push the far child onto the stack of the lane's level (circular, drops
 // the oldest entry when full)
-DEV uint2 spec_take_i(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push) {
+DEV uint2 spec_take_i(const DevScene &S, SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push) {
     const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
     if (push) {
         const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
         const uint32_t b = r.bits, top = b & SB_TOP;
         const bool inner = (b & SB_INST) != 0;
-        const uint32_t cap = inner ? (uint32_t)INNER_STACK : (uint32_t)OUTER_STACK;
+        const uint32_t cap = inner ? S.capGrp : S.capTop;
         const uint32_t i = top * TRACE_BLOCK + lane_here();
         if (inner) { s_grpNode[i] = other; s_grpT[i] = r.tmax; }
         else { s_outNode[i] = other; s_outT[i] = r.tmax; }
@@ -751,7 +778,7 @@ DEV uint2 spec_take_i(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bo
 // back to the top level after a group traversal: restore the saved state,
 // keep the hit flag, reload the world-space ray
 DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4 *wd) {
-    const uint32_t found = r.bits & SB_FOUND;
+    const uint32_t found = r.bits & (SB_FOUND | SB_ERR);
     r.cur = make_uint2(save_word(S, 0), save_word(S, 1));
     r.tmin = __uint_as_float(save_word(S, 2));
     r.tmax = __uint_as_float(save_word(S, 3));
@@ -806,14 +833,14 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     }
     if (inner) {
         if (COUNT) cnt.nodes++;
-        const uint2 c = spec_take_i(r, p0, tsplit, goLeft, push);
+        const uint2 c = spec_take_i(S, r, p0, tsplit, goLeft, push);
         r.cur = c;
         if (rootKind && !(c.x & 0x80000000u)) {
             if (COUNT) cnt.nodes++;
             float ts2;
             bool gl2, push2;
             spec_plan(r, c, ts2, gl2, push2);
-            r.cur = spec_take_i(r, pc, ts2, gl2, push2);
+            r.cur = spec_take_i(S, r, pc, ts2, gl2, push2);
         }
     }
     if (enter) {
@@ -889,7 +916,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         r.lfEnd = nonEmpty ? c.y : r.lfEnd;
         r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
         const uint32_t b = r.bits;
-        const uint32_t cap = inInst ? (uint32_t)INNER_STACK : (uint32_t)OUTER_STACK;
+        const uint32_t cap = inInst ? S.capGrp : S.capTop;
         if (b & SB_N) {
             const uint32_t top = b & SB_TOP, k = top == 0 ? cap - 1 : top - 1u;
             const uint32_t i = k * TRACE_BLOCK + lane_here();
@@ -899,14 +926,8 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
             r.tmin = r.tmax;
             r.tmax = fminf(t, r.best);
         } else {
-            const bool restart = (b & SB_DROPPED) != 0;
-            const float t0 = r.tmax;
-            r.tmin = restart ? t0 : r.tmin;
-            r.tmax = restart ? r.best : r.tmax;
-            const uint2 root = inInst ? inst_root(S, save_word(S, 8)) : S.root2;
-            r.cur = restart ? root : c;
-            if (COUNT && restart) cnt.restarts++;
-            r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
+            if (COUNT && (b & SB_DROPPED)) cnt.restarts++;
+            kd_restart(S, r, b, inInst ? inst_root(S, save_word(S, 8)) : S.root2, c);
         }
     }
     const bool done = leave || ((r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f);
@@ -1030,6 +1051,7 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
                     }
                 }
             }
+            if (r.bits & SB_ERR) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);
             // closest: hits were written through, only a miss needs a record
             if (!(r.bits & SB_FOUND)) {
                 if (r.bits & SB_SHADOW) shadow_unoccluded(P, idx);
@@ -2112,7 +2134,7 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
         }
     }
     if ((SMP == MTSG_SAMPLER_HALTON || SMP == MTSG_SAMPLER_HAMMERSLEY || SMP == MTSG_SAMPLER_SOBOL) && smp.dimError)
-        atomicOr(&P.cnt[CNT_ERR], 1u);   // the render fails as Mitsuba's Log(EError) would
+        atomicOr(&P.cnt[CNT_ERR], CNT_ERR_QMC_DIM);   // the render fails as Mitsuba's Log(EError) would
     const float4 finalL = make_float4(L.x, L.y, L.z, L4.w);
     if (cont) {
         out.state(make_float4(T.x, T.y, T.z, eta), finalL, make_uint4(depth | flags, smp.dim, slot, smp.n2));
@@ -2577,6 +2599,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
             else done = spec_iter<false>(S, r, stk, tc, P.hit + idx);
         }
         if (done) {
+            if (r.bits & SB_ERR) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);
             if (r.bits & SB_SHADOW) {
                 if (!(r.bits & SB_FOUND)) shadow_unoccluded(P, idx);
                 state = FS_IDLE;

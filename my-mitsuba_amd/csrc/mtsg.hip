@@ -298,6 +298,8 @@ DevSampler make_sampler(const mtsg_scene *s, uint32_t spp) {
     return S;
 }
 
+const char *const traversal_error =
+    "kd-tree traversal: a ray reached the restart limit without making progress (kernels.h kd_restart)";
 // Mitsuba's Log(EError) of Halton/Hammersley (halton.cpp:343-386) and sobol (sobol.cpp:223-239)
 const char *dim_error(int sampler) {
     return sampler == MTSG_SAMPLER_SOBOL
@@ -553,7 +555,12 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             HIP_TRY(hipEventSynchronize(L.cntEv[L.last & 1]));
             account(l, L.last);
             // the error word is sticky within the batch: the last copy holds it
-            if (hostCnt(l, L.last)[CNT_ERR]) {
+            const uint32_t err = hostCnt(l, L.last)[CNT_ERR];
+            if (err & CNT_ERR_TRAVERSAL) {
+                g_err = traversal_error;
+                return MTSG_ERR_TRAVERSAL;
+            }
+            if (err) {
                 g_err = dim_error(s->samplerType);
                 return MTSG_ERR_INVALID;
             }
@@ -843,6 +850,22 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         if ((rc = up(in.data(), in.size(), &dinst))) return fail(rc);
         ds.inst = dinst;
     }
+    // traversal stacks and the kd-restart guard (kernels.h kd_restart); the
+    // MTSG_STACK_CAP / MTSG_RESTART_GUARD / MTSG_RESTART_LIMIT overrides exist
+    // to exercise the guard (tests/test_gpu_edge_rays.py)
+    ds.capFlat = SHORT_STACK;
+    ds.capGrp = INNER_STACK;
+    ds.capTop = OUTER_STACK;
+    ds.rstGuard = RST_GUARD;
+    ds.rstMax = RST_MAX;
+    if (const char *c = getenv("MTSG_STACK_CAP")) {
+        const uint32_t cap = (uint32_t)std::max(1, atoi(c));
+        ds.capFlat = std::min(ds.capFlat, cap);
+        ds.capGrp = std::min(ds.capGrp, cap);
+        ds.capTop = std::min(ds.capTop, cap);
+    }
+    if (const char *g = getenv("MTSG_RESTART_GUARD")) ds.rstGuard = (uint32_t)std::max(0, atoi(g));
+    if (const char *g = getenv("MTSG_RESTART_LIMIT")) ds.rstMax = std::min<uint32_t>(RST_MAX, (uint32_t)std::max(0, atoi(g)));
     // environment emitter tables (envmap.h)
     ds.has_env = d->has_envmap ? 1 : 0;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
@@ -1079,6 +1102,10 @@ int mtsg_debug_stragglers(mtsg_scene *s, float *out, uint32_t max_rays) {
     return (int)n;
 }
 
+void mtsg_cancel_clear(mtsg_scene *s) {
+    if (s) s->cancel.store(0);
+}
+
 void mtsg_cancel(mtsg_scene *s) {
     if (s) s->cancel.store(1);
 }
@@ -1200,8 +1227,11 @@ static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, fl
     e = hipStreamSynchronize(s->stream);
     if (e == hipSuccess) e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpy(out.data(), *po, f4, hipMemcpyDeviceToHost);
+    uint32_t err = 0;
+    if (e == hipSuccess) e = hipMemcpy(&err, D.cnt + CNT_ERR, sizeof(uint32_t), hipMemcpyDeviceToHost);
     cleanup();
     if (e != hipSuccess) { g_err = hipGetErrorString(e); return MTSG_ERR_DEVICE; }
+    if (err & CNT_ERR_TRAVERSAL) { g_err = traversal_error; return MTSG_ERR_TRAVERSAL; }
     for (uint32_t i = 0; i < n; ++i) {
         if (shadow) {
             occ[i] = out[i].x == 0.f ? 1 : 0;

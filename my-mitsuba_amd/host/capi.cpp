@@ -29,6 +29,11 @@ int mtsh_clip_triangle(const float *v, const float *box, float *out) {
 void mtsh_set_instancing(int mode) { mtsh::g_instancing = mode == MTSH_INSTANCING_TWO_LEVEL ? 1 : 0; }
 
 mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_defines) {
+    return mtsh_scene_load_overrides(path, defines, n_defines, nullptr);
+}
+
+mtsh_scene *mtsh_scene_load_overrides(const char *path, const char *const *defines, int n_defines,
+                                      const mtsh_scene_overrides *overrides) {
     try {
         std::map<std::string, std::string> defs;
         for (int i = 0; i < n_defines; ++i) {
@@ -38,7 +43,7 @@ mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_
             defs[d.substr(0, eq)] = d.substr(eq + 1);
         }
         auto s = std::make_unique<mtsh_scene>();
-        s->scene = mtsh::loadScene(path, defs);
+        s->scene = mtsh::loadScene(path, defs, overrides);
         return s.release();
     } catch (const std::exception &e) {
         g_err = e.what();

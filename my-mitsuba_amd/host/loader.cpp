@@ -1560,7 +1560,8 @@ bool readPFM(const std::string &path, int &w, int &h, std::vector<float> &rgb, s
 int g_defaultKDThreads = 0;
 int g_instancing = 0;
 
-std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::string, std::string> &defines) {
+std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::string, std::string> &defines,
+                                 const mtsh_scene_overrides *ov) {
     auto scene = std::make_unique<Scene>();
     scene->kd.threads = g_defaultKDThreads;
     scene->twoLevel = g_instancing == 1;
@@ -1584,6 +1585,37 @@ std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::st
     if (!scene->sensor.present) throw err("scene has no <sensor>");
     for (auto &e : scene->emitters)
         if (e.type == MTSG_EMITTER_AREA && e.shape < 0) throw err("area emitter without a parent shape");
+    if (ov) {
+        // the in-memory values of a Mitsuba plugin (mtsh.h mtsh_scene_overrides)
+        if (ov->mask & MTSH_OVERRIDE_FILM_SIZE) {
+            Film &f = scene->film;
+            if (ov->film_width <= 0 || ov->film_height <= 0) throw err("override: film size must be positive");
+            if (f.cropX != 0 || f.cropY != 0 || f.cropW != f.width || f.cropH != f.height)
+                throw err("hdrfilm crop windows are outside this build's scope");
+            f.width = f.cropW = ov->film_width;
+            f.height = f.cropH = ov->film_height;
+        }
+        if (ov->mask & MTSH_OVERRIDE_SAMPLE_COUNT) {
+            if (ov->sample_count <= 0) throw err("sampleCount must be > 0");
+            scene->sampleCount = ov->sample_count;
+            if (scene->sampler.type == MTSG_SAMPLER_LDSAMPLER) {   // ldsampler.cpp:82-95
+                uint32_t r = 1;
+                while (r < (uint32_t)ov->sample_count) r <<= 1;
+                scene->sampleCount = (int)r;
+            }
+        }
+        if (ov->mask & MTSH_OVERRIDE_INTEGRATOR) {
+            IntegratorProps &ip = scene->integrator;
+            if (ip.type != "path") throw err("integrator overrides apply to the `path` integrator");
+            // MonteCarloIntegrator's own checks (integrator.cpp:184-196)
+            if (ov->rr_depth <= 0) throw err("'rrDepth' must be set to a value greater than zero!");
+            if (ov->max_depth <= 0 && ov->max_depth != -1) throw err("'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
+            ip.maxDepth = ov->max_depth;
+            ip.rrDepth = ov->rr_depth;
+            ip.strictNormals = ov->strict_normals != 0;
+            ip.hideEmitters = ov->hide_emitters != 0;
+        }
+    }
     scene->finalize();
     return scene;
 }

@@ -34,9 +34,14 @@ struct mtsh_path_job {
     // cancel(): the job's flag is checked by each worker before its render
     // starts; the handles' flags stop renders already running (per bounce)
     std::atomic<int> cancel{0};
-    std::vector<std::atomic<int>> rendering;   // per GPU: its mtsg_render is running
+    // per GPU, under gpuLock[g]: its mtsg_render is running, and a cancel was
+    // sent to it.  A cancel that reaches the handle after its render returned
+    // would stay set and cancel the job's next render, so the worker withdraws
+    // it (mtsg_cancel_clear) when its render is over; the lock orders the two.
+    std::vector<int> rendering, sent;
+    std::vector<std::mutex> gpuLock;
     std::mutex renderLock;   // one render at a time per job
-    explicit mtsh_path_job(int n) : rendering(n) {}
+    explicit mtsh_path_job(int n) : rendering(n, 0), sent(n, 0), gpuLock(n) {}
 };
 
 extern "C" {
@@ -98,10 +103,18 @@ int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, f
             mtsg_render_params p = *params;
             p.tile_stride = S * n;
             p.tile_offset = p.tile_stride > 1 ? off + g * S : 0;
-            job->rendering[g].store(1);
+            {
+                std::lock_guard<std::mutex> gl(job->gpuLock[g]);
+                job->rendering[g] = 1;
+            }
             if (job->cancel.load()) rcs[g] = MTSG_ERR_CANCELLED;
             else rcs[g] = mtsg_render(job->handles[g], &p, blocks[g].data());
-            job->rendering[g].store(0);
+            {
+                std::lock_guard<std::mutex> gl(job->gpuLock[g]);
+                job->rendering[g] = 0;
+                if (job->sent[g]) mtsg_cancel_clear(job->handles[g]);
+                job->sent[g] = 0;
+            }
             // the device library's error is thread-local: capture it here
             if (rcs[g] != MTSG_OK) errs[g] = device_error();
         });
@@ -127,10 +140,14 @@ int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, f
 void mtsh_path_job_cancel(mtsh_path_job *job) {
     if (!job) return;
     job->cancel.store(1);
-    // only renders still running are told: a handle's flag set after its
-    // render returned would cancel the job's next render
-    for (size_t g = 0; g < job->handles.size(); ++g)
-        if (job->rendering[g].load()) mtsg_cancel(job->handles[g]);
+    // only renders still running are told (see mtsh_path_job::sent)
+    for (size_t g = 0; g < job->handles.size(); ++g) {
+        std::lock_guard<std::mutex> gl(job->gpuLock[g]);
+        if (job->rendering[g]) {
+            mtsg_cancel(job->handles[g]);
+            job->sent[g] = 1;
+        }
+    }
 }
 
 void mtsh_path_job_destroy(mtsh_path_job *job) {

@@ -10,6 +10,7 @@
 
 #include "hmath.h"
 #include "../../include/mtsg.h"
+#include "../../include/mtsh.h"
 
 namespace mtsh {
 
@@ -246,7 +247,8 @@ bool readEXR(const std::string &path, int &w, int &h, std::vector<float> &rgb, s
 
 // XML loading (src/librender/scenehandler.cpp), `-D name=value` defines
 std::unique_ptr<Scene> loadScene(const std::string &path,
-                                 const std::map<std::string, std::string> &defines);
+                                 const std::map<std::string, std::string> &defines,
+                                 const mtsh_scene_overrides *overrides = nullptr);
 
 // Mesh loaders
 void loadPLY(const std::string &path, Mesh &mesh);   // src/shapes/ply.cpp

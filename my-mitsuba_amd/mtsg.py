@@ -143,20 +143,29 @@ class SceneInfo(C.Structure):
     ]
 
 
+class SceneOverrides(C.Structure):
+    """mtsh_scene_overrides: the values a Mitsuba plugin holds in memory."""
+    _fields_ = [("mask", C.c_uint32), ("film_width", C.c_int32), ("film_height", C.c_int32),
+                ("sample_count", C.c_int32), ("max_depth", C.c_int32), ("rr_depth", C.c_int32),
+                ("strict_normals", C.c_int32), ("hide_emitters", C.c_int32)]
+
+
+MTSH_OVERRIDE_FILM_SIZE, MTSH_OVERRIDE_SAMPLE_COUNT, MTSH_OVERRIDE_INTEGRATOR = 1, 2, 4
+
 _host = None
 _dev = None
 
 DEVICE_SYMBOLS = [
     "mtsg_device_count", "mtsg_scene_create", "mtsg_render", "mtsg_render_device",
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
-    "mtsg_cancel", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
+    "mtsg_cancel", "mtsg_cancel_clear", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
     "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_kd_build", "mtsg_kd_free",
     "mtsg_sampler_draws", "mtsg_debug_wavetimes",
     "mtsg_debug_stragglers",
 ]
 HOST_SYMBOLS = [
-    "mtsh_scene_load", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
+    "mtsh_scene_load", "mtsh_scene_load_overrides", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
     "mtsh_read_image", "mtsh_clip_triangle", "mtsh_texture_image", "mtsh_build_mipmap", "mtsh_scene_textures", "mtsh_scene_om", "mtsh_scene_prim_bounds", "mtsh_scene_set_kdtree",
     "mtsh_last_error",
@@ -199,6 +208,8 @@ def host_lib() -> C.CDLL:
         lib = C.CDLL(path)
         lib.mtsh_scene_load.restype = C.c_void_p
         lib.mtsh_scene_load.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_int]
+        lib.mtsh_scene_load_overrides.restype = C.c_void_p
+        lib.mtsh_scene_load_overrides.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_int, C.POINTER(SceneOverrides)]
         lib.mtsh_scene_desc.restype = C.c_void_p
         lib.mtsh_scene_desc.argtypes = [C.c_void_p]
         lib.mtsh_scene_render_params.argtypes = [C.c_void_p, C.POINTER(RenderParams)]
@@ -247,6 +258,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_device_memset.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         lib.mtsg_device_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
         lib.mtsg_cancel.argtypes = [C.c_void_p]
+        lib.mtsg_cancel_clear.argtypes = [C.c_void_p]
         lib.mtsg_set_flags.argtypes = [C.c_void_p, C.c_uint32]
         lib.mtsg_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
         lib.mtsg_set_batch_paths.argtypes = [C.c_void_p, C.c_uint32]
@@ -281,7 +293,8 @@ def _ptr(a: np.ndarray) -> C.c_void_p:
 class Scene:
     """A loaded Mitsuba XML scene (host side; owns the flat descriptor)."""
 
-    def __init__(self, path: str, defines: dict | None = None, kd_threads: int = 0, instancing: str = "flatten"):
+    def __init__(self, path: str, defines: dict | None = None, kd_threads: int = 0, instancing: str = "flatten",
+                 overrides: SceneOverrides | None = None):
         """instancing: "flatten" (instances become world-space triangles of the
         one scene tree) or "two-level" (Mitsuba's instance / shapegroup
         structure: per-group trees, rays transformed per instance visit)."""
@@ -292,7 +305,10 @@ class Scene:
         lib.mtsh_set_instancing(MTSH_INSTANCING_TWO_LEVEL if instancing == "two-level" else MTSH_INSTANCING_FLATTEN)
         defs = [f"{k}={v}".encode() for k, v in (defines or {}).items()]
         arr = (C.c_char_p * max(1, len(defs)))(*defs)
-        self._h = lib.mtsh_scene_load(path.encode(), arr, len(defs))
+        if overrides is None:
+            self._h = lib.mtsh_scene_load(path.encode(), arr, len(defs))
+        else:
+            self._h = lib.mtsh_scene_load_overrides(path.encode(), arr, len(defs), C.byref(overrides))
         if not self._h:
             raise RuntimeError("scene load failed: " + _err(lib, "mtsh_last_error"))
         self.path = path
@@ -596,3 +612,4 @@ class PathJob:
 
 
 MTSG_ERR_CANCELLED = -4
+MTSG_ERR_TRAVERSAL = -6

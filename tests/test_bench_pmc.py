@@ -1,0 +1,34 @@
+"""bench.py quotes PMC counters (roofline.traffic, tcc_hit_rate, per-kernel
+GB/s) only from a committed set collected on the same kernel instantiation
+and configuration (a two-level line once carried the flattened
+kernel's traffic)."""
+import argparse
+import json
+
+import bench
+
+
+def args(**kw):
+    a = dict(workload="bunny15", instancing="flatten", kd_build="host", width=1280, height=720, spp=256,
+             emulate_ranks=0)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def test_trace_kernel_names():
+    assert bench.trace_kernel(args()) == "k_trace_s<false, 16, false>"
+    assert bench.trace_kernel(args(instancing="two-level")) == "k_trace_s<false, 16, true>"
+
+
+def test_lookup_matches_the_whole_key_only(tmp_path):
+    flat = bench.pmc_key(args())
+    two = bench.pmc_key(args(instancing="two-level"))
+    dev = bench.pmc_key(args(kd_build="device"))
+    share = bench.pmc_key(args(emulate_ranks=8))
+    assert len({json.dumps(k, sort_keys=True) for k in (flat, two, dev, share)}) == 4
+    (tmp_path / "r03_pmc_c3.json").write_text(json.dumps({"key": flat, "kernels": {"k_trace_s<false, 16, false>": {}}}))
+    (tmp_path / "r02_pmc_c3.json").write_text(json.dumps({"key": flat, "kernels": {"old": {}}}))
+    j, src = bench.pmc_lookup(flat, str(tmp_path))
+    assert src.endswith("r03_pmc_c3.json") and "k_trace_s<false, 16, false>" in j["kernels"]
+    for k in (two, dev, share):
+        assert bench.pmc_lookup(k, str(tmp_path)) == (None, None)

@@ -111,3 +111,92 @@ def test_empty_intervals_miss(scene_pair):
     assert not g.trace_shadow(rays).any()
     _, _, _, p0 = O.trace_closest(s.desc, rays)
     assert (p0 == 0xFFFFFFFF).all()
+
+
+def corner_rays(scene, n, seed):
+    """Rays from and towards corners of primitive bounds: points where three
+    candidate split planes of the SAH build meet, so the traversal crosses
+    several split planes at exactly the same distance (the case a short
+    stack can drop entries on, again and again, at one restart distance)."""
+    rng = np.random.default_rng(seed)
+    p = planes(scene)
+    a = p[rng.integers(0, p.shape[0], n)]
+    b = p[rng.integers(0, p.shape[0], n)]
+    ca = np.where(rng.random((n, 3)) < 0.5, a[:, :3], a[:, 3:])
+    cb = np.where(rng.random((n, 3)) < 0.5, b[:, :3], b[:, 3:])
+    d = (cb - ca).astype(np.float64)
+    ln = np.linalg.norm(d, axis=1)
+    ok = ln > 1e-6
+    d = (d[ok] / ln[ok, None]).astype(np.float32)
+    rays = np.zeros((d.shape[0], 8), np.float32)
+    # start behind the first corner so that the ray passes through it
+    rays[:, 0:3] = ca[ok] - 0.25 * d
+    rays[:, 3:6] = d
+    rays[:, 6] = 1e-4
+    rays[:, 7] = np.inf
+    return rays
+
+
+@pytest.mark.parametrize("name", ["cbox", "bunny15", "bunny15-two-level"])
+def test_restart_guard_terminates_and_matches(name, monkeypatch):
+    """Every traversal stack cut to one entry (MTSG_STACK_CAP=1): far children
+    are dropped at almost every second push, rays kd-restart many times, and
+    rays through split-plane corners return to the same restart distance.
+    Without the guard such rays live-lock (they reach the restart limit:
+    MTSG_ERR_TRAVERSAL instead of a hang); with it (kernels.h kd_restart)
+    every query terminates with the same closest hits, bit for bit, as the
+    full stacks give.  (Exact corner rays are a degenerate case of Mitsuba's
+    traversal itself -- the oracle's Havran restatement and brute force
+    disagree on ~1% of them -- so the reference here is the full-stack
+    traversal; test_degenerate_closest compares that with the oracle.)"""
+    inst = "two-level" if name.endswith("two-level") else "flatten"
+    xml = "cbox.xml" if name == "cbox" else "bunny15.xml"
+    s = mtsg.Scene(os.path.join(SCENES, xml), {"width": 32, "height": 24, "spp": 1}, instancing=inst)
+    rays = np.concatenate([corner_rays(s, 30000, 51), degenerate_rays(*bounds(s), 20000, 52, planes(s))])
+    sh = rays.copy()
+    sh[:, 7] = np.random.default_rng(53).uniform(0.01, 4.0, len(sh))
+    g = mtsg.GPUScene(s, 0)
+    ref, ref_sh = g.trace_closest(rays), g.trace_shadow(sh)
+    g.close()
+    monkeypatch.setenv("MTSG_STACK_CAP", "1")
+    monkeypatch.setenv("MTSG_RESTART_GUARD", "100000")   # guard off
+    g = mtsg.GPUScene(s, 0)
+    try:
+        with pytest.raises(RuntimeError, match=r"\(-6\).*restart limit"):
+            g.trace_closest(rays)
+    finally:
+        g.close()
+    monkeypatch.delenv("MTSG_RESTART_GUARD")
+    g = mtsg.GPUScene(s, 0)
+    try:
+        got, got_sh = g.trace_closest(rays), g.trace_shadow(sh)
+    finally:
+        g.close()
+    np.testing.assert_array_equal(got[3], ref[3])
+    for k in range(3):
+        np.testing.assert_array_equal(got[k], ref[k])
+    np.testing.assert_array_equal(got_sh, ref_sh)
+
+
+def test_restart_limit_fails_the_query(monkeypatch):
+    """A ray that reaches the restart limit ends with an error the caller
+    sees (MTSG_ERR_TRAVERSAL), from the debug queries and from the render,
+    instead of the kernel spinning: limit 0 makes the first restart fail."""
+    s = mtsg.Scene(os.path.join(SCENES, "bunny15.xml"), {"width": 64, "height": 36, "spp": 1})
+    monkeypatch.setenv("MTSG_STACK_CAP", "1")
+    monkeypatch.setenv("MTSG_RESTART_LIMIT", "0")
+    g = mtsg.GPUScene(s, 0)
+    try:
+        with pytest.raises(RuntimeError, match=r"\(-6\).*restart limit"):
+            g.trace_closest(corner_rays(s, 20000, 54))
+        with pytest.raises(RuntimeError, match=r"\(-6\).*restart limit"):
+            g.render(s.params(), s.border)
+    finally:
+        g.close()
+    # with the default limit the frame renders
+    monkeypatch.delenv("MTSG_RESTART_LIMIT")
+    g = mtsg.GPUScene(s, 0)
+    try:
+        g.render(s.params(), s.border)
+    finally:
+        g.close()

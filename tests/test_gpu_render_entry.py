@@ -162,3 +162,54 @@ def test_path_job_reports_the_failing_gpu(c3_full):
     assert rc == -1
     assert job.last_error().startswith("GPU 0: spp")
     job.close()
+
+
+def test_path_job_cancel_racing_the_end_of_a_render(c3_full):
+    """cancel() calls that land around the moment a render returns never
+    leave a stale flag behind: the job's next render completes (ADVICE r02:
+    mtsh_path_job_cancel's check-then-cancel window)."""
+    job = mtsg.PathJob(c3_full, 1)
+    small = c3_full.params(tile_w=128, tile_h=64, spp=2)
+    stop = threading.Event()
+
+    def spam():
+        while not stop.is_set():
+            job.cancel()
+    for _ in range(20):
+        th = threading.Thread(target=spam)
+        th.start()
+        rc, _, _ = job.render(small, c3_full.border)
+        stop.set()
+        th.join()
+        stop.clear()
+        assert rc in (0, mtsg.MTSG_ERR_CANCELLED), job.last_error()
+        rc, img, _ = job.render(small, c3_full.border)
+        assert rc == 0, job.last_error()
+        assert img[..., 4].sum() > 0
+    job.close()
+
+
+def test_plugin_flow_with_overriding_defines():
+    """INTEGRATION.md's plugin: Mitsuba parsed the scene with -D width/height/
+    spp/maxDepth; the plugin passes the values it holds in memory to
+    mtsh_scene_load_overrides in preprocess(), creates the job once, and
+    render() goes through mtsh_path_job_render.  The block has the overridden
+    size, every pixel got the overridden sample count, and the image equals
+    the one of the scene loaded with the same -D map."""
+    from test_plugin_overrides import overrides_for
+    xml = os.path.join(SCENES, "bunny15.xml")
+    by_defines = mtsg.Scene(xml, {"width": 96, "height": 40, "spp": 3, "maxDepth": 5})
+    by_plugin = mtsg.Scene(xml, {}, overrides=overrides_for(96, 40, 3, max_depth=5))
+    p = by_plugin.params()
+    assert (p.tile_w, p.tile_h, p.spp, p.max_depth) == (96, 40, 3, 5)
+    job = mtsg.PathJob(by_plugin, 0)
+    rc, img, _ = job.render(p, by_plugin.border)
+    assert rc == 0, job.last_error()
+    b = by_plugin.border
+    assert img.shape == (40 + 2 * b, 96 + 2 * b, 5)
+    job.close()
+    ref_job = mtsg.PathJob(by_defines, 0)
+    rc, ref, _ = ref_job.render(by_defines.params(), by_defines.border)
+    ref_job.close()
+    assert rc == 0
+    np.testing.assert_array_equal(img, ref)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# rocprofv3 set of one bench configuration: kernel stats, then FETCH_SIZE,
+# WRITE_SIZE and TCC hit/miss in separate --pmc passes of one step each,
+# summarised per kernel and keyed by the configuration (tools/pmc_kernels.py).
+#   tools/gpu_pmc_config.sh r03 c3 [bench.py args...]
+R=$1; TAG=$2; shift 2
+O=gpurun_out/pmc_${R}_${TAG}
+mkdir -p $O
+export TMPDIR=/tmp
+step() { local name=$1 lim=$2; shift 2; echo "== $TAG $name $(date +%T)"; timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; if [ $rc -ne 0 ]; then tail -n 5 "$O/$name.log"; exit $rc; fi; }
+ARGS="--no-cpu --no-parity --no-count $*"
+step stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O -o stats -- python bench.py $ARGS --steps 3 --warmup 1
+step fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O -o fetch -- python bench.py $ARGS --steps 1 --warmup 0
+step write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O -o write -- python bench.py $ARGS --steps 1 --warmup 0
+step tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O -o tcc -- python bench.py $ARGS --steps 1 --warmup 0
+KEY=$(python bench.py $ARGS --print-pmc-key)
+python tools/pmc_kernels.py $O "$KEY" > $O/pmc.json && echo "pmc summary: $O/pmc.json"
