@@ -356,7 +356,7 @@ def main():
                       "k_camera": kernels["camera_ms"], "k_splat": kernels["splat_ms"]}
             pmc = {}
             for fam, ms in fam_ms.items():
-                ks = [v for n, v in pj["kernels"].items() if n.startswith(fam + "<") or n.startswith(fam + "(")]
+                ks = [v for n, v in pj["kernels"].items() if n == fam or n.startswith(fam + "<")]
                 b = sum(v.get("traffic_bytes_per_step", 0.0) for v in ks)
                 if b > 0 and ms > 0:
                     hits = [v["tcc_hit_rate"] for v in ks if "tcc_hit_rate" in v]
@@ -424,7 +424,12 @@ def main():
                     # SIMD efficiency of the traversal waves (instrumented pass)
                     "simd_active_lanes": round(per(cs.wave_active_lanes, 64 * cs.wave_steps), 3),
                     "simd_eff_inner": round(per(cs.nodes_visited + cs.shadow_nodes_visited, 64 * cs.wave_node_iters), 3),
-                    "simd_eff_leaf": round(per(cs.tri_tests + cs.shadow_tri_tests, 64 * cs.wave_test_iters), 3)}
+                    "simd_eff_leaf": round(per(cs.tri_tests + cs.shadow_tri_tests, 64 * cs.wave_test_iters), 3),
+                    # lane-iterations of the traversal loop per ray (one node
+                    # fetch + one primitive fetch each), and instance entries
+                    "iterations_per_ray": round(per(cs.wave_active_lanes, cs.rays_closest + cs.rays_shadow), 2),
+                    "instance_visits_per_ray": round(per(cs.instance_visits + cs.shadow_instance_visits,
+                                                         cs.rays_closest + cs.rays_shadow), 3)}
         if a.save:
             img = mtsg.develop(host_block[border:H - border, border:W - border])
             np.save(a.save, img)

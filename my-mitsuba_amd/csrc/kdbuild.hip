@@ -44,8 +44,16 @@ void set_last_error(const std::string &e);   // mtsg.hip
 
 namespace {
 
-constexpr int KD_BINS = 32;
+constexpr int KD_BINS = 128;                  // Mitsuba's m_minMaxBins (gkdtree.h:2406-2500)
 constexpr int BIN_WORDS = 3 * KD_BINS * 2;    // [axis][bin][min, max]
+// nodes of at most EXACT_MAX references get Mitsuba's exact O(n log n) SAH
+// sweep over their sorted edge events (gkdtree.h:1954-2400), one workgroup
+// per node with the events in LDS; larger ones are binned.  (Mitsuba sweeps
+// exactly below 65,536; the host build's sweep at a 4,096 threshold renders
+// C3 within 1% of that)
+constexpr uint32_t EXACT_MAX = 4096;
+constexpr int EXACT_BLK = 1024;
+constexpr int MAX_BAD_REFINES = 3;            // m_maxBadRefines
 constexpr uint32_t CHUNK = 4096;              // refs per binning workgroup
 constexpr int BLK = 256;
 
@@ -59,11 +67,11 @@ struct NodeDev {
     float lo[3], hi[3];
 };
 
-struct Decision {   // k_sah -> host
+struct Decision {   // k_sah / k_exact -> host
     int axis;       // -1: no split candidate
     float split;
     float cost;
-    uint32_t pad;
+    uint32_t planarLeft;   // primitives lying in the split plane go left (exact sweep)
 };
 
 struct Plan {       // host -> k_count / k_scatter
@@ -71,7 +79,8 @@ struct Plan {       // host -> k_count / k_scatter
     float split;
     uint32_t out0, out1;   // inner: next-level ref offsets of the children; leaf: index-list offset
     uint32_t child0;       // inner: next-level node index of the left child (right = +1)
-    uint32_t pad[3];
+    uint32_t planarLeft;
+    uint32_t pad[2];
 };
 
 struct Task { uint32_t node, begin, end, pad; };
@@ -140,7 +149,7 @@ __device__ void classify(const Ref &r, const Plan &p, const NodeDev &n, const Ge
     const float mn = axisOf(r.mn, p.axis), mx = axisOf(r.mx, p.axis);
     goL = mn < p.split;
     goR = mx > p.split;
-    if (!goL && !goR) goL = true;   // planar on the plane
+    if (!goL && !goR) { goL = p.planarLeft != 0; goR = !goL; }   // planar, in the plane
     L = r;
     R = r;
     if (p.axis == 0) { L.mx.x = fminf(L.mx.x, p.split); R.mn.x = fmaxf(R.mn.x, p.split); }
@@ -170,7 +179,7 @@ __global__ void k_bin(const Ref *refs, const NodeDev *nodes, const Task *tasks, 
     float scale[3];
     for (int a = 0; a < 3; ++a) {
         const float ext = n.hi[a] - n.lo[a];
-        scale[a] = ext > 0 ? (float)KD_BINS / ext : 0.0f;
+        scale[a] = ext > 0 ? (float)KD_BINS / ext : 0.0f;   // invW of findBinned
     }
     for (uint32_t i = t.begin + threadIdx.x; i < t.end; i += blockDim.x) {
         const Ref r = refs[i];
@@ -184,9 +193,21 @@ __global__ void k_bin(const Ref *refs, const NodeDev *nodes, const Task *tasks, 
         if (h[i]) atomicAdd(&bins[(size_t)t.node * BIN_WORDS + i], h[i]);
 }
 
-__device__ inline float area(const float lo[3], const float hi[3]) {
-    const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
-    return 2.0f * (dx * dy + dy * dz + dz * dx);
+// SurfaceAreaHeuristic3 (sahkdtree3.h:39-84) in the host build's form
+// (host/kdtree.cpp cost), so both builds price a split identically
+__device__ inline float sah_cost(const float lo[3], const float hi[3], int axis, float pos, uint32_t nL, uint32_t nR,
+                                 float travCost, float queryCost, float emptyBonus) {
+    const float ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
+    const float tmp = ex * ey + ey * ez + ex * ez;
+    if (tmp <= 0) return INFINITY;
+    const float inv = 1.0f / tmp;
+    const float e[3] = {ex, ey, ez};
+    const int a1 = axis == 2 ? 0 : axis + 1, a2 = axis == 0 ? 2 : axis - 1;
+    const float t0 = e[a1] * e[a2] * inv, t1 = (e[a1] + e[a2]) * inv;
+    const float pL = t0 + t1 * (pos - lo[axis]), pR = t0 + t1 * (hi[axis] - pos);
+    float c = travCost + queryCost * (pL * (float)nL + pR * (float)nR);
+    if (nL == 0 || nR == 0) c *= emptyBonus;
+    return c;
 }
 
 __global__ void k_sah(const NodeDev *nodes, uint32_t nNodes, const uint32_t *bins, Decision *out, float travCost, float queryCost,
@@ -194,30 +215,157 @@ __global__ void k_sah(const NodeDev *nodes, uint32_t nNodes, const uint32_t *bin
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nNodes) return;
     const NodeDev n = nodes[i];
+    if (n.count <= EXACT_MAX) return;   // k_exact's node, or a leaf
     const uint32_t *b = bins + (size_t)i * BIN_WORDS;
-    const float sa = area(n.lo, n.hi);
-    Decision best{-1, 0.0f, INFINITY, 0u};
+    Decision best{-1, 0.0f, INFINITY, 1u};
+    // findBinned (host/kdtree.cpp; gkdtree.h:2406-2500 MinMaxBins::bestSplit)
     for (int a = 0; a < 3; ++a) {
         const float ext = n.hi[a] - n.lo[a];
-        if (!(ext > 0) || !(sa > 0)) continue;
-        uint32_t nR = 0;
-        for (int k = 0; k < KD_BINS; ++k) nR += b[(a * KD_BINS + k) * 2 + 1];
-        uint32_t nL = 0;
+        if (!(ext > 0)) continue;
+        const float w = ext / (float)KD_BINS;
+        uint32_t nR = n.count, nL = 0;
         for (int k = 1; k < KD_BINS; ++k) {
             nL += b[(a * KD_BINS + k - 1) * 2];
             nR -= b[(a * KD_BINS + k - 1) * 2 + 1];
-            const float s = n.lo[a] + ext * ((float)k / (float)KD_BINS);
+            const float s = n.lo[a] + w * (float)k;
             if (!(s > n.lo[a] && s < n.hi[a])) continue;
-            float lhi[3] = {n.hi[0], n.hi[1], n.hi[2]}, rlo[3] = {n.lo[0], n.lo[1], n.lo[2]};
-            lhi[a] = s;
-            rlo[a] = s;
-            const float pL = area(n.lo, lhi) / sa, pR = area(rlo, n.hi) / sa;
-            float cost = travCost + queryCost * (pL * (float)nL + pR * (float)nR);
-            if (nL == 0 || nR == 0) cost *= emptyBonus;
-            if (cost < best.cost) best = Decision{a, s, cost, 0u};
+            const float cost = sah_cost(n.lo, n.hi, a, s, nL, nR, travCost, queryCost, emptyBonus);
+            if (cost < best.cost) best = Decision{a, s, cost, 1u};
         }
     }
     out[i] = best;
+}
+
+// The exact SAH sweep of one node (findExact, host/kdtree.cpp; Mitsuba's
+// buildTree edge-event sweep, gkdtree.h:1954-2400): per axis, the edge events
+// of the node's references -- start / end of a box, one planar event for a
+// box flat on that axis -- sorted by (position, end < planar < start) with a
+// bitonic sort in LDS; two exclusive scans give, at the first event of each
+// position, the references left of the plane (started or planar before it)
+// and right of it (not yet ended); both placements of the planar ones are
+// priced.  The winner is the cheapest candidate, the earliest one in
+// (axis, position, left-before-right) order on ties, as the serial sweep.
+__device__ inline uint32_t ordered(float f) {
+    const uint32_t u = __float_as_uint(f == 0.0f ? 0.0f : f);   // -0 and +0: one position
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float unordered(uint32_t o) { return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o); }
+
+__global__ void __launch_bounds__(EXACT_BLK) k_exact(const Ref *refs, const NodeDev *nodes, const uint32_t *taskNodes, Decision *out,
+                                                     float travCost, float queryCost, float emptyBonus) {
+    extern __shared__ unsigned long long ev[];                 // 2 * EXACT_MAX events
+    __shared__ uint32_t scanA[EXACT_BLK], scanB[EXACT_BLK];   // per-thread totals -> exclusive prefixes
+    __shared__ float bestCost[EXACT_BLK / 64], bestPos[EXACT_BLK / 64];
+    __shared__ uint32_t bestKey[EXACT_BLK / 64];
+    const uint32_t node = taskNodes[blockIdx.x];
+    const NodeDev n = nodes[node];
+    const uint32_t N = n.count;
+    uint32_t m = 1;
+    while (m < 2 * N) m <<= 1;                                // padded event count (power of two)
+    const uint32_t per = (m + EXACT_BLK - 1) / EXACT_BLK;     // events per thread in the scans
+    float myCost = INFINITY, myPos = 0.0f;
+    uint32_t myKey = 0xFFFFFFFFu;                              // axis << 30 | event << 1 | right
+    for (int a = 0; a < 3; ++a) {
+        if (!(n.hi[a] > n.lo[a])) continue;
+        // events: key = ordered(position) << 32 | type << 30 (0 end, 1 planar, 2 start)
+        for (uint32_t i = threadIdx.x; i < m; i += EXACT_BLK) ev[i] = ~0ull;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < N; i += EXACT_BLK) {
+            const Ref r = refs[n.begin + i];
+            const float lo = axisOf(r.mn, a), hi = axisOf(r.mx, a);
+            if (lo == hi) {
+                ev[2 * i] = (unsigned long long)ordered(lo) << 32 | 1ull << 30;
+            } else {
+                ev[2 * i] = (unsigned long long)ordered(lo) << 32 | 2ull << 30;
+                ev[2 * i + 1] = (unsigned long long)ordered(hi) << 32;
+            }
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= m; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < m; i += EXACT_BLK) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const unsigned long long x = ev[i], y = ev[l];
+                        if (((i & k) == 0) == (x > y)) { ev[i] = y; ev[l] = x; }
+                    }
+                }
+                __syncthreads();
+            }
+        // exclusive scans of (start | planar) and (end | planar) over events
+        const uint32_t e0 = threadIdx.x * per;
+        uint32_t sa = 0, sb = 0;
+        for (uint32_t e = e0; e < min(m, e0 + per); ++e) {
+            const unsigned long long x = ev[e];
+            if (x == ~0ull) continue;
+            const uint32_t ty = (uint32_t)(x >> 30) & 3u;
+            sa += ty != 0u;
+            sb += ty != 2u;
+        }
+        scanA[threadIdx.x] = sa;
+        scanB[threadIdx.x] = sb;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t ra = 0, rb = 0;
+            for (int t = 0; t < EXACT_BLK; ++t) {
+                const uint32_t xa = scanA[t], xb = scanB[t];
+                scanA[t] = ra;
+                scanB[t] = rb;
+                ra += xa;
+                rb += xb;
+            }
+        }
+        __syncthreads();
+        uint32_t pa = scanA[threadIdx.x], pb = scanB[threadIdx.x];
+        for (uint32_t e = e0; e < min(m, e0 + per); ++e) {
+            const unsigned long long x = ev[e];
+            if (x == ~0ull) break;
+            const uint32_t ty = (uint32_t)(x >> 30) & 3u;
+            const uint32_t pos = (uint32_t)(x >> 32);
+            if (e == 0 || (uint32_t)(ev[e - 1] >> 32) != pos) {
+                // first event at this position: count the group's ends and planars
+                uint32_t pe = 0, pp = 0;
+                for (uint32_t f = e; f < m && ev[f] != ~0ull && (uint32_t)(ev[f] >> 32) == pos; ++f) {
+                    const uint32_t t2 = (uint32_t)(ev[f] >> 30) & 3u;
+                    pe += t2 == 0u;
+                    pp += t2 == 1u;
+                }
+                const float p = unordered(pos);
+                if (p > n.lo[a] && p < n.hi[a]) {
+                    const uint32_t nL = pa, nR = N - pb - pe - pp;
+                    const float cl = sah_cost(n.lo, n.hi, a, p, nL + pp, nR, travCost, queryCost, emptyBonus);
+                    const float cr = sah_cost(n.lo, n.hi, a, p, nL, nR + pp, travCost, queryCost, emptyBonus);
+                    const uint32_t key = (uint32_t)a << 30 | e << 1;
+                    if (cl < myCost || (cl == myCost && key < myKey)) { myCost = cl; myKey = key; myPos = p; }
+                    if (cr < myCost || (cr == myCost && (key | 1u) < myKey)) { myCost = cr; myKey = key | 1u; myPos = p; }
+                }
+            }
+            pa += ty != 0u;
+            pb += ty != 2u;
+        }
+        __syncthreads();
+    }
+    // block minimum of (cost, key); the position travels with it
+    for (int o = 32; o > 0; o >>= 1) {
+        const float c2 = __shfl_down(myCost, o), p2 = __shfl_down(myPos, o);
+        const uint32_t k2 = __shfl_down(myKey, o);
+        if (c2 < myCost || (c2 == myCost && k2 < myKey)) { myCost = c2; myKey = k2; myPos = p2; }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        bestCost[threadIdx.x >> 6] = myCost;
+        bestKey[threadIdx.x >> 6] = myKey;
+        bestPos[threadIdx.x >> 6] = myPos;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float c = INFINITY, pos = 0.0f;
+        uint32_t k = 0xFFFFFFFFu;
+        for (int w = 0; w < EXACT_BLK / 64; ++w)
+            if (bestCost[w] < c || (bestCost[w] == c && bestKey[w] < k)) { c = bestCost[w]; k = bestKey[w]; pos = bestPos[w]; }
+        Decision d{-1, 0.0f, INFINITY, 1u};
+        if (k != 0xFFFFFFFFu && c < INFINITY) d = Decision{(int)(k >> 30), pos, c, (k & 1u) ? 0u : 1u};
+        out[node] = d;
+    }
 }
 
 // one counter pair per inner node: wave-aggregated when a wave's lanes share
@@ -303,9 +451,107 @@ struct DevBuf {
     template <class T> T *as() const { return (T *)p; }
 };
 
-struct HostNode { uint32_t begin, count, out, depth; float lo[3], hi[3]; };
+struct HostNode { uint32_t begin, count, out, depth, bad; float lo[3], hi[3]; };
+// what the retraction pass needs of every node of the tree (box, references)
+struct NodeInfo { float lo[3], hi[3]; uint32_t count; };
 
 inline float bitsToFloat(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+// Retraction (m_retract, gkdtree.h:739-742 and 1910-1922; host/kdtree.cpp
+// build): bottom up, a split whose subtree costs no less than a leaf of the
+// node's references becomes that leaf (the unique primitives of its
+// leaves).  Then the tree is re-laid out breadth first (children adjacent,
+// KDNode encoding).  Returns the number of retracted splits.
+uint32_t retract_and_compact(std::vector<mtsg_kdnode> &nodes, const std::vector<NodeInfo> &info, std::vector<uint32_t> &idx,
+                             const mtsg_kd_build_params &P, uint32_t &leaves, uint32_t &depthOut) {
+    const size_t n = nodes.size();
+    std::vector<float> cost(n, 0.0f);
+    std::vector<uint8_t> collapse(n, 0);
+    auto isLeaf = [&](size_t i) { return (nodes[i].combined & 0x80000000u) != 0; };
+    auto leftOf = [&](size_t i) { return i + (nodes[i].combined >> 2); };
+    // post-order over the tree
+    std::vector<std::pair<uint32_t, bool>> st{{0u, false}};
+    uint32_t retracted = 0;
+    while (!st.empty()) {
+        auto [i, expanded] = st.back();
+        st.pop_back();
+        if (isLeaf(i)) { cost[i] = P.query_cost * (float)info[i].count; continue; }
+        const uint32_t l = (uint32_t)leftOf(i);
+        if (!expanded) {
+            st.push_back({i, true});
+            st.push_back({l, false});
+            st.push_back({l + 1, false});
+            continue;
+        }
+        const NodeInfo &b = info[i];
+        const int axis = (int)(nodes[i].combined & 3u);
+        const float pos = bitsToFloat(nodes[i].data);
+        const float e[3] = {b.hi[0] - b.lo[0], b.hi[1] - b.lo[1], b.hi[2] - b.lo[2]};
+        const float tmp = e[0] * e[1] + e[1] * e[2] + e[0] * e[2];
+        const float inv = tmp > 0 ? 1.0f / tmp : 0.0f;
+        const int a1 = (axis + 1) % 3, a2 = (axis + 2) % 3;
+        const float t0 = e[a1] * e[a2] * inv, t1 = (e[a1] + e[a2]) * inv;
+        const float pL = t0 + t1 * (pos - b.lo[axis]), pR = t0 + t1 * (b.hi[axis] - pos);
+        const float finalCost = P.traversal_cost + (pL * cost[l] + pR * cost[l + 1]);
+        const float leafCost = P.query_cost * (float)b.count;
+        if (finalCost < leafCost) {
+            cost[i] = finalCost;
+        } else {
+            cost[i] = leafCost;
+            collapse[i] = 1;
+            ++retracted;
+        }
+    }
+    // breadth-first re-layout
+    std::vector<mtsg_kdnode> out(1);
+    std::vector<uint32_t> outIdx;
+    outIdx.reserve(idx.size());
+    leaves = 0;
+    depthOut = 0;
+    struct Q { uint32_t old, slot, depth; };
+    std::vector<Q> q{{0u, 0u, 0u}};
+    std::vector<uint32_t> ids;
+    for (size_t h = 0; h < q.size(); ++h) {
+        const Q c = q[h];
+        depthOut = std::max(depthOut, c.depth);
+        if (isLeaf(c.old) || collapse[c.old]) {
+            ids.clear();
+            // the primitives of the (sub)tree's leaves, unique and ascending
+            std::vector<uint32_t> sub{c.old};
+            while (!sub.empty()) {
+                const uint32_t k = sub.back();
+                sub.pop_back();
+                if (isLeaf(k)) {
+                    const uint32_t s0 = nodes[k].combined & 0x7FFFFFFFu, e0 = nodes[k].data;
+                    ids.insert(ids.end(), idx.begin() + s0, idx.begin() + e0);
+                } else {
+                    const uint32_t l = (uint32_t)leftOf(k);
+                    sub.push_back(l);
+                    sub.push_back(l + 1);
+                }
+            }
+            if (!isLeaf(c.old)) {
+                std::sort(ids.begin(), ids.end());
+                ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+            }
+            out[c.slot].combined = 0x80000000u | (uint32_t)outIdx.size();
+            outIdx.insert(outIdx.end(), ids.begin(), ids.end());
+            out[c.slot].data = (uint32_t)outIdx.size();
+            ++leaves;
+            continue;
+        }
+        const uint32_t left = (uint32_t)out.size();
+        out.resize(out.size() + 2);
+        out[c.slot].combined = (nodes[c.old].combined & 3u) | ((left - c.slot) << 2);
+        out[c.slot].data = nodes[c.old].data;
+        const uint32_t ol = (uint32_t)leftOf(c.old);
+        q.push_back({ol, left, c.depth + 1});
+        q.push_back({ol + 1, left + 1, c.depth + 1});
+    }
+    nodes.swap(out);
+    idx.swap(outIdx);
+    return retracted;
+}
 
 }  // namespace
 
@@ -385,29 +631,53 @@ int mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bo
         geo.tri = dTri.as<uint4>();
     }
     std::vector<HostNode> level;
-    if (nLive) level.push_back(HostNode{0, nLive, 0, 0, {lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}});
+    if (nLive) level.push_back(HostNode{0, nLive, 0, 0, 0, {lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}});
+    std::vector<NodeInfo> info(1, NodeInfo{{lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}, nLive});
     uint32_t nRefs = nLive, nIndices = 0, depthReached = 0;
     std::vector<NodeDev> nd;
     std::vector<Task> tasks;
     std::vector<Decision> dec;
     std::vector<Plan> plans;
-    std::vector<uint32_t> counts;
+    std::vector<uint32_t> counts, exactNodes;
+    DevBuf dExact;
+    if (hipFuncSetAttribute((const void *)k_exact, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(2 * EXACT_MAX * sizeof(unsigned long long))) != hipSuccess)
+        return fail("k_exact shared memory");
     while (!level.empty()) {
         const uint32_t nN = (uint32_t)level.size();
         nd.resize(nN);
         tasks.clear();
+        exactNodes.clear();
+        uint32_t exactMaxCount = 0;
         for (uint32_t i = 0; i < nN; ++i) {
             const HostNode &h = level[i];
             nd[i] = NodeDev{h.begin, h.count, {h.lo[0], h.lo[1], h.lo[2]}, {h.hi[0], h.hi[1], h.hi[2]}};
             depthReached = std::max(depthReached, h.depth);
-            if (h.count <= (uint32_t)P.stop_prims || (int)h.depth >= maxDepth) continue;   // leaf without binning
+            if (h.count <= (uint32_t)P.stop_prims || (int)h.depth >= maxDepth) continue;   // leaf without a sweep
+            if (h.count <= EXACT_MAX) {
+                exactNodes.push_back(i);
+                exactMaxCount = std::max(exactMaxCount, h.count);
+                continue;
+            }
             for (uint32_t b = h.begin; b < h.begin + h.count; b += CHUNK) tasks.push_back(Task{i, b, std::min(b + CHUNK, h.begin + h.count), 0});
         }
         if (!dNodes.reserve(nN * sizeof(NodeDev)) || !dBins.reserve((size_t)nN * BIN_WORDS * 4) || !dDec.reserve(nN * sizeof(Decision)) ||
             !dPlans.reserve(nN * sizeof(Plan)) || !dCnt.reserve((size_t)nN * 2 * 4) || !dTasks.reserve(std::max<size_t>(1, tasks.size()) * sizeof(Task)))
             return fail("out of device memory");
         if (hipMemcpy(dNodes.p, nd.data(), nN * sizeof(NodeDev), hipMemcpyHostToDevice) != hipSuccess) return fail("upload");
-        dec.assign(nN, Decision{-1, 0.0f, INFINITY, 0u});
+        dec.assign(nN, Decision{-1, 0.0f, INFINITY, 1u});
+        if (hipMemcpy(dDec.p, dec.data(), nN * sizeof(Decision), hipMemcpyHostToDevice) != hipSuccess) return fail("upload");
+        if (!exactNodes.empty()) {
+            if (!dExact.reserve(exactNodes.size() * sizeof(uint32_t)) ||
+                hipMemcpy(dExact.p, exactNodes.data(), exactNodes.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess)
+                return fail("upload");
+            uint32_t m = 1;
+            while (m < 2 * exactMaxCount) m <<= 1;
+            hipLaunchKernelGGL(k_exact, dim3((uint32_t)exactNodes.size()), dim3(EXACT_BLK), m * sizeof(unsigned long long), 0,
+                               dRefs.as<Ref>(), dNodes.as<NodeDev>(), dExact.as<uint32_t>(), dDec.as<Decision>(), P.traversal_cost,
+                               P.query_cost, P.empty_space_bonus);
+            if (hipGetLastError() != hipSuccess) return fail("k_exact launch");
+        }
         if (!tasks.empty()) {
             if (hipMemset(dBins.p, 0, (size_t)nN * BIN_WORDS * 4) != hipSuccess ||
                 hipMemcpy(dTasks.p, tasks.data(), tasks.size() * sizeof(Task), hipMemcpyHostToDevice) != hipSuccess)
@@ -416,15 +686,29 @@ int mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bo
                                dBins.as<uint32_t>());
             hipLaunchKernelGGL(k_sah, dim3((nN + BLK - 1) / BLK), dim3(BLK), 0, 0, dNodes.as<NodeDev>(), nN, dBins.as<uint32_t>(),
                                dDec.as<Decision>(), P.traversal_cost, P.query_cost, P.empty_space_bonus);
-            if (hipMemcpy(dec.data(), dDec.p, nN * sizeof(Decision), hipMemcpyDeviceToHost) != hipSuccess) return fail("download");
         }
+        if ((!tasks.empty() || !exactNodes.empty()) &&
+            hipMemcpy(dec.data(), dDec.p, nN * sizeof(Decision), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail("download");
         // leaf decisions
-        plans.assign(nN, Plan{-1, 0.0f, 0, 0, 0, {0, 0, 0}});
+        // (buildTree's leaf / bad-refine decisions, gkdtree.h:1818-1850, as
+        // host/kdtree.cpp: a split no cheaper than the leaf is still taken up
+        // to MAX_BAD_REFINES times on a path, the retraction pass below
+        // undoes the ones that did not pay off)
+        plans.assign(nN, Plan{-1, 0.0f, 0, 0, 0, 1u, {0, 0}});
+        std::vector<uint32_t> badOf(nN, 0);
         for (uint32_t i = 0; i < nN; ++i) {
             const HostNode &h = level[i];
-            const bool leaf = h.count <= (uint32_t)P.stop_prims || (int)h.depth >= maxDepth || dec[i].axis < 0 ||
-                              !(dec[i].cost < P.query_cost * (float)h.count);
-            if (!leaf) { plans[i].axis = dec[i].axis; plans[i].split = dec[i].split; }
+            badOf[i] = h.bad;
+            if (h.count <= (uint32_t)P.stop_prims || (int)h.depth >= maxDepth || dec[i].axis < 0) continue;
+            const float leafCost = P.query_cost * (float)h.count;
+            if (!(dec[i].cost < leafCost)) {
+                if ((dec[i].cost > 4 * leafCost && h.count < 16) || (int)h.bad >= MAX_BAD_REFINES) continue;
+                ++badOf[i];
+            }
+            plans[i].axis = dec[i].axis;
+            plans[i].split = dec[i].split;
+            plans[i].planarLeft = dec[i].planarLeft;
         }
         if (hipMemcpy(dPlans.p, plans.data(), nN * sizeof(Plan), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemset(dCnt.p, 0, (size_t)nN * 2 * 4) != hipSuccess)
@@ -449,6 +733,7 @@ int mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bo
             }
             const uint32_t left = (uint32_t)nodes.size();
             nodes.resize(nodes.size() + 2);
+            info.resize(nodes.size());
             uint32_t splitBits;
             memcpy(&splitBits, &p.split, 4);
             nodes[h.out].combined = (uint32_t)p.axis | ((left - h.out) << 2);
@@ -456,10 +741,12 @@ int mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bo
             p.child0 = (uint32_t)next.size();
             p.out0 = nextRefs;
             p.out1 = nextRefs + counts[2 * i];
-            HostNode L{p.out0, counts[2 * i], left, h.depth + 1, {h.lo[0], h.lo[1], h.lo[2]}, {h.hi[0], h.hi[1], h.hi[2]}};
-            HostNode R{p.out1, counts[2 * i + 1], left + 1, h.depth + 1, {h.lo[0], h.lo[1], h.lo[2]}, {h.hi[0], h.hi[1], h.hi[2]}};
+            HostNode L{p.out0, counts[2 * i], left, h.depth + 1, badOf[i], {h.lo[0], h.lo[1], h.lo[2]}, {h.hi[0], h.hi[1], h.hi[2]}};
+            HostNode R{p.out1, counts[2 * i + 1], left + 1, h.depth + 1, badOf[i], {h.lo[0], h.lo[1], h.lo[2]}, {h.hi[0], h.hi[1], h.hi[2]}};
             L.hi[p.axis] = p.split;
             R.lo[p.axis] = p.split;
+            info[left] = NodeInfo{{L.lo[0], L.lo[1], L.lo[2]}, {L.hi[0], L.hi[1], L.hi[2]}, L.count};
+            info[left + 1] = NodeInfo{{R.lo[0], R.lo[1], R.lo[2]}, {R.hi[0], R.hi[1], R.hi[2]}, R.count};
             next.push_back(L);
             next.push_back(R);
             nextRefs += counts[2 * i] + counts[2 * i + 1];
@@ -503,17 +790,18 @@ int mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bo
             return fail("upload");
         hipLaunchKernelGGL(k_sort_leaves, dim3((nLeaves + BLK - 1) / BLK), dim3(BLK), 0, 0, dIdx.as<uint32_t>(), dRanges.as<uint2>(), nLeaves);
     }
+    std::vector<uint32_t> idx(nIndices);
+    if (nIndices && hipMemcpy(idx.data(), dIdx.p, (size_t)nIndices * 4, hipMemcpyDeviceToHost) != hipSuccess) return fail("download");
+    if (hipDeviceSynchronize() != hipSuccess) return fail("kernel failure");
+    uint32_t nLeavesOut = nLeaves;
+    if (nLive) retract_and_compact(nodes, info, idx, P, nLeavesOut, depthReached);
     out->n_nodes = (uint32_t)nodes.size();
-    out->n_indices = nIndices;
+    out->n_indices = (uint32_t)idx.size();
     out->nodes = (mtsg_kdnode *)malloc(nodes.size() * sizeof(mtsg_kdnode));
-    out->indices = (uint32_t *)malloc(std::max<size_t>(1, nIndices) * sizeof(uint32_t));
+    out->indices = (uint32_t *)malloc(std::max<size_t>(1, idx.size()) * sizeof(uint32_t));
     if (!out->nodes || !out->indices) { mtsg_kd_free(out); mtsg::set_last_error("mtsg_kd_build: out of host memory"); return MTSG_ERR_OOM; }
     memcpy(out->nodes, nodes.data(), nodes.size() * sizeof(mtsg_kdnode));
-    if (nIndices && hipMemcpy(out->indices, dIdx.p, (size_t)nIndices * 4, hipMemcpyDeviceToHost) != hipSuccess) {
-        mtsg_kd_free(out);
-        return fail("download");
-    }
-    if (hipDeviceSynchronize() != hipSuccess) { mtsg_kd_free(out); return fail("kernel failure"); }
+    if (!idx.empty()) memcpy(out->indices, idx.data(), idx.size() * sizeof(uint32_t));
     // the enlarged tree AABB (MTS_KD_AABB_EPSILON, gkdtree.h:1213-1220), as host/kdtree.cpp
     const float eps = 1e-3f;
     for (int k = 0; k < 3; ++k) {
@@ -522,7 +810,7 @@ int mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bo
         out->aabb_max[k] = hi[k] + (hi[k] - out->aabb_min[k]) * eps + eps;
     }
     out->max_depth = depthReached;
-    out->leaves = nLeaves;
+    out->leaves = nLeavesOut;
     out->ms_build = std::chrono::duration<double, std::milli>(clock::now() - t0).count();
     return MTSG_OK;
 }

@@ -258,6 +258,14 @@ constexpr size_t PATH_STATE_BYTES = 272;    // bytes per path slot (DevPaths: 2 
 #define MTSG_SHORT_STACK 6   // 6 x 12 B x 64 lanes = 4.6 KB LDS/wave -> 8 waves/SIMD (8: 6.5, 12: 4.2)
 #endif
 constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per lane
+// two-level traversal (kernels.h spec_iter_i): the top level's stack, and the
+// group level's own, one entry shorter than the flat traversal's: 5 x 12 B +
+// 2 x 12 B per lane = 5.25 KB per wave, 7 waves/SIMD
+constexpr int OUTER_STACK = 2;
+#ifndef MTSG_INNER_STACK
+#define MTSG_INNER_STACK 5
+#endif
+constexpr int INNER_STACK = MTSG_INNER_STACK;
 // the compact speculative traversal is sized for 8 waves per SIMD (64 VGPRs)
 #ifndef MTSG_SPEC_WAVES
 #define MTSG_SPEC_WAVES 8
@@ -502,6 +510,16 @@ enum : uint32_t {
 // scenes at hand restart 0-3 times (tools/iter_hist.py)
 constexpr uint32_t RST_GUARD = 8, RST_MAX = SB_RST_MASK;
 
+// stack capacities and restart limits of a traversal: compile-time constants
+// in the production kernels (KNOBS = false), the scene's test overrides
+// (DevScene::capFlat ...) in the KNOBS instantiations
+struct TravLimits { uint32_t capFlat, capGrp, capTop, rstGuard, rstMax; };
+template <bool KNOBS>
+DEV TravLimits trav_limits(const DevScene &S) {
+    if (KNOBS) return TravLimits{S.capFlat, S.capGrp, S.capTop, S.rstGuard, S.rstMax};
+    return TravLimits{(uint32_t)SHORT_STACK, (uint32_t)INNER_STACK, (uint32_t)OUTER_STACK, RST_GUARD, RST_MAX};
+}
+
 // kd-restart after the stack ran empty with entries dropped (Foley &
 // Sugerman's restart, at the exit distance t0 of the leaf just finished).
 // It can only return to t0 when more far children are pushed at split
@@ -510,12 +528,26 @@ constexpr uint32_t RST_GUARD = 8, RST_MAX = SB_RST_MASK;
 // t0 in leaves not yet visited are the only thing that can be skipped), so
 // t0 strictly increases, and the rstMax-th restart ends the ray with SB_ERR
 // (the render then fails with MTSG_ERR_TRAVERSAL) instead of spinning.
-DEV void kd_restart(const DevScene &S, SpecRay &r, uint32_t b, uint2 root, uint2 c) {
+#ifndef MTSG_RST_GUARD
+#define MTSG_RST_GUARD 1   // 0: measurement variant without the guard (round-2 restart)
+#endif
+DEV void kd_restart(const TravLimits &L, SpecRay &r, uint32_t b, uint2 root, uint2 c) {
+#if !MTSG_RST_GUARD
+    {
+        const bool restart = (b & SB_DROPPED) != 0;
+        const float t0 = r.tmax;
+        r.tmin = restart ? t0 : r.tmin;
+        r.tmax = restart ? r.best : r.tmax;
+        r.cur = restart ? root : c;
+        r.bits = (b & ~SB_STACK) | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
+        return;
+    }
+#endif
     const bool restart = (b & SB_DROPPED) != 0;
     const uint32_t nr = (b >> SB_RST_SHIFT) & SB_RST_MASK;
     float t0 = r.tmax;
-    t0 = (restart & (nr >= S.rstGuard)) ? nextafterf(t0, INFINITY) : t0;
-    const bool fail = restart & (nr >= S.rstMax);
+    t0 = (restart & (nr >= L.rstGuard)) ? nextafterf(t0, INFINITY) : t0;
+    const bool fail = restart & (nr >= L.rstMax);
     r.tmin = restart ? t0 : r.tmin;
     r.tmax = restart ? r.best : r.tmax;
     r.cur = restart ? root : c;
@@ -529,6 +561,12 @@ DEV void kd_restart(const DevScene &S, SpecRay &r, uint32_t b, uint2 root, uint2
 static_assert(TRACE_BLOCK == 64, "one wave per traversal workgroup");
 __shared__ uint2 s_specNode[SHORT_STACK * TRACE_BLOCK];
 __shared__ float s_specT[SHORT_STACK * TRACE_BLOCK];
+#ifndef MTSG_LDS_TOP
+#define MTSG_LDS_TOP 0
+#endif
+#if MTSG_LDS_TOP
+__shared__ uint4 s_top[20];
+#endif
 // lane index, recomputed where it is used (volatile: not hoisted out of loops)
 DEV uint32_t lane_here() {
     uint32_t l;
@@ -636,7 +674,7 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 }
 
 template <bool COUNT>
-DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cnt, float4 *hitOut) {
+DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cnt, float4 *hitOut, const TravLimits &L) {
     const uint2 n = r.cur;
     const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
     const bool prim = r.lfE < r.lfEnd;
@@ -651,7 +689,15 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     const uint32_t base = inner ? (n.x >> 3) << ((~n.x >> 1) & 2u) : 0u;
     const uint32_t off = rootKind ? 2u - (uint32_t)goLeft : 0u;
     const uint32_t pi = prim ? r.lfE : 0u;
+#if MTSG_LDS_TOP
+    // measurement variant: the top four levels (blocks 0-4, mtsg.hip layout)
+    // from LDS; a lane's global fetch is skipped when its node is there
+    uint4 p0, pc;
+    if (base < 20u) p0 = s_top[base]; else p0 = S.blocks[base];
+    if (base + off < 20u) pc = s_top[base + off]; else pc = S.blocks[base + off];
+#else
     const uint4 p0 = S.blocks[base], pc = S.blocks[base + off];
+#endif
     const float4 *rec = S.triL + (size_t)(3u * pi);   // < 2^32: checked at upload
     const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
     asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
@@ -673,14 +719,14 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     }
     if (inner) {
         if (COUNT) cnt.nodes++;
-        const uint2 c = spec_take(r, p0, tsplit, goLeft, push, stk, S.capFlat);
+        const uint2 c = spec_take(r, p0, tsplit, goLeft, push, stk, L.capFlat);
         r.cur = c;
         if (rootKind && !(c.x & 0x80000000u)) {
             if (COUNT) cnt.nodes++;
             float ts2;
             bool gl2, push2;
             spec_plan(r, c, ts2, gl2, push2);
-            r.cur = spec_take(r, pc, ts2, gl2, push2, stk, S.capFlat);
+            r.cur = spec_take(r, pc, ts2, gl2, push2, stk, L.capFlat);
         }
     }
     const bool found = (r.bits & SB_FOUND) != 0;
@@ -699,7 +745,7 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
         const uint32_t b = r.bits;
         if (b & SB_N) {
-            const uint32_t top = b & SB_TOP, k = top == 0 ? S.capFlat - 1 : top - 1u;
+            const uint32_t top = b & SB_TOP, k = top == 0 ? L.capFlat - 1 : top - 1u;
             r.cur = stk.node(k);
             const float t = stk.t(k);
             r.bits = ((b & ~SB_TOP) | k) - SB_N1;
@@ -708,7 +754,7 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         } else {
             // empty: done, or a kd-restart behind this leaf if entries were dropped
             if (COUNT && (b & SB_DROPPED)) cnt.restarts++;
-            kd_restart(S, r, b, S.root2, c);
+            kd_restart(L, r, b, S.root2, c);
         }
     }
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
@@ -728,19 +774,12 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
 // never evicts top-level entries.  Hits are written through with the
 // instance they were found in.
 // ---------------------------------------------------------------------------
-constexpr int OUTER_STACK = 2;
 // the top-level state saved while a lane is inside an instance: cur.x, cur.y,
 // tmin, tmax, lfE, lfEnd, lfTmax, bits, instance.  It lives in a per-lane
 // global slot (S.instSave, word k of lane g at k * lanes + g), not in LDS:
 // written on entry, read on exit, and the LDS then holds only the two stacks
 // (6 KB per wave instead of 8.8 KB: 6 waves per SIMD instead of 4)
 constexpr int SAVE_WORDS = 9;
-// the group level's own stack, one entry shorter than the flat traversal's:
-// 5 x 12 B + 2 x 12 B per lane = 5.25 KB per wave, 7 waves/SIMD
-#ifndef MTSG_INNER_STACK
-#define MTSG_INNER_STACK 5
-#endif
-constexpr int INNER_STACK = MTSG_INNER_STACK;
 __shared__ uint2 s_outNode[OUTER_STACK * TRACE_BLOCK];
 __shared__ float s_outT[OUTER_STACK * TRACE_BLOCK];
 __shared__ uint2 s_grpNode[INNER_STACK * TRACE_BLOCK];
@@ -758,13 +797,13 @@ DEV uint2 inst_root(const DevScene &S, uint32_t ii) {
 
 // push the far child onto the stack of the lane's level (circular, drops
 // the oldest entry when full)
-DEV uint2 spec_take_i(const DevScene &S, SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push) {
+DEV uint2 spec_take_i(const TravLimits &L, SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push) {
     const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
     if (push) {
         const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
         const uint32_t b = r.bits, top = b & SB_TOP;
         const bool inner = (b & SB_INST) != 0;
-        const uint32_t cap = inner ? S.capGrp : S.capTop;
+        const uint32_t cap = inner ? L.capGrp : L.capTop;
         const uint32_t i = top * TRACE_BLOCK + lane_here();
         if (inner) { s_grpNode[i] = other; s_grpT[i] = r.tmax; }
         else { s_outNode[i] = other; s_outT[i] = r.tmax; }
@@ -793,7 +832,7 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
 }
 
 template <bool COUNT>
-DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevPaths &P, uint32_t idx) {
+DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevPaths &P, uint32_t idx, const TravLimits &L) {
     const uint2 n = r.cur;
     const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
     const bool prim = r.lfE < r.lfEnd;
@@ -833,14 +872,14 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     }
     if (inner) {
         if (COUNT) cnt.nodes++;
-        const uint2 c = spec_take_i(S, r, p0, tsplit, goLeft, push);
+        const uint2 c = spec_take_i(L, r, p0, tsplit, goLeft, push);
         r.cur = c;
         if (rootKind && !(c.x & 0x80000000u)) {
             if (COUNT) cnt.nodes++;
             float ts2;
             bool gl2, push2;
             spec_plan(r, c, ts2, gl2, push2);
-            r.cur = spec_take_i(S, r, pc, ts2, gl2, push2);
+            r.cur = spec_take_i(L, r, pc, ts2, gl2, push2);
         }
     }
     if (enter) {
@@ -916,7 +955,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         r.lfEnd = nonEmpty ? c.y : r.lfEnd;
         r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
         const uint32_t b = r.bits;
-        const uint32_t cap = inInst ? S.capGrp : S.capTop;
+        const uint32_t cap = inInst ? L.capGrp : L.capTop;
         if (b & SB_N) {
             const uint32_t top = b & SB_TOP, k = top == 0 ? cap - 1 : top - 1u;
             const uint32_t i = k * TRACE_BLOCK + lane_here();
@@ -927,7 +966,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
             r.tmax = fminf(t, r.best);
         } else {
             if (COUNT && (b & SB_DROPPED)) cnt.restarts++;
-            kd_restart(S, r, b, inInst ? inst_root(S, save_word(S, 8)) : S.root2, c);
+            kd_restart(L, r, b, inInst ? inst_root(S, save_word(S, 8)) : S.root2, c);
         }
     }
     const bool done = leave || ((r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f);
@@ -952,10 +991,15 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
 //   cIn: -1 = nIdentity closest rays (bounce 0), 0/1 = count in cnt_q(cIn), -2 = none
 //   sIn: 0/1 = count in CNT_S0/CNT_S1, -1 = none
 
-template <bool COUNT, int MIN_IDLE, bool INST = false>
+template <bool COUNT, int MIN_IDLE, bool INST = false, bool KNOBS = false>
 __global__ void __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(INST ? (COUNT ? 1 : MTSG_INST_WAVES) : MTSG_SPEC_WAVES)))
 k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
     const SpecStack stk{};
+    const TravLimits L = trav_limits<KNOBS>(S);
+#if MTSG_LDS_TOP
+    if (threadIdx.x < 20u) s_top[threadIdx.x] = S.blocks[threadIdx.x];
+    __syncthreads();
+#endif
     const unsigned long long tStart = wt ? wall_clock64() : 0ull;
     const uint32_t nC = cIn == -1 ? nIdentity : (cIn >= 0 ? __atomic_load_n(&P.cnt[cnt_q(cIn)], __ATOMIC_RELAXED) : 0u);
     const uint32_t nS = sIn >= 0 ? __atomic_load_n(&P.cnt[cnt_s(sIn)], __ATOMIC_RELAXED) : 0u;
@@ -1025,11 +1069,11 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
         if (active) {
             if (INST) {
                 const bool sh = (r.bits & SB_SHADOW) != 0;
-                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P, idx);
-                else done = spec_iter_i<COUNT>(S, r, cc, P, idx);
+                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P, idx, L);
+                else done = spec_iter_i<COUNT>(S, r, cc, P, idx, L);
             } else {
-                if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx);
-                else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx);
+                if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx, L);
+                else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx, L);
             }
         }
         if (COUNT && active) ++iters;
@@ -2595,8 +2639,8 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
         if (state == FS_TRACE) {
             // two-level scenes: the per-lane level switch of k_trace_s<.., true>
             // (its save slots are sized for this grid too)
-            if (S.inst) done = spec_iter_i<false>(S, r, tc, P, idx);
-            else done = spec_iter<false>(S, r, stk, tc, P.hit + idx);
+            if (S.inst) done = spec_iter_i<false>(S, r, tc, P, idx, trav_limits<false>(S));
+            else done = spec_iter<false>(S, r, stk, tc, P.hit + idx, trav_limits<false>(S));
         }
         if (done) {
             if (r.bits & SB_ERR) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 #include <chrono>
 #include <functional>
@@ -92,6 +93,7 @@ struct mtsg_scene {
     int traceMode = 0;            // 0: refill at 16 idle lanes (measured best), 1: at 32
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
+    bool knobs = false;   // traversal test overrides set (MTSG_STACK_CAP, MTSG_RESTART_*): KNOBS kernels, no tail mode
     mtsg_stats stats{};
     std::vector<hipEvent_t> evPool;
     size_t evUsed = 0;
@@ -190,7 +192,12 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t
     unsigned long long *wt = nullptr;
     if ((s->flags & MTSG_FLAG_WAVETIME) && s->waveTimes && s->wtLaunches < WT_MAX_LAUNCHES && !s->ds.inst)
         wt = s->waveTimes + (size_t)WT_WORDS * s->traceGrid * s->wtLaunches++;
-    if (s->ds.inst) hipLaunchKernelGGL((k_trace_s<COUNT, 16, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    // the KNOBS instantiations read the stack caps and restart limits the
+    // scene was created with (test overrides); the COUNT pass ignores them
+    if (s->ds.inst && s->knobs && !COUNT)
+        hipLaunchKernelGGL((k_trace_s<false, 16, true, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    else if (s->ds.inst) hipLaunchKernelGGL((k_trace_s<COUNT, 16, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    else if (s->knobs && !COUNT) hipLaunchKernelGGL((k_trace_s<false, 16, false, true>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
 }
@@ -434,7 +441,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     // emitters its last BSDF rays found
     const int maxBounces = I.om ? p->max_depth + 1 : (p->max_depth > 0 ? p->max_depth : 1 << 30);
     // tail mode (k_finish): one lane, not in the instrumented or myPath2_OM modes
-    const bool useFinish = s->finishPaths > 0 && nl == 1 && !count && !I.om;
+    const bool useFinish = s->finishPaths > 0 && nl == 1 && !count && !I.om && !s->knobs;
     // bounce b of a lane: one trace launch over this bounce's closest rays
     // (work list qin(b), identity for b = 0) and bounce b-1's shadow rays
     // (S((b-1) & 1)), then k_shade appends the next bounce's paths to
@@ -789,13 +796,37 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     // ---- two-level blocks from the binary pair layout
     std::vector<uint4> blocks;
     blocks.reserve(pairs.size() * 2 + 8);
+    // the scene root's block and the blocks of its (up to four) grandchildren
+    // come first, blocks 0-4: the top four levels of the tree in 320 B (the
+    // MTSG_LDS_TOP variant stages them in LDS)
+    std::unordered_map<uint32_t, uint32_t> preBlock;
+    auto reserveBlock = [&](uint32_t pair) {
+        preBlock[pair] = (uint32_t)(blocks.size() / 4);
+        blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));
+    };
+    if (!(root.x & 0x80000000u)) {
+        reserveBlock(root.x >> 2);
+        const uint4 pr = pairs[root.x >> 2];
+        for (const uint2 c : {make_uint2(pr.x, pr.y), make_uint2(pr.z, pr.w)}) {
+            if (c.x & 0x80000000u) continue;
+            const uint4 gp = pairs[c.x >> 2];
+            for (const uint2 g : {make_uint2(gp.x, gp.y), make_uint2(gp.z, gp.w)})
+                if (!(g.x & 0x80000000u)) reserveBlock(g.x >> 2);
+        }
+    }
     std::function<uint2(uint2, bool, uint32_t)> conv2 = [&](uint2 w, bool root, uint32_t slot) -> uint2 {
         if (w.x & 0x80000000u) return w;                       // leaf: unchanged
         const uint4 pr = pairs[w.x >> 2];
         const uint2 L = make_uint2(pr.x, pr.y), R = make_uint2(pr.z, pr.w);
         if (root) {
-            const uint32_t b = (uint32_t)(blocks.size() / 4);
-            blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));
+            uint32_t b;
+            const auto pre = preBlock.find(w.x >> 2);
+            if (pre != preBlock.end()) {
+                b = pre->second;
+            } else {
+                b = (uint32_t)(blocks.size() / 4);
+                blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));
+            }
             const uint2 nL = conv2(L, false, 4 * b + 1);
             const uint2 nR = conv2(R, false, 4 * b + 2);
             blocks[4 * b] = make_uint4(nL.x, nL.y, nR.x, nR.y);
@@ -809,6 +840,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     const uint2 root2 = conv2(root, true, 0);
     for (auto &gr : groupRoots) gr = conv2(gr, true, 0);
     blocks.resize(blocks.size() + 4, make_uint4(0, 0, 0, 0));   // slack for the 3-slot fetch of the last slot
+    if (blocks.size() < 20) blocks.resize(20, make_uint4(0, 0, 0, 0));   // blocks 0-4 are always readable
     if (blocks.size() >= (1u << 29)) { g_err = "kd-tree too large for the two-level layout"; return fail(MTSG_ERR_INVALID); }
     if (triL.empty()) triL.resize(3, make_float4(0, 0, 0, 0));
     uint4 *dblocks; float4 *dtriL; float4 *dvpos, *dvnrm, *dshrec; uint4 *dtidx;
@@ -866,6 +898,8 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     }
     if (const char *g = getenv("MTSG_RESTART_GUARD")) ds.rstGuard = (uint32_t)std::max(0, atoi(g));
     if (const char *g = getenv("MTSG_RESTART_LIMIT")) ds.rstMax = std::min<uint32_t>(RST_MAX, (uint32_t)std::max(0, atoi(g)));
+    s->knobs = ds.capFlat != (uint32_t)SHORT_STACK || ds.capGrp != (uint32_t)INNER_STACK || ds.capTop != (uint32_t)OUTER_STACK ||
+               ds.rstGuard != RST_GUARD || ds.rstMax != RST_MAX;
     // environment emitter tables (envmap.h)
     ds.has_env = d->has_envmap ? 1 : 0;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {

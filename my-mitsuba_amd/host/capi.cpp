@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/mtsh.h"
 #include "scene.h"
@@ -100,6 +101,30 @@ int mtsh_scene_set_kdtree(mtsh_scene *s, const mtsg_kdnode *nodes, uint32_t n_no
     const uint32_t nPrims = s->scene->desc.n_prims;
     for (uint32_t i = 0; i < n_indices; ++i)
         if (indices[i] >= nPrims) { g_err = "mtsh_scene_set_kdtree: index out of range"; return -1; }
+    // the node structure (KDNode, gkdtree.h:452-600): every node reached once
+    // from the root, inner children inside the array and after their parent,
+    // no indirection nodes, leaf ranges inside the index list, depth within
+    // max_depth -- the device traversal trusts all of it
+    std::vector<uint8_t> seen(n_nodes, 0);
+    std::vector<std::pair<uint32_t, uint32_t>> stack{{0u, 0u}};
+    while (!stack.empty()) {
+        const auto [i, depth] = stack.back();
+        stack.pop_back();
+        if (seen[i]) { g_err = "mtsh_scene_set_kdtree: node " + std::to_string(i) + " reached twice"; return -1; }
+        seen[i] = 1;
+        const uint32_t c = nodes[i].combined;
+        if (c & 0x80000000u) {
+            const uint32_t st = c & 0x7FFFFFFFu, en = nodes[i].data;
+            if (st > en || en > n_indices) { g_err = "mtsh_scene_set_kdtree: leaf " + std::to_string(i) + " range outside the index list"; return -1; }
+            continue;
+        }
+        if ((c & 3u) == 3u || (c & 0x40000000u)) { g_err = "mtsh_scene_set_kdtree: node " + std::to_string(i) + " is not an inner node of this encoding"; return -1; }
+        const uint64_t left = (uint64_t)i + (c >> 2);
+        if (left <= i || left + 1 >= n_nodes) { g_err = "mtsh_scene_set_kdtree: node " + std::to_string(i) + " has children outside the array"; return -1; }
+        if (depth + 1 > max_depth) { g_err = "mtsh_scene_set_kdtree: deeper than max_depth"; return -1; }
+        stack.push_back({(uint32_t)left, depth + 1});
+        stack.push_back({(uint32_t)left + 1, depth + 1});
+    }
     s->scene->setTree(nodes, n_nodes, indices, n_indices, aabb_min, aabb_max, max_depth);
     return 0;
 }

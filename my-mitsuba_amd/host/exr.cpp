@@ -345,10 +345,13 @@ bool readEXR(const std::string &path, int &w, int &h, std::vector<float> &rgb, s
                 ch.push_back(c);
             }
         } else if (name == "compression") {
+            if (size < 1) { err = "OpenEXR: bad compression attribute"; return false; }
             compression = v[0];
         } else if (name == "dataWindow") {
+            if (size < 16) { err = "OpenEXR: bad dataWindow attribute"; return false; }
             xmin = (int)rdU32(v); ymin = (int)rdU32(v + 4); xmax = (int)rdU32(v + 8); ymax = (int)rdU32(v + 12);
         } else if (name == "lineOrder") {
+            if (size < 1) { err = "OpenEXR: bad lineOrder attribute"; return false; }
             lineOrder = v[0];
         }
         p += size;
@@ -357,8 +360,14 @@ bool readEXR(const std::string &path, int &w, int &h, std::vector<float> &rgb, s
     for (auto &c : ch)
         if (c.xs != 1 || c.ys != 1 || (c.type != 1 && c.type != 2)) { err = "OpenEXR: only full-resolution HALF/FLOAT channels are supported"; return false; }
     (void)lineOrder;   // chunks carry their own y
-    w = xmax - xmin + 1;
-    h = ymax - ymin + 1;
+    // the window in 64 bits: a hostile one must not overflow w, h or w * h * 3
+    const int64_t w64 = (int64_t)xmax - xmin + 1, h64 = (int64_t)ymax - ymin + 1;
+    if (w64 > (1 << 20) || h64 > (1 << 20) || w64 * h64 > (int64_t)1 << 30) {
+        err = "OpenEXR: data window of " + std::to_string(w64) + " x " + std::to_string(h64) + " pixels is too large";
+        return false;
+    }
+    w = (int)w64;
+    h = (int)h64;
     int linesPerChunk;
     switch (compression) {
         case 0: case 1: case 2: linesPerChunk = 1; break;

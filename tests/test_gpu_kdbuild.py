@@ -66,8 +66,12 @@ def test_structure_and_brute_force_hits(name, defs):
     np.testing.assert_array_equal(hit1, hit0)
     both = hit0 & hit1
     same = both & (p0 == p1)
-    assert same.sum() >= 0.999 * both.sum()
     np.testing.assert_array_equal(t1[same], t0[same])
+    # another primitive only on ties: coplanar triangles sharing the hit point
+    # (brute force reports the lowest index, Havran the first in leaf order)
+    diff = both & (p0 != p1)
+    np.testing.assert_allclose(t1[diff], t0[diff], rtol=1e-6)
+    assert same.sum() >= 0.995 * both.sum()
 
 
 @pytest.fixture(scope="module")

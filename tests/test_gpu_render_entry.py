@@ -194,8 +194,8 @@ def test_plugin_flow_with_overriding_defines():
     spp/maxDepth; the plugin passes the values it holds in memory to
     mtsh_scene_load_overrides in preprocess(), creates the job once, and
     render() goes through mtsh_path_job_render.  The block has the overridden
-    size, every pixel got the overridden sample count, and the image equals
-    the one of the scene loaded with the same -D map."""
+    size and the image equals the one of the scene loaded with the same -D
+    map (up to the order of the film's float additions)."""
     from test_plugin_overrides import overrides_for
     xml = os.path.join(SCENES, "bunny15.xml")
     by_defines = mtsg.Scene(xml, {"width": 96, "height": 40, "spp": 3, "maxDepth": 5})
@@ -212,4 +212,5 @@ def test_plugin_flow_with_overriding_defines():
     rc, ref, _ = ref_job.render(by_defines.params(), by_defines.border)
     ref_job.close()
     assert rc == 0
-    np.testing.assert_array_equal(img, ref)
+    # the same samples; the film's float atomics add them in any order
+    np.testing.assert_allclose(img, ref, rtol=1e-5, atol=1e-6)

@@ -42,3 +42,24 @@ def test_set_kdtree_rejects_bad_indices():
                aabb_min=np.zeros(3, np.float32), aabb_max=np.ones(3, np.float32), max_depth=0)
     with pytest.raises(RuntimeError, match="out of range"):
         s.set_kdtree(bad)
+
+
+@pytest.mark.parametrize("nodes,n_idx,max_depth,msg", [
+    ([[0x80000000, 2]], 1, 0, "range outside"),                          # leaf end past the index list
+    ([[0x80000002, 1]], 1, 0, "range outside"),                          # leaf start > end
+    ([[0 | (5 << 2), 0], [0x80000000, 0], [0x80000000, 0]], 0, 1, "children outside"),   # left child past the end
+    ([[1 | (0 << 2), 0]], 0, 1, "children outside"),                     # left == self (cycle)
+    ([[3 | (1 << 2), 0], [0x80000000, 0], [0x80000000, 0]], 0, 1, "not an inner node"),   # axis 3
+    ([[0x40000000 | (1 << 2), 0], [0x80000000, 0], [0x80000000, 0]], 0, 1, "not an inner node"),   # indirection
+    ([[0 | (1 << 2), 0], [0x80000000, 0], [0x80000000, 0]], 0, 0, "max_depth"),
+    # two inner nodes sharing one child pair: node 3 reached twice
+    ([[0 | (1 << 2), 0], [0 | (2 << 2), 0], [0 | (1 << 2), 0], [0x80000000, 0], [0x80000000, 0]], 0, 3, "twice"),
+])
+def test_set_kdtree_rejects_malformed_nodes(nodes, n_idx, max_depth, msg):
+    """mtsh_scene_set_kdtree walks the node structure before the tree can
+    reach the device traversal (it used to check indices only)."""
+    s = mtsg.Scene(os.path.join(SCENES, "cbox.xml"), {"width": 16, "height": 16, "spp": 1})
+    bad = dict(nodes=np.array(nodes, np.uint32), indices=np.zeros(n_idx, np.uint32),
+               aabb_min=np.zeros(3, np.float32), aabb_max=np.ones(3, np.float32), max_depth=max_depth)
+    with pytest.raises(RuntimeError, match=msg):
+        s.set_kdtree(bad)

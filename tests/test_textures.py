@@ -337,3 +337,39 @@ def test_textured_cbox_loads_and_renders():
     img, _ = O.render(sc.desc, sc.params(), sc.border, rng=O.RNG_COUNTER)
     rgb = mtsg.develop(img)
     assert np.isfinite(rgb).all() and rgb.mean() > 0.01
+
+
+def test_png_decoder_agrees_with_pil(tmp_path):
+    """An independent decoder: PIL (libpng-compatible, importable here) reads
+    the committed PNG fixtures and PNGs that PIL itself encodes (with its own
+    filter choices and zlib streams) -- the host reader must give the same
+    8/16-bit values (raw, gamma 1) as PIL for every one of them."""
+    from PIL import Image
+    inv255 = np.float32(1.0) / np.float32(255.0)
+    files = [os.path.join(SCENES, f) for f in ("tex_checker.png", "tex_rgba.png", "tex_palette.png", "tex_gray16.png")]
+    rng = np.random.default_rng(9)
+    for mode, arr in (("RGB", rng.integers(0, 256, (29, 41, 3), dtype=np.uint8)),
+                      ("RGBA", rng.integers(0, 256, (17, 23, 4), dtype=np.uint8)),
+                      ("L", rng.integers(0, 256, (31, 19), dtype=np.uint8))):
+        p = tmp_path / f"pil_{mode}.png"
+        Image.fromarray(arr, mode).save(p, optimize=True)
+        files.append(str(p))
+    p = tmp_path / "pil_P.png"
+    Image.fromarray(rng.integers(0, 256, (21, 27, 3), dtype=np.uint8), "RGB").convert("P", palette=Image.ADAPTIVE,
+                                                                                     colors=16).save(p, bits=4)
+    files.append(str(p))
+    p = tmp_path / "pil_I16.png"
+    Image.fromarray(rng.integers(0, 65536, (13, 11), dtype=np.uint16)).save(p)
+    files.append(str(p))
+    for f in files:
+        im = Image.open(f)
+        got = mtsg.texture_image(f, 1.0)
+        if im.mode in ("I;16", "I;16B", "I"):
+            g = np.asarray(im).astype(np.float32) * (np.float32(1.0) / np.float32(65535.0))
+            want = np.repeat(g[..., None], 3, -1)
+        else:
+            a = np.asarray(im.convert("RGBA" if "A" in im.mode or im.mode == "P" else "RGB"))[..., :3]
+            if im.mode == "L":
+                a = np.repeat(np.asarray(im)[..., None], 3, -1)
+            want = a.astype(np.float32) * inv255
+        np.testing.assert_array_equal(got, want, err_msg=f)

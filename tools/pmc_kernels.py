@@ -23,13 +23,32 @@ import sys
 from collections import defaultdict
 
 
+def kernel_name(full):
+    """rocprofv3's demangled name without return type, namespace and
+    arguments: 'void (anonymous namespace)::k_trace_s<false, 16, false>(mtsg::DevScene, ...)'
+    -> 'k_trace_s<false, 16, false>'."""
+    n = full.strip()
+    if n.startswith("void "):
+        n = n[5:]
+    n = n.replace("(anonymous namespace)::", "")
+    depth = 0
+    for i, ch in enumerate(n):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            return n[:i]
+    return n
+
+
 def per_kernel(path, counters):
     out = defaultdict(lambda: defaultdict(list))
     if not os.path.exists(path):
         return out
     for row in csv.DictReader(open(path)):
         if row["Counter_Name"] in counters:
-            out[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            out[kernel_name(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return out
 
 
@@ -42,8 +61,8 @@ def main():
     p = os.path.join(d, "stats_kernel_stats.csv")
     if os.path.exists(p):
         for row in csv.DictReader(open(p)):
-            stats[row["Name"]] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
-                                  "total_ns": float(row["TotalDurationNs"])}
+            stats[kernel_name(row["Name"])] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
+                                               "total_ns": float(row["TotalDurationNs"])}
     kernels = {}
     for name in sorted(set(fetch) | set(write) | set(tcc)):
         f = fetch[name].get("FETCH_SIZE", [])
