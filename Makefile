@@ -81,10 +81,12 @@ scenes/sky512.pfm: tools/gen_envmap.py
 clean:
 	rm -f $(HOST_LIB) $(DEV_LIB) $(PATH_LIB) $(CLI) $(ORACLE) $(ORACLE_FAST)
 
-# Measurement variants of the device library (build/var/, loaded with MTSG_LIB=...)
+# Measurement variants of the device library (my-mitsuba_amd/var/, loaded with
+# MTSG_LIB=...; objects in build/var/, which gpurun does not ship)
 VARIANTS := fm16:-DMTSG_FETCH_MIN=16 fm64:-DMTSG_FETCH_MIN=64 gs1:-DMTSG_GUIDE_SPLIT=1 gs4:-DMTSG_GUIDE_SPLIT=4 noguide:-DMTSG_FETCH_MIN=256 wt:-DMTSG_WT_DRAIN=1 ss5:-DMTSG_SHORT_STACK=5 ldstop:-DMTSG_LDS_TOP=1 noguard:-DMTSG_RST_GUARD=0
-VAR_LIBS := $(foreach v,$(VARIANTS),build/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
+VAR_LIBS := $(foreach v,$(VARIANTS),$(PKG)/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
 .PHONY: variants
 variants: $(VAR_LIBS)
-build/var/libmtsg_%.so: $(DEV_SRC) $(DEV_HDR)
+$(PKG)/var/libmtsg_%.so: $(DEV_SRC) $(DEV_HDR)
+	@mkdir -p $(PKG)/var
 	$(MAKE) DEV_OBJ=build/var/$* DEV_LIB=$@ DEV_EXTRA="$(subst @, ,$(word 2,$(subst :, ,$(filter $*:%,$(VARIANTS)))))" $@

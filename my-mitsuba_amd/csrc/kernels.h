@@ -546,7 +546,10 @@ DEV void kd_restart(const TravLimits &L, SpecRay &r, uint32_t b, uint2 root, uin
     const bool restart = (b & SB_DROPPED) != 0;
     const uint32_t nr = (b >> SB_RST_SHIFT) & SB_RST_MASK;
     float t0 = r.tmax;
-    t0 = (restart & (nr >= L.rstGuard)) ? nextafterf(t0, INFINITY) : t0;
+    // nextafterf(t0, +inf) for finite t0, in integer arithmetic
+    const uint32_t u = __float_as_uint(t0);
+    const float up = __uint_as_float(t0 >= 0.0f ? (u & 0x7FFFFFFFu) + 1u : u - 1u);
+    t0 = (restart & (nr >= L.rstGuard)) ? up : t0;
     const bool fail = restart & (nr >= L.rstMax);
     r.tmin = restart ? t0 : r.tmin;
     r.tmax = restart ? r.best : r.tmax;
@@ -567,6 +570,13 @@ __shared__ float s_specT[SHORT_STACK * TRACE_BLOCK];
 #if MTSG_LDS_TOP
 __shared__ uint4 s_top[20];
 #endif
+// every kernel that runs spec_iter stages the top blocks first (variant only)
+DEV void lds_top_init(const DevScene &S) {
+#if MTSG_LDS_TOP
+    if (threadIdx.x < 20u) s_top[threadIdx.x] = S.blocks[threadIdx.x];
+    __syncthreads();
+#endif
+}
 // lane index, recomputed where it is used (volatile: not hoisted out of loops)
 DEV uint32_t lane_here() {
     uint32_t l;
@@ -996,10 +1006,7 @@ __global__ void __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_e
 k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
     const SpecStack stk{};
     const TravLimits L = trav_limits<KNOBS>(S);
-#if MTSG_LDS_TOP
-    if (threadIdx.x < 20u) s_top[threadIdx.x] = S.blocks[threadIdx.x];
-    __syncthreads();
-#endif
+    lds_top_init(S);
     const unsigned long long tStart = wt ? wall_clock64() : 0ull;
     const uint32_t nC = cIn == -1 ? nIdentity : (cIn >= 0 ? __atomic_load_n(&P.cnt[cnt_q(cIn)], __ATOMIC_RELAXED) : 0u);
     const uint32_t nS = sIn >= 0 ? __atomic_load_n(&P.cnt[cnt_s(sIn)], __ATOMIC_RELAXED) : 0u;
@@ -2567,6 +2574,7 @@ constexpr uint32_t FINISH_FETCH = 64;   // paths per wave draw (small pools: the
 template <bool ENV, int SMP, bool EXT>
 __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int qin, int hasAlpha, uint32_t shadeMin) {
     const SpecStack stk{};
+    lds_top_init(S);
     const uint32_t n = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     Fetch F{&P.cnt[CNT_FETCH], n, blockIdx.x % XGROUPS, 0, max(1u, gridDim.x / XGROUPS * GUIDE_SPLIT), FINISH_FETCH};
     TraceCounts tc{0, 0, 0, 0, 0, 0, 0, 0, 0};

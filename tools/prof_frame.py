@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Render one frame of a benchmark scene on cuda:0 (for rocprofv3 runs).
-usage: python tools/prof_frame.py [bunny15|cbox] [spp] [frames] [tile_stride]"""
+usage: python tools/prof_frame.py [bunny15|cbox] [spp] [frames] [tile_stride] [flatten|two-level]"""
 import os
 import sys
 import time
@@ -12,7 +12,9 @@ import mtsg  # noqa: E402
 name = sys.argv[1] if len(sys.argv) > 1 else "bunny15"
 spp = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 frames = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-scene = mtsg.Scene(os.path.join(REPO, "scenes", name + ".xml"), {"width": 1280, "height": 720, "spp": spp, "maxDepth": 8})
+inst = sys.argv[5] if len(sys.argv) > 5 else "flatten"
+scene = mtsg.Scene(os.path.join(REPO, "scenes", name + ".xml"), {"width": 1280, "height": 720, "spp": spp, "maxDepth": 8},
+                   instancing=inst)
 p = scene.params()
 stride = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 p.tile_stride = stride
