@@ -65,8 +65,8 @@ struct DevScene {
     const float4 *__restrict__ ttex;
     int cam_diffs;        // bounce 0 carries the camera's ray differentials in T / aux
     // two-level traversal: per-lane save slots of the top-level state
-    // (SAVE_WORDS words per lane of the traversal grid); nullptr: no instances
-    uint32_t *__restrict__ instSave;
+    // (SAVE_VECS uint4 per lane of the traversal grid); nullptr: no instances
+    uint4 *__restrict__ instSave;
     // myPath2_OM occupancy maps (om.cpp; nullptr unless that integrator)
     const mtsg_om *__restrict__ om;
     const uint32_t *__restrict__ om_bits;
@@ -544,18 +544,22 @@ DEV void kd_restart(const TravLimits &L, SpecRay &r, uint32_t b, uint2 root, uin
     }
 #endif
     const bool restart = (b & SB_DROPPED) != 0;
-    const uint32_t nr = (b >> SB_RST_SHIFT) & SB_RST_MASK;
     float t0 = r.tmax;
-    // nextafterf(t0, +inf) for finite t0, in integer arithmetic
-    const uint32_t u = __float_as_uint(t0);
-    const float up = __uint_as_float(t0 >= 0.0f ? (u & 0x7FFFFFFFu) + 1u : u - 1u);
-    t0 = (restart & (nr >= L.rstGuard)) ? up : t0;
-    const bool fail = restart & (nr >= L.rstMax);
+    uint32_t nb = b & ~SB_STACK;
+    if (restart) {   // lanes that restart (the others finish their ray here)
+        const uint32_t nr = (b >> SB_RST_SHIFT) & SB_RST_MASK;
+        nb += SB_RST1;
+        if (nr >= L.rstGuard) {
+            // nextafterf(t0, +inf) for finite t0, in integer arithmetic
+            const uint32_t u = __float_as_uint(t0);
+            t0 = __uint_as_float(t0 >= 0.0f ? (u & 0x7FFFFFFFu) + 1u : u - 1u);
+            if (nr >= L.rstMax) nb |= SB_ERR | SB_TRAVDONE;
+        }
+    }
     r.tmin = restart ? t0 : r.tmin;
     r.tmax = restart ? r.best : r.tmax;
     r.cur = restart ? root : c;
-    r.bits = ((b & ~SB_STACK) + (restart ? SB_RST1 : 0u)) |
-             ((!restart | fail | !(t0 < r.best)) ? SB_TRAVDONE : 0u) | (fail ? SB_ERR : 0u);
+    r.bits = nb | ((!restart | !(t0 < r.best)) ? SB_TRAVDONE : 0u);
 }
 
 // short stack of the compact traversal: entry k of lane i at [k * TRACE_BLOCK
@@ -784,19 +788,20 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
 // never evicts top-level entries.  Hits are written through with the
 // instance they were found in.
 // ---------------------------------------------------------------------------
-// the top-level state saved while a lane is inside an instance: cur.x, cur.y,
-// tmin, tmax, lfE, lfEnd, lfTmax, bits, instance.  It lives in a per-lane
-// global slot (S.instSave, word k of lane g at k * lanes + g), not in LDS:
-// written on entry, read on exit, and the LDS then holds only the two stacks
-// (6 KB per wave instead of 8.8 KB: 6 waves per SIMD instead of 4)
-constexpr int SAVE_WORDS = 9;
-__shared__ uint2 s_outNode[OUTER_STACK * TRACE_BLOCK];
-__shared__ float s_outT[OUTER_STACK * TRACE_BLOCK];
-__shared__ uint2 s_grpNode[INNER_STACK * TRACE_BLOCK];
-__shared__ float s_grpT[INNER_STACK * TRACE_BLOCK];
+// the top-level state saved while a lane is inside an instance, two uint4 per
+// lane: {cur.x, cur.y, tmin, tmax}, {lfE, lfEnd, lfTmax, bits}.  It lives in
+// per-lane global slots (S.instSave, vector k of lane g at k * lanes + g: one
+// coalesced 16-B access per vector), not in LDS, which holds only the stacks
+// (5.25 KB per wave: 7 waves per SIMD; 2.3 KB more would allow 5).  The
+// instance a lane is inside stays in a register (k_trace_s / k_finish `inst`).
+constexpr int SAVE_VECS = 2;
+// the two levels' stacks in one LDS array: top level in entries
+// [0, OUTER_STACK), group level in [OUTER_STACK, OUTER_STACK + INNER_STACK)
+__shared__ uint2 s_lvNode[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
+__shared__ float s_lvT[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
 enum : uint32_t { SB_INST = 1u << 22 };
 
-DEV uint32_t &save_word(const DevScene &S, uint32_t k) {
+DEV uint4 &save_vec(const DevScene &S, uint32_t k) {
     return S.instSave[(size_t)k * (gridDim.x * TRACE_BLOCK) + blockIdx.x * TRACE_BLOCK + lane_here()];
 }
 // the group tree's root words of instance ii (its 8-float4 record, words 6.w / 7.w)
@@ -814,9 +819,9 @@ DEV uint2 spec_take_i(const TravLimits &L, SpecRay &r, const uint4 &pr, float ts
         const uint32_t b = r.bits, top = b & SB_TOP;
         const bool inner = (b & SB_INST) != 0;
         const uint32_t cap = inner ? L.capGrp : L.capTop;
-        const uint32_t i = top * TRACE_BLOCK + lane_here();
-        if (inner) { s_grpNode[i] = other; s_grpT[i] = r.tmax; }
-        else { s_outNode[i] = other; s_outT[i] = r.tmax; }
+        const uint32_t i = (top + (inner ? (uint32_t)OUTER_STACK : 0u)) * TRACE_BLOCK + lane_here();
+        s_lvNode[i] = other;
+        s_lvT[i] = r.tmax;
         const bool full = (b & SB_N) == cap * SB_N1;
         r.bits = ((b & ~SB_TOP) | (top == cap - 1 ? 0u : top + 1u)) + (full ? SB_DROPPED - (b & SB_DROPPED) : SB_N1);
         r.tmax = tsplit;
@@ -828,13 +833,14 @@ DEV uint2 spec_take_i(const TravLimits &L, SpecRay &r, const uint4 &pr, float ts
 // keep the hit flag, reload the world-space ray
 DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4 *wd) {
     const uint32_t found = r.bits & (SB_FOUND | SB_ERR);
-    r.cur = make_uint2(save_word(S, 0), save_word(S, 1));
-    r.tmin = __uint_as_float(save_word(S, 2));
-    r.tmax = __uint_as_float(save_word(S, 3));
-    r.lfE = save_word(S, 4);
-    r.lfEnd = save_word(S, 5);
-    r.lfTmax = __uint_as_float(save_word(S, 6));
-    r.bits = save_word(S, 7) | found;
+    const uint4 a = save_vec(S, 0), b = save_vec(S, 1);
+    r.cur = make_uint2(a.x, a.y);
+    r.tmin = __uint_as_float(a.z);
+    r.tmax = __uint_as_float(a.w);
+    r.lfE = b.x;
+    r.lfEnd = b.y;
+    r.lfTmax = __uint_as_float(b.z);
+    r.bits = b.w | found;
     float4 ro = ldS(wo), rd = ldS(wd);
     r.o = xyz(ro);
     r.d = xyz(rd);
@@ -842,7 +848,8 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
 }
 
 template <bool COUNT>
-DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevPaths &P, uint32_t idx, const TravLimits &L) {
+DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevPaths &P, uint32_t idx, const TravLimits &L,
+                     uint32_t &inst) {
     const uint2 n = r.cur;
     const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
     const bool prim = r.lfE < r.lfEnd;
@@ -875,7 +882,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
                 if (r.bits & SB_SHADOW) return true;   // any hit occludes
                 r.best = t;
                 stS(P.hit + idx, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
-                P.hitInst[idx] = (r.bits & SB_INST) ? save_word(S, 8) : 0xFFFFFFFFu;
+                P.hitInst[idx] = (r.bits & SB_INST) ? inst : 0xFFFFFFFFu;
             }
         }
         ++r.lfE;
@@ -921,15 +928,9 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         }
         const float t0 = fmaxf(r.mint, nearT), t1 = fminf(r.best, farT);
         if (ok & (nearT <= farT) & (t1 > t0)) {
-            save_word(S, 0) = r.cur.x;
-            save_word(S, 1) = r.cur.y;
-            save_word(S, 2) = __float_as_uint(r.tmin);
-            save_word(S, 3) = __float_as_uint(r.tmax);
-            save_word(S, 4) = r.lfE;
-            save_word(S, 5) = r.lfEnd;
-            save_word(S, 6) = __float_as_uint(r.lfTmax);
-            save_word(S, 7) = r.bits & ~SB_FOUND;
-            save_word(S, 8) = ii;
+            save_vec(S, 0) = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
+            save_vec(S, 1) = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
+            inst = ii;
             const uint2 root = make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w));
             r.o = lo;
             r.d = ld;
@@ -968,15 +969,15 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         const uint32_t cap = inInst ? L.capGrp : L.capTop;
         if (b & SB_N) {
             const uint32_t top = b & SB_TOP, k = top == 0 ? cap - 1 : top - 1u;
-            const uint32_t i = k * TRACE_BLOCK + lane_here();
-            r.cur = inInst ? s_grpNode[i] : s_outNode[i];
-            const float t = inInst ? s_grpT[i] : s_outT[i];
+            const uint32_t i = (k + (inInst ? (uint32_t)OUTER_STACK : 0u)) * TRACE_BLOCK + lane_here();
+            r.cur = s_lvNode[i];
+            const float t = s_lvT[i];
             r.bits = ((b & ~SB_TOP) | k) - SB_N1;
             r.tmin = r.tmax;
             r.tmax = fminf(t, r.best);
         } else {
             if (COUNT && (b & SB_DROPPED)) cnt.restarts++;
-            kd_restart(L, r, b, inInst ? inst_root(S, save_word(S, 8)) : S.root2, c);
+            kd_restart(L, r, b, inInst ? inst_root(S, inst) : S.root2, c);
         }
     }
     const bool done = leave || ((r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f);
@@ -1016,6 +1017,7 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
     bool exhausted = false;
     bool active = false;
     uint32_t idx = 0;                      // index into the ray's own list
+    uint32_t inst = 0;                     // INST: the instance the lane is inside
     uint32_t iters = 0;                    // COUNT: iterations of this ray
     uint32_t n0 = 0, t0c = 0, r0 = 0;      // COUNT: the lane's node / test / restart totals at its start
     unsigned long long tExh = 0;           // wt: when the work list was found empty
@@ -1076,8 +1078,8 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
         if (active) {
             if (INST) {
                 const bool sh = (r.bits & SB_SHADOW) != 0;
-                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P, idx, L);
-                else done = spec_iter_i<COUNT>(S, r, cc, P, idx, L);
+                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P, idx, L, inst);
+                else done = spec_iter_i<COUNT>(S, r, cc, P, idx, L, inst);
             } else {
                 if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx, L);
                 else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx, L);
@@ -2583,6 +2585,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
     uint32_t state = FS_IDLE;
     bool pendingCont = false;   // tracing the NEE shadow ray of a path that continues
     uint32_t idx = 0;
+    uint32_t inst = 0;          // two-level: the instance the lane is inside
     SpecRay r;
     // the continuation ray of path idx (written by shade_path); a ray that
     // misses the scene bounds gets its miss record and is shaded next
@@ -2647,7 +2650,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
         if (state == FS_TRACE) {
             // two-level scenes: the per-lane level switch of k_trace_s<.., true>
             // (its save slots are sized for this grid too)
-            if (S.inst) done = spec_iter_i<false>(S, r, tc, P, idx, trav_limits<false>(S));
+            if (S.inst) done = spec_iter_i<false>(S, r, tc, P, idx, trav_limits<false>(S), inst);
             else done = spec_iter<false>(S, r, stk, tc, P.hit + idx, trav_limits<false>(S));
         }
         if (done) {

@@ -1055,13 +1055,13 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     perCU = 0;
     if ((perCU = finish_blocks_per_cu()) <= 0) perCU = 4;
     s->finishGrid = s->cuCount * perCU;
-    // two-level traversal: the per-lane save slots of its grid (kernels.h save_word)
+    // two-level traversal: the per-lane save slots of its grid (kernels.h save_vec)
     s->ds.instSave = nullptr;
     if (s->ds.inst) {
-        uint32_t *save = nullptr;
+        uint4 *save = nullptr;
         // slots for the larger of the two grids that switch levels (k_trace_s, k_finish)
         const size_t lanes = (size_t)std::max(s->traceGridInst, s->finishGrid) * TRACE_BLOCK;
-        if (hipMalloc((void **)&save, (size_t)SAVE_WORDS * lanes * sizeof(uint32_t)) != hipSuccess) {
+        if (hipMalloc((void **)&save, (size_t)SAVE_VECS * lanes * sizeof(uint4)) != hipSuccess) {
             g_err = "out of device memory (instance save slots)";
             return fail(MTSG_ERR_OOM);
         }
