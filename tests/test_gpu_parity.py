@@ -315,3 +315,48 @@ def test_envmap_synthetic_sky_parity():
     _, c, gi = render_pair(scene, g)
     g.close()
     check_render(c, gi)
+
+
+def test_coplanar_tie_policy():
+    """Coplanar primitives: with -D glassY=-0.7 the glass box's bottom face
+    lies on the floor (as the tall box's always does), so rays through the
+    footprints meet a box triangle and the floor rectangle at exactly the
+    same distance.  Mitsuba keeps the first primitive that improves the
+    best distance strictly, in leaf order, skipping mailboxed ones
+    (sahkdtree3.h:250-290); the GPU tests the leaf-ordered copies with the
+    same strict comparison, so the winner must be the oracle's, bit for
+    bit -- from below the floor, from inside the boxes, and in a render of
+    the dielectric scene with the box standing on the floor."""
+    scene = mtsg.Scene(os.path.join(SCENES, "cbox_glass.xml"), {"width": 48, "height": 48, "spp": 8, "glassY": -0.7})
+    b = scene.prim_bounds()
+    flat = np.flatnonzero((b[:, 1] == -1.0) & (b[:, 4] == -1.0))
+    assert flat.size >= 5   # two triangles of each box bottom + the floor
+    rng = np.random.default_rng(17)
+    rays = []
+    for p in flat[:-1]:   # footprints of the box bottoms
+        n = 4000
+        x = rng.uniform(b[p, 0], b[p, 3], n)
+        z = rng.uniform(b[p, 2], b[p, 5], n)
+        for y0, dy in ((-1.0 - 0.25, 1.0), (-1.0 + 0.05, -1.0)):   # from below the floor, from inside the box
+            r = np.zeros((n, 8), np.float32)
+            r[:, 0], r[:, 1], r[:, 2] = x, y0, z
+            d = np.stack([rng.normal(0, 0.05, n), np.full(n, dy), rng.normal(0, 0.05, n)], 1)
+            r[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+            r[:, 6], r[:, 7] = 1e-4, np.inf
+            rays.append(r)
+    rays = np.concatenate(rays)
+    g = mtsg.GPUScene(scene, 0)
+    try:
+        t0, u0, v0, p0 = O.trace_closest(scene.desc, rays)
+        t1, u1, v1, p1 = g.trace_closest(rays)
+        hit = p0 != 0xFFFFFFFF
+        nt = scene.info.n_triangles
+        ids = np.where(flat < nt, flat, 0x80000000 | (flat - nt)).astype(np.uint32)
+        assert np.isin(p0[hit], ids).mean() > 0.5    # the rays do meet the coplanar pairs
+        np.testing.assert_array_equal(p1, p0)
+        np.testing.assert_array_equal(t1, t0)
+        np.testing.assert_array_equal(u1[hit], u0[hit])
+        _, c, gi = render_pair(scene, g)
+        check_render(c, gi)
+    finally:
+        g.close()
