@@ -46,7 +46,7 @@ struct DevScene {
     const mtsg_emitter *__restrict__ emitters;
     const float *__restrict__ emitter_cdf;
     const float *__restrict__ emitter_tri_cdf;
-    uint32_t n_emitters, n_tri;
+    uint32_t n_emitters, n_tri, n_bsdfs;
     float bmin[3], bmax[3];
     int has_env;
     DevEnv env;
@@ -2022,9 +2022,21 @@ struct ShadeStage {
 // (Out::shadow: NEE shadow ray + contribution; Out::next: continuation ray;
 // Out::state: throughput, radiance, meta of a continuing path).  A path that
 // ends writes its sample's final radiance.  first: bounce 0 (camera rays).
+// the small per-scene tables a path reads after its shading record: the BSDF
+// records, the emitters and their discrete CDF.  k_shade stages them in LDS
+// when they are small (MTSG_SHADE_LDS), so those reads are not another L2
+// round trip in each path's chain of dependent loads; elsewhere they point
+// at the scene's global arrays.
+struct ShadeTables {
+    const mtsg_bsdf *bsdfs;
+    const mtsg_emitter *emitters;
+    const float *emitter_cdf;
+};
+DEV ShadeTables global_tables(const DevScene &S) { return ShadeTables{S.bsdfs, S.emitters, S.emitter_cdf}; }
+
 template <bool ENV, int SMP, bool EXT, class Out>
 DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, bool first, uint32_t i,
-                    const uint4 meta, int hasAlpha, Out &out, bool &cont, bool &shadow) {
+                    const uint4 meta, int hasAlpha, Out &out, bool &cont, bool &shadow, const ShadeTables &tb) {
     const uint32_t slot = meta.z;
     const float4 h = ldS(&P.hit[i]);
     const float4 ro4 = ldS(&P.ray_o[i]), rd4 = ldS(&P.ray_d[i]);
@@ -2077,7 +2089,7 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
                     float lumPdf = 0.0f;
                     if (!(flags & F_DELTA))   // Scene::pdfEmitterDirect -> EnvironmentMap::pdfDirect
                         lumPdf = env_internal_pdf(S.env, env_rot(S.env.E->to_local, rd)) *
-                                 S.emitters[S.env.E->emitter].pdf_discrete;
+                                 tb.emitters[S.env.E->emitter].pdf_discrete;
                     L += T * value * mis(ldS(&P.aux[i]).w, lumPdf);
                 }
             }
@@ -2085,7 +2097,7 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
         } else {
             const int em = its.emitter;
             if (em >= 0) {
-                const mtsg_emitter &E = S.emitters[em];
+                const mtsg_emitter &E = tb.emitters[em];
                 const float3 value = dot(its.sh.n, -rd) > 0 ? ld3(E.radiance) : mk3(0, 0, 0);
                 float lumPdf = 0.0f;
                 if (!(flags & F_DELTA)) {
@@ -2107,18 +2119,18 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
     }
     if (!done && !((int)depth <= I.max_depth || I.max_depth < 0)) done = true;
     if (!done) {
-        const mtsg_bsdf &bsdf = S.bsdfs[its.bsdf];
+        const mtsg_bsdf &bsdf = tb.bsdfs[its.bsdf];
         const float3 wi = its.sh.toLocal(-rd);
         float3 alb;
         if (EXT) {
-            const mtsg_bsdf &eff = (bsdf.twosided && !(wi.z > 0)) ? S.bsdfs[bsdf.back] : bsdf;
+            const mtsg_bsdf &eff = (bsdf.twosided && !(wi.z > 0)) ? tb.bsdfs[bsdf.back] : bsdf;
             alb = eff.texture ? texture_eval(S, eff.texture - 1, h, inst, its, ro, first && S.cam_diffs, rxd, ryd)
                               : ld3(eff.reflectance);
         } else {
             alb = ld3(bsdf.reflectance);
         }
         if (first && its.emitter >= 0 && !I.hide_emitters) {
-            if (dot(its.sh.n, -rd) > 0) L += T * ld3(S.emitters[its.emitter].radiance);
+            if (dot(its.sh.n, -rd) > 0) L += T * ld3(tb.emitters[its.emitter].radiance);
         }
         if (((int)depth >= I.max_depth && I.max_depth > 0) ||
             (I.strict_normals && dot(rd, its.geoN) * wi.z >= 0)) {
@@ -2130,8 +2142,8 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
                 float sx, sy;
                 next2D<SMP>(I, smp, sx, sy);
                 float emPdf;
-                const uint32_t ei = pmf_sample_reuse(S.emitter_cdf, S.n_emitters, sx, emPdf);
-                const mtsg_emitter &E = S.emitters[ei];
+                const uint32_t ei = pmf_sample_reuse(tb.emitter_cdf, S.n_emitters, sx, emPdf);
+                const mtsg_emitter &E = tb.emitters[ei];
                 float3 dd, value;
                 float dist, pdf;
                 bool accepted;
@@ -2480,6 +2492,10 @@ __global__ void __launch_bounds__(SHADE_BLOCK) k_shade_om(DevScene S, DevIntegra
 }
 
 // qin < 0: bounce 0 over the identity queue of nIdentity slots
+#ifndef MTSG_SHADE_LDS
+#define MTSG_SHADE_LDS 0   // measurement variant: BSDF / emitter tables in LDS (k_shade)
+#endif
+constexpr int SHADE_LDS_BSDFS = 4, SHADE_LDS_EMITTERS = 16;
 #ifndef MTSG_SHADE_WAVES
 #define MTSG_SHADE_WAVES 4   // 127 VGPRs: 4 waves/SIMD (3 at 144; 5+ spill heavily)
 #endif
@@ -2496,6 +2512,24 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
     __shared__ ShadeStage stage;
+#if MTSG_SHADE_LDS
+    __shared__ mtsg_bsdf s_bsdfs[SHADE_LDS_BSDFS];
+    __shared__ mtsg_emitter s_emitters[SHADE_LDS_EMITTERS];
+    __shared__ float s_ecdf[SHADE_LDS_EMITTERS + 1];
+    ShadeTables tb = global_tables(S);
+    const uint32_t nb = S.n_bsdfs, ne = S.n_emitters;
+    if (nb <= (uint32_t)SHADE_LDS_BSDFS && ne <= (uint32_t)SHADE_LDS_EMITTERS) {
+        for (uint32_t w = threadIdx.x; w < nb * (uint32_t)(sizeof(mtsg_bsdf) / 4); w += blockDim.x)
+            ((uint32_t *)s_bsdfs)[w] = ((const uint32_t *)S.bsdfs)[w];
+        for (uint32_t w = threadIdx.x; w < ne * (uint32_t)(sizeof(mtsg_emitter) / 4); w += blockDim.x)
+            ((uint32_t *)s_emitters)[w] = ((const uint32_t *)S.emitters)[w];
+        for (uint32_t w = threadIdx.x; w <= ne; w += blockDim.x) s_ecdf[w] = S.emitter_cdf[w];
+        __syncthreads();
+        tb = ShadeTables{s_bsdfs, s_emitters, s_ecdf};
+    }
+#else
+    const ShadeTables tb = global_tables(S);
+#endif
     uint32_t count = nIdentity;
     if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     const uint32_t nIter = (count + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
@@ -2511,7 +2545,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
         }
         if (alive) {
             StageOut out{stage};
-            shade_path<ENV, SMP, EXT>(S, I, B, P, bounce == 0, i, meta, hasAlpha, out, cont, shadow);
+            shade_path<ENV, SMP, EXT>(S, I, B, P, bounce == 0, i, meta, hasAlpha, out, cont, shadow, tb);
         }
         const uint32_t slot = meta.z;
         // The output positions come from the workgroup-aggregated append; the
@@ -2630,7 +2664,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
                 const uint4 meta = ldS(&P.meta[idx]);
                 FinishOut out{P, idx, make_float4(0.f, 0.f, 0.f, 0.f)};
                 bool cont = false, shadow = false;
-                shade_path<ENV, SMP, EXT>(S, I, B, P, false, idx, meta, hasAlpha, out, cont, shadow);
+                shade_path<ENV, SMP, EXT>(S, I, B, P, false, idx, meta, hasAlpha, out, cont, shadow, global_tables(S));
                 state = FS_IDLE;
                 if (shadow) {
                     out.c.w = __uint_as_float(cont ? idx : (0x80000000u | meta.z));

@@ -984,6 +984,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     }
     ds.n_emitters = d->n_emitters;
     ds.n_tri = d->n_triangles;
+    ds.n_bsdfs = d->n_bsdfs;
     for (int k = 0; k < 3; ++k) { ds.bmin[k] = d->aabb_min[k]; ds.bmax[k] = d->aabb_max[k]; }
     DevCamera &c = s->cam;
     const mtsg_camera &hc = d->camera;
