@@ -796,7 +796,10 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
 // coalesced 16-B access per vector), not in LDS, which holds only the stacks
 // (5.25 KB per wave: 7 waves per SIMD; 2.3 KB more would allow 5).  The
 // instance a lane is inside stays in a register (k_trace_s / k_finish `inst`).
-constexpr int SAVE_VECS = 2;
+#ifndef MTSG_SAVE_RAY
+#define MTSG_SAVE_RAY 0   // variant: the world ray saved with the state (two more vectors)
+#endif
+constexpr int SAVE_VECS = MTSG_SAVE_RAY ? 4 : 2;
 // the two levels' stacks in one LDS array: top level in entries
 // [0, OUTER_STACK), group level in [OUTER_STACK, OUTER_STACK + INNER_STACK)
 __shared__ uint2 s_lvNode[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
@@ -843,7 +846,13 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
     r.lfEnd = b.y;
     r.lfTmax = __uint_as_float(b.z);
     r.bits = b.w | found;
+#if MTSG_SAVE_RAY
+    const uint4 c = save_vec(S, 2), e = save_vec(S, 3);
+    const float4 ro = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), 0.f);
+    const float4 rd = make_float4(__uint_as_float(c.w), __uint_as_float(e.x), __uint_as_float(e.y), 0.f);
+#else
     float4 ro = ldS(wo), rd = ldS(wd);
+#endif
     r.o = xyz(ro);
     r.d = xyz(rd);
     r.inv = mk3(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
@@ -932,6 +941,10 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         if (ok & (nearT <= farT) & (t1 > t0)) {
             save_vec(S, 0) = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
             save_vec(S, 1) = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
+#if MTSG_SAVE_RAY
+            save_vec(S, 2) = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(d.x));
+            save_vec(S, 3) = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), 0u, 0u);
+#endif
             inst = ii;
             const uint2 root = make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w));
             r.o = lo;

@@ -32,3 +32,18 @@ def test_lookup_matches_the_whole_key_only(tmp_path):
     assert src.endswith("r03_pmc_c3.json") and "k_trace_s<false, 16, false>" in j["kernels"]
     for k in (two, dev, share):
         assert bench.pmc_lookup(k, str(tmp_path)) == (None, None)
+
+
+def test_rocprof_names_normalise_to_the_instantiation():
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "pmc_kernels", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "pmc_kernels.py"))
+    pk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pk)
+    n = pk.kernel_name
+    assert n("void (anonymous namespace)::k_trace_s<false, 16, false>(mtsg::DevScene, mtsg::DevPaths, int, int, "
+             "unsigned int, unsigned long long*)") == "k_trace_s<false, 16, false>"
+    assert n("void (anonymous namespace)::k_trace_s<false, 16, true, false>(mtsg::DevScene)") == "k_trace_s<false, 16, true, false>"
+    assert n("(anonymous namespace)::k_camera(mtsg::DevCamera, mtsg::DevIntegrator)") == "k_camera"
+    assert n("void (anonymous namespace)::k_splat<5, 4>(mtsg::DevCamera, float*, int, int)") == "k_splat<5, 4>"
