@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def trace_kernel(a):
     """rocprofv3's name of the timed traversal instantiation this run launches
     (the instrumented COUNT pass runs k_trace_s<true, ...>)."""
-    return "k_trace_s<false, 16, true>" if a.instancing == "two-level" else "k_trace_s<false, 16, false>"
+    return "k_trace_s<false, 16, true, false>" if a.instancing == "two-level" else "k_trace_s<false, 16, false, false>"
 
 
 def pmc_key(a, world=1):

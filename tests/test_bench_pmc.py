@@ -16,8 +16,8 @@ def args(**kw):
 
 
 def test_trace_kernel_names():
-    assert bench.trace_kernel(args()) == "k_trace_s<false, 16, false>"
-    assert bench.trace_kernel(args(instancing="two-level")) == "k_trace_s<false, 16, true>"
+    assert bench.trace_kernel(args()) == "k_trace_s<false, 16, false, false>"
+    assert bench.trace_kernel(args(instancing="two-level")) == "k_trace_s<false, 16, true, false>"
 
 
 def test_lookup_matches_the_whole_key_only(tmp_path):
@@ -26,10 +26,10 @@ def test_lookup_matches_the_whole_key_only(tmp_path):
     dev = bench.pmc_key(args(kd_build="device"))
     share = bench.pmc_key(args(emulate_ranks=8))
     assert len({json.dumps(k, sort_keys=True) for k in (flat, two, dev, share)}) == 4
-    (tmp_path / "r03_pmc_c3.json").write_text(json.dumps({"key": flat, "kernels": {"k_trace_s<false, 16, false>": {}}}))
+    (tmp_path / "r03_pmc_c3.json").write_text(json.dumps({"key": flat, "kernels": {"k_trace_s<false, 16, false, false>": {}}}))
     (tmp_path / "r02_pmc_c3.json").write_text(json.dumps({"key": flat, "kernels": {"old": {}}}))
     j, src = bench.pmc_lookup(flat, str(tmp_path))
-    assert src.endswith("r03_pmc_c3.json") and "k_trace_s<false, 16, false>" in j["kernels"]
+    assert src.endswith("r03_pmc_c3.json") and "k_trace_s<false, 16, false, false>" in j["kernels"]
     for k in (two, dev, share):
         assert bench.pmc_lookup(k, str(tmp_path)) == (None, None)
 
