@@ -1998,7 +1998,47 @@ DEV void emitter_sample_position(const DevScene &S, const mtsg_emitter &em, floa
 struct BlockAppend {
     uint32_t cnt[2];
     uint32_t base[2];
+    uint32_t bin[8];   // block_append2_oct: survivors per direction octant, then their offsets
 };
+
+#ifndef MTSG_SORT_OCT
+#define MTSG_SORT_OCT 0   // variant: a workgroup's survivors grouped by direction octant
+#endif
+// block_append2 with the survivors (p1) of the workgroup grouped by key (the
+// octant of the continuation direction): a trace wave takes consecutive work
+// list entries, so its lanes then start from nearby origins (paths of one
+// workgroup) in one octant.  The order of the paths does not change the
+// image (the random numbers are keyed by pixel and sample).
+DEV void block_append2_oct(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p0, bool p1, uint32_t key,
+                           uint32_t &i0, uint32_t &i1) {
+    if (threadIdx.x < 8) ba.bin[threadIdx.x] = 0;
+    if (threadIdx.x == 0) ba.cnt[0] = 0;
+    __syncthreads();
+    const unsigned long long below = (1ull << lane_id()) - 1ull;
+    const unsigned long long m0 = __ballot(p0);
+    uint32_t w0 = 0;
+    if (lane_id() == 0 && m0) w0 = atomicAdd(&ba.cnt[0], (uint32_t)__popcll(m0));
+    w0 = __shfl(w0, 0);
+    uint32_t rank = 0, wk = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+        const unsigned long long mk = __ballot(p1 && key == k);
+        uint32_t w = 0;
+        if (lane_id() == 0 && mk) w = atomicAdd(&ba.bin[k], (uint32_t)__popcll(mk));
+        w = __shfl(w, 0);
+        if (key == k) { rank = (uint32_t)__popcll(mk & below); wk = w; }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ba.base[0] = ba.cnt[0] ? atomicAdd(gcnt0, ba.cnt[0]) : 0u;
+        uint32_t run = 0;
+        for (int k = 0; k < 8; ++k) { const uint32_t c = ba.bin[k]; ba.bin[k] = run; run += c; }
+        ba.base[1] = run ? atomicAdd(gcnt1, run) : 0u;
+    }
+    __syncthreads();
+    i0 = ba.base[0] + w0 + (uint32_t)__popcll(m0 & below);
+    i1 = ba.base[1] + ba.bin[key & 7u] + wk + rank;
+}
 
 DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p0, bool p1, uint32_t &i0, uint32_t &i1) {
     if (threadIdx.x == 0) { ba.cnt[0] = 0; ba.cnt[1] = 0; }
@@ -2566,7 +2606,13 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
         // in registers live across its barriers.
         const int tid = threadIdx.x;
         uint32_t is, ic;
+#if MTSG_SORT_OCT
+        const float4 nd = stage.d[tid];
+        const uint32_t key = (nd.x < 0.f ? 1u : 0u) | (nd.y < 0.f ? 2u : 0u) | (nd.z < 0.f ? 4u : 0u);
+        block_append2_oct(ba, &P.cnt[cnt_s(bounce & 1)], &P.cnt[cnt_q(qout)], shadow, cont, cont ? key : 0u, is, ic);
+#else
         block_append2(ba, &P.cnt[cnt_s(bounce & 1)], &P.cnt[cnt_q(qout)], shadow, cont, is, ic);
+#endif
         if (cont) {
             // survivor: compacted into the next bounce's arrays
             stS(&P.n_ray_o[ic], stage.o[tid]);
