@@ -259,11 +259,12 @@ constexpr size_t PATH_STATE_BYTES = 272;    // bytes per path slot (DevPaths: 2 
 #endif
 constexpr int SHORT_STACK = MTSG_SHORT_STACK;   // LDS short stack entries per lane
 // two-level traversal (kernels.h spec_iter_i): the top level's stack, and the
-// group level's own, one entry shorter than the flat traversal's: 5 x 12 B +
-// 2 x 12 B per lane = 5.25 KB per wave, 7 waves/SIMD
+// group level's own, as deep as the flat traversal's: 6 x 12 B + 2 x 12 B per
+// lane = 6 KB per wave, 6.6 waves/SIMD (the kernel runs 6, register bound).
+// 6 entries measured 1.2% faster than 5 on C3-two-level (r03 variants gs6).
 constexpr int OUTER_STACK = 2;
 #ifndef MTSG_INNER_STACK
-#define MTSG_INNER_STACK 5
+#define MTSG_INNER_STACK 6
 #endif
 constexpr int INNER_STACK = MTSG_INNER_STACK;
 // the compact speculative traversal is sized for 8 waves per SIMD (64 VGPRs)
@@ -271,10 +272,10 @@ constexpr int INNER_STACK = MTSG_INNER_STACK;
 #define MTSG_SPEC_WAVES 8
 #endif
 #define SPEC_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SPEC_WAVES)))
-// the two-level kernel: its LDS (group stack + top-level stack, 5.25 KB/wave)
-// would allow 7 waves/SIMD, but at 72 VGPRs the compiler spills 20 B/lane to
-// scratch; with the registers of 6 (80) it does not, and C3 renders 13% faster
-// (1043 vs 920 Msamples/s, round 3)
+// the two-level kernel runs 6 waves/SIMD: at 7 (72 VGPRs) the compiler spills
+// 20 B/lane to scratch; with the registers of 6 (80) it does not, and C3
+// renders 13% faster (1043 vs 920 Msamples/s, round 3).  Its LDS (group stack
+// + top-level stack, 6 KB/wave) allows 6.6 waves/SIMD.
 #ifndef MTSG_INST_WAVES
 #define MTSG_INST_WAVES 6
 #endif
@@ -793,11 +794,14 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
 // the top-level state saved while a lane is inside an instance, two uint4 per
 // lane: {cur.x, cur.y, tmin, tmax}, {lfE, lfEnd, lfTmax, bits}.  It lives in
 // per-lane global slots (S.instSave, vector k of lane g at k * lanes + g: one
-// coalesced 16-B access per vector), not in LDS, which holds only the stacks
-// (5.25 KB per wave: 7 waves per SIMD; 2.3 KB more would allow 5).  The
-// instance a lane is inside stays in a register (k_trace_s / k_finish `inst`).
+// coalesced 16-B access per vector), not in LDS, which holds only the stacks.
+// The world ray is saved too (vectors 2-3: {o, d.x}, {d.y, d.z, -, -}), so
+// leaving an instance reloads it from the lane's own coalesced slots instead of the
+// ray gathered back from the work list through the path index: 3% faster on
+// C3-two-level (r03 variants wsave).  The instance a lane is inside stays in a
+// register (k_trace_s / k_finish `inst`).
 #ifndef MTSG_SAVE_RAY
-#define MTSG_SAVE_RAY 0   // variant: the world ray saved with the state (two more vectors)
+#define MTSG_SAVE_RAY 1
 #endif
 constexpr int SAVE_VECS = MTSG_SAVE_RAY ? 4 : 2;
 // the two levels' stacks in one LDS array: top level in entries
@@ -2546,7 +2550,7 @@ __global__ void __launch_bounds__(SHADE_BLOCK) k_shade_om(DevScene S, DevIntegra
 
 // qin < 0: bounce 0 over the identity queue of nIdentity slots
 #ifndef MTSG_SHADE_LDS
-#define MTSG_SHADE_LDS 0   // measurement variant: BSDF / emitter tables in LDS (k_shade)
+#define MTSG_SHADE_LDS 1   // BSDF / emitter tables staged in LDS when they fit (k_shade): +1.4% on C3
 #endif
 constexpr int SHADE_LDS_BSDFS = 4, SHADE_LDS_EMITTERS = 16;
 #ifndef MTSG_SHADE_WAVES
