@@ -499,6 +499,7 @@ struct SpecRay {
     uint32_t lfE, lfEnd; // primitive range of the held leaf
     float lfTmax;        // exit distance of the held leaf; < 0: none held
     uint32_t bits;       // see SB_*
+    uint32_t mb;         // mailbox state of exact ties (mailbox_step)
 };
 // bits: top slot of the circular short stack (0-2), entries held (3-5),
 // entries dropped since the last restart (6), kd-restarts of the ray at this
@@ -653,6 +654,7 @@ DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float r
     r.lfE = r.lfEnd = 0;
     r.lfTmax = -1.0f;
     r.bits = dneg << SB_DNEG | (shadow ? SB_SHADOW : 0u);
+    r.mb = 0;
     return true;
 }
 
@@ -688,6 +690,48 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
         r.tmax = tsplit;
     }
     return c;
+}
+
+// Mitsuba's mailbox on exact ties.  Its leaf loop skips a primitive still in
+// the 8-entry direct-mapped mailbox (slot = TriAccel index & 7, written by
+// every test: sahkdtree3.h:30-32,138-152,277-291) and accepts a hit at t <=
+// the best distance, so of primitives hit at exactly the same t the winner is
+// the one tested last, retests of still-boxed primitives not counting.  Only
+// a tie can tell a retest from a first test (a retested primitive hits at the
+// t it hit before, which can only equal the best), and the only retests that
+// could change the winner are of the best and of the best it displaced at the
+// same t ("prev"), so instead of the 8 entries the lane keeps which slots
+// have been written since each of the two was boxed (r.mb): bits 0-7 since
+// the best, 8-15 since prev, 16 prev exists, 17-19 prev's slot, 20-22 the
+// best's slot; prev's identity in LDS, the best's in its hit record.  A miss
+// or a closer hit costs a shift and an or; ties take the branch.  Exact for
+// ties of two primitives; of three or more, a retest of the earliest one after
+// the later two is accepted where Mitsuba may skip it.
+#ifndef MTSG_MAILBOX
+#define MTSG_MAILBOX 1   // 0: measurement variant, the last primitive tested wins a tie
+#endif
+__shared__ uint32_t s_mbPrev[TRACE_BLOCK];
+DEV bool mailbox_step(SpecRay &r, uint32_t key, uint32_t id, bool h, float t, const float4 *hitOut) {
+    const uint32_t sl = key & 7u, mb = r.mb;
+    if (!(h & (bool)(r.bits & SB_FOUND) & (t == r.best))) {
+        // the test writes slot sl; a closer hit is the new best, just boxed
+        r.mb = h ? sl << 20 : mb | (0x101u << sl);
+        return h;
+    }
+    const uint32_t bs = (mb >> 20) & 7u, ps = (mb >> 17) & 7u;
+    const uint32_t bestId = ((const uint32_t *)hitOut)[3];
+    const uint32_t prevId = s_mbPrev[lane_here()];
+    if (id == bestId) {
+        // the best itself: skipped if boxed, else retested (same hit) and re-boxed
+        r.mb = (mb & ~(1u << bs)) | (0x100u << bs);
+        return false;
+    }
+    if ((mb & 0x10000u) && id == prevId && !(mb & (0x100u << ps))) return false;   // prev, still boxed
+    // tested for the first time or evicted: the tie winner; the best it
+    // displaces becomes prev (boxed unless its slot was written since)
+    s_mbPrev[lane_here()] = bestId;
+    r.mb = sl << 20 | bs << 17 | 0x10000u | ((mb & 0xFFu) | (1u << sl)) << 8;
+    return true;
 }
 
 template <bool COUNT>
@@ -726,11 +770,15 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
         const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
         if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+        const uint32_t id = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
+#if MTSG_MAILBOX
+        if (!(r.bits & SB_SHADOW)) h = mailbox_step(r, __float_as_uint(f2.z), id, h, t, hitOut);
+#endif
         if (h) {
             r.bits |= SB_FOUND;
             if (r.bits & SB_SHADOW) return true;   // any hit occludes
             r.best = t;
-            stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
+            stS(hitOut, make_float4(t, u, v, __uint_as_float(id)));
         }
         ++r.lfE;
     }

@@ -761,6 +761,9 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
                     if (ta.prim_index >= d->n_instances) { layoutOk = false; break; }
                     ta.k = KINST;
                 }
+                // the traversal keys Mitsuba's mailbox on the TriAccel index
+                // (kernels.h mailbox_step), not the shape index
+                ta.shape_index = p;
                 const float4 *t = (const float4 *)&ta;
                 triL.push_back(t[0]); triL.push_back(t[1]); triL.push_back(t[2]);
             }

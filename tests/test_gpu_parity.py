@@ -321,12 +321,14 @@ def test_coplanar_tie_policy():
     """Coplanar primitives: with -D glassY=-0.7 the glass box's bottom face
     lies on the floor (as the tall box's always does), so rays through the
     footprints meet a box triangle and the floor rectangle at exactly the
-    same distance.  Mitsuba keeps the first primitive that improves the
-    best distance strictly, in leaf order, skipping mailboxed ones
-    (sahkdtree3.h:250-290); the GPU tests the leaf-ordered copies with the
-    same strict comparison, so the winner must be the oracle's, bit for
-    bit -- from below the floor, from inside the boxes, and in a render of
-    the dielectric scene with the box standing on the floor."""
+    same distance.  Mitsuba accepts a hit at t <= the best distance, in
+    leaf order, skipping primitives still in its 8-entry mailbox
+    (sahkdtree3.h:250-290), so the tie goes to the primitive tested last
+    whose retest was not a mailbox hit; the GPU emulates the mailbox on
+    ties (kernels.h mailbox_step), so the winner must be the oracle's, bit
+    for bit -- from below the floor, from inside the boxes, from random
+    points of the scene (ties on every coplanar face pair it has), and in
+    a render of the dielectric scene with the box standing on the floor."""
     scene = mtsg.Scene(os.path.join(SCENES, "cbox_glass.xml"), {"width": 48, "height": 48, "spp": 8, "glassY": -0.7})
     b = scene.prim_bounds()
     flat = np.flatnonzero((b[:, 1] == -1.0) & (b[:, 4] == -1.0))
@@ -344,6 +346,13 @@ def test_coplanar_tie_policy():
             r[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
             r[:, 6], r[:, 7] = 1e-4, np.inf
             rays.append(r)
+    n = 100000
+    r = np.zeros((n, 8), np.float32)
+    r[:, :3] = rng.uniform(-1, 1, (n, 3))
+    d = rng.normal(size=(n, 3))
+    r[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    r[:, 6], r[:, 7] = 1e-4, np.inf
+    rays.append(r)
     rays = np.concatenate(rays)
     g = mtsg.GPUScene(scene, 0)
     try:
@@ -352,7 +361,7 @@ def test_coplanar_tie_policy():
         hit = p0 != 0xFFFFFFFF
         nt = scene.info.n_triangles
         ids = np.where(flat < nt, flat, 0x80000000 | (flat - nt)).astype(np.uint32)
-        assert np.isin(p0[hit], ids).mean() > 0.5    # the rays do meet the coplanar pairs
+        assert np.isin(p0[:32000][hit[:32000]], ids).mean() > 0.5    # the rays do meet the coplanar pairs
         np.testing.assert_array_equal(p1, p0)
         np.testing.assert_array_equal(t1, t0)
         np.testing.assert_array_equal(u1[hit], u0[hit])
