@@ -346,6 +346,7 @@ def test_coplanar_tie_policy():
             r[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
             r[:, 6], r[:, 7] = 1e-4, np.inf
             rays.append(r)
+    n_cop = sum(len(x) for x in rays)
     n = 100000
     r = np.zeros((n, 8), np.float32)
     r[:, :3] = rng.uniform(-1, 1, (n, 3))
@@ -361,7 +362,7 @@ def test_coplanar_tie_policy():
         hit = p0 != 0xFFFFFFFF
         nt = scene.info.n_triangles
         ids = np.where(flat < nt, flat, 0x80000000 | (flat - nt)).astype(np.uint32)
-        assert np.isin(p0[:32000][hit[:32000]], ids).mean() > 0.5    # the rays do meet the coplanar pairs
+        assert np.isin(p0[:n_cop][hit[:n_cop]], ids).mean() > 0.5    # the rays do meet the coplanar pairs
         np.testing.assert_array_equal(p1, p0)
         np.testing.assert_array_equal(t1, t0)
         np.testing.assert_array_equal(u1[hit], u0[hit])
