@@ -126,6 +126,7 @@ struct DevPaths {
     uint4 *n_meta;
     float4 *hit;      // t, u, v, prim (bits) of ray i
     uint32_t *hitInst;   // instance of hit i (0xFFFFFFFF: none); two-level scenes only
+    uint32_t *tie;       // closest rays of a trace launch that met an exact tie (cnt[CNT_TIE] of them)
     float4 *L;        // per sample slot: final radiance, alpha (k_splat input)
     float4 *sh_o;     // shadow ray i: origin, maxt
     float4 *sh_d;     // direction, mint
@@ -213,6 +214,7 @@ constexpr int XGROUPS = 8;                  // XCDs: blocks b and b + 8 share on
 // (ping-pong: bounce b appends to S(b & 1) while its trace reads S((b-1) & 1))
 constexpr int CNT_Q0 = 0, CNT_Q1 = 64, CNT_S0 = 128, CNT_S1 = 192;
 constexpr int CNT_ERR = 96;   // sticky error flags (CNT_ERR_*)
+constexpr int CNT_TIE = 224;  // entries of P.tie (k_trace_s appends, k_tie reads)
 constexpr uint32_t CNT_ERR_QMC_DIM = 1u, CNT_ERR_TRAVERSAL = 2u;
 constexpr int CNT_FETCH = 256;                           // XGROUPS counters, 32 words apart
 constexpr int CNT_WORDS = CNT_FETCH + 32 * XGROUPS;
@@ -253,7 +255,7 @@ constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 28;
 #ifndef MTSG_LANES
 #define MTSG_LANES 1
 #endif
-constexpr size_t PATH_STATE_BYTES = 272;    // bytes per path slot (DevPaths: 2 x 96 dense + hit, L, 3 x shadow)
+constexpr size_t PATH_STATE_BYTES = 276;    // bytes per path slot (DevPaths: 2 x 96 dense + hit, L, 3 x shadow, tie)
 #ifndef MTSG_SHORT_STACK
 #define MTSG_SHORT_STACK 6   // 6 x 12 B x 64 lanes = 4.6 KB LDS/wave -> 8 waves/SIMD (8: 6.5, 12: 4.2)
 #endif
@@ -500,15 +502,18 @@ struct SpecRay {
     float lfTmax;        // exit distance of the held leaf; < 0: none held
     uint32_t bits;       // see SB_*
     uint32_t mb;         // mailbox state of exact ties (mailbox_step)
+    uint32_t bestKey;    // TriAccel index of the best hit (mailbox key)
 };
 // bits: top slot of the circular short stack (0-2), entries held (3-5),
 // entries dropped since the last restart (6), kd-restarts of the ray at this
 // level (7-15), ray direction signs (16-18), traversal done (19), hit found
-// (20), shadow ray (21), inside an instance (22), restart limit hit (31)
+// (20), shadow ray (21), inside an instance (22), an exact tie met (23),
+// restart limit hit (31)
 enum : uint32_t {
     SB_TOP = 7u, SB_N = 7u << 3, SB_N1 = 1u << 3, SB_DROPPED = 1u << 6, SB_STACK = 0x7Fu,
     SB_RST_SHIFT = 7, SB_RST1 = 1u << 7, SB_RST_MASK = 0x1FFu,
-    SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20, SB_SHADOW = 1u << 21, SB_ERR = 1u << 31
+    SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20, SB_SHADOW = 1u << 21, SB_TIE = 1u << 23,
+    SB_ERR = 1u << 31
 };
 // the restart guard's defaults (DevScene::rstGuard / rstMax): rays of the
 // scenes at hand restart 0-3 times (tools/iter_hist.py)
@@ -703,38 +708,45 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 // same t ("prev"), so instead of the 8 entries the lane keeps which slots
 // have been written since each of the two was boxed (r.mb): bits 0-7 since
 // the best, 8-15 since prev, 16 prev exists, 17-19 prev's slot, 20-22 the
-// best's slot; prev's identity in LDS, the best's in its hit record.  A miss
-// or a closer hit costs a shift and an or; ties take the branch.  Exact for
+// best's slot; prev's identity in LDS, the best's in its hit record.  Exact for
 // ties of two primitives; of three or more, a retest of the earliest one after
 // the later two is accepted where Mitsuba may skip it.
 #ifndef MTSG_MAILBOX
 #define MTSG_MAILBOX 1   // 0: measurement variant, the last primitive tested wins a tie
 #endif
 __shared__ uint32_t s_mbPrev[TRACE_BLOCK];
-DEV bool mailbox_step(SpecRay &r, uint32_t key, uint32_t id, bool h, float t, const float4 *hitOut) {
-    const uint32_t sl = key & 7u, mb = r.mb;
-    if (!(h & (bool)(r.bits & SB_FOUND) & (t == r.best))) {
-        // the test writes slot sl; a closer hit is the new best, just boxed
-        r.mb = h ? sl << 20 : mb | (0x101u << sl);
-        return h;
-    }
+// the tie branch of mailbox_step (mb: the state before this test)
+DEV bool mailbox_tie(SpecRay &r, uint32_t mb, uint32_t sl, uint32_t id, const float4 *hitOut) {
+    if (!(r.bits & SB_FOUND)) return true;   // a first hit exactly at the far end of the interval
     const uint32_t bs = (mb >> 20) & 7u, ps = (mb >> 17) & 7u;
     const uint32_t bestId = ((const uint32_t *)hitOut)[3];
-    const uint32_t prevId = s_mbPrev[lane_here()];
     if (id == bestId) {
         // the best itself: skipped if boxed, else retested (same hit) and re-boxed
         r.mb = (mb & ~(1u << bs)) | (0x100u << bs);
         return false;
     }
-    if ((mb & 0x10000u) && id == prevId && !(mb & (0x100u << ps))) return false;   // prev, still boxed
+    if ((mb & 0x10000u) && id == s_mbPrev[lane_here()] && !(mb & (0x100u << ps))) {
+        r.mb = mb;   // prev, still boxed
+        return false;
+    }
     // tested for the first time or evicted: the tie winner; the best it
     // displaces becomes prev (boxed unless its slot was written since)
     s_mbPrev[lane_here()] = bestId;
     r.mb = sl << 20 | bs << 17 | 0x10000u | ((mb & 0xFFu) | (1u << sl)) << 8;
     return true;
 }
+// one primitive test's mailbox bookkeeping (key: its TriAccel index, tag:
+// slot << 20 | 0x101 << slot): a miss ors in the low half (the slot written,
+// in both masks), a closer hit keeps only the slot (a new best, just boxed);
+// ties take the branch
+DEV bool mailbox_step(SpecRay &r, uint32_t key, bool isRect, uint32_t prim, bool h, float t, const float4 *hitOut) {
+    const uint32_t mb = r.mb, tag = (key & 7u) << 20 | 0x101u << (key & 7u);
+    r.mb = h ? (tag & 0x700000u) : ((tag & 0xFFFFu) | mb);
+    if (h & (t == r.best)) h = mailbox_tie(r, mb, tag >> 20, isRect ? (0x80000000u | prim) : prim, hitOut);
+    return h;
+}
 
-template <bool COUNT>
+template <bool COUNT, bool MB = false>
 DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cnt, float4 *hitOut, const TravLimits &L) {
     const uint2 n = r.cur;
     const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
@@ -770,15 +782,20 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
         const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
         if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
-        const uint32_t id = isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w);
 #if MTSG_MAILBOX
-        if (!(r.bits & SB_SHADOW)) h = mailbox_step(r, __float_as_uint(f2.z), id, h, t, hitOut);
+        // a tie is only flagged here; the ray is then traced again with the
+        // mailbox (tie_retrace).  Shadow rays end at their first hit.
+        // (a primitive spanning leaves is retested at the same t: not a tie)
+        const uint32_t key = __float_as_uint(f2.z);
+        if (MB) h = mailbox_step(r, key, isRect, __float_as_uint(f2.w), h, t, hitOut);
+        else r.bits |= (h & (t == r.best) & (key != r.bestKey)) ? SB_TIE : 0u;
+        if (h) r.bestKey = key;
 #endif
         if (h) {
             r.bits |= SB_FOUND;
             if (r.bits & SB_SHADOW) return true;   // any hit occludes
             r.best = t;
-            stS(hitOut, make_float4(t, u, v, __uint_as_float(id)));
+            stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
         }
         ++r.lfE;
     }
@@ -823,6 +840,19 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         }
     }
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
+}
+
+// A closest-hit ray whose traversal met an exact tie (SB_TIE: a hit at the
+// best distance so far) is traced again from its start with Mitsuba's mailbox
+// emulated (mailbox_step): that can only change which of the tied primitives
+// its hit record names.  Ties are rare (coplanar faces, shared edges), so the
+// traversal loop pays one compare per test for them instead of the mailbox.
+DEV void tie_retrace(const DevScene &S, SpecRay &r, SpecStack stk, const float4 *rayO, const float4 *rayD,
+                     float4 *hitOut, const TravLimits &L) {
+    const float4 ro = ldS(rayO), rd = ldS(rayD);
+    TraceCounts tc{0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (!spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, false, r)) return;
+    while (!spec_iter<false, true>(S, r, stk, tc, hitOut, L)) {}
 }
 
 // ---------------------------------------------------------------------------
@@ -1155,6 +1185,9 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
         if (COUNT && active) ++iters;
         if (done) {
             active = false;
+            // k_tie traces it again with the mailbox
+            if (MTSG_MAILBOX && !INST && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE)
+                P.tie[atomicAdd(&P.cnt[CNT_TIE], 1u)] = idx;
             if (COUNT) {
                 const bool sh = (r.bits & SB_SHADOW) != 0;
                 atomicMax(&P.ctr[sh ? 15 : 7], (unsigned long long)iters);
@@ -2801,6 +2834,8 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
             else done = spec_iter<false>(S, r, stk, tc, P.hit + idx, trav_limits<false>(S));
         }
         if (done) {
+            if (MTSG_MAILBOX && !S.inst && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE)
+                tie_retrace(S, r, stk, P.ray_o + idx, P.ray_d + idx, P.hit + idx, trav_limits<false>(S));
             if (r.bits & SB_ERR) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);
             if (r.bits & SB_SHADOW) {
                 if (!(r.bits & SB_FOUND)) shadow_unoccluded(P, idx);
@@ -2937,6 +2972,23 @@ __global__ void k_reset(uint32_t *cnt, int qout, int sOut) {
         if (sOut >= 0) cnt[sOut ? CNT_S1 : CNT_S0] = 0;
     }
     if (threadIdx.x < XGROUPS) cnt[CNT_FETCH + 32 * threadIdx.x] = 0;
+    if (threadIdx.x == 32) cnt[CNT_TIE] = 0;
+}
+
+// the closest rays of the trace launch before it that met an exact tie,
+// traced again with the mailbox (tie_retrace); its grid strides over them
+template <bool KNOBS>
+__global__ void __launch_bounds__(TRACE_BLOCK) k_tie(DevScene S, DevPaths P) {
+    const SpecStack stk{};
+    lds_top_init(S);
+    const uint32_t n = __atomic_load_n(&P.cnt[CNT_TIE], __ATOMIC_RELAXED);
+    const TravLimits L = trav_limits<KNOBS>(S);
+    SpecRay r;
+    for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
+        const uint32_t idx = P.tie[i];
+        tie_retrace(S, r, stk, P.ray_o + idx, P.ray_d + idx, P.hit + idx, L);
+        if (r.bits & SB_ERR) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);
+    }
 }
 
 }  // namespace

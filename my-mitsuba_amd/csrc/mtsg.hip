@@ -141,6 +141,7 @@ int ensure_batch(mtsg_scene *s, uint32_t paths, int lanes) {
     A(n_ray_o, float4); A(n_ray_d, float4); A(n_T, float4); A(n_aux, float4); A(n_Lp, float4); A(n_meta, uint4);
     A(hit, float4); A(L, float4); A(sh_o, float4); A(sh_d, float4); A(sh_c, float4);
     if (s->ds.inst) { A(hitInst, uint32_t); } else P.hitInst = nullptr;
+    A(tie, uint32_t);
 #undef A
     if ((rc = alloc(CNT_WORDS * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
     if ((rc = alloc(CTR_WORDS * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
@@ -200,6 +201,13 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t
     else if (s->knobs && !COUNT) hipLaunchKernelGGL((k_trace_s<false, 16, false, true>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    // closest rays that met an exact tie: traced again with the mailbox
+    // (flat traversal only; a grid a quarter of the trace grid's)
+    if (MTSG_MAILBOX && !s->ds.inst && cIn != -2) {
+        const dim3 tg(std::max<unsigned>(1u, (unsigned)s->traceGrid / 4u));
+        if (s->knobs) hipLaunchKernelGGL((k_tie<true>), tg, blk, 0, st, s->ds, P);
+        else hipLaunchKernelGGL((k_tie<false>), tg, blk, 0, st, s->ds, P);
+    }
 }
 void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn, uint32_t n, hipStream_t st) {
     if (count) launch_trace_c<true>(s, P, cIn, sIn, n, st);
@@ -761,8 +769,8 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
                     if (ta.prim_index >= d->n_instances) { layoutOk = false; break; }
                     ta.k = KINST;
                 }
-                // the traversal keys Mitsuba's mailbox on the TriAccel index
-                // (kernels.h mailbox_step), not the shape index
+                // the TriAccel index (Mitsuba's mailbox key, kernels.h
+                // mailbox_step) in place of the shape index
                 ta.shape_index = p;
                 const float4 *t = (const float4 *)&ta;
                 triL.push_back(t[0]); triL.push_back(t[1]); triL.push_back(t[2]);
@@ -1256,6 +1264,7 @@ static int trace_rays(mtsg_scene *s, uint32_t n, const float *rays, float *t, fl
     if (e == hipSuccess) e = alloc((void **)po, f4, out.data());
     if (e == hipSuccess && shadow) e = alloc((void **)&D.sh_c, f4, c.data());
     if (e == hipSuccess && s->ds.inst) e = alloc((void **)&D.hitInst, (size_t)n * sizeof(uint32_t), nullptr);
+    if (e == hipSuccess && !shadow) e = alloc((void **)&D.tie, (size_t)n * sizeof(uint32_t), nullptr);
     if (e == hipSuccess) e = alloc((void **)&D.cnt, CNT_WORDS * sizeof(uint32_t), nullptr);
     if (e == hipSuccess) e = alloc((void **)&D.ctr, CTR_WORDS * sizeof(unsigned long long), nullptr);
     if (e == hipSuccess && shadow) e = hipMemcpy(D.cnt + CNT_S0, &n, sizeof(uint32_t), hipMemcpyHostToDevice);
