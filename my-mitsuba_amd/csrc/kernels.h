@@ -881,7 +881,10 @@ DEV void tie_retrace(const DevScene &S, SpecRay &r, SpecStack stk, const float4 
 #ifndef MTSG_SAVE_RAY
 #define MTSG_SAVE_RAY 1
 #endif
-constexpr int SAVE_VECS = MTSG_SAVE_RAY ? 4 : 2;
+#ifndef MTSG_SAVE_INV
+#define MTSG_SAVE_INV 0   // variant: the reciprocal direction saved too (no divisions on exit; 2% slower, r03)
+#endif
+constexpr int SAVE_VECS = MTSG_SAVE_RAY ? (MTSG_SAVE_INV ? 5 : 4) : 2;
 // the two levels' stacks in one LDS array: top level in entries
 // [0, OUTER_STACK), group level in [OUTER_STACK, OUTER_STACK + INNER_STACK)
 __shared__ uint2 s_lvNode[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
@@ -937,7 +940,15 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
 #endif
     r.o = xyz(ro);
     r.d = xyz(rd);
+#if MTSG_SAVE_RAY && MTSG_SAVE_INV
+    // the world reciprocal direction as saved: a wave runs this block whenever
+    // any of its lanes leaves an instance, so its three IEEE divisions were
+    // paid on most iterations
+    const uint4 g = save_vec(S, 4);
+    r.inv = mk3(__uint_as_float(e.z), __uint_as_float(e.w), __uint_as_float(g.x));
+#else
     r.inv = mk3(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
+#endif
 }
 
 template <bool COUNT>
@@ -1025,7 +1036,12 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
             save_vec(S, 1) = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
 #if MTSG_SAVE_RAY
             save_vec(S, 2) = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(d.x));
+#if MTSG_SAVE_INV
+            save_vec(S, 3) = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), __float_as_uint(r.inv.x), __float_as_uint(r.inv.y));
+            save_vec(S, 4) = make_uint4(__float_as_uint(r.inv.z), 0u, 0u, 0u);
+#else
             save_vec(S, 3) = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), 0u, 0u);
+#endif
 #endif
             inst = ii;
             const uint2 root = make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w));
