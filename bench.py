@@ -210,9 +210,16 @@ def cpu_baseline(scene, params, border, target_s):
     }
 
 
+def _share(params, stride, offset):
+    p = params.copy()
+    if stride > 1:
+        p.tile_stride, p.tile_offset = stride, offset
+    return p
+
+
 def parity_at_headline(scene, gpu, params, border, stride):
     """Per-pixel L1 of the GPU frame vs the CPU oracle at the full spp: the
-    tile share t % stride == 0 (1/stride of the 16x16 tiles, every pixel of
+    tile share key % stride == 0 (1/stride of the 16x16 tiles, every pixel of
     them, all samples) rendered by both in counter mode (identical random
     numbers per pixel / sample / dimension), developed (sum w L / sum w) and
     compared on the pixels of those tiles.  Runs after the timed region."""
@@ -229,9 +236,7 @@ def parity_at_headline(scene, gpu, params, border, stride):
     b = border
     rgb_g = mtsg.develop(img_g[b:b + p.tile_h, b:b + p.tile_w])
     rgb_c = mtsg.develop(img_c[b:b + p.tile_h, b:b + p.tile_w])
-    ty, tx = np.meshgrid(np.arange(p.tile_h) // 16, np.arange(p.tile_w) // 16, indexing="ij")
-    tiles_x = (p.tile_w + 15) // 16
-    own = ((ty * tiles_x + tx) % stride) == 0
+    own = (mtsg.tile_deal_keys(p.tile_w, p.tile_h) % stride) == 0
     d = np.abs(rgb_g - rgb_c)[own]
     l1 = float(d.mean())
     mean = float(rgb_c[own].mean())
@@ -242,7 +247,7 @@ def parity_at_headline(scene, gpu, params, border, stride):
             "frac_over_1e-3": float((px > 1e-3).mean()), "frac_over_1e-3_of_mean": float((px > 1e-3 * mean).mean())}
     return {"l1": l1, "mean": round(mean, 6), "l1_rel_mean": l1 / max(mean, 1e-12),
             "max_abs": float(d.max()), "per_pixel": dist, "pixels": int(own.sum()), "spp": int(p.spp),
-            "samples": int(st.samples), "tiles": f"16x16 tiles t % {stride} == 0 of {p.tile_w}x{p.tile_h}",
+            "samples": int(st.samples), "tiles": f"16x16 tiles with deal key % {stride} == 0 of {p.tile_w}x{p.tile_h}",
             "bar": "l1 < 1e-3 (and l1_rel_mean < 1e-3)", "pass": bool(l1 < 1e-3 and l1 < 1e-3 * max(mean, 1e-12)),
             "rng": "counter mode on both sides", "oracle_seconds": round(t_cpu, 1), "gpu_seconds": round(t_gpu, 2)}
 
@@ -285,7 +290,28 @@ def main():
     film = gpu.alloc(nbytes)
     host_block = np.zeros((H, W, 5), np.float32)
 
+    # a rank whose share is a fraction of the tiles returns its tiles' own
+    # ImageBlocks (mtsg_render_device_tiles: 16 + 2b square windows, the
+    # per-block ImageBlocks of BlockedRenderProcess) instead of a block of the
+    # whole frame: 3.6 MB instead of 18.7 MB over PCIe per 1/8 C3 share.  The
+    # host puts them into the frame's block after the timed region.
+    def windows_for(p):
+        n, w = gpu.tile_windows(p)
+        return (n, w) if p.tile_stride > 1 and n * w * w < W * H else None
+    cand = ([_share(params, a.emulate_ranks, o) for o in range(a.emulate_ranks)]
+            if a.emulate_ranks > 1 and world == 1 else [params])
+    win_max = max(((windows_for(pp) or (0, 0))[0] for pp in cand), default=0)
+    wbuf = gpu.alloc(win_max * (16 + 2 * border) ** 2 * 5 * 4) if win_max else None
+    host_win = np.zeros((max(1, win_max), 16 + 2 * border, 16 + 2 * border, 5), np.float32)
+
     def step():
+        nw = windows_for(params)
+        if nw:
+            wbytes = nw[0] * nw[1] * nw[1] * 5 * 4
+            mtsg.device_lib().mtsg_device_memset(gpu._h, wbuf, wbytes)
+            gpu.render_device_tiles(params, wbuf)
+            mtsg.device_lib().mtsg_device_to_host(gpu._h, host_win.ctypes.data, wbuf, wbytes)
+            return
         mtsg.device_lib().mtsg_device_memset(gpu._h, film, nbytes)
         gpu.render_device(params, film)
         mtsg.device_lib().mtsg_device_to_host(gpu._h, host_block.ctypes.data, film, nbytes)
@@ -431,6 +457,11 @@ def main():
                     "instance_visits_per_ray": round(per(cs.instance_visits + cs.shadow_instance_visits,
                                                          cs.rays_closest + cs.rays_shadow), 3)}
         if a.save:
+            nw = windows_for(params)
+            if nw:   # the host-side gather of this rank's tile windows
+                host_block[:] = 0
+                mtsg.put_tile_windows(host_block, host_win[:nw[0]], params.tile_w, params.tile_h, border,
+                                      params.tile_stride, params.tile_offset)
             img = mtsg.develop(host_block[border:H - border, border:W - border])
             np.save(a.save, img)
 
@@ -442,6 +473,8 @@ def main():
         cpu = cpu_baseline(scene, params, border, a.cpu_seconds)
 
     gpu.free(film)
+    if wbuf is not None:
+        gpu.free(wbuf)
     gpu.close()
     if rank == 0:
         out = {

@@ -407,9 +407,12 @@ typedef struct mtsg_render_params {
     /* pixel rectangle (film coordinates, inside the crop window) whose
      * samples are generated by this call */
     int32_t tile_x, tile_y, tile_w, tile_h;
-    /* multi-GPU film tiling: the rectangle is cut into 16x16 splat tiles in
-     * row-major order and this call renders tiles t with
-     * t % tile_stride == tile_offset (tile_stride 0 or 1 = all tiles).  The
+    /* multi-GPU film tiling: the rectangle is cut into a grid of 16x16 splat
+     * tiles, tiles_x per row; tile (tx, ty) has the deal key
+     * ty * tiles_x + (tx - ty) mod tiles_x (each row rotated by its index, so
+     * N ranks get diagonal, not column, stripes) and this call renders the
+     * tiles with key % tile_stride == tile_offset (tile_stride 0 or 1 = all
+     * tiles).  The
      * output block always covers the whole rectangle + border; blocks of
      * different offsets are merged by addition (imageblock.h:103-107). */
     int32_t tile_stride, tile_offset;
@@ -502,6 +505,24 @@ int  mtsg_render(mtsg_scene *scene, const mtsg_render_params *params,
  * to the host.  Used by the benchmark (inputs and outputs stay in HBM). */
 int  mtsg_render_device(mtsg_scene *scene, const mtsg_render_params *params,
                         float *rgbaw_device);
+
+/* Per-tile ImageBlocks (the multi-GPU gather): instead of one block of the
+ * whole rectangle, the call's tiles each get their own window of
+ * window x window x 5 floats (window = 16 + 2*border: the tile plus its
+ * filter border), window v holding the tile of deal key
+ * tile_offset + v * tile_stride (see tile_stride above).  These are the
+ * per-block ImageBlocks of BlockedRenderProcess (renderproc.cpp:41-50) that
+ * ImageBlock::put(const ImageBlock *) adds into the film
+ * (imageblock.h:103-107); texels outside the rectangle's block stay zero.
+ * A rank copies ntiles * window^2 * 5 floats to the host instead of the
+ * whole block (1/N of the tiles: 3.6 MB instead of 18.7 MB per 1/8 C3
+ * share).  mtsg_tile_windows gives ntiles and window for params;
+ * mtsg_render_device_tiles accumulates into a zeroed device buffer of that
+ * size. */
+int  mtsg_tile_windows(mtsg_scene *scene, const mtsg_render_params *params,
+                       uint32_t *ntiles, int32_t *window);
+int  mtsg_render_device_tiles(mtsg_scene *scene, const mtsg_render_params *params,
+                              float *windows_device);
 
 /* Device buffer helpers for mtsg_render_device (plain hipMalloc/hipMemcpy). */
 int  mtsg_device_alloc(mtsg_scene *scene, size_t bytes, void **out);

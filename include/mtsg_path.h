@@ -5,7 +5,8 @@
  * Replaces SamplingIntegrator::render (reference src/librender/integrator.cpp:99-133)
  * together with BlockedRenderProcess (src/librender/renderproc.cpp:26-186):
  * instead of 32x32 blocks handed to CPU workers, the film's 16x16 tiles are
- * dealt round-robin to one host thread per GPU (tile t -> GPU t % N), each
+ * dealt round-robin by deal key (include/mtsg.h, tile_stride) to one host
+ * thread per GPU (key k -> GPU k % N), each
  * GPU renders its tiles into an ImageBlock of the full rectangle plus filter
  * border, and the blocks are merged by addition as ImageBlock::put(const
  * ImageBlock *) does (include/mitsuba/render/imageblock.h:103-107).  No
@@ -41,7 +42,8 @@ int mtsh_path_job_gpus(const mtsh_path_job *job);
 /* Render params->tile_* into rgbaw_out ((tile_h + 2b) x (tile_w + 2b) x 5
  * floats, b = border).  The rectangle's 16x16 tiles selected by
  * params->tile_stride / tile_offset (all tiles when stride <= 1) are dealt
- * over the job's N GPUs: GPU g renders tiles offset + (g + k N) stride.
+ * over the job's N GPUs: GPU g renders the tiles of deal keys
+ * offset + (g + k N) stride.
  * seconds_out (optional) receives the render time.  Blocking; returns an mtsg
  * error code (MTSG_ERR_CANCELLED after mtsh_path_job_cancel). */
 int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, float *rgbaw_out,

@@ -103,10 +103,23 @@ struct DevBatch {
     int rect_x, rect_y, rect_w, rect_h;   // render rectangle (film coords)
     int tiles_x;                          // tiles per row of the rectangle
     int tile0, ntiles;                    // virtual tile range of this batch
-    int tstride, toffset;                 // global tile = toffset + virtual * tstride
+    int tstride, toffset;                 // deal key = toffset + virtual * tstride (tile_of_key)
     uint32_t s0, ns;
     uint32_t nslots;
 };
+
+// Multi-GPU tile deal (mtsg_render_params.tile_stride / tile_offset): tile
+// (tx, ty) of the rectangle's tile grid has the deal key ty * tiles_x +
+// (tx - ty) mod tiles_x, and a call renders the tiles whose key % stride ==
+// offset.  Rotating row ty by ty tiles turns the column stripes that a plain
+// row-major deal gives when the stride divides tiles_x (C3: 80 tiles per row,
+// 2/4/8 ranks) into diagonal stripes, so every rank's share samples every
+// column of the frame: the eight 1/8 C3 shares were 22.1-23.2 ms apart as
+// columns (round 3, profiles/r03_bench_c4_e8.json).
+__host__ __device__ inline void tile_of_key(int key, int tiles_x, int &tx, int &ty) {
+    ty = key / tiles_x;
+    tx = (key % tiles_x + ty % tiles_x) % tiles_x;
+}
 
 // Path state.  The paths of a bounce are stored densely by their position in
 // that bounce's work list (the camera's slot order at bounce 0, then the order
@@ -1253,8 +1266,8 @@ DEV void slot_pixel(const DevBatch &B, uint32_t slot, int &x, int &y, uint32_t &
     const uint32_t rest = slot >> 8;
     const uint32_t sl = rest % B.ns;
     const uint32_t tl = rest / B.ns;
-    const int tile = B.toffset + (B.tile0 + (int)tl) * B.tstride;
-    const int tx = tile % B.tiles_x, ty = tile / B.tiles_x;
+    int tx, ty;
+    tile_of_key(B.toffset + (B.tile0 + (int)tl) * B.tstride, B.tiles_x, tx, ty);
     x = B.rect_x + tx * TILE + (int)(pix % TILE);
     y = B.rect_y + ty * TILE + (int)(pix / TILE);
     s = B.s0 + sl;
@@ -2884,14 +2897,17 @@ constexpr int SPLAT_CHUNK = 16;             // samples per pixel per workgroup
 // phase shifts every window by the same offset, so no two threads touch the
 // same texel: no atomics, fixed order) and flushes the tile with one float
 // atomic per texel and channel into the HBM ImageBlock.
+// winSz > 0: film holds one winSz x winSz window (the tile and its border) per tile of
+// the call, window v = virtual tile v (mtsg_render_device_tiles)
 template <int K, int CH>
-__global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P, float *film, int blockW, int blockH) {
+__global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P, float *film, int blockW, int blockH,
+                                                 int winSz) {
     __shared__ float acc[CH][LT * LT];
     constexpr int R = K / 2;
     for (int k = threadIdx.x; k < CH * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
     const int tl = blockIdx.x;
-    const int tile = B.toffset + (B.tile0 + tl) * B.tstride;
-    const int tx = tile % B.tiles_x, ty = tile / B.tiles_x;
+    int tx, ty;
+    tile_of_key(B.toffset + (B.tile0 + tl) * B.tstride, B.tiles_x, tx, ty);
     const int x0 = B.rect_x + tx * TILE, y0 = B.rect_y + ty * TILE;   // tile origin (film coords)
     const int bord = C.border;
     const int pix = threadIdx.x;
@@ -2971,7 +2987,10 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
         if (fx < 0 || fy < 0 || fx >= blockW || fy >= blockH) continue;
         const float w = acc[CH - 1][k];
         if (w == 0.0f) continue;
-        float *dst = film + ((size_t)fy * blockW + fx) * 5;
+        // window texel (the filter's support ends at the border: outside it w == 0)
+        const int wx = tx2 - (MAX_BORDER - bord), wy = ty2 - (MAX_BORDER - bord);
+        if (winSz && (wx < 0 || wy < 0 || wx >= winSz || wy >= winSz)) continue;
+        float *dst = winSz ? film + (((size_t)(B.tile0 + tl) * winSz + wy) * winSz + wx) * 5 : film + ((size_t)fy * blockW + fx) * 5;
         unsafeAtomicAdd(dst + 0, acc[0][k]);
         unsafeAtomicAdd(dst + 1, acc[1][k]);
         unsafeAtomicAdd(dst + 2, acc[2][k]);

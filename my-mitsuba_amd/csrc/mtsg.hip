@@ -354,7 +354,9 @@ int validate(const mtsg_render_params *p, const mtsg_scene *s) {
     return MTSG_OK;
 }
 
-int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
+// win = 0: film is the ImageBlock of the whole rectangle + border; win > 0:
+// film holds one win x win window per tile of this call (mtsg_render_device_tiles)
+int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win = 0) {
     int rc;
     if ((rc = validate(p, s)) != MTSG_OK) return rc;
     if ((rc = set_device(s)) != MTSG_OK) return rc;
@@ -555,12 +557,12 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             timed_launch(s, K_SPLAT, st, [&]() {
                 dim3 g(B.ntiles, (B.ns + SPLAT_CHUNK - 1) / SPLAT_CHUNK);
                 const int K = 2 * s->cam.border + 1;
-                if (K == 5 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<5, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
-                else if (K == 5) hipLaunchKernelGGL((k_splat<5, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
-                else if (K <= 3 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<3, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
-                else if (K <= 3) hipLaunchKernelGGL((k_splat<3, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
-                else if (!s->cam.has_alpha) hipLaunchKernelGGL((k_splat<9, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
-                else hipLaunchKernelGGL((k_splat<9, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH);
+                if (K == 5 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<5, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH, win);
+                else if (K == 5) hipLaunchKernelGGL((k_splat<5, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH, win);
+                else if (K <= 3 && !s->cam.has_alpha) hipLaunchKernelGGL((k_splat<3, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH, win);
+                else if (K <= 3) hipLaunchKernelGGL((k_splat<3, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH, win);
+                else if (!s->cam.has_alpha) hipLaunchKernelGGL((k_splat<9, 4>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH, win);
+                else hipLaunchKernelGGL((k_splat<9, 5>), g, dim3(BLOCK), 0, st, s->cam, I, B, P, film, blockW, blockH, win);
             });
             s->stats.samples += (uint64_t)B.nslots;
         }
@@ -589,8 +591,9 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film) {
             for (uint32_t slot = 0; slot < B.nslots; ++slot) {
                 const uint32_t pix = slot & (TILE * TILE - 1), rest = slot >> 8;
                 const uint32_t sl = rest % B.ns, tl = rest / B.ns;
-                const int tile = B.toffset + (B.tile0 + (int)tl) * B.tstride;
-                const int x = (tile % B.tiles_x) * TILE + (int)(pix % TILE), y = (tile / B.tiles_x) * TILE + (int)(pix / TILE);
+                int tx, ty;
+                tile_of_key(B.toffset + (B.tile0 + (int)tl) * B.tstride, B.tiles_x, tx, ty);
+                const int x = tx * TILE + (int)(pix % TILE), y = ty * TILE + (int)(pix / TILE);
                 if (x >= p->tile_w || y >= p->tile_h) continue;
                 float *o = s->dumpL + (((size_t)y * p->tile_w + x) * p->spp + B.s0 + sl) * 4;
                 o[0] = L[slot].x; o[1] = L[slot].y; o[2] = L[slot].z; o[3] = L[slot].w;
@@ -1189,6 +1192,27 @@ int mtsg_device_to_host(mtsg_scene *s, void *dst, const void *src, size_t bytes)
 int mtsg_render_device(mtsg_scene *s, const mtsg_render_params *p, float *film) {
     if (!s || !film) { g_err = "null argument"; return MTSG_ERR_INVALID; }
     return render_impl(s, p, film);
+}
+
+static uint32_t tile_count(const mtsg_render_params *p) {
+    const uint32_t allTiles = (uint32_t)((p->tile_w + TILE - 1) / TILE) * (uint32_t)((p->tile_h + TILE - 1) / TILE);
+    const uint32_t tstride = p->tile_stride > 1 ? (uint32_t)p->tile_stride : 1u;
+    const uint32_t toffset = p->tile_stride > 1 ? (uint32_t)p->tile_offset : 0u;
+    return toffset < allTiles ? (allTiles - toffset + tstride - 1) / tstride : 0u;
+}
+
+int mtsg_tile_windows(mtsg_scene *s, const mtsg_render_params *p, uint32_t *ntiles, int32_t *window) {
+    if (!s || !ntiles || !window) { g_err = "null argument"; return MTSG_ERR_INVALID; }
+    int rc;
+    if ((rc = validate(p, s)) != MTSG_OK) return rc;
+    *ntiles = tile_count(p);
+    *window = TILE + 2 * s->cam.border;
+    return MTSG_OK;
+}
+
+int mtsg_render_device_tiles(mtsg_scene *s, const mtsg_render_params *p, float *windows) {
+    if (!s || !windows) { g_err = "null argument"; return MTSG_ERR_INVALID; }
+    return render_impl(s, p, windows, TILE + 2 * s->cam.border);
 }
 
 int mtsg_render(mtsg_scene *s, const mtsg_render_params *p, float *rgbaw_out) {

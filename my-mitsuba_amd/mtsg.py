@@ -157,6 +157,7 @@ _dev = None
 
 DEVICE_SYMBOLS = [
     "mtsg_device_count", "mtsg_scene_create", "mtsg_render", "mtsg_render_device",
+    "mtsg_tile_windows", "mtsg_render_device_tiles",
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_cancel_clear", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
@@ -253,6 +254,9 @@ def device_lib() -> C.CDLL:
         lib.mtsg_scene_create.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         lib.mtsg_render.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
         lib.mtsg_render_device.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
+        lib.mtsg_tile_windows.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.POINTER(C.c_uint32),
+                                          C.POINTER(C.c_int32)]
+        lib.mtsg_render_device_tiles.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
         lib.mtsg_device_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
         lib.mtsg_device_free.argtypes = [C.c_void_p, C.c_void_p]
         lib.mtsg_device_memset.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
@@ -374,6 +378,37 @@ class Scene:
         if getattr(self, "_h", None):
             host_lib().mtsh_scene_free(self._h)
             self._h = None
+
+
+def tile_deal_keys(tile_w: int, tile_h: int) -> np.ndarray:
+    """Deal key of every pixel of a tile_w x tile_h rectangle (include/mtsg.h
+    mtsg_render_params.tile_stride): tile (tx, ty) has key ty * tiles_x +
+    (tx - ty) mod tiles_x, and a call with (stride, offset) renders the tiles
+    whose key % stride == offset."""
+    tiles_x = (tile_w + 15) // 16
+    ty, tx = np.meshgrid(np.arange(tile_h) // 16, np.arange(tile_w) // 16, indexing="ij")
+    return ty * tiles_x + (tx - ty) % tiles_x
+
+
+def put_tile_windows(block: np.ndarray, windows: np.ndarray, tile_w: int, tile_h: int, border: int,
+                     stride: int, offset: int) -> np.ndarray:
+    """Add per-tile ImageBlocks (mtsg_render_device_tiles: window v = the tile of
+    deal key offset + v * stride, window = 16 + 2 * border) into the block of the
+    whole rectangle + border, as ImageBlock::put(const ImageBlock *) does
+    (imageblock.h:103-107).  block: (tile_h + 2b, tile_w + 2b, 5)."""
+    tiles_x = (tile_w + 15) // 16
+    stride = max(1, stride)
+    offset = offset if stride > 1 else 0
+    win = windows.shape[1]
+    for v in range(windows.shape[0]):
+        key = offset + v * stride
+        ty = key // tiles_x
+        tx = (key % tiles_x + ty) % tiles_x
+        x0, y0 = 16 * tx, 16 * ty   # window origin in block coordinates (the tile origin minus the border)
+        h = min(win, block.shape[0] - y0)
+        w = min(win, block.shape[1] - x0)
+        block[y0:y0 + h, x0:x0 + w] += windows[v, :h, :w]
+    return block
 
 
 def develop(rgbaw: np.ndarray) -> np.ndarray:
@@ -557,6 +592,17 @@ class GPUScene:
 
     def render_device(self, params: RenderParams, film: C.c_void_p) -> None:
         self._check(device_lib().mtsg_render_device(self._h, C.byref(params), film), "mtsg_render_device")
+
+    def tile_windows(self, params: RenderParams):
+        """(ntiles, window) of params' per-tile ImageBlocks (mtsg_tile_windows)."""
+        n, w = C.c_uint32(0), C.c_int32(0)
+        self._check(device_lib().mtsg_tile_windows(self._h, C.byref(params), C.byref(n), C.byref(w)),
+                    "mtsg_tile_windows")
+        return n.value, w.value
+
+    def render_device_tiles(self, params: RenderParams, windows: C.c_void_p) -> None:
+        self._check(device_lib().mtsg_render_device_tiles(self._h, C.byref(params), windows),
+                    "mtsg_render_device_tiles")
 
     def download(self, film: C.c_void_p, shape) -> np.ndarray:
         out = np.zeros(shape, dtype=np.float32)

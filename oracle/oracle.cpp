@@ -2699,10 +2699,12 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
                     for (int x = bx0; x < bx0 + bw; ++x) {
                         // multi-GPU contract (mtsg_render_params.tile_stride): this
                         // call owns the 16x16 tiles t of the rectangle with
-                        // t % tile_stride == tile_offset
+                        // deal key % tile_stride == tile_offset, the key of tile
+                        // (tx, ty) being ty * tilesX + (tx - ty) mod tilesX
                         if (p->tile_stride > 1) {
-                            const int t = ((y - p->tile_y) / 16) * tilesX + (x - p->tile_x) / 16;
-                            if (t % p->tile_stride != p->tile_offset) continue;
+                            const int ty = (y - p->tile_y) / 16, tx = (x - p->tile_x) / 16;
+                            const int key = ty * tilesX + ((tx - ty % tilesX) % tilesX + tilesX) % tilesX;
+                            if (key % p->tile_stride != p->tile_offset) continue;
                         }
                         for (uint32_t s = 0; s < p->spp; ++s) {
                             smp.begin(&qmc, p->seed, cam.film_w, p->spp, x, y, s);

@@ -70,3 +70,27 @@ def test_scene_without_emitters_is_rejected(tmp_path):
     p.write_text(src[:start] + src[end:])
     with pytest.raises(RuntimeError, match="no emitters"):
         mtsg.Scene(str(p), {"width": 32, "height": 32, "spp": 4})
+
+
+@pytest.mark.parametrize("stride,offset,over", [(1, 0, {}), (3, 2, {}), (8, 5, {}),
+                                                (2, 1, dict(tile_x=5, tile_y=3, tile_w=41, tile_h=37))])
+def test_per_tile_image_blocks_sum_to_the_block(cbox_small, gpu, stride, offset, over):
+    # mtsg_render_device_tiles: one window (tile + filter border) per tile of
+    # the call; put into the rectangle's block they equal mtsg_render's block
+    # (up to the order of the float additions at the tile borders)
+    p = cbox_small.params(tile_stride=stride, tile_offset=offset, **over)
+    b = cbox_small.border
+    n, win = gpu.tile_windows(p)
+    tiles_x, tiles_y = (p.tile_w + 15) // 16, (p.tile_h + 15) // 16
+    assert win == 16 + 2 * b and n == len(range(offset if stride > 1 else 0, tiles_x * tiles_y, stride))
+    buf = gpu.alloc(max(1, n) * win * win * 5 * 4)
+    try:
+        gpu.render_device_tiles(p, buf)
+        windows = gpu.download(buf, (n, win, win, 5))
+    finally:
+        gpu.free(buf)
+    block = mtsg.put_tile_windows(np.zeros((p.tile_h + 2 * b, p.tile_w + 2 * b, 5), np.float32), windows,
+                                  p.tile_w, p.tile_h, b, stride, offset)
+    ref = gpu.render(p, b)
+    assert ref[..., 4].sum() > 0
+    np.testing.assert_allclose(block, ref, rtol=1e-5, atol=1e-6)

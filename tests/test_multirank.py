@@ -64,8 +64,13 @@ def test_two_rank_tile_sharding_sums_to_full_frame(tmp_path):
     full, st = O.render(scene.desc, p, scene.border, rng=O.RNG_COUNTER, threads=2)
     summed = np.load(tmp_path / "sum.npy")
     assert np.load(tmp_path / "max.npy")[0] == 2.0
-    # 72x40 -> 5x3 = 15 tiles; rank 0 owns tiles 0,2,..,14 (8 tiles, ragged last column)
-    own0 = sum(min(16, 72 - 16 * (t % 5)) * min(16, 40 - 16 * (t // 5)) for t in range(0, 15, 2))
+    # 72x40 -> 5x3 = 15 tiles (ragged last column and row); rank 0 owns the
+    # tiles of even deal key ty * 5 + (tx - ty) mod 5 (include/mtsg.h)
+    own0 = sum(min(16, 72 - 16 * tx) * min(16, 40 - 16 * ty) for ty in range(3) for tx in range(5)
+               if (ty * 5 + (tx - ty) % 5) % 2 == 0)
+    assert own0 != sum(min(16, 72 - 16 * (t % 5)) * min(16, 40 - 16 * (t // 5)) for t in range(0, 15, 2))
     assert np.load(tmp_path / "samples0.npy")[0] == own0 * 4
+    keys = mtsg.tile_deal_keys(72, 40)
+    assert keys[0, 16] == 1 and keys[16, 0] == 9 and keys[16, 16] == 5   # (tx, ty) = (1, 0), (0, 1), (1, 1)
     assert full[..., 4].sum() > 0
     np.testing.assert_allclose(summed, full, rtol=1e-5, atol=1e-6)
