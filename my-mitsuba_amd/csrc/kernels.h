@@ -104,6 +104,7 @@ struct DevBatch {
     int tiles_x;                          // tiles per row of the rectangle
     int tile0, ntiles;                    // virtual tile range of this batch
     int tstride, toffset;                 // deal key = toffset + virtual * tstride (tile_of_key)
+    int skew;                             // deal: row ty rotated by ty * skew tiles (1; MTSG_DEAL_SKEW measures others)
     uint32_t s0, ns;
     uint32_t nslots;
 };
@@ -116,9 +117,9 @@ struct DevBatch {
 // 2/4/8 ranks) into diagonal stripes, so every rank's share samples every
 // column of the frame: the eight 1/8 C3 shares were 22.1-23.2 ms apart as
 // columns (round 3, profiles/r03_bench_c4_e8.json).
-__host__ __device__ inline void tile_of_key(int key, int tiles_x, int &tx, int &ty) {
+__host__ __device__ inline void tile_of_key(int key, int tiles_x, int &tx, int &ty, int skew = 1) {
     ty = key / tiles_x;
-    tx = (key % tiles_x + ty % tiles_x) % tiles_x;
+    tx = (key % tiles_x + (ty * skew) % tiles_x) % tiles_x;
 }
 
 // Path state.  The paths of a bounce are stored densely by their position in
@@ -1267,7 +1268,7 @@ DEV void slot_pixel(const DevBatch &B, uint32_t slot, int &x, int &y, uint32_t &
     const uint32_t sl = rest % B.ns;
     const uint32_t tl = rest / B.ns;
     int tx, ty;
-    tile_of_key(B.toffset + (B.tile0 + (int)tl) * B.tstride, B.tiles_x, tx, ty);
+    tile_of_key(B.toffset + (B.tile0 + (int)tl) * B.tstride, B.tiles_x, tx, ty, B.skew);
     x = B.rect_x + tx * TILE + (int)(pix % TILE);
     y = B.rect_y + ty * TILE + (int)(pix / TILE);
     s = B.s0 + sl;
@@ -2907,7 +2908,7 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
     for (int k = threadIdx.x; k < CH * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
     const int tl = blockIdx.x;
     int tx, ty;
-    tile_of_key(B.toffset + (B.tile0 + tl) * B.tstride, B.tiles_x, tx, ty);
+    tile_of_key(B.toffset + (B.tile0 + tl) * B.tstride, B.tiles_x, tx, ty, B.skew);
     const int x0 = B.rect_x + tx * TILE, y0 = B.rect_y + ty * TILE;   // tile origin (film coords)
     const int bord = C.border;
     const int pix = threadIdx.x;

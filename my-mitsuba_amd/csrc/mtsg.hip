@@ -407,6 +407,10 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
     // the cancel flag is consumed (cleared) when a render returns, so a
     // cancel that races with the start of a render is not lost
     if (count) HIP_TRY(hipMemsetAsync(s->LP[0].ctr, 0, CTR_WORDS * sizeof(unsigned long long), s->stream));
+    // row rotation of the tile deal (include/mtsg.h); MTSG_DEAL_SKEW: other
+    // rotations for measurement only (the oracle and mtsg.py deal with 1)
+    int dealSkew = 1;
+    if (const char *k = getenv("MTSG_DEAL_SKEW")) dealSkew = std::max(0, atoi(k));
     // the batches of this call, tile-major
     std::vector<DevBatch> batches;
     for (uint32_t t0i = 0; t0i < ntiles; t0i += tilesPerBatch) {
@@ -414,6 +418,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
             DevBatch B;
             B.rect_x = p->tile_x; B.rect_y = p->tile_y; B.rect_w = p->tile_w; B.rect_h = p->tile_h;
             B.tiles_x = (int)tilesX;
+            B.skew = dealSkew;
             B.tile0 = (int)t0i;
             B.tstride = (int)tstride;
             B.toffset = (int)toffset;
@@ -592,7 +597,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
                 const uint32_t pix = slot & (TILE * TILE - 1), rest = slot >> 8;
                 const uint32_t sl = rest % B.ns, tl = rest / B.ns;
                 int tx, ty;
-                tile_of_key(B.toffset + (B.tile0 + (int)tl) * B.tstride, B.tiles_x, tx, ty);
+                tile_of_key(B.toffset + (B.tile0 + (int)tl) * B.tstride, B.tiles_x, tx, ty, B.skew);
                 const int x = tx * TILE + (int)(pix % TILE), y = ty * TILE + (int)(pix / TILE);
                 if (x >= p->tile_w || y >= p->tile_h) continue;
                 float *o = s->dumpL + (((size_t)y * p->tile_w + x) * p->spp + B.s0 + sl) * 4;
