@@ -135,7 +135,7 @@ DEV float sobol_sample(const DevSampler &S, uint64_t index, uint32_t dim) {
     uint32_t result = (uint32_t)S.sobolScramble;
     const uint32_t *col = S.sobolM + dim * MTSG_SOBOL_COLUMNS;
     uint32_t lo = (uint32_t)index, hi = (uint32_t)(index >> 32);
-    for (uint32_t i = 0; lo; lo &= lo - 1u) result ^= col[__builtin_ctz(lo)];
+    for (; lo; lo &= lo - 1u) result ^= col[__builtin_ctz(lo)];
     for (; hi; hi &= hi - 1u) result ^= col[32 + __builtin_ctz(hi)];
     return fminf((float)result * (1.0f / 4294967296.0f), kOneMinusEps);
 }
