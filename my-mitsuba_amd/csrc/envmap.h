@@ -28,7 +28,7 @@ DEV float3 env_rot(const float *m, float3 v) {
 // rays carrying (scaled) differentials -> EWA, otherwise bilinear level 0
 DEV float3 env_eval(const DevEnv &V, float3 dWorld, bool hasDiff, float3 rxD, float3 ryD) {
     const float3 v = env_rot(V.E->to_local, dWorld);
-    const float ux = atan2f(v.x, -v.z) * kInvTwoPi, uy = acosf(fminf(1.0f, fmaxf(-1.0f, v.y))) * kInvPi;
+    const float ux = mt_atan2f(v.x, -v.z) * kInvTwoPi, uy = mt_acosf(fminf(1.0f, fmaxf(-1.0f, v.y))) * kInvPi;
     float3 value;
     if (!hasDiff) {
         value = mip_bilinear(env_mip(V), 0, ux, uy);
@@ -78,8 +78,8 @@ DEV void env_internal_sample(const DevEnv &V, float sx, float sy, float3 &d, flo
     pdf = (env_lum(value1) * V.rowWeights[min(max(yPos, 0), H - 1)] +
            env_lum(value2) * V.rowWeights[min(max(yPos + 1, 0), H - 1)]) * V.E->normalization;
     float sinPhi, cosPhi, sinTheta, cosTheta;
-    sincosf(V.E->pixel_size[0] * (px + 0.5f), &sinPhi, &cosPhi);
-    sincosf(V.E->pixel_size[1] * (py + 0.5f), &sinTheta, &cosTheta);
+    mt_sincosf(V.E->pixel_size[0] * (px + 0.5f), &sinPhi, &cosPhi);
+    mt_sincosf(V.E->pixel_size[1] * (py + 0.5f), &sinTheta, &cosTheta);
     d = mk3(sinPhi * sinTheta, cosTheta, -cosPhi * sinTheta);
     pdf /= fmaxf(fabsf(sinTheta), kEpsilon);
 }
@@ -88,7 +88,7 @@ DEV void env_internal_sample(const DevEnv &V, float sx, float sy, float3 &d, flo
 DEV float env_internal_pdf(const DevEnv &V, float3 d) {
     const int W = V.E->mip.level_w[0], H = V.E->mip.level_h[0];
     const DevMip M = env_mip(V);
-    const float ux = atan2f(d.x, -d.z) * kInvTwoPi, uy = acosf(fminf(1.0f, fmaxf(-1.0f, d.y))) * kInvPi;
+    const float ux = mt_atan2f(d.x, -d.z) * kInvTwoPi, uy = mt_acosf(fminf(1.0f, fmaxf(-1.0f, d.y))) * kInvPi;
     if (!isfinite(ux) || !isfinite(uy)) return 0.0f;
     const float u = ux * W - 0.5f, v = uy * H - 0.5f;
     const int xPos = (int)floorf(u), yPos = (int)floorf(v);

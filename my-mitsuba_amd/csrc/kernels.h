@@ -1343,7 +1343,7 @@ DEV float3 cosine_hemisphere(float sx, float sy) {
     else if (r1 * r1 > r2 * r2) { r = r1; phi = (kPi / 4.0f) * (r2 / r1); }
     else { r = r2; phi = (kPi / 2.0f) - (r1 / r2) * (kPi / 4.0f); }
     float sinPhi, cosPhi;
-    sincosf(phi, &sinPhi, &cosPhi);
+    mt_sincosf(phi, &sinPhi, &cosPhi);
     float px = r * cosPhi, py = r * sinPhi;
     float z = sqrtf(fmaxf(0.0f, 1.0f - px * px - py * py));
     if (z == 0) z = 1e-10f;
@@ -1352,7 +1352,7 @@ DEV float3 cosine_hemisphere(float sx, float sy) {
 
 // math.cpp:25-70
 DEV float erfinv_m(float x) {
-    float w = -logf((1.0f - x) * (1.0f + x));
+    float w = -mt_logf((1.0f - x) * (1.0f + x));
     float p;
     if (w < 5.0f) {
         w = w - 2.5f;
@@ -1385,7 +1385,7 @@ DEV float erf_m(float x) {
     float sign = copysignf(1.0f, x);
     x = fabsf(x);
     float t = 1.0f / (1.0f + p * x);
-    float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * expf(-x * x);
+    float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * mt_expf(-x * x);
     return sign * y;
 }
 DEV float hypot2_m(float a, float b) {   // math.cpp:74-86
@@ -1423,9 +1423,9 @@ struct MF {
         float ct2 = m.z * m.z;
         float be = ((m.x * m.x) / (au * au) + (m.y * m.y) / (av * av)) / ct2;
         float result;
-        if (type == MTSG_MF_BECKMANN) result = expf(-be) / (kPi * au * av * ct2 * ct2);
+        if (type == MTSG_MF_BECKMANN) result = mt_expf(-be) / (kPi * au * av * ct2 * ct2);
         else if (type == MTSG_MF_GGX) { float root = (1.0f + be) * ct2; result = 1.0f / (kPi * au * av * root * root); }
-        else result = sqrtf((eu + 2) * (ev + 2)) * (0.5f * kInvPi) * powf(m.z, phong_exponent(m));
+        else result = sqrtf((eu + 2) * (ev + 2)) * (0.5f * kInvPi) * mt_powf(m.z, phong_exponent(m));
         if (result * m.z < 1e-20f) result = 0;
         return result;
     }
@@ -1448,23 +1448,23 @@ struct MF {
         if (type == MTSG_MF_BECKMANN) {
             const float SQRT_PI_INV = 0.56418958354775628695f;
             if (thetaI < 1e-4f) {
-                float r = sqrtf(-logf(1.0f - sx));
+                float r = sqrtf(-mt_logf(1.0f - sx));
                 float sp, cp;
-                sincosf(2 * kPi * sy, &sp, &cp);
+                mt_sincosf(2 * kPi * sy, &sp, &cp);
                 slx = r * cp; sly = r * sp;
                 return;
             }
-            float tanThetaI = tanf(thetaI), cotThetaI = 1 / tanThetaI;
+            float tanThetaI = mt_tanf(thetaI), cotThetaI = 1 / tanThetaI;
             float aa = -1, c = erf_m(cotThetaI);
             float sample_x = fmaxf(sx, 1e-6f);
             float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
-            float b = c - (1 + c) * powf(1 - sample_x, fit);
-            float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * expf(-cotThetaI * cotThetaI));
+            float b = c - (1 + c) * mt_powf(1 - sample_x, fit);
+            float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * mt_expf(-cotThetaI * cotThetaI));
             int it = 0;
             while (++it < 10) {
                 if (!(b >= aa && b <= c)) b = 0.5f * (aa + c);
                 float invErf = erfinv_m(b);
-                float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * expf(-invErf * invErf)) - sample_x;
+                float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * mt_expf(-invErf * invErf)) - sample_x;
                 float derivative = normalization * (1 - invErf * tanThetaI);
                 if (fabsf(value) < 1e-5f) break;
                 if (value > 0) c = b; else aa = b;
@@ -1477,11 +1477,11 @@ struct MF {
         if (thetaI < 1e-4f) {
             float r = sqrtf(fmaxf(0.0f, sx / (1 - sx)));
             float sp, cp;
-            sincosf(2 * kPi * sy, &sp, &cp);
+            mt_sincosf(2 * kPi * sy, &sp, &cp);
             slx = r * cp; sly = r * sp;
             return;
         }
-        float tanThetaI = tanf(thetaI);
+        float tanThetaI = mt_tanf(thetaI);
         float aa = 1 / tanThetaI;
         float G1v = 2.0f / (1.0f + sqrtf(fmaxf(0.0f, 1.0f + 1.0f / (aa * aa))));
         float A = 2.0f * sx / G1v - 1.0f;
@@ -1503,9 +1503,9 @@ struct MF {
         if (visible) {
             float3 wi = normalize(mk3(au * wi_.x, av * wi_.y, wi_.z));
             float theta = 0, phi = 0;
-            if (wi.z < 0.99999f) { theta = acosf(wi.z); phi = atan2f(wi.y, wi.x); }
+            if (wi.z < 0.99999f) { theta = mt_acosf(wi.z); phi = mt_atan2f(wi.y, wi.x); }
             float sinPhi, cosPhi;
-            sincosf(phi, &sinPhi, &cosPhi);
+            mt_sincosf(phi, &sinPhi, &cosPhi);
             float slx, sly;
             visible11(theta, sx, sy, slx, sly);
             float rx = cosPhi * slx - sinPhi * sly, ry = sinPhi * slx + cosPhi * sly;
@@ -1533,22 +1533,22 @@ struct MF {
                 phong_quadrant(4 * (1 - sy), phiM, exponent);
                 phiM = 2 * kPi - phiM;
             }
-            sincosf(phiM, &sinPhiM, &cosPhiM);
-            cosThetaM = powf(sx, 1.0f / (exponent + 2.0f));
-            pdf = sqrtf((eu + 2.0f) * (ev + 2.0f)) * (0.5f * kInvPi) * powf(cosThetaM, exponent + 1.0f);
+            mt_sincosf(phiM, &sinPhiM, &cosPhiM);
+            cosThetaM = mt_powf(sx, 1.0f / (exponent + 2.0f));
+            pdf = sqrtf((eu + 2.0f) * (ev + 2.0f)) * (0.5f * kInvPi) * mt_powf(cosThetaM, exponent + 1.0f);
         } else {
             float alphaSqr;
             if (iso()) {
-                sincosf((2.0f * kPi) * sy, &sinPhiM, &cosPhiM);
+                mt_sincosf((2.0f * kPi) * sy, &sinPhiM, &cosPhiM);
                 alphaSqr = au * au;
             } else {
-                const float phiM = atanf(av / au * tanf(kPi + 2 * kPi * sy)) + kPi * floorf(2 * sy + 0.5f);
-                sincosf(phiM, &sinPhiM, &cosPhiM);
+                const float phiM = mt_atanf(av / au * mt_tanf(kPi + 2 * kPi * sy)) + kPi * floorf(2 * sy + 0.5f);
+                mt_sincosf(phiM, &sinPhiM, &cosPhiM);
                 const float cosSc = cosPhiM / au, sinSc = sinPhiM / av;
                 alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
             }
             if (type == MTSG_MF_BECKMANN) {
-                float t2 = alphaSqr * -logf(1.0f - sx);
+                float t2 = alphaSqr * -mt_logf(1.0f - sx);
                 cosThetaM = 1.0f / sqrtf(1.0f + t2);
                 pdf = (1.0f - sx) / (kPi * au * av * cosThetaM * cosThetaM * cosThetaM);
             } else {
@@ -1578,9 +1578,9 @@ struct MF {
     }
     // sampleFirstQuadrant (microfacet.h:707-715)
     DEV void phong_quadrant(float u1, float &phi, float &exponent) const {
-        phi = atanf(sqrtf((eu + 2.0f) / (ev + 2.0f)) * tanf(kPi * u1 * 0.5f));
+        phi = mt_atanf(sqrtf((eu + 2.0f) / (ev + 2.0f)) * mt_tanf(kPi * u1 * 0.5f));
         float sinPhi, cosPhi;
-        sincosf(phi, &sinPhi, &cosPhi);
+        mt_sincosf(phi, &sinPhi, &cosPhi);
         exponent = eu * cosPhi * cosPhi + ev * sinPhi * sinPhi;
     }
 };
@@ -1654,7 +1654,7 @@ DEV float cubic_interp1d(float x, const float *v, int n) {
 // RoughTransmittance::eval with eta and alpha fixed (rtrans.h:169-181, 205-206)
 DEV float rough_trans(const mtsg_bsdf &b, float cosTheta) {
     if (!(cosTheta >= 0)) return 0.0f;
-    const float r = cubic_interp1d(powf(fabsf(cosTheta), 0.25f), b.rtrans, MTSG_RTRANS_SAMPLES);
+    const float r = cubic_interp1d(mt_powf(fabsf(cosTheta), 0.25f), b.rtrans, MTSG_RTRANS_SAMPLES);
     return fminf(1.0f, fmaxf(0.0f, r));
 }
 
@@ -2391,7 +2391,7 @@ DEV int om_index(float3 &d) {
     if (d.z < 0) d = -d;
     const double PI = 3.14159265358979323846;
     const float r = sqrtf(1 - d.z);
-    float phi = atan2f(d.y, d.x);
+    float phi = mt_atan2f(d.y, d.x);
     float u = 0, v = 0;
     if (r != 0) {
         float a, b;

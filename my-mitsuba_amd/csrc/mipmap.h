@@ -100,7 +100,7 @@ DEV float hypot2_m(float a, float b) {   // math.cpp:74-86
     return r;
 }
 
-DEV float log2_m(float v) { return logf(v) * (1.0f / 0.69314718055994530942f); }   // math.cpp:103-106
+DEV float log2_m(float v) { return mt_logf(v) * (1.0f / 0.69314718055994530942f); }   // math.cpp:103-106
 
 // TMIPMap::eval(uv, d0, d1): the filtered lookup (mipmap.h:633-722)
 DEV float3 mip_filtered(const DevMip &V, float ux, float uy, float d0x, float d0y, float d1x, float d1y) {
@@ -121,9 +121,9 @@ DEV float3 mip_filtered(const DevMip &V, float ux, float uy, float d0x, float d0
     }
     if (minorRadius * V.M->max_anisotropy < majorRadius) {
         minorRadius = majorRadius / V.M->max_anisotropy;
-        const float theta = 0.5f * atanf(B / (A - C));
+        const float theta = 0.5f * mt_atanf(B / (A - C));
         float sinTheta, cosTheta;
-        sincosf(theta, &sinTheta, &cosTheta);
+        mt_sincosf(theta, &sinTheta, &cosTheta);
         const float a2 = majorRadius * majorRadius, b2 = minorRadius * minorRadius, sinTheta2 = sinTheta * sinTheta,
                     cosTheta2 = cosTheta * cosTheta, sin2Theta = 2 * sinTheta * cosTheta;
         A = a2 * cosTheta2 + b2 * sinTheta2;
