@@ -29,6 +29,8 @@ def gpu_c3(bunny_c3_small):
     g.close()
 
 
+@pytest.mark.skipif(bool(os.environ.get("MTSG_LIB")),
+                    reason="libmtsg_path.so links the default libmtsg.so, not the MTSG_LIB variant")
 def test_path_render_matches_device_render(bunny_c3_small, gpu_c3):
     p = bunny_c3_small.params()
     b = bunny_c3_small.border
