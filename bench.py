@@ -10,11 +10,17 @@ the host.  Scene load, kd-tree build and upload are excluded (as Mitsuba
 logs them separately, renderjob.cpp:102,113).
 
 Multi-GPU (config C4): one process per GPU; the film's 16x16 tiles are dealt
-round-robin (tile t -> rank t % N); no collective touches the data path (the
-host-side additive gather happens after the timed region).  Total work is the
-fixed frame, so scaling is "strong".
+round-robin (deal key k -> rank k % N); no collective touches the data path.
+After the timed region every rank's per-tile ImageBlocks are gathered to rank 0
+over gloo and put into the frame (ImageBlock::put, imageblock.h:103-107); the
+parity leg runs on that assembled frame, and rank 0 checks it against a
+whole-frame render of its own GPU.  Total work is the fixed frame, so scaling
+is "strong".  `--gpus N` without a launcher starts the N ranks itself (through
+torch.distributed.run, before any GPU call) and refuses to run when fewer than
+N GPUs are visible, unless --allow-shared is given (a rehearsal of N ranks on
+fewer GPUs; the line then says so).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload bunny15|cbox]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload bunny15|cbox|c5]
 """
 import argparse
 import json
@@ -64,6 +70,8 @@ def pmc_lookup(key, directory=None):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--allow-shared", action="store_true",
+                    help="N>1: allow ranks to share GPUs when fewer than N are visible (rehearsal only)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", default="bunny15", choices=["bunny15", "cbox", "c5"])
@@ -87,6 +95,35 @@ def parse():
                     help="skip the instrumented (untimed) pass of per-ray counts (profiler runs)")
     ap.add_argument("--print-pmc-key", action="store_true", help="print this configuration's PMC key and exit")
     return ap.parse_args()
+
+
+def visible_gpus():
+    """GPUs visible to this process, counted without initialising the GPU
+    (torch.cuda.device_count() does not on this image; HIP_VISIBLE_DEVICES and
+    ROCR_VISIBLE_DEVICES apply)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(a, argv):
+    """`bench.py --gpus N` run without a launcher: start the N ranks as children
+    (torch.distributed.run, one process per GPU, rendezvous on 127.0.0.1) and
+    return their exit code.  Nothing here touches the GPU, so the children are
+    started from a process that never initialised it."""
+    import socket
+    import subprocess
+    n = visible_gpus()
+    if n < a.gpus and not a.allow_shared:
+        raise SystemExit(f"bench.py --gpus {a.gpus}: only {n} GPU(s) visible; refusing to run {a.gpus} ranks "
+                         f"on them (--allow-shared rehearses N ranks on fewer GPUs)")
+    if n < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
 
 
 def dist_setup(n):
@@ -217,26 +254,68 @@ def _share(params, stride, offset):
     return p
 
 
-def parity_at_headline(scene, gpu, params, border, stride):
-    """Per-pixel L1 of the GPU frame vs the CPU oracle at the full spp: the
-    tile share key % stride == 0 (1/stride of the 16x16 tiles, every pixel of
-    them, all samples) rendered by both in counter mode (identical random
-    numbers per pixel / sample / dimension), developed (sum w L / sum w) and
-    compared on the pixels of those tiles.  Runs after the timed region."""
+def parity_keys(world, stride):
+    """Deal keys the parity leg compares: k mod (world * stride) < world, i.e.
+    1/stride of the frame's tiles with the same number from every rank (for
+    world 1: k % stride == 0)."""
+    return world * stride, world
+
+
+def all_gather_obj(pg, obj, world):
+    if pg is None:
+        return [obj]
+    out = [None] * world
+    pg.all_gather_object(out, obj)
+    return out
+
+
+def gather_frame(pg, rank, world, part, tile_w, tile_h, border):
+    """Host-side tile gather (no collective on the data path: it runs after
+    the timed region): every rank's share -- ("win", its per-tile ImageBlocks,
+    mtsg_render_device_tiles) or ("block", a block of the whole rectangle) --
+    goes to rank 0 over gloo and is put into the frame's ImageBlock
+    (ImageBlock::put, imageblock.h:103-107; BlockedRenderProcess's merge,
+    imageproc.cpp:28-78).  Returns the frame on rank 0, None elsewhere."""
+    import mtsg
+    parts = [part]
+    if pg is not None:
+        parts = [None] * world if rank == 0 else None
+        pg.gather_object(part, parts, dst=0)
+    if rank != 0:
+        return None
+    frame = np.zeros((tile_h + 2 * border, tile_w + 2 * border, 5), np.float32)
+    for r, (kind, arr) in enumerate(parts):
+        if kind == "win":
+            mtsg.put_tile_windows(frame, arr, tile_w, tile_h, border, world, r)
+        else:
+            frame += arr
+    return frame
+
+
+def parity_at_headline(scene, frame, params, border, stride, world):
+    """Per-pixel L1 of the GPU frame vs the CPU oracle at the full spp.  `frame`
+    is the ImageBlock the timed steps produced, assembled from every rank's
+    tiles; the oracle renders the tiles of parity_keys (1/stride of the frame,
+    every pixel of them, all samples) in counter mode (identical random numbers
+    per pixel / sample / dimension); both are developed (sum w L / sum w) and
+    compared on those pixels.  Runs after the timed region."""
     import mtsg
     from oracle import pyoracle as O
+    mod, below = parity_keys(world, stride)
     p = params.copy()
-    p.tile_stride, p.tile_offset = stride, 0
+    p.tile_stride = mod
+    img_c, samples = None, 0
     t0 = time.time()
-    img_g = gpu.render(p, border)
-    t_gpu = time.time() - t0
-    t0 = time.time()
-    img_c, st = O.render(scene.desc, p, border, rng=O.RNG_COUNTER)
+    for r in range(below):
+        p.tile_offset = r
+        blk, st = O.render(scene.desc, p, border, rng=O.RNG_COUNTER)
+        img_c = blk if img_c is None else img_c + blk
+        samples += st.samples
     t_cpu = time.time() - t0
     b = border
-    rgb_g = mtsg.develop(img_g[b:b + p.tile_h, b:b + p.tile_w])
+    rgb_g = mtsg.develop(frame[b:b + p.tile_h, b:b + p.tile_w])
     rgb_c = mtsg.develop(img_c[b:b + p.tile_h, b:b + p.tile_w])
-    own = (mtsg.tile_deal_keys(p.tile_w, p.tile_h) % stride) == 0
+    own = (mtsg.tile_deal_keys(p.tile_w, p.tile_h) % mod) < below
     d = np.abs(rgb_g - rgb_c)[own]
     l1 = float(d.mean())
     mean = float(rgb_c[own].mean())
@@ -247,9 +326,12 @@ def parity_at_headline(scene, gpu, params, border, stride):
             "frac_over_1e-3": float((px > 1e-3).mean()), "frac_over_1e-3_of_mean": float((px > 1e-3 * mean).mean())}
     return {"l1": l1, "mean": round(mean, 6), "l1_rel_mean": l1 / max(mean, 1e-12),
             "max_abs": float(d.max()), "per_pixel": dist, "pixels": int(own.sum()), "spp": int(p.spp),
-            "samples": int(st.samples), "tiles": f"16x16 tiles with deal key % {stride} == 0 of {p.tile_w}x{p.tile_h}",
+            "samples": int(samples),
+            "tiles": (f"16x16 tiles with deal key % {mod} < {below} of {p.tile_w}x{p.tile_h}"
+                      + (f" ({below // world} per rank's share), from the frame assembled from all {world} ranks"
+                         if world > 1 else ", from the timed steps' last frame")),
             "bar": "l1 < 1e-3 (and l1_rel_mean < 1e-3)", "pass": bool(l1 < 1e-3 and l1 < 1e-3 * max(mean, 1e-12)),
-            "rng": "counter mode on both sides", "oracle_seconds": round(t_cpu, 1), "gpu_seconds": round(t_gpu, 2)}
+            "rng": "counter mode on both sides", "oracle_seconds": round(t_cpu, 1)}
 
 
 def main():
@@ -257,12 +339,24 @@ def main():
     if a.print_pmc_key:
         print(json.dumps(pmc_key(a, int(os.environ.get("WORLD_SIZE", "1")))))
         return
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a, sys.argv[1:]))
     rank, world, local, pg = dist_setup(a.gpus)
     import mtsg
-    # one GPU per rank (LOCAL_RANK); more ranks than visible GPUs share them
-    # round-robin (a rehearsal of the multi-process path on a smaller box)
-    ndev = max(1, mtsg.device_lib().mtsg_device_count())
+    # one GPU per rank (LOCAL_RANK); ranks share GPUs only with --allow-shared
+    # (a rehearsal of the multi-process path on a smaller box)
+    ndev = mtsg.device_lib().mtsg_device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no gfx950 device visible")
     dev = local % ndev if world > 1 else 0
+    devices = None
+    if world > 1:
+        # every rank sees every rank's device identity, so all refuse together
+        ids = all_gather_obj(pg, mtsg.device_pci_id(dev), world)
+        devices = {"distinct": len(set(ids)), "pci": ids, "shared": len(set(ids)) < world}
+        if len(set(ids)) < world and not a.allow_shared:
+            raise SystemExit(f"bench.py: {world} ranks but only {len(set(ids))} distinct GPU(s) ({ids}); "
+                             "refusing (--allow-shared rehearses N ranks on fewer GPUs)")
 
     path, defs = scene_args(a)
     t_load = time.time()
@@ -456,18 +550,33 @@ def main():
                     "iterations_per_ray": round(per(cs.wave_active_lanes, cs.rays_closest + cs.rays_shadow), 2),
                     "instance_visits_per_ray": round(per(cs.instance_visits + cs.shadow_instance_visits,
                                                          cs.rays_closest + cs.rays_shadow), 3)}
-        if a.save:
-            nw = windows_for(params)
-            if nw:   # the host-side gather of this rank's tile windows
-                host_block[:] = 0
-                mtsg.put_tile_windows(host_block, host_win[:nw[0]], params.tile_w, params.tile_h, border,
-                                      params.tile_stride, params.tile_offset)
-            img = mtsg.develop(host_block[border:H - border, border:W - border])
-            np.save(a.save, img)
 
-    parity = None
-    if rank == 0 and world == 1 and not a.no_parity and a.emulate_ranks <= 1:
-        parity = parity_at_headline(scene, gpu, params, border, a.parity_stride)
+    # the host-side tile gather: every rank's share of the timed steps' last
+    # frame into rank 0's ImageBlock (after the timed region)
+    frame = assembly = parity = None
+    if not (a.emulate_ranks > 1 and world == 1):
+        nw = windows_for(params)
+        part = ("win", host_win[:nw[0]].copy()) if nw else ("block", host_block.copy())
+        frame = gather_frame(pg, rank, world, part, params.tile_w, params.tile_h, border)
+    if rank == 0 and world > 1:
+        # the assembled frame vs the whole frame rendered by rank 0's GPU alone
+        # (global RNG keys: the same samples; the film's float additions may
+        # run in another order)
+        pw = params.copy()
+        pw.tile_stride, pw.tile_offset = 1, 0
+        mtsg.device_lib().mtsg_device_memset(gpu._h, film, nbytes)
+        gpu.render_device(pw, film)
+        whole = gpu.download(film, (H, W, 5))
+        diff = np.abs(frame - whole)
+        assembly = {"check": f"frame assembled from {world} ranks' tile ImageBlocks vs the whole frame rendered on rank 0's GPU",
+                    "max_abs_diff": float(diff.max()), "max_value": float(np.abs(whole).max()),
+                    "pass": bool(np.allclose(frame, whole, rtol=1e-5, atol=1e-6)),
+                    "tiles_per_rank": [int(((mtsg.tile_deal_keys(params.tile_w, params.tile_h)[::16, ::16]) % world == r).sum())
+                                       for r in range(world)]}
+    if rank == 0 and a.save and frame is not None:
+        np.save(a.save, mtsg.develop(frame[border:H - border, border:W - border]))
+    if rank == 0 and frame is not None and not a.no_parity:
+        parity = parity_at_headline(scene, frame, params, border, a.parity_stride, world)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(scene, params, border, a.cpu_seconds)
@@ -481,6 +590,7 @@ def main():
             "metric": "Msamples/sec at 1280x720x256spp, 1/2/4/8 MI355X; per-pixel L1 vs CPU ref",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 2), "higher_is_better": True, "scaling": "strong",
+            **({"devices": devices} if devices else {}),
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": {"bunny15": ("C3 bunny x15, 1,041,765 triangles, roughconductor Cu GGX 0.2" + (
                                         ", 15 instances flattened to world-space triangles" if a.instancing == "flatten" else "")),
@@ -501,10 +611,12 @@ def main():
                 "note": "one GPU rendering each rank's 1/N tile share in turn; value = frame samples / the slowest "
                         "share's time (the N-GPU frame time without launch and gather overheads); kernels = share 0"}
                if a.emulate_ranks > 1 and world == 1 else {}),
-            "roofline": roofline, "cpu_baseline": cpu, "parity": parity, "kernels": kernels,
+            "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
+            **({"assembly": assembly} if assembly else {}), "kernels": kernels,
         }
         print(json.dumps(out))
     if pg is not None:
+        barrier(pg)   # the other ranks wait for rank 0's checks
         pg.destroy_process_group()
 
 

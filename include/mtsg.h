@@ -489,6 +489,12 @@ typedef struct mtsg_scene mtsg_scene;
 /* Number of visible gfx950 devices. */
 int  mtsg_device_count(void);
 
+/* PCI address ("dddd:bb:dd.f") of visible device `device`, NUL-terminated in
+ * buf[len]: the identity bench.py's ranks compare to prove they drive distinct
+ * GPUs (one process per GPU; no reference counterpart -- Mitsuba's workers
+ * are host threads). */
+int  mtsg_device_pci_id(int device, char *buf, int len);
+
 /* Upload a scene to `device`; *out receives the handle. */
 int  mtsg_scene_create(const mtsg_scene_desc *desc, int device, mtsg_scene **out);
 

@@ -73,8 +73,9 @@ struct DevScene {
     // traversal stacks in use (<= SHORT_STACK / INNER_STACK / OUTER_STACK;
     // smaller only to exercise the restart guard) and the restart guard:
     // from restart rstGuard of a ray (per level) on, a restart starts one ulp
-    // beyond its exit distance; restart rstMax ends the ray with SB_ERR
-    uint32_t capFlat, capGrp, capTop, rstGuard, rstMax;
+    // beyond its exit distance; restart rstMax (rstMaxC for closest-hit
+    // rays) ends the ray with SB_ERR
+    uint32_t capFlat, capGrp, capTop, rstGuard, rstMax, rstMaxC;
 };
 
 struct DevCamera {
@@ -104,7 +105,7 @@ struct DevBatch {
     int tiles_x;                          // tiles per row of the rectangle
     int tile0, ntiles;                    // virtual tile range of this batch
     int tstride, toffset;                 // deal key = toffset + virtual * tstride (tile_of_key)
-    int skew;                             // deal: row ty rotated by ty * skew tiles (1; MTSG_DEAL_SKEW measures others)
+    int skew;                             // deal: row ty rotated by ty * skew tiles (always 1)
     uint32_t s0, ns;
     uint32_t nslots;
 };
@@ -536,11 +537,11 @@ constexpr uint32_t RST_GUARD = 8, RST_MAX = SB_RST_MASK;
 // stack capacities and restart limits of a traversal: compile-time constants
 // in the production kernels (KNOBS = false), the scene's test overrides
 // (DevScene::capFlat ...) in the KNOBS instantiations
-struct TravLimits { uint32_t capFlat, capGrp, capTop, rstGuard, rstMax; };
+struct TravLimits { uint32_t capFlat, capGrp, capTop, rstGuard, rstMax, rstMaxC; };
 template <bool KNOBS>
 DEV TravLimits trav_limits(const DevScene &S) {
-    if (KNOBS) return TravLimits{S.capFlat, S.capGrp, S.capTop, S.rstGuard, S.rstMax};
-    return TravLimits{(uint32_t)SHORT_STACK, (uint32_t)INNER_STACK, (uint32_t)OUTER_STACK, RST_GUARD, RST_MAX};
+    if (KNOBS) return TravLimits{S.capFlat, S.capGrp, S.capTop, S.rstGuard, S.rstMax, S.rstMaxC};
+    return TravLimits{(uint32_t)SHORT_STACK, (uint32_t)INNER_STACK, (uint32_t)OUTER_STACK, RST_GUARD, RST_MAX, RST_MAX};
 }
 
 // kd-restart after the stack ran empty with entries dropped (Foley &
@@ -571,7 +572,7 @@ DEV void kd_restart(const TravLimits &L, SpecRay &r, uint32_t b, uint2 root, uin
     uint32_t nb = b & ~SB_STACK;
     if (restart) {   // lanes that restart (the others finish their ray here)
         const uint32_t nr = (b >> SB_RST_SHIFT) & SB_RST_MASK;
-        if (nr >= L.rstMax) nb |= SB_ERR | SB_TRAVDONE;   // the limit (the counter saturates)
+        if (nr >= ((b & SB_SHADOW) ? L.rstMax : L.rstMaxC)) nb |= SB_ERR | SB_TRAVDONE;   // the limit (the counter saturates)
         else nb += SB_RST1;
         if (nr >= L.rstGuard) {
             // nextafterf(t0, +inf) for finite t0, in integer arithmetic
@@ -674,6 +675,8 @@ DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float r
     r.lfTmax = -1.0f;
     r.bits = dneg << SB_DNEG | (shadow ? SB_SHADOW : 0u);
     r.mb = 0;
+    r.bestKey = 0xFFFFFFFFu;   // no best yet (a first hit exactly at a finite maxt is flagged
+                              // and traced again with the mailbox: the same answer)
     return true;
 }
 

@@ -407,10 +407,11 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
     // the cancel flag is consumed (cleared) when a render returns, so a
     // cancel that races with the start of a render is not lost
     if (count) HIP_TRY(hipMemsetAsync(s->LP[0].ctr, 0, CTR_WORDS * sizeof(unsigned long long), s->stream));
-    // row rotation of the tile deal (include/mtsg.h); MTSG_DEAL_SKEW: other
-    // rotations for measurement only (the oracle and mtsg.py deal with 1)
-    int dealSkew = 1;
-    if (const char *k = getenv("MTSG_DEAL_SKEW")) dealSkew = std::max(0, atoi(k));
+    // row rotation of the tile deal (include/mtsg.h): fixed at 1, as the
+    // oracle, mtsg_tile_windows and mtsg.put_tile_windows assume (the round-3
+    // measurement override is gone: a rank with another rotation would put
+    // its tiles in the wrong places without an error)
+    const int dealSkew = 1;
     // the batches of this call, tile-major
     std::vector<DevBatch> batches;
     for (uint32_t t0i = 0; t0i < ntiles; t0i += tilesPerBatch) {
@@ -558,6 +559,11 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
                 hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, P.cnt, -1, -1);
                 timed_launch(s, K_SHADOW, st, [&]() { launch_trace(s, count, P, -2, L.last & 1, 0u, st); });
                 s->stats.launches_trace_shadow++;
+                // the error word again, after this launch: a traversal error of
+                // the last bounce's shadow rays fails the render too (the copy
+                // of bounce L.last's counters was taken before this launch)
+                HIP_TRY(hipMemcpyAsync(hostCnt(l, L.last) + CNT_ERR, P.cnt + CNT_ERR, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipEventRecord(L.cntEv[L.last & 1], st));
             }
             timed_launch(s, K_SPLAT, st, [&]() {
                 dim3 g(B.ntiles, (B.ns + SPLAT_CHUNK - 1) / SPLAT_CHUNK);
@@ -676,6 +682,12 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
 // C-ABI
 // ===========================================================================
 extern "C" {
+
+int mtsg_device_pci_id(int device, char *buf, int len) {
+    if (!buf || len < 13) { g_err = "mtsg_device_pci_id: buffer too small"; return MTSG_ERR_INVALID; }
+    if (hipDeviceGetPCIBusId(buf, len, device) != hipSuccess) { g_err = "hipDeviceGetPCIBusId failed"; return MTSG_ERR_DEVICE; }
+    return MTSG_OK;
+}
 
 int mtsg_device_count(void) {
     int n = 0;
@@ -917,8 +929,12 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     }
     if (const char *g = getenv("MTSG_RESTART_GUARD")) ds.rstGuard = (uint32_t)std::max(0, atoi(g));
     if (const char *g = getenv("MTSG_RESTART_LIMIT")) ds.rstMax = std::min<uint32_t>(RST_MAX, (uint32_t)std::max(0, atoi(g)));
+    // MTSG_RESTART_LIMIT_SHADOW_ONLY=1: the limit applies to shadow rays only
+    // (a test of the error word of the shadow launches)
+    const char *so = getenv("MTSG_RESTART_LIMIT_SHADOW_ONLY");
+    ds.rstMaxC = (so && atoi(so)) ? RST_MAX : ds.rstMax;
     s->knobs = ds.capFlat != (uint32_t)SHORT_STACK || ds.capGrp != (uint32_t)INNER_STACK || ds.capTop != (uint32_t)OUTER_STACK ||
-               ds.rstGuard != RST_GUARD || ds.rstMax != RST_MAX;
+               ds.rstGuard != RST_GUARD || ds.rstMax != RST_MAX || ds.rstMaxC != RST_MAX;
     // environment emitter tables (envmap.h)
     ds.has_env = d->has_envmap ? 1 : 0;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {

@@ -156,7 +156,7 @@ _host = None
 _dev = None
 
 DEVICE_SYMBOLS = [
-    "mtsg_device_count", "mtsg_scene_create", "mtsg_render", "mtsg_render_device",
+    "mtsg_device_count", "mtsg_device_pci_id", "mtsg_scene_create", "mtsg_render", "mtsg_render_device",
     "mtsg_tile_windows", "mtsg_render_device_tiles",
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_cancel_clear", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
@@ -251,6 +251,7 @@ def device_lib() -> C.CDLL:
                                "(run `make device` / __graft_entry__.build()); no CPU fallback exists")
         lib = C.CDLL(path)
         lib.mtsg_device_count.restype = C.c_int
+        lib.mtsg_device_pci_id.argtypes = [C.c_int, C.c_char_p, C.c_int]
         lib.mtsg_scene_create.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         lib.mtsg_render.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
         lib.mtsg_render_device.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
@@ -282,6 +283,15 @@ def device_lib() -> C.CDLL:
         lib.mtsg_last_error.argtypes = [C.c_char_p, C.c_size_t]
         _dev = lib
     return _dev
+
+
+def device_pci_id(device: int) -> str:
+    """PCI address of visible device `device` (mtsg_device_pci_id)."""
+    buf = C.create_string_buffer(64)
+    lib = device_lib()
+    if lib.mtsg_device_pci_id(device, buf, 64) != MTSG_OK:
+        raise RuntimeError(_err(lib, "mtsg_last_error"))
+    return buf.value.decode()
 
 
 def _err(lib, fn) -> str:

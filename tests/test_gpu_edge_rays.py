@@ -208,3 +208,28 @@ def test_restart_limit_fails_the_query(monkeypatch):
         g.render(s.params(), s.border)
     finally:
         g.close()
+
+
+def test_restart_limit_of_shadow_rays_fails_the_render(monkeypatch):
+    """The limit applied to shadow rays only (MTSG_RESTART_LIMIT_SHADOW_ONLY):
+    closest-hit rays traverse normally, and a shadow ray that reaches the limit
+    still fails the render.  Shadow rays are traced in the next bounce's launch
+    or in the final shadow launch after the last bounce; the error word is read
+    after both (the final launch's errors were not read)."""
+    s = mtsg.Scene(os.path.join(SCENES, "bunny15.xml"), {"width": 64, "height": 36, "spp": 1})
+    monkeypatch.setenv("MTSG_STACK_CAP", "1")
+    monkeypatch.setenv("MTSG_RESTART_LIMIT", "0")
+    monkeypatch.setenv("MTSG_RESTART_LIMIT_SHADOW_ONLY", "1")
+    g = mtsg.GPUScene(s, 0)
+    try:
+        rays = corner_rays(s, 20000, 55)
+        g.trace_closest(rays)   # closest-hit rays are not limited
+        sh = rays.copy()
+        sh[:, 7] = 1e30
+        with pytest.raises(RuntimeError, match=r"\(-6\).*restart limit"):
+            g.trace_shadow(sh)
+        for depth in (2, 3, -1):
+            with pytest.raises(RuntimeError, match=r"\(-6\).*restart limit"):
+                g.render(s.params(max_depth=depth), s.border)
+    finally:
+        g.close()
