@@ -23,7 +23,7 @@ ORACLE      := oracle/liboracle.so
 ORACLE_FAST := oracle/liboracle_fast.so
 
 .PHONY: all host device oracle clean
-all: host device oracle $(PATH_LIB) $(CLI) scenes/sky512.pfm
+all: host device oracle $(PATH_LIB) $(CLI) scenes/sky512.pfm tools/math_probe tools/check_glibc_mathf
 host: $(HOST_LIB)
 device: $(DEV_LIB)
 oracle: $(ORACLE) $(ORACLE_FAST)
@@ -77,6 +77,13 @@ $(ORACLE_FAST): oracle/oracle.cpp oracle/oracle.h include/mtsg.h
 	$(CXX) -std=c++17 -O3 -msse2 -march=nocona -funsafe-math-optimizations -fPIC -shared \
 	    -o $@ oracle/oracle.cpp -lpthread
 
+# glibc_mathf.h (the device's glibc float transcendentals) against libm: on
+# the GPU (math_probe) and on the host (check_glibc_mathf)
+tools/math_probe: tools/math_probe.hip $(PKG)/csrc/glibc_mathf.h
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -ffp-contract=off -o $@ $< -lpthread
+tools/check_glibc_mathf: tools/check_glibc_mathf.cpp $(PKG)/csrc/glibc_mathf.h
+	$(HIPCC) -O2 -mfma -std=c++17 -ffp-contract=off -o $@ $< -lpthread
+
 # synthetic HDR environment for the envmap scenes (tools/gen_envmap.py)
 scenes/sky512.pfm: tools/gen_envmap.py
 	python3 tools/gen_envmap.py $@ 512 256
@@ -86,7 +93,7 @@ clean:
 
 # Measurement variants of the device library (my-mitsuba_amd/var/, loaded with
 # MTSG_LIB=...; objects in build/var/, which gpurun does not ship)
-VARIANTS := fm16:-DMTSG_FETCH_MIN=16 fm64:-DMTSG_FETCH_MIN=64 gs1:-DMTSG_GUIDE_SPLIT=1 gs4:-DMTSG_GUIDE_SPLIT=4 noguide:-DMTSG_FETCH_MIN=256 wt:-DMTSG_WT_DRAIN=1 ss5:-DMTSG_SHORT_STACK=5 ldstop:-DMTSG_LDS_TOP=1 noguard:-DMTSG_RST_GUARD=0 iw7:-DMTSG_INST_WAVES=7 gs5:-DMTSG_INNER_STACK=5 noshlds:-DMTSG_SHADE_LDS=0 nosave:-DMTSG_SAVE_RAY=0 soct:-DMTSG_SORT_OCT=1 nomb:-DMTSG_MAILBOX=0 sinv:-DMTSG_SAVE_INV=1 silp:-mllvm@-amdgpu-sched-strategy=max-ilp smem:-mllvm@-amdgpu-sched-strategy=max-memory-clause flmath:-DMTSG_CR_MATH=0 crsc:-DMTSG_CR_MATH=1
+VARIANTS := fm16:-DMTSG_FETCH_MIN=16 fm64:-DMTSG_FETCH_MIN=64 gs1:-DMTSG_GUIDE_SPLIT=1 gs4:-DMTSG_GUIDE_SPLIT=4 noguide:-DMTSG_FETCH_MIN=256 wt:-DMTSG_WT_DRAIN=1 ss5:-DMTSG_SHORT_STACK=5 ldstop:-DMTSG_LDS_TOP=1 noguard:-DMTSG_RST_GUARD=0 iw7:-DMTSG_INST_WAVES=7 gs5:-DMTSG_INNER_STACK=5 noshlds:-DMTSG_SHADE_LDS=0 nosave:-DMTSG_SAVE_RAY=0 soct:-DMTSG_SORT_OCT=1 nomb:-DMTSG_MAILBOX=0 sinv:-DMTSG_SAVE_INV=1 silp:-mllvm@-amdgpu-sched-strategy=max-ilp smem:-mllvm@-amdgpu-sched-strategy=max-memory-clause ocmlmath:-DMTSG_GLIBC_MATH=0
 VAR_LIBS := $(foreach v,$(VARIANTS),$(PKG)/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
 .PHONY: variants
 variants: $(VAR_LIBS)

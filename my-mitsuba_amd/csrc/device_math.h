@@ -7,69 +7,43 @@
 #define DEV __device__ __forceinline__
 #endif
 
+#include "glibc_mathf.h"
+
 // Float transcendentals of the shading code.  Mitsuba (and the oracle) call
-// glibc's float functions.  Measured on gfx950 over 4M arguments per function
-// (tools/math_probe.hip), ROCm's float versions return a different float than
-// glibc on 6-39% of arguments, versions evaluated in double and rounded once on
-// 0.06-16% (sincos: 16-21% -> 1.3%).  MTSG_CR_MATH is a bit mask of the
-// functions evaluated in double.  Measured with the library's double sincos
-// (mask 1): C5 parity 3.9e-4 -> 1.1e-4 of the mean, but C5 7% slower
-// (k_shade scratch at its 128-VGPR limit; exp/log/pow/acos/atan2 in double spill
-// more).  The default stays the float library until the short polynomial
-// mt_sincos_d (variant crsc; exact vs the correctly rounded sin/cos on 20M CPU
-// arguments) is measured.
-#ifndef MTSG_CR_MATH
-#define MTSG_CR_MATH 0   // bit mask: 1 sincos, 2 pow, 4 tan, 8 log, 16 exp, 32 atan2, 64 atan, 128 acos
+// glibc's float functions; ROCm's float library returns another float on
+// 6-39% of arguments, and an ulp can send a long specular path elsewhere
+// (DESIGN §5).  MTSG_GLIBC_MATH=1 (the default) evaluates glibc 2.35's own
+// algorithms (glibc_mathf.h: the same float for every argument, checked over
+// all 2^32 floats on the host and on the GPU, tools/check_glibc_mathf.cpp,
+// tools/math_probe.hip); 0 is the measurement variant on ROCm's library.
+// Mitsuba's fastexp / fastlog are the double functions rounded to float on
+// Linux x86-64 (include/mitsuba/core/math.h:175-199): the device's double
+// exp / log, which round to the same float as glibc's but in ~2^-29 of cases.
+#ifndef MTSG_GLIBC_MATH
+#define MTSG_GLIBC_MATH 1
 #endif
-#define MTSG_CR(bit, dbl, flt) ((MTSG_CR_MATH & (bit)) ? (dbl) : (flt))
-// double sincos for |x| <= 1e5 (the shading code's angles stay within a few pi):
-// Cody-Waite reduction by pi/2 in two parts (fdlibm's pio2_1 / pio2_1t), Taylor
-// polynomials on |r| <= pi/4 to degree 17 / 18 (truncation < 1e-18)
-DEV void mt_sincos_d(double x, double *s, double *c) {
-    const double k = rint(x * 6.36619772367581382433e-01);
-    const double r = fma(-k, 6.07710050650619224932e-11, fma(-k, 1.57079632673412561417e+00, x));
-    const double z = r * r;
-    double ps = 1.0 / 355687428096000.0;                      // 1/17!
-    ps = fma(ps, z, -1.0 / 1307674368000.0);                  // 1/15!
-    ps = fma(ps, z, 1.0 / 6227020800.0);
-    ps = fma(ps, z, -1.0 / 39916800.0);
-    ps = fma(ps, z, 1.0 / 362880.0);
-    ps = fma(ps, z, -1.0 / 5040.0);
-    ps = fma(ps, z, 1.0 / 120.0);
-    ps = fma(ps, z, -1.0 / 6.0);
-    const double sn = fma(ps * z, r, r);
-    double pc = 1.0 / 6402373705728000.0;                     // 1/18!
-    pc = fma(pc, z, -1.0 / 20922789888000.0);                 // 1/16!
-    pc = fma(pc, z, 1.0 / 87178291200.0);
-    pc = fma(pc, z, -1.0 / 479001600.0);
-    pc = fma(pc, z, 1.0 / 3628800.0);
-    pc = fma(pc, z, -1.0 / 40320.0);
-    pc = fma(pc, z, 1.0 / 720.0);
-    pc = fma(pc, z, -1.0 / 24.0);
-    pc = fma(pc, z, 0.5);
-    const double cs = fma(-pc, z, 1.0);
-    const int q = (int)k & 3;
-    const double s0 = (q & 1) ? cs : sn, c0 = (q & 1) ? sn : cs;
-    *s = (q & 2) ? -s0 : s0;
-    *c = ((q + 1) & 2) ? -c0 : c0;
-}
-DEV void mt_sincosf(float x, float *s, float *c) {
-#if MTSG_CR_MATH & 1
-    double sd, cd;
-    mt_sincos_d((double)x, &sd, &cd);
-    *s = (float)sd;
-    *c = (float)cd;
+#if MTSG_GLIBC_MATH
+DEV void mt_sincosf(float x, float *s, float *c) { gmf::sincosf(x, s, c); }
+DEV float mt_tanf(float x) { return gmf::tanf(x); }
+DEV float mt_logf(float x) { return gmf::logf(x); }
+DEV float mt_expf(float x) { return gmf::expf(x); }
+DEV float mt_atan2f(float y, float x) { return gmf::atan2f(y, x); }
+DEV float mt_atanf(float x) { return gmf::atanf(x); }
+DEV float mt_acosf(float x) { return gmf::acosf(x); }
 #else
-    sincosf(x, s, c);
+DEV void mt_sincosf(float x, float *s, float *c) { sincosf(x, s, c); }
+DEV float mt_tanf(float x) { return tanf(x); }
+DEV float mt_logf(float x) { return logf(x); }
+DEV float mt_expf(float x) { return expf(x); }
+DEV float mt_atan2f(float y, float x) { return atan2f(y, x); }
+DEV float mt_atanf(float x) { return atanf(x); }
+DEV float mt_acosf(float x) { return acosf(x); }
 #endif
-}
-DEV float mt_powf(float x, float y) { return MTSG_CR(2, (float)pow((double)x, (double)y), powf(x, y)); }
-DEV float mt_tanf(float x) { return MTSG_CR(4, (float)tan((double)x), tanf(x)); }
-DEV float mt_logf(float x) { return MTSG_CR(8, (float)log((double)x), logf(x)); }
-DEV float mt_expf(float x) { return MTSG_CR(16, (float)exp((double)x), expf(x)); }
-DEV float mt_atan2f(float y, float x) { return MTSG_CR(32, (float)atan2((double)y, (double)x), atan2f(y, x)); }
-DEV float mt_atanf(float x) { return MTSG_CR(64, (float)atan((double)x), atanf(x)); }
-DEV float mt_acosf(float x) { return MTSG_CR(128, (float)acos((double)x), acosf(x)); }
+// powf (phong, Beckmann's visible sampling, roughplastic's rtrans lookup): ROCm's
+DEV float mt_powf(float x, float y) { return powf(x, y); }
+// math::fastexp / math::fastlog (math.h:185-199)
+DEV float mt_fastexp(float x) { return (float)exp((double)x); }
+DEV float mt_fastlog(float x) { return (float)log((double)x); }
 
 namespace mtsg {
 

@@ -1355,7 +1355,7 @@ DEV float3 cosine_hemisphere(float sx, float sy) {
 
 // math.cpp:25-70
 DEV float erfinv_m(float x) {
-    float w = -mt_logf((1.0f - x) * (1.0f + x));
+    float w = -mt_fastlog((1.0f - x) * (1.0f + x));
     float p;
     if (w < 5.0f) {
         w = w - 2.5f;
@@ -1388,7 +1388,7 @@ DEV float erf_m(float x) {
     float sign = copysignf(1.0f, x);
     x = fabsf(x);
     float t = 1.0f / (1.0f + p * x);
-    float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * mt_expf(-x * x);
+    float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * mt_fastexp(-x * x);
     return sign * y;
 }
 DEV float hypot2_m(float a, float b) {   // math.cpp:74-86
@@ -1426,7 +1426,7 @@ struct MF {
         float ct2 = m.z * m.z;
         float be = ((m.x * m.x) / (au * au) + (m.y * m.y) / (av * av)) / ct2;
         float result;
-        if (type == MTSG_MF_BECKMANN) result = mt_expf(-be) / (kPi * au * av * ct2 * ct2);
+        if (type == MTSG_MF_BECKMANN) result = mt_fastexp(-be) / (kPi * au * av * ct2 * ct2);
         else if (type == MTSG_MF_GGX) { float root = (1.0f + be) * ct2; result = 1.0f / (kPi * au * av * root * root); }
         else result = sqrtf((eu + 2) * (ev + 2)) * (0.5f * kInvPi) * mt_powf(m.z, phong_exponent(m));
         if (result * m.z < 1e-20f) result = 0;
@@ -1451,7 +1451,7 @@ struct MF {
         if (type == MTSG_MF_BECKMANN) {
             const float SQRT_PI_INV = 0.56418958354775628695f;
             if (thetaI < 1e-4f) {
-                float r = sqrtf(-mt_logf(1.0f - sx));
+                float r = sqrtf(-mt_fastlog(1.0f - sx));
                 float sp, cp;
                 mt_sincosf(2 * kPi * sy, &sp, &cp);
                 slx = r * cp; sly = r * sp;
@@ -1551,7 +1551,7 @@ struct MF {
                 alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
             }
             if (type == MTSG_MF_BECKMANN) {
-                float t2 = alphaSqr * -mt_logf(1.0f - sx);
+                float t2 = alphaSqr * -mt_fastlog(1.0f - sx);
                 cosThetaM = 1.0f / sqrtf(1.0f + t2);
                 pdf = (1.0f - sx) / (kPi * au * av * cosThetaM * cosThetaM * cosThetaM);
             } else {

@@ -100,7 +100,7 @@ DEV float hypot2_m(float a, float b) {   // math.cpp:74-86
     return r;
 }
 
-DEV float log2_m(float v) { return mt_logf(v) * (1.0f / 0.69314718055994530942f); }   // math.cpp:103-106
+DEV float log2_m(float v) { return mt_fastlog(v) * (1.0f / 0.69314718055994530942f); }   // math.cpp:103-106 (fastlog)
 
 // TMIPMap::eval(uv, d0, d1): the filtered lookup (mipmap.h:633-722)
 DEV float3 mip_filtered(const DevMip &V, float ux, float uy, float d0x, float d0y, float d1x, float d1y) {

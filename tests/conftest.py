@@ -24,7 +24,7 @@ def _ensure_built():
     runs -- a prebuilt library that no longer matches the sources is never
     tested silently."""
     import subprocess
-    targets = ["host", "device", "oracle", "my-mitsuba_amd/libmtsg_path.so", "scenes/sky512.pfm"]
+    targets = ["host", "device", "oracle", "my-mitsuba_amd/libmtsg_path.so", "scenes/sky512.pfm", "tools/check_glibc_mathf"]
     if subprocess.call(["make", "-C", REPO, "-q"] + targets, stdout=subprocess.DEVNULL) != 0:
         print(f"conftest: rebuilding stale native libraries ({' '.join(targets)})", flush=True)
         subprocess.check_call(["make", "-C", REPO, "-j8"] + targets)

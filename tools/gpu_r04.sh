@@ -11,6 +11,8 @@ PYT="python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread"
 for w in ${*:-tests bench}; do
   case $w in
     tests) step tests 900 $PYT tests ;;
+    mathprobe) step mathprobe 300 tools/math_probe 3 ;;
+    tests-parity) step tests-parity 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_c4.py ;;
     tests-new) step tests-new 600 $PYT tests/test_gpu_00_bench_ranks.py tests/test_gpu_c4.py tests/test_gpu_edge_rays.py ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     inst) step inst 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity ;;

@@ -1,67 +1,104 @@
-// Device vs glibc float transcendentals: how often does the device library's
-// float function (ROCm OCML) and a double-evaluated, rounded-to-float version
-// differ from glibc's float result on the same arguments?  (DESIGN §9, C5's
-// per-pixel tail.)  Build: hipcc --offload-arch=gfx950 -O2 -ffp-contract=off
-// -o tools/math_probe tools/math_probe.hip
+// On the GPU: the device's float transcendentals vs the host's glibc, bit for
+// bit, over a strided sweep of all 2^32 float arguments (NaN results only need
+// to be NaN on both sides).  Two device versions per function:
+//   gmf::*  my-mitsuba_amd/csrc/glibc_mathf.h, glibc 2.35's algorithms (what the
+//           path integrator calls, device_math.h mt_*)
+//   ocml    ROCm's float library (sinf, expf, ...), for comparison
+// atan2f takes y = the argument and x from a hash of it.  DESIGN §5.
+// Build: make tools/math_probe   Run: tools/math_probe [stride]  (default 3)
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <thread>
 #include <vector>
 
-enum { NF = 9 };
-static const char *kName[NF] = {"sin", "cos", "acos", "atan2", "exp", "log", "pow", "tan", "atan"};
+#include "../my-mitsuba_amd/csrc/glibc_mathf.h"
 
-__global__ void k_probe(const float4 *in, float *outF, float *outD, int n) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+enum { NF = 8 };
+static const char *kName[NF] = {"sinf", "cosf", "tanf", "expf", "logf", "atanf", "acosf", "atan2f"};
+
+__host__ __device__ inline float arg_y(uint32_t u) {
+    uint32_t h = u * 0x9E3779B9u;
+    h ^= h >> 16;
+    return gmf::asfloat((h & 0x807fffffu) | (((h >> 7) % 254u + 1u) << 23));   // a finite float from u
+}
+
+__global__ void k_probe(uint64_t start, uint64_t stride, uint32_t n, float *outG, float *outO) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float4 a = in[i];
-    const float x = a.x, y = a.y, z = a.z, p = a.w;
-    const float q = fabsf(a.w) * 0.375f + 1e-3f;   // log / pow base in (0, 1.5]
-    float s, c;
-    sincosf(x, &s, &c);
-    float f[NF] = {s, c, acosf(y), atan2f(y, z), expf(x), logf(q), powf(q, p), tanf(x * 0.25f), atanf(x)};
-    float d[NF] = {(float)sin((double)x), (float)cos((double)x), (float)acos((double)y), (float)atan2((double)y, (double)z),
-                   (float)exp((double)x), (float)log((double)q), (float)pow((double)q, (double)p),
-                   (float)tan((double)(x * 0.25f)), (float)atan((double)x)};
+    const uint32_t u = (uint32_t)(start + (uint64_t)i * stride);
+    const float x = gmf::asfloat(u), y = arg_y(u);
+    const float g[NF] = {gmf::sinf(x), gmf::cosf(x), gmf::tanf(x), gmf::expf(x), gmf::logf(x), gmf::atanf(x),
+                         gmf::acosf(x), gmf::atan2f(x, y)};
+    const float o[NF] = {sinf(x), cosf(x), tanf(x), expf(x), logf(x), atanf(x), acosf(x), atan2f(x, y)};
     for (int k = 0; k < NF; ++k) {
-        outF[(size_t)k * n + i] = f[k];
-        outD[(size_t)k * n + i] = d[k];
+        outG[(size_t)k * n + i] = g[k];
+        outO[(size_t)k * n + i] = o[k];
     }
 }
 
+static bool same(float a, float b) {
+    if (a != a || b != b) return a != a && b != b;
+    return gmf::asuint(a) == gmf::asuint(b);
+}
+
 int main(int argc, char **argv) {
-    const int n = argc > 1 ? atoi(argv[1]) : 4000000;
-    std::vector<float4> in(n);
-    uint64_t st = 88172645463325252ull;
-    auto rnd = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return (st >> 11) * (1.0 / 9007199254740992.0); };
-    for (int i = 0; i < n; ++i)
-        in[i] = make_float4((float)((rnd() * 2 - 1) * 6.3), (float)(rnd() * 2 - 1), (float)(rnd() * 2 - 1), (float)(rnd() * 4));
-    float4 *din; float *dF, *dD;
-    if (hipMalloc(&din, sizeof(float4) * n) || hipMalloc(&dF, sizeof(float) * NF * n) || hipMalloc(&dD, sizeof(float) * NF * n)) return 2;
-    hipMemcpy(din, in.data(), sizeof(float4) * n, hipMemcpyHostToDevice);
-    hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, 0, din, dF, dD, n);
-    if (hipDeviceSynchronize() != hipSuccess) return 3;
-    std::vector<float> F((size_t)NF * n), D((size_t)NF * n);
-    hipMemcpy(F.data(), dF, sizeof(float) * NF * n, hipMemcpyDeviceToHost);
-    hipMemcpy(D.data(), dD, sizeof(float) * NF * n, hipMemcpyDeviceToHost);
-    long mF[NF] = {0}, mD[NF] = {0}, mFD[NF] = {0};
-    for (int i = 0; i < n; ++i) {
-        const float x = in[i].x, y = in[i].y, z = in[i].z, p = in[i].w, q = fabsf(in[i].w) * 0.375f + 1e-3f;
-        float s, c;
-        sincosf(x, &s, &c);
-        const float g[NF] = {s, c, acosf(y), atan2f(y, z), expf(x), logf(q), powf(q, p), tanf(x * 0.25f), atanf(x)};
-        for (int k = 0; k < NF; ++k) {
-            const float f = F[(size_t)k * n + i], d = D[(size_t)k * n + i];
-            mF[k] += f != g[k];
-            mD[k] += d != g[k];
-            mFD[k] += f != d;
-        }
+    const uint64_t stride = argc > 1 ? strtoull(argv[1], nullptr, 0) : 3;
+    const uint32_t chunk = 1u << 24;
+    float *dG, *dO;
+    if (hipMalloc(&dG, sizeof(float) * NF * chunk) || hipMalloc(&dO, sizeof(float) * NF * chunk)) return 2;
+    std::vector<float> G((size_t)NF * chunk), O((size_t)NF * chunk);
+    uint64_t badG[NF] = {0}, badO[NF] = {0}, total = 0;
+    uint32_t firstG[NF];
+    for (int k = 0; k < NF; ++k) firstG[k] = 0xffffffffu;
+    const int nth = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    for (uint64_t start = 0; start < (1ull << 32); start += (uint64_t)chunk * stride) {
+        const uint32_t n = (uint32_t)std::min<uint64_t>(chunk, ((1ull << 32) - start + stride - 1) / stride);
+        hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, 0, start, stride, n, dG, dO);
+        if (hipDeviceSynchronize() != hipSuccess) { fprintf(stderr, "kernel failed\n"); return 3; }
+        hipMemcpy(G.data(), dG, sizeof(float) * NF * n, hipMemcpyDeviceToHost);
+        hipMemcpy(O.data(), dO, sizeof(float) * NF * n, hipMemcpyDeviceToHost);
+        std::vector<std::thread> th;
+        std::vector<uint64_t> bG((size_t)nth * NF, 0), bO((size_t)nth * NF, 0);
+        std::vector<uint32_t> fG((size_t)nth * NF, 0xffffffffu);
+        for (int t = 0; t < nth; ++t)
+            th.emplace_back([&, t]() {
+                for (uint32_t i = t; i < n; i += nth) {
+                    const uint32_t u = (uint32_t)(start + (uint64_t)i * stride);
+                    const float x = gmf::asfloat(u), y = arg_y(u);
+                    const float ref[NF] = {::sinf(x), ::cosf(x), ::tanf(x), ::expf(x), ::logf(x), ::atanf(x), ::acosf(x),
+                                           ::atan2f(x, y)};
+                    for (int k = 0; k < NF; ++k) {
+                        if (!same(G[(size_t)k * n + i], ref[k])) {
+                            if (bG[t * NF + k]++ == 0) fG[t * NF + k] = u;
+                        }
+                        bO[t * NF + k] += !same(O[(size_t)k * n + i], ref[k]);
+                    }
+                }
+            });
+        for (auto &x : th) x.join();
+        for (int t = 0; t < nth; ++t)
+            for (int k = 0; k < NF; ++k) {
+                badG[k] += bG[t * NF + k];
+                badO[k] += bO[t * NF + k];
+                if (fG[t * NF + k] < firstG[k]) firstG[k] = fG[t * NF + k];
+            }
+        total += n;
+        fprintf(stderr, "\r%.0f%%", 100.0 * (double)(start + (uint64_t)chunk * stride) / 4294967296.0);
     }
-    printf("%-6s %14s %14s %14s\n", "fn", "ocml!=glibc", "cr!=glibc", "ocml!=cr");
-    for (int k = 0; k < NF; ++k)
-        printf("%-6s %14.3e %14.3e %14.3e\n", kName[k], mF[k] / (double)n, mD[k] / (double)n, mFD[k] / (double)n);
-    hipFree(din); hipFree(dF); hipFree(dD);
-    return 0;
+    fprintf(stderr, "\n");
+    printf("%llu arguments (every %llu-th float bit pattern), device vs this host's glibc, bit for bit\n",
+           (unsigned long long)total, (unsigned long long)stride);
+    printf("%-7s %16s %16s\n", "fn", "gmf!=glibc", "ocml!=glibc");
+    int fails = 0;
+    for (int k = 0; k < NF; ++k) {
+        printf("%-7s %16llu %16llu", kName[k], (unsigned long long)badG[k], (unsigned long long)badO[k]);
+        if (badG[k]) { printf("   first 0x%08x", firstG[k]); ++fails; }
+        printf("\n");
+    }
+    hipFree(dG);
+    hipFree(dO);
+    return fails ? 1 : 0;
 }
