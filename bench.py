@@ -292,13 +292,28 @@ def gather_frame(pg, rank, world, part, tile_w, tile_h, border):
     return frame
 
 
+def interior_pixels(sel, border):
+    """The pixels of the selected tiles whose reconstruction-filter footprint
+    (radius `border`) lies in selected tiles only: in the frame they receive
+    samples of the selected tiles alone, as in the oracle's block of those
+    tiles (outside the frame nothing is splatted on either side)."""
+    h, w = sel.shape
+    pad = np.pad(sel, border, constant_values=True)
+    ok = sel.copy()
+    for dy in range(-border, border + 1):
+        for dx in range(-border, border + 1):
+            ok &= pad[border + dy:border + dy + h, border + dx:border + dx + w]
+    return ok
+
+
 def parity_at_headline(scene, frame, params, border, stride, world):
     """Per-pixel L1 of the GPU frame vs the CPU oracle at the full spp.  `frame`
     is the ImageBlock the timed steps produced, assembled from every rank's
     tiles; the oracle renders the tiles of parity_keys (1/stride of the frame,
     every pixel of them, all samples) in counter mode (identical random numbers
     per pixel / sample / dimension); both are developed (sum w L / sum w) and
-    compared on those pixels.  Runs after the timed region."""
+    compared on those of their pixels that receive no sample of another tile
+    (interior_pixels).  Runs after the timed region."""
     import mtsg
     from oracle import pyoracle as O
     mod, below = parity_keys(world, stride)
@@ -315,7 +330,7 @@ def parity_at_headline(scene, frame, params, border, stride, world):
     b = border
     rgb_g = mtsg.develop(frame[b:b + p.tile_h, b:b + p.tile_w])
     rgb_c = mtsg.develop(img_c[b:b + p.tile_h, b:b + p.tile_w])
-    own = (mtsg.tile_deal_keys(p.tile_w, p.tile_h) % mod) < below
+    own = interior_pixels((mtsg.tile_deal_keys(p.tile_w, p.tile_h) % mod) < below, border)
     d = np.abs(rgb_g - rgb_c)[own]
     l1 = float(d.mean())
     mean = float(rgb_c[own].mean())
@@ -327,7 +342,8 @@ def parity_at_headline(scene, frame, params, border, stride, world):
     return {"l1": l1, "mean": round(mean, 6), "l1_rel_mean": l1 / max(mean, 1e-12),
             "max_abs": float(d.max()), "per_pixel": dist, "pixels": int(own.sum()), "spp": int(p.spp),
             "samples": int(samples),
-            "tiles": (f"16x16 tiles with deal key % {mod} < {below} of {p.tile_w}x{p.tile_h}"
+            "tiles": (f"16x16 tiles with deal key % {mod} < {below} of {p.tile_w}x{p.tile_h}, the pixels whose "
+                      f"{2 * border + 1}x{2 * border + 1} filter window lies in those tiles"
                       + (f" ({below // world} per rank's share), from the frame assembled from all {world} ranks"
                          if world > 1 else ", from the timed steps' last frame")),
             "bar": "l1 < 1e-3 (and l1_rel_mean < 1e-3)", "pass": bool(l1 < 1e-3 and l1 < 1e-3 * max(mean, 1e-12)),

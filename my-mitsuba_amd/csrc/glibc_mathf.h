@@ -33,7 +33,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifndef GMF_NOINLINE
+#define GMF_NOINLINE 0   // 1: the entry points are out-of-line calls (measurement variant)
+#endif
 #define GMF __host__ __device__ __forceinline__
+#if GMF_NOINLINE
+#define GMF_ENTRY __host__ __device__ inline __attribute__((noinline))
+#else
+#define GMF_ENTRY GMF
+#endif
 // the large-argument reductions are rare: kept out of line, so they do not
 // add to the register pressure of the shading kernels that call sinf / tanf
 #define GMF_COLD __host__ __device__ inline __attribute__((noinline))
@@ -57,15 +65,16 @@ constexpr double kS1 = -0x1.555545995a603p-3, kS2 = 0x1.1107605230bc4p-7, kS3 = 
 constexpr double kPi63 = 0x1.921FB54442D18p-62;     // 2pi * 2^-64
 constexpr float kPio4f = 0x1.921FB6p-1f;
 
-// sinf_poly: n even -> the sine polynomial, odd -> the cosine one
-GMF float sinf_poly(double x, double x2, bool neg, int n) {
-    if ((n & 1) == 0) {
-        const double x3 = x * x2;
-        const double s1 = fma(x2, kS3, kS2);
-        const double x7 = x3 * x2;
-        const double s = fma(x3, kS1, x);
-        return (float)fma(x7, s1, s);
-    }
+// the two polynomials of sinf_poly / sincosf_poly: the sine one on x, the
+// cosine one on x2 (coefficients negated when `neg`: table entry [1])
+GMF double sin_poly(double x, double x2) {
+    const double x3 = x * x2;
+    const double s1 = fma(x2, kS3, kS2);
+    const double x7 = x3 * x2;
+    const double s = fma(x3, kS1, x);
+    return fma(x7, s1, s);
+}
+GMF double cos_poly(double x2, bool neg) {
     const double c0 = neg ? -kC0 : kC0, c1 = neg ? -kC1 : kC1, c2 = neg ? -kC2 : kC2,
                  c3 = neg ? -kC3 : kC3, c4 = neg ? -kC4 : kC4;
     const double x4 = x2 * x2;
@@ -73,7 +82,12 @@ GMF float sinf_poly(double x, double x2, bool neg, int n) {
     const double cc1 = fma(x2, c1, c0);
     const double x6 = x4 * x2;
     const double c = fma(x4, c2, cc1);
-    return (float)fma(x6, cc2, c);
+    return fma(x6, cc2, c);
+}
+
+// sinf_poly: n even -> the sine polynomial, odd -> the cosine one
+GMF float sinf_poly(double x, double x2, bool neg, int n) {
+    return (float)((n & 1) ? cos_poly(x2, neg) : sin_poly(x, x2));
 }
 
 // reduce_fast: |x| < 120, quadrant by scaled float-to-int conversion
@@ -128,13 +142,13 @@ GMF_COLD void sincosf_large(float y, float *sinp, float *cosp) {
 // sincosf (s_sincosf.c): the sine and cosine polynomials of sinf / cosf on one
 // reduction (sincosf_poly performs the same operations as sinf_poly, so each
 // result equals the separate sinf / cosf call)
-GMF void sincosf(float y, float *sinp, float *cosp) {
+GMF_ENTRY void sincosf(float y, float *sinp, float *cosp) {
     const uint32_t top = abstop12(y);
     if (top < abstop12(kPio4f)) {
         if (top < abstop12(0x1p-12f)) { *sinp = y; *cosp = 1.0f; return; }
         const double x = y, x2 = x * x;
-        *sinp = sinf_poly(x, x2, false, 0);
-        *cosp = sinf_poly(x, x2, false, 1);
+        *sinp = (float)sin_poly(x, x2);
+        *cosp = (float)cos_poly(x2, false);
         return;
     }
     if (top >= abstop12(120.0f)) {
@@ -146,8 +160,10 @@ GMF void sincosf(float y, float *sinp, float *cosp) {
     const double x = reduce_fast((double)y, n);
     const double xs = ((n + 1) & 2) ? -x : x;   // sign[n & 3] = {1, -1, -1, 1}
     const double x2 = x * x;
-    *sinp = sinf_poly(xs, x2, (n & 2) != 0, n);
-    *cosp = sinf_poly(xs, x2, (n & 2) != 0, n ^ 1);
+    // both polynomials, swapped for odd quadrants (no divergent branch)
+    const float ps = (float)sin_poly(xs, x2), pc = (float)cos_poly(x2, (n & 2) != 0);
+    *sinp = (n & 1) ? pc : ps;
+    *cosp = (n & 1) ? ps : pc;
 }
 
 GMF float sinf(float y) { float s, c; gmf::sincosf(y, &s, &c); return s; }
@@ -165,7 +181,7 @@ constexpr uint64_t kExp2fTab[32] = {
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
 
-GMF float expf(float x) {
+GMF_ENTRY float expf(float x) {
     const double xd = (double)x;
     const uint32_t abstop = abstop12(x) & 0x7ff;
     if (abstop >= abstop12(88.0f)) {
@@ -199,7 +215,7 @@ GMF float expf(float x) {
 constexpr double kLogfInvc[16] = {0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0, 0x1.3c995b0b80385p+0, 0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0, 0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0, 0x1.0953f419900a7p+0, 0x1p+0, 0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1, 0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
 constexpr double kLogfLogc[16] = {-0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2, -0x1.b31d8a68224e9p-3, -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c81p-3, -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611cccp-4, -0x1.252f438e10c1ep-5, 0x0p+0, 0x1.aa5aa5df25984p-5, 0x1.c5e53aa362eb4p-4, 0x1.526e57720db08p-3, 0x1.bc2860d22477p-3, 0x1.1058bc8a07ee1p-2, 0x1.4043057b6ee09p-2};
 
-GMF float logf(float x) {
+GMF_ENTRY float logf(float x) {
     uint32_t ix = asuint(x);
     if (ix == 0x3f800000u) return 0.0f;
     if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
@@ -231,42 +247,42 @@ GMF float logf(float x) {
 constexpr float kAtanHi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
 constexpr float kAtanLo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
 
-GMF float atanf(float x) {
+GMF_ENTRY float atanf(float x) {
     constexpr float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
                     aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
                     aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
                     aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
     const int32_t hx = (int32_t)asuint(x);
     const int32_t ix = hx & 0x7fffffff;
-    int id;
     if (ix >= 0x4c000000) {   // |x| >= 2^25
         if (ix > 0x7f800000) return x + x;
         return hx > 0 ? kAtanHi[3] + kAtanLo[3] : -kAtanHi[3] - kAtanLo[3];
     }
-    if (ix < 0x3ee00000) {   // |x| < 0.4375
-        if (ix < 0x31000000) return x;   // |x| < 2^-29
-        id = -1;
-    } else {
-        x = fabsf(x);
-        if (ix < 0x3f980000) {          // |x| < 1.1875
-            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); }
-            else { id = 1; x = (x - 1.0f) / (x + 1.0f); }
-        } else {
-            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); }
-            else { id = 3; x = -1.0f / x; }
-        }
-    }
-    const float z = x * x;
+    if (ix < 0x31000000) return x;   // |x| < 2^-29
+    // the argument reduction of each range, as one division of selected
+    // operands (the same float operations as s_atanf.c's branches):
+    //   id -1 |x| < 0.4375        none
+    //   id 0  [0.4375, 0.6875)    (2|x| - 1) / (2 + |x|)
+    //   id 1  [0.6875, 1.1875)    (|x| - 1) / (|x| + 1)
+    //   id 2  [1.1875, 2.4375)    (|x| - 1.5) / (1 + 1.5|x|)
+    //   id 3  [2.4375, 2^25)      -1 / |x|
+    const float ax = fabsf(x);
+    const int id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
+    const float num = id == 0 ? 2.0f * ax - 1.0f : id == 1 ? ax - 1.0f : id == 2 ? ax - 1.5f : -1.0f;
+    const float den = id == 0 ? 2.0f + ax : id == 1 ? ax + 1.0f : id == 2 ? 1.0f + 1.5f * ax : ax;
+    const float q = num / den;
+    const float xr = id < 0 ? x : q;
+    const float z = xr * xr;
     const float w = z * z;
     const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
     const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    if (id < 0) return x - x * (s1 + s2);
-    const float zz = kAtanHi[id] - ((x * (s1 + s2) - kAtanLo[id]) - x);
+    if (id < 0) return xr - xr * (s1 + s2);
+    const float zz = kAtanHi[id] - ((xr * (s1 + s2) - kAtanLo[id]) - xr);
     return hx < 0 ? -zz : zz;
 }
 
 // ---- atan2f (e_atan2f.c) ---------------------------------------------------
-GMF float atan2f(float y, float x) {
+GMF_ENTRY float atan2f(float y, float x) {
     constexpr float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
                     pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
     const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff;
@@ -310,7 +326,7 @@ GMF float atan2f(float y, float x) {
 }
 
 // ---- acosf (e_acosf.c) -----------------------------------------------------
-GMF float acosf(float x) {
+GMF_ENTRY float acosf(float x) {
     constexpr float pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f,
                     pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f,
                     pS3 = -4.0055535734e-02f, pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f,
@@ -319,30 +335,23 @@ GMF float acosf(float x) {
     const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff;
     if (ix == 0x3f800000) return hx > 0 ? 0.0f : pi + 2.0f * pio2_lo;
     if (ix > 0x3f800000) return (x - x) / (x - x);
-    if (ix < 0x3f000000) {   // |x| < 0.5
-        if (ix <= 0x23000000) return pio2_hi + pio2_lo;
-        const float z = x * x;
-        const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-        const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        const float r = p / q;
-        return pio2_hi - (x - (pio2_lo - x * r));
-    }
-    if (hx < 0) {            // x < -0.5
-        const float z = (1.0f + x) * 0.5f;
-        const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-        const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        const float s = sqrtf(z);
-        const float r = p / q;
-        const float w = r * s - pio2_lo;
-        return pi - 2.0f * (s + w);
-    }
-    const float z = (1.0f - x) * 0.5f;   // x > 0.5
-    const float s = sqrtf(z);
-    const float df = asfloat(asuint(s) & 0xfffff000u);
-    const float c = (z - df * df) / (s + df);
+    if (ix <= 0x23000000) return pio2_hi + pio2_lo;
+    // e_acosf.c's three ranges on one rational approximation: z = x^2
+    // (|x| < 0.5), (1 + x) / 2 (x <= -0.5), (1 - x) / 2 (x >= 0.5); each
+    // range's own combination below, selected
+    const bool small = ix < 0x3f000000;
+    const float z = small ? x * x : hx < 0 ? (1.0f + x) * 0.5f : (1.0f - x) * 0.5f;
     const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
     const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
     const float r = p / q;
+    if (small) return pio2_hi - (x - (pio2_lo - x * r));
+    const float s = sqrtf(z);
+    if (hx < 0) {
+        const float w = r * s - pio2_lo;
+        return pi - 2.0f * (s + w);
+    }
+    const float df = asfloat(asuint(s) & 0xfffff000u);
+    const float c = (z - df * df) / (s + df);
     const float w = r * s + c;
     return 2.0f * (df + w);
 }
@@ -388,7 +397,8 @@ GMF float kernel_tanf(float x, float y, int iy) {
             return -1.0f / x;
         }
     }
-    if (ix >= 0x3f2ca140) {   // |x| >= 0.6744
+    const bool big = ix >= 0x3f2ca140;   // |x| >= 0.6744: tan(pi/4 - |x|) form
+    if (big) {
         if (hx < 0) { x = -x; y = -y; }
         const float z = pio4 - x;
         const float w = pio4lo - y;
@@ -404,21 +414,20 @@ GMF float kernel_tanf(float x, float y, int iy) {
     r = y + z * (s * (r + v) + y);
     r += T0 * s;
     w = x + r;
-    if (ix >= 0x3f2ca140) {
-        v = (float)iy;
-        return (float)(1 - ((hx >> 30) & 2)) * (v - 2.0f * (x - (w * w / (w + v) - r)));
-    }
-    if (iy == 1) return w;
-    // -1/(x+r) computed accurately
+    if (!big && iy == 1) return w;
+    // the one division of either final form: w^2 / (w + iy) (big), -1 / w
+    const float vi = (float)iy;
+    const float q = big ? (w * w) / (w + vi) : -1.0f / w;
+    if (big) return (float)(1 - ((hx >> 30) & 2)) * (vi - 2.0f * (x - (q - r)));
+    // -1/(x+r) accurately: a = q
     const float zz = asfloat(asuint(w) & 0xfffff000u);
     v = r - (zz - x);
-    const float a = -1.0f / w;
-    const float t = asfloat(asuint(a) & 0xfffff000u);
+    const float t = asfloat(asuint(q) & 0xfffff000u);
     const float ss = 1.0f + t * zz;
-    return t + a * (ss + t * v);
+    return t + q * (ss + t * v);
 }
 
-GMF float tanf(float x) {
+GMF_ENTRY float tanf(float x) {
     const int32_t ix = (int32_t)asuint(x) & 0x7fffffff;
     if (ix <= 0x3f490fda) return kernel_tanf(x, 0.0f, 1);
     if (ix >= 0x7f800000) return x - x;

@@ -23,6 +23,10 @@ for w in ${*:-tests bench}; do
       step ranks-torchrun 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu --allow-shared
       step ranks-self 600 python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu --allow-shared
       echo "== ranks-refuse"; timeout -k 10 300 python bench.py --gpus 2 --steps 1 --warmup 0 --no-cpu > $O/ranks-refuse.log 2>&1; echo "ranks-refuse rc=$? (non-zero expected)"; tail -n 2 $O/ranks-refuse.log ;;
+    bench-ocml) MTSG_LIB=my-mitsuba_amd/var/libmtsg_ocmlmath.so step bench-ocml 600 python bench.py --steps 10 --warmup 3 --no-cpu ;;
+    c5-ocml) MTSG_LIB=my-mitsuba_amd/var/libmtsg_ocmlmath.so step c5-ocml 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu ;;
+    bench-mathcall) MTSG_LIB=my-mitsuba_amd/var/libmtsg_mathcall.so step bench-mathcall 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity ;;
+    c5-mathcall) MTSG_LIB=my-mitsuba_amd/var/libmtsg_mathcall.so step c5-mathcall 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity ;;
     c5) step c5 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 ;;
     c2) step c2 600 python bench.py --steps 5 --warmup 2 --workload cbox ;;
     kd) step kd 300 python bench.py --steps 5 --warmup 2 --kd-build device --no-cpu --no-parity ;;
