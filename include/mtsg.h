@@ -548,6 +548,18 @@ void mtsg_cancel(mtsg_scene *scene);
  * the end of their renders, as libmtsg_path's job does. */
 void mtsg_cancel_clear(mtsg_scene *scene);
 
+/* Tile completion: after `fn` is set, mtsg_render / mtsg_render_device /
+ * mtsg_render_device_tiles call fn(user, key, x, y, w, h) on the rendering
+ * thread once per 16x16 tile of the call, when the last of its samples has
+ * been splatted into the ImageBlock (its deal key and its rectangle in film
+ * pixels, inside the params' rectangle).  The plugin's hook for
+ * RenderQueue::signalWorkEnd and the progress reporter
+ * (BlockedRenderProcess::processResult, renderproc.cpp:144-154,179): a
+ * batch's tiles complete together (the whole frame is one batch unless
+ * mtsg_set_batch_paths makes them smaller).  fn = NULL removes it. */
+typedef void (*mtsg_tile_fn)(void *user, int32_t key, int32_t x, int32_t y, int32_t w, int32_t h);
+int  mtsg_set_tile_callback(mtsg_scene *scene, mtsg_tile_fn fn, void *user);
+
 int  mtsg_set_flags(mtsg_scene *scene, uint32_t flags);
 int  mtsg_get_stats(mtsg_scene *scene, mtsg_stats *out);
 /* Debug: rays of the last MTSG_FLAG_COUNT render that needed >= 300

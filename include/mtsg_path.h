@@ -49,6 +49,14 @@ int mtsh_path_job_gpus(const mtsh_path_job *job);
 int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, float *rgbaw_out,
                          double *seconds_out);
 
+/* Tile completion of the job's renders: fn(user, gpu, x, y, w, h) once per
+ * 16x16 tile when its ImageBlock contribution is complete on GPU `gpu` (see
+ * mtsg_set_tile_callback); calls from the job's GPU threads are serialised,
+ * so fn need not be thread-safe.  The plugin's RenderQueue::signalWorkEnd /
+ * progress hook (renderproc.cpp:144-154,179).  fn = NULL removes it. */
+typedef void (*mtsh_path_tile_fn)(void *user, int32_t gpu, int32_t x, int32_t y, int32_t w, int32_t h);
+int mtsh_path_job_set_tile_callback(mtsh_path_job *job, mtsh_path_tile_fn fn, void *user);
+
 /* Cancel the job's running render (async-safe; no effect when idle). */
 void mtsh_path_job_cancel(mtsh_path_job *job);
 

@@ -38,16 +38,20 @@ mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_
  * finalised, so the device renders the film, sample count and integrator
  * parameters the user asked for.  `mask` selects the groups that apply. */
 enum {
-    MTSH_OVERRIDE_FILM_SIZE    = 1,   /* Film::getSize (crop = the full film)       */
+    MTSH_OVERRIDE_FILM_SIZE    = 1,   /* Film::getSize (crop = the full film unless */
+                                      /* FILM_CROP is given too)                    */
     MTSH_OVERRIDE_SAMPLE_COUNT = 2,   /* Sampler::getSampleCount                    */
-    MTSH_OVERRIDE_INTEGRATOR   = 4    /* MonteCarloIntegrator m_maxDepth, m_rrDepth, */
+    MTSH_OVERRIDE_INTEGRATOR   = 4,   /* MonteCarloIntegrator m_maxDepth, m_rrDepth, */
                                       /* m_strictNormals, m_hideEmitters            */
+    MTSH_OVERRIDE_FILM_CROP    = 8    /* Film::getCropOffset / getCropSize          */
+                                      /* (film.cpp:36-48)                           */
 };
 typedef struct mtsh_scene_overrides {
     uint32_t mask;
     int32_t film_width, film_height;
     int32_t sample_count;
     int32_t max_depth, rr_depth, strict_normals, hide_emitters;
+    int32_t crop_x, crop_y, crop_width, crop_height;   /* MTSH_OVERRIDE_FILM_CROP */
 } mtsh_scene_overrides;
 
 /* mtsh_scene_load, then the overrides (may be NULL) before finalisation. */

@@ -67,6 +67,8 @@ int upload(const T *src, size_t n, T **dst) {
 
 struct mtsg_scene {
     int device = 0;
+    mtsg_tile_fn tileFn = nullptr;   // tile completion (mtsg_set_tile_callback)
+    void *tileUser = nullptr;
     hipStream_t stream = nullptr;
     DevScene ds{};
     DevCamera cam{};
@@ -591,6 +593,22 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
             if (err) {
                 g_err = dim_error(s->samplerType);
                 return MTSG_ERR_INVALID;
+            }
+        }
+        if (s->tileFn) {
+            // the tiles whose last samples this batch splatted are complete
+            for (uint32_t l = 0; l < nb; ++l) {
+                HIP_TRY(hipStreamSynchronize(s->lstream[l]));
+                const DevBatch &B = lr[l].B;
+                if (B.s0 + B.ns < p->spp) continue;
+                for (int tl = 0; tl < B.ntiles; ++tl) {
+                    const int key = B.toffset + (B.tile0 + tl) * B.tstride;
+                    int tx, ty;
+                    tile_of_key(key, B.tiles_x, tx, ty, B.skew);
+                    const int x = tx * TILE, y = ty * TILE;
+                    s->tileFn(s->tileUser, key, p->tile_x + x, p->tile_y + y, std::min(TILE, p->tile_w - x),
+                              std::min(TILE, p->tile_h - y));
+                }
             }
         }
         if (s->dumpL) {
@@ -1170,6 +1188,13 @@ int mtsg_debug_stragglers(mtsg_scene *s, float *out, uint32_t max_rays) {
         o[11] = 0.0f;
     }
     return (int)n;
+}
+
+int mtsg_set_tile_callback(mtsg_scene *s, mtsg_tile_fn fn, void *user) {
+    if (!s) return MTSG_ERR_INVALID;
+    s->tileFn = fn;
+    s->tileUser = user;
+    return MTSG_OK;
 }
 
 void mtsg_cancel_clear(mtsg_scene *s) {

@@ -400,8 +400,12 @@ void Scene::finalize() {
 
     // ---------------- sensor / film ----------------
     Film &f = film;
-    if (f.cropX != 0 || f.cropY != 0 || f.cropW != f.width || f.cropH != f.height)
-        throw std::runtime_error("hdrfilm crop windows are outside this build's scope");
+    // Film::Film's check (film.cpp:44-48); the crop window is the rectangle
+    // the render params cover (mtsh_scene_render_params), the camera keeps the
+    // full film's projection
+    if (f.cropX < 0 || f.cropY < 0 || f.cropW <= 0 || f.cropH <= 0 || f.cropX + f.cropW > f.width ||
+        f.cropY + f.cropH > f.height)
+        throw std::runtime_error("Invalid crop window specification!");
     mtsg_camera &cam = camera;
     memset(&cam, 0, sizeof(cam));
     float aspect = (float)f.width / (float)f.height;

@@ -1587,13 +1587,30 @@ std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::st
         if (e.type == MTSG_EMITTER_AREA && e.shape < 0) throw err("area emitter without a parent shape");
     if (ov) {
         // the in-memory values of a Mitsuba plugin (mtsh.h mtsh_scene_overrides)
-        if (ov->mask & MTSH_OVERRIDE_FILM_SIZE) {
+        if (ov->mask & (MTSH_OVERRIDE_FILM_SIZE | MTSH_OVERRIDE_FILM_CROP)) {
             Film &f = scene->film;
-            if (ov->film_width <= 0 || ov->film_height <= 0) throw err("override: film size must be positive");
-            if (f.cropX != 0 || f.cropY != 0 || f.cropW != f.width || f.cropH != f.height)
-                throw err("hdrfilm crop windows are outside this build's scope");
-            f.width = f.cropW = ov->film_width;
-            f.height = f.cropH = ov->film_height;
+            if (ov->mask & MTSH_OVERRIDE_FILM_SIZE) {
+                if (ov->film_width <= 0 || ov->film_height <= 0) throw err("override: film size must be positive");
+                // a new size without a crop: the crop is the whole film (the
+                // XML's crop no longer fits a film of another size)
+                if (!(ov->mask & MTSH_OVERRIDE_FILM_CROP) &&
+                    (f.cropX != 0 || f.cropY != 0 || f.cropW != f.width || f.cropH != f.height) &&
+                    (ov->film_width != f.width || ov->film_height != f.height))
+                    throw err("override: the film size changes but the XML's crop window is kept; pass the crop "
+                              "(MTSH_OVERRIDE_FILM_CROP) too");
+                if (!(ov->mask & MTSH_OVERRIDE_FILM_CROP) && f.cropW == f.width && f.cropH == f.height) {
+                    f.cropW = ov->film_width;
+                    f.cropH = ov->film_height;
+                }
+                f.width = ov->film_width;
+                f.height = ov->film_height;
+            }
+            if (ov->mask & MTSH_OVERRIDE_FILM_CROP) {
+                f.cropX = ov->crop_x;
+                f.cropY = ov->crop_y;
+                f.cropW = ov->crop_width;
+                f.cropH = ov->crop_height;
+            }
         }
         if (ov->mask & MTSH_OVERRIDE_SAMPLE_COUNT) {
             if (ov->sample_count <= 0) throw err("sampleCount must be > 0");

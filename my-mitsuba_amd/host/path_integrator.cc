@@ -41,8 +41,22 @@ struct mtsh_path_job {
     std::vector<int> rendering, sent;
     std::vector<std::mutex> gpuLock;
     std::mutex renderLock;   // one render at a time per job
+    // tile completion: the caller's hook, serialised over the GPU threads
+    mtsh_path_tile_fn tileFn = nullptr;
+    void *tileUser = nullptr;
+    std::mutex tileLock;
+    struct TileCtx { mtsh_path_job *job; int gpu; };
+    std::vector<TileCtx> tileCtx;
     explicit mtsh_path_job(int n) : rendering(n, 0), sent(n, 0), gpuLock(n) {}
 };
+
+namespace {
+void tile_trampoline(void *user, int32_t, int32_t x, int32_t y, int32_t w, int32_t h) {
+    auto *c = static_cast<mtsh_path_job::TileCtx *>(user);
+    std::lock_guard<std::mutex> lock(c->job->tileLock);
+    if (c->job->tileFn) c->job->tileFn(c->job->tileUser, c->gpu, x, y, w, h);
+}
+}  // namespace
 
 extern "C" {
 
@@ -75,6 +89,22 @@ int mtsh_path_job_create(const mtsh_scene *scene, int n_gpus, mtsh_path_job **ou
 }
 
 int mtsh_path_job_gpus(const mtsh_path_job *job) { return job ? (int)job->handles.size() : 0; }
+
+int mtsh_path_job_set_tile_callback(mtsh_path_job *job, mtsh_path_tile_fn fn, void *user) {
+    if (!job) { g_perr = "null argument"; return MTSG_ERR_INVALID; }
+    std::lock_guard<std::mutex> lock(job->renderLock);   // not while a render runs
+    {
+        std::lock_guard<std::mutex> tl(job->tileLock);
+        job->tileFn = fn;
+        job->tileUser = user;
+    }
+    job->tileCtx.resize(job->handles.size());
+    for (size_t g = 0; g < job->handles.size(); ++g) {
+        job->tileCtx[g] = {job, (int)g};
+        mtsg_set_tile_callback(job->handles[g], fn ? tile_trampoline : nullptr, fn ? &job->tileCtx[g] : nullptr);
+    }
+    return MTSG_OK;
+}
 
 int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, float *rgbaw_out,
                          double *seconds_out) {

@@ -147,10 +147,11 @@ class SceneOverrides(C.Structure):
     """mtsh_scene_overrides: the values a Mitsuba plugin holds in memory."""
     _fields_ = [("mask", C.c_uint32), ("film_width", C.c_int32), ("film_height", C.c_int32),
                 ("sample_count", C.c_int32), ("max_depth", C.c_int32), ("rr_depth", C.c_int32),
-                ("strict_normals", C.c_int32), ("hide_emitters", C.c_int32)]
+                ("strict_normals", C.c_int32), ("hide_emitters", C.c_int32),
+                ("crop_x", C.c_int32), ("crop_y", C.c_int32), ("crop_width", C.c_int32), ("crop_height", C.c_int32)]
 
 
-MTSH_OVERRIDE_FILM_SIZE, MTSH_OVERRIDE_SAMPLE_COUNT, MTSH_OVERRIDE_INTEGRATOR = 1, 2, 4
+MTSH_OVERRIDE_FILM_SIZE, MTSH_OVERRIDE_SAMPLE_COUNT, MTSH_OVERRIDE_INTEGRATOR, MTSH_OVERRIDE_FILM_CROP = 1, 2, 4, 8
 
 _host = None
 _dev = None
@@ -162,7 +163,7 @@ DEVICE_SYMBOLS = [
     "mtsg_cancel", "mtsg_cancel_clear", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
     "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_kd_build", "mtsg_kd_free",
-    "mtsg_sampler_draws", "mtsg_debug_wavetimes",
+    "mtsg_sampler_draws", "mtsg_debug_wavetimes", "mtsg_set_tile_callback",
     "mtsg_debug_stragglers",
 ]
 HOST_SYMBOLS = [
@@ -173,8 +174,11 @@ HOST_SYMBOLS = [
 ]
 PATH_SYMBOLS = [
     "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
-    "mtsh_path_job_destroy", "mtsh_path_render", "mtsh_path_last_error",
+    "mtsh_path_job_destroy", "mtsh_path_render", "mtsh_path_last_error", "mtsh_path_job_set_tile_callback",
 ]
+
+# tile completion hooks (mtsg_set_tile_callback, mtsh_path_job_set_tile_callback)
+TILE_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32)
 _path = None
 
 
@@ -193,6 +197,7 @@ def path_lib() -> C.CDLL:
                                              C.POINTER(C.c_double)]
         lib.mtsh_path_job_cancel.argtypes = [C.c_void_p]
         lib.mtsh_path_job_destroy.argtypes = [C.c_void_p]
+        lib.mtsh_path_job_set_tile_callback.argtypes = [C.c_void_p, TILE_FN, C.c_void_p]
         lib.mtsh_path_render.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p,
                                          C.POINTER(C.c_double)]
         lib.mtsh_path_last_error.argtypes = [C.c_char_p, C.c_size_t]
@@ -280,6 +285,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_sampler_draws.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int, C.c_uint32,
                                            C.c_uint32, C.c_void_p, C.c_void_p]
         lib.mtsg_scene_destroy.argtypes = [C.c_void_p]
+        lib.mtsg_set_tile_callback.argtypes = [C.c_void_p, TILE_FN, C.c_void_p]
         lib.mtsg_last_error.argtypes = [C.c_char_p, C.c_size_t]
         _dev = lib
     return _dev
@@ -622,6 +628,11 @@ class GPUScene:
     def cancel(self) -> None:
         device_lib().mtsg_cancel(self._h)
 
+    def set_tile_callback(self, fn) -> None:
+        """fn(key, x, y, w, h) per completed tile (mtsg_set_tile_callback); None removes it."""
+        self._tile_cb = TILE_FN(lambda _u, key, x, y, w, h: fn(key, x, y, w, h)) if fn else None
+        self._check(device_lib().mtsg_set_tile_callback(self._h, self._tile_cb, None), "mtsg_set_tile_callback")
+
     def close(self):
         if getattr(self, "_h", None):
             device_lib().mtsg_scene_destroy(self._h)
@@ -657,6 +668,12 @@ class PathJob:
 
     def cancel(self) -> None:
         path_lib().mtsh_path_job_cancel(self._h)
+
+    def set_tile_callback(self, fn) -> None:
+        """fn(gpu, x, y, w, h) per completed tile (mtsh_path_job_set_tile_callback); None removes it."""
+        self._tile_cb = TILE_FN(lambda _u, gpu, x, y, w, h: fn(gpu, x, y, w, h)) if fn else None
+        if path_lib().mtsh_path_job_set_tile_callback(self._h, self._tile_cb, None) != MTSG_OK:
+            raise RuntimeError(self.last_error())
 
     def close(self):
         if getattr(self, "_h", None):

@@ -216,3 +216,73 @@ def test_plugin_flow_with_overriding_defines():
     assert rc == 0
     # the same samples; the film's float atomics add them in any order
     np.testing.assert_allclose(img, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_crop_window_through_the_job_equals_the_rectangle(tmp_path):
+    """An hdrfilm crop (film.cpp:36-48) rendered through the job (the plugin's
+    render()) equals the same rectangle of the uncropped scene on the device,
+    and the oracle's crop render."""
+    from oracle import pyoracle as O
+    from test_crop import cropped_xml
+    defs = {"width": 320, "height": 180, "spp": 4}
+    cropped = mtsg.Scene(cropped_xml(tmp_path, "bunny15.xml", dict(x=100, y=40, w=72, h=56)), defs)
+    full = mtsg.Scene(os.path.join(SCENES, "bunny15.xml"), defs)
+    p = cropped.params()
+    assert (p.tile_x, p.tile_y, p.tile_w, p.tile_h) == (100, 40, 72, 56)
+    job = mtsg.PathJob(cropped, 0)
+    rc, img, _ = job.render(p, cropped.border)
+    job.close()
+    assert rc == 0
+    g = mtsg.GPUScene(full, 0)
+    rect = g.render(full.params(tile_x=100, tile_y=40, tile_w=72, tile_h=56), full.border)
+    g.close()
+    np.testing.assert_allclose(img, rect, rtol=1e-5, atol=1e-6)
+    ref, _ = O.render(cropped.desc, p, cropped.border, rng=O.RNG_COUNTER)
+    b = cropped.border
+    d = np.abs(mtsg.develop(img[b:-b, b:-b]) - mtsg.develop(ref[b:-b, b:-b]))
+    assert d.mean() < 1e-3 * mtsg.develop(ref[b:-b, b:-b]).mean()
+
+
+def _tiles_of(p):
+    out = set()
+    for ty in range((p.tile_h + 15) // 16):
+        for tx in range((p.tile_w + 15) // 16):
+            out.add((p.tile_x + 16 * tx, p.tile_y + 16 * ty, min(16, p.tile_w - 16 * tx), min(16, p.tile_h - 16 * ty)))
+    return out
+
+
+def test_tile_callbacks_report_every_tile_once(bunny_c3_small):
+    """mtsg_set_tile_callback / mtsh_path_job_set_tile_callback: every tile of a
+    render is reported once, with its rectangle, after its samples are in the
+    block -- with small batches (several per frame, so reports arrive while
+    the frame renders) and through the job (the plugin's signalWorkEnd /
+    progress hook, renderproc.cpp:144-154)."""
+    s = bunny_c3_small
+    p = s.params(tile_x=8, tile_y=4, tile_w=300, tile_h=170)
+    g = mtsg.GPUScene(s, 0)
+    seen = []
+    g.set_tile_callback(lambda key, x, y, w, h: seen.append((key, x, y, w, h)))
+    g.set_batch_paths(16 * 16 * p.spp * 40)   # 40 tiles per batch
+    img = g.render(p, s.border)
+    assert img[..., 4].sum() > 0
+    assert len(seen) == len({k for k, *_ in seen}) == len(_tiles_of(p))
+    assert {r[1:] for r in seen} == _tiles_of(p)
+    # a share: only its tiles
+    seen.clear()
+    q = p.copy()
+    q.tile_stride, q.tile_offset = 3, 2
+    g.render(q, s.border)
+    assert seen and all(k % 3 == 2 for k, *_ in seen)
+    g.set_tile_callback(None)
+    seen.clear()
+    g.render(p, s.border)
+    assert not seen
+    g.close()
+    job = mtsg.PathJob(s, 0)
+    got = []
+    job.set_tile_callback(lambda gpu, x, y, w, h: got.append((gpu, x, y, w, h)))
+    rc, _, _ = job.render(p, s.border)
+    job.close()
+    assert rc == 0
+    assert sorted(r[1:] for r in got) == sorted(_tiles_of(p))
+    assert {r[0] for r in got} <= set(range(mtsg.device_lib().mtsg_device_count()))

@@ -12,6 +12,8 @@ for w in ${*:-tests bench}; do
   case $w in
     tests) step tests 900 $PYT tests ;;
     mathprobe) step mathprobe 300 tools/math_probe 3 ;;
+    mathbench) step mathbench 120 tools/math_bench ;;
+    tests-entry) step tests-entry 600 $PYT tests/test_gpu_render_entry.py tests/test_gpu_edge_rays.py ;;
     tests-parity) step tests-parity 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_c4.py ;;
     tests-new) step tests-new 600 $PYT tests/test_gpu_00_bench_ranks.py tests/test_gpu_c4.py tests/test_gpu_edge_rays.py ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
