@@ -565,7 +565,23 @@ def main():
                     # fetch + one primitive fetch each), and instance entries
                     "iterations_per_ray": round(per(cs.wave_active_lanes, cs.rays_closest + cs.rays_shadow), 2),
                     "instance_visits_per_ray": round(per(cs.instance_visits + cs.shadow_instance_visits,
-                                                         cs.rays_closest + cs.rays_shadow), 3)}
+                                                         cs.rays_closest + cs.rays_shadow), 3),
+                    # the exactness paths (flattened traversal): exact-tie
+                    # retraces with the mailbox (k_tie) and the restart
+                    # guard's one-ulp steps, in the instrumented pass and
+                    # scaled to one frame at the run's spp
+                    "exactness_paths": {
+                        "count_pass_spp": int(pc.spp),
+                        "tie_retraces": int(cs.tie_retraces),
+                        "tie_retraces_per_frame": round(cs.tie_retraces * params.spp / pc.spp),
+                        "kd_restarts_closest": int(cs.restarts_closest), "kd_restarts_shadow": int(cs.restarts_shadow),
+                        "guard_rays_closest": int(cs.guard_rays_closest), "guard_rays_shadow": int(cs.guard_rays_shadow),
+                        "guard_steps_closest": int(cs.guard_steps_closest),
+                        "guard_steps_shadow": int(cs.guard_steps_shadow),
+                        "guard_rays_per_frame": round((cs.guard_rays_closest + cs.guard_rays_shadow)
+                                                      * params.spp / pc.spp),
+                        "scope": ("flattened traversal" if a.instancing == "flatten"
+                                  else "two-level: not counted (per-level restart counters)")}}
 
     # the host-side tile gather: every rank's share of the timed steps' last
     # frame into rank 0's ImageBlock (after the timed region)

@@ -476,6 +476,12 @@ typedef struct mtsg_stats {
      * took over; its launches).  Their traversal is not in rays_* above.   */
     double ms_finish;
     uint64_t paths_finish, launches_finish;
+    /* exactness paths of the flattened traversal (MTSG_FLAG_COUNT): closest
+     * rays traced again with the mailbox after an exact tie (k_tie); rays that
+     * took the restart guard's one-ulp step, and those steps; kd-restarts   */
+    uint64_t tie_retraces;
+    uint64_t guard_rays_closest, guard_rays_shadow, guard_steps_closest, guard_steps_shadow;
+    uint64_t restarts_closest, restarts_shadow;
 } mtsg_stats;
 
 enum {

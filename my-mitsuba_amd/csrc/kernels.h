@@ -1219,10 +1219,22 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
         if (done) {
             active = false;
             // k_tie traces it again with the mailbox
-            if (MTSG_MAILBOX && !INST && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE)
+            if (MTSG_MAILBOX && !INST && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE) {
                 P.tie[atomicAdd(&P.cnt[CNT_TIE], 1u)] = idx;
+                if (COUNT) atomicAdd(&P.ctr[51], 1ull);
+            }
             if (COUNT) {
                 const bool sh = (r.bits & SB_SHADOW) != 0;
+                if (!INST) {
+                    // kd-restarts of the ray, and those that took the guard's
+                    // one-ulp step (restart number >= rstGuard, kd_restart)
+                    const uint32_t nr = (r.bits >> SB_RST_SHIFT) & SB_RST_MASK;
+                    if (nr) atomicAdd(&P.ctr[56 + sh], (unsigned long long)nr);
+                    if (nr > L.rstGuard) {
+                        atomicAdd(&P.ctr[52 + sh], 1ull);
+                        atomicAdd(&P.ctr[54 + sh], (unsigned long long)(nr - L.rstGuard));
+                    }
+                }
                 atomicMax(&P.ctr[sh ? 15 : 7], (unsigned long long)iters);
                 atomicAdd(&P.ctr[(sh ? 32 : 16) + min(15, 31 - __clz(max(iters, 1u)))], 1ull);
                 if (iters >= STRAGGLER_ITERS) {

@@ -689,6 +689,13 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
         s->stragglers.assign(c + 64, c + 64 + 8 * std::min<unsigned long long>(c[48], STRAGGLER_MAX));
         s->stats.instance_visits = c[49];
         s->stats.shadow_instance_visits = c[50];
+        s->stats.tie_retraces = c[51];
+        s->stats.guard_rays_closest = c[52];
+        s->stats.guard_rays_shadow = c[53];
+        s->stats.guard_steps_closest = c[54];
+        s->stats.guard_steps_shadow = c[55];
+        s->stats.restarts_closest = c[56];
+        s->stats.restarts_shadow = c[57];
     }
     s->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return MTSG_OK;

@@ -69,6 +69,9 @@ class Stats(C.Structure):
         ("iter_hist_closest", C.c_uint64 * 16), ("iter_hist_shadow", C.c_uint64 * 16),
         ("instance_visits", C.c_uint64), ("shadow_instance_visits", C.c_uint64),
         ("ms_finish", C.c_double), ("paths_finish", C.c_uint64), ("launches_finish", C.c_uint64),
+        ("tie_retraces", C.c_uint64), ("guard_rays_closest", C.c_uint64), ("guard_rays_shadow", C.c_uint64),
+        ("guard_steps_closest", C.c_uint64), ("guard_steps_shadow", C.c_uint64),
+        ("restarts_closest", C.c_uint64), ("restarts_shadow", C.c_uint64),
     ]
 
 
