@@ -48,6 +48,12 @@
 
 namespace gmf {
 
+// float pairs: two independent polynomials of one function evaluated side by
+// side (v_pk_mul_f32 / v_pk_add_f32 on gfx950); each lane is the same IEEE
+// multiply and add as the scalar expression, so the results do not change
+typedef float f2 __attribute__((ext_vector_type(2)));
+GMF f2 mk2(float a, float b) { f2 v; v.x = a; v.y = b; return v; }
+
 GMF uint32_t asuint(float f) { return __builtin_bit_cast(uint32_t, f); }
 GMF float asfloat(uint32_t u) { return __builtin_bit_cast(float, u); }
 GMF uint64_t asuint64(double f) { return __builtin_bit_cast(uint64_t, f); }
@@ -144,26 +150,25 @@ GMF_COLD void sincosf_large(float y, float *sinp, float *cosp) {
 // result equals the separate sinf / cosf call)
 GMF_ENTRY void sincosf(float y, float *sinp, float *cosp) {
     const uint32_t top = abstop12(y);
-    if (top < abstop12(kPio4f)) {
-        if (top < abstop12(0x1p-12f)) { *sinp = y; *cosp = 1.0f; return; }
-        const double x = y, x2 = x * x;
-        *sinp = (float)sin_poly(x, x2);
-        *cosp = (float)cos_poly(x2, false);
-        return;
-    }
-    if (top >= abstop12(120.0f)) {
-        if (top >= 0x7f8) { *sinp = *cosp = y - y; return; }   // NaN
+    if (top >= abstop12(120.0f) && top < 0x7f8) {   // rare: out of line
         sincosf_large(y, sinp, cosp);
         return;
     }
+    // |x| < pi/4 takes reduce_fast's n = 0 exactly (x - 0 * pi/2 = x), so
+    // s_sincosf.c's small-argument branch is the same computation; the
+    // special cases are selected at the end instead of branched to
     int n;
     const double x = reduce_fast((double)y, n);
     const double xs = ((n + 1) & 2) ? -x : x;   // sign[n & 3] = {1, -1, -1, 1}
     const double x2 = x * x;
     // both polynomials, swapped for odd quadrants (no divergent branch)
     const float ps = (float)sin_poly(xs, x2), pc = (float)cos_poly(x2, (n & 2) != 0);
-    *sinp = (n & 1) ? pc : ps;
-    *cosp = (n & 1) ? ps : pc;
+    float sv = (n & 1) ? pc : ps, cv = (n & 1) ? ps : pc;
+    const bool tinyArg = top < abstop12(0x1p-12f), bad = top >= 0x7f8;
+    sv = tinyArg ? y : bad ? y - y : sv;
+    cv = tinyArg ? 1.0f : bad ? y - y : cv;
+    *sinp = sv;
+    *cosp = cv;
 }
 
 GMF float sinf(float y) { float s, c; gmf::sincosf(y, &s, &c); return s; }
@@ -254,11 +259,6 @@ GMF_ENTRY float atanf(float x) {
                     aT9 = -3.6531571299e-02f, aT10 = 1.6285819933e-02f;
     const int32_t hx = (int32_t)asuint(x);
     const int32_t ix = hx & 0x7fffffff;
-    if (ix >= 0x4c000000) {   // |x| >= 2^25
-        if (ix > 0x7f800000) return x + x;
-        return hx > 0 ? kAtanHi[3] + kAtanLo[3] : -kAtanHi[3] - kAtanLo[3];
-    }
-    if (ix < 0x31000000) return x;   // |x| < 2^-29
     // the argument reduction of each range, as one division of selected
     // operands (the same float operations as s_atanf.c's branches):
     //   id -1 |x| < 0.4375        none
@@ -266,6 +266,8 @@ GMF_ENTRY float atanf(float x) {
     //   id 1  [0.6875, 1.1875)    (|x| - 1) / (|x| + 1)
     //   id 2  [1.1875, 2.4375)    (|x| - 1.5) / (1 + 1.5|x|)
     //   id 3  [2.4375, 2^25)      -1 / |x|
+    // and the special cases (|x| < 2^-29: x; |x| >= 2^25: +-atan(inf); NaN)
+    // selected at the end
     const float ax = fabsf(x);
     const int id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
     const float num = id == 0 ? 2.0f * ax - 1.0f : id == 1 ? ax - 1.0f : id == 2 ? ax - 1.5f : -1.0f;
@@ -274,11 +276,23 @@ GMF_ENTRY float atanf(float x) {
     const float xr = id < 0 ? x : q;
     const float z = xr * xr;
     const float w = z * z;
-    const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
-    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
-    if (id < 0) return xr - xr * (s1 + s2);
-    const float zz = kAtanHi[id] - ((xr * (s1 + s2) - kAtanLo[id]) - xr);
-    return hx < 0 ? -zz : zz;
+    // s1 = z (aT0 + w (aT2 + w (aT4 + w (aT6 + w (aT8 + w aT10))))),
+    // s2 = w (aT1 + w (aT3 + w (aT5 + w (aT7 + w aT9)))), as a pair
+    const f2 ww = mk2(w, w);
+    f2 u = mk2(aT8, aT7) + ww * mk2(aT10, aT9);
+    u = mk2(aT6, aT5) + ww * u;
+    u = mk2(aT4, aT3) + ww * u;
+    u = mk2(aT2, aT1) + ww * u;
+    const float s1 = z * (aT0 + w * u.x);
+    const float s2 = w * u.y;
+    const float hi = id == 0 ? kAtanHi[0] : id == 1 ? kAtanHi[1] : id == 2 ? kAtanHi[2] : kAtanHi[3];
+    const float lo = id == 0 ? kAtanLo[0] : id == 1 ? kAtanLo[1] : id == 2 ? kAtanLo[2] : kAtanLo[3];
+    const float zz = hi - ((xr * (s1 + s2) - lo) - xr);
+    float r = id < 0 ? xr - xr * (s1 + s2) : hx < 0 ? -zz : zz;
+    r = ix < 0x31000000 ? x : r;
+    constexpr float atanInf = kAtanHi[3] + kAtanLo[3];
+    r = ix >= 0x4c000000 ? (ix > 0x7f800000 ? x + x : hx > 0 ? atanInf : -atanInf) : r;
+    return r;
 }
 
 // ---- atan2f (e_atan2f.c) ---------------------------------------------------
@@ -287,42 +301,25 @@ GMF_ENTRY float atan2f(float y, float x) {
                     pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
     const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff;
     const int32_t hy = (int32_t)asuint(y), iy = hy & 0x7fffffff;
-    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
-    if (hx == 0x3f800000) return gmf::atanf(y);
-    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
-    if (iy == 0) {
-        if (m < 2) return y;
-        return m == 2 ? pi + tiny : -pi - tiny;
-    }
-    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
-    if (ix == 0x7f800000) {
-        if (iy == 0x7f800000) {
-            switch (m) {
-            case 0: return pi_o_4 + tiny;
-            case 1: return -pi_o_4 - tiny;
-            case 2: return 3.0f * pi_o_4 + tiny;
-            default: return -3.0f * pi_o_4 - tiny;
-            }
-        }
-        switch (m) {
-        case 0: return 0.0f;
-        case 1: return -0.0f;
-        case 2: return pi + tiny;
-        default: return -pi - tiny;
-        }
-    }
-    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);   // 2 sign(x) + sign(y)
+    // the general case; e_atan2f.c's special cases are selected afterwards in
+    // reverse order of its tests.  x == 1 (atanf(y) there) is the general
+    // case here: y / 1 is exact and atanf is odd to the bit.
     const int k = (iy - ix) >> 23;
-    float z;
-    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
-    else if (hx < 0 && k < -60) z = 0.0f;
-    else z = gmf::atanf(fabsf(y / x));
-    switch (m) {
-    case 0: return z;
-    case 1: return asfloat(asuint(z) ^ 0x80000000u);
-    case 2: return pi - (z - pi_lo);
-    default: return (z - pi_lo) - pi;
+    const float za = gmf::atanf(fabsf(y / x));
+    const float z = k > 60 ? pi_o_2 + 0.5f * pi_lo : (hx < 0 && k < -60) ? 0.0f : za;
+    float r = m == 0 ? z : m == 1 ? asfloat(asuint(z) ^ 0x80000000u) : m == 2 ? pi - (z - pi_lo) : (z - pi_lo) - pi;
+    r = iy == 0x7f800000 ? (hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny) : r;
+    if (ix == 0x7f800000) {
+        const float both = m == 0 ? pi_o_4 + tiny : m == 1 ? -pi_o_4 - tiny : m == 2 ? 3.0f * pi_o_4 + tiny
+                                                                                      : -3.0f * pi_o_4 - tiny;
+        const float xinf = m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? pi + tiny : -pi - tiny;
+        r = iy == 0x7f800000 ? both : xinf;
     }
+    r = ix == 0 ? (hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny) : r;
+    r = iy == 0 ? (m < 2 ? y : m == 2 ? pi + tiny : -pi - tiny) : r;
+    r = (ix > 0x7f800000 || iy > 0x7f800000) ? x + y : r;
+    return r;
 }
 
 // ---- acosf (e_acosf.c) -----------------------------------------------------
@@ -333,27 +330,31 @@ GMF_ENTRY float acosf(float x) {
                     qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f, qS3 = -6.8828397989e-01f,
                     qS4 = 7.7038154006e-02f;
     const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff;
-    if (ix == 0x3f800000) return hx > 0 ? 0.0f : pi + 2.0f * pio2_lo;
-    if (ix > 0x3f800000) return (x - x) / (x - x);
-    if (ix <= 0x23000000) return pio2_hi + pio2_lo;
     // e_acosf.c's three ranges on one rational approximation: z = x^2
     // (|x| < 0.5), (1 + x) / 2 (x <= -0.5), (1 - x) / 2 (x >= 0.5); each
-    // range's own combination below, selected
+    // range's own combination, and the special cases, selected at the end
     const bool small = ix < 0x3f000000;
     const float z = small ? x * x : hx < 0 ? (1.0f + x) * 0.5f : (1.0f - x) * 0.5f;
-    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
-    const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    // p = z (pS0 + z (pS1 + ... + z pS5)), q = 1 + z (qS1 + ... + z qS4), as a pair
+    const f2 zz2 = mk2(z, z);
+    f2 u = mk2(pS4, qS3) + zz2 * mk2(pS5, qS4);
+    u = mk2(pS3, qS2) + zz2 * u;
+    u = mk2(pS2, qS1) + zz2 * u;
+    u = mk2(pS1, 1.0f) + zz2 * u;
+    const float p = z * (pS0 + z * u.x);
+    const float q = u.y;
     const float r = p / q;
-    if (small) return pio2_hi - (x - (pio2_lo - x * r));
     const float s = sqrtf(z);
-    if (hx < 0) {
-        const float w = r * s - pio2_lo;
-        return pi - 2.0f * (s + w);
-    }
-    const float df = asfloat(asuint(s) & 0xfffff000u);
+    const float rs = pio2_hi - (x - (pio2_lo - x * r));   // |x| < 0.5
+    const float rn = pi - 2.0f * (s + (r * s - pio2_lo));  // x <= -0.5
+    const float df = asfloat(asuint(s) & 0xfffff000u);     // x >= 0.5
     const float c = (z - df * df) / (s + df);
-    const float w = r * s + c;
-    return 2.0f * (df + w);
+    const float rp = 2.0f * (df + (r * s + c));
+    float res = small ? rs : hx < 0 ? rn : rp;
+    res = ix <= 0x23000000 ? pio2_hi + pio2_lo : res;
+    res = ix == 0x3f800000 ? (hx > 0 ? 0.0f : pi + 2.0f * pio2_lo) : res;
+    res = ix > 0x3f800000 ? (x - x) / (x - x) : res;
+    return res;
 }
 
 // ---- tanf (s_tanf.c, k_tanf.c) ---------------------------------------------
@@ -398,33 +399,40 @@ GMF float kernel_tanf(float x, float y, int iy) {
         }
     }
     const bool big = ix >= 0x3f2ca140;   // |x| >= 0.6744: tan(pi/4 - |x|) form
-    if (big) {
-        if (hx < 0) { x = -x; y = -y; }
-        const float z = pio4 - x;
-        const float w = pio4lo - y;
-        x = z + w;
-        y = 0.0f;
-        if (fabsf(x) < 0x1p-13f) return (float)((1 - ((hx >> 30) & 2)) * iy) * (1.0f - 2 * iy * x);
+    {
+        const float xa = hx < 0 ? -x : x, ya = hx < 0 ? -y : y;
+        const float xb = (pio4 - xa) + (pio4lo - ya);
+        x = big ? xb : x;
+        y = big ? 0.0f : y;
     }
+    const float nearPio4 = (float)((1 - ((hx >> 30) & 2)) * iy) * (1.0f - 2 * iy * x);   // |pi/4 - |x|| < 2^-13
     const float z = x * x;
     float w = z * z;
-    float r = T1 + w * (T3 + w * (T5 + w * (T7 + w * (T9 + w * T11))));
-    float v = z * (T2 + w * (T4 + w * (T6 + w * (T8 + w * (T10 + w * T12)))));
+    // r = T1 + w (T3 + ... + w T11), v = z (T2 + w (T4 + ... + w T12)), as a pair
+    const f2 ww = mk2(w, w);
+    f2 u = mk2(T9, T10) + ww * mk2(T11, T12);
+    u = mk2(T7, T8) + ww * u;
+    u = mk2(T5, T6) + ww * u;
+    u = mk2(T3, T4) + ww * u;
+    u = mk2(T1, T2) + ww * u;
+    float r = u.x;
+    float v = z * u.y;
     const float s = z * x;
     r = y + z * (s * (r + v) + y);
     r += T0 * s;
     w = x + r;
-    if (!big && iy == 1) return w;
     // the one division of either final form: w^2 / (w + iy) (big), -1 / w
     const float vi = (float)iy;
     const float q = big ? (w * w) / (w + vi) : -1.0f / w;
-    if (big) return (float)(1 - ((hx >> 30) & 2)) * (vi - 2.0f * (x - (q - r)));
+    const float rb = (float)(1 - ((hx >> 30) & 2)) * (vi - 2.0f * (x - (q - r)));
     // -1/(x+r) accurately: a = q
     const float zz = asfloat(asuint(w) & 0xfffff000u);
     v = r - (zz - x);
     const float t = asfloat(asuint(q) & 0xfffff000u);
     const float ss = 1.0f + t * zz;
-    return t + q * (ss + t * v);
+    const float rm = t + q * (ss + t * v);
+    float res = big ? (fabsf(x) < 0x1p-13f ? nearPio4 : rb) : iy == 1 ? w : rm;
+    return res;
 }
 
 GMF_ENTRY float tanf(float x) {

@@ -633,7 +633,7 @@ class GPUScene:
 
     def set_tile_callback(self, fn) -> None:
         """fn(key, x, y, w, h) per completed tile (mtsg_set_tile_callback); None removes it."""
-        self._tile_cb = TILE_FN(lambda _u, key, x, y, w, h: fn(key, x, y, w, h)) if fn else None
+        self._tile_cb = TILE_FN(lambda _u, key, x, y, w, h: fn(key, x, y, w, h)) if fn else TILE_FN()
         self._check(device_lib().mtsg_set_tile_callback(self._h, self._tile_cb, None), "mtsg_set_tile_callback")
 
     def close(self):
@@ -674,7 +674,7 @@ class PathJob:
 
     def set_tile_callback(self, fn) -> None:
         """fn(gpu, x, y, w, h) per completed tile (mtsh_path_job_set_tile_callback); None removes it."""
-        self._tile_cb = TILE_FN(lambda _u, gpu, x, y, w, h: fn(gpu, x, y, w, h)) if fn else None
+        self._tile_cb = TILE_FN(lambda _u, gpu, x, y, w, h: fn(gpu, x, y, w, h)) if fn else TILE_FN()
         if path_lib().mtsh_path_job_set_tile_callback(self._h, self._tile_cb, None) != MTSG_OK:
             raise RuntimeError(self.last_error())
 
