@@ -33,14 +33,38 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#ifndef GMF_NOINLINE
-#define GMF_NOINLINE 0   // 1: the entry points are out-of-line calls (measurement variant)
+// GMF_CALLS: entry points compiled as out-of-line calls instead of inlined
+// (bit mask: 1 sincosf, 2 tanf, 4 atanf / atan2f, 8 acosf, 16 expf / logf);
+// a call keeps a long function's registers out of its caller's allocation
+#ifndef GMF_CALLS
+#define GMF_CALLS 0
 #endif
 #define GMF __host__ __device__ __forceinline__
-#if GMF_NOINLINE
-#define GMF_ENTRY __host__ __device__ inline __attribute__((noinline))
+#define GMF_CALL __host__ __device__ inline __attribute__((noinline))
+#if GMF_CALLS & 1
+#define GMF_ENTRY_SC GMF_CALL
 #else
-#define GMF_ENTRY GMF
+#define GMF_ENTRY_SC GMF
+#endif
+#if GMF_CALLS & 2
+#define GMF_ENTRY_TAN GMF_CALL
+#else
+#define GMF_ENTRY_TAN GMF
+#endif
+#if GMF_CALLS & 4
+#define GMF_ENTRY_ATAN GMF_CALL
+#else
+#define GMF_ENTRY_ATAN GMF
+#endif
+#if GMF_CALLS & 8
+#define GMF_ENTRY_ACOS GMF_CALL
+#else
+#define GMF_ENTRY_ACOS GMF
+#endif
+#if GMF_CALLS & 16
+#define GMF_ENTRY_EXPLOG GMF_CALL
+#else
+#define GMF_ENTRY_EXPLOG GMF
 #endif
 // the large-argument reductions are rare: kept out of line, so they do not
 // add to the register pressure of the shading kernels that call sinf / tanf
@@ -53,6 +77,28 @@ namespace gmf {
 // multiply and add as the scalar expression, so the results do not change
 typedef float f2 __attribute__((ext_vector_type(2)));
 GMF f2 mk2(float a, float b) { f2 v; v.x = a; v.y = b; return v; }
+
+// Division inside the 1-D functions (atanf, acosf, tanf), whose operands stay
+// in the normal range: on the device a Newton-refined reciprocal and one
+// Markstein correction (6 instructions instead of the 11 of the IEEE
+// expansion); its quotients are checked against glibc over every float
+// argument of those functions on the GPU (tools/math_probe 1).  The host
+// (the exhaustive checker) divides in IEEE.  GMF_FAST_DIV=0: IEEE everywhere.
+#ifndef GMF_FAST_DIV
+#define GMF_FAST_DIV 1
+#endif
+GMF float fdiv_n(float a, float b) {
+#if GMF_FAST_DIV && defined(__HIP_DEVICE_COMPILE__)
+    float y = __builtin_amdgcn_rcpf(b);
+    const float e = fmaf(-b, y, 1.0f);
+    y = fmaf(e, y, y);
+    const float q = a * y;
+    const float r = fmaf(-b, q, a);
+    return fmaf(r, y, q);
+#else
+    return a / b;
+#endif
+}
 
 GMF uint32_t asuint(float f) { return __builtin_bit_cast(uint32_t, f); }
 GMF float asfloat(uint32_t u) { return __builtin_bit_cast(float, u); }
@@ -148,7 +194,7 @@ GMF_COLD void sincosf_large(float y, float *sinp, float *cosp) {
 // sincosf (s_sincosf.c): the sine and cosine polynomials of sinf / cosf on one
 // reduction (sincosf_poly performs the same operations as sinf_poly, so each
 // result equals the separate sinf / cosf call)
-GMF_ENTRY void sincosf(float y, float *sinp, float *cosp) {
+GMF_ENTRY_SC void sincosf(float y, float *sinp, float *cosp) {
     const uint32_t top = abstop12(y);
     if (top >= abstop12(120.0f) && top < 0x7f8) {   // rare: out of line
         sincosf_large(y, sinp, cosp);
@@ -186,7 +232,7 @@ constexpr uint64_t kExp2fTab[32] = {
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
 
-GMF_ENTRY float expf(float x) {
+GMF_ENTRY_EXPLOG float expf(float x) {
     const double xd = (double)x;
     const uint32_t abstop = abstop12(x) & 0x7ff;
     if (abstop >= abstop12(88.0f)) {
@@ -220,7 +266,7 @@ GMF_ENTRY float expf(float x) {
 constexpr double kLogfInvc[16] = {0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0, 0x1.3c995b0b80385p+0, 0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0, 0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0, 0x1.0953f419900a7p+0, 0x1p+0, 0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1, 0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
 constexpr double kLogfLogc[16] = {-0x1.57bf7808caadep-2, -0x1.2bef0a7c06ddbp-2, -0x1.01eae7f513a67p-2, -0x1.b31d8a68224e9p-3, -0x1.6574f0ac07758p-3, -0x1.1aa2bc79c81p-3, -0x1.a4e76ce8c0e5ep-4, -0x1.1973c5a611cccp-4, -0x1.252f438e10c1ep-5, 0x0p+0, 0x1.aa5aa5df25984p-5, 0x1.c5e53aa362eb4p-4, 0x1.526e57720db08p-3, 0x1.bc2860d22477p-3, 0x1.1058bc8a07ee1p-2, 0x1.4043057b6ee09p-2};
 
-GMF_ENTRY float logf(float x) {
+GMF_ENTRY_EXPLOG float logf(float x) {
     uint32_t ix = asuint(x);
     if (ix == 0x3f800000u) return 0.0f;
     if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
@@ -252,7 +298,7 @@ GMF_ENTRY float logf(float x) {
 constexpr float kAtanHi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
 constexpr float kAtanLo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
 
-GMF_ENTRY float atanf(float x) {
+GMF_ENTRY_ATAN float atanf(float x) {
     constexpr float aT0 = 3.3333334327e-01f, aT1 = -2.0000000298e-01f, aT2 = 1.4285714924e-01f,
                     aT3 = -1.1111110449e-01f, aT4 = 9.0908870101e-02f, aT5 = -7.6918758452e-02f,
                     aT6 = 6.6610731184e-02f, aT7 = -5.8335702866e-02f, aT8 = 4.9768779427e-02f,
@@ -272,7 +318,7 @@ GMF_ENTRY float atanf(float x) {
     const int id = ix < 0x3ee00000 ? -1 : ix < 0x3f300000 ? 0 : ix < 0x3f980000 ? 1 : ix < 0x401c0000 ? 2 : 3;
     const float num = id == 0 ? 2.0f * ax - 1.0f : id == 1 ? ax - 1.0f : id == 2 ? ax - 1.5f : -1.0f;
     const float den = id == 0 ? 2.0f + ax : id == 1 ? ax + 1.0f : id == 2 ? 1.0f + 1.5f * ax : ax;
-    const float q = num / den;
+    const float q = fdiv_n(num, den);
     const float xr = id < 0 ? x : q;
     const float z = xr * xr;
     const float w = z * z;
@@ -296,7 +342,7 @@ GMF_ENTRY float atanf(float x) {
 }
 
 // ---- atan2f (e_atan2f.c) ---------------------------------------------------
-GMF_ENTRY float atan2f(float y, float x) {
+GMF_ENTRY_ATAN float atan2f(float y, float x) {
     constexpr float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
                     pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
     const int32_t hx = (int32_t)asuint(x), ix = hx & 0x7fffffff;
@@ -323,7 +369,7 @@ GMF_ENTRY float atan2f(float y, float x) {
 }
 
 // ---- acosf (e_acosf.c) -----------------------------------------------------
-GMF_ENTRY float acosf(float x) {
+GMF_ENTRY_ACOS float acosf(float x) {
     constexpr float pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f,
                     pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f,
                     pS3 = -4.0055535734e-02f, pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f,
@@ -343,12 +389,12 @@ GMF_ENTRY float acosf(float x) {
     u = mk2(pS1, 1.0f) + zz2 * u;
     const float p = z * (pS0 + z * u.x);
     const float q = u.y;
-    const float r = p / q;
+    const float r = fdiv_n(p, q);
     const float s = sqrtf(z);
     const float rs = pio2_hi - (x - (pio2_lo - x * r));   // |x| < 0.5
     const float rn = pi - 2.0f * (s + (r * s - pio2_lo));  // x <= -0.5
     const float df = asfloat(asuint(s) & 0xfffff000u);     // x >= 0.5
-    const float c = (z - df * df) / (s + df);
+    const float c = fdiv_n(z - df * df, s + df);
     const float rp = 2.0f * (df + (r * s + c));
     float res = small ? rs : hx < 0 ? rn : rp;
     res = ix <= 0x23000000 ? pio2_hi + pio2_lo : res;
@@ -423,7 +469,7 @@ GMF float kernel_tanf(float x, float y, int iy) {
     w = x + r;
     // the one division of either final form: w^2 / (w + iy) (big), -1 / w
     const float vi = (float)iy;
-    const float q = big ? (w * w) / (w + vi) : -1.0f / w;
+    const float q = big ? fdiv_n(w * w, w + vi) : fdiv_n(-1.0f, w);
     const float rb = (float)(1 - ((hx >> 30) & 2)) * (vi - 2.0f * (x - (q - r)));
     // -1/(x+r) accurately: a = q
     const float zz = asfloat(asuint(w) & 0xfffff000u);
@@ -435,7 +481,7 @@ GMF float kernel_tanf(float x, float y, int iy) {
     return res;
 }
 
-GMF_ENTRY float tanf(float x) {
+GMF_ENTRY_TAN float tanf(float x) {
     const int32_t ix = (int32_t)asuint(x) & 0x7fffffff;
     if (ix <= 0x3f490fda) return kernel_tanf(x, 0.0f, 1);
     if (ix >= 0x7f800000) return x - x;

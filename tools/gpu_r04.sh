@@ -13,6 +13,7 @@ for w in ${*:-tests bench}; do
     tests) step tests 900 $PYT tests ;;
     mathprobe) step mathprobe 300 tools/math_probe 3 ;;
     mathbench) step mathbench 120 tools/math_bench ;;
+    mathprobe1) step mathprobe1 900 tools/math_probe 1 ;;
     tests-entry) step tests-entry 600 $PYT tests/test_gpu_render_entry.py tests/test_gpu_edge_rays.py ;;
     tests-parity) step tests-parity 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_c4.py ;;
     tests-new) step tests-new 600 $PYT tests/test_gpu_00_bench_ranks.py tests/test_gpu_c4.py tests/test_gpu_edge_rays.py ;;
@@ -27,8 +28,8 @@ for w in ${*:-tests bench}; do
       echo "== ranks-refuse"; timeout -k 10 300 python bench.py --gpus 2 --steps 1 --warmup 0 --no-cpu > $O/ranks-refuse.log 2>&1; echo "ranks-refuse rc=$? (non-zero expected)"; tail -n 2 $O/ranks-refuse.log ;;
     bench-ocml) MTSG_LIB=my-mitsuba_amd/var/libmtsg_ocmlmath.so step bench-ocml 600 python bench.py --steps 10 --warmup 3 --no-cpu ;;
     c5-ocml) MTSG_LIB=my-mitsuba_amd/var/libmtsg_ocmlmath.so step c5-ocml 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu ;;
-    bench-mathcall) MTSG_LIB=my-mitsuba_amd/var/libmtsg_mathcall.so step bench-mathcall 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity ;;
-    c5-mathcall) MTSG_LIB=my-mitsuba_amd/var/libmtsg_mathcall.so step c5-mathcall 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity ;;
+    var-*) v=${w#var-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count ;;
+    c5var-*) v=${w#c5var-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
     c5) step c5 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 ;;
     c2) step c2 600 python bench.py --steps 5 --warmup 2 --workload cbox ;;
     kd) step kd 300 python bench.py --steps 5 --warmup 2 --kd-build device --no-cpu --no-parity ;;
