@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--width", type=int, default=1280)
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--batch-paths", type=int, default=0)
+    ap.add_argument("--finish-paths", type=int, default=-1,
+                    help="tail-mode threshold (paths; 0 = off; default: the library's, mtsg_set_finish_paths)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-parity", action="store_true", help="skip the headline parity leg")
     ap.add_argument("--parity-stride", type=int, default=8,
@@ -395,6 +397,8 @@ def main():
     gpu = mtsg.GPUScene(scene, dev)
     if a.batch_paths:
         gpu.set_batch_paths(a.batch_paths)
+    if a.finish_paths >= 0:
+        gpu.set_finish_paths(a.finish_paths)
     W, H = params.tile_w + 2 * border, params.tile_h + 2 * border
     nbytes = W * H * 5 * 4
     film = gpu.alloc(nbytes)

@@ -902,6 +902,19 @@ DEV void tie_retrace(const DevScene &S, SpecRay &r, SpecStack stk, const float4 
 #define MTSG_SAVE_INV 0   // variant: the reciprocal direction saved too (no divisions on exit; 2% slower, r03)
 #endif
 constexpr int SAVE_VECS = MTSG_SAVE_RAY ? (MTSG_SAVE_INV ? 5 : 4) : 2;
+// MTSG_INST_REGSAVE=1 (variant): the saved top-level state and world ray stay
+// in the lane's registers (TopSave, 14 VGPRs) instead of the global slots:
+// no save / restore traffic and no load latency when a lane leaves an
+// instance, for fewer waves per SIMD
+#ifndef MTSG_INST_REGSAVE
+#define MTSG_INST_REGSAVE 0
+#endif
+struct TopSave {
+#if MTSG_INST_REGSAVE
+    uint4 a, b;
+    float3 o, d;
+#endif
+};
 // the two levels' stacks in one LDS array: top level in entries
 // [0, OUTER_STACK), group level in [OUTER_STACK, OUTER_STACK + INNER_STACK)
 __shared__ uint2 s_lvNode[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
@@ -938,8 +951,21 @@ DEV uint2 spec_take_i(const TravLimits &L, SpecRay &r, const uint4 &pr, float ts
 
 // back to the top level after a group traversal: restore the saved state,
 // keep the hit flag, reload the world-space ray
-DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4 *wd) {
+DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4 *wd, const TopSave &ts) {
     const uint32_t found = r.bits & (SB_FOUND | SB_ERR);
+#if MTSG_INST_REGSAVE
+    const uint4 a = ts.a, b = ts.b;
+    r.cur = make_uint2(a.x, a.y);
+    r.tmin = __uint_as_float(a.z);
+    r.tmax = __uint_as_float(a.w);
+    r.lfE = b.x;
+    r.lfEnd = b.y;
+    r.lfTmax = __uint_as_float(b.z);
+    r.bits = b.w | found;
+    r.o = ts.o;
+    r.d = ts.d;
+    r.inv = mk3(1.0f / ts.d.x, 1.0f / ts.d.y, 1.0f / ts.d.z);
+#else
     const uint4 a = save_vec(S, 0), b = save_vec(S, 1);
     r.cur = make_uint2(a.x, a.y);
     r.tmin = __uint_as_float(a.z);
@@ -966,11 +992,12 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
 #else
     r.inv = mk3(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
 #endif
+#endif
 }
 
 template <bool COUNT>
 DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevPaths &P, uint32_t idx, const TravLimits &L,
-                     uint32_t &inst) {
+                     uint32_t &inst, TopSave &ts) {
     const uint2 n = r.cur;
     const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
     const bool prim = r.lfE < r.lfEnd;
@@ -1049,6 +1076,12 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         }
         const float t0 = fmaxf(r.mint, nearT), t1 = fminf(r.best, farT);
         if (ok & (nearT <= farT) & (t1 > t0)) {
+#if MTSG_INST_REGSAVE
+            ts.a = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
+            ts.b = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
+            ts.o = o;
+            ts.d = d;
+#else
             save_vec(S, 0) = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
             save_vec(S, 1) = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
 #if MTSG_SAVE_RAY
@@ -1058,6 +1091,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
             save_vec(S, 4) = make_uint4(__float_as_uint(r.inv.z), 0u, 0u, 0u);
 #else
             save_vec(S, 3) = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), 0u, 0u);
+#endif
 #endif
 #endif
             inst = ii;
@@ -1113,7 +1147,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     const bool done = leave || ((r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f);
     if (done && inInst) {
         const bool sh = (r.bits & SB_SHADOW) != 0;
-        inst_exit(S, r, (sh ? P.sh_o : P.ray_o) + idx, (sh ? P.sh_d : P.ray_d) + idx);
+        inst_exit(S, r, (sh ? P.sh_o : P.ray_o) + idx, (sh ? P.sh_d : P.ray_d) + idx, ts);
         return false;
     }
     return done;
@@ -1148,6 +1182,7 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
     bool active = false;
     uint32_t idx = 0;                      // index into the ray's own list
     uint32_t inst = 0;                     // INST: the instance the lane is inside
+    TopSave ts;                            // (MTSG_INST_REGSAVE: its top-level state)
     uint32_t iters = 0;                    // COUNT: iterations of this ray
     uint32_t n0 = 0, t0c = 0, r0 = 0;      // COUNT: the lane's node / test / restart totals at its start
     unsigned long long tExh = 0;           // wt: when the work list was found empty
@@ -1208,8 +1243,8 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
         if (active) {
             if (INST) {
                 const bool sh = (r.bits & SB_SHADOW) != 0;
-                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P, idx, L, inst);
-                else done = spec_iter_i<COUNT>(S, r, cc, P, idx, L, inst);
+                if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P, idx, L, inst, ts);
+                else done = spec_iter_i<COUNT>(S, r, cc, P, idx, L, inst, ts);
             } else {
                 if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx, L);
                 else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx, L);
@@ -2811,6 +2846,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
     bool pendingCont = false;   // tracing the NEE shadow ray of a path that continues
     uint32_t idx = 0;
     uint32_t inst = 0;          // two-level: the instance the lane is inside
+    TopSave ts;                 // (MTSG_INST_REGSAVE: its top-level state)
     SpecRay r;
     // the continuation ray of path idx (written by shade_path); a ray that
     // misses the scene bounds gets its miss record and is shaded next
@@ -2875,7 +2911,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
         if (state == FS_TRACE) {
             // two-level scenes: the per-lane level switch of k_trace_s<.., true>
             // (its save slots are sized for this grid too)
-            if (S.inst) done = spec_iter_i<false>(S, r, tc, P, idx, trav_limits<false>(S), inst);
+            if (S.inst) done = spec_iter_i<false>(S, r, tc, P, idx, trav_limits<false>(S), inst, ts);
             else done = spec_iter<false>(S, r, stk, tc, P.hit + idx, trav_limits<false>(S));
         }
         if (done) {

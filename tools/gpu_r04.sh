@@ -19,6 +19,10 @@ for w in ${*:-tests bench}; do
     tests-new) step tests-new 600 $PYT tests/test_gpu_00_bench_ranks.py tests/test_gpu_c4.py tests/test_gpu_edge_rays.py ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
     quick) step quick 300 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count ;;
+    c5fin-*) v=${w#c5fin-}; step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count --finish-paths $v ;;
+    c3fin-*) v=${w#c3fin-}; step $w 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count --finish-paths $v ;;
+    inst-quick) step inst-quick 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity --no-count ;;
+    instvar-*) v=${w#instvar-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity --no-count ;;
     c5quick) step c5quick 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
     c2quick) step c2quick 300 python bench.py --steps 5 --warmup 2 --workload cbox --no-cpu --no-parity --no-count ;;
     inst) step inst 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity ;;
