@@ -902,12 +902,13 @@ DEV void tie_retrace(const DevScene &S, SpecRay &r, SpecStack stk, const float4 
 #define MTSG_SAVE_INV 0   // variant: the reciprocal direction saved too (no divisions on exit; 2% slower, r03)
 #endif
 constexpr int SAVE_VECS = MTSG_SAVE_RAY ? (MTSG_SAVE_INV ? 5 : 4) : 2;
-// MTSG_INST_REGSAVE=1 (variant): the saved top-level state and world ray stay
-// in the lane's registers (TopSave, 14 VGPRs) instead of the global slots:
-// no save / restore traffic and no load latency when a lane leaves an
-// instance, for fewer waves per SIMD
+// MTSG_INST_REGSAVE=1 (the default): the saved top-level state and world ray
+// stay in the lane's registers (TopSave, 14 VGPRs) instead of the global
+// slots: no save / restore traffic and no load latency when a lane leaves an
+// instance.  The kernel still fits 6 waves/SIMD (80 VGPRs); measured r04:
+// C3 two-level 1070 -> 1164 Msamples/s (0: the round-3 global slots)
 #ifndef MTSG_INST_REGSAVE
-#define MTSG_INST_REGSAVE 0
+#define MTSG_INST_REGSAVE 1
 #endif
 struct TopSave {
 #if MTSG_INST_REGSAVE
@@ -919,7 +920,7 @@ struct TopSave {
 // [0, OUTER_STACK), group level in [OUTER_STACK, OUTER_STACK + INNER_STACK)
 __shared__ uint2 s_lvNode[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
 __shared__ float s_lvT[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
-enum : uint32_t { SB_INST = 1u << 22 };
+enum : uint32_t { SB_INST = 1u << 22, SB_PEND = 1u << 24 };   // inside an instance; entering one next iteration
 
 DEV uint4 &save_vec(const DevScene &S, uint32_t k) {
     return S.instSave[(size_t)k * (gridDim.x * TRACE_BLOCK) + blockIdx.x * TRACE_BLOCK + lane_here()];
@@ -995,12 +996,82 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
 #endif
 }
 
+// Instance::rayIntersect (instance.cpp:115-130): the ray in group space
+// (Transform::operator()(Ray), transform.h:262-278), clipped to the group
+// tree's AABB; when the clipped interval is not empty the top-level state is
+// saved and the lane continues in the group tree.  L0-L2: the instance's
+// to_local rows, A0 / A1: the group AABB with the root words in .w
+DEV bool inst_enter(SpecRay &r, TopSave &ts, const DevScene &S, uint32_t ii, float4 L0, float4 L1, float4 L2, float4 A0,
+                    float4 A1) {
+    const float3 o = r.o, d = r.d;   // (the library is built with -ffp-contract=off)
+    const float3 lo = mk3(L0.x * o.x + L0.y * o.y + L0.z * o.z + L0.w, L1.x * o.x + L1.y * o.y + L1.z * o.z + L1.w,
+                          L2.x * o.x + L2.y * o.y + L2.z * o.z + L2.w);
+    const float3 ld = mk3(L0.x * d.x + L0.y * d.y + L0.z * d.z, L1.x * d.x + L1.y * d.y + L1.z * d.z,
+                          L2.x * d.x + L2.y * d.y + L2.z * d.z);
+    const float3 li = mk3(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
+    float nearT = -INFINITY, farT = INFINITY;
+    bool ok = true;
+    const float bmn[3] = {A0.x, A0.y, A0.z}, bmx[3] = {A1.x, A1.y, A1.z};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float oi = comp(lo, i), di = comp(ld, i), iv = comp(li, i);
+        if (di == 0.0f) {
+            if (oi < bmn[i] || oi > bmx[i]) ok = false;
+        } else {
+            const float t1 = (bmn[i] - oi) * iv, t2 = (bmx[i] - oi) * iv;
+            nearT = fmaxf(fminf(t1, t2), nearT);
+            farT = fminf(fmaxf(t1, t2), farT);
+        }
+    }
+    const float t0 = fmaxf(r.mint, nearT), t1 = fminf(r.best, farT);
+    if (!(ok & (nearT <= farT) & (t1 > t0))) return false;
+#if MTSG_INST_REGSAVE
+    ts.a = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
+    ts.b = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
+    ts.o = o;
+    ts.d = d;
+#else
+    save_vec(S, 0) = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
+    save_vec(S, 1) = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
+#if MTSG_SAVE_RAY
+    save_vec(S, 2) = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(d.x));
+#if MTSG_SAVE_INV
+    save_vec(S, 3) = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), __float_as_uint(r.inv.x), __float_as_uint(r.inv.y));
+    save_vec(S, 4) = make_uint4(__float_as_uint(r.inv.z), 0u, 0u, 0u);
+#else
+    save_vec(S, 3) = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), 0u, 0u);
+#endif
+#endif
+#endif
+    r.o = lo;
+    r.d = ld;
+    r.inv = li;
+    r.tmin = t0;
+    r.tmax = t1;
+    r.cur = make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w));
+    r.lfE = r.lfEnd = 0;
+    r.lfTmax = -1.0f;
+    const uint32_t dneg = (ld.x <= 0.0f ? 1u : 0u) | (ld.y <= 0.0f ? 2u : 0u) | (ld.z <= 0.0f ? 4u : 0u);
+    r.bits = (r.bits & (SB_FOUND | SB_SHADOW)) | SB_INST | dneg << SB_DNEG;
+    return true;
+}
+
+// One iteration of the two-level traversal.  An instance primitive met in a
+// top-level leaf is entered in the lane's NEXT iteration (SB_PEND): that
+// iteration's fetch slots load the instance record (to_local rows and group
+// AABB, 80 B) in place of a node pair and a primitive, so the record is not a
+// dependent fetch on the leaf record inside one iteration -- in a 64-lane wave
+// some lane enters an instance in almost every iteration, and the wave waited
+// for that second round trip each time.  The sequence of top-level state
+// transitions is unchanged (the leaf logic that followed an unsuccessful
+// entry runs in the entry iteration), so hits are the same bit for bit.
 template <bool COUNT>
 DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevPaths &P, uint32_t idx, const TravLimits &L,
                      uint32_t &inst, TopSave &ts) {
     const uint2 n = r.cur;
-    const bool inner = !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
-    const bool prim = r.lfE < r.lfEnd;
+    const bool pend = (r.bits & SB_PEND) != 0;
+    const bool inner = !pend && !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
+    const bool prim = !pend && r.lfE < r.lfEnd;
     const bool rootKind = inner && !(n.x & 4u);
     float tsplit;
     bool goLeft, push;
@@ -1008,12 +1079,24 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     const uint32_t base = inner ? (n.x >> 3) << ((~n.x >> 1) & 2u) : 0u;
     const uint32_t off = rootKind ? 2u - (uint32_t)goLeft : 0u;
     const uint32_t pi = prim ? r.lfE : 0u;
-    const uint4 p0 = S.blocks[base], pc = S.blocks[base + off];
-    const float4 *rec = S.triL + (size_t)(3u * pi);
+    // a pending entry reads the instance record through the same slots
+    const float4 *irec = S.inst + 8 * (size_t)inst;
+    const uint4 *a0 = pend ? reinterpret_cast<const uint4 *>(irec + 6) : S.blocks + base;
+    const uint4 *a1 = pend ? reinterpret_cast<const uint4 *>(irec + 7) : S.blocks + base + off;
+    const float4 *rec = pend ? irec : S.triL + (size_t)(3u * pi);
+    const uint4 p0 = *a0, pc = *a1;
     const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
     asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
                  "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
                  "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
+    if (pend) {
+        r.bits &= ~SB_PEND;
+        if (COUNT) cnt.inst++;
+        const float4 A0 = make_float4(__uint_as_float(p0.x), __uint_as_float(p0.y), __uint_as_float(p0.z), __uint_as_float(p0.w));
+        const float4 A1 = make_float4(__uint_as_float(pc.x), __uint_as_float(pc.y), __uint_as_float(pc.z), __uint_as_float(pc.w));
+        if (inst_enter(r, ts, S, inst, f0, f1, f2, A0, A1)) return false;
+        // not entered: the leaf logic below, as after the primitive step
+    }
     bool enter = false;
     if (prim) {
         if (COUNT) cnt.refs++;
@@ -1032,6 +1115,9 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
                 stS(P.hit + idx, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
                 P.hitInst[idx] = (r.bits & SB_INST) ? inst : 0xFFFFFFFFu;
             }
+        } else {
+            inst = __float_as_uint(f2.w);
+            r.bits |= SB_PEND;
         }
         ++r.lfE;
     }
@@ -1047,68 +1133,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
             r.cur = spec_take_i(L, r, pc, ts2, gl2, push2);
         }
     }
-    if (enter) {
-        // Instance::rayIntersect: the ray in group space (Transform::operator()
-        // (Ray), transform.h:262-278), clipped to the group tree's AABB
-        if (COUNT) cnt.inst++;
-        const uint32_t ii = __float_as_uint(f2.w);
-        const float4 *I = S.inst + 8 * (size_t)ii;
-        const float4 L0 = I[0], L1 = I[1], L2 = I[2], A0 = I[6], A1 = I[7];
-        const float3 o = r.o, d = r.d;   // (the library is built with -ffp-contract=off)
-        const float3 lo = mk3(L0.x * o.x + L0.y * o.y + L0.z * o.z + L0.w, L1.x * o.x + L1.y * o.y + L1.z * o.z + L1.w,
-                              L2.x * o.x + L2.y * o.y + L2.z * o.z + L2.w);
-        const float3 ld = mk3(L0.x * d.x + L0.y * d.y + L0.z * d.z, L1.x * d.x + L1.y * d.y + L1.z * d.z,
-                              L2.x * d.x + L2.y * d.y + L2.z * d.z);
-        const float3 li = mk3(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
-        float nearT = -INFINITY, farT = INFINITY;
-        bool ok = true;
-        const float bmn[3] = {A0.x, A0.y, A0.z}, bmx[3] = {A1.x, A1.y, A1.z};
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const float oi = comp(lo, i), di = comp(ld, i), iv = comp(li, i);
-            if (di == 0.0f) {
-                if (oi < bmn[i] || oi > bmx[i]) ok = false;
-            } else {
-                const float t1 = (bmn[i] - oi) * iv, t2 = (bmx[i] - oi) * iv;
-                nearT = fmaxf(fminf(t1, t2), nearT);
-                farT = fminf(fmaxf(t1, t2), farT);
-            }
-        }
-        const float t0 = fmaxf(r.mint, nearT), t1 = fminf(r.best, farT);
-        if (ok & (nearT <= farT) & (t1 > t0)) {
-#if MTSG_INST_REGSAVE
-            ts.a = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
-            ts.b = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
-            ts.o = o;
-            ts.d = d;
-#else
-            save_vec(S, 0) = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
-            save_vec(S, 1) = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
-#if MTSG_SAVE_RAY
-            save_vec(S, 2) = make_uint4(__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(d.x));
-#if MTSG_SAVE_INV
-            save_vec(S, 3) = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), __float_as_uint(r.inv.x), __float_as_uint(r.inv.y));
-            save_vec(S, 4) = make_uint4(__float_as_uint(r.inv.z), 0u, 0u, 0u);
-#else
-            save_vec(S, 3) = make_uint4(__float_as_uint(d.y), __float_as_uint(d.z), 0u, 0u);
-#endif
-#endif
-#endif
-            inst = ii;
-            const uint2 root = make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w));
-            r.o = lo;
-            r.d = ld;
-            r.inv = li;
-            r.tmin = t0;
-            r.tmax = t1;
-            r.cur = root;
-            r.lfE = r.lfEnd = 0;
-            r.lfTmax = -1.0f;
-            const uint32_t dneg = (ld.x <= 0.0f ? 1u : 0u) | (ld.y <= 0.0f ? 2u : 0u) | (ld.z <= 0.0f ? 4u : 0u);
-            r.bits = (r.bits & (SB_FOUND | SB_SHADOW)) | SB_INST | dneg << SB_DNEG;
-            return false;
-        }
-    }
+    if (enter) return false;   // entered (or not) in the next iteration
     const bool found = (r.bits & SB_FOUND) != 0;
     const bool inInst = (r.bits & SB_INST) != 0;
     const bool leafDone = (r.lfTmax >= 0.0f) & (r.lfE >= r.lfEnd);

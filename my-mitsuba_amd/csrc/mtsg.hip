@@ -1118,7 +1118,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     s->finishGrid = s->cuCount * perCU;
     // two-level traversal: the per-lane save slots of its grid (kernels.h save_vec)
     s->ds.instSave = nullptr;
-    if (s->ds.inst) {
+    if (s->ds.inst && !MTSG_INST_REGSAVE) {
         uint4 *save = nullptr;
         // slots for the larger of the two grids that switch levels (k_trace_s, k_finish)
         const size_t lanes = (size_t)std::max(s->traceGridInst, s->finishGrid) * TRACE_BLOCK;

@@ -14,6 +14,7 @@ for w in ${*:-tests bench}; do
     mathprobe) step mathprobe 300 tools/math_probe 3 ;;
     mathbench) step mathbench 120 tools/math_bench ;;
     mathprobe1) step mathprobe1 900 tools/math_probe 1 ;;
+    tests-inst) step tests-inst 600 $PYT tests/test_gpu_instancing.py tests/test_gpu_edge_rays.py tests/test_gpu_finish.py ;;
     tests-entry) step tests-entry 600 $PYT tests/test_gpu_render_entry.py tests/test_gpu_edge_rays.py ;;
     tests-parity) step tests-parity 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_c4.py ;;
     tests-new) step tests-new 600 $PYT tests/test_gpu_00_bench_ranks.py tests/test_gpu_c4.py tests/test_gpu_edge_rays.py ;;
