@@ -953,7 +953,7 @@ DEV uint2 spec_take_i(const TravLimits &L, SpecRay &r, const uint4 &pr, float ts
 // back to the top level after a group traversal: restore the saved state,
 // keep the hit flag, reload the world-space ray
 DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4 *wd, const TopSave &ts) {
-    const uint32_t found = r.bits & (SB_FOUND | SB_ERR);
+    const uint32_t found = r.bits & (SB_FOUND | SB_ERR | SB_TIE);
 #if MTSG_INST_REGSAVE
     const uint4 a = ts.a, b = ts.b;
     r.cur = make_uint2(a.x, a.y);
@@ -1052,7 +1052,7 @@ DEV bool inst_enter(SpecRay &r, TopSave &ts, const DevScene &S, uint32_t ii, flo
     r.lfE = r.lfEnd = 0;
     r.lfTmax = -1.0f;
     const uint32_t dneg = (ld.x <= 0.0f ? 1u : 0u) | (ld.y <= 0.0f ? 2u : 0u) | (ld.z <= 0.0f ? 4u : 0u);
-    r.bits = (r.bits & (SB_FOUND | SB_SHADOW)) | SB_INST | dneg << SB_DNEG;
+    r.bits = (r.bits & (SB_FOUND | SB_SHADOW | SB_TIE)) | SB_INST | dneg << SB_DNEG;
     return true;
 }
 
@@ -1108,6 +1108,14 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
             bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
             const bool isRect = k == MTSG_TRIACCEL_SHAPE;
             if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+#if MTSG_MAILBOX
+            // an exact tie is flagged (the ray is traced again by
+            // tie_retrace_i); the key tells a primitive of one instance from
+            // the same primitive of another, and a retest from a tie
+            const uint32_t key = __float_as_uint(f2.z) ^ ((r.bits & SB_INST) ? (inst + 1u) * 0x9E3779B1u : 0u);
+            r.bits |= (h & (t == r.best) & (key != r.bestKey)) ? SB_TIE : 0u;
+            if (h) r.bestKey = key;
+#endif
             if (h) {
                 r.bits |= SB_FOUND;
                 if (r.bits & SB_SHADOW) return true;   // any hit occludes
@@ -1176,6 +1184,152 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         return false;
     }
     return done;
+}
+
+// ---------------------------------------------------------------------------
+// Exact ties in two-level scenes.  The two-level iteration flags a closest
+// ray when a different primitive hits at exactly the best distance so far
+// (SB_TIE, as the flat one), and the ray is traced again here by a literal
+// SAHKDTree3D::rayIntersectHavran (sahkdtree3.h:178-308): entry / exit
+// points, a full stack and the 8-entry hashed mailbox, one fresh traversal
+// (and mailbox) per level as the reference runs one per ShapeKDTree -- the
+// scene's, and the group's inside Instance::rayIntersect (instance.cpp:
+// 115-130, skdtree.h:431-458).  Ties are rare (coincident faces, shared
+// edges), so this path is written for exactness, not speed: its stack lives
+// in scratch.  Mailbox keys are the TriAccel indices of the leaf records
+// (the oracle's keys, oracle.cpp havranTree).
+// ---------------------------------------------------------------------------
+constexpr int HAVRAN_DEPTH = 72;   // the layout refuses trees deeper than 64 (mtsg.hip convert)
+struct HavranHit {
+    float4 rec;      // t, u, v, primitive (0x80000000 | rectangle)
+    uint32_t inst;   // instance of the hit, ~0: top level
+    bool err;        // stack overflow (the render fails with MTSG_ERR_TRAVERSAL)
+};
+// one level; returns whether a primitive of this level (or of an instance
+// entered from it) was accepted; maxt shrinks with the accepted hits
+template <bool TOP>
+DEV bool havran_level(const DevScene &S, float3 o, float3 d, float mint, float maxt, uint2 root, uint32_t inst, HavranHit &H) {
+#pragma clang fp contract(off)
+    struct Ent { uint2 node; float t; uint32_t prev; float3 p; };
+    Ent st[HAVRAN_DEPTH];
+    uint32_t mbox[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mbox[k] = 0xFFFFFFFFu;
+    const float3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    auto at = [&](float t) { return mk3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t); };
+    uint32_t en = 0, ex = 1;
+    st[0].t = mint;
+    st[0].p = at(mint);
+    st[1].t = maxt;
+    st[1].p = at(maxt);
+    st[1].node = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);   // end of the traversal
+    bool found = false;
+    uint2 cur = root;
+    while (!(cur.x == 0xFFFFFFFFu && cur.y == 0xFFFFFFFFu)) {
+        while (!(cur.x & 0x80000000u)) {
+            const uint32_t axis = cur.x & 3u;
+            const float split = __uint_as_float(cur.y);
+            const uint4 pr = S.blocks[(cur.x & 4u) ? (cur.x >> 3) : (cur.x >> 3) * 4u];
+            const uint2 left = make_uint2(pr.x, pr.y), right = make_uint2(pr.z, pr.w);
+            uint2 farChild;
+            if (comp(st[en].p, axis) <= split) {
+                if (comp(st[ex].p, axis) <= split) { cur = left; continue; }
+                if (comp(st[en].p, axis) == split) { cur = right; continue; }
+                cur = left;
+                farChild = right;
+            } else {
+                if (split < comp(st[ex].p, axis)) { cur = right; continue; }
+                farChild = left;
+                cur = right;
+            }
+            const float dist = (split - comp(o, axis)) * comp(inv, axis);
+            const uint32_t tmp = ex++;
+            if (ex == en) ++ex;
+            if (ex >= (uint32_t)HAVRAN_DEPTH) { H.err = true; return found; }
+            st[ex].prev = tmp;
+            st[ex].t = dist;
+            st[ex].node = farChild;
+            float3 p = at(dist);
+            if (axis == 0u) p.x = split; else if (axis == 1u) p.y = split; else p.z = split;
+            st[ex].p = p;
+        }
+        for (uint32_t e = cur.x & 0x7FFFFFFFu; e < cur.y; ++e) {
+            const float4 *rec = S.triL + 3 * (size_t)e;
+            const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
+            const uint32_t key = __float_as_uint(f2.z);
+            if (mbox[key & 7u] == key) continue;
+            const uint32_t k = __float_as_uint(f0.x);
+            if (TOP && k == KINST) {
+                // Instance::rayIntersect: the group's tree on the clipped interval
+                const uint32_t ii = __float_as_uint(f2.w);
+                const float4 *I = S.inst + 8 * (size_t)ii;
+                const float4 L0 = I[0], L1 = I[1], L2 = I[2], A0 = I[6], A1 = I[7];
+                const float3 lo = mk3(L0.x * o.x + L0.y * o.y + L0.z * o.z + L0.w, L1.x * o.x + L1.y * o.y + L1.z * o.z + L1.w,
+                                      L2.x * o.x + L2.y * o.y + L2.z * o.z + L2.w);
+                const float3 ld = mk3(L0.x * d.x + L0.y * d.y + L0.z * d.z, L1.x * d.x + L1.y * d.y + L1.z * d.z,
+                                      L2.x * d.x + L2.y * d.y + L2.z * d.z);
+                const float3 li = mk3(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
+                float nearT = -INFINITY, farT = INFINITY;
+                bool ok = true;
+                const float bmn[3] = {A0.x, A0.y, A0.z}, bmx[3] = {A1.x, A1.y, A1.z};
+                for (int a = 0; a < 3 && ok; ++a) {
+                    const float oa = comp(lo, a), da = comp(ld, a);
+                    if (da == 0.0f) {
+                        if (oa < bmn[a] || oa > bmx[a]) ok = false;
+                    } else {
+                        float t1 = (bmn[a] - oa) * comp(li, a), t2 = (bmx[a] - oa) * comp(li, a);
+                        if (t1 > t2) { const float x = t1; t1 = t2; t2 = x; }
+                        nearT = t1 < nearT ? nearT : t1;   // std::max / std::min (aabb.h:308-338)
+                        farT = farT < t2 ? farT : t2;
+                        if (!(nearT <= farT)) ok = false;
+                    }
+                }
+                if (ok) {
+                    if (mint > nearT) nearT = mint;
+                    if (maxt < farT) farT = maxt;
+                    if (farT > nearT &&
+                        havran_level<false>(S, lo, ld, nearT, farT, make_uint2(__float_as_uint(A0.w), __float_as_uint(A1.w)), ii, H)) {
+                        maxt = H.rec.x;
+                        found = true;
+                    }
+                    if (H.err) return found;
+                }
+            } else {
+                float t, u, v;
+                bool h;
+                if (k == MTSG_TRIACCEL_SHAPE) h = rect_test(S.rects[__float_as_uint(f2.w)], o, d, mint, maxt, t, u, v);
+                else h = tri_test(f0, f1, f2, o, d, mint, maxt, u, v, t);
+                if (h) {
+                    maxt = t;
+                    found = true;
+                    const uint32_t p = __float_as_uint(f2.w);
+                    H.rec = make_float4(t, u, v, __uint_as_float(k == MTSG_TRIACCEL_SHAPE ? (0x80000000u | p) : p));
+                    H.inst = TOP ? 0xFFFFFFFFu : inst;
+                }
+            }
+            mbox[key & 7u] = key;
+        }
+        if (st[ex].t > maxt) break;
+        en = ex;
+        cur = st[ex].node;
+        ex = st[en].prev;
+    }
+    return found;
+}
+
+// a closest ray of a two-level scene traced again exactly (ray from its work
+// list entry, as spec_init clips it): rewrites its hit record and instance
+__attribute__((noinline)) DEV void tie_retrace_i(const DevScene &S, const DevPaths &P, uint32_t idx, bool &err) {
+    const float4 ro = ldS(P.ray_o + idx), rd = ldS(P.ray_d + idx);
+    SpecRay r;
+    if (!spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, false, r)) return;
+    HavranHit H;
+    H.err = false;
+    if (havran_level<true>(S, r.o, r.d, r.mint, r.best, S.root2, 0xFFFFFFFFu, H)) {
+        stS(P.hit + idx, H.rec);
+        P.hitInst[idx] = H.inst;
+    }
+    err = H.err;
 }
 
 // Persistent traversal kernel with lane-level refill (the "while-while +
@@ -1279,7 +1433,7 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
         if (done) {
             active = false;
             // k_tie traces it again with the mailbox
-            if (MTSG_MAILBOX && !INST && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE) {
+            if (MTSG_MAILBOX && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE) {
                 P.tie[atomicAdd(&P.cnt[CNT_TIE], 1u)] = idx;
                 if (COUNT) atomicAdd(&P.ctr[51], 1ull);
             }
@@ -2940,8 +3094,15 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
             else done = spec_iter<false>(S, r, stk, tc, P.hit + idx, trav_limits<false>(S));
         }
         if (done) {
-            if (MTSG_MAILBOX && !S.inst && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE)
-                tie_retrace(S, r, stk, P.ray_o + idx, P.ray_d + idx, P.hit + idx, trav_limits<false>(S));
+            if (MTSG_MAILBOX && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE) {
+                if (!S.inst) {
+                    tie_retrace(S, r, stk, P.ray_o + idx, P.ray_d + idx, P.hit + idx, trav_limits<false>(S));
+                } else {
+                    bool herr = false;
+                    tie_retrace_i(S, P, idx, herr);
+                    if (herr) r.bits |= SB_ERR;
+                }
+            }
             if (r.bits & SB_ERR) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);
             if (r.bits & SB_SHADOW) {
                 if (!(r.bits & SB_FOUND)) shadow_unoccluded(P, idx);
@@ -3100,6 +3261,16 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_tie(DevScene S, DevPaths P) {
         const uint32_t idx = P.tie[i];
         tie_retrace(S, r, stk, P.ray_o + idx, P.ray_d + idx, P.hit + idx, L);
         if (r.bits & SB_ERR) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);
+    }
+}
+
+// the same for two-level scenes: the exact two-level Havran (tie_retrace_i)
+__global__ void __launch_bounds__(TRACE_BLOCK) k_tie_i(DevScene S, DevPaths P) {
+    const uint32_t n = __atomic_load_n(&P.cnt[CNT_TIE], __ATOMIC_RELAXED);
+    for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
+        bool err = false;
+        tie_retrace_i(S, P, P.tie[i], err);
+        if (err) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);
     }
 }
 

@@ -82,3 +82,70 @@ def test_two_level_c3_full_frame_parity():
     g.close()
     l1, mean = check_render(c, gi)
     print(f"C3 two-level 1280x720x2spp: per-pixel L1 {l1:.3e}, mean {mean:.4f}")
+
+
+def _rot_y(deg):
+    a = np.radians(deg)
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+
+
+def test_two_level_coplanar_tie_policy():
+    """Exact ties inside instances (scenes/cbox_inst.xml: a group of three
+    touching cubes, so two pairs of its faces coincide).  Rays from inside a
+    cube through a shared face meet two triangles of the group at exactly
+    the same distance.  Mitsuba resolves that in the group's own
+    ShapeKDTree, with that traversal's own 8-entry mailbox (instance.cpp:
+    115-130, sahkdtree3.h:250-290); the GPU flags the tie in its two-level
+    iteration and traces the ray again with a literal two-level Havran
+    (kernels.h tie_retrace_i), so the winner, t and u must be the oracle's
+    bit for bit -- and a render of the scene is at parity."""
+    scene = mtsg.Scene(os.path.join(SCENES, "cbox_inst.xml"), {"width": 48, "height": 48, "spp": 8},
+                       instancing="two-level")
+    rng = np.random.default_rng(23)
+    # (group-space cube centre, main direction): through x = 0.25 and y = 0.25
+    cases = [((0, 0, 0), (1, 0, 0)), ((0.5, 0, 0), (-1, 0, 0)), ((0, 0, 0), (0, 1, 0)), ((0, 0.5, 0), (0, -1, 0))]
+    inst = [(np.eye(3), np.array([-0.5, -0.75, -0.25])), (_rot_y(-25), np.array([0.125, -0.75, 0.375]))]
+    rays, planes = [], []
+    n = 3000
+    for R, off in inst:
+        for c, dmain in cases:
+            og = np.asarray(c) + rng.uniform(-0.2, 0.2, (n, 3))
+            dg = np.asarray(dmain, float) + rng.normal(0, 0.15, (n, 3))
+            dg /= np.linalg.norm(dg, axis=1, keepdims=True)
+            r = np.zeros((n, 8), np.float32)
+            r[:, :3] = og @ R.T + off
+            r[:, 3:6] = dg @ R.T
+            r[:, 6], r[:, 7] = 1e-4, np.inf
+            rays.append(r)
+            planes.append((R, off, 0 if dmain[0] else 1))
+    n_cop = len(rays) * n
+    m = 60000
+    r = np.zeros((m, 8), np.float32)
+    r[:, :3] = rng.uniform(-0.95, 0.95, (m, 3))
+    d = rng.normal(size=(m, 3))
+    r[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    r[:, 6], r[:, 7] = 1e-4, np.inf
+    allr = np.concatenate(rays + [r])
+    g = mtsg.GPUScene(scene, 0)
+    try:
+        t0, u0, v0, p0 = O.trace_closest(scene.desc, allr)
+        t1, u1, v1, p1 = g.trace_closest(allr)
+        # the designed rays do end on the coincident faces (group-space
+        # coordinate 0.25 on the crossed axis)
+        on = 0
+        for k, (R, off, ax) in enumerate(planes):
+            sl = slice(k * n, (k + 1) * n)
+            hp = allr[sl, :3] + allr[sl, 3:6] * t0[sl, None]
+            gp = (hp - off) @ R
+            on += int((np.abs(gp[:, ax] - 0.25) < 1e-5).sum())
+        assert on > 0.5 * n_cop, on
+        hit = p0 != 0xFFFFFFFF
+        np.testing.assert_array_equal(p1, p0)
+        np.testing.assert_array_equal(t1, t0)
+        np.testing.assert_array_equal(u1[hit], u0[hit])
+        np.testing.assert_array_equal(v1[hit], v0[hit])
+        _, c, gi = render_pair(scene, g)
+        check_render(c, gi)
+    finally:
+        g.close()
