@@ -41,6 +41,9 @@ struct DevScene {
     //   p0 p1 p2 | n0 n1 n2 | dpdu | shape, bsdf | faceNormals << 31, emitter
     const float4 *__restrict__ shrec;
     const mtsg_rect *__restrict__ rects;
+    // per rectangle its to_object rows as 3 float4 (48 B, the size of a
+    // TriAccel record): MTSG_RECT_PEND reads them through the primitive slot
+    const float4 *__restrict__ rectM;
     const mtsg_shape *__restrict__ shapes;
     const mtsg_bsdf *__restrict__ bsdfs;
     const mtsg_emitter *__restrict__ emitters;
@@ -368,9 +371,8 @@ DEV bool tri_test(const float4 f0, const float4 f1, const float4 f2, float3 o, f
 }
 
 // Rectangle::rayIntersect (rectangle.cpp:115-139)
-DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float maxt, float &t, float &lx, float &ly) {
+DEV bool rect_test_m(const float *m, float3 wo, float3 wd, float mint, float maxt, float &t, float &lx, float &ly) {
 #pragma clang fp contract(off)
-    const float *m = r.to_object;
     float3 o = mk3(m[0] * wo.x + m[1] * wo.y + m[2] * wo.z + m[3], m[4] * wo.x + m[5] * wo.y + m[6] * wo.z + m[7],
                    m[8] * wo.x + m[9] * wo.y + m[10] * wo.z + m[11]);
     float3 d = mk3(m[0] * wd.x + m[1] * wd.y + m[2] * wd.z, m[4] * wd.x + m[5] * wd.y + m[6] * wd.z,
@@ -380,6 +382,15 @@ DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float m
     float x = o.x + d.x * hit, y = o.y + d.y * hit;
     if (fabsf(x) <= 1 && fabsf(y) <= 1) { t = hit; lx = x; ly = y; return true; }
     return false;
+}
+DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float maxt, float &t, float &lx, float &ly) {
+    return rect_test_m(r.to_object, wo, wd, mint, maxt, t, lx, ly);
+}
+// the same test on to_object rows already in registers (MTSG_RECT_PEND)
+DEV bool rect_test_rows(float4 r0, float4 r1, float4 r2, float3 wo, float3 wd, float mint, float maxt, float &t, float &lx,
+                        float &ly) {
+    const float m[12] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w};
+    return rect_test_m(m, wo, wd, mint, maxt, t, lx, ly);
 }
 
 // ---------------------------------------------------------------------------
@@ -518,17 +529,18 @@ struct SpecRay {
     uint32_t bits;       // see SB_*
     uint32_t mb;         // mailbox state of exact ties (mailbox_step)
     uint32_t bestKey;    // TriAccel index of the best hit (mailbox key)
+    uint32_t rpend;      // MTSG_RECT_PEND: the rectangle tested in the lane's next iteration
 };
 // bits: top slot of the circular short stack (0-2), entries held (3-5),
 // entries dropped since the last restart (6), kd-restarts of the ray at this
 // level (7-15), ray direction signs (16-18), traversal done (19), hit found
 // (20), shadow ray (21), inside an instance (22), an exact tie met (23),
-// restart limit hit (31)
+// a rectangle pending (25, MTSG_RECT_PEND), restart limit hit (31)
 enum : uint32_t {
     SB_TOP = 7u, SB_N = 7u << 3, SB_N1 = 1u << 3, SB_DROPPED = 1u << 6, SB_STACK = 0x7Fu,
     SB_RST_SHIFT = 7, SB_RST1 = 1u << 7, SB_RST_MASK = 0x1FFu,
     SB_DNEG = 16, SB_TRAVDONE = 1u << 19, SB_FOUND = 1u << 20, SB_SHADOW = 1u << 21, SB_TIE = 1u << 23,
-    SB_ERR = 1u << 31
+    SB_RPEND = 1u << 25, SB_ERR = 1u << 31
 };
 // the restart guard's defaults (DevScene::rstGuard / rstMax): rays of the
 // scenes at hand restart 0-3 times (tools/iter_hist.py)
@@ -728,6 +740,9 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 // best's slot; prev's identity in LDS, the best's in its hit record.  Exact for
 // ties of two primitives; of three or more, a retest of the earliest one after
 // the later two is accepted where Mitsuba may skip it.
+#ifndef MTSG_RECT_PEND
+#define MTSG_RECT_PEND 0   // 1: a rectangle of the flat traversal is tested in the lane's next iteration
+#endif
 #ifndef MTSG_MAILBOX
 #define MTSG_MAILBOX 1   // 0: measurement variant, the last primitive tested wins a tie
 #endif
@@ -788,23 +803,53 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
 #else
     const uint4 p0 = S.blocks[base], pc = S.blocks[base + off];
 #endif
+#if MTSG_RECT_PEND
+    // a rectangle met in the held leaf is tested in the lane's next
+    // iteration, its to_object rows read through the primitive slot: no
+    // dependent fetch of the rectangle inside an iteration
+    const bool rp = (r.bits & SB_RPEND) != 0;
+    const float4 *rec = rp ? S.rectM + (size_t)(3u * r.rpend) : S.triL + (size_t)(3u * pi);
+#else
     const float4 *rec = S.triL + (size_t)(3u * pi);   // < 2^32: checked at upload
+#endif
     const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
     asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
                  "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
                  "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
+#if MTSG_RECT_PEND
+    if (prim && !rp && __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE) {
+        r.rpend = __float_as_uint(f2.w);
+        r.bits |= SB_RPEND;
+    } else if (prim) {
+        if (COUNT) { cnt.refs++; cnt.tests++; }
+        float t, u, v;
+        const bool isRect = rp;
+        bool h;
+        uint32_t key, pid;
+        if (rp) {
+            h = rect_test_rows(f0, f1, f2, r.o, r.d, r.mint, r.best, t, u, v);
+            key = S.n_tri + r.rpend;
+            pid = r.rpend;
+            r.bits &= ~SB_RPEND;
+        } else {
+            h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+            key = __float_as_uint(f2.z);
+            pid = __float_as_uint(f2.w);
+        }
+#else
     if (prim) {
         if (COUNT) { cnt.refs++; cnt.tests++; }
         float t, u, v;
         bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
         const bool isRect = __float_as_uint(f0.x) == MTSG_TRIACCEL_SHAPE;
         if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+        const uint32_t key = __float_as_uint(f2.z), pid = __float_as_uint(f2.w);
+#endif
 #if MTSG_MAILBOX
         // a tie is only flagged here; the ray is then traced again with the
         // mailbox (tie_retrace).  Shadow rays end at their first hit.
         // (a primitive spanning leaves is retested at the same t: not a tie)
-        const uint32_t key = __float_as_uint(f2.z);
-        if (MB) h = mailbox_step(r, key, isRect, __float_as_uint(f2.w), h, t, hitOut);
+        if (MB) h = mailbox_step(r, key, isRect, pid, h, t, hitOut);
         else r.bits |= (h & (t == r.best) & (key != r.bestKey)) ? SB_TIE : 0u;
         if (h) r.bestKey = key;
 #endif
@@ -812,7 +857,7 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
             r.bits |= SB_FOUND;
             if (r.bits & SB_SHADOW) return true;   // any hit occludes
             r.best = t;
-            stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
+            stS(hitOut, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | pid) : pid)));
         }
         ++r.lfE;
     }
@@ -2431,18 +2476,49 @@ struct ShadeTables {
 };
 DEV ShadeTables global_tables(const DevScene &S) { return ShadeTables{S.bsdfs, S.emitters, S.emitter_cdf}; }
 
-template <bool ENV, int SMP, bool EXT, class Out>
-DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, bool first, uint32_t i,
-                    const uint4 meta, int hasAlpha, Out &out, bool &cont, bool &shadow, const ShadeTables &tb) {
-    const uint32_t slot = meta.z;
-    const float4 h = ldS(&P.hit[i]);
-    const float4 ro4 = ldS(&P.ray_o[i]), rd4 = ldS(&P.ray_d[i]);
-    const float3 ro = xyz(ro4), rd = xyz(rd4);
+// the path's records at position i that do not depend on its meta word:
+// loaded together with it, so the hit -> shading record chain starts one
+// memory round trip earlier (k_shade issues them before it knows whether a
+// bounce-0 slot is live)
+struct PathLoads {
+    float4 h, ro4, rd4, L4, T4;
+};
+DEV PathLoads load_path(const DevScene &S, const DevPaths &P, uint32_t i, bool first) {
+    PathLoads pl;
+    pl.h = ldS(&P.hit[i]);
+    pl.ro4 = ldS(&P.ray_o[i]);
+    pl.rd4 = ldS(&P.ray_d[i]);
     // a camera path starts with L = 0, alpha 1, T = 1, eta = 1: k_camera writes
     // neither array then (T holds the ray differentials when cam_diffs)
     const bool fresh = first && !S.cam_diffs;
-    float4 L4 = fresh ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
-    float4 T4 = fresh ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
+    pl.L4 = fresh ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
+    pl.T4 = fresh ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
+    return pl;
+}
+DEV PathLoads load_path_rest(const DevScene &S, const DevPaths &P, uint32_t i, bool first) {
+    PathLoads pl;
+    pl.ro4 = ldS(&P.ray_o[i]);
+    pl.rd4 = ldS(&P.ray_d[i]);
+    const bool fresh = first && !S.cam_diffs;
+    pl.L4 = fresh ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
+    pl.T4 = fresh ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
+    return pl;
+}
+// MTSG_SHADE_PRELOAD: what k_shade loads together with the meta word (1:
+// every record of load_path, 2: the hit only, 0: nothing -- round 3)
+#ifndef MTSG_SHADE_PRELOAD
+#define MTSG_SHADE_PRELOAD 1
+#endif
+
+template <bool ENV, int SMP, bool EXT, class Out>
+DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, bool first, uint32_t i,
+                    const uint4 meta, const PathLoads &pl, int hasAlpha, Out &out, bool &cont, bool &shadow,
+                    const ShadeTables &tb) {
+    const uint32_t slot = meta.z;
+    const float4 h = pl.h;
+    const float3 ro = xyz(pl.ro4), rd = xyz(pl.rd4);
+    float4 L4 = pl.L4;
+    float4 T4 = pl.T4;
     PathSampler smp;
     {
         int x, y;
@@ -2936,13 +3012,28 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
         bool alive = i < count;
         bool cont = false, shadow = false;
         uint4 meta = make_uint4(0u, 0u, 0u, 0u);
+        PathLoads pl;
         if (alive) {
             meta = ldS(&P.meta[i]);
+#if MTSG_SHADE_PRELOAD == 1
+            pl = load_path(S, P, i, bounce == 0);
+#elif MTSG_SHADE_PRELOAD == 2
+            pl.h = ldS(&P.hit[i]);
+#endif
             if (meta.x == 0u) alive = false;   // dead slot (bounce 0)
         }
         if (alive) {
+#if MTSG_SHADE_PRELOAD == 0
+            pl = load_path(S, P, i, bounce == 0);
+#elif MTSG_SHADE_PRELOAD == 2
+            {
+                const float4 h = pl.h;
+                pl = load_path_rest(S, P, i, bounce == 0);
+                pl.h = h;
+            }
+#endif
             StageOut out{stage};
-            shade_path<ENV, SMP, EXT>(S, I, B, P, bounce == 0, i, meta, hasAlpha, out, cont, shadow, tb);
+            shade_path<ENV, SMP, EXT>(S, I, B, P, bounce == 0, i, meta, pl, hasAlpha, out, cont, shadow, tb);
         }
         const uint32_t slot = meta.z;
         // The output positions come from the workgroup-aggregated append; the
@@ -3068,7 +3159,8 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
                 const uint4 meta = ldS(&P.meta[idx]);
                 FinishOut out{P, idx, make_float4(0.f, 0.f, 0.f, 0.f)};
                 bool cont = false, shadow = false;
-                shade_path<ENV, SMP, EXT>(S, I, B, P, false, idx, meta, hasAlpha, out, cont, shadow, global_tables(S));
+                shade_path<ENV, SMP, EXT>(S, I, B, P, false, idx, meta, load_path(S, P, idx, false), hasAlpha, out, cont, shadow,
+                                          global_tables(S));
                 state = FS_IDLE;
                 if (shadow) {
                     out.c.w = __uint_as_float(cont ? idx : (0x80000000u | meta.z));

@@ -914,6 +914,18 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         return fail(rc);
     ds.blocks = dblocks; ds.root2 = root2;
     ds.triL = dtriL; ds.vpos = dvpos; ds.vnrm = dvnrm;
+    {
+        // to_object rows of every rectangle, 48 B each (DevScene::rectM)
+        std::vector<float4> rm((size_t)3 * std::max<uint32_t>(d->n_rects, 1u), make_float4(0, 0, 0, 0));
+        for (uint32_t i = 0; i < d->n_rects; ++i)
+            for (int k = 0; k < 3; ++k) {
+                const float *m = d->rects[i].to_object + 4 * k;
+                rm[3 * i + k] = make_float4(m[0], m[1], m[2], m[3]);
+            }
+        float4 *drm;
+        if ((rc = up(rm.data(), rm.size(), &drm))) return fail(rc);
+        ds.rectM = drm;
+    }
     ds.tidx = dtidx; ds.shrec = dshrec; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
     ds.inst = nullptr;

@@ -36,6 +36,7 @@ for w in ${*:-tests bench}; do
       echo "== ranks-refuse"; timeout -k 10 300 python bench.py --gpus 2 --steps 1 --warmup 0 --no-cpu > $O/ranks-refuse.log 2>&1; echo "ranks-refuse rc=$? (non-zero expected)"; tail -n 2 $O/ranks-refuse.log ;;
     bench-ocml) MTSG_LIB=my-mitsuba_amd/var/libmtsg_ocmlmath.so step bench-ocml 600 python bench.py --steps 10 --warmup 3 --no-cpu ;;
     c5-ocml) MTSG_LIB=my-mitsuba_amd/var/libmtsg_ocmlmath.so step c5-ocml 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu ;;
+    vtests-*) v=${w#vtests-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_edge_rays.py ;;
     var-*) v=${w#var-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count ;;
     c5var-*) v=${w#c5var-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
     c5) step c5 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 ;;
