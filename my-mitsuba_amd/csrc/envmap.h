@@ -12,10 +12,23 @@ namespace mtsg {
 
 constexpr float kInvTwoPi = 0.15915494309189533577f;   // constants.h:65
 
+// MTSG_ENV_GUIDE: the CDF searches of the importance sampling start from a
+// guide table (ENV_GUIDE + 1 entries per CDF: the lower_bound of g /
+// ENV_GUIDE), so a search reads 1-3 CDF entries instead of ~log2(size): the
+// same index as the full std::lower_bound (the answer for a sample in
+// [g, g+1) / ENV_GUIDE lies between the guides of g and g + 1), with a chain
+// of dependent loads 3x shorter.  0: the full search (round 3).
+#ifndef MTSG_ENV_GUIDE
+#define MTSG_ENV_GUIDE 1
+#endif
+constexpr uint32_t ENV_GUIDE = 128;   // C5 (envmap.exr): 2.4 column search steps on average instead of 9
+
 struct DevEnv {
     const mtsg_envmap *E;        // device copy of the table header
     const float *texels;         // RGB, all levels
     const float *cdfRows, *cdfCols, *rowWeights;
+    const uint32_t *guideRows;   // ENV_GUIDE + 1 entries
+    const uint32_t *guideCols;   // (ENV_GUIDE + 1) per row
 };
 
 DEV DevMip env_mip(const DevEnv &V) { return DevMip{&V.E->mip, V.texels}; }   // u repeats, v clamps
@@ -56,6 +69,22 @@ DEV uint32_t env_sample_reuse(const float *cdf, uint32_t size, float &sample) {
     return index;
 }
 
+// the same over [guide[g], guide[g + 1]] (the sample is in [0, 1): g = floor(sample * ENV_GUIDE) is exact)
+DEV uint32_t env_sample_reuse_guided(const float *cdf, uint32_t size, const uint32_t *guide, float &sample) {
+    const uint32_t g = min((uint32_t)(sample * (float)ENV_GUIDE), ENV_GUIDE - 1u);
+    uint32_t lo = guide[g];
+    const uint32_t hi = min(guide[g + 1], size);
+    uint32_t len = hi + 1 - lo;
+    while (len > 0) {
+        const uint32_t half = len >> 1;
+        if (cdf[lo + half] < sample) { lo += half + 1; len -= half + 1; }
+        else len = half;
+    }
+    const uint32_t index = min((uint32_t)max((int)lo - 1, 0), size - 1);
+    sample = (sample - cdf[index]) / (cdf[index + 1] - cdf[index]);
+    return index;
+}
+
 DEV float env_tent(float sample) {   // warp.cpp:143-155
     float sign;
     if (sample < 0.5f) { sign = 1; sample *= 2; }
@@ -67,8 +96,14 @@ DEV float env_tent(float sample) {   // warp.cpp:143-155
 DEV void env_internal_sample(const DevEnv &V, float sx, float sy, float3 &d, float3 &value, float &pdf) {
     const int W = V.E->mip.level_w[0], H = V.E->mip.level_h[0];
     const DevMip M = env_mip(V);
+#if MTSG_ENV_GUIDE
+    const uint32_t row = env_sample_reuse_guided(V.cdfRows, (uint32_t)H, V.guideRows, sy);
+    const uint32_t col =
+        env_sample_reuse_guided(V.cdfCols + row * (uint32_t)(W + 1), (uint32_t)W, V.guideCols + row * (ENV_GUIDE + 1u), sx);
+#else
     const uint32_t row = env_sample_reuse(V.cdfRows, (uint32_t)H, sy);
     const uint32_t col = env_sample_reuse(V.cdfCols + row * (uint32_t)(W + 1), (uint32_t)W, sx);
+#endif
     const float px = (float)col + env_tent(sx), py = (float)row + env_tent(sy);
     const int xPos = (int)floorf(px), yPos = (int)floorf(py);
     const float dx1 = px - xPos, dx2 = 1.0f - dx1, dy1 = py - yPos, dy2 = 1.0f - dy1;

@@ -1128,7 +1128,14 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     const float4 *irec = S.inst + 8 * (size_t)inst;
     const uint4 *a0 = pend ? reinterpret_cast<const uint4 *>(irec + 6) : S.blocks + base;
     const uint4 *a1 = pend ? reinterpret_cast<const uint4 *>(irec + 7) : S.blocks + base + off;
+#if MTSG_RECT_PEND
+    // a top-level rectangle is tested in the lane's next iteration (its index
+    // waits in `inst`, unused at the top level: groups hold no rectangles)
+    const bool rp = (r.bits & SB_RPEND) != 0;
+    const float4 *rec = pend ? irec : (rp ? S.rectM + (size_t)(3u * inst) : S.triL + (size_t)(3u * pi));
+#else
     const float4 *rec = pend ? irec : S.triL + (size_t)(3u * pi);
+#endif
     const uint4 p0 = *a0, pc = *a1;
     const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
     asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
@@ -1144,35 +1151,59 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     }
     bool enter = false;
     if (prim) {
-        if (COUNT) cnt.refs++;
         const uint32_t k = __float_as_uint(f0.x);
+#if MTSG_RECT_PEND
+        const bool isRect = rp, defer = !rp && k == MTSG_TRIACCEL_SHAPE;
+        enter = !rp && k == KINST;
+#else
+        const bool isRect = k == MTSG_TRIACCEL_SHAPE, defer = false;
         enter = k == KINST;
-        if (!enter) {
+#endif
+        if (COUNT && !defer) cnt.refs++;
+        if (defer) {
+            inst = __float_as_uint(f2.w);
+            r.bits |= SB_RPEND;
+        } else if (!enter) {
             if (COUNT) cnt.tests++;
             float t, u, v;
+#if MTSG_RECT_PEND
+            bool h;
+            uint32_t key, pid;
+            if (rp) {
+                h = rect_test_rows(f0, f1, f2, r.o, r.d, r.mint, r.best, t, u, v);
+                key = S.n_tri + inst;
+                pid = inst;
+                r.bits &= ~SB_RPEND;
+            } else {
+                h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
+                key = __float_as_uint(f2.z);
+                pid = __float_as_uint(f2.w);
+            }
+#else
             bool h = tri_test(f0, f1, f2, r.o, r.d, r.mint, r.best, u, v, t);
-            const bool isRect = k == MTSG_TRIACCEL_SHAPE;
             if (isRect) h = rect_test(S.rects[__float_as_uint(f2.w)], r.o, r.d, r.mint, r.best, t, u, v);
+            const uint32_t key = __float_as_uint(f2.z), pid = __float_as_uint(f2.w);
+#endif
 #if MTSG_MAILBOX
             // an exact tie is flagged (the ray is traced again by
             // tie_retrace_i); the key tells a primitive of one instance from
             // the same primitive of another, and a retest from a tie
-            const uint32_t key = __float_as_uint(f2.z) ^ ((r.bits & SB_INST) ? (inst + 1u) * 0x9E3779B1u : 0u);
-            r.bits |= (h & (t == r.best) & (key != r.bestKey)) ? SB_TIE : 0u;
-            if (h) r.bestKey = key;
+            const uint32_t tkey = key ^ ((r.bits & SB_INST) ? (inst + 1u) * 0x9E3779B1u : 0u);
+            r.bits |= (h & (t == r.best) & (tkey != r.bestKey)) ? SB_TIE : 0u;
+            if (h) r.bestKey = tkey;
 #endif
             if (h) {
                 r.bits |= SB_FOUND;
                 if (r.bits & SB_SHADOW) return true;   // any hit occludes
                 r.best = t;
-                stS(P.hit + idx, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | __float_as_uint(f2.w)) : __float_as_uint(f2.w))));
+                stS(P.hit + idx, make_float4(t, u, v, __uint_as_float(isRect ? (0x80000000u | pid) : pid)));
                 P.hitInst[idx] = (r.bits & SB_INST) ? inst : 0xFFFFFFFFu;
             }
         } else {
             inst = __float_as_uint(f2.w);
             r.bits |= SB_PEND;
         }
-        ++r.lfE;
+        if (!defer) ++r.lfE;
     }
     if (inner) {
         if (COUNT) cnt.nodes++;

@@ -985,7 +985,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
             return fail(MTSG_ERR_INVALID);
         }
     }
-    ds.env = DevEnv{nullptr, nullptr, nullptr, nullptr, nullptr};
+    ds.env = DevEnv{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (d->has_envmap) {
         const mtsg_envmap &E = d->envmap;
         const mtsg_mipmap &EM = E.mip;
@@ -999,12 +999,23 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
             need = std::max(need, (size_t)EM.level_offset[l] + 3 * (size_t)EM.level_w[l] * EM.level_h[l]);
         if (need > d->n_env_texels) { g_err = "environment map texel array too small"; return fail(MTSG_ERR_INVALID); }
         mtsg_envmap *dE; float *dt, *dr, *dc, *dw;
+        uint32_t *dgr, *dgc;
         const int W = EM.level_w[0], H = EM.level_h[0];
+        // guide tables of the CDF searches (envmap.h env_sample_reuse_guided):
+        // entry g = std::lower_bound of g / ENV_GUIDE over the size + 1 entries
+        auto guides = [](const float *cdf, uint32_t size, uint32_t *out) {
+            for (uint32_t g = 0; g <= ENV_GUIDE; ++g)
+                out[g] = (uint32_t)(std::lower_bound(cdf, cdf + size + 1, (float)g / (float)ENV_GUIDE) - cdf);
+        };
+        std::vector<uint32_t> gr(ENV_GUIDE + 1), gc((size_t)(ENV_GUIDE + 1) * H);
+        guides(d->env_cdf_rows, (uint32_t)H, gr.data());
+        for (int y = 0; y < H; ++y) guides(d->env_cdf_cols + (size_t)y * (W + 1), (uint32_t)W, gc.data() + (size_t)y * (ENV_GUIDE + 1));
         if ((rc = up(&E, 1, &dE)) || (rc = up(d->env_texels, d->n_env_texels, &dt)) ||
             (rc = up(d->env_cdf_rows, (size_t)H + 1, &dr)) || (rc = up(d->env_cdf_cols, (size_t)(W + 1) * H, &dc)) ||
-            (rc = up(d->env_row_weights, (size_t)H, &dw)))
+            (rc = up(d->env_row_weights, (size_t)H, &dw)) || (rc = up(gr.data(), gr.size(), &dgr)) ||
+            (rc = up(gc.data(), gc.size(), &dgc)))
             return fail(rc);
-        ds.env = DevEnv{dE, dt, dr, dc, dw};
+        ds.env = DevEnv{dE, dt, dr, dc, dw, dgr, dgc};
     }
     // bitmap textures (mipmap.h) and the per-triangle records of their lookups
     ds.textures = nullptr; ds.tex_texels = nullptr; ds.ttex = nullptr;
