@@ -44,6 +44,12 @@ struct DevScene {
     // per rectangle its to_object rows as 3 float4 (48 B, the size of a
     // TriAccel record): MTSG_RECT_PEND reads them through the primitive slot
     const float4 *__restrict__ rectM;
+    // per rectangle its shading data, 2 float4 (one fetch per hit instead of
+    // the rectangle, then its shape): {frame_n, shape}, {dpdu, bsdf | (emitter + 1) << 16}
+    const float4 *__restrict__ rectSh;
+    // per emitter 4 float4: a rectangle's to_world rows, then {frame_n, shape
+    // type}; the sampling of a rectangle emitter reads only these
+    const float4 *__restrict__ emitRect;
     const mtsg_shape *__restrict__ shapes;
     const mtsg_bsdf *__restrict__ bsdfs;
     const mtsg_emitter *__restrict__ emitters;
@@ -2294,13 +2300,14 @@ DEV void fill_its(const DevScene &S, float3 ro, float3 rd, float4 h, uint32_t in
                         W2.x * pl.x + W2.y * pl.y + W2.z * pl.z + W2.w);
         }
     } else {
-        const mtsg_rect &r = S.rects[p & 0x7FFFFFFFu];
-        its.shape = (int)r.shape_index;
-        its.bsdf = S.shapes[its.shape].bsdf;
-        its.emitter = S.shapes[its.shape].emitter;
-        its.geoN = ld3(r.frame_n);
+        const float4 a = S.rectSh[2 * (size_t)(p & 0x7FFFFFFFu)], b = S.rectSh[2 * (size_t)(p & 0x7FFFFFFFu) + 1];
+        its.shape = (int)__float_as_uint(a.w);
+        const uint32_t be = __float_as_uint(b.w);
+        its.bsdf = (int)(be & 0xFFFFu);
+        its.emitter = (int)(be >> 16) - 1;
+        its.geoN = xyz(a);
         n = its.geoN;
-        dpdu = ld3(r.dpdu);
+        dpdu = xyz(b);
         its.p = ro + rd * h.x;
     }
     its.sh.n = n;
@@ -2389,9 +2396,12 @@ DEV float3 texture_eval(const DevScene &S, int tex, float4 h, uint32_t inst, con
 
 // Shape::sampleDirect over TriMesh / Rectangle samplePosition (shape.cpp:102-115,
 // trimesh.cpp:412-423, triangle.cpp:24-60, rectangle.cpp:200-207)
-DEV void emitter_sample_position(const DevScene &S, const mtsg_emitter &em, float sx, float sy, float3 &p, float3 &n) {
-    const mtsg_shape &sh = S.shapes[em.shape];
-    if (sh.type == MTSG_SHAPE_MESH) {
+DEV void emitter_sample_position(const DevScene &S, const mtsg_emitter &em, uint32_t ei, float sx, float sy, float3 &p,
+                                 float3 &n) {
+    const float4 *er = S.emitRect + 4 * (size_t)ei;
+    const float4 r0 = er[0], r1 = er[1], r2 = er[2], r3 = er[3];
+    if (__float_as_uint(r3.w) == (uint32_t)MTSG_SHAPE_MESH) {
+        const mtsg_shape &sh = S.shapes[em.shape];
         float pdfDummy;
         uint32_t index = pmf_sample_reuse(S.emitter_tri_cdf + em.cdf_offset, sh.tri_count, sy, pdfDummy);
         const uint4 ti = S.tidx[sh.tri_begin + index];
@@ -2405,11 +2415,9 @@ DEV void emitter_sample_position(const DevScene &S, const mtsg_emitter &em, floa
         else
             n = normalize(cross(sideA, sideB));
     } else {
-        const mtsg_rect &r = S.rects[sh.rect];
-        const float *m = r.to_world;
-        float x = sx * 2 - 1, y = sy * 2 - 1;
-        p = mk3(m[0] * x + m[1] * y + m[3], m[4] * x + m[5] * y + m[7], m[8] * x + m[9] * y + m[11]);
-        n = ld3(r.frame_n);
+        const float x = sx * 2 - 1, y = sy * 2 - 1;
+        p = mk3(r0.x * x + r0.y * y + r0.w, r1.x * x + r1.y * y + r1.w, r2.x * x + r2.y * y + r2.w);
+        n = xyz(r3);
     }
 }
 
@@ -2655,7 +2663,7 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
                     accepted = env_sample_direct(S.env, its.p, sx, sy, dd, dist, value, pdf);
                 } else {
                     float3 ep, en;
-                    emitter_sample_position(S, E, sx, sy, ep, en);
+                    emitter_sample_position(S, E, ei, sx, sy, ep, en);
                     dd = ep - its.p;
                     const float distSquared = dot(dd, dd);
                     dist = sqrtf(distSquared);
@@ -2899,7 +2907,7 @@ DEV void shade_path_om(const DevScene &S, const DevIntegrator &I, const DevBatch
                 onSurface = false;
             } else {
                 float3 en;
-                emitter_sample_position(S, E, sx, sy, ep, en);
+                emitter_sample_position(S, E, ei, sx, sy, ep, en);
                 dd = ep - its.p;
                 const float distSquared = dot(dd, dd);
                 dist = sqrtf(distSquared);

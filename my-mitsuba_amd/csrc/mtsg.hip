@@ -922,9 +922,43 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
                 const float *m = d->rects[i].to_object + 4 * k;
                 rm[3 * i + k] = make_float4(m[0], m[1], m[2], m[3]);
             }
-        float4 *drm;
-        if ((rc = up(rm.data(), rm.size(), &drm))) return fail(rc);
+        // per rectangle its shading data, per emitter its rectangle's rows
+        // (DevScene::rectSh / emitRect)
+        if (d->n_bsdfs >= 0xFFFFu || d->n_emitters >= 0xFFFEu) { g_err = "too many BSDFs or emitters"; return fail(MTSG_ERR_INVALID); }
+        std::vector<float4> rs((size_t)2 * std::max<uint32_t>(d->n_rects, 1u), make_float4(0, 0, 0, 0));
+        for (uint32_t i = 0; i < d->n_rects; ++i) {
+            const mtsg_rect &R = d->rects[i];
+            if (R.shape_index >= d->n_shapes) { g_err = "rectangle with an invalid shape index"; return fail(MTSG_ERR_INVALID); }
+            const mtsg_shape &sh = d->shapes[R.shape_index];
+            uint32_t be = ((uint32_t)sh.bsdf & 0xFFFFu) | (uint32_t)(sh.emitter + 1) << 16, si = R.shape_index;
+            float bef, sif;
+            memcpy(&bef, &be, 4);
+            memcpy(&sif, &si, 4);
+            rs[2 * i] = make_float4(R.frame_n[0], R.frame_n[1], R.frame_n[2], sif);
+            rs[2 * i + 1] = make_float4(R.dpdu[0], R.dpdu[1], R.dpdu[2], bef);
+        }
+        std::vector<float4> er((size_t)4 * std::max<uint32_t>(d->n_emitters, 1u), make_float4(0, 0, 0, 0));
+        for (uint32_t e = 0; e < d->n_emitters; ++e) {
+            const int32_t sidx = d->emitters[e].shape;
+            uint32_t type = (uint32_t)MTSG_SHAPE_MESH + 100u;   // not a shape emitter (environment)
+            if (sidx >= 0 && (uint32_t)sidx < d->n_shapes) {
+                const mtsg_shape &sh = d->shapes[sidx];
+                type = (uint32_t)sh.type;
+                if (sh.type == MTSG_SHAPE_RECT && sh.rect < d->n_rects) {
+                    const mtsg_rect &R = d->rects[sh.rect];
+                    for (int k = 0; k < 3; ++k)
+                        er[4 * e + k] = make_float4(R.to_world[4 * k], R.to_world[4 * k + 1], R.to_world[4 * k + 2], R.to_world[4 * k + 3]);
+                    er[4 * e + 3] = make_float4(R.frame_n[0], R.frame_n[1], R.frame_n[2], 0.f);
+                }
+            }
+            memcpy(&er[4 * e + 3].w, &type, 4);
+        }
+        float4 *drm, *drs, *der;
+        if ((rc = up(rm.data(), rm.size(), &drm)) || (rc = up(rs.data(), rs.size(), &drs)) || (rc = up(er.data(), er.size(), &der)))
+            return fail(rc);
         ds.rectM = drm;
+        ds.rectSh = drs;
+        ds.emitRect = der;
     }
     ds.tidx = dtidx; ds.shrec = dshrec; ds.rects = rects; ds.shapes = shapes; ds.bsdfs = bsdfs;
     ds.emitters = emitters; ds.emitter_cdf = ecdf; ds.emitter_tri_cdf = etcdf;
