@@ -488,8 +488,11 @@ def main():
                    "finish_ms": acc["ms_finish"] / k, "finish_paths": acc["paths_finish"] // k,
                    "finish_launches": acc["launches_finish"] // k}
         # counter-backed bandwidth of the other kernels: memory-side bytes of
-        # one frame (the committed PMC set of this configuration) / this
-        # run's HIP-event time of that kernel per frame
+        # one frame (the committed PMC set of this configuration) / the same
+        # set's rocprofv3 kernel time per frame (average duration x launches
+        # per frame, so bytes and time come from one profiler on the same
+        # kernels; HIP events bracket short kernels loosely, round-3 VERDICT
+        # weak #6); this run's HIP-event time is reported beside it
         pj, psrc = pmc_lookup(pmc_key(a, world))
         if pj:
             fam_ms = {"k_shade": kernels["shade_ms"], "k_finish": kernels["finish_ms"],
@@ -498,10 +501,14 @@ def main():
             for fam, ms in fam_ms.items():
                 ks = [v for n, v in pj["kernels"].items() if n == fam or n.startswith(fam + "<")]
                 b = sum(v.get("traffic_bytes_per_step", 0.0) for v in ks)
-                if b > 0 and ms > 0:
+                rp_ns = sum(v["rocprof_stats"]["avg_ns"] * v.get("launches_fetch_pass", 0) for v in ks
+                            if "rocprof_stats" in v)
+                if b > 0 and rp_ns > 0:
                     hits = [v["tcc_hit_rate"] for v in ks if "tcc_hit_rate" in v]
-                    pmc[fam] = {"bytes_per_frame": round(b), "GBps": round(b / (ms / 1e3) / 1e9, 1),
-                                "frac_of_hbm_peak": round(b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                    gbps = b / (rp_ns / 1e9) / 1e9
+                    pmc[fam] = {"bytes_per_frame": round(b), "rocprof_ms_per_frame": round(rp_ns / 1e6, 3),
+                                "GBps": round(gbps, 1), "frac_of_hbm_peak": round(gbps / HBM_PEAK_GBS, 4),
+                                "GBps_hip_events": round(b / (ms / 1e3) / 1e9, 1) if ms > 0 else None,
                                 "tcc_hit_rate": hits[0] if len(hits) == 1 else None}
             kernels["pmc"] = pmc
             kernels["pmc_source"] = psrc
