@@ -647,6 +647,17 @@ typedef struct mtsg_kd_tree {
 
 int  mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bounds, const mtsg_kd_build_params *params,
                    mtsg_kd_tree *out);
+/* Refit (the reference rebuilds, gkdtree.h:958-1240): `tree`'s
+ * node structure and split planes kept, its leaves refilled on the GPU from
+ * the scene's current primitives (prim_bounds / vtx_pos / tri_idx of the same
+ * primitive numbering), straddling triangles clipped to the child boxes as the
+ * build clips them.  For geometry that moved or deformed between frames: every
+ * primitive is referenced by every leaf its clipped box overlaps, so
+ * traversal stays exact; the old planes' SAH quality is what degrades.  Leaf
+ * ranges are re-laid out breadth first; the AABB is recomputed.  Free with
+ * mtsg_kd_free. */
+int  mtsg_kd_refit(int device, const mtsg_scene_desc *scene, const float *prim_bounds, const mtsg_kd_tree *tree,
+                   mtsg_kd_tree *out);
 void mtsg_kd_free(mtsg_kd_tree *tree);
 
 /* Debug: the scene sampler's draws for sample s of film pixel (x, y): kinds[i]

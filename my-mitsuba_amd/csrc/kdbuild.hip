@@ -815,6 +815,217 @@ int mtsg_kd_build(int device, const mtsg_scene_desc *scene, const float *prim_bo
     return MTSG_OK;
 }
 
+// Refit: a tree's topology and split planes kept, its leaves refilled from the
+// primitives' current bounds (deforming or moving geometry between frames, a
+// rebuild without the SAH search).  The references are pushed down the given
+// tree level by level with the build's own classification (k_count /
+// k_scatter: straddling triangles clipped to each child box, Mitsuba's perfect
+// splits), planar references in a split plane going left; every primitive
+// therefore lands in every leaf its clipped box overlaps, so the tree answers
+// exactly, at the SAH cost of the old planes.  Leaf ranges are re-laid out
+// breadth first in the build's index order; inner nodes keep their words.
+int mtsg_kd_refit(int device, const mtsg_scene_desc *scene, const float *prim_bounds, const mtsg_kd_tree *tree,
+                  mtsg_kd_tree *out) {
+    using clock = std::chrono::steady_clock;
+    const uint32_t n_prims = scene ? scene->n_prims : 0;
+    if (!out || !scene || !tree || !tree->nodes || tree->n_nodes == 0 || (n_prims && !prim_bounds) ||
+        (scene->n_triangles && (!scene->vtx_pos || !scene->tri_idx)) || scene->n_triangles > n_prims) {
+        mtsg::set_last_error("mtsg_kd_refit: invalid arguments");
+        return MTSG_ERR_INVALID;
+    }
+    // the input tree must be well formed: children inside the array, acyclic
+    // (each node reached once), breadth-first child pairs as the build writes
+    {
+        std::vector<uint8_t> seen(tree->n_nodes, 0);
+        std::vector<uint32_t> st{0u};
+        seen[0] = 1;
+        while (!st.empty()) {
+            const uint32_t i = st.back();
+            st.pop_back();
+            const mtsg_kdnode &N = tree->nodes[i];
+            if (N.combined & 0x80000000u) continue;
+            const uint64_t l = (uint64_t)i + ((N.combined & ~(3u | 0x40000000u)) >> 2);
+            if ((N.combined & 3u) == 3u || l <= i || l + 1 >= tree->n_nodes || seen[l] || seen[l + 1]) {
+                mtsg::set_last_error("mtsg_kd_refit: malformed tree");
+                return MTSG_ERR_INVALID;
+            }
+            seen[l] = seen[l + 1] = 1;
+            st.push_back((uint32_t)l);
+            st.push_back((uint32_t)l + 1);
+        }
+    }
+    memset(out, 0, sizeof(*out));
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        mtsg::set_last_error("mtsg_kd_refit: no such device");
+        return MTSG_ERR_NODEVICE;
+    }
+    if (hipSetDevice(device) != hipSuccess) { mtsg::set_last_error("hipSetDevice failed"); return MTSG_ERR_DEVICE; }
+    const auto t0 = clock::now();
+    auto fail = [&](const char *what) {
+        mtsg::set_last_error(std::string("mtsg_kd_refit: ") + what);
+        return MTSG_ERR_DEVICE;
+    };
+    std::vector<Ref> refs0;
+    refs0.reserve(n_prims);
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = 0; i < n_prims; ++i) {
+        const float *b = prim_bounds + 6 * (size_t)i;
+        if (!(b[0] <= b[3] && b[1] <= b[4] && b[2] <= b[5])) continue;
+        Ref r;
+        r.mn = make_float4(b[0], b[1], b[2], bitsToFloat(i));
+        r.mx = make_float4(b[3], b[4], b[5], bitsToFloat(0u));
+        refs0.push_back(r);
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], b[k]); hi[k] = std::max(hi[k], b[3 + k]); }
+    }
+    const uint32_t nLive = (uint32_t)refs0.size();
+    if (nLive == 0)
+        for (int k = 0; k < 3; ++k) { lo[k] = 0; hi[k] = 0; }
+    std::vector<mtsg_kdnode> nodes(tree->nodes, tree->nodes + tree->n_nodes);
+    DevBuf dRefs, dNext, dNodes, dPlans, dCnt, dIdx, dRanges, dVtx, dTri;
+    size_t capRefs = std::max<size_t>(1024, (size_t)nLive * 2);
+    size_t capIdx = capRefs;
+    if (!dRefs.reserve(capRefs * sizeof(Ref)) || !dNext.reserve(capRefs * sizeof(Ref)) || !dIdx.reserve(capIdx * sizeof(uint32_t)))
+        return fail("out of device memory");
+    if (nLive && hipMemcpy(dRefs.p, refs0.data(), (size_t)nLive * sizeof(Ref), hipMemcpyHostToDevice) != hipSuccess) return fail("upload");
+    Geo geo{nullptr, nullptr, scene->n_triangles};
+    if (scene->n_triangles) {
+        std::vector<float4> v(scene->n_vertices);
+        std::vector<uint4> t(scene->n_triangles);
+        for (uint32_t i = 0; i < scene->n_vertices; ++i)
+            v[i] = make_float4(scene->vtx_pos[3 * i], scene->vtx_pos[3 * i + 1], scene->vtx_pos[3 * i + 2], 0.f);
+        for (uint32_t i = 0; i < scene->n_triangles; ++i) {
+            t[i] = make_uint4(scene->tri_idx[3 * i], scene->tri_idx[3 * i + 1], scene->tri_idx[3 * i + 2], 0u);
+            if (t[i].x >= scene->n_vertices || t[i].y >= scene->n_vertices || t[i].z >= scene->n_vertices) {
+                mtsg::set_last_error("mtsg_kd_refit: triangle index out of range");
+                return MTSG_ERR_INVALID;
+            }
+        }
+        if (!dVtx.reserve(v.size() * sizeof(float4)) || !dTri.reserve(t.size() * sizeof(uint4)) ||
+            hipMemcpy(dVtx.p, v.data(), v.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dTri.p, t.data(), t.size() * sizeof(uint4), hipMemcpyHostToDevice) != hipSuccess)
+            return fail("upload");
+        geo.vtx = dVtx.as<float4>();
+        geo.tri = dTri.as<uint4>();
+    }
+    std::vector<HostNode> level;
+    level.push_back(HostNode{0, nLive, 0, 0, 0, {lo[0], lo[1], lo[2]}, {hi[0], hi[1], hi[2]}});
+    std::vector<uint2> leafRanges;
+    std::vector<NodeDev> nd;
+    std::vector<Plan> plans;
+    std::vector<uint32_t> counts;
+    uint32_t nRefs = nLive, nIndices = 0, depthReached = 0;
+    while (!level.empty()) {
+        const uint32_t nN = (uint32_t)level.size();
+        nd.resize(nN);
+        plans.assign(nN, Plan{-1, 0.0f, 0, 0, 0, 1u, {0, 0}});
+        for (uint32_t i = 0; i < nN; ++i) {
+            const HostNode &h = level[i];
+            nd[i] = NodeDev{h.begin, h.count, {h.lo[0], h.lo[1], h.lo[2]}, {h.hi[0], h.hi[1], h.hi[2]}};
+            depthReached = std::max(depthReached, h.depth);
+            const mtsg_kdnode &N = nodes[h.out];
+            if (!(N.combined & 0x80000000u)) {
+                plans[i].axis = (int)(N.combined & 3u);
+                plans[i].split = bitsToFloat(N.data);
+            }
+        }
+        if (!dNodes.reserve(nN * sizeof(NodeDev)) || !dPlans.reserve(nN * sizeof(Plan)) || !dCnt.reserve((size_t)nN * 2 * 4))
+            return fail("out of device memory");
+        if (hipMemcpy(dNodes.p, nd.data(), nN * sizeof(NodeDev), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dPlans.p, plans.data(), nN * sizeof(Plan), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemset(dCnt.p, 0, (size_t)nN * 2 * 4) != hipSuccess)
+            return fail("upload");
+        if (nRefs)
+            hipLaunchKernelGGL(k_count, dim3((nRefs + BLK - 1) / BLK), dim3(BLK), 0, 0, dRefs.as<Ref>(), nRefs, dPlans.as<Plan>(),
+                               dNodes.as<NodeDev>(), geo, dCnt.as<uint32_t>());
+        counts.resize((size_t)nN * 2);
+        if (hipMemcpy(counts.data(), dCnt.p, counts.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return fail("download");
+        std::vector<HostNode> next;
+        uint32_t nextRefs = 0;
+        for (uint32_t i = 0; i < nN; ++i) {
+            const HostNode &h = level[i];
+            Plan &p = plans[i];
+            mtsg_kdnode &N = nodes[h.out];
+            if (p.axis < 0) {
+                p.out0 = nIndices;
+                N.combined = 0x80000000u | nIndices;
+                N.data = nIndices + h.count;
+                leafRanges.push_back(make_uint2(nIndices, nIndices + h.count));
+                nIndices += h.count;
+                continue;
+            }
+            const uint32_t left = h.out + ((N.combined & ~(3u | 0x40000000u)) >> 2);
+            p.child0 = (uint32_t)next.size();
+            p.out0 = nextRefs;
+            p.out1 = nextRefs + counts[2 * i];
+            HostNode L{p.out0, counts[2 * i], left, h.depth + 1, 0, {h.lo[0], h.lo[1], h.lo[2]}, {h.hi[0], h.hi[1], h.hi[2]}};
+            HostNode R{p.out1, counts[2 * i + 1], left + 1, h.depth + 1, 0, {h.lo[0], h.lo[1], h.lo[2]}, {h.hi[0], h.hi[1], h.hi[2]}};
+            L.hi[p.axis] = p.split;
+            R.lo[p.axis] = p.split;
+            next.push_back(L);
+            next.push_back(R);
+            nextRefs += counts[2 * i] + counts[2 * i + 1];
+        }
+        if (nextRefs > capRefs) {
+            const size_t cap = (size_t)nextRefs * 3 / 2;
+            DevBuf grown;
+            if (!grown.reserve(cap * sizeof(Ref)) ||
+                (nRefs && hipMemcpy(grown.p, dRefs.p, (size_t)nRefs * sizeof(Ref), hipMemcpyDeviceToDevice) != hipSuccess))
+                return fail("out of device memory");
+            std::swap(dRefs.p, grown.p);
+            std::swap(dRefs.bytes, grown.bytes);
+            if (!dNext.reserve(cap * sizeof(Ref))) return fail("out of device memory");
+            capRefs = cap;
+        }
+        if (nIndices > capIdx) {
+            const size_t cap = (size_t)nIndices * 3 / 2;
+            DevBuf grown;
+            if (!grown.reserve(cap * 4) || hipMemcpy(grown.p, dIdx.p, capIdx * 4, hipMemcpyDeviceToDevice) != hipSuccess)
+                return fail("out of device memory");
+            std::swap(dIdx.p, grown.p);
+            std::swap(dIdx.bytes, grown.bytes);
+            capIdx = cap;
+        }
+        if (hipMemcpy(dPlans.p, plans.data(), nN * sizeof(Plan), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemset(dCnt.p, 0, (size_t)nN * 2 * 4) != hipSuccess)
+            return fail("upload");
+        if (nRefs)
+            hipLaunchKernelGGL(k_scatter, dim3((nRefs + BLK - 1) / BLK), dim3(BLK), 0, 0, dRefs.as<Ref>(), nRefs, dPlans.as<Plan>(),
+                               dNodes.as<NodeDev>(), geo, dCnt.as<uint32_t>(), dNext.as<Ref>(), dIdx.as<uint32_t>());
+        std::swap(dRefs.p, dNext.p);
+        std::swap(dRefs.bytes, dNext.bytes);
+        nRefs = nextRefs;
+        level.swap(next);
+    }
+    const uint32_t nLeaves = (uint32_t)leafRanges.size();
+    if (nLeaves) {
+        if (!dRanges.reserve(nLeaves * sizeof(uint2)) ||
+            hipMemcpy(dRanges.p, leafRanges.data(), nLeaves * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess)
+            return fail("upload");
+        hipLaunchKernelGGL(k_sort_leaves, dim3((nLeaves + BLK - 1) / BLK), dim3(BLK), 0, 0, dIdx.as<uint32_t>(), dRanges.as<uint2>(), nLeaves);
+    }
+    std::vector<uint32_t> idx(nIndices);
+    if (nIndices && hipMemcpy(idx.data(), dIdx.p, (size_t)nIndices * 4, hipMemcpyDeviceToHost) != hipSuccess) return fail("download");
+    if (hipDeviceSynchronize() != hipSuccess) return fail("kernel failure");
+    out->n_nodes = (uint32_t)nodes.size();
+    out->n_indices = (uint32_t)idx.size();
+    out->nodes = (mtsg_kdnode *)malloc(nodes.size() * sizeof(mtsg_kdnode));
+    out->indices = (uint32_t *)malloc(std::max<size_t>(1, idx.size()) * sizeof(uint32_t));
+    if (!out->nodes || !out->indices) { mtsg_kd_free(out); mtsg::set_last_error("mtsg_kd_refit: out of host memory"); return MTSG_ERR_OOM; }
+    memcpy(out->nodes, nodes.data(), nodes.size() * sizeof(mtsg_kdnode));
+    if (!idx.empty()) memcpy(out->indices, idx.data(), idx.size() * sizeof(uint32_t));
+    const float eps = 1e-3f;   // the enlarged AABB of the build (gkdtree.h:1213-1220)
+    for (int k = 0; k < 3; ++k) {
+        const float ext = hi[k] - lo[k];
+        out->aabb_min[k] = lo[k] - ext * eps - eps;
+        out->aabb_max[k] = hi[k] + (hi[k] - out->aabb_min[k]) * eps + eps;
+    }
+    out->max_depth = depthReached;
+    out->leaves = nLeaves;
+    out->ms_build = std::chrono::duration<double, std::milli>(clock::now() - t0).count();
+    return MTSG_OK;
+}
+
 void mtsg_kd_free(mtsg_kd_tree *t) {
     if (!t) return;
     free(t->nodes);

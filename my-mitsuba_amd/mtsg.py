@@ -111,6 +111,10 @@ def kd_build(scene: "Scene", bounds: np.ndarray | None = None, device: int = 0, 
     t = KDTree()
     if lib.mtsg_kd_build(device, scene.desc, _ptr(b), C.byref(p), C.byref(t)) != 0:
         raise RuntimeError(_err(lib, "mtsg_last_error"))
+    return _take_tree(lib, t)
+
+
+def _take_tree(lib, t: "KDTree") -> dict:
     try:
         out = dict(nodes=np.ctypeslib.as_array(t.nodes, (t.n_nodes * 2,)).reshape(-1, 2).copy(),
                    indices=np.ctypeslib.as_array(t.indices, (max(t.n_indices, 1),))[:t.n_indices].copy(),
@@ -119,6 +123,25 @@ def kd_build(scene: "Scene", bounds: np.ndarray | None = None, device: int = 0, 
     finally:
         lib.mtsg_kd_free(C.byref(t))
     return out
+
+
+def kd_refit(scene: "Scene", tree: dict, bounds: np.ndarray | None = None, device: int = 0) -> dict:
+    """The tree's nodes and split planes kept, its leaves refilled on the GPU
+    from the scene's current primitives (mtsg_kd_refit); tree: a dict of
+    kd_build's form (nodes (n, 2) uint32, indices)."""
+    lib = device_lib()
+    b = np.ascontiguousarray(scene.prim_bounds() if bounds is None else bounds, dtype=np.float32)
+    nodes = np.ascontiguousarray(tree["nodes"], dtype=np.uint32)
+    idx = np.ascontiguousarray(tree["indices"], dtype=np.uint32)
+    tin = KDTree()
+    tin.nodes = nodes.ctypes.data_as(C.POINTER(C.c_uint32))
+    tin.n_nodes = nodes.shape[0]
+    tin.indices = idx.ctypes.data_as(C.POINTER(C.c_uint32))
+    tin.n_indices = idx.size
+    t = KDTree()
+    if lib.mtsg_kd_refit(device, scene.desc, _ptr(b), C.byref(tin), C.byref(t)) != 0:
+        raise RuntimeError(_err(lib, "mtsg_last_error"))
+    return _take_tree(lib, t)
 
 
 class OMHeader(C.Structure):
@@ -165,7 +188,7 @@ DEVICE_SYMBOLS = [
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_cancel_clear", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
-    "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_kd_build", "mtsg_kd_free",
+    "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_kd_build", "mtsg_kd_refit", "mtsg_kd_free",
     "mtsg_sampler_draws", "mtsg_debug_wavetimes", "mtsg_set_tile_callback",
     "mtsg_debug_stragglers",
 ]
@@ -284,6 +307,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_tex_eval.argtypes = [C.c_void_p, C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_kd_build.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.POINTER(KDBuildParams), C.POINTER(KDTree)]
         lib.mtsg_kd_free.argtypes = [C.POINTER(KDTree)]
+        lib.mtsg_kd_refit.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.POINTER(KDTree), C.POINTER(KDTree)]
         lib.mtsg_om_query.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_sampler_draws.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_int, C.c_uint32,
                                            C.c_uint32, C.c_void_p, C.c_void_p]

@@ -109,3 +109,75 @@ def test_c3_device_tree(c3):
     check_render(c, gi)
     gh.close()
     gd.close()
+
+
+def leaf_sets(tree):
+    """{node index: the leaf's primitive indices} of a tree dict"""
+    nodes, idx = tree["nodes"], tree["indices"]
+    out = {}
+    for i in range(nodes.shape[0]):
+        c, d = int(nodes[i, 0]), int(nodes[i, 1])
+        if c & 0x80000000:
+            out[i] = tuple(idx[c & 0x7FFFFFFF:d].tolist())
+    return out
+
+
+def test_refit_unchanged_geometry_gives_the_same_leaves():
+    """mtsg_kd_refit over the geometry the tree was built on: every leaf gets
+    back exactly its primitives (the build's classification and clipping,
+    the retracted leaves hold the union of their former subtrees)."""
+    s = mtsg.Scene(os.path.join(SCENES, "cbox_glass.xml"), {"width": 32, "height": 24, "spp": 1})
+    b = s.prim_bounds()
+    tree = mtsg.kd_build(s, b)
+    re = mtsg.kd_refit(s, tree, b)
+    walk(re, b.shape[0], b)
+    np.testing.assert_array_equal(re["nodes"][:, 0] & 0x80000003, tree["nodes"][:, 0] & 0x80000003)
+    inner = (tree["nodes"][:, 0] & 0x80000000) == 0
+    np.testing.assert_array_equal(re["nodes"][inner], tree["nodes"][inner])
+    assert leaf_sets(re) == leaf_sets(tree)
+
+
+def test_refit_moved_geometry_answers_exactly():
+    """The tree of the Cornell box with the glass box on its default place,
+    refit after the box moved 0.5 up (the same XML, -D glassY): the refit tree
+    must answer every closest-hit query as brute force over the moved scene
+    does (the Havran traversal of the oracle over it), and the GPU over it must
+    render the moved scene at parity."""
+    a = mtsg.Scene(os.path.join(SCENES, "cbox_glass.xml"), {"width": 32, "height": 24, "spp": 1})
+    m = mtsg.Scene(os.path.join(SCENES, "cbox_glass.xml"), {"width": 32, "height": 24, "spp": 2, "glassY": -0.199})
+    ba, bm = a.prim_bounds(), m.prim_bounds()
+    assert ba.shape == bm.shape and not np.array_equal(ba, bm)
+    tree = mtsg.kd_build(a, ba)
+    re = mtsg.kd_refit(m, tree, bm)
+    walk(re, bm.shape[0], bm)
+    m.set_kdtree(re)
+    rays = random_rays(20000, -0.95, 0.95, seed=5)
+    t0, p0 = O.trace_closest_brute(m.desc, rays)
+    t1, _, _, p1 = O.trace_closest(m.desc, rays)
+    hit0, hit1 = p0 != 0xFFFFFFFF, p1 != 0xFFFFFFFF
+    np.testing.assert_array_equal(hit1, hit0)
+    same = hit0 & (p0 == p1)
+    np.testing.assert_array_equal(t1[same], t0[same])
+    assert same.sum() >= 0.995 * hit0.sum()
+    g = mtsg.GPUScene(m, 0)
+    try:
+        t2, _, _, p2 = g.trace_closest(rays)
+        np.testing.assert_array_equal(p2, p1)
+        np.testing.assert_array_equal(t2, t1)
+        _, c, gi = render_pair(m, g)
+        check_render(c, gi)
+    finally:
+        g.close()
+
+
+def test_c3_refit_time(c3):
+    """Refit of the C3 device tree over its own geometry: the time a
+    per-frame update of 1M triangles costs against the full build."""
+    host, dev, tree, b = c3
+    mtsg.kd_refit(dev, tree, b)   # warm-up
+    re = mtsg.kd_refit(dev, tree, b)
+    walk(re, b.shape[0], b)
+    print(f"C3 refit: {re['ms']:.1f} ms (device build {tree['ms']:.1f} ms), {re['indices'].size} refs "
+          f"(build {tree['indices'].size})")
+    assert re["indices"].size == tree["indices"].size
+    assert re["ms"] < tree["ms"]
