@@ -131,9 +131,9 @@ def test_refit_unchanged_geometry_gives_the_same_leaves():
     tree = mtsg.kd_build(s, b)
     re = mtsg.kd_refit(s, tree, b)
     walk(re, b.shape[0], b)
-    np.testing.assert_array_equal(re["nodes"][:, 0] & 0x80000003, tree["nodes"][:, 0] & 0x80000003)
-    inner = (tree["nodes"][:, 0] & 0x80000000) == 0
-    np.testing.assert_array_equal(re["nodes"][inner], tree["nodes"][inner])
+    leaf = (tree["nodes"][:, 0] & 0x80000000) != 0
+    np.testing.assert_array_equal((re["nodes"][:, 0] & 0x80000000) != 0, leaf)
+    np.testing.assert_array_equal(re["nodes"][~leaf], tree["nodes"][~leaf])
     assert leaf_sets(re) == leaf_sets(tree)
 
 
