@@ -9,6 +9,7 @@ export TMPDIR=/tmp
 step() { local name=$1 lim=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; tail -n 3 "$O/$name.log" | cut -c1-1500; if [ $rc -ne 0 ] && ! { [ "${name%%-*}" = tests ] && [ $rc -eq 1 ]; }; then exit $rc; fi; }
 PYT="python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread"
 for w in ${*:-tests bench}; do
+  # a step may be repeated as name@k (its own log); the variant name drops the @k
   case $w in
     tests) step tests 900 $PYT tests ;;
     mathprobe) step mathprobe 300 tools/math_probe 3 ;;
@@ -17,14 +18,15 @@ for w in ${*:-tests bench}; do
     tests-inst) step tests-inst 600 $PYT tests/test_gpu_instancing.py tests/test_gpu_edge_rays.py tests/test_gpu_finish.py ;;
     tests-entry) step tests-entry 600 $PYT tests/test_gpu_render_entry.py tests/test_gpu_edge_rays.py ;;
     tests-parity) step tests-parity 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_c4.py ;;
+    tests-kd) step tests-kd 600 $PYT tests/test_gpu_kdbuild.py ;;
     tests-new) step tests-new 600 $PYT tests/test_gpu_00_bench_ranks.py tests/test_gpu_c4.py tests/test_gpu_edge_rays.py ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
-    quick) step quick 300 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count ;;
+    quick*) step $w 300 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count ;;
     c5fin-*) v=${w#c5fin-}; step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count --finish-paths $v ;;
     c3fin-*) v=${w#c3fin-}; step $w 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count --finish-paths $v ;;
-    inst-quick) step inst-quick 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity --no-count ;;
-    instvar-*) v=${w#instvar-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity --no-count ;;
-    c5quick) step c5quick 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
+    inst-quick*) step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity --no-count ;;
+    instvar-*) v=${w#instvar-}; v=${v%@*}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity --no-count ;;
+    c5quick*) step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
     c2quick) step c2quick 300 python bench.py --steps 5 --warmup 2 --workload cbox --no-cpu --no-parity --no-count ;;
     inst) step inst 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity ;;
     e8) step e8 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity ;;
@@ -37,8 +39,8 @@ for w in ${*:-tests bench}; do
     bench-ocml) MTSG_LIB=my-mitsuba_amd/var/libmtsg_ocmlmath.so step bench-ocml 600 python bench.py --steps 10 --warmup 3 --no-cpu ;;
     c5-ocml) MTSG_LIB=my-mitsuba_amd/var/libmtsg_ocmlmath.so step c5-ocml 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu ;;
     vtests-*) v=${w#vtests-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_edge_rays.py ;;
-    var-*) v=${w#var-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count ;;
-    c5var-*) v=${w#c5var-}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
+    var-*) v=${w#var-}; v=${v%@*}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 python bench.py --steps 10 --warmup 3 --no-cpu --no-parity --no-count ;;
+    c5var-*) v=${w#c5var-}; v=${v%@*}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
     c5) step c5 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 ;;
     c2) step c2 600 python bench.py --steps 5 --warmup 2 --workload cbox ;;
     kd) step kd 300 python bench.py --steps 5 --warmup 2 --kd-build device --no-cpu --no-parity ;;
