@@ -37,7 +37,7 @@
 // (bit mask: 1 sincosf, 2 tanf, 4 atanf / atan2f, 8 acosf, 16 expf / logf);
 // a call keeps a long function's registers out of its caller's allocation
 #ifndef GMF_CALLS
-#define GMF_CALLS 0
+#define GMF_CALLS 13   // measured r04 (C3 / C5 Msamples/s): 0: 1500 / 1378, 13: 1515 / 1427, 31: 1506 / 1430, 14: 1484 / 1370
 #endif
 #define GMF __host__ __device__ __forceinline__
 #define GMF_CALL __host__ __device__ inline __attribute__((noinline))

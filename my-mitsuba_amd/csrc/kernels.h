@@ -171,7 +171,7 @@ struct ShadeLaunch {
     uint32_t nIdentity;
     int hasAlpha;
     uint32_t shadeMin;   // k_finish
-    bool env, ext;
+    bool env, ext, inst;   // inst: two-level instancing (k_finish<.., INST>)
 };
 template <int SMP> void launch_shade_smp(const ShadeLaunch &a);
 template <int SMP> void launch_finish_smp(const ShadeLaunch &a);
@@ -746,8 +746,15 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 // best's slot; prev's identity in LDS, the best's in its hit record.  Exact for
 // ties of two primitives; of three or more, a retest of the earliest one after
 // the later two is accepted where Mitsuba may skip it.
+// a rectangle met in a leaf is tested in the lane's next iteration, its rows
+// read through the primitive slot (no dependent fetch inside an iteration):
+// flat traversal (MTSG_RECT_PEND, measured r04: trace -0.7%, C3 +0.4%) and
+// two-level (MTSG_RECT_PEND_I, measured r04: 3% slower, off)
 #ifndef MTSG_RECT_PEND
-#define MTSG_RECT_PEND 0   // 1: a rectangle of the flat traversal is tested in the lane's next iteration
+#define MTSG_RECT_PEND 1
+#endif
+#ifndef MTSG_RECT_PEND_I
+#define MTSG_RECT_PEND_I 0
 #endif
 #ifndef MTSG_MAILBOX
 #define MTSG_MAILBOX 1   // 0: measurement variant, the last primitive tested wins a tie
@@ -1134,7 +1141,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     const float4 *irec = S.inst + 8 * (size_t)inst;
     const uint4 *a0 = pend ? reinterpret_cast<const uint4 *>(irec + 6) : S.blocks + base;
     const uint4 *a1 = pend ? reinterpret_cast<const uint4 *>(irec + 7) : S.blocks + base + off;
-#if MTSG_RECT_PEND
+#if MTSG_RECT_PEND_I
     // a top-level rectangle is tested in the lane's next iteration (its index
     // waits in `inst`, unused at the top level: groups hold no rectangles)
     const bool rp = (r.bits & SB_RPEND) != 0;
@@ -1158,7 +1165,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     bool enter = false;
     if (prim) {
         const uint32_t k = __float_as_uint(f0.x);
-#if MTSG_RECT_PEND
+#if MTSG_RECT_PEND_I
         const bool isRect = rp, defer = !rp && k == MTSG_TRIACCEL_SHAPE;
         enter = !rp && k == KINST;
 #else
@@ -1172,7 +1179,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         } else if (!enter) {
             if (COUNT) cnt.tests++;
             float t, u, v;
-#if MTSG_RECT_PEND
+#if MTSG_RECT_PEND_I
             bool h;
             uint32_t key, pid;
             if (rp) {
@@ -2546,7 +2553,7 @@ DEV PathLoads load_path_rest(const DevScene &S, const DevPaths &P, uint32_t i, b
 // MTSG_SHADE_PRELOAD: what k_shade loads together with the meta word (1:
 // every record of load_path, 2: the hit only, 0: nothing -- round 3)
 #ifndef MTSG_SHADE_PRELOAD
-#define MTSG_SHADE_PRELOAD 1
+#define MTSG_SHADE_PRELOAD 0   // measured r04: 1 (all) C3 -0.5%, C5 -3.5% (spills at the 128-VGPR cap); 2 (hit) C3 -0.4%
 #endif
 
 template <bool ENV, int SMP, bool EXT, class Out>
@@ -3142,7 +3149,10 @@ constexpr uint32_t FINISH_FETCH = 64;   // paths per wave draw (small pools: the
 // qin: work list of the paths at their current bounce (their hits are ready:
 // the bounce's trace launch ran).  shadeMin: a wave shades once that many of
 // its busy lanes wait for shading (or none is tracing).
-template <bool ENV, int SMP, bool EXT>
+// INST: the two-level traversal (and its exact tie retrace) is compiled only
+// into the instantiations for instanced scenes, so the flat kernel carries
+// neither its registers nor the retrace's scratch stack
+template <bool ENV, int SMP, bool EXT, bool INST>
 __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int qin, int hasAlpha, uint32_t shadeMin) {
     const SpecStack stk{};
     lds_top_init(S);
@@ -3161,7 +3171,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
     // misses the scene bounds gets its miss record and is shaded next
     auto startClosest = [&]() {
         const float4 ro = ldS(&P.ray_o[idx]), rd = ldS(&P.ray_d[idx]);
-        if (S.inst) P.hitInst[idx] = 0xFFFFFFFFu;   // two-level: no instance until a hit in one
+        if (INST) P.hitInst[idx] = 0xFFFFFFFFu;   // two-level: no instance until a hit in one
         if (spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, false, r)) {
             state = FS_TRACE;
         } else {
@@ -3221,12 +3231,12 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
         if (state == FS_TRACE) {
             // two-level scenes: the per-lane level switch of k_trace_s<.., true>
             // (its save slots are sized for this grid too)
-            if (S.inst) done = spec_iter_i<false>(S, r, tc, P, idx, trav_limits<false>(S), inst, ts);
+            if (INST) done = spec_iter_i<false>(S, r, tc, P, idx, trav_limits<false>(S), inst, ts);
             else done = spec_iter<false>(S, r, stk, tc, P.hit + idx, trav_limits<false>(S));
         }
         if (done) {
             if (MTSG_MAILBOX && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE) {
-                if (!S.inst) {
+                if (!INST) {
                     tie_retrace(S, r, stk, P.ray_o + idx, P.ray_d + idx, P.hit + idx, trav_limits<false>(S));
                 } else {
                     bool herr = false;

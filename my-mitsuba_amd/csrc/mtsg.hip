@@ -235,6 +235,7 @@ ShadeLaunch shade_args(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B,
     a.shadeMin = s->finishShadeMin;
     a.env = s->ds.has_env != 0;
     a.ext = s->extBsdfs;
+    a.inst = s->ds.inst != nullptr;
     return a;
 }
 void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {

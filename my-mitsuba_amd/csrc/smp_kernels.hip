@@ -29,26 +29,35 @@ void launch_shade_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
     }
 }
 
-template <>
-void launch_finish_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
+template <bool INST>
+void launch_finish_inst(const ShadeLaunch &a) {
     constexpr int SMP = MTSG_TU_SAMPLER;
     if (a.ext) {
-        if (a.env) hipLaunchKernelGGL((k_finish<true, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
-        else hipLaunchKernelGGL((k_finish<false, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
+        if (a.env) hipLaunchKernelGGL((k_finish<true, SMP, true, INST>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
+        else hipLaunchKernelGGL((k_finish<false, SMP, true, INST>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
     } else {
-        if (a.env) hipLaunchKernelGGL((k_finish<true, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
-        else hipLaunchKernelGGL((k_finish<false, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
+        if (a.env) hipLaunchKernelGGL((k_finish<true, SMP, false, INST>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
+        else hipLaunchKernelGGL((k_finish<false, SMP, false, INST>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
     }
+}
+
+template <>
+void launch_finish_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
+    if (a.inst) launch_finish_inst<true>(a);
+    else launch_finish_inst<false>(a);
 }
 
 #ifdef MTSG_TU_OCCUPANCY
 // persistent grid of k_finish (the register-heaviest variant bounds them all)
 int finish_blocks_per_cu() {
     int perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_finish<true, MTSG_SAMPLER_INDEPENDENT, true>, TRACE_BLOCK, 0) !=
-        hipSuccess)
+    int perCU2 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_finish<true, MTSG_SAMPLER_INDEPENDENT, true, false>, TRACE_BLOCK,
+                                                     0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU2, (const void *)k_finish<true, MTSG_SAMPLER_INDEPENDENT, true, true>, TRACE_BLOCK,
+                                                     0) != hipSuccess)
         return 0;
-    return perCU;
+    return std::min(perCU, perCU2);
 }
 #endif
 
