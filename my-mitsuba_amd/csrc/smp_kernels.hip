@@ -29,9 +29,11 @@ void launch_shade_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
     }
 }
 
-template <bool INST>
+// SMP is a template parameter (not this unit's constant): every unit defines
+// this template, and instantiations that differed only in their body would be
+// merged by the linker
+template <int SMP, bool INST>
 void launch_finish_inst(const ShadeLaunch &a) {
-    constexpr int SMP = MTSG_TU_SAMPLER;
     if (a.ext) {
         if (a.env) hipLaunchKernelGGL((k_finish<true, SMP, true, INST>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
         else hipLaunchKernelGGL((k_finish<false, SMP, true, INST>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.qin, a.hasAlpha, a.shadeMin);
@@ -43,8 +45,8 @@ void launch_finish_inst(const ShadeLaunch &a) {
 
 template <>
 void launch_finish_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
-    if (a.inst) launch_finish_inst<true>(a);
-    else launch_finish_inst<false>(a);
+    if (a.inst) launch_finish_inst<MTSG_TU_SAMPLER, true>(a);
+    else launch_finish_inst<MTSG_TU_SAMPLER, false>(a);
 }
 
 #ifdef MTSG_TU_OCCUPANCY
