@@ -748,10 +748,11 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 // the later two is accepted where Mitsuba may skip it.
 // a rectangle met in a leaf is tested in the lane's next iteration, its rows
 // read through the primitive slot (no dependent fetch inside an iteration):
-// flat traversal (MTSG_RECT_PEND, measured r04: trace -0.7%, C3 +0.4%) and
+// flat traversal (MTSG_RECT_PEND, measured r04: C3 trace -0.7%, but C5 trace
+// +3%: the 4 more VGPRs and the address select cost every iteration, off) and
 // two-level (MTSG_RECT_PEND_I, measured r04: 3% slower, off)
 #ifndef MTSG_RECT_PEND
-#define MTSG_RECT_PEND 1
+#define MTSG_RECT_PEND 0
 #endif
 #ifndef MTSG_RECT_PEND_I
 #define MTSG_RECT_PEND_I 0
