@@ -37,11 +37,17 @@ DEV float3 env_rot(const float *m, float3 v) {
     return mk3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z, m[6] * v.x + m[7] * v.y + m[8] * v.z);
 }
 
+// the lookup coordinates of a local direction (envmap.cpp:386-387 and
+// 606-607 compute the same two values)
+DEV void env_uv(float3 v, float &ux, float &uy) {
+    ux = mt_atan2f(v.x, -v.z) * kInvTwoPi;
+    uy = mt_acosf(fminf(1.0f, fmaxf(-1.0f, v.y))) * kInvPi;
+}
+
 // EnvironmentMap::evalEnvironment (envmap.cpp:380-410); hasDiff: camera
-// rays carrying (scaled) differentials -> EWA, otherwise bilinear level 0
-DEV float3 env_eval(const DevEnv &V, float3 dWorld, bool hasDiff, float3 rxD, float3 ryD) {
-    const float3 v = env_rot(V.E->to_local, dWorld);
-    const float ux = mt_atan2f(v.x, -v.z) * kInvTwoPi, uy = mt_acosf(fminf(1.0f, fmaxf(-1.0f, v.y))) * kInvPi;
+// rays carrying (scaled) differentials -> EWA, otherwise bilinear level 0.
+// env_eval_uv: v = the local direction and its env_uv already computed
+DEV float3 env_eval_uv(const DevEnv &V, float3 v, float ux, float uy, bool hasDiff, float3 rxD, float3 ryD) {
     float3 value;
     if (!hasDiff) {
         value = mip_bilinear(env_mip(V), 0, ux, uy);
@@ -52,6 +58,12 @@ DEV float3 env_eval(const DevEnv &V, float3 dWorld, bool hasDiff, float3 rxD, fl
                              t2 * dvdy.y);
     }
     return value * V.E->scale;
+}
+DEV float3 env_eval(const DevEnv &V, float3 dWorld, bool hasDiff, float3 rxD, float3 ryD) {
+    const float3 v = env_rot(V.E->to_local, dWorld);
+    float ux, uy;
+    env_uv(v, ux, uy);
+    return env_eval_uv(V, v, ux, uy, hasDiff, rxD, ryD);
 }
 
 DEV float env_lum(float3 c) { return c.x * 0.212671f + c.y * 0.715160f + c.z * 0.072169f; }
@@ -119,11 +131,10 @@ DEV void env_internal_sample(const DevEnv &V, float sx, float sy, float3 &d, flo
     pdf /= fmaxf(fabsf(sinTheta), kEpsilon);
 }
 
-// internalPdfDirection (envmap.cpp:603-633), local direction
-DEV float env_internal_pdf(const DevEnv &V, float3 d) {
+// internalPdfDirection (envmap.cpp:603-633), local direction d and its env_uv
+DEV float env_internal_pdf_uv(const DevEnv &V, float3 d, float ux, float uy) {
     const int W = V.E->mip.level_w[0], H = V.E->mip.level_h[0];
     const DevMip M = env_mip(V);
-    const float ux = mt_atan2f(d.x, -d.z) * kInvTwoPi, uy = mt_acosf(fminf(1.0f, fmaxf(-1.0f, d.y))) * kInvPi;
     if (!isfinite(ux) || !isfinite(uy)) return 0.0f;
     const float u = ux * W - 0.5f, v = uy * H - 0.5f;
     const int xPos = (int)floorf(u), yPos = (int)floorf(v);
@@ -134,6 +145,11 @@ DEV float env_internal_pdf(const DevEnv &V, float3 d) {
     return (env_lum(value1) * V.rowWeights[min(max(yPos, 0), H - 1)] +
             env_lum(value2) * V.rowWeights[min(max(yPos + 1, 0), H - 1)]) *
            V.E->normalization / fmaxf(fabsf(sinTheta), kEpsilon);
+}
+DEV float env_internal_pdf(const DevEnv &V, float3 d) {
+    float ux, uy;
+    env_uv(d, ux, uy);
+    return env_internal_pdf_uv(V, d, ux, uy);
 }
 
 // BSphere::rayIntersect + solveQuadratic (bsphere.h:88-95, util.cpp:447-485)

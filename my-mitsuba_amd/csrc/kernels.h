@@ -2603,13 +2603,18 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
         if (!valid) {
             // environment hit by the BSDF sample (path.cpp:236-246, 257-265)
             if (ENV && !(I.hide_emitters && !(flags & F_SCATTERED))) {
-                const float3 value = env_eval(S.env, rd, false, rd, rd);
+                // evalEnvironment and pdfDirect look the same local
+                // direction up (envmap.cpp:386-387, 606-607): its atan2f /
+                // acosf are evaluated once for both
+                const float3 v = env_rot(S.env.E->to_local, rd);
+                float ux, uy;
+                env_uv(v, ux, uy);
+                const float3 value = env_eval_uv(S.env, v, ux, uy, false, rd, rd);
                 float nearT, farT;
                 if (env_sphere(S.env, ro, rd, nearT, farT) && !(nearT > 0) && !(farT < 0)) {
                     float lumPdf = 0.0f;
                     if (!(flags & F_DELTA))   // Scene::pdfEmitterDirect -> EnvironmentMap::pdfDirect
-                        lumPdf = env_internal_pdf(S.env, env_rot(S.env.E->to_local, rd)) *
-                                 tb.emitters[S.env.E->emitter].pdf_discrete;
+                        lumPdf = env_internal_pdf_uv(S.env, v, ux, uy) * tb.emitters[S.env.E->emitter].pdf_discrete;
                     L += T * value * mis(ldS(&P.aux[i]).w, lumPdf);
                 }
             }
