@@ -536,6 +536,7 @@ struct SpecRay {
     uint32_t mb;         // mailbox state of exact ties (mailbox_step)
     uint32_t bestKey;    // TriAccel index of the best hit (mailbox key)
     uint32_t rpend;      // MTSG_RECT_PEND: the rectangle tested in the lane's next iteration
+    uint2 rroot;         // MTSG_PUSHDOWN: the node a kd-restart starts from
 };
 // bits: top slot of the circular short stack (0-2), entries held (3-5),
 // entries dropped since the last restart (6), kd-restarts of the ray at this
@@ -689,6 +690,7 @@ DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float r
     r.tmin = r.mint;
     r.tmax = r.best;
     r.cur = S.root2;
+    r.rroot = S.root2;
     r.lfE = r.lfEnd = 0;
     r.lfTmax = -1.0f;
     r.bits = dneg << SB_DNEG | (shadow ? SB_SHADOW : 0u);
@@ -718,8 +720,23 @@ DEV void spec_plan(const SpecRay &r, uint2 n, float &tsplit, bool &goLeft, bool 
     goLeft = belowFirst != goSecond;
 }
 
+// Push-down (Horn et al. 2007, "Interactive k-d tree GPU raytracing"): while
+// nothing is held on the stack and nothing was dropped, a descent step that enters
+// one child only leaves the ray's whole remaining segment inside that child,
+// so a later kd-restart can start there instead of at the root.  It takes the
+// same one-sided steps the root restart would (its interval [t0, best] lies
+// inside the one the step was decided on), so the leaves and their order do
+// not change; only the re-descent is shorter.
+#ifndef MTSG_PUSHDOWN
+#define MTSG_PUSHDOWN 1
+#endif
 DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push, SpecStack stk, uint32_t cap) {
     const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
+#if MTSG_PUSHDOWN
+    // (nothing held and nothing dropped: after drops the segment beyond the
+    // popped subtrees still belongs to the restart, which keeps its node)
+    if (!push && !(r.bits & (SB_N | SB_DROPPED))) r.rroot = c;
+#endif
     if (push) {
         // circular short stack: a push onto a full stack drops the oldest entry
         const uint2 other = goLeft ? make_uint2(pr.z, pr.w) : make_uint2(pr.x, pr.y);
@@ -912,7 +929,11 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         } else {
             // empty: done, or a kd-restart behind this leaf if entries were dropped
             if (COUNT && (b & SB_DROPPED)) cnt.restarts++;
+#if MTSG_PUSHDOWN
+            kd_restart(L, r, b, r.rroot, c);
+#else
             kd_restart(L, r, b, S.root2, c);
+#endif
         }
     }
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;

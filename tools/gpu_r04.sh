@@ -29,6 +29,9 @@ for w in ${*:-tests bench}; do
     c5quick*) step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
     c2quick) step c2quick 300 python bench.py --steps 5 --warmup 2 --workload cbox --no-cpu --no-parity --no-count ;;
     inst) step inst 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity ;;
+    e8var-*) v=${w#e8var-}; v=${v%@*}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity --no-count ;;
+    e8fin-*) v=${w#e8fin-}; v=${v%@*}; step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity --no-count --finish-paths $v ;;
+    e8quick*) step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity --no-count ;;
     e8) step e8 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity ;;
     ranks)
       # the launcher path (as the driver runs it) and the self-launching path,
