@@ -728,7 +728,7 @@ DEV void spec_plan(const SpecRay &r, uint2 n, float &tsplit, bool &goLeft, bool 
 // inside the one the step was decided on), so the leaves and their order do
 // not change; only the re-descent is shorter.
 #ifndef MTSG_PUSHDOWN
-#define MTSG_PUSHDOWN 1
+#define MTSG_PUSHDOWN 0   // measured r04: C3 trace +1.6%, C5 +2.5% (2 more VGPRs and a compare per step for 0.08 restarts per ray)
 #endif
 DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool push, SpecStack stk, uint32_t cap) {
     const uint2 c = goLeft ? make_uint2(pr.x, pr.y) : make_uint2(pr.z, pr.w);
