@@ -3291,7 +3291,10 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
 // ---------------------------------------------------------------------------
 constexpr int MAX_BORDER = 4;
 constexpr int LT = TILE + 2 * MAX_BORDER;   // LDS tile edge
-constexpr int SPLAT_CHUNK = 16;             // samples per pixel per workgroup
+#ifndef MTSG_SPLAT_CHUNK
+#define MTSG_SPLAT_CHUNK 16
+#endif
+constexpr int SPLAT_CHUNK = MTSG_SPLAT_CHUNK;   // samples per pixel per workgroup
 
 // One workgroup = one 16x16 tile x one chunk of SPLAT_CHUNK samples per pixel.
 // Each thread owns one pixel: all its samples fall in [x, x+1) x [y, y+1), so
