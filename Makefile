@@ -23,7 +23,7 @@ ORACLE      := oracle/liboracle.so
 ORACLE_FAST := oracle/liboracle_fast.so
 
 .PHONY: all host device oracle clean
-all: host device oracle $(PATH_LIB) $(CLI) scenes/sky512.pfm tools/math_probe tools/math_bench tools/check_glibc_mathf
+all: host device oracle $(PATH_LIB) $(CLI) scenes/sky512.pfm tools/math_probe tools/math_bench tools/check_glibc_mathf tools/check_env_guide
 host: $(HOST_LIB)
 device: $(DEV_LIB)
 oracle: $(ORACLE) $(ORACLE_FAST)
@@ -85,6 +85,10 @@ tools/math_bench: tools/math_bench.hip $(PKG)/csrc/glibc_mathf.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -Wno-unused-result -o $@ $<
 tools/check_glibc_mathf: tools/check_glibc_mathf.cpp $(PKG)/csrc/glibc_mathf.h
 	$(HIPCC) -O2 -mfma -std=c++17 -ffp-contract=off -o $@ $< -lpthread
+
+# the device's guided envmap CDF searches against std::lower_bound, on the host
+tools/check_env_guide: tools/check_env_guide.cpp $(PKG)/csrc/envmap.h $(HOST_LIB)
+	$(HIPCC) -O2 -std=c++17 -ffp-contract=off -Iinclude -o $@ $< -L$(PKG) -lmtsg_host -Wl,-rpath,'$$ORIGIN/../$(PKG)'
 
 # synthetic HDR environment for the envmap scenes (tools/gen_envmap.py)
 scenes/sky512.pfm: tools/gen_envmap.py

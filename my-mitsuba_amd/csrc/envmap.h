@@ -69,7 +69,7 @@ DEV float3 env_eval(const DevEnv &V, float3 dWorld, bool hasDiff, float3 rxD, fl
 DEV float env_lum(float3 c) { return c.x * 0.212671f + c.y * 0.715160f + c.z * 0.072169f; }
 
 // std::lower_bound-based sampleReuse (envmap.cpp:628-633)
-DEV uint32_t env_sample_reuse(const float *cdf, uint32_t size, float &sample) {
+__host__ __device__ inline uint32_t env_sample_reuse(const float *cdf, uint32_t size, float &sample) {   // (host: tools/check_env_guide)
     uint32_t lo = 0, len = size + 1;
     while (len > 0) {
         const uint32_t half = len >> 1;
@@ -82,7 +82,7 @@ DEV uint32_t env_sample_reuse(const float *cdf, uint32_t size, float &sample) {
 }
 
 // the same over [guide[g], guide[g + 1]] (the sample is in [0, 1): g = floor(sample * ENV_GUIDE) is exact)
-DEV uint32_t env_sample_reuse_guided(const float *cdf, uint32_t size, const uint32_t *guide, float &sample) {
+__host__ __device__ inline uint32_t env_sample_reuse_guided(const float *cdf, uint32_t size, const uint32_t *guide, float &sample) {
     const uint32_t g = min((uint32_t)(sample * (float)ENV_GUIDE), ENV_GUIDE - 1u);
     uint32_t lo = guide[g];
     const uint32_t hi = min(guide[g + 1], size);
