@@ -13,7 +13,7 @@ import pytest
 from conftest import REPO, SCENES
 
 
-@pytest.mark.parametrize("scene", ["env_glass.xml", "cbox_textured.xml"])
+@pytest.mark.parametrize("scene", ["env_glass.xml"])
 def test_guided_cdf_search_equals_lower_bound(scene):
     r = subprocess.run([os.path.join(REPO, "tools", "check_env_guide"), os.path.join(SCENES, scene), "500"],
                        capture_output=True, text=True, timeout=300)
