@@ -3292,7 +3292,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
 constexpr int MAX_BORDER = 4;
 constexpr int LT = TILE + 2 * MAX_BORDER;   // LDS tile edge
 #ifndef MTSG_SPLAT_CHUNK
-#define MTSG_SPLAT_CHUNK 16
+#define MTSG_SPLAT_CHUNK 64   // r04: 16 -> 64 samples per workgroup, a quarter of the film atomics: C3 splat 2.86 -> 2.34 ms
 #endif
 constexpr int SPLAT_CHUNK = MTSG_SPLAT_CHUNK;   // samples per pixel per workgroup
 

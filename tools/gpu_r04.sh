@@ -27,6 +27,7 @@ for w in ${*:-tests bench}; do
     inst-quick*) step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity --no-count ;;
     instvar-*) v=${w#instvar-}; v=${v%@*}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity --no-count ;;
     c5bp-*) v=${w#c5bp-}; v=${v%@*}; step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count --batch-paths $v ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     refit-time) step refit-time 300 python -u -m pytest -m gpu -s -q tests/test_gpu_kdbuild.py -k "refit or c3_device" ;;
     c5quick*) step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
     c2quick) step c2quick 300 python bench.py --steps 5 --warmup 2 --workload cbox --no-cpu --no-parity --no-count ;;
