@@ -204,12 +204,9 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t
     else if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     // closest rays that met an exact tie: traced again with the mailbox
-    // (two-level: the exact Havran).  Ties are rare (C3: ~100 per frame), so
-    // the grid is one workgroup per CU, striding over them: a launch that
-    // finds none costs ~5 us instead of the ~35 us of a quarter trace grid
-    // (7 launches per frame: 1% of a 1/8 share's time, r04)
+    // (a grid a quarter of the trace grid's; two-level: the exact Havran)
     if (MTSG_MAILBOX && cIn != -2) {
-        const dim3 tg(std::max<unsigned>(1u, (unsigned)s->cuCount));
+        const dim3 tg(std::max<unsigned>(1u, (unsigned)s->traceGrid / 4u));
         if (s->ds.inst) hipLaunchKernelGGL(k_tie_i, tg, blk, 0, st, s->ds, P);
         else if (s->knobs) hipLaunchKernelGGL((k_tie<true>), tg, blk, 0, st, s->ds, P);
         else hipLaunchKernelGGL((k_tie<false>), tg, blk, 0, st, s->ds, P);
