@@ -58,6 +58,119 @@ typedef struct mtsh_scene_overrides {
 mtsh_scene *mtsh_scene_load_overrides(const char *path, const char *const *defines, int n_defines,
                                       const mtsh_scene_overrides *overrides);
 
+/* ---- building the scene Mitsuba holds in memory --------------------------
+ *
+ * The XML route above re-reads a scene file.  A Mitsuba-side plugin already
+ * holds the parsed scene, with every `-D` substituted (mitsuba.cpp:168-174,
+ * scenehandler.cpp:211): each object's plugin name and the Properties it was
+ * created from (ConfigurableObject::getProperties, cobject.h:77;
+ * Properties::getPluginName / getPropertyNames / getType, properties.h:49-229)
+ * and each TriMesh's arrays (trimesh.h:127-153).  The builder turns exactly
+ * that into the device scene: objects are added in Mitsuba's order (the order
+ * fixes the descriptor's arrays), then mtsh_scene_finish builds the kd-tree,
+ * the emitter CDFs and the environment tables as mtsh_scene_load does --
+ * mtsh_scene_load is itself a client of the same constructors.
+ *
+ * Ids returned by the add calls are >= 0; -1 signals an error (message in
+ * mtsh_last_error; the builder stays usable).  String properties naming
+ * files resolve against base_dir unless absolute. */
+typedef struct mtsh_builder mtsh_builder;
+
+/* One entry of a Properties object (properties.h:49-70 EPropertyType, RGB
+ * mode), plus references to objects created earlier in this builder. */
+enum {
+    MTSH_PROP_BOOLEAN = 0,   /* i                                        */
+    MTSH_PROP_INTEGER,       /* i                                        */
+    MTSH_PROP_FLOAT,         /* f                                        */
+    MTSH_PROP_POINT,         /* v[0..2]                                  */
+    MTSH_PROP_VECTOR,        /* v[0..2]                                  */
+    MTSH_PROP_TRANSFORM,     /* m (row-major 4x4), inv (its inverse; all */
+                             /* zero: computed in double, as Transform(m)) */
+    MTSH_PROP_SPECTRUM,      /* v[0..2]: the RGB Spectrum                */
+    MTSH_PROP_STRING,        /* s                                        */
+    MTSH_PROP_TEXTURE        /* i: a texture id (a BSDF's textured       */
+                             /* parameter: a nested <texture> child)     */
+};
+typedef struct mtsh_prop {
+    const char *name;
+    int32_t type;            /* MTSH_PROP_*                              */
+    int32_t pad;
+    int64_t i;
+    float f;
+    float v[3];
+    float m[16], inv[16];
+    const char *s;
+} mtsh_prop;
+
+/* A TriMesh as Mitsuba holds it after TriMesh::configure (trimesh.cpp:362-386):
+ * positions and (unless face_normals) vertex normals in world space, the
+ * winding already flipped for flipped face normals.  Optional inputs make the
+ * builder do configure's work instead: to_world (16 floats row-major, NULL =
+ * identity; normals use its inverse transpose) is applied to positions and
+ * normals, and NULL normals are
+ * computed (TriMesh::computeNormals, trimesh.cpp:608-681), negated when
+ * flip_normals is set. */
+typedef struct mtsh_mesh {
+    const char *name;
+    uint32_t n_vertices, n_triangles;
+    const float *positions;      /* 3 * n_vertices                       */
+    const float *normals;        /* 3 * n_vertices or NULL               */
+    const float *texcoords;      /* 2 * n_vertices or NULL               */
+    const uint32_t *indices;     /* 3 * n_triangles                      */
+    int32_t face_normals, flip_normals;
+    const float *to_world;       /* NULL or 16 floats                    */
+    const float *to_world_inv;   /* its inverse as Mitsuba's Transform   */
+                                 /* holds it, or NULL: computed          */
+} mtsh_mesh;
+
+/* Start a scene (the instancing mode of mtsh_set_instancing applies). */
+mtsh_builder *mtsh_scene_begin(const char *base_dir);
+/* `bitmap` texture (bitmap.cpp:179-302) -> texture id. */
+int32_t mtsh_scene_add_texture(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props);
+/* BSDF plugin (diffuse, roughconductor, conductor, dielectric,
+ * roughdielectric, plastic, roughplastic, twosided) -> BSDF id.  nested:
+ * twosided's one or two BSDF ids (twosided.cpp:52-80), else none. */
+int32_t mtsh_scene_add_bsdf(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props,
+                            const int32_t *nested, int32_t n_nested);
+/* Emitter: `area` (area.cpp:67-78; attach it to one shape) or `envmap`
+ * (envmap.cpp:105-185; the scene's environment) -> emitter id. */
+int32_t mtsh_scene_add_emitter(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props);
+/* Shape group (shapegroup.cpp) -> group id for the shape calls' `group`. */
+int32_t mtsh_scene_add_group(mtsh_builder *b, const char *id);
+/* Shape from its plugin and Properties (ply, obj, serialized, cube,
+ * rectangle): bsdf -1 = the default BSDF (shape.cpp:47-70), emitter -1 =
+ * none, group -1 = the scene.  Returns 0 or -1. */
+int32_t mtsh_scene_add_shape(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props,
+                             int32_t bsdf, int32_t emitter, int32_t group);
+/* Triangle mesh from its arrays (see mtsh_mesh).  Returns 0 or -1. */
+int32_t mtsh_scene_add_mesh(mtsh_builder *b, const mtsh_mesh *mesh, int32_t bsdf, int32_t emitter, int32_t group);
+/* Instance of a shape group (instance.cpp:57-130); props: its `toWorld`. */
+int32_t mtsh_scene_add_instance(mtsh_builder *b, int32_t group, const mtsh_prop *props, int32_t n_props);
+/* The sensor and what it holds (sensor.cpp:150-262, hdrfilm.cpp:209-220,
+ * rfilter.cpp, independent.cpp / halton.cpp / ...), the integrator
+ * (integrator.cpp:199-234; myPath2_OM.cpp:61-85).  Return 0 or -1. */
+int32_t mtsh_scene_set_sensor(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props);
+int32_t mtsh_scene_set_film(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props,
+                            const char *rfilter, const mtsh_prop *rfilter_props, int32_t n_rfilter_props);
+int32_t mtsh_scene_set_sampler(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props);
+int32_t mtsh_scene_set_integrator(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props);
+/* Finalise (kd-tree, CDFs, environment tables; overrides may be NULL) and
+ * free the builder.  Returns the scene, or NULL (see mtsh_last_error). */
+mtsh_scene *mtsh_scene_finish(mtsh_builder *b, const mtsh_scene_overrides *overrides);
+/* Drop an unfinished builder. */
+void mtsh_scene_abort(mtsh_builder *b);
+
+/* Fingerprint of a scene's device descriptor: one entry per array of
+ * mtsg_scene_desc and one ("scalars") for its other fields, FNV-1a 64 of
+ * the bytes, so two routes to a scene can be compared byte for byte.
+ * Returns the entry count; out (may be NULL) receives up to capacity. */
+typedef struct mtsh_digest_entry {
+    char name[32];
+    uint64_t bytes;
+    uint64_t hash;
+} mtsh_digest_entry;
+int32_t mtsh_scene_digest(const mtsh_scene *scene, mtsh_digest_entry *out, int32_t capacity);
+
 /* Override kd-tree build parameters before loading (0 = default). */
 void mtsh_set_kd_threads(int threads);
 

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "../../include/mtsh.h"
+#include "digest.h"
 #include "scene.h"
 
 struct mtsh_scene {
@@ -53,6 +54,205 @@ mtsh_scene *mtsh_scene_load_overrides(const char *path, const char *const *defin
 }
 
 const mtsg_scene_desc *mtsh_scene_desc(const mtsh_scene *s) { return &s->scene->desc; }
+
+}  // extern "C"
+
+// ---- builder (the scene Mitsuba holds in memory) ----
+struct mtsh_builder {
+    std::unique_ptr<mtsh::Scene> scene;
+    std::unique_ptr<mtsh::SceneBuilder> b;
+};
+
+namespace {
+// mtsh_prop list -> Properties (and a BSDF's textured parameters)
+mtsh::Properties toProps(const mtsh_prop *p, int32_t n, std::map<std::string, int> *textures = nullptr) {
+    if (n < 0 || (n > 0 && !p)) throw std::runtime_error("invalid property list");
+    mtsh::Properties props;
+    for (int32_t k = 0; k < n; ++k) {
+        if (!p[k].name) throw std::runtime_error("a property without a name");
+        const std::string name = p[k].name;
+        if (props.has(name) || (textures && textures->count(name)))
+            throw std::runtime_error("Property \"" + name + "\" was specified multiple times!");
+        switch (p[k].type) {
+            case MTSH_PROP_BOOLEAN: props.bools[name] = p[k].i != 0; break;
+            case MTSH_PROP_INTEGER: props.ints[name] = (long long)p[k].i; break;
+            case MTSH_PROP_FLOAT: props.floats[name] = p[k].f; break;
+            case MTSH_PROP_POINT:
+            case MTSH_PROP_VECTOR: props.points[name] = mtsh::V3(p[k].v[0], p[k].v[1], p[k].v[2]); break;
+            case MTSH_PROP_SPECTRUM: props.spectra[name] = mtsh::V3(p[k].v[0], p[k].v[1], p[k].v[2]); break;
+            case MTSH_PROP_STRING:
+                if (!p[k].s) throw std::runtime_error("string property \"" + name + "\" without a value");
+                props.strings[name] = p[k].s;
+                break;
+            case MTSH_PROP_TRANSFORM: {
+                bool haveInv = false;
+                for (int j = 0; j < 16; ++j) haveInv |= p[k].inv[j] != 0.0f;
+                mtsh::Transform t;
+                if (haveInv) {
+                    // as Mitsuba holds it: the matrix and its inverse
+                    for (int j = 0; j < 16; ++j) { t.m[j / 4][j % 4] = p[k].m[j]; t.inv[j / 4][j % 4] = p[k].inv[j]; }
+                } else {
+                    float a[4][4];
+                    for (int j = 0; j < 16; ++j) a[j / 4][j % 4] = p[k].m[j];
+                    t = mtsh::Transform::fromMatrixF(a);
+                }
+                props.transforms[name] = t;
+                break;
+            }
+            case MTSH_PROP_TEXTURE:
+                if (!textures) throw std::runtime_error("texture property \"" + name + "\" outside a BSDF");
+                (*textures)[name] = (int)p[k].i;
+                break;
+            default: throw std::runtime_error("property \"" + name + "\" has an unknown type");
+        }
+    }
+    return props;
+}
+template <class F> int32_t guarded(mtsh_builder *b, F &&f) {
+    if (!b) { g_err = "invalid builder"; return -1; }
+    try {
+        return f();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+}  // namespace
+
+extern "C" {
+
+mtsh_builder *mtsh_scene_begin(const char *base_dir) {
+    try {
+        auto b = std::make_unique<mtsh_builder>();
+        b->scene = mtsh::SceneBuilder::newScene();
+        b->b = std::make_unique<mtsh::SceneBuilder>(*b->scene);
+        b->b->dirStack.push_back(base_dir && *base_dir ? base_dir : ".");
+        return b.release();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+int32_t mtsh_scene_add_texture(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n) {
+    return guarded(b, [&] { return (int32_t)b->b->texture(plugin ? plugin : "", toProps(props, n), ""); });
+}
+
+int32_t mtsh_scene_add_bsdf(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n, const int32_t *nested,
+                            int32_t n_nested) {
+    return guarded(b, [&] {
+        std::map<std::string, int> tex;
+        mtsh::Properties pr = toProps(props, n, &tex);
+        if (n_nested < 0 || (n_nested > 0 && !nested)) throw std::runtime_error("invalid nested BSDF list");
+        std::vector<int> kids(nested, nested + n_nested);
+        return (int32_t)b->b->bsdf(plugin ? plugin : "", pr, tex, kids, "");
+    });
+}
+
+int32_t mtsh_scene_add_emitter(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n) {
+    return guarded(b, [&] { return (int32_t)b->b->emitter(plugin ? plugin : "", toProps(props, n)); });
+}
+
+int32_t mtsh_scene_add_group(mtsh_builder *b, const char *id) {
+    return guarded(b, [&] { return (int32_t)b->b->group(id ? id : ""); });
+}
+
+int32_t mtsh_scene_add_shape(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n, int32_t bsdf,
+                             int32_t emitter, int32_t group) {
+    return guarded(b, [&] {
+        b->b->shape(plugin ? plugin : "", toProps(props, n), bsdf, emitter, group);
+        return 0;
+    });
+}
+
+int32_t mtsh_scene_add_mesh(mtsh_builder *b, const mtsh_mesh *mesh, int32_t bsdf, int32_t emitter, int32_t group) {
+    return guarded(b, [&] {
+        if (!mesh || !mesh->positions || !mesh->indices || !mesh->n_vertices || !mesh->n_triangles)
+            throw std::runtime_error("mtsh_scene_add_mesh: a mesh needs positions and triangles");
+        mtsh::Mesh m;
+        m.name = mesh->name ? mesh->name : "";
+        const size_t nv = mesh->n_vertices, nt = mesh->n_triangles;
+        m.p.resize(nv);
+        for (size_t i = 0; i < nv; ++i) m.p[i] = mtsh::V3(mesh->positions[3 * i], mesh->positions[3 * i + 1], mesh->positions[3 * i + 2]);
+        if (mesh->normals && !mesh->face_normals) {
+            m.n.resize(nv);
+            for (size_t i = 0; i < nv; ++i) m.n[i] = mtsh::V3(mesh->normals[3 * i], mesh->normals[3 * i + 1], mesh->normals[3 * i + 2]);
+        }
+        if (mesh->texcoords) m.uv.assign(mesh->texcoords, mesh->texcoords + 2 * nv);
+        m.idx.assign(mesh->indices, mesh->indices + 3 * nt);
+        m.faceNormals = mesh->face_normals != 0;
+        mtsh::Transform tw;
+        if (mesh->to_world && mesh->to_world_inv) {
+            for (int j = 0; j < 16; ++j) { tw.m[j / 4][j % 4] = mesh->to_world[j]; tw.inv[j / 4][j % 4] = mesh->to_world_inv[j]; }
+        } else if (mesh->to_world) {
+            float a[4][4];
+            for (int j = 0; j < 16; ++j) a[j / 4][j % 4] = mesh->to_world[j];
+            tw = mtsh::Transform::fromMatrixF(a);
+        }
+        b->b->mesh(std::move(m), mesh->to_world ? &tw : nullptr, mesh->flip_normals != 0, bsdf, emitter, group);
+        return 0;
+    });
+}
+
+int32_t mtsh_scene_add_instance(mtsh_builder *b, int32_t group, const mtsh_prop *props, int32_t n) {
+    return guarded(b, [&] {
+        b->b->instance(group, toProps(props, n).getTransform("toWorld", mtsh::Transform()));
+        return 0;
+    });
+}
+
+int32_t mtsh_scene_set_sensor(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n) {
+    return guarded(b, [&] {
+        b->b->sensor(plugin ? plugin : "", toProps(props, n));
+        return 0;
+    });
+}
+
+int32_t mtsh_scene_set_film(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n, const char *rfilter,
+                            const mtsh_prop *rprops, int32_t nr) {
+    return guarded(b, [&] {
+        b->b->film(plugin ? plugin : "", toProps(props, n));
+        if (rfilter) b->b->rfilter(rfilter, toProps(rprops, nr));
+        return 0;
+    });
+}
+
+int32_t mtsh_scene_set_sampler(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n) {
+    return guarded(b, [&] {
+        b->b->sampler(plugin ? plugin : "", toProps(props, n));
+        return 0;
+    });
+}
+
+int32_t mtsh_scene_set_integrator(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n) {
+    return guarded(b, [&] {
+        b->b->integrator(plugin ? plugin : "", toProps(props, n));
+        return 0;
+    });
+}
+
+mtsh_scene *mtsh_scene_finish(mtsh_builder *b, const mtsh_scene_overrides *overrides) {
+    if (!b) { g_err = "invalid builder"; return nullptr; }
+    std::unique_ptr<mtsh_builder> own(b);
+    try {
+        own->b->finish(overrides);
+        auto s = std::make_unique<mtsh_scene>();
+        s->scene = std::move(own->scene);
+        return s.release();
+    } catch (const std::exception &e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+void mtsh_scene_abort(mtsh_builder *b) { delete b; }
+
+int32_t mtsh_scene_digest(const mtsh_scene *s, mtsh_digest_entry *out, int32_t capacity) {
+    if (!s) { g_err = "invalid scene"; return -1; }
+    const auto d = mtsh::sceneDigest(s->scene->desc);
+    for (int32_t i = 0; out && i < (int32_t)d.size() && i < capacity; ++i) out[i] = d[i];
+    return (int32_t)d.size();
+}
 
 void mtsh_scene_render_params(const mtsh_scene *s, mtsg_render_params *p) {
     memset(p, 0, sizeof(*p));

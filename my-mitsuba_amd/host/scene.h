@@ -5,6 +5,7 @@
 #pragma once
 #include <map>
 #include <memory>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -244,6 +245,59 @@ bool readPFM(const std::string &path, int &w, int &h, std::vector<float> &rgb, s
 // OpenEXR scanline image (Bitmap::readOpenEXR, bitmap.cpp:2780; exr.cpp):
 // RGB float, rows top-down
 bool readEXR(const std::string &path, int &w, int &h, std::vector<float> &rgb, std::string &err);
+
+// A `shapegroup` being filled (src/shapes/shapegroup.cpp): flattening keeps
+// its shapes in object space until an instance places a copy; the two-level
+// mode sends them straight to Scene::meshes under Scene::groups[index]
+struct ShapeGroup {
+    std::string id;
+    std::vector<Mesh> meshes;
+    std::vector<Rect> rects;
+    int index = -1;
+};
+
+// Plugin construction from Properties (builder.cpp), shared by the XML
+// loader and the in-memory builder C-ABI (mtsh_scene_begin / _add_* /
+// _finish).  Objects are created in the caller's order, which fixes the
+// order of the descriptor's arrays; ids are indices into the scene's
+// bsdfs / emitters / textures, and into this builder's shape groups.
+// `line` (> 0) prefixes error messages with an XML line number.
+class SceneBuilder {
+public:
+    explicit SceneBuilder(Scene &s);
+    static std::unique_ptr<Scene> newScene();   // instancing mode, kd build parameters
+    std::vector<std::string> dirStack;          // relative file names resolve against these, innermost last
+    std::string resolve(const std::string &f) const;
+
+    int texture(const std::string &type, const Properties &props, const std::string &id, int line = 0);
+    // textures: BSDF parameter name -> texture id; nested: twosided's BSDFs
+    int bsdf(const std::string &type, const Properties &props, const std::map<std::string, int> &textures,
+             const std::vector<int> &nested, const std::string &id, int line = 0);
+    int emitter(const std::string &type, const Properties &props, int line = 0);   // area (for a shape) or envmap
+    // shapes: bsdf / emitter -1 = none; group -1 = the scene
+    void shape(const std::string &type, const Properties &props, int bsdf, int emitter, int group, int line = 0);
+    void mesh(Mesh &&m, const Transform *toWorld, bool flipNormals, int bsdf, int emitter, int group);
+    int group(const std::string &id);
+    void instance(int group, const Transform &toWorld);
+    void integrator(const std::string &type, const Properties &props, int line = 0);
+    void sensor(const std::string &type, const Properties &props, int line = 0);
+    void film(const std::string &type, const Properties &props);
+    void rfilter(const std::string &type, const Properties &props);
+    void sampler(const std::string &type, const Properties &props);
+    void finish(const mtsh_scene_overrides *overrides);   // validation, overrides, Scene::finalize
+
+private:
+    Scene &scene;
+    std::vector<ShapeGroup> groups;
+    std::set<int> claimed;   // area emitters attached to a shape
+    V3 reflectance(const Properties &props, int tex, const V3 &constant, mtsg_bsdf &d, float &maxOut);
+    int defaultBsdf(bool emitter);
+    void checkEmitter(int emitter, bool inGroup, bool claim);
+    ShapeGroup &groupAt(int group);
+    void addRect(Rect r, int group);
+    void addMesh(Mesh &&m, int group);
+    static void buildCube(Mesh &m);
+};
 
 // XML loading (src/librender/scenehandler.cpp), `-D name=value` defines
 std::unique_ptr<Scene> loadScene(const std::string &path,

@@ -179,6 +179,29 @@ class SceneOverrides(C.Structure):
 
 MTSH_OVERRIDE_FILM_SIZE, MTSH_OVERRIDE_SAMPLE_COUNT, MTSH_OVERRIDE_INTEGRATOR, MTSH_OVERRIDE_FILM_CROP = 1, 2, 4, 8
 
+
+class Prop(C.Structure):
+    """mtsh_prop: one entry of a Mitsuba Properties object (include/mtsh.h)."""
+    _fields_ = [("name", C.c_char_p), ("type", C.c_int32), ("pad", C.c_int32), ("i", C.c_int64), ("f", C.c_float),
+                ("v", C.c_float * 3), ("m", C.c_float * 16), ("inv", C.c_float * 16), ("s", C.c_char_p)]
+
+
+class MeshArrays(C.Structure):
+    """mtsh_mesh: a TriMesh's arrays."""
+    _fields_ = [("name", C.c_char_p), ("n_vertices", C.c_uint32), ("n_triangles", C.c_uint32),
+                ("positions", C.c_void_p), ("normals", C.c_void_p), ("texcoords", C.c_void_p), ("indices", C.c_void_p),
+                ("face_normals", C.c_int32), ("flip_normals", C.c_int32), ("to_world", C.c_void_p),
+                ("to_world_inv", C.c_void_p)]
+
+
+class DigestEntry(C.Structure):
+    """mtsh_digest_entry."""
+    _fields_ = [("name", C.c_char * 32), ("bytes", C.c_uint64), ("hash", C.c_uint64)]
+
+
+PROP_TYPES = {"boolean": 0, "integer": 1, "float": 2, "point": 3, "vector": 4, "transform": 5, "spectrum": 6,
+              "string": 7, "texture": 8}
+
 _host = None
 _dev = None
 
@@ -197,6 +220,9 @@ HOST_SYMBOLS = [
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
     "mtsh_read_image", "mtsh_clip_triangle", "mtsh_texture_image", "mtsh_build_mipmap", "mtsh_scene_textures", "mtsh_scene_om", "mtsh_scene_prim_bounds", "mtsh_scene_set_kdtree",
     "mtsh_last_error",
+    "mtsh_scene_begin", "mtsh_scene_add_texture", "mtsh_scene_add_bsdf", "mtsh_scene_add_emitter", "mtsh_scene_add_group",
+    "mtsh_scene_add_shape", "mtsh_scene_add_mesh", "mtsh_scene_add_instance", "mtsh_scene_set_sensor", "mtsh_scene_set_film",
+    "mtsh_scene_set_sampler", "mtsh_scene_set_integrator", "mtsh_scene_finish", "mtsh_scene_abort", "mtsh_scene_digest",
 ]
 PATH_SYMBOLS = [
     "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
@@ -265,6 +291,30 @@ def host_lib() -> C.CDLL:
         lib.mtsh_build_mipmap.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
                                           C.POINTER(MipMapHeader), C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
                                           C.c_void_p, C.c_void_p]
+        PP = C.POINTER(Prop)
+        lib.mtsh_scene_begin.restype = C.c_void_p
+        lib.mtsh_scene_begin.argtypes = [C.c_char_p]
+        for fn in ("mtsh_scene_add_texture", "mtsh_scene_add_emitter", "mtsh_scene_set_sensor", "mtsh_scene_set_sampler",
+                   "mtsh_scene_set_integrator"):
+            getattr(lib, fn).restype = C.c_int32
+            getattr(lib, fn).argtypes = [C.c_void_p, C.c_char_p, PP, C.c_int32]
+        lib.mtsh_scene_add_bsdf.restype = C.c_int32
+        lib.mtsh_scene_add_bsdf.argtypes = [C.c_void_p, C.c_char_p, PP, C.c_int32, C.POINTER(C.c_int32), C.c_int32]
+        lib.mtsh_scene_add_group.restype = C.c_int32
+        lib.mtsh_scene_add_group.argtypes = [C.c_void_p, C.c_char_p]
+        lib.mtsh_scene_add_shape.restype = C.c_int32
+        lib.mtsh_scene_add_shape.argtypes = [C.c_void_p, C.c_char_p, PP, C.c_int32, C.c_int32, C.c_int32, C.c_int32]
+        lib.mtsh_scene_add_mesh.restype = C.c_int32
+        lib.mtsh_scene_add_mesh.argtypes = [C.c_void_p, C.POINTER(MeshArrays), C.c_int32, C.c_int32, C.c_int32]
+        lib.mtsh_scene_add_instance.restype = C.c_int32
+        lib.mtsh_scene_add_instance.argtypes = [C.c_void_p, C.c_int32, PP, C.c_int32]
+        lib.mtsh_scene_set_film.restype = C.c_int32
+        lib.mtsh_scene_set_film.argtypes = [C.c_void_p, C.c_char_p, PP, C.c_int32, C.c_char_p, PP, C.c_int32]
+        lib.mtsh_scene_finish.restype = C.c_void_p
+        lib.mtsh_scene_finish.argtypes = [C.c_void_p, C.POINTER(SceneOverrides)]
+        lib.mtsh_scene_abort.argtypes = [C.c_void_p]
+        lib.mtsh_scene_digest.restype = C.c_int32
+        lib.mtsh_scene_digest.argtypes = [C.c_void_p, C.POINTER(DigestEntry), C.c_int32]
         _host = lib
     return _host
 
@@ -364,6 +414,26 @@ class Scene:
         self.info = SceneInfo()
         lib.mtsh_scene_get_info(self._h, C.byref(self.info))
 
+    @classmethod
+    def _adopt(cls, handle, label: str, instancing: str) -> "Scene":
+        """A scene made by SceneBuilder.finish (it takes the handle over)."""
+        self = cls.__new__(cls)
+        self._h = handle
+        self.path = label
+        self.defines = {}
+        self.instancing = instancing
+        self.info = SceneInfo()
+        host_lib().mtsh_scene_get_info(self._h, C.byref(self.info))
+        return self
+
+    def digest(self) -> dict:
+        """mtsh_scene_digest: {descriptor array: (bytes, FNV-1a 64)}."""
+        lib = host_lib()
+        n = lib.mtsh_scene_digest(self._h, None, 0)
+        arr = (DigestEntry * n)()
+        lib.mtsh_scene_digest(self._h, arr, n)
+        return {e.name.decode(): (int(e.bytes), int(e.hash)) for e in arr}
+
     @property
     def desc(self) -> C.c_void_p:
         return C.c_void_p(host_lib().mtsh_scene_desc(self._h))
@@ -421,6 +491,135 @@ class Scene:
         if getattr(self, "_h", None):
             host_lib().mtsh_scene_free(self._h)
             self._h = None
+
+
+def _props(props) -> tuple:
+    """[(name, kind, value)] -> (Prop array, keep-alive list).  kind is a
+    Properties type ("boolean", "integer", "float", "point", "vector",
+    "spectrum", "string", "transform": (m 4x4[, inverse 4x4]), "texture": an
+    id of SceneBuilder.texture)."""
+    props = list(props or [])
+    arr = (Prop * max(1, len(props)))()
+    keep = []
+    for k, (name, kind, value) in enumerate(props):
+        p = arr[k]
+        nb = name.encode()
+        keep.append(nb)
+        p.name = nb
+        p.type = PROP_TYPES[kind]
+        if kind in ("boolean", "integer", "texture"):
+            p.i = int(value)
+        elif kind == "float":
+            p.f = float(value)
+        elif kind in ("point", "vector", "spectrum"):
+            v = np.broadcast_to(np.asarray(value, np.float32), (3,))
+            p.v[:] = [float(x) for x in v]
+        elif kind == "string":
+            sb = str(value).encode()
+            keep.append(sb)
+            p.s = sb
+        elif kind == "transform":
+            m, inv = value if isinstance(value, tuple) else (value, None)
+            p.m[:] = [float(x) for x in np.asarray(m, np.float32).reshape(16)]
+            if inv is not None:
+                p.inv[:] = [float(x) for x in np.asarray(inv, np.float32).reshape(16)]
+        else:
+            raise ValueError(f"unknown property kind {kind!r}")
+    return arr, len(props), keep
+
+
+class SceneBuilder:
+    """The in-memory scene builder (mtsh_scene_begin / _add_* / _finish):
+    what a Mitsuba-side plugin hands over from the objects it holds."""
+
+    def __init__(self, base_dir: str = ".", instancing: str = "flatten", kd_threads: int = 0):
+        lib = host_lib()
+        lib.mtsh_set_kd_threads(kd_threads)
+        lib.mtsh_set_instancing(MTSH_INSTANCING_TWO_LEVEL if instancing == "two-level" else MTSH_INSTANCING_FLATTEN)
+        self.instancing = instancing
+        self._b = lib.mtsh_scene_begin(base_dir.encode())
+        if not self._b:
+            raise RuntimeError(_err(lib, "mtsh_last_error"))
+
+    def _rc(self, rc: int, what: str) -> int:
+        if rc < 0:
+            raise RuntimeError(f"{what}: " + _err(host_lib(), "mtsh_last_error"))
+        return rc
+
+    def texture(self, plugin: str, props) -> int:
+        a, n, _k = _props(props)
+        return self._rc(host_lib().mtsh_scene_add_texture(self._b, plugin.encode(), a, n), plugin)
+
+    def bsdf(self, plugin: str, props, nested=()) -> int:
+        a, n, _k = _props(props)
+        kids = (C.c_int32 * max(1, len(nested)))(*nested)
+        return self._rc(host_lib().mtsh_scene_add_bsdf(self._b, plugin.encode(), a, n, kids, len(nested)), plugin)
+
+    def emitter(self, plugin: str, props) -> int:
+        a, n, _k = _props(props)
+        return self._rc(host_lib().mtsh_scene_add_emitter(self._b, plugin.encode(), a, n), plugin)
+
+    def group(self, gid: str) -> int:
+        return self._rc(host_lib().mtsh_scene_add_group(self._b, gid.encode()), "shapegroup")
+
+    def shape(self, plugin: str, props, bsdf: int = -1, emitter: int = -1, group: int = -1) -> None:
+        a, n, _k = _props(props)
+        self._rc(host_lib().mtsh_scene_add_shape(self._b, plugin.encode(), a, n, bsdf, emitter, group), plugin)
+
+    def mesh(self, positions, indices, normals=None, texcoords=None, to_world=None, to_world_inv=None,
+             face_normals: bool = False, flip_normals: bool = False, bsdf: int = -1, emitter: int = -1, group: int = -1,
+             name: str = "") -> None:
+        pos = np.ascontiguousarray(positions, np.float32).reshape(-1, 3)
+        idx = np.ascontiguousarray(indices, np.uint32).reshape(-1, 3)
+        keep = [pos, idx]
+        m = MeshArrays()
+        nb = name.encode()
+        m.name = nb
+        m.n_vertices, m.n_triangles = pos.shape[0], idx.shape[0]
+        m.positions, m.indices = _ptr(pos), _ptr(idx)
+        for field, arr, width in (("normals", normals, 3), ("texcoords", texcoords, 2), ("to_world", to_world, 16),
+                                  ("to_world_inv", to_world_inv, 16)):
+            if arr is not None:
+                a = np.ascontiguousarray(arr, np.float32).reshape(-1)
+                keep.append(a)
+                setattr(m, field, _ptr(a))
+        m.face_normals, m.flip_normals = int(face_normals), int(flip_normals)
+        self._rc(host_lib().mtsh_scene_add_mesh(self._b, C.byref(m), bsdf, emitter, group), "mesh " + name)
+
+    def instance(self, group: int, props) -> None:
+        a, n, _k = _props(props)
+        self._rc(host_lib().mtsh_scene_add_instance(self._b, group, a, n), "instance")
+
+    def sensor(self, plugin: str, props) -> None:
+        a, n, _k = _props(props)
+        self._rc(host_lib().mtsh_scene_set_sensor(self._b, plugin.encode(), a, n), plugin)
+
+    def film(self, plugin: str, props, rfilter: str | None = None, rfilter_props=None) -> None:
+        a, n, _k = _props(props)
+        ra, rn, _rk = _props(rfilter_props)
+        self._rc(host_lib().mtsh_scene_set_film(self._b, plugin.encode(), a, n, rfilter.encode() if rfilter else None,
+                                                 ra, rn), plugin)
+
+    def sampler(self, plugin: str, props) -> None:
+        a, n, _k = _props(props)
+        self._rc(host_lib().mtsh_scene_set_sampler(self._b, plugin.encode(), a, n), plugin)
+
+    def integrator(self, plugin: str, props) -> None:
+        a, n, _k = _props(props)
+        self._rc(host_lib().mtsh_scene_set_integrator(self._b, plugin.encode(), a, n), plugin)
+
+    def finish(self, overrides: SceneOverrides | None = None, label: str = "<builder>") -> Scene:
+        lib = host_lib()
+        b, self._b = self._b, None
+        h = lib.mtsh_scene_finish(b, C.byref(overrides) if overrides is not None else None)
+        if not h:
+            raise RuntimeError("scene build failed: " + _err(lib, "mtsh_last_error"))
+        return Scene._adopt(h, label, self.instancing)
+
+    def __del__(self):
+        if getattr(self, "_b", None):
+            host_lib().mtsh_scene_abort(self._b)
+            self._b = None
 
 
 def tile_deal_keys(tile_w: int, tile_h: int) -> np.ndarray:
