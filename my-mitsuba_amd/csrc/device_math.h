@@ -30,6 +30,10 @@ DEV float mt_expf(float x) { return gmf::expf(x); }
 DEV float mt_atan2f(float y, float x) { return gmf::atan2f(y, x); }
 DEV float mt_atanf(float x) { return gmf::atanf(x); }
 DEV float mt_acosf(float x) { return gmf::acosf(x); }
+// powf: phong (microfacet.h:219,371-373), Beckmann's visible-normal sampling
+// (microfacet.h:604, Mitsuba's default roughconductor) and roughplastic's
+// rough-transmittance lookup (rtrans.h)
+DEV float mt_powf(float x, float y) { return gmf::powf(x, y); }
 #else
 DEV void mt_sincosf(float x, float *s, float *c) { sincosf(x, s, c); }
 DEV float mt_tanf(float x) { return tanf(x); }
@@ -38,9 +42,8 @@ DEV float mt_expf(float x) { return expf(x); }
 DEV float mt_atan2f(float y, float x) { return atan2f(y, x); }
 DEV float mt_atanf(float x) { return atanf(x); }
 DEV float mt_acosf(float x) { return acosf(x); }
-#endif
-// powf (phong, Beckmann's visible sampling, roughplastic's rtrans lookup): ROCm's
 DEV float mt_powf(float x, float y) { return powf(x, y); }
+#endif
 // math::fastexp / math::fastlog (math.h:185-199)
 DEV float mt_fastexp(float x) { return (float)exp((double)x); }
 DEV float mt_fastlog(float x) { return (float)log((double)x); }

@@ -14,14 +14,15 @@
 //                          polynomials, Szabolcs Nagy / Arm optimized-routines)
 //   expf                   e_expf.c, e_exp2f_data.c
 //   logf                   e_logf.c, e_logf_data.c
+//   powf                   e_powf.c, e_powf_log2_data.c (log2 / exp2 in double)
 //   atanf, atan2f, acosf   s_atanf.c, e_atan2f.c, e_acosf.c (fdlibm's float
 //                          versions)
 //   tanf                   s_tanf.c (the sincosf range reductions) and k_tanf.c
 //                          (fdlibm's float kernel)
-// On x86-64 glibc selects an FMA build of sinf / cosf / sincosf / expf / logf
+// On x86-64 glibc selects an FMA build of sinf / cosf / sincosf / expf / logf / powf
 // at run time when the CPU has FMA (sysdeps/x86_64/fpu/multiarch, the *-fma
 // variants: the same C compiled with -mfma, so a*b+c is contracted); both
-// the container's Xeon and the GPU box's EPYC do, so those five use fma()
+// the container's Xeon and the GPU box's EPYC do, so those six use fma()
 // exactly where that build contracts.  atanf, atan2f, acosf and tanf are not
 // multiarch: no contraction (the device library is built with
 // -ffp-contract=off).  Data tables are the published values; the
@@ -34,10 +35,11 @@
 #include <stdint.h>
 
 // GMF_CALLS: entry points compiled as out-of-line calls instead of inlined
-// (bit mask: 1 sincosf, 2 tanf, 4 atanf / atan2f, 8 acosf, 16 expf / logf);
+// (bit mask: 1 sincosf, 2 tanf, 4 atanf / atan2f, 8 acosf, 16 expf / logf,
+// 32 powf);
 // a call keeps a long function's registers out of its caller's allocation
 #ifndef GMF_CALLS
-#define GMF_CALLS 13   // measured r04 (C3 / C5 Msamples/s): 0: 1500 / 1378, 13: 1515 / 1427, 31: 1506 / 1430, 14: 1484 / 1370
+#define GMF_CALLS 45   // (13 | 32: powf out of line) measured r04 (C3 / C5 Msamples/s): 0: 1500 / 1378, 13: 1515 / 1427, 31: 1506 / 1430, 14: 1484 / 1370
 #endif
 #define GMF __host__ __device__ __forceinline__
 #define GMF_CALL __host__ __device__ inline __attribute__((noinline))
@@ -65,6 +67,11 @@
 #define GMF_ENTRY_EXPLOG GMF_CALL
 #else
 #define GMF_ENTRY_EXPLOG GMF
+#endif
+#if GMF_CALLS & 32
+#define GMF_ENTRY_POW GMF_CALL
+#else
+#define GMF_ENTRY_POW GMF
 #endif
 // the large-argument reductions are rare: kept out of line, so they do not
 // add to the register pressure of the shading kernels that call sinf / tanf
@@ -488,6 +495,115 @@ GMF_ENTRY_TAN float tanf(float x) {
     float y0, y1;
     const int n = rem_pio2f(x, y0, y1);
     return kernel_tanf(y0, y1, 1 - ((n & 1) << 1));
+}
+
+// ---- powf (e_powf.c, e_powf_log2_data.c, POWF_LOG2_TABLE_BITS 4) ----------
+// The FMA build (sysdeps/x86_64/fpu/multiarch e_powf-fma.c) contracts every
+// a * b + c of log2_inline and exp2_inline; y * log2(x) is not fused (it is
+// also compared against the overflow bounds).  log2 table: {1/c, log2(c)} of
+// the 16 subintervals (the same 1/c as logf's; log2(c) = -log2(1/c) rounded,
+// checked by the host test), poly: log2(1 + r) of degree 5.
+constexpr double kPowfLogc[16] = {-0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2, -0x1.01d9bf3f2b631p-2, -0x1.97c1d1b3b7afp-3, -0x1.2f9e393af3c9fp-3, -0x1.960cbbf788d5cp-4, -0x1.a6f9db6475fcep-5, 0x0p+0, 0x1.338ca9f24f53dp-4, 0x1.476a9543891bap-3, 0x1.e840b4ac4e4d2p-3, 0x1.40645f0c6651cp-2, 0x1.88e9c2c1b9ff8p-2, 0x1.ce0a44eb17bccp-2};
+
+// 0: not an integer, 1: odd, 2: even (iy: a non-zero finite float's bits)
+GMF int powf_checkint(uint32_t iy) {
+    const int e = (int)(iy >> 23 & 0xff);
+    if (e < 0x7f) return 0;
+    if (e > 0x7f + 23) return 2;
+    if (iy & ((1u << (0x7f + 23 - e)) - 1)) return 0;
+    if (iy & (1u << (0x7f + 23 - e))) return 1;
+    return 2;
+}
+GMF bool powf_zeroinfnan(uint32_t ix) { return 2 * ix - 1 >= 2u * 0x7f800000u - 1; }
+GMF bool powf_issignaling(float x) { return 2 * (asuint(x) ^ 0x00400000u) > 2u * 0x7fc00000u; }
+
+GMF double powf_log2(uint32_t ix) {
+    constexpr uint32_t OFF = 0x3f330000u;
+    constexpr double A0 = 0x1.27616c9496e0bp-2, A1 = -0x1.71969a075c67ap-2, A2 = 0x1.ec70a6ca7baddp-2,
+                     A3 = -0x1.7154748bef6c8p-1, A4 = 0x1.71547652ab82bp0;
+    const uint32_t tmp = ix - OFF;
+    const uint32_t i = (tmp >> (23 - 4)) % 16;
+    const uint32_t top = tmp & 0xff800000u;
+    const uint32_t iz = ix - top;
+    const int k = (int32_t)top >> 23;
+    const double invc = kLogfInvc[i], logc = kPowfLogc[i];
+    const double z = (double)asfloat(iz);
+    const double r = fma(z, invc, -1.0);
+    const double y0 = logc + (double)k;
+    const double r2 = r * r;
+    double y = fma(A0, r, A1);
+    const double p = fma(A2, r, A3);
+    const double r4 = r2 * r2;
+    double q = fma(A4, r, y0);
+    q = fma(p, r2, q);
+    y = fma(y, r4, q);
+    return y;
+}
+
+GMF float powf_exp2(double xd, uint32_t signBias) {
+    // xd is log2 unscaled (POWF_SCALE_BITS 0 without toint intrinsics): the
+    // shift rounds it to multiples of 1/32 and r is in [-1/64, 1/64], so the
+    // unscaled __exp2f_data.poly applies
+    constexpr double Shift = 0x1.8p+52 / 32;
+    constexpr double C0 = 0x1.c6af84b912394p-5, C1 = 0x1.ebfce50fac4f3p-3, C2 = 0x1.62e42ff0c52d6p-1;
+    double kd = xd + Shift;
+    const uint64_t ki = asuint64(kd);
+    kd -= Shift;
+    const double r = xd - kd;
+    uint64_t t = kExp2fTab[ki % 32];
+    const uint64_t ski = ki + signBias;
+    t += ski << (52 - 5);
+    const double s = asdouble(t);
+    const double z = fma(C0, r, C1);
+    const double r2 = r * r;
+    double y = fma(C2, r, 1.0);
+    y = fma(z, r2, y);
+    y = y * s;
+    return (float)y;
+}
+
+GMF_ENTRY_POW float powf(float x, float y) {
+    constexpr uint32_t SIGN_BIAS = 1u << (5 + 11);
+    uint32_t signBias = 0;
+    uint32_t ix = asuint(x);
+    const uint32_t iy = asuint(y);
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u || powf_zeroinfnan(iy)) {
+        // x < 0x1p-126, inf or nan, or y 0, inf or nan
+        if (powf_zeroinfnan(iy)) {
+            if (2 * iy == 0) return powf_issignaling(x) ? x + y : 1.0f;
+            if (ix == 0x3f800000u) return powf_issignaling(y) ? x + y : 1.0f;
+            if (2 * ix > 2u * 0x7f800000u || 2 * iy > 2u * 0x7f800000u) return x + y;
+            if (2 * ix == 2 * 0x3f800000u) return 1.0f;
+            if ((2 * ix < 2 * 0x3f800000u) == !(iy & 0x80000000u)) return 0.0f;   // |x|<1 && y==inf or |x|>1 && y==-inf
+            return y * y;
+        }
+        if (powf_zeroinfnan(ix)) {
+            float x2 = x * x;
+            if ((ix & 0x80000000u) && powf_checkint(iy) == 1) x2 = -x2;
+            return (iy & 0x80000000u) ? 1.0f / x2 : x2;
+        }
+        // x and y are non-zero finite
+        if (ix & 0x80000000u) {
+            const int yint = powf_checkint(iy);
+            if (yint == 0) return (x - x) / (x - x);   // __math_invalidf
+            if (yint == 1) signBias = SIGN_BIAS;
+            ix &= 0x7fffffffu;
+        }
+        if (ix < 0x00800000u) {
+            // normalise a subnormal x so that its exponent becomes negative
+            ix = asuint(x * 0x1p23f);
+            ix &= 0x7fffffffu;
+            ix -= 23u << 23;
+        }
+    }
+    const double logx = powf_log2(ix);
+    const double ylogx = (double)y * logx;   // y is 0 if logx is 0
+    if ((asuint64(ylogx) >> 47 & 0xffff) >= asuint64(126.0) >> 47) {
+        // |y * log(x)| >= 126
+        if (ylogx > 0x1.fffffffd1d571p+6) return signBias ? -0x1p97f * 0x1p97f : 0x1p97f * 0x1p97f;   // __math_oflowf
+        if (ylogx <= -150.0) return signBias ? -0x1p-95f * 0x1p-95f : 0x1p-95f * 0x1p-95f;         // __math_uflowf
+    }
+    return powf_exp2(ylogx, signBias);
 }
 
 }  // namespace gmf

@@ -2672,7 +2672,7 @@ int oracle_render(const mtsg_scene_desc *d, const mtsg_render_params *p, int rng
             }
         }
         Sfmt parent;
-        parent.initGenRand(5489ULL);
+        parent.initGenRand(5489ULL + p->seed);   // seed 0: Mitsuba's default (random.cpp:486); others: independent streams for the tests
         std::vector<Sfmt> clones(T);
         for (int t = 0; t < T; ++t) clones[t].seedFrom(parent);   // renderjob.cpp:57-69
 

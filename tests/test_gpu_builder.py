@@ -21,13 +21,13 @@ def per_pixel(a, b):
     return np.abs(mtsg.develop(a) - mtsg.develop(b)).mean(axis=-1)
 
 
-# the share of pixels above a per-pixel L1 of 1e-3 allowed: none on the
-# bunnies; on the glass scene a long specular chain can still leave the
-# oracle's path by an ulp, 0.5% as test_gpu_configs' crop test
+# the share of pixels above a per-pixel L1 of 1e-3 allowed: none (glibc's
+# float algorithms on the device keep even the glass scene's long specular
+# chains on the oracle's paths)
 @pytest.mark.parametrize("xml,defines,instancing,tail", [
     ("bunny15.xml", {"width": 96, "height": 54, "spp": 8}, "flatten", 0.0),
     ("bunny15.xml", {"width": 96, "height": 54, "spp": 8}, "two-level", 0.0),
-    ("env_glass.xml", {"width": 96, "height": 54, "spp": 8, "maxDepth": 16}, "flatten", 0.005),
+    ("env_glass.xml", {"width": 96, "height": 54, "spp": 8, "maxDepth": 16}, "flatten", 0.0),
 ])
 def test_builder_scene_renders_at_oracle_parity(xml, defines, instancing, tail):
     scene = W.build(os.path.join(SCENES, xml), defines, instancing=instancing, meshes="world")

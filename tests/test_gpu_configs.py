@@ -45,21 +45,27 @@ def run_config(name, defs, expect):
     return dist
 
 
+# Per-pixel bars at about twice what the current build measures (round 5,
+# profiles/r05_gpu_tests.log.txt): the samples follow the oracle's paths, and
+# what remains is the order of the splat's float sums (a few 1e-6).
 def test_c1_cornell_box_at_its_size():
-    run_config("cbox.xml", {}, (256, 256, 16, -1))
+    dist = run_config("cbox.xml", {}, (256, 256, 16, -1))
+    assert dist["frac_over_1e-3"] == 0 and dist["max"] < 3e-5, dist      # measured max 1.2e-5
 
 
 def test_c2_full_frame_parity():
-    run_config("cbox.xml", {"width": 1280, "height": 720, "spp": 2, "maxDepth": 8}, (1280, 720, 2, 8))
+    dist = run_config("cbox.xml", {"width": 1280, "height": 720, "spp": 2, "maxDepth": 8}, (1280, 720, 2, 8))
+    assert dist["frac_over_1e-3"] == 0 and dist["max"] < 1e-5, dist      # measured max 4.9e-6
 
 
 def test_c5_full_frame_parity():
     dist = run_config("env_glass.xml", {"width": 1920, "height": 1080, "spp": 1, "maxDepth": 64},
                       (1920, 1080, 1, 64))
-    # long specular chains may diverge through ulp-level differences of the
-    # device transcendentals (DESIGN §5 "FMA and path chaos"): a few pixels,
-    # not a systematic difference
-    assert dist["frac_over_1e-3"] < 0.01, dist
+    # long specular chains diverged through ulp-level differences of the
+    # device transcendentals until round 4 (DESIGN §5 "FMA and path chaos",
+    # 5.1% of the pixels above 1e-3 at 1024 spp in round 3); with glibc's
+    # float algorithms on the device no pixel leaves the oracle's paths
+    assert dist["frac_over_1e-3"] == 0 and dist["max"] < 1.5e-5, dist    # measured max 6.4e-6
 
 
 def test_c5_per_pixel_tail_on_a_crop():
@@ -68,8 +74,8 @@ def test_c5_per_pixel_tail_on_a_crop():
     1-spp full frame above).  A sample whose long specular chain leaves the
     oracle's path through an ulp carries another environment texel, bright
     beside a 1/16 share; with glibc's float algorithms on the device
-    (glibc_mathf.h) that must stay rare: at most 0.5% of the pixels above
-    1e-3 (round 3, ROCm's float library, at 1024 spp: 5.1%)."""
+    (glibc_mathf.h) none does: no pixel above 1e-3 and a per-pixel maximum
+    of a few 1e-6 (round 3, ROCm's float library, at 1024 spp: 5.1% above)."""
     scene = mtsg.Scene(os.path.join(SCENES, "env_glass.xml"), {"width": 1920, "height": 1080, "spp": 16, "maxDepth": 64})
     p = scene.params(tile_x=720, tile_y=405, tile_w=480, tile_h=270)
     b = scene.border
@@ -82,4 +88,4 @@ def test_c5_per_pixel_tail_on_a_crop():
     l1, mean = check_render(img_c, img_g)
     dist = l1_distribution(img_c, img_g, b)
     print(f"C5 crop 480x270x16spp: per-pixel L1 {l1:.3e}, mean {mean:.4f}, {dist}")
-    assert dist["frac_over_1e-3"] <= 0.005, dist
+    assert dist["frac_over_1e-3"] == 0 and dist["max"] < 1e-5, dist      # measured max 3.7e-6

@@ -4,7 +4,8 @@
 //   gmf::*  my-mitsuba_amd/csrc/glibc_mathf.h, glibc 2.35's algorithms (what the
 //           path integrator calls, device_math.h mt_*)
 //   ocml    ROCm's float library (sinf, expf, ...), for comparison
-// atan2f takes y = the argument and x from a hash of it.  DESIGN §5.
+// atan2f takes y = the argument and x from a hash of it; powf takes |x| and
+// an exponent in [-8, 8) from another hash (and 0.25, roughplastic's).  DESIGN §5.
 // Build: make tools/math_probe   Run: tools/math_probe [stride]  (default 3)
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -16,13 +17,19 @@
 
 #include "../my-mitsuba_amd/csrc/glibc_mathf.h"
 
-enum { NF = 8 };
-static const char *kName[NF] = {"sinf", "cosf", "tanf", "expf", "logf", "atanf", "acosf", "atan2f"};
+enum { NF = 10 };
+static const char *kName[NF] = {"sinf", "cosf", "tanf", "expf", "logf", "atanf", "acosf", "atan2f", "powf", "powf.25"};
 
 __host__ __device__ inline float arg_y(uint32_t u) {
     uint32_t h = u * 0x9E3779B9u;
     h ^= h >> 16;
     return gmf::asfloat((h & 0x807fffffu) | (((h >> 7) % 254u + 1u) << 23));   // a finite float from u
+}
+// powf's exponent: uniform in [-8, 8) from a hash of u
+__host__ __device__ inline float arg_p(uint32_t u) {
+    uint32_t h = (u ^ 0x5bd1e995u) * 0x85EBCA6Bu;
+    h ^= h >> 13;
+    return -8.0f + 16.0f * (float)(h >> 8) * 0x1p-24f;
 }
 
 __global__ void k_probe(uint64_t start, uint64_t stride, uint32_t n, float *outG, float *outO) {
@@ -30,9 +37,11 @@ __global__ void k_probe(uint64_t start, uint64_t stride, uint32_t n, float *outG
     if (i >= n) return;
     const uint32_t u = (uint32_t)(start + (uint64_t)i * stride);
     const float x = gmf::asfloat(u), y = arg_y(u);
+    const float p = arg_p(u), ax = fabsf(x);
     const float g[NF] = {gmf::sinf(x), gmf::cosf(x), gmf::tanf(x), gmf::expf(x), gmf::logf(x), gmf::atanf(x),
-                         gmf::acosf(x), gmf::atan2f(x, y)};
-    const float o[NF] = {sinf(x), cosf(x), tanf(x), expf(x), logf(x), atanf(x), acosf(x), atan2f(x, y)};
+                         gmf::acosf(x), gmf::atan2f(x, y), gmf::powf(ax, p), gmf::powf(ax, 0.25f)};
+    const float o[NF] = {sinf(x), cosf(x), tanf(x), expf(x), logf(x), atanf(x), acosf(x), atan2f(x, y), powf(ax, p),
+                         powf(ax, 0.25f)};
     for (int k = 0; k < NF; ++k) {
         outG[(size_t)k * n + i] = g[k];
         outO[(size_t)k * n + i] = o[k];
@@ -68,8 +77,9 @@ int main(int argc, char **argv) {
                 for (uint32_t i = t; i < n; i += nth) {
                     const uint32_t u = (uint32_t)(start + (uint64_t)i * stride);
                     const float x = gmf::asfloat(u), y = arg_y(u);
+                    const float p = arg_p(u), ax = fabsf(x);
                     const float ref[NF] = {::sinf(x), ::cosf(x), ::tanf(x), ::expf(x), ::logf(x), ::atanf(x), ::acosf(x),
-                                           ::atan2f(x, y)};
+                                           ::atan2f(x, y), ::powf(ax, p), ::powf(ax, 0.25f)};
                     for (int k = 0; k < NF; ++k) {
                         if (!same(G[(size_t)k * n + i], ref[k])) {
                             if (bG[t * NF + k]++ == 0) fG[t * NF + k] = u;
