@@ -43,11 +43,27 @@ def trace_kernel(a):
     return "k_trace_s<false, 16, true, false>" if a.instancing == "two-level" else "k_trace_s<false, 16, false, false>"
 
 
+def device_build_id():
+    """The device library this run loads (MTSG_LIB or the in-tree
+    libmtsg.so): the first 16 hex digits of its SHA-256."""
+    import hashlib
+    alt = os.environ.get("MTSG_LIB")
+    path = os.path.join(REPO, alt) if alt else os.path.join(REPO, "my-mitsuba_amd", "libmtsg.so")
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def pmc_key(a, world=1):
     """The configuration a committed PMC set must have been collected on for
-    this run to quote it (tools/gpu_pmc_config.sh, tools/pmc_kernels.py)."""
+    this run to quote it (tools/gpu_pmc_config.sh, tools/pmc_kernels.py):
+    the workload, its size and share, the batch and tail-kernel settings and
+    the device library's build -- counters of another build or batch size
+    describe other launches and are never quoted."""
     return {"workload": a.workload, "instancing": a.instancing, "kd_build": a.kd_build, "width": a.width,
-            "height": a.height, "spp": a.spp, "share": max(world, a.emulate_ranks, 1)}
+            "height": a.height, "spp": a.spp, "share": max(world, a.emulate_ranks, 1),
+            "batch_paths": a.batch_paths or 0, "finish_paths": a.finish_paths, "build": device_build_id()}
 
 
 def pmc_lookup(key, directory=None):
@@ -397,6 +413,12 @@ def main():
     gpu = mtsg.GPUScene(scene, dev)
     if a.batch_paths:
         gpu.set_batch_paths(a.batch_paths)
+    elif devices and devices["shared"]:
+        # ranks sharing a GPU size their batches from free-memory snapshots
+        # that can coincide: cap each rank at its share of the default batch
+        # (2^29 paths, 148 GB) so that together they fit the 288 GB HBM
+        sharing = devices["pci"].count(devices["pci"][rank])
+        gpu.set_batch_paths(max(1 << 20, (1 << 29) // sharing))
     if a.finish_paths >= 0:
         gpu.set_finish_paths(a.finish_paths)
     W, H = params.tile_w + 2 * border, params.tile_h + 2 * border

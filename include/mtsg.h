@@ -562,7 +562,11 @@ void mtsg_cancel_clear(mtsg_scene *scene);
  * RenderQueue::signalWorkEnd and the progress reporter
  * (BlockedRenderProcess::processResult, renderproc.cpp:144-154,179): a
  * batch's tiles complete together (the whole frame is one batch unless
- * mtsg_set_batch_paths makes them smaller).  fn = NULL removes it. */
+ * mtsg_set_batch_paths makes them smaller).  When fn runs the tile's samples
+ * are in the device-side ImageBlock; mtsg_render copies the block into its
+ * host buffer (and the path job sums the GPUs' blocks) only after the last
+ * batch, so a listener uses the call for progress, not to read pixels.
+ * fn = NULL removes it. */
 typedef void (*mtsg_tile_fn)(void *user, int32_t key, int32_t x, int32_t y, int32_t w, int32_t h);
 int  mtsg_set_tile_callback(mtsg_scene *scene, mtsg_tile_fn fn, void *user);
 
@@ -592,6 +596,21 @@ int  mtsg_set_batch_paths(mtsg_scene *scene, uint32_t paths);
  * MTSG_DEFAULT_FINISH_PATHS (environment override MTSG_FINISH).            */
 #define MTSG_DEFAULT_FINISH_PATHS 524288u
 int  mtsg_set_finish_paths(mtsg_scene *scene, uint32_t paths);
+
+/* TEST ONLY: the traversal's limits, to exercise the kd-restart guard
+ * (tests/test_gpu_edge_rays.py; kernels.h kd_restart).  stack_cap > 0
+ * shrinks every short stack to that many entries; restart_guard >= 0 is the
+ * restart number from which a restart starts one ulp beyond its distance
+ * (default 8; a large value turns the guard off, which can change results);
+ * restart_limit >= 0 is the restart number that ends a ray with
+ * MTSG_ERR_TRAVERSAL (default 511), applied to shadow rays only when
+ * limit_shadow_only.  Any change selects separate kernel instantiations;
+ * NULL restores the defaults.  Production renders never call this: no
+ * environment variable or other setting changes these limits. */
+typedef struct mtsg_test_knobs {
+    int32_t stack_cap, restart_guard, restart_limit, limit_shadow_only;
+} mtsg_test_knobs;
+int  mtsg_set_test_knobs(mtsg_scene *scene, const mtsg_test_knobs *knobs);
 
 /* Debug/parity entry points over SoA rays (host buffers).  Semantics of
  * ShapeKDTree::rayIntersect (src/librender/skdtree.cpp:112-142) including

@@ -39,7 +39,8 @@
 // 32 powf);
 // a call keeps a long function's registers out of its caller's allocation
 #ifndef GMF_CALLS
-#define GMF_CALLS 45   // (13 | 32: powf out of line) measured r04 (C3 / C5 Msamples/s): 0: 1500 / 1378, 13: 1515 / 1427, 31: 1506 / 1430, 14: 1484 / 1370
+#define GMF_CALLS 13   // measured r04 (C3 / C5 Msamples/s): 0: 1500 / 1378, 13: 1515 / 1427, 31: 1506 / 1430, 14: 1484 / 1370;
+                       // r05: 45 (powf out of line too) C3 1509-1512 vs 1526 (13)
 #endif
 #define GMF __host__ __device__ __forceinline__
 #define GMF_CALL __host__ __device__ inline __attribute__((noinline))

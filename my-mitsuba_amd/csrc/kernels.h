@@ -85,6 +85,10 @@ struct DevScene {
     // beyond its exit distance; restart rstMax (rstMaxC for closest-hit
     // rays) ends the ray with SB_ERR
     uint32_t capFlat, capGrp, capTop, rstGuard, rstMax, rstMaxC;
+    // two-level exact-tie keys: key + (instance + 1) * instKeyStride, where
+    // the stride is the number of TriAccel keys when keys x (instances + 1)
+    // fit 32 bits (one key per (primitive, instance) pair, no collisions)
+    uint32_t instKeyStride;
 };
 
 struct DevCamera {
@@ -1222,8 +1226,9 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
 #if MTSG_MAILBOX
             // an exact tie is flagged (the ray is traced again by
             // tie_retrace_i); the key tells a primitive of one instance from
-            // the same primitive of another, and a retest from a tie
-            const uint32_t tkey = key ^ ((r.bits & SB_INST) ? (inst + 1u) * 0x9E3779B1u : 0u);
+            // the same primitive of another, and a retest from a tie: distinct
+            // for every (primitive, instance) pair (DevScene::instKeyStride)
+            const uint32_t tkey = key + ((r.bits & SB_INST) ? (inst + 1u) * S.instKeyStride : 0u);
             r.bits |= (h & (t == r.best) & (tkey != r.bestKey)) ? SB_TIE : 0u;
             if (h) r.bestKey = tkey;
 #endif

@@ -95,7 +95,7 @@ struct mtsg_scene {
     int traceMode = 0;            // 0: refill at 16 idle lanes (measured best), 1: at 32
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
-    bool knobs = false;   // traversal test overrides set (MTSG_STACK_CAP, MTSG_RESTART_*): KNOBS kernels, no tail mode
+    bool knobs = false;   // traversal test overrides set (mtsg_set_test_knobs): KNOBS kernels, no tail mode
     mtsg_stats stats{};
     std::vector<hipEvent_t> evPool;
     size_t evUsed = 0;
@@ -986,28 +986,21 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         if ((rc = up(in.data(), in.size(), &dinst))) return fail(rc);
         ds.inst = dinst;
     }
-    // traversal stacks and the kd-restart guard (kernels.h kd_restart); the
-    // MTSG_STACK_CAP / MTSG_RESTART_GUARD / MTSG_RESTART_LIMIT overrides exist
-    // to exercise the guard (tests/test_gpu_edge_rays.py)
+    // traversal stacks and the kd-restart guard (kernels.h kd_restart): the
+    // compile-time defaults; only mtsg_set_test_knobs (tests) changes them
     ds.capFlat = SHORT_STACK;
     ds.capGrp = INNER_STACK;
     ds.capTop = OUTER_STACK;
     ds.rstGuard = RST_GUARD;
     ds.rstMax = RST_MAX;
-    if (const char *c = getenv("MTSG_STACK_CAP")) {
-        const uint32_t cap = (uint32_t)std::max(1, atoi(c));
-        ds.capFlat = std::min(ds.capFlat, cap);
-        ds.capGrp = std::min(ds.capGrp, cap);
-        ds.capTop = std::min(ds.capTop, cap);
-    }
-    if (const char *g = getenv("MTSG_RESTART_GUARD")) ds.rstGuard = (uint32_t)std::max(0, atoi(g));
-    if (const char *g = getenv("MTSG_RESTART_LIMIT")) ds.rstMax = std::min<uint32_t>(RST_MAX, (uint32_t)std::max(0, atoi(g)));
-    // MTSG_RESTART_LIMIT_SHADOW_ONLY=1: the limit applies to shadow rays only
-    // (a test of the error word of the shadow launches)
-    const char *so = getenv("MTSG_RESTART_LIMIT_SHADOW_ONLY");
-    ds.rstMaxC = (so && atoi(so)) ? RST_MAX : ds.rstMax;
-    s->knobs = ds.capFlat != (uint32_t)SHORT_STACK || ds.capGrp != (uint32_t)INNER_STACK || ds.capTop != (uint32_t)OUTER_STACK ||
-               ds.rstGuard != RST_GUARD || ds.rstMax != RST_MAX || ds.rstMaxC != RST_MAX;
+    ds.rstMaxC = RST_MAX;
+    s->knobs = false;
+    // two-level tie keys (kernels.h spec_iter_i): the TriAccel key count as
+    // the per-instance stride, so keys of different (primitive, instance)
+    // pairs never coincide; scenes too large for 32-bit keys fall back to an
+    // odd multiplier (a bijection per instance; pairs across instances can
+    // then collide, which only hides a tie of two such primitives)
+    ds.instKeyStride = (uint64_t)d->n_prims * ((uint64_t)d->n_instances + 1) <= 0xFFFFFFFFull ? d->n_prims : 0x9E3779B1u;
     // environment emitter tables (envmap.h)
     ds.has_env = d->has_envmap ? 1 : 0;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
@@ -1204,6 +1197,32 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
 int mtsg_set_batch_paths(mtsg_scene *s, uint32_t paths) {
     if (!s || paths < TILE * TILE) { g_err = "batch must hold at least 256 paths"; return MTSG_ERR_INVALID; }
     s->requestedBatch = paths;
+    return MTSG_OK;
+}
+
+int mtsg_set_test_knobs(mtsg_scene *s, const mtsg_test_knobs *k) {
+    if (!s) return MTSG_ERR_INVALID;
+    DevScene &ds = s->ds;
+    ds.capFlat = SHORT_STACK;
+    ds.capGrp = INNER_STACK;
+    ds.capTop = OUTER_STACK;
+    ds.rstGuard = RST_GUARD;
+    ds.rstMax = RST_MAX;
+    if (k) {
+        if (k->stack_cap > 0) {
+            const uint32_t cap = (uint32_t)k->stack_cap;
+            ds.capFlat = std::min(ds.capFlat, cap);
+            ds.capGrp = std::min(ds.capGrp, cap);
+            ds.capTop = std::min(ds.capTop, cap);
+        }
+        if (k->restart_guard >= 0) ds.rstGuard = (uint32_t)k->restart_guard;
+        if (k->restart_limit >= 0) ds.rstMax = std::min<uint32_t>(RST_MAX, (uint32_t)k->restart_limit);
+    }
+    ds.rstMaxC = (k && k->limit_shadow_only) ? RST_MAX : ds.rstMax;
+    // any change selects the KNOBS kernel instantiations (the production
+    // kernels keep their compile-time constants) and turns the tail kernel off
+    s->knobs = ds.capFlat != (uint32_t)SHORT_STACK || ds.capGrp != (uint32_t)INNER_STACK || ds.capTop != (uint32_t)OUTER_STACK ||
+               ds.rstGuard != RST_GUARD || ds.rstMax != RST_MAX || ds.rstMaxC != RST_MAX;
     return MTSG_OK;
 }
 

@@ -47,6 +47,12 @@ class RenderParams(C.Structure):
         return p
 
 
+class TestKnobs(C.Structure):
+    """mtsg_test_knobs (TEST ONLY: the traversal's stack sizes and restart guard)."""
+    _fields_ = [("stack_cap", C.c_int32), ("restart_guard", C.c_int32), ("restart_limit", C.c_int32),
+                ("limit_shadow_only", C.c_int32)]
+
+
 class Stats(C.Structure):
     """mtsg_stats."""
     _fields_ = [
@@ -213,7 +219,7 @@ DEVICE_SYMBOLS = [
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
     "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_kd_build", "mtsg_kd_refit", "mtsg_kd_free",
     "mtsg_sampler_draws", "mtsg_debug_wavetimes", "mtsg_set_tile_callback",
-    "mtsg_debug_stragglers",
+    "mtsg_debug_stragglers", "mtsg_set_test_knobs",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_scene_load_overrides", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
@@ -363,6 +369,7 @@ def device_lib() -> C.CDLL:
                                            C.c_uint32, C.c_void_p, C.c_void_p]
         lib.mtsg_scene_destroy.argtypes = [C.c_void_p]
         lib.mtsg_set_tile_callback.argtypes = [C.c_void_p, TILE_FN, C.c_void_p]
+        lib.mtsg_set_test_knobs.argtypes = [C.c_void_p, C.POINTER(TestKnobs)]
         lib.mtsg_last_error.argtypes = [C.c_char_p, C.c_size_t]
         _dev = lib
     return _dev
@@ -754,6 +761,13 @@ class GPUScene:
 
     def set_batch_paths(self, n: int) -> None:
         self._check(device_lib().mtsg_set_batch_paths(self._h, n), "mtsg_set_batch_paths")
+
+    def set_test_knobs(self, stack_cap: int = 0, restart_guard: int = -1, restart_limit: int = -1,
+                       limit_shadow_only: bool = False) -> None:
+        """TEST ONLY (mtsg_set_test_knobs): shrink the traversal stacks / move
+        the kd-restart guard; the defaults restore the production limits."""
+        k = TestKnobs(stack_cap, restart_guard, restart_limit, int(limit_shadow_only))
+        self._check(device_lib().mtsg_set_test_knobs(self._h, C.byref(k)), "mtsg_set_test_knobs")
 
     def set_finish_paths(self, n: int) -> None:
         """Tail-mode threshold (paths; 0: off), see mtsg_set_finish_paths."""

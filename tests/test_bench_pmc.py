@@ -10,7 +10,7 @@ import bench
 
 def args(**kw):
     a = dict(workload="bunny15", instancing="flatten", kd_build="host", width=1280, height=720, spp=256,
-             emulate_ranks=0)
+             emulate_ranks=0, batch_paths=0, finish_paths=-1)
     a.update(kw)
     return argparse.Namespace(**a)
 
@@ -25,12 +25,16 @@ def test_lookup_matches_the_whole_key_only(tmp_path):
     two = bench.pmc_key(args(instancing="two-level"))
     dev = bench.pmc_key(args(kd_build="device"))
     share = bench.pmc_key(args(emulate_ranks=8))
-    assert len({json.dumps(k, sort_keys=True) for k in (flat, two, dev, share)}) == 4
+    batch = bench.pmc_key(args(batch_paths=1 << 28))     # other launches: other counters
+    finish = bench.pmc_key(args(finish_paths=0))
+    build = dict(flat, build="0123456789abcdef")          # counters of another libmtsg.so
+    assert flat["build"] == bench.device_build_id() and flat["build"]
+    assert len({json.dumps(k, sort_keys=True) for k in (flat, two, dev, share, batch, finish, build)}) == 7
     (tmp_path / "r03_pmc_c3.json").write_text(json.dumps({"key": flat, "kernels": {"k_trace_s<false, 16, false, false>": {}}}))
     (tmp_path / "r02_pmc_c3.json").write_text(json.dumps({"key": flat, "kernels": {"old": {}}}))
     j, src = bench.pmc_lookup(flat, str(tmp_path))
     assert src.endswith("r03_pmc_c3.json") and "k_trace_s<false, 16, false, false>" in j["kernels"]
-    for k in (two, dev, share):
+    for k in (two, dev, share, batch, finish, build):
         assert bench.pmc_lookup(k, str(tmp_path)) == (None, None)
 
 

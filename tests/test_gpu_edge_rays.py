@@ -138,8 +138,8 @@ def corner_rays(scene, n, seed):
 
 
 @pytest.mark.parametrize("name", ["cbox", "bunny15", "bunny15-two-level"])
-def test_restart_guard_terminates_and_matches(name, monkeypatch):
-    """Every traversal stack cut to one entry (MTSG_STACK_CAP=1): far children
+def test_restart_guard_terminates_and_matches(name):
+    """Every traversal stack cut to one entry (mtsg_set_test_knobs): far children
     are dropped at almost every second push, rays kd-restart many times, and
     rays through split-plane corners return to the same restart distance.
     Without the guard such rays live-lock (they reach the restart limit:
@@ -158,17 +158,12 @@ def test_restart_guard_terminates_and_matches(name, monkeypatch):
     g = mtsg.GPUScene(s, 0)
     ref, ref_sh = g.trace_closest(rays), g.trace_shadow(sh)
     g.close()
-    monkeypatch.setenv("MTSG_STACK_CAP", "1")
-    monkeypatch.setenv("MTSG_RESTART_GUARD", "100000")   # guard off
     g = mtsg.GPUScene(s, 0)
     try:
+        g.set_test_knobs(stack_cap=1, restart_guard=100000)   # guard off
         with pytest.raises(RuntimeError, match=r"\(-6\).*restart limit"):
             g.trace_closest(rays)
-    finally:
-        g.close()
-    monkeypatch.delenv("MTSG_RESTART_GUARD")
-    g = mtsg.GPUScene(s, 0)
-    try:
+        g.set_test_knobs(stack_cap=1)
         got, got_sh = g.trace_closest(rays), g.trace_shadow(sh)
     finally:
         g.close()
@@ -186,42 +181,37 @@ def test_restart_guard_terminates_and_matches(name, monkeypatch):
     np.testing.assert_array_equal(got_sh, ref_sh)
 
 
-def test_restart_limit_fails_the_query(monkeypatch):
+def test_restart_limit_fails_the_query():
     """A ray that reaches the restart limit ends with an error the caller
     sees (MTSG_ERR_TRAVERSAL), from the debug queries and from the render,
     instead of the kernel spinning: limit 0 makes the first restart fail."""
     s = mtsg.Scene(os.path.join(SCENES, "bunny15.xml"), {"width": 64, "height": 36, "spp": 1})
-    monkeypatch.setenv("MTSG_STACK_CAP", "1")
-    monkeypatch.setenv("MTSG_RESTART_LIMIT", "0")
     g = mtsg.GPUScene(s, 0)
     try:
+        g.set_test_knobs(stack_cap=1, restart_limit=0)
         with pytest.raises(RuntimeError, match=r"\(-6\).*restart limit"):
             g.trace_closest(corner_rays(s, 20000, 54))
         with pytest.raises(RuntimeError, match=r"\(-6\).*restart limit"):
             g.render(s.params(), s.border)
-    finally:
-        g.close()
-    # with the default limit the frame renders
-    monkeypatch.delenv("MTSG_RESTART_LIMIT")
-    g = mtsg.GPUScene(s, 0)
-    try:
+        # with the default limit the frame renders
+        g.set_test_knobs(stack_cap=1)
+        g.render(s.params(), s.border)
+        g.set_test_knobs()
         g.render(s.params(), s.border)
     finally:
         g.close()
 
 
-def test_restart_limit_of_shadow_rays_fails_the_render(monkeypatch):
-    """The limit applied to shadow rays only (MTSG_RESTART_LIMIT_SHADOW_ONLY):
+def test_restart_limit_of_shadow_rays_fails_the_render():
+    """The limit applied to shadow rays only (limit_shadow_only):
     closest-hit rays traverse normally, and a shadow ray that reaches the limit
     still fails the render.  Shadow rays are traced in the next bounce's launch
     or in the final shadow launch after the last bounce; the error word is read
     after both (the final launch's errors were not read)."""
     s = mtsg.Scene(os.path.join(SCENES, "bunny15.xml"), {"width": 64, "height": 36, "spp": 1})
-    monkeypatch.setenv("MTSG_STACK_CAP", "1")
-    monkeypatch.setenv("MTSG_RESTART_LIMIT", "0")
-    monkeypatch.setenv("MTSG_RESTART_LIMIT_SHADOW_ONLY", "1")
     g = mtsg.GPUScene(s, 0)
     try:
+        g.set_test_knobs(stack_cap=1, restart_limit=0, limit_shadow_only=True)
         rays = corner_rays(s, 20000, 55)
         g.trace_closest(rays)   # closest-hit rays are not limited
         sh = rays.copy()

@@ -21,6 +21,7 @@ for w in ${*:-tests bench}; do
     tests-kd) step tests-kd 600 $PYT tests/test_gpu_kdbuild.py ;;
     tests-new) step tests-new 600 $PYT tests/test_gpu_00_bench_ranks.py tests/test_gpu_c4.py tests/test_gpu_edge_rays.py ;;
     tests-builder) step tests-builder 600 $PYT tests/test_gpu_builder.py ;;
+    tests-edge) step tests-edge 600 $PYT tests/test_gpu_edge_rays.py tests/test_gpu_kdbuild.py tests/test_gpu_instancing.py ;;
     tests-sfmt) step tests-sfmt 600 $PYT -s tests/test_gpu_rng_sfmt.py ;;
     tests-pp) step tests-pp 900 $PYT -s tests/test_gpu_parity.py tests/test_gpu_configs.py -k "roughconductor or rough_conductor or roughplastic or c5 or c1 or c2" ;;
     bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
