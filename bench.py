@@ -63,7 +63,8 @@ def pmc_key(a, world=1):
     describe other launches and are never quoted."""
     return {"workload": a.workload, "instancing": a.instancing, "kd_build": a.kd_build, "width": a.width,
             "height": a.height, "spp": a.spp, "share": max(world, a.emulate_ranks, 1),
-            "batch_paths": a.batch_paths or 0, "finish_paths": a.finish_paths, "build": device_build_id()}
+            "batch_paths": a.batch_paths or 0, "finish_paths": a.finish_paths,
+            "balance_rounds": a.balance_rounds if max(world, a.emulate_ranks, 1) > 1 else 0, "build": device_build_id()}
 
 
 def pmc_lookup(key, directory=None):
@@ -108,6 +109,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="single process: render only rank 0's tile share of an N-GPU run (scaling rehearsal)")
+    ap.add_argument("--balance-rounds", type=int, default=4,
+                    help="shares > 1: warm-up rounds that re-cut the ranks' tile shares from their measured step "
+                         "times (mtsg_set_tile_list); 0 = the fixed stride deal")
     ap.add_argument("--save", default="", help="write the developed image (.npy) here (rank 0)")
     ap.add_argument("--no-count", action="store_true",
                     help="skip the instrumented (untimed) pass of per-ray counts (profiler runs)")
@@ -302,9 +306,10 @@ def gather_frame(pg, rank, world, part, tile_w, tile_h, border):
     if rank != 0:
         return None
     frame = np.zeros((tile_h + 2 * border, tile_w + 2 * border, 5), np.float32)
-    for r, (kind, arr) in enumerate(parts):
+    for r, (kind, arr, *rest) in enumerate(parts):
+        keys = rest[0] if rest else None   # a tile list's keys (balanced shares), else the stride deal
         if kind == "win":
-            mtsg.put_tile_windows(frame, arr, tile_w, tile_h, border, world, r)
+            mtsg.put_tile_windows(frame, arr, tile_w, tile_h, border, world, r, keys=keys)
         else:
             frame += arr
     return frame
@@ -431,12 +436,40 @@ def main():
     # per-block ImageBlocks of BlockedRenderProcess) instead of a block of the
     # whole frame: 3.6 MB instead of 18.7 MB over PCIe per 1/8 C3 share.  The
     # host puts them into the frame's block after the timed region.
+    # Shares.  With --balance-rounds > 0 (default) a share is an explicit
+    # list of deal keys (mtsg_set_tile_list): a run of balance_order, whose
+    # length the warm-up rounds re-cut from the shares' measured step times
+    # (the reference's scheduler gives the next block to whichever worker is
+    # free, src/libcore/sched.cpp:427-496); without it, the stride deal.
+    emulated = a.emulate_ranks > 1 and world == 1
+    n_shares = a.emulate_ranks if emulated else world
+    n_tiles = ((params.tile_w + 15) // 16) * ((params.tile_h + 15) // 16)
+    balanced = n_shares > 1 and a.balance_rounds > 0
+    order = mtsg.balance_order(n_tiles)
+    counts = np.array([len(range(r, n_tiles, n_shares)) for r in range(n_shares)], dtype=np.int64)
+    cur = {"keys": None}
+
+    def share_keys(r):
+        lo = int(counts[:r].sum())
+        return np.sort(order[lo:lo + int(counts[r])])
+
+    def use_share(r):
+        if balanced:
+            cur["keys"] = share_keys(r)
+            gpu.set_tile_list(cur["keys"])
+        else:
+            params.tile_stride, params.tile_offset = (n_shares, r) if n_shares > 1 else (1, 0)
+
+    def use_whole():
+        cur["keys"] = None
+        gpu.set_tile_list(None)
+        params.tile_stride, params.tile_offset = 1, 0
+
     def windows_for(p):
         n, w = gpu.tile_windows(p)
-        return (n, w) if p.tile_stride > 1 and n * w * w < W * H else None
-    cand = ([_share(params, a.emulate_ranks, o) for o in range(a.emulate_ranks)]
-            if a.emulate_ranks > 1 and world == 1 else [params])
-    win_max = max(((windows_for(pp) or (0, 0))[0] for pp in cand), default=0)
+        return (n, w) if (cur["keys"] is not None or p.tile_stride > 1) and n * w * w < W * H else None
+    # window buffer: room for any share the balancing may cut
+    win_max = n_tiles if n_shares > 1 else 0
     wbuf = gpu.alloc(win_max * (16 + 2 * border) ** 2 * 5 * 4) if win_max else None
     host_win = np.zeros((max(1, win_max), 16 + 2 * border, 16 + 2 * border, 5), np.float32)
 
@@ -454,11 +487,39 @@ def main():
 
     # --emulate-ranks N: every rank's tile share in turn on this one GPU, each
     # timed like a rank of an N-GPU run (max over the shares = the frame time)
-    shares = list(range(a.emulate_ranks)) if (a.emulate_ranks > 1 and world == 1) else [params.tile_offset]
+    shares = list(range(a.emulate_ranks)) if emulated else [rank]
+    balance_log = []
+    if balanced:
+        # warm-up rounds that re-cut the shares: every share renders one step
+        # (the first, untimed, allocates), then the tile counts follow the
+        # measured rates (mtsg.balance_cuts); every rank computes the same cuts
+        # from the all-gathered times
+        for r in shares:
+            use_share(r)
+            step()
+        for _ in range(a.balance_rounds):
+            times = {}
+            for r in shares:
+                use_share(r)
+                # the faster of two steps: a share that grew past the batch
+                # buffers reallocates them in its first step
+                best = None
+                for _ in range(2):
+                    barrier(pg)
+                    t0 = time.perf_counter()
+                    step()
+                    dt = time.perf_counter() - t0
+                    best = dt if best is None else min(best, dt)
+                times[r] = best
+            if not emulated:
+                times = dict(enumerate(all_gather_obj(pg, times[rank], world)))
+            t = [times[r] for r in range(n_shares)]
+            balance_log.append({"tiles": counts.tolist(), "ms": [round(x * 1e3, 3) for x in t]})
+            counts = mtsg.balance_cuts(counts, t)
     share_s = []
     acc = {}
     for off in shares:
-        params.tile_offset = off
+        use_share(off)
         for _ in range(a.warmup):
             step()
         # per-kernel HIP events on the library's stream stay on through the
@@ -478,19 +539,19 @@ def main():
         barrier(pg)
         share_s.append(time.perf_counter() - t0)
         gpu.set_flags(0)
-    params.tile_offset = shares[0]
+    use_share(shares[0])
     elapsed = max_over_ranks(pg, max(share_s))
     whole_s = None
     if len(shares) > 1:
         # the whole frame on this GPU, for the per-share speedups
-        params.tile_stride, params.tile_offset = 1, 0
+        use_whole()
         for _ in range(a.warmup):
             step()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             step()
         whole_s = time.perf_counter() - t0
-        params.tile_stride, params.tile_offset = a.emulate_ranks, shares[0]
+        use_share(shares[0])
     samples_total = params.tile_w * params.tile_h * params.spp * a.steps
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
@@ -619,10 +680,12 @@ def main():
     # the host-side tile gather: every rank's share of the timed steps' last
     # frame into rank 0's ImageBlock (after the timed region)
     frame = assembly = parity = None
-    if not (a.emulate_ranks > 1 and world == 1):
+    if not emulated:
         nw = windows_for(params)
-        part = ("win", host_win[:nw[0]].copy()) if nw else ("block", host_block.copy())
+        keys = None if cur["keys"] is None else cur["keys"].copy()
+        part = ("win", host_win[:nw[0]].copy(), keys) if nw else ("block", host_block.copy(), None)
         frame = gather_frame(pg, rank, world, part, params.tile_w, params.tile_h, border)
+    use_whole()
     if rank == 0 and world > 1:
         # the assembled frame vs the whole frame rendered by rank 0's GPU alone
         # (global RNG keys: the same samples; the film's float additions may
@@ -636,8 +699,7 @@ def main():
         assembly = {"check": f"frame assembled from {world} ranks' tile ImageBlocks vs the whole frame rendered on rank 0's GPU",
                     "max_abs_diff": float(diff.max()), "max_value": float(np.abs(whole).max()),
                     "pass": bool(np.allclose(frame, whole, rtol=1e-5, atol=1e-6)),
-                    "tiles_per_rank": [int(((mtsg.tile_deal_keys(params.tile_w, params.tile_h)[::16, ::16]) % world == r).sum())
-                                       for r in range(world)]}
+                    "tiles_per_rank": counts.tolist()}
     if rank == 0 and a.save and frame is not None:
         np.save(a.save, mtsg.develop(frame[border:H - border, border:W - border]))
     if rank == 0 and frame is not None and not a.no_parity:
@@ -673,9 +735,15 @@ def main():
                 "whole_frame_ms_per_step": round(whole_s / a.steps * 1e3, 3) if whole_s else None,
                 "share_speedups": [round(whole_s / t, 3) for t in share_s] if whole_s else None,
                 "share_speedup_min": round(whole_s / max(share_s), 3) if whole_s else None,
-                "note": "one GPU rendering each rank's 1/N tile share in turn; value = frame samples / the slowest "
+                "note": "one GPU rendering each rank's tile share in turn; value = frame samples / the slowest "
                         "share's time (the N-GPU frame time without launch and gather overheads); kernels = share 0"}
                if a.emulate_ranks > 1 and world == 1 else {}),
+            **({"balance": {"rounds": balance_log, "tiles_per_share": counts.tolist(),
+                            "method": "shares are runs of the golden-ratio key order (mtsg.balance_order); each "
+                                      "warm-up round times every share (the faster of two steps) and gives share r "
+                                      "tiles in proportion to its measured rate, damped 1/2 (mtsg.balance_cuts); "
+                                      "the timed steps use the last cut"}}
+               if balanced else {}),
             "roofline": roofline, "cpu_baseline": cpu, "parity": parity,
             **({"assembly": assembly} if assembly else {}), "kernels": kernels,
         }

@@ -536,6 +536,19 @@ int  mtsg_tile_windows(mtsg_scene *scene, const mtsg_render_params *params,
 int  mtsg_render_device_tiles(mtsg_scene *scene, const mtsg_render_params *params,
                               float *windows_device);
 
+/* Explicit tile share (dynamic balancing): after this call the render calls
+ * of the handle take exactly the tiles with deal keys keys[0..n) (the keys of
+ * tile_stride above, distinct, each inside the params' rectangle, else the
+ * render fails with MTSG_ERR_INVALID), in that order -- mtsg_render_device_tiles
+ * window v holds the tile keys[v] -- instead of tile_stride / tile_offset.
+ * n = 0 returns to the stride deal.  The per-sample random numbers are keyed
+ * by pixel and sample, so any split of the keys over ranks sums to the
+ * whole-frame image bit for bit.  The share a rank takes can then follow
+ * its measured speed, as the reference's scheduler hands the next block to
+ * whichever worker is free (src/libcore/sched.cpp:427-496); bench.py
+ * re-cuts the shares from the warm-up steps' times. */
+int  mtsg_set_tile_list(mtsg_scene *scene, const int32_t *keys, uint32_t n);
+
 /* Device buffer helpers for mtsg_render_device (plain hipMalloc/hipMemcpy). */
 int  mtsg_device_alloc(mtsg_scene *scene, size_t bytes, void **out);
 int  mtsg_device_free(mtsg_scene *scene, void *ptr);

@@ -41,13 +41,28 @@ int mtsh_path_job_gpus(const mtsh_path_job *job);
 
 /* Render params->tile_* into rgbaw_out ((tile_h + 2b) x (tile_w + 2b) x 5
  * floats, b = border).  The rectangle's 16x16 tiles selected by
- * params->tile_stride / tile_offset (all tiles when stride <= 1) are dealt
- * over the job's N GPUs: GPU g renders the tiles of deal keys
- * offset + (g + k N) stride.
+ * params->tile_stride / tile_offset (all tiles when stride <= 1) are shared
+ * over the job's N GPUs (mtsg_set_tile_list): GPU g renders a run of those
+ * deal keys in golden-ratio order (key k at frac(k * 0.618...)), so every
+ * share is spread over the whole rectangle.  The first render of a tile set
+ * gives the GPUs equal runs; a render of the same set again (same rectangle,
+ * deal, spp, depth and integrator) re-cuts them from the GPUs' measured
+ * rates (tiles / second of the last render, damped by half), so a slower
+ * share shrinks -- the job's stand-in for the reference scheduler handing
+ * the next block to a free worker (src/libcore/sched.cpp:427-496).  The
+ * image does not depend on the cut.
  * seconds_out (optional) receives the render time.  Blocking; returns an mtsg
  * error code (MTSG_ERR_CANCELLED after mtsh_path_job_cancel). */
 int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, float *rgbaw_out,
                          double *seconds_out);
+
+/* Share balancing on (default) or off (equal runs every render); either
+ * call forgets the last render's rates. */
+int mtsh_path_job_set_balance(mtsh_path_job *job, int on);
+
+/* The last render's tiles and seconds per GPU (arrays of mtsh_path_job_gpus
+ * entries; either may be NULL). */
+int mtsh_path_job_shares(const mtsh_path_job *job, int32_t *tiles, double *seconds);
 
 /* Tile completion of the job's renders: fn(user, gpu, x, y, w, h) once per
  * 16x16 tile when its ImageBlock contribution is complete on GPU `gpu` (see

@@ -121,7 +121,10 @@ struct DevBatch {
     int skew;                             // deal: row ty rotated by ty * skew tiles (always 1)
     uint32_t s0, ns;
     uint32_t nslots;
+    const int32_t *keys;                  // mtsg_set_tile_list: deal key of virtual tile v = keys[v] (device); null: arithmetic
 };
+// deal key of virtual tile v of a call
+__host__ __device__ inline int batch_key(const DevBatch &B, int v) { return B.keys ? B.keys[v] : B.toffset + v * B.tstride; }
 
 // Multi-GPU tile deal (mtsg_render_params.tile_stride / tile_offset): tile
 // (tx, ty) of the rectangle's tile grid has the deal key ty * tiles_x +
@@ -1613,7 +1616,7 @@ DEV void slot_pixel(const DevBatch &B, uint32_t slot, int &x, int &y, uint32_t &
     const uint32_t sl = rest % B.ns;
     const uint32_t tl = rest / B.ns;
     int tx, ty;
-    tile_of_key(B.toffset + (B.tile0 + (int)tl) * B.tstride, B.tiles_x, tx, ty, B.skew);
+    tile_of_key(batch_key(B, B.tile0 + (int)tl), B.tiles_x, tx, ty, B.skew);
     x = B.rect_x + tx * TILE + (int)(pix % TILE);
     y = B.rect_y + ty * TILE + (int)(pix / TILE);
     s = B.s0 + sl;
@@ -3321,7 +3324,7 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
     for (int k = threadIdx.x; k < CH * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
     const int tl = blockIdx.x;
     int tx, ty;
-    tile_of_key(B.toffset + (B.tile0 + tl) * B.tstride, B.tiles_x, tx, ty, B.skew);
+    tile_of_key(batch_key(B, B.tile0 + tl), B.tiles_x, tx, ty, B.skew);
     const int x0 = B.rect_x + tx * TILE, y0 = B.rect_y + ty * TILE;   // tile origin (film coords)
     const int bord = C.border;
     const int pix = threadIdx.x;

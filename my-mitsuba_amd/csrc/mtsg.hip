@@ -80,6 +80,10 @@ struct mtsg_scene {
     int stagger = 0;               // bounces between the starts of consecutive lanes
     int lanesAlloc = 0;            // lanes with path state allocated
     hipStream_t lstream[MTSG_MAX_LANES] = {};   // lstream[0] == stream
+    // mtsg_set_tile_list: the deal keys a render call takes (empty: tile_stride / tile_offset)
+    std::vector<int32_t> tileKeys;
+    int32_t *tileKeysDev = nullptr;
+    size_t tileKeysCap = 0;
     DevPaths LP[MTSG_MAX_LANES]{};
     std::vector<void *> batchAllocs;
     uint32_t *hostCnt = nullptr;   // pinned copy of the queue counters (2 per lane)
@@ -380,7 +384,13 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
     const uint32_t allTiles = tilesX * tilesY;
     const uint32_t tstride = p->tile_stride > 1 ? (uint32_t)p->tile_stride : 1u;
     const uint32_t toffset = p->tile_stride > 1 ? (uint32_t)p->tile_offset : 0u;
-    const uint32_t ntiles = toffset < allTiles ? (allTiles - toffset + tstride - 1) / tstride : 0u;
+    const bool listed = !s->tileKeys.empty();
+    const uint32_t ntiles = listed ? (uint32_t)s->tileKeys.size() : toffset < allTiles ? (allTiles - toffset + tstride - 1) / tstride : 0u;
+    if (listed)
+        for (int32_t k : s->tileKeys)
+            if ((uint32_t)k >= allTiles) { g_err = "tile list: a deal key lies outside the rectangle's tiles"; return MTSG_ERR_INVALID; }
+    // the deal key of virtual tile v, on the host
+    auto hostKey = [&](int v) { return listed ? s->tileKeys[v] : (int)toffset + v * (int)tstride; };
     // Lanes: independent batches on their own streams, issued bounce by bounce
     // in lock step, so one lane's launch tail (its slowest rays) overlaps the
     // other lane's launch.  The debug and counting modes use one lane.
@@ -431,6 +441,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
             B.s0 = s0;
             B.ns = std::min(sppPerBatch, p->spp - s0);
             B.nslots = (uint32_t)B.ntiles * B.ns * TILE * TILE;
+            B.keys = listed ? s->tileKeysDev : nullptr;
             batches.push_back(B);
         }
     }
@@ -604,7 +615,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
                 const DevBatch &B = lr[l].B;
                 if (B.s0 + B.ns < p->spp) continue;
                 for (int tl = 0; tl < B.ntiles; ++tl) {
-                    const int key = B.toffset + (B.tile0 + tl) * B.tstride;
+                    const int key = hostKey(B.tile0 + tl);
                     int tx, ty;
                     tile_of_key(key, B.tiles_x, tx, ty, B.skew);
                     const int x = tx * TILE, y = ty * TILE;
@@ -623,7 +634,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
                 const uint32_t pix = slot & (TILE * TILE - 1), rest = slot >> 8;
                 const uint32_t sl = rest % B.ns, tl = rest / B.ns;
                 int tx, ty;
-                tile_of_key(B.toffset + (B.tile0 + (int)tl) * B.tstride, B.tiles_x, tx, ty, B.skew);
+                tile_of_key(hostKey(B.tile0 + (int)tl), B.tiles_x, tx, ty, B.skew);
                 const int x = tx * TILE + (int)(pix % TILE), y = ty * TILE + (int)(pix / TILE);
                 if (x >= p->tile_w || y >= p->tile_h) continue;
                 float *o = s->dumpL + (((size_t)y * p->tile_w + x) * p->spp + B.s0 + sl) * 4;
@@ -650,7 +661,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
     if (e != hipSuccess) { g_err = std::string("kernel launch: ") + hipGetErrorString(e); return MTSG_ERR_DEVICE; }
     if (result != MTSG_OK) return result;
     // samples actually inside the rectangle (all tiles of this call)
-    if (tstride == 1) s->stats.samples = (uint64_t)p->tile_w * p->tile_h * p->spp;
+    if (tstride == 1 && !listed) s->stats.samples = (uint64_t)p->tile_w * p->tile_h * p->spp;
     if (s->flags & MTSG_FLAG_TIMING) {
         for (auto &te : s->timed) {
             float ms = 0;
@@ -1325,7 +1336,8 @@ int mtsg_render_device(mtsg_scene *s, const mtsg_render_params *p, float *film) 
     return render_impl(s, p, film);
 }
 
-static uint32_t tile_count(const mtsg_render_params *p) {
+static uint32_t tile_count(const mtsg_scene *s, const mtsg_render_params *p) {
+    if (!s->tileKeys.empty()) return (uint32_t)s->tileKeys.size();
     const uint32_t allTiles = (uint32_t)((p->tile_w + TILE - 1) / TILE) * (uint32_t)((p->tile_h + TILE - 1) / TILE);
     const uint32_t tstride = p->tile_stride > 1 ? (uint32_t)p->tile_stride : 1u;
     const uint32_t toffset = p->tile_stride > 1 ? (uint32_t)p->tile_offset : 0u;
@@ -1336,8 +1348,31 @@ int mtsg_tile_windows(mtsg_scene *s, const mtsg_render_params *p, uint32_t *ntil
     if (!s || !ntiles || !window) { g_err = "null argument"; return MTSG_ERR_INVALID; }
     int rc;
     if ((rc = validate(p, s)) != MTSG_OK) return rc;
-    *ntiles = tile_count(p);
+    *ntiles = tile_count(s, p);
     *window = TILE + 2 * s->cam.border;
+    return MTSG_OK;
+}
+
+int mtsg_set_tile_list(mtsg_scene *s, const int32_t *keys, uint32_t n) {
+    if (!s || (n && !keys)) { g_err = "null argument"; return MTSG_ERR_INVALID; }
+    std::vector<int32_t> k(keys, keys + n), sorted(k);
+    std::sort(sorted.begin(), sorted.end());
+    for (uint32_t i = 0; i < n; ++i)
+        if (sorted[i] < 0 || (i && sorted[i] == sorted[i - 1])) {
+            g_err = "tile list: deal keys must be distinct and non-negative";
+            return MTSG_ERR_INVALID;
+        }
+    int rc;
+    if ((rc = set_device(s)) != MTSG_OK) return rc;
+    if (n > s->tileKeysCap) {
+        if (s->tileKeysDev) hipFree(s->tileKeysDev);
+        s->tileKeysDev = nullptr;
+        s->tileKeysCap = 0;
+        HIP_TRY(hipMalloc((void **)&s->tileKeysDev, n * sizeof(int32_t)));
+        s->tileKeysCap = n;
+    }
+    if (n) HIP_TRY(hipMemcpy(s->tileKeysDev, k.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+    s->tileKeys.swap(k);
     return MTSG_OK;
 }
 
@@ -1617,6 +1652,7 @@ void mtsg_scene_destroy(mtsg_scene *s) {
     for (int l = 1; l < MTSG_MAX_LANES; ++l)
         if (s->lstream[l]) hipStreamDestroy(s->lstream[l]);
     if (s->stream) hipStreamDestroy(s->stream);
+    if (s->tileKeysDev) hipFree(s->tileKeysDev);
     delete s;
 }
 

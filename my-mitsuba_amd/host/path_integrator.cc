@@ -2,12 +2,15 @@
 // src/integrators/path/path.cpp) whose render() drives the GPU library
 // instead of the per-sample CPU loop of SamplingIntegrator::render
 // (src/librender/integrator.cpp:99-133): one host thread per GPU, each
-// renders an interleaved subset of the 16x16 film tiles into its own
+// renders a share of the 16x16 film tiles (balanced from the last render's
+// rates, see mtsh_path_job_render) into its own
 // ImageBlock (tile rect + border), and the blocks are merged by addition
 // exactly like ImageBlock::put(const ImageBlock*) (imageblock.h:103-107).
 // No collectives: the film is the only thing exchanged (host-side gather).
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -47,6 +50,12 @@ struct mtsh_path_job {
     std::mutex tileLock;
     struct TileCtx { mtsh_path_job *job; int gpu; };
     std::vector<TileCtx> tileCtx;
+    // share balancing (mtsh_path_job_set_balance): the last render's tiles
+    // and seconds per GPU, for the next render of the same tile set
+    int balance = 1;
+    std::vector<int> lastCount;
+    std::vector<double> lastSec;
+    std::vector<int64_t> lastSig;
     explicit mtsh_path_job(int n) : rendering(n, 0), sent(n, 0), gpuLock(n) {}
 };
 
@@ -55,6 +64,55 @@ void tile_trampoline(void *user, int32_t, int32_t x, int32_t y, int32_t w, int32
     auto *c = static_cast<mtsh_path_job::TileCtx *>(user);
     std::lock_guard<std::mutex> lock(c->job->tileLock);
     if (c->job->tileFn) c->job->tileFn(c->job->tileUser, c->gpu, x, y, w, h);
+}
+// The caller's tiles in the order balanced shares are cut from: deal key k
+// at position frac(k * golden ratio), so a run of any length is spread over
+// the whole rectangle (mtsg.balance_order is the same order)
+std::vector<int32_t> balance_order(const std::vector<int32_t> &keys) {
+    const double phi = (std::sqrt(5.0) - 1.0) / 2.0;
+    std::vector<std::pair<double, int32_t>> o;
+    o.reserve(keys.size());
+    for (int32_t k : keys) {
+        double ip;
+        o.emplace_back(std::modf((double)k * phi, &ip), k);
+    }
+    std::stable_sort(o.begin(), o.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::vector<int32_t> out;
+    out.reserve(o.size());
+    for (auto &e : o) out.push_back(e.second);
+    return out;
+}
+
+// next tile counts from the last render (mtsg.balance_cuts): GPU g took
+// sec[g] for count[g] tiles, so it is given count[g] / sec[g] of the total,
+// mixed half and half with its old count; every GPU keeps at least one tile
+std::vector<int> balance_cuts(const std::vector<int> &count, const std::vector<double> &sec) {
+    const size_t n = count.size();
+    double total = 0, rsum = 0;
+    for (size_t g = 0; g < n; ++g) {
+        total += count[g];
+        rsum += count[g] / std::max(sec[g], 1e-9);
+    }
+    std::vector<double> want(n);
+    std::vector<int> out(n);
+    long sum = 0;
+    for (size_t g = 0; g < n; ++g) {
+        const double target = count[g] / std::max(sec[g], 1e-9) / rsum * total;
+        want[g] = 0.5 * count[g] + 0.5 * target;
+        out[g] = std::max(1, (int)std::floor(want[g]));
+        sum += out[g];
+    }
+    std::vector<size_t> order(n);
+    for (size_t g = 0; g < n; ++g) order[g] = g;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](size_t a, size_t b) { return want[a] - std::floor(want[a]) > want[b] - std::floor(want[b]); });
+    long rest = (long)std::llround(total) - sum;
+    for (size_t k = 0; rest != 0 && k < 4 * n + (size_t)std::labs(rest) * n; ++k) {
+        const size_t g = order[k % n];
+        if (rest > 0) { ++out[g]; --rest; }
+        else if (out[g] > 1) { --out[g]; ++rest; }
+    }
+    return out;
 }
 }  // namespace
 
@@ -118,12 +176,38 @@ int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, f
         return MTSG_ERR_INVALID;
     }
     const size_t W = (size_t)params->tile_w + 2 * b, H = (size_t)params->tile_h + 2 * b;
-    // compose the caller's tile subset with the deal over GPUs: of the
-    // caller's tiles off + k * S, GPU g takes every n-th one
+    // the caller's tile subset: deal keys off + k * S of the rectangle's tiles
     const int S = params->tile_stride > 1 ? params->tile_stride : 1;
     const int off = params->tile_stride > 1 ? params->tile_offset : 0;
+    const int allTiles = ((params->tile_w + 15) / 16) * ((params->tile_h + 15) / 16);
+    std::vector<int32_t> keys;
+    for (int k = off; k < allTiles; k += S) keys.push_back(k);
+    // Shares.  A GPU renders its share as one wavefront batch, so handing out
+    // tile groups from a queue during the render (the reference scheduler's
+    // acquireWork, src/libcore/sched.cpp:427-496) would cut the share into
+    // batches that each pay the per-bounce launch drain;
+    // instead each GPU takes a run of the golden-ratio key order, and a render
+    // of the same tile set as the last one re-cuts the runs from the GPUs'
+    // measured rates (balance_cuts).  Any cut gives the same image: the
+    // random numbers are keyed by pixel and sample.
+    const std::vector<int64_t> sig = {params->tile_x, params->tile_y, params->tile_w, params->tile_h, S, off,
+                                      (int64_t)params->spp, params->max_depth, params->integrator};
+    std::vector<int> count(n, 0);
+    if (job->balance && n > 1 && job->lastSig == sig && (int)job->lastCount.size() == n &&
+        (int)keys.size() >= n) {
+        count = balance_cuts(job->lastCount, job->lastSec);
+    } else {
+        for (int g = 0; g < n; ++g) count[g] = (int)(keys.size() / n + ((size_t)g < keys.size() % n ? 1 : 0));
+    }
+    const std::vector<int32_t> order = balance_order(keys);
+    std::vector<std::vector<int32_t>> share(n);
+    for (int g = 0, lo = 0; g < n; lo += count[g], ++g) {
+        share[g].assign(order.begin() + lo, order.begin() + lo + count[g]);
+        std::sort(share[g].begin(), share[g].end());
+    }
     std::vector<std::vector<float>> blocks(n, std::vector<float>(W * H * 5));
     std::vector<int> rcs(n, MTSG_OK);
+    std::vector<double> sec(n, 0.0);
     std::vector<std::string> errs(n);
     job->cancel.store(0);   // a cancel() while idle has no effect
     auto t0 = std::chrono::steady_clock::now();
@@ -131,14 +215,18 @@ int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, f
     for (int g = 0; g < n; ++g)
         threads.emplace_back([&, g]() {
             mtsg_render_params p = *params;
-            p.tile_stride = S * n;
-            p.tile_offset = p.tile_stride > 1 ? off + g * S : 0;
+            p.tile_stride = 1;
+            p.tile_offset = 0;
             {
                 std::lock_guard<std::mutex> gl(job->gpuLock[g]);
                 job->rendering[g] = 1;
             }
+            const auto tg = std::chrono::steady_clock::now();
             if (job->cancel.load()) rcs[g] = MTSG_ERR_CANCELLED;
-            else rcs[g] = mtsg_render(job->handles[g], &p, blocks[g].data());
+            else if (share[g].empty()) rcs[g] = MTSG_OK;   // fewer tiles than GPUs: this one idles
+            else if ((rcs[g] = mtsg_set_tile_list(job->handles[g], share[g].data(), (uint32_t)share[g].size())) == MTSG_OK)
+                rcs[g] = mtsg_render(job->handles[g], &p, blocks[g].data());
+            sec[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - tg).count();
             {
                 std::lock_guard<std::mutex> gl(job->gpuLock[g]);
                 job->rendering[g] = 0;
@@ -164,6 +252,27 @@ int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, f
     std::memset(rgbaw_out, 0, W * H * 5 * sizeof(float));
     for (int g = 0; g < n; ++g)
         for (size_t i = 0; i < W * H * 5; ++i) rgbaw_out[i] += blocks[g][i];
+    job->lastSig = sig;
+    job->lastCount = count;
+    job->lastSec = sec;
+    return MTSG_OK;
+}
+
+int mtsh_path_job_set_balance(mtsh_path_job *job, int on) {
+    if (!job) { g_perr = "null argument"; return MTSG_ERR_INVALID; }
+    std::lock_guard<std::mutex> lock(job->renderLock);
+    job->balance = on != 0;
+    job->lastSig.clear();
+    return MTSG_OK;
+}
+
+int mtsh_path_job_shares(const mtsh_path_job *job, int32_t *tiles, double *seconds) {
+    if (!job) { g_perr = "null argument"; return MTSG_ERR_INVALID; }
+    const size_t n = job->handles.size();
+    for (size_t g = 0; g < n; ++g) {
+        if (tiles) tiles[g] = g < job->lastCount.size() ? job->lastCount[g] : 0;
+        if (seconds) seconds[g] = g < job->lastSec.size() ? job->lastSec[g] : 0.0;
+    }
     return MTSG_OK;
 }
 

@@ -213,7 +213,7 @@ _dev = None
 
 DEVICE_SYMBOLS = [
     "mtsg_device_count", "mtsg_device_pci_id", "mtsg_scene_create", "mtsg_render", "mtsg_render_device",
-    "mtsg_tile_windows", "mtsg_render_device_tiles",
+    "mtsg_tile_windows", "mtsg_render_device_tiles", "mtsg_set_tile_list",
     "mtsg_device_alloc", "mtsg_device_free", "mtsg_device_memset", "mtsg_device_to_host",
     "mtsg_cancel", "mtsg_cancel_clear", "mtsg_set_flags", "mtsg_get_stats", "mtsg_set_batch_paths", "mtsg_set_finish_paths",
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
@@ -233,6 +233,7 @@ HOST_SYMBOLS = [
 PATH_SYMBOLS = [
     "mtsh_path_job_create", "mtsh_path_job_gpus", "mtsh_path_job_render", "mtsh_path_job_cancel",
     "mtsh_path_job_destroy", "mtsh_path_render", "mtsh_path_last_error", "mtsh_path_job_set_tile_callback",
+    "mtsh_path_job_set_balance", "mtsh_path_job_shares",
 ]
 
 # tile completion hooks (mtsg_set_tile_callback, mtsh_path_job_set_tile_callback)
@@ -256,6 +257,8 @@ def path_lib() -> C.CDLL:
         lib.mtsh_path_job_cancel.argtypes = [C.c_void_p]
         lib.mtsh_path_job_destroy.argtypes = [C.c_void_p]
         lib.mtsh_path_job_set_tile_callback.argtypes = [C.c_void_p, TILE_FN, C.c_void_p]
+        lib.mtsh_path_job_set_balance.argtypes = [C.c_void_p, C.c_int]
+        lib.mtsh_path_job_shares.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsh_path_render.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_int, C.c_void_p,
                                          C.POINTER(C.c_double)]
         lib.mtsh_path_last_error.argtypes = [C.c_char_p, C.c_size_t]
@@ -345,6 +348,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_tile_windows.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.POINTER(C.c_uint32),
                                           C.POINTER(C.c_int32)]
         lib.mtsg_render_device_tiles.argtypes = [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]
+        lib.mtsg_set_tile_list.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
         lib.mtsg_device_alloc.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]
         lib.mtsg_device_free.argtypes = [C.c_void_p, C.c_void_p]
         lib.mtsg_device_memset.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
@@ -640,17 +644,18 @@ def tile_deal_keys(tile_w: int, tile_h: int) -> np.ndarray:
 
 
 def put_tile_windows(block: np.ndarray, windows: np.ndarray, tile_w: int, tile_h: int, border: int,
-                     stride: int, offset: int) -> np.ndarray:
+                     stride: int, offset: int, keys=None) -> np.ndarray:
     """Add per-tile ImageBlocks (mtsg_render_device_tiles: window v = the tile of
-    deal key offset + v * stride, window = 16 + 2 * border) into the block of the
-    whole rectangle + border, as ImageBlock::put(const ImageBlock *) does
-    (imageblock.h:103-107).  block: (tile_h + 2b, tile_w + 2b, 5)."""
+    deal key offset + v * stride, or keys[v] for a tile list, window = 16 + 2 *
+    border) into the block of the whole rectangle + border, as
+    ImageBlock::put(const ImageBlock *) does (imageblock.h:103-107).
+    block: (tile_h + 2b, tile_w + 2b, 5)."""
     tiles_x = (tile_w + 15) // 16
     stride = max(1, stride)
     offset = offset if stride > 1 else 0
     win = windows.shape[1]
     for v in range(windows.shape[0]):
-        key = offset + v * stride
+        key = int(keys[v]) if keys is not None else offset + v * stride
         ty = key // tiles_x
         tx = (key % tiles_x + ty) % tiles_x
         x0, y0 = 16 * tx, 16 * ty   # window origin in block coordinates (the tile origin minus the border)
@@ -658,6 +663,43 @@ def put_tile_windows(block: np.ndarray, windows: np.ndarray, tile_w: int, tile_h
         w = min(win, block.shape[1] - x0)
         block[y0:y0 + h, x0:x0 + w] += windows[v, :h, :w]
     return block
+
+
+def balance_order(n_tiles: int) -> np.ndarray:
+    """The deal keys 0..n_tiles-1 in the order balanced shares cut into
+    contiguous runs: key k at position frac(k * golden ratio), so a run of any
+    length is spread over the whole rectangle (as the stride deal is) and a
+    share can grow or shrink by single tiles."""
+    phi = (np.sqrt(5.0) - 1.0) / 2.0
+    return np.argsort(np.modf(np.arange(n_tiles) * phi)[0], kind="stable").astype(np.int32)
+
+
+def balance_cuts(counts, times, damping: float = 0.5):
+    """New tile counts per share from the last step: share r took times[r]
+    for counts[r] tiles, so it is given counts[r] / times[r] of the total
+    (its measured rate), mixed with its old count by `damping`; the counts
+    still sum to the total and every share keeps at least one tile."""
+    counts = np.asarray(counts, dtype=np.float64)
+    times = np.maximum(np.asarray(times, dtype=np.float64), 1e-9)
+    total = int(round(counts.sum()))
+    target = counts / times
+    target = target / target.sum() * total
+    new = (1.0 - damping) * counts + damping * target
+    out = np.maximum(1, np.floor(new)).astype(np.int64)
+    # hand the rounding remainder to the fastest shares (largest fraction first)
+    rest = total - int(out.sum())
+    order = np.argsort(-(new - np.floor(new)))
+    k = 0
+    while rest != 0:
+        i = order[k % len(order)]
+        if rest > 0:
+            out[i] += 1
+            rest -= 1
+        elif out[i] > 1:
+            out[i] -= 1
+            rest += 1
+        k += 1
+    return out
 
 
 def develop(rgbaw: np.ndarray) -> np.ndarray:
@@ -856,6 +898,15 @@ class GPUScene:
                     "mtsg_tile_windows")
         return n.value, w.value
 
+    def set_tile_list(self, keys=None) -> None:
+        """Render exactly these deal keys, in this order (mtsg_set_tile_list);
+        None or empty: back to tile_stride / tile_offset."""
+        if keys is None or len(keys) == 0:
+            self._check(device_lib().mtsg_set_tile_list(self._h, None, 0), "mtsg_set_tile_list")
+            return
+        k = np.ascontiguousarray(keys, dtype=np.int32)
+        self._check(device_lib().mtsg_set_tile_list(self._h, _ptr(k), len(k)), "mtsg_set_tile_list")
+
     def render_device_tiles(self, params: RenderParams, windows: C.c_void_p) -> None:
         self._check(device_lib().mtsg_render_device_tiles(self._h, C.byref(params), windows),
                     "mtsg_render_device_tiles")
@@ -902,6 +953,19 @@ class PathJob:
         secs = C.c_double(0.0)
         rc = path_lib().mtsh_path_job_render(self._h, C.byref(params), _ptr(out), C.byref(secs))
         return rc, out, secs.value
+
+    def set_balance(self, on: bool) -> None:
+        """Share balancing between renders of the same tile set (mtsh_path_job_set_balance)."""
+        if path_lib().mtsh_path_job_set_balance(self._h, int(bool(on))) != MTSG_OK:
+            raise RuntimeError(self.last_error())
+
+    def shares(self):
+        """(tiles, seconds) per GPU of the last render (mtsh_path_job_shares)."""
+        t = np.zeros(self.gpus, np.int32)
+        s = np.zeros(self.gpus, np.float64)
+        if path_lib().mtsh_path_job_shares(self._h, _ptr(t), _ptr(s)) != MTSG_OK:
+            raise RuntimeError(self.last_error())
+        return t, s
 
     def last_error(self) -> str:
         return _err(path_lib(), "mtsh_path_last_error")

@@ -10,7 +10,7 @@ import bench
 
 def args(**kw):
     a = dict(workload="bunny15", instancing="flatten", kd_build="host", width=1280, height=720, spp=256,
-             emulate_ranks=0, batch_paths=0, finish_paths=-1)
+             emulate_ranks=0, batch_paths=0, finish_paths=-1, balance_rounds=4)
     a.update(kw)
     return argparse.Namespace(**a)
 

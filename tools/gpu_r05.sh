@@ -39,6 +39,9 @@ for w in ${*:-tests bench}; do
     e8var-*) v=${w#e8var-}; v=${v%@*}; MTSG_LIB=my-mitsuba_amd/var/libmtsg_$v.so step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity --no-count ;;
     e8fin-*) v=${w#e8fin-}; v=${v%@*}; step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity --no-count --finish-paths $v ;;
     e8quick*) step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity --no-count ;;
+    e8nb*) step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity --no-count --balance-rounds 0 ;;
+    e8br-*) v=${w#e8br-}; v=${v%@*}; step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity --no-count --balance-rounds $v ;;
+    tests-c4) step tests-c4 600 $PYT tests/test_gpu_c4.py tests/test_gpu_00_bench_ranks.py ;;
     e8) step e8 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity ;;
     ranks)
       # the launcher path (as the driver runs it) and the self-launching path,
