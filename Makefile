@@ -23,7 +23,7 @@ ORACLE      := oracle/liboracle.so
 ORACLE_FAST := oracle/liboracle_fast.so
 
 .PHONY: all host device oracle clean
-all: host device oracle $(PATH_LIB) $(CLI) scenes/sky512.pfm tools/math_probe tools/math_bench tools/check_glibc_mathf tools/check_env_guide
+all: host device oracle $(PATH_LIB) $(CLI) scenes/sky512.pfm tools/math_probe tools/math_bench tools/div_probe tools/check_glibc_mathf tools/check_env_guide
 host: $(HOST_LIB)
 device: $(DEV_LIB)
 oracle: $(ORACLE) $(ORACLE_FAST)
@@ -81,6 +81,9 @@ $(ORACLE_FAST): oracle/oracle.cpp oracle/oracle.h include/mtsg.h
 # the GPU (math_probe) and on the host (check_glibc_mathf)
 tools/math_probe: tools/math_probe.hip $(PKG)/csrc/glibc_mathf.h
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -ffp-contract=off -o $@ $< -lpthread
+# fast reciprocal / division sequences against the IEEE division, on the GPU
+tools/div_probe: tools/div_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -Wno-unused-result -o $@ $<
 tools/math_bench: tools/math_bench.hip $(PKG)/csrc/glibc_mathf.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -Wno-unused-result -o $@ $<
 tools/check_glibc_mathf: tools/check_glibc_mathf.cpp $(PKG)/csrc/glibc_mathf.h

@@ -50,6 +50,34 @@ DEV float mt_fastlog(float x) { return (float)log((double)x); }
 
 namespace mtsg {
 
+// 1.0f / x, correctly rounded (the IEEE division the oracle and Mitsuba's
+// SSE build compute: dRcp of the kd traversal, kdtree_h / instance.cpp):
+// v_rcp_f32 (1 ulp) and one FMA Newton step give the correctly rounded
+// reciprocal for every x whose exponent field lies in [1, 252] -- tools/
+// div_probe checked all 2^32 bit patterns on the GPU (profiles/
+// r05_div_probe.txt: the 3 x 2^24 that differ are exactly exponent fields 0,
+// 253 and 254, where x or 1/x is denormal or zero) -- and the other
+// exponents take the IEEE division, a branch the wave skips when no lane
+// needs it.  5 VALU instead of the division's ~11.
+#ifndef MTSG_FAST_RCP
+#define MTSG_FAST_RCP 1
+#endif
+DEV float rcp_exact(float x) {
+#if MTSG_FAST_RCP
+    const uint32_t e = (__float_as_uint(x) >> 23) & 0xFFu;
+    float y;
+    if (__builtin_expect(e - 1u < 252u, 1)) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        y = __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+    } else {
+        y = 1.0f / x;
+    }
+    return y;
+#else
+    return 1.0f / x;
+#endif
+}
+
 DEV float3 mk3(float x, float y, float z) { return make_float3(x, y, z); }
 DEV float3 xyz(const float4 &v) { return make_float3(v.x, v.y, v.z); }
 DEV float3 operator+(float3 a, float3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }

@@ -669,7 +669,7 @@ DEV float4 miss_record() {
 DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float rayMaxt, bool shadow, SpecRay &r) {
     r.o = o;
     r.d = d;
-    r.inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.inv = mk3(rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z));
     const uint32_t dneg = (d.x <= 0.0f ? 1u : 0u) | (d.y <= 0.0f ? 2u : 0u) | (d.z <= 0.0f ? 4u : 0u);
     float nearT = -INFINITY, farT = INFINITY;
     bool ok = true;
@@ -986,7 +986,8 @@ DEV void tie_retrace(const DevScene &S, SpecRay &r, SpecStack stk, const float4 
 #define MTSG_SAVE_RAY 1
 #endif
 #ifndef MTSG_SAVE_INV
-#define MTSG_SAVE_INV 0   // variant: the reciprocal direction saved too (no divisions on exit; 2% slower, r03)
+#define MTSG_SAVE_INV 1   // the world reciprocal direction saved too: no divisions on exit (register save:
+                          // free at 80 VGPRs, C3 two-level 1102 -> 1119, r05; global slots: 2% slower, r03)
 #endif
 constexpr int SAVE_VECS = MTSG_SAVE_RAY ? (MTSG_SAVE_INV ? 5 : 4) : 2;
 // MTSG_INST_REGSAVE=1 (the default): the saved top-level state and world ray
@@ -1001,6 +1002,9 @@ struct TopSave {
 #if MTSG_INST_REGSAVE
     uint4 a, b;
     float3 o, d;
+#if MTSG_SAVE_INV
+    float3 inv;   // variant: the world reciprocal kept (no divisions on exit; 3 more VGPRs)
+#endif
 #endif
 };
 // the two levels' stacks in one LDS array: top level in entries
@@ -1052,7 +1056,11 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
     r.bits = b.w | found;
     r.o = ts.o;
     r.d = ts.d;
-    r.inv = mk3(1.0f / ts.d.x, 1.0f / ts.d.y, 1.0f / ts.d.z);
+#if MTSG_SAVE_INV
+    r.inv = ts.inv;
+#else
+    r.inv = mk3(rcp_exact(ts.d.x), rcp_exact(ts.d.y), rcp_exact(ts.d.z));
+#endif
 #else
     const uint4 a = save_vec(S, 0), b = save_vec(S, 1);
     r.cur = make_uint2(a.x, a.y);
@@ -1078,7 +1086,7 @@ DEV void inst_exit(const DevScene &S, SpecRay &r, const float4 *wo, const float4
     const uint4 g = save_vec(S, 4);
     r.inv = mk3(__uint_as_float(e.z), __uint_as_float(e.w), __uint_as_float(g.x));
 #else
-    r.inv = mk3(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
+    r.inv = mk3(rcp_exact(rd.x), rcp_exact(rd.y), rcp_exact(rd.z));
 #endif
 #endif
 }
@@ -1095,7 +1103,7 @@ DEV bool inst_enter(SpecRay &r, TopSave &ts, const DevScene &S, uint32_t ii, flo
                           L2.x * o.x + L2.y * o.y + L2.z * o.z + L2.w);
     const float3 ld = mk3(L0.x * d.x + L0.y * d.y + L0.z * d.z, L1.x * d.x + L1.y * d.y + L1.z * d.z,
                           L2.x * d.x + L2.y * d.y + L2.z * d.z);
-    const float3 li = mk3(1.0f / ld.x, 1.0f / ld.y, 1.0f / ld.z);
+    const float3 li = mk3(rcp_exact(ld.x), rcp_exact(ld.y), rcp_exact(ld.z));
     float nearT = -INFINITY, farT = INFINITY;
     bool ok = true;
     const float bmn[3] = {A0.x, A0.y, A0.z}, bmx[3] = {A1.x, A1.y, A1.z};
@@ -1117,6 +1125,9 @@ DEV bool inst_enter(SpecRay &r, TopSave &ts, const DevScene &S, uint32_t ii, flo
     ts.b = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
     ts.o = o;
     ts.d = d;
+#if MTSG_SAVE_INV
+    ts.inv = r.inv;
+#endif
 #else
     save_vec(S, 0) = make_uint4(r.cur.x, r.cur.y, __float_as_uint(r.tmin), __float_as_uint(r.tmax));
     save_vec(S, 1) = make_uint4(r.lfE, r.lfEnd, __float_as_uint(r.lfTmax), r.bits & ~SB_FOUND);
