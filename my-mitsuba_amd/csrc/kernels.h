@@ -625,10 +625,19 @@ __shared__ float s_specT[SHORT_STACK * TRACE_BLOCK];
 __shared__ uint4 s_top[20];
 #endif
 // every kernel that runs spec_iter stages the top blocks first (variant only)
+#ifndef MTSG_LDS_PAD
+#define MTSG_LDS_PAD 0   // measurement: bytes of unused LDS per traversal workgroup (caps its occupancy)
+#endif
+#if MTSG_LDS_PAD
+__shared__ uint32_t s_ldsPad[MTSG_LDS_PAD / 4];
+#endif
 DEV void lds_top_init(const DevScene &S) {
 #if MTSG_LDS_TOP
     if (threadIdx.x < 20u) s_top[threadIdx.x] = S.blocks[threadIdx.x];
     __syncthreads();
+#endif
+#if MTSG_LDS_PAD
+    if (threadIdx.x == 0) ((volatile uint32_t *)s_ldsPad)[(S.n_tri & 0xFFFFu) % (MTSG_LDS_PAD / 4)] = 0u;
 #endif
 }
 // lane index, recomputed where it is used (volatile: not hoisted out of loops)
