@@ -3417,8 +3417,12 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
             for (int h = 0; h < CH; ++h) acc[h][o] += win[r][c][h];
             __syncthreads();
         }
-    // flush into the HBM block (blockW x blockH x 5, origin = rect - border)
-    for (int k = threadIdx.x; k < LT * LT; k += BLOCK) {
+    // flush into the HBM block (blockW x blockH x 5, origin = rect - border):
+    // one float per lane, so the lanes of a wave add to consecutive floats of
+    // a texel row (4-5 64-B atomic requests per wave instruction, where one
+    // texel per lane with its 5 channels strided 20 B apart touched ~20)
+    for (int j = threadIdx.x; j < LT * LT * 5; j += BLOCK) {
+        const int k = j / 5, h = j - 5 * k;
         const int ty2 = k / LT, tx2 = k % LT;
         const int fx = x0 - MAX_BORDER + tx2 - (B.rect_x - bord), fy = y0 - MAX_BORDER + ty2 - (B.rect_y - bord);
         if (fx < 0 || fy < 0 || fx >= blockW || fy >= blockH) continue;
@@ -3428,11 +3432,9 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
         const int wx = tx2 - (MAX_BORDER - bord), wy = ty2 - (MAX_BORDER - bord);
         if (winSz && (wx < 0 || wy < 0 || wx >= winSz || wy >= winSz)) continue;
         float *dst = winSz ? film + (((size_t)(B.tile0 + tl) * winSz + wy) * winSz + wx) * 5 : film + ((size_t)fy * blockW + fx) * 5;
-        unsafeAtomicAdd(dst + 0, acc[0][k]);
-        unsafeAtomicAdd(dst + 1, acc[1][k]);
-        unsafeAtomicAdd(dst + 2, acc[2][k]);
-        unsafeAtomicAdd(dst + 3, CH == 5 ? acc[3][k] : w);   // no alpha channel: alpha == 1 per sample
-        unsafeAtomicAdd(dst + 4, w);
+        // no alpha channel (CH == 4): alpha == 1 per sample, so its sum is the weight
+        const float v = h < 3 ? acc[h][k] : (h == 3 && CH == 5 ? acc[CH == 5 ? 3 : 0][k] : w);
+        unsafeAtomicAdd(dst + h, v);
     }
 }
 
