@@ -790,6 +790,19 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 #ifndef MTSG_RECT_PEND_I
 #define MTSG_RECT_PEND_I 0
 #endif
+// batched instance entry and exit (two-level, spec_iter_i), measured r05 on
+// C3 two-level: entry when >= 1/2, 1/4, 1/8, 1/16 of the busy lanes pend:
+// 1064 / 1153 / 1157-1160 / 1143 vs 1119-1123 unbatched; exit batching on top
+// of entry at 1/8: 1070-1085 (the exit block is cheap, the waits are not)
+#ifndef MTSG_ENTER_BATCH
+#define MTSG_ENTER_BATCH 8
+#endif
+#ifndef MTSG_INST_MIN_IDLE
+#define MTSG_INST_MIN_IDLE 16   // two-level traversal: idle lanes that trigger a refill (flat: 16)
+#endif
+#ifndef MTSG_EXIT_BATCH
+#define MTSG_EXIT_BATCH 0
+#endif
 #ifndef MTSG_MAILBOX
 #define MTSG_MAILBOX 1   // 0: measurement variant, the last primitive tested wins a tie
 #endif
@@ -1020,7 +1033,8 @@ struct TopSave {
 // [0, OUTER_STACK), group level in [OUTER_STACK, OUTER_STACK + INNER_STACK)
 __shared__ uint2 s_lvNode[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
 __shared__ float s_lvT[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
-enum : uint32_t { SB_INST = 1u << 22, SB_PEND = 1u << 24 };   // inside an instance; entering one next iteration
+enum : uint32_t { SB_INST = 1u << 22, SB_PEND = 1u << 24, SB_XPEND = 1u << 26 };   // inside an instance; entering one next
+                                                                                  // iteration; leaving it (MTSG_EXIT_BATCH)
 
 DEV uint4 &save_vec(const DevScene &S, uint32_t k) {
     return S.instSave[(size_t)k * (gridDim.x * TRACE_BLOCK) + blockIdx.x * TRACE_BLOCK + lane_here()];
@@ -1176,7 +1190,35 @@ template <bool COUNT>
 DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevPaths &P, uint32_t idx, const TravLimits &L,
                      uint32_t &inst, TopSave &ts) {
     const uint2 n = r.cur;
+#if MTSG_EXIT_BATCH
+    // batched exit (as the batched entry): a lane whose group traversal ended
+    // waits until 1/MTSG_EXIT_BATCH of the busy lanes have, then all of them
+    // restore their top-level state together
+    {
+        const bool xp = (r.bits & SB_XPEND) != 0;
+        const uint32_t nX = (uint32_t)__popcll(__ballot(xp)), nAll = (uint32_t)__popcll(__ballot(1));
+        if (xp) {
+            if (nX * MTSG_EXIT_BATCH >= nAll) {
+                const bool sh = (r.bits & SB_SHADOW) != 0;
+                inst_exit(S, r, (sh ? P.sh_o : P.ray_o) + idx, (sh ? P.sh_d : P.ray_d) + idx, ts);
+            }
+            return false;
+        }
+    }
+#endif
     const bool pend = (r.bits & SB_PEND) != 0;
+#if MTSG_ENTER_BATCH
+    // batched entry: pending lanes wait until at least 1/MTSG_ENTER_BATCH of
+    // the wave's busy lanes are pending (always true once no other lane is
+    // busy), so the entry block (transform, clip, reciprocals, state save:
+    // ~110 VALU that the wave issues whenever any lane enters) runs for
+    // several lanes at once; a waiting lane fetches a cached dummy and changes
+    // nothing, so every lane takes the same steps as unbatched
+    const uint32_t nPend = (uint32_t)__popcll(__ballot(pend)), nBusy = (uint32_t)__popcll(__ballot(1));
+    const bool waiting = pend && !(nPend * MTSG_ENTER_BATCH >= nBusy);
+#else
+    constexpr bool waiting = false;
+#endif
     const bool inner = !pend && !(r.bits & SB_TRAVDONE) && !(n.x & 0x80000000u);
     const bool prim = !pend && r.lfE < r.lfEnd;
     const bool rootKind = inner && !(n.x & 4u);
@@ -1188,21 +1230,22 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     const uint32_t pi = prim ? r.lfE : 0u;
     // a pending entry reads the instance record through the same slots
     const float4 *irec = S.inst + 8 * (size_t)inst;
-    const uint4 *a0 = pend ? reinterpret_cast<const uint4 *>(irec + 6) : S.blocks + base;
-    const uint4 *a1 = pend ? reinterpret_cast<const uint4 *>(irec + 7) : S.blocks + base + off;
+    const uint4 *a0 = pend && !waiting ? reinterpret_cast<const uint4 *>(irec + 6) : S.blocks + base;
+    const uint4 *a1 = pend && !waiting ? reinterpret_cast<const uint4 *>(irec + 7) : S.blocks + base + off;
 #if MTSG_RECT_PEND_I
     // a top-level rectangle is tested in the lane's next iteration (its index
     // waits in `inst`, unused at the top level: groups hold no rectangles)
     const bool rp = (r.bits & SB_RPEND) != 0;
     const float4 *rec = pend ? irec : (rp ? S.rectM + (size_t)(3u * inst) : S.triL + (size_t)(3u * pi));
 #else
-    const float4 *rec = pend ? irec : S.triL + (size_t)(3u * pi);
+    const float4 *rec = pend && !waiting ? irec : S.triL + (size_t)(3u * pi);
 #endif
     const uint4 p0 = *a0, pc = *a1;
     const float4 f0 = rec[0], f1 = rec[1], f2 = rec[2];
     asm volatile("" ::"v"(p0.x), "v"(p0.y), "v"(p0.z), "v"(p0.w), "v"(pc.x), "v"(pc.y), "v"(pc.z), "v"(pc.w),
                  "v"(f0.x), "v"(f0.y), "v"(f0.z), "v"(f0.w),
                  "v"(f1.x), "v"(f1.y), "v"(f1.z), "v"(f1.w), "v"(f2.x), "v"(f2.y), "v"(f2.z), "v"(f2.w));
+    if (waiting) return false;
     if (pend) {
         r.bits &= ~SB_PEND;
         if (COUNT) cnt.inst++;
@@ -1318,8 +1361,12 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
     }
     const bool done = leave || ((r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f);
     if (done && inInst) {
+#if MTSG_EXIT_BATCH
+        r.bits |= SB_XPEND;
+#else
         const bool sh = (r.bits & SB_SHADOW) != 0;
         inst_exit(S, r, (sh ? P.sh_o : P.ray_o) + idx, (sh ? P.sh_d : P.ray_d) + idx, ts);
+#endif
         return false;
     }
     return done;

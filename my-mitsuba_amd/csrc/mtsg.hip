@@ -202,8 +202,8 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t
     // the KNOBS instantiations read the stack caps and restart limits the
     // scene was created with (test overrides); the COUNT pass ignores them
     if (s->ds.inst && s->knobs && !COUNT)
-        hipLaunchKernelGGL((k_trace_s<false, 16, true, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
-    else if (s->ds.inst) hipLaunchKernelGGL((k_trace_s<COUNT, 16, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+        hipLaunchKernelGGL((k_trace_s<false, MTSG_INST_MIN_IDLE, true, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    else if (s->ds.inst) hipLaunchKernelGGL((k_trace_s<COUNT, MTSG_INST_MIN_IDLE, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else if (s->knobs && !COUNT) hipLaunchKernelGGL((k_trace_s<false, 16, false, true>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
@@ -1171,7 +1171,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         perCU = 8;
     s->traceGrid = s->cuCount * perCU;
     perCU = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace_s<false, 16, true>, TRACE_BLOCK, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace_s<false, MTSG_INST_MIN_IDLE, true>, TRACE_BLOCK, 0) != hipSuccess ||
         perCU <= 0)
         perCU = 4;
     s->traceGridInst = s->cuCount * perCU;
