@@ -3117,6 +3117,9 @@ __global__ void __launch_bounds__(SHADE_BLOCK) k_shade_om(DevScene S, DevIntegra
 #define MTSG_SHADE_LDS 1   // BSDF / emitter tables staged in LDS when they fit (k_shade): +1.4% on C3
 #endif
 constexpr int SHADE_LDS_BSDFS = 4, SHADE_LDS_EMITTERS = 16;
+#ifndef MTSG_SHADE_LDS_PAD
+#define MTSG_SHADE_LDS_PAD 0
+#endif
 #ifndef MTSG_SHADE_WAVES
 #define MTSG_SHADE_WAVES 4   // 127 VGPRs: 4 waves/SIMD (3 at 144; 5+ spill heavily)
 #endif
@@ -3133,6 +3136,11 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
     __shared__ ShadeStage stage;
+#if MTSG_SHADE_LDS_PAD
+    // measurement: unused LDS that caps the workgroups per CU
+    __shared__ uint32_t s_shadePad[MTSG_SHADE_LDS_PAD / 4];
+    if (threadIdx.x == 0) ((volatile uint32_t *)s_shadePad)[(S.n_tri & 0xFFFFu) % (MTSG_SHADE_LDS_PAD / 4)] = 0u;
+#endif
 #if MTSG_SHADE_LDS
     __shared__ mtsg_bsdf s_bsdfs[SHADE_LDS_BSDFS];
     __shared__ mtsg_emitter s_emitters[SHADE_LDS_EMITTERS];
