@@ -5,8 +5,9 @@
  * Replaces SamplingIntegrator::render (reference src/librender/integrator.cpp:99-133)
  * together with BlockedRenderProcess (src/librender/renderproc.cpp:26-186):
  * instead of 32x32 blocks handed to CPU workers, the film's 16x16 tiles are
- * dealt round-robin by deal key (include/mtsg.h, tile_stride) to one host
- * thread per GPU (key k -> GPU k % N), each
+ * shared over one host thread per GPU -- each GPU takes a run of the tiles'
+ * deal keys in golden-ratio order (mtsg_set_tile_list), re-cut from the GPUs'
+ * measured rates between renders (mtsh_path_job_render) -- each
  * GPU renders its tiles into an ImageBlock of the full rectangle plus filter
  * border, and the blocks are merged by addition as ImageBlock::put(const
  * ImageBlock *) does (include/mitsuba/render/imageblock.h:103-107).  No
