@@ -53,12 +53,11 @@ namespace mtsg {
 // 1.0f / x, correctly rounded (the IEEE division the oracle and Mitsuba's
 // SSE build compute: dRcp of the kd traversal, kdtree_h / instance.cpp):
 // v_rcp_f32 (1 ulp) and one FMA Newton step give the correctly rounded
-// reciprocal for every x whose exponent field lies in [1, 252] -- tools/
-// div_probe checked all 2^32 bit patterns on the GPU (profiles/
-// r05_div_probe.txt: the 3 x 2^24 that differ are exactly exponent fields 0,
-// 253 and 254, where x or 1/x is denormal or zero) -- and the other
-// exponents take the IEEE division, a branch the wave skips when no lane
-// needs it.  5 VALU instead of the division's ~11.
+// reciprocal for every x whose exponent field lies in [1, 252], and the other
+// exponents (x or 1/x denormal or zero, inf, NaN) take the IEEE division, a
+// branch the wave skips when no lane needs it -- tools/div_probe compared this
+// function's sequence with 1.0f / x on all 2^32 bit patterns on the GPU: 0
+// differ (profiles/r05_div_probe.txt).  5 VALU instead of the division's ~11.
 #ifndef MTSG_FAST_RCP
 #define MTSG_FAST_RCP 1
 #endif

@@ -30,6 +30,19 @@ __device__ inline float rcp_nr2(float x) {
     const float e = __builtin_fmaf(-x, y, 1.0f);
     return __builtin_fmaf(e, y, y);
 }
+// the kernels' guarded form (my-mitsuba_amd/csrc/device_math.h rcp_exact):
+// the Newton reciprocal for exponent fields 1..252, else the IEEE division
+__device__ inline float rcp_guarded(float x) {
+    const uint32_t e = (asu(x) >> 23) & 0xFFu;
+    float y;
+    if (__builtin_expect(e - 1u < 252u, 1)) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        y = __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+    } else {
+        y = 1.0f / x;
+    }
+    return y;
+}
 // a / b: the Newton reciprocal, a quotient and one Markstein correction
 __device__ inline float div_m1(float a, float b) {
     const float y = rcp_nr1(b);
@@ -66,8 +79,12 @@ __device__ inline float range_from(uint32_t u, int lo, int hi) {
     return asf((u & 0x80000000u) | (e << 23) | (hash32(u) & 0x7fffffu));
 }
 
-enum { NV = 6, KEEP = 8 };
-// variants: 0 rcp_nr1, 1 rcp_nr2 (all x); 2 div_m1 any, 3 div_m2 any, 4 div_m1 tri, 5 div_m2 tri
+enum { NV = 7, KEEP = 8 };
+// rcp_nr1 mismatches per exponent field of x (all 2^32 x): which inputs the
+// kernels' guard (device_math.h rcp_exact) must send to the IEEE division
+__device__ unsigned long long g_rcpByExp[256];
+// variants: 0 rcp_nr1, 1 rcp_nr2 (all x); 2 div_m1 any, 3 div_m2 any, 4 div_m1 tri, 5 div_m2 tri;
+// 6 rcp_guarded (all x)
 __global__ void k_probe(uint64_t base, uint32_t n, unsigned long long *cnt, float *keep) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -77,9 +94,11 @@ __global__ void k_probe(uint64_t base, uint32_t n, unsigned long long *cnt, floa
     {
         const float x = asf(u), ref = 1.0f / x;
         bad[0] = !same(rcp_nr1(x), ref);
+        if (bad[0]) atomicAdd(&g_rcpByExp[(u >> 23) & 0xFFu], 1ull);
         bad[1] = !same(rcp_nr2(x), ref);
-        a1[0] = a1[1] = 1.0f;
-        b1[0] = b1[1] = x;
+        bad[6] = !same(rcp_guarded(x), ref);
+        a1[0] = a1[1] = a1[6] = 1.0f;
+        b1[0] = b1[1] = b1[6] = x;
     }
     {
         const float a = finite_from(hash32(u * 2u + 1u)), b = finite_from(hash32(u * 2u + 2u) ^ 0x5bd1e995u);
@@ -124,8 +143,14 @@ int main(int argc, char **argv) {
     unsigned long long c[NV];
     float k[NV * KEEP * 2];
     if (hipMemcpy(c, dc, sizeof(c), hipMemcpyDeviceToHost) || hipMemcpy(k, dk, sizeof(k), hipMemcpyDeviceToHost)) return 2;
+    unsigned long long byExp[256];
+    if (hipMemcpyFromSymbol(byExp, HIP_SYMBOL(g_rcpByExp), sizeof(byExp))) return 2;
+    printf("rcp_nr1 mismatches by exponent field of x:");
+    for (int e = 0; e < 256; ++e)
+        if (byExp[e]) printf(" [%d] %llu", e, byExp[e]);
+    printf("\n");
     static const char *name[NV] = {"rcp_nr1 (all 2^32 x)", "rcp_nr2 (all 2^32 x)", "div_m1 any", "div_m2 any",
-                                   "div_m1 tri", "div_m2 tri"};
+                                   "div_m1 tri", "div_m2 tri", "rcp_exact (all 2^32 x)"};
     for (int v = 0; v < NV; ++v) {
         printf("%-22s %llu of %llu differ", name[v], c[v], (unsigned long long)total);
         for (unsigned long long j = 0; j < c[v] && j < KEEP; ++j)
