@@ -660,6 +660,12 @@ def main():
                     "iterations_per_ray": round(per(cs.wave_active_lanes, cs.rays_closest + cs.rays_shadow), 2),
                     "instance_visits_per_ray": round(per(cs.instance_visits + cs.shadow_instance_visits,
                                                          cs.rays_closest + cs.rays_shadow), 3),
+                    # entries whose group-box clip left an empty interval
+                    "instance_entries_rejected": round(per(cs.instance_rejects,
+                                                           cs.instance_visits + cs.shadow_instance_visits), 3),
+                    # instance primitives the world-box prefilter skipped, per ray
+                    "instance_prefiltered_per_ray": round(per(cs.instance_prefiltered,
+                                                              cs.rays_closest + cs.rays_shadow), 3),
                     # the exactness paths (flattened traversal): exact-tie
                     # retraces with the mailbox (k_tie) and the restart
                     # guard's one-ulp steps, in the instrumented pass and

@@ -482,6 +482,13 @@ typedef struct mtsg_stats {
     uint64_t tie_retraces;
     uint64_t guard_rays_closest, guard_rays_shadow, guard_steps_closest, guard_steps_shadow;
     uint64_t restarts_closest, restarts_shadow;
+    /* two-level (MTSG_FLAG_COUNT): instance entries whose group-box clip
+     * left an empty interval (closest and shadow rays; of instance_visits +
+     * shadow_instance_visits)                                              */
+    uint64_t instance_rejects;
+    /* ... and instance primitives the world-box prefilter skipped before any
+     * entry (not counted in instance_visits)                                */
+    uint64_t instance_prefiltered;
 } mtsg_stats;
 
 enum {

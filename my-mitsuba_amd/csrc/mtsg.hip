@@ -702,6 +702,8 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
         s->stragglers.assign(c + 64, c + 64 + 8 * std::min<unsigned long long>(c[48], STRAGGLER_MAX));
         s->stats.instance_visits = c[49];
         s->stats.shadow_instance_visits = c[50];
+        s->stats.instance_rejects = c[58];
+        s->stats.instance_prefiltered = c[59];
         s->stats.tie_retraces = c[51];
         s->stats.guard_rays_closest = c[52];
         s->stats.guard_rays_shadow = c[53];
@@ -826,6 +828,43 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
                     d->shapes[ta.shape_index].type == MTSG_SHAPE_INSTANCE) {
                     if (ta.prim_index >= d->n_instances) { layoutOk = false; break; }
                     ta.k = KINST;
+                    // the instance's world box in the record's free words
+                    // (n_u n_v n_d = min, a_u a_v b_nu = max): the group box's
+                    // corners through to_world in double, widened by 1e-4 of
+                    // its size and position and rounded outward, so the
+                    // traversal's prefilter (kernels.h inst_box) never drops an
+                    // entry the exact group-space clip would take
+                    const mtsg_instance &I = d->instances[ta.prim_index];
+                    if (I.group >= d->n_groups) { layoutOk = false; break; }
+                    const mtsg_group &G = d->groups[I.group];
+                    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                    for (int c = 0; c < 8; ++c) {
+                        const double q[3] = {(c & 1) ? G.aabb_max[0] : G.aabb_min[0], (c & 2) ? G.aabb_max[1] : G.aabb_min[1],
+                                             (c & 4) ? G.aabb_max[2] : G.aabb_min[2]};
+                        for (int a = 0; a < 3; ++a) {
+                            const float *W = I.to_world + 4 * a;
+                            const double w = (double)W[0] * q[0] + (double)W[1] * q[1] + (double)W[2] * q[2] + (double)W[3];
+                            lo[a] = std::min(lo[a], w);
+                            hi[a] = std::max(hi[a], w);
+                        }
+                    }
+                    double ext = 0, mag = 0;
+                    for (int a = 0; a < 3; ++a) {
+                        ext = std::max(ext, hi[a] - lo[a]);
+                        mag = std::max(mag, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
+                    }
+                    const double m = 1e-4 * (ext + mag) + 1e-30;
+                    float bmin[3], bmax[3];
+                    for (int a = 0; a < 3; ++a) {
+                        bmin[a] = std::nextafter((float)(lo[a] - m), -INFINITY);
+                        bmax[a] = std::nextafter((float)(hi[a] + m), INFINITY);
+                    }
+                    if (!std::isfinite(bmin[0] + bmin[1] + bmin[2] + bmax[0] + bmax[1] + bmax[2])) {
+                        // a degenerate or unbounded transform: a box that takes every ray
+                        for (int a = 0; a < 3; ++a) { bmin[a] = -INFINITY; bmax[a] = INFINITY; }
+                    }
+                    ta.n_u = bmin[0]; ta.n_v = bmin[1]; ta.n_d = bmin[2];
+                    ta.a_u = bmax[0]; ta.a_v = bmax[1]; ta.b_nu = bmax[2];
                 }
                 // the TriAccel index (Mitsuba's mailbox key, kernels.h
                 // mailbox_step) in place of the shape index

@@ -78,6 +78,7 @@ class Stats(C.Structure):
         ("tie_retraces", C.c_uint64), ("guard_rays_closest", C.c_uint64), ("guard_rays_shadow", C.c_uint64),
         ("guard_steps_closest", C.c_uint64), ("guard_steps_shadow", C.c_uint64),
         ("restarts_closest", C.c_uint64), ("restarts_shadow", C.c_uint64),
+        ("instance_rejects", C.c_uint64), ("instance_prefiltered", C.c_uint64),
     ]
 
 
