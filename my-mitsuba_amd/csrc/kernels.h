@@ -1184,26 +1184,25 @@ DEV bool inst_enter(SpecRay &r, TopSave &ts, const DevScene &S, uint32_t ii, flo
 // two-level left an empty group-space clip (round 5, stats.instance_rejects);
 // rejected here, they cost neither the pending iteration nor the entry block.
 // Conservative: a ray this test rejects misses the widened box, so the exact
-// clip of inst_enter would reject it as well; parallel axes test the origin.
+// clip of inst_enter would reject it as well.  An axis the ray runs parallel
+// to (inv = +-inf) needs no branch: inside the slab it gives (-inf, inf),
+// outside it an empty interval, and exactly on a face (0 * inf = NaN, which
+// fminf / fmaxf pass over) a rejection -- of a ray that lies the margin
+// outside the group box, which the exact clip rejects too.
 #ifndef MTSG_INST_PREFILTER
 #define MTSG_INST_PREFILTER 1
 #endif
 DEV bool inst_box(const SpecRay &r, float4 f0, float4 f1) {
     float t0 = r.mint, t1 = r.best;
-    bool ok = true;
     const float bmn[3] = {f0.y, f0.z, f0.w}, bmx[3] = {f1.x, f1.y, f1.z};
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        const float oa = comp(r.o, a), da = comp(r.d, a), ia = comp(r.inv, a);
-        if (da == 0.0f) {
-            ok &= (oa >= bmn[a]) & (oa <= bmx[a]);
-        } else {
-            const float u = (bmn[a] - oa) * ia, v = (bmx[a] - oa) * ia;
-            t0 = fmaxf(t0, fminf(u, v));
-            t1 = fminf(t1, fmaxf(u, v));
-        }
+        const float oa = comp(r.o, a), ia = comp(r.inv, a);
+        const float u = (bmn[a] - oa) * ia, v = (bmx[a] - oa) * ia;
+        t0 = fmaxf(t0, fminf(u, v));
+        t1 = fminf(t1, fmaxf(u, v));
     }
-    return ok & (t0 <= t1);
+    return t0 <= t1;
 }
 
 // One iteration of the two-level traversal.  An instance primitive met in a
