@@ -684,14 +684,13 @@ DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float r
     bool ok = true;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
+        // the two cases of aabb.h:308-338 as selects (no exec-mask branches)
         const float oi = comp(o, i), di = comp(d, i), ii = comp(r.inv, i);
-        if (di == 0.0f) {
-            if (oi < S.bmin[i] || oi > S.bmax[i]) ok = false;
-        } else {
-            const float t1 = (S.bmin[i] - oi) * ii, t2 = (S.bmax[i] - oi) * ii;
-            nearT = fmaxf(fminf(t1, t2), nearT);
-            farT = fminf(fmaxf(t1, t2), farT);
-        }
+        const bool par = di == 0.0f;
+        const float t1 = (S.bmin[i] - oi) * ii, t2 = (S.bmax[i] - oi) * ii;
+        nearT = par ? nearT : fmaxf(fminf(t1, t2), nearT);
+        farT = par ? farT : fminf(fmaxf(t1, t2), farT);
+        ok &= !par | ((oi >= S.bmin[i]) & (oi <= S.bmax[i]));
     }
     if (!ok || !(nearT <= farT)) return false;
     float rayMinT = rayMint;
@@ -1132,14 +1131,13 @@ DEV bool inst_enter(SpecRay &r, TopSave &ts, const DevScene &S, uint32_t ii, flo
     const float bmn[3] = {A0.x, A0.y, A0.z}, bmx[3] = {A1.x, A1.y, A1.z};
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
+        // (as spec_init: the two cases as selects)
         const float oi = comp(lo, i), di = comp(ld, i), iv = comp(li, i);
-        if (di == 0.0f) {
-            if (oi < bmn[i] || oi > bmx[i]) ok = false;
-        } else {
-            const float t1 = (bmn[i] - oi) * iv, t2 = (bmx[i] - oi) * iv;
-            nearT = fmaxf(fminf(t1, t2), nearT);
-            farT = fminf(fmaxf(t1, t2), farT);
-        }
+        const bool par = di == 0.0f;
+        const float t1 = (bmn[i] - oi) * iv, t2 = (bmx[i] - oi) * iv;
+        nearT = par ? nearT : fmaxf(fminf(t1, t2), nearT);
+        farT = par ? farT : fminf(fmaxf(t1, t2), farT);
+        ok &= !par | ((oi >= bmn[i]) & (oi <= bmx[i]));
     }
     const float t0 = fmaxf(r.mint, nearT), t1 = fminf(r.best, farT);
     if (!(ok & (nearT <= farT) & (t1 > t0))) return false;
