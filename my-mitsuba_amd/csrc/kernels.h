@@ -390,11 +390,14 @@ DEV bool rect_test_m(const float *m, float3 wo, float3 wd, float mint, float max
                    m[8] * wo.x + m[9] * wo.y + m[10] * wo.z + m[11]);
     float3 d = mk3(m[0] * wd.x + m[1] * wd.y + m[2] * wd.z, m[4] * wd.x + m[5] * wd.y + m[6] * wd.z,
                    m[8] * wd.x + m[9] * wd.y + m[10] * wd.z);
-    float hit = -o.z / d.z;
-    if (!(hit >= mint && hit <= maxt)) return false;
-    float x = o.x + d.x * hit, y = o.y + d.y * hit;
-    if (fabsf(x) <= 1 && fabsf(y) <= 1) { t = hit; lx = x; ly = y; return true; }
-    return false;
+    // Rectangle::rayIntersect's early returns as one condition (no exec-mask
+    // branches); t / lx / ly are written either way and read only on a hit
+    const float hit = -o.z / d.z;
+    const float x = o.x + d.x * hit, y = o.y + d.y * hit;
+    t = hit;
+    lx = x;
+    ly = y;
+    return (hit >= mint) & (hit <= maxt) & (fabsf(x) <= 1.0f) & (fabsf(y) <= 1.0f);
 }
 DEV bool rect_test(const mtsg_rect &r, float3 wo, float3 wd, float mint, float maxt, float &t, float &lx, float &ly) {
     return rect_test_m(r.to_object, wo, wd, mint, maxt, t, lx, ly);
@@ -693,12 +696,10 @@ DEV bool spec_init(const DevScene &S, float3 o, float3 d, float rayMint, float r
         ok &= !par | ((oi >= S.bmin[i]) & (oi <= S.bmax[i]));
     }
     if (!ok || !(nearT <= farT)) return false;
-    float rayMinT = rayMint;
-    if (rayMinT == kEpsilon) {
-        float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-        if (!shadow) m = fmaxf(m, kEpsilon);
-        rayMinT *= m;
-    }
+    // the adaptive epsilon as a select (skdtree.cpp:112-142 / 207-226)
+    float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    if (!shadow) m = fmaxf(m, kEpsilon);
+    const float rayMinT = rayMint == kEpsilon ? rayMint * m : rayMint;
     r.mint = fmaxf(nearT, rayMinT);
     r.best = fminf(farT, rayMaxt);
     if (!(r.best > r.mint)) return false;
