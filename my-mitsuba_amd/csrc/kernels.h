@@ -599,6 +599,16 @@ DEV void kd_restart(const TravLimits &L, SpecRay &r, uint32_t b, uint2 root, uin
     const bool restart = (b & SB_DROPPED) != 0;
     float t0 = r.tmax;
     uint32_t nb = b & ~SB_STACK;
+#if MTSG_POPSEL
+    // selects, no exec-mask branches
+    const uint32_t nr = (b >> SB_RST_SHIFT) & SB_RST_MASK;
+    const bool limit = nr >= ((b & SB_SHADOW) ? L.rstMax : L.rstMaxC);   // the limit (the counter saturates)
+    nb = restart ? (limit ? (nb | SB_ERR | SB_TRAVDONE) : nb + SB_RST1) : nb;
+    // the guard: nextafterf(t0, +inf) for finite t0, in integer arithmetic
+    const uint32_t u = __float_as_uint(t0);
+    const float tg = __uint_as_float(t0 >= 0.0f ? (u & 0x7FFFFFFFu) + 1u : u - 1u);
+    t0 = (restart & (nr >= L.rstGuard)) ? tg : t0;
+#else
     if (restart) {   // lanes that restart (the others finish their ray here)
         const uint32_t nr = (b >> SB_RST_SHIFT) & SB_RST_MASK;
         if (nr >= ((b & SB_SHADOW) ? L.rstMax : L.rstMaxC)) nb |= SB_ERR | SB_TRAVDONE;   // the limit (the counter saturates)
@@ -609,6 +619,7 @@ DEV void kd_restart(const TravLimits &L, SpecRay &r, uint32_t b, uint2 root, uin
             t0 = __uint_as_float(t0 >= 0.0f ? (u & 0x7FFFFFFFu) + 1u : u - 1u);
         }
     }
+#endif
     r.tmin = restart ? t0 : r.tmin;
     r.tmax = restart ? r.best : r.tmax;
     r.cur = restart ? root : c;
@@ -797,6 +808,9 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 #ifndef MTSG_ENTER_BATCH
 #define MTSG_ENTER_BATCH 8
 #endif
+#ifndef MTSG_POPSEL
+#define MTSG_POPSEL 0   // measurement: stack pop / kd-restart as selects in the flat traversal
+#endif
 #ifndef MTSG_INST_MIN_IDLE
 #define MTSG_INST_MIN_IDLE 16   // two-level traversal: idle lanes that trigger a refill (flat: 16)
 #endif
@@ -948,6 +962,26 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
         r.lfEnd = nonEmpty ? c.y : r.lfEnd;
         r.lfTmax = nonEmpty ? r.tmax : r.lfTmax;
         const uint32_t b = r.bits;
+#if MTSG_POPSEL
+        // pop the stack, or (empty) finish or kd-restart behind this leaf if
+        // entries were dropped: both computed, one selected (the stack read
+        // of an empty stack is a stale entry, not used)
+        const bool hasN = (b & SB_N) != 0;
+        const uint32_t top = b & SB_TOP, k = top == 0 ? L.capFlat - 1 : top - 1u;
+        const uint2 pn = stk.node(k);
+        const float pt = stk.t(k);
+        SpecRay rr = r;
+        if (COUNT && !hasN && (b & SB_DROPPED)) cnt.restarts++;
+#if MTSG_PUSHDOWN
+        kd_restart(L, rr, b, r.rroot, c);
+#else
+        kd_restart(L, rr, b, S.root2, c);
+#endif
+        r.cur = hasN ? pn : rr.cur;
+        r.bits = hasN ? ((b & ~SB_TOP) | k) - SB_N1 : rr.bits;
+        r.tmin = hasN ? r.tmax : rr.tmin;
+        r.tmax = hasN ? fminf(pt, r.best) : rr.tmax;
+#else
         if (b & SB_N) {
             const uint32_t top = b & SB_TOP, k = top == 0 ? L.capFlat - 1 : top - 1u;
             r.cur = stk.node(k);
@@ -964,6 +998,7 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
             kd_restart(L, r, b, S.root2, c);
 #endif
         }
+#endif
     }
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
 }
