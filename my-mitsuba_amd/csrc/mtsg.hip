@@ -1214,7 +1214,10 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         perCU <= 0)
         perCU = 4;
     s->traceGridInst = s->cuCount * perCU;
-    s->shadeGrid = s->cuCount * 8 * 256 / SHADE_BLOCK;
+#ifndef MTSG_SHADE_WG_PER_CU
+#define MTSG_SHADE_WG_PER_CU 8   // k_shade workgroups of 256 per CU (grid-stride; 4 are resident)
+#endif
+    s->shadeGrid = s->cuCount * MTSG_SHADE_WG_PER_CU * 256 / SHADE_BLOCK;
     perCU = 0;
     if ((perCU = finish_blocks_per_cu()) <= 0) perCU = 4;
     s->finishGrid = s->cuCount * perCU;
