@@ -1215,7 +1215,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         perCU = 4;
     s->traceGridInst = s->cuCount * perCU;
 #ifndef MTSG_SHADE_WG_PER_CU
-#define MTSG_SHADE_WG_PER_CU 8   // k_shade workgroups of 256 per CU (grid-stride; 4 are resident)
+#define MTSG_SHADE_WG_PER_CU 64   // k_shade workgroups of 256 per CU, 4 resident (r05_shade_launch.txt: 8 -> 64, C3 shade -5%)
 #endif
     s->shadeGrid = s->cuCount * MTSG_SHADE_WG_PER_CU * 256 / SHADE_BLOCK;
     perCU = 0;
