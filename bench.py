@@ -116,6 +116,8 @@ def parse():
     ap.add_argument("--no-count", action="store_true",
                     help="skip the instrumented (untimed) pass of per-ray counts (profiler runs)")
     ap.add_argument("--print-pmc-key", action="store_true", help="print this configuration's PMC key and exit")
+    ap.add_argument("--shade-generic", action="store_true",
+                    help="shade with the all-materials kernel instead of the scene's material set (A/B measurement)")
     return ap.parse_args()
 
 
@@ -426,6 +428,8 @@ def main():
         gpu.set_batch_paths(max(1 << 20, (1 << 29) // sharing))
     if a.finish_paths >= 0:
         gpu.set_finish_paths(a.finish_paths)
+    if a.shade_generic:
+        gpu.set_option(mtsg.MTSG_OPT_SHADE_GENERIC, 1)
     W, H = params.tile_w + 2 * border, params.tile_h + 2 * border
     nbytes = W * H * 5 * 4
     film = gpu.alloc(nbytes)

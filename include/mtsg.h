@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define MTSG_ABI_VERSION 7
+#define MTSG_ABI_VERSION 8
 
 /* ---- error codes (mtsg_last_error() gives the message) ------------------ */
 enum {
@@ -613,9 +613,31 @@ int  mtsg_set_batch_paths(mtsg_scene *scene, uint32_t paths);
  * persistent launch carries them through all their remaining bounces
  * instead of a trace + shade launch per bounce (same arithmetic in the same
  * order: the image is unchanged).  0 turns it off; the default is
- * MTSG_DEFAULT_FINISH_PATHS (environment override MTSG_FINISH).            */
+ * MTSG_DEFAULT_FINISH_PATHS.                                              */
 #define MTSG_DEFAULT_FINISH_PATHS 524288u
 int  mtsg_set_finish_paths(mtsg_scene *scene, uint32_t paths);
+
+/* Execution options of a handle, set explicitly by the caller (no library
+ * reads the environment).  They change how a render is scheduled, never its
+ * pixels (every option's renders are bit-identical):
+ *   MTSG_OPT_TRACE_REFILL     idle lanes that make a traversal wave refill
+ *                             from the work list: 16 (default) or 32
+ *   MTSG_OPT_FINISH_SHADE_MIN tail kernel: a wave shades once that many of its
+ *                             busy lanes wait for shading (1..64, default 1)
+ *   MTSG_OPT_LANES            concurrent batches on their own streams (1..4,
+ *                             default 1; measured slower)
+ *   MTSG_OPT_STAGGER          bounces between the lanes' starts (0..16)
+ *   MTSG_OPT_SHADE_GENERIC    1: shade with the kernel that holds every material
+ *                             class instead of the scene's own set (A/B tests)
+ * Unknown keys and values out of range return MTSG_ERR_INVALID. */
+enum {
+    MTSG_OPT_TRACE_REFILL = 1,
+    MTSG_OPT_FINISH_SHADE_MIN = 2,
+    MTSG_OPT_LANES = 3,
+    MTSG_OPT_STAGGER = 4,
+    MTSG_OPT_SHADE_GENERIC = 5
+};
+int  mtsg_set_option(mtsg_scene *scene, int32_t key, int64_t value);
 
 /* TEST ONLY: the traversal's limits, to exercise the kd-restart guard
  * (tests/test_gpu_edge_rays.py; kernels.h kd_restart).  stack_cap > 0

@@ -179,6 +179,7 @@ struct ShadeLaunch {
     int hasAlpha;
     uint32_t shadeMin;   // k_finish
     bool env, ext, inst;   // inst: two-level instancing (k_finish<.., INST>)
+    int mats;              // the scene's material classes (MAT_*), or MATS_ALL
 };
 template <int SMP> void launch_shade_smp(const ShadeLaunch &a);
 template <int SMP> void launch_finish_smp(const ShadeLaunch &a);
@@ -820,6 +821,12 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 #ifndef MTSG_MAILBOX
 #define MTSG_MAILBOX 1   // 0: measurement variant, the last primitive tested wins a tie
 #endif
+// flat traversal: a tie's retrace runs in the lane that met it, inside the
+// trace launch (round 6), instead of in a k_tie launch after every trace launch
+#ifndef MTSG_TIE_INLINE
+#define MTSG_TIE_INLINE 1
+#endif
+constexpr bool TIE_INLINE = MTSG_TIE_INLINE;
 __shared__ uint32_t s_mbPrev[TRACE_BLOCK];
 // the tie branch of mailbox_step (mb: the state before this test)
 DEV bool mailbox_tie(SpecRay &r, uint32_t mb, uint32_t sl, uint32_t id, const float4 *hitOut) {
@@ -1068,7 +1075,7 @@ struct TopSave {
 // [0, OUTER_STACK), group level in [OUTER_STACK, OUTER_STACK + INNER_STACK)
 __shared__ uint2 s_lvNode[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
 __shared__ float s_lvT[(OUTER_STACK + INNER_STACK) * TRACE_BLOCK];
-enum : uint32_t { SB_INST = 1u << 22, SB_PEND = 1u << 24, SB_XPEND = 1u << 26 };   // inside an instance; entering one next
+enum : uint32_t { SB_INST = 1u << 22, SB_PEND = 1u << 24, SB_XPEND = 1u << 26, SB_MBRUN = 1u << 27 };   // inside an instance; entering one next
                                                                                   // iteration; leaving it (MTSG_EXIT_BATCH)
 
 DEV uint4 &save_vec(const DevScene &S, uint32_t k) {
@@ -1681,19 +1688,32 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
                 const bool sh = (r.bits & SB_SHADOW) != 0;
                 if (COUNT && sh) done = spec_iter_i<COUNT>(S, r, cs, P, idx, L, inst, ts);
                 else done = spec_iter_i<COUNT>(S, r, cc, P, idx, L, inst, ts);
+            } else if (TIE_INLINE && (r.bits & SB_MBRUN)) {
+                // the retrace of a tie (below): Mitsuba's mailbox emulated (not counted)
+                done = spec_iter<false, true>(S, r, stk, cc, P.hit + idx, L);
             } else {
                 if (COUNT && (r.bits & SB_SHADOW)) done = spec_iter<COUNT>(S, r, stk, cs, P.hit + idx, L);
                 else done = spec_iter<COUNT>(S, r, stk, cc, P.hit + idx, L);
             }
         }
         if (COUNT && active) ++iters;
+        if (done && MTSG_MAILBOX && (r.bits & (SB_TIE | SB_SHADOW | SB_MBRUN)) == SB_TIE) {
+            if (COUNT) atomicAdd(&P.ctr[51], 1ull);
+            if (!INST && TIE_INLINE) {
+                // a closest ray that met an exact tie is traced again from its
+                // start in this lane with the mailbox (tie_retrace), inside the
+                // launch: its drain absorbs the retrace, no k_tie launch follows
+                const float4 ro = ldS(P.ray_o + idx), rd = ldS(P.ray_d + idx);
+                spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, false, r);   // true: it passed before
+                r.bits |= SB_MBRUN;
+                done = false;
+            } else {
+                // k_tie_i traces it again with the two-level mailboxes
+                P.tie[atomicAdd(&P.cnt[CNT_TIE], 1u)] = idx;
+            }
+        }
         if (done) {
             active = false;
-            // k_tie traces it again with the mailbox
-            if (MTSG_MAILBOX && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE) {
-                P.tie[atomicAdd(&P.cnt[CNT_TIE], 1u)] = idx;
-                if (COUNT) atomicAdd(&P.ctr[51], 1ull);
-            }
             if (COUNT) {
                 const bool sh = (r.bits & SB_SHADOW) != 0;
                 if (!INST) {
@@ -1820,6 +1840,22 @@ struct BsdfSample {
     float pdf, eta;
     uint32_t delta;
 };
+
+// Material classes compiled into a shading kernel (MATS, a template parameter
+// of k_shade).  A kernel's VGPR budget is the maximum over all the BSDF code
+// it holds, so a scene whose records are all diffuse / GGX roughconductor /
+// dielectric (the per-BSDF dispatch of path.cpp:145-264 over diffuse.cpp:93-150,
+// roughconductor.cpp:168-415, dielectric.cpp:148-333) runs a kernel without the
+// Beckmann / Phong microfacet code or the classes it does not use
+// (mtsg_scene_create picks the smallest compiled set, mats_kernel_set).
+enum : int { MAT_DIFFUSE = 1, MAT_RC_GGX = 2, MAT_RC_OTHER = 4, MAT_DIELECTRIC = 8, MATS_ALL = 15 };
+// the compiled sets (k_shade<.., MATS> in smp_kernels.hip), smallest first
+__host__ __device__ inline int mats_kernel_set(int m) {
+    const int sets[3] = {MAT_DIFFUSE, MAT_DIFFUSE | MAT_RC_GGX, MAT_DIFFUSE | MAT_RC_GGX | MAT_DIELECTRIC};
+    for (int c : sets)
+        if ((m & ~c) == 0) return c;
+    return MATS_ALL;
+}
 
 // warp.cpp:43-52,81-102
 DEV float3 cosine_hemisphere(float sx, float sy) {
@@ -2072,14 +2108,17 @@ struct MF {
 };
 
 // MicrofacetDistribution(props) after the loader's clamping (microfacet.h:96-144):
-// Phong never samples visible normals
+// Phong never samples visible normals.  MATS without MAT_RC_OTHER: every
+// microfacet record of the scene is GGX (the distribution is then a constant
+// and the Beckmann / Phong branches compile away)
+template <int MATS = MATS_ALL>
 DEV MF make_mf(const mtsg_bsdf &b) {
     MF m;
-    m.type = b.distribution;
+    m.type = (MATS & MAT_RC_OTHER) ? b.distribution : (int)MTSG_MF_GGX;
     m.au = b.alpha_u;
     m.av = b.alpha_v;
-    m.visible = b.sample_visible != 0 && b.distribution != MTSG_MF_PHONG;
-    const bool phong = b.distribution == MTSG_MF_PHONG;
+    m.visible = b.sample_visible != 0 && m.type != MTSG_MF_PHONG;
+    const bool phong = m.type == MTSG_MF_PHONG;
     m.eu = phong ? fmaxf(2.0f / (m.au * m.au) - 2.0f, 0.0f) : 0.0f;
     m.ev = phong ? fmaxf(2.0f / (m.av * m.av) - 2.0f, 0.0f) : 0.0f;
     return m;
@@ -2150,18 +2189,18 @@ DEV float rough_trans(const mtsg_bsdf &b, float cosTheta) {
 // diffuse + roughconductor + dielectric kernel its register budget)
 // alb: the record's reflectance (`reflectance` / `diffuseReflectance`), the
 // constant or its texture's value at the hit (texture_eval)
-template <bool EXT>
+template <bool EXT, int MATS = MATS_ALL>
 DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 alb, float3 wi, float3 wo, float &pdf) {
     pdf = 0.0f;
-    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:107-126
+    if ((MATS & MAT_DIFFUSE) && b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:107-126
         if (!b.smooth || wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
         pdf = kInvPi * wo.z;
         return alb * (kInvPi * wo.z);
     }
-    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:235-293
+    if ((MATS & (MAT_RC_GGX | MAT_RC_OTHER)) && b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:235-293
         if (wi.z <= 0 || wo.z <= 0) return mk3(0, 0, 0);
         float3 H = normalize(wo + wi);
-        const MF mf = make_mf(b);
+        const MF mf = make_mf<MATS>(b);
         const float Dv = mf.D(H);
         if (mf.visible) pdf = Dv * mf.G1(wi, H) / (4.0f * wi.z);
         else pdf = Dv * H.z / (4 * fabsf(dot(wo, H)));
@@ -2230,20 +2269,20 @@ DEV float3 bsdf_eval1(const mtsg_bsdf &b, float3 alb, float3 wi, float3 wo, floa
 
 // next1d: the sampler's next1D, drawn only where Mitsuba draws it
 // (roughdielectric's reflect/refract choice: roughdielectric.cpp:531-539)
-template <bool EXT, class Next1D>
+template <bool EXT, int MATS, class Next1D>
 DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 alb, float3 wi, float sx, float sy, BsdfSample &r, Next1D &&next1d) {
     r.eta = 1.0f;
     r.delta = 0;
-    if (b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
+    if ((MATS & MAT_DIFFUSE) && b.type == MTSG_BSDF_DIFFUSE) {   // diffuse.cpp:139-150
         if (wi.z <= 0) return false;
         r.wo = cosine_hemisphere(sx, sy);
         r.pdf = kInvPi * r.wo.z;
         r.weight = alb;
         return !isZero(r.weight);
     }
-    if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:345-394
+    if ((MATS & (MAT_RC_GGX | MAT_RC_OTHER)) && b.type == MTSG_BSDF_ROUGHCONDUCTOR) {   // roughconductor.cpp:345-394
         if (wi.z < 0) return false;
-        const MF mf = make_mf(b);
+        const MF mf = make_mf<MATS>(b);
         float pdf;
         float3 m = mf.sample(wi, sx, sy, pdf);
         if (pdf == 0) return false;
@@ -2257,7 +2296,7 @@ DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 alb, float3 wi, float sx, float
         r.weight = F * weight;
         return !isZero(r.weight);
     }
-    if (b.type == MTSG_BSDF_DIELECTRIC) {   // dielectric.cpp:277-333
+    if ((MATS & MAT_DIELECTRIC) && b.type == MTSG_BSDF_DIELECTRIC) {   // dielectric.cpp:277-333
         float cosThetaT;
         float F = fresnel_dielectric(wi.z, cosThetaT, b.ior_eta);
         r.delta = 1;
@@ -2340,7 +2379,7 @@ DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 alb, float3 wi, float sx, float
             r.wo = cosine_hemisphere(sx, sy);
         }
         float pdf;
-        const float3 val = bsdf_eval1<EXT>(b, alb, wi, r.wo, pdf);
+        const float3 val = bsdf_eval1<EXT, MATS>(b, alb, wi, r.wo, pdf);
         if (pdf == 0) return false;
         r.pdf = pdf;
         r.weight = val / pdf;
@@ -2371,25 +2410,25 @@ DEV bool bsdf_sample1(const mtsg_bsdf &b, float3 alb, float3 wi, float sx, float
 // bsdfs[back] with the z components negated
 // alb belongs to the record that answers (the back record for back-side
 // queries of a twosided front record)
-template <bool EXT>
+template <bool EXT, int MATS = MATS_ALL>
 DEV float3 bsdf_eval(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 alb, float3 wi, float3 wo, float &pdf) {
     if (EXT && b.twosided && !(wi.z > 0)) {
         wi.z = -wi.z;
         wo.z = -wo.z;
-        return bsdf_eval1<EXT>(all[b.back], alb, wi, wo, pdf);
+        return bsdf_eval1<EXT, MATS>(all[b.back], alb, wi, wo, pdf);
     }
-    return bsdf_eval1<EXT>(b, alb, wi, wo, pdf);
+    return bsdf_eval1<EXT, MATS>(b, alb, wi, wo, pdf);
 }
-template <bool EXT, class Next1D>
+template <bool EXT, int MATS = MATS_ALL, class Next1D>
 DEV bool bsdf_sample(const mtsg_bsdf *all, const mtsg_bsdf &b, float3 alb, float3 wi, float sx, float sy, BsdfSample &r,
                      Next1D &&next1d) {
     if (EXT && b.twosided && wi.z < 0) {
         wi.z = -wi.z;
-        if (!bsdf_sample1<EXT>(all[b.back], alb, wi, sx, sy, r, next1d)) return false;
+        if (!bsdf_sample1<EXT, MATS>(all[b.back], alb, wi, sx, sy, r, next1d)) return false;
         r.wo.z = -r.wo.z;
         return true;
     }
-    return bsdf_sample1<EXT>(b, alb, wi, sx, sy, r, next1d);
+    return bsdf_sample1<EXT, MATS>(b, alb, wi, sx, sy, r, next1d);
 }
 
 DEV float mis(float pdfA, float pdfB) {   // path.cpp:296-300
@@ -2665,11 +2704,19 @@ DEV void block_append2(BlockAppend &ba, uint32_t *gcnt0, uint32_t *gcnt1, bool p
     i1 = ba.base[1] + w1 + (uint32_t)__popcll(m1 & below);
 }
 
-// outgoing records of one workgroup (36 KB: 4 workgroups per CU at 4 waves/SIMD)
+// outgoing records of one workgroup: 7 rows of 16 B per lane, 28 KB, so with
+// the staged tables a 256-thread workgroup stays under 32 KB and 5 fit a CU
+// (5 waves/SIMD; 9 rows, 36 KB, held k_shade at 4).  The continuation origin
+// and the shadow origin are the same point (its.p), and the constant .w words
+// of the outgoing rays (mint = Epsilon, maxt = inf; shadow mint = Epsilon)
+// carry the path's meta words instead (depth | flags, dimension, 2D
+// requests; the slot is the caller's): the write-out restores the constants.
 struct ShadeStage {
-    float4 o[SHADE_BLOCK], d[SHADE_BLOCK], T[SHADE_BLOCK], aux[SHADE_BLOCK], L[SHADE_BLOCK];
-    uint4 meta[SHADE_BLOCK];
-    float4 sho[SHADE_BLOCK], shd[SHADE_BLOCK], shc[SHADE_BLOCK];
+    float4 p[SHADE_BLOCK];     // its.p, shadow maxt
+    float4 d[SHADE_BLOCK];     // continuation direction, meta.x
+    float4 T[SHADE_BLOCK], aux[SHADE_BLOCK], L[SHADE_BLOCK];
+    float4 shd[SHADE_BLOCK];   // shadow direction, meta.y
+    float4 shc[SHADE_BLOCK];   // NEE contribution, meta.w
 };
 
 // One bounce of one path (the body of MIPathTracer::Li's loop, path.cpp:119-294,
@@ -2724,7 +2771,7 @@ DEV PathLoads load_path_rest(const DevScene &S, const DevPaths &P, uint32_t i, b
 #define MTSG_SHADE_PRELOAD 0   // measured r04: 1 (all) C3 -0.5%, C5 -3.5% (spills at the 128-VGPR cap); 2 (hit) C3 -0.4%
 #endif
 
-template <bool ENV, int SMP, bool EXT, class Out>
+template <bool ENV, int SMP, bool EXT, class Out, int MATS = MATS_ALL>
 DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, bool first, uint32_t i,
                     const uint4 meta, const PathLoads &pl, int hasAlpha, Out &out, bool &cont, bool &shadow,
                     const ShadeTables &tb) {
@@ -2858,7 +2905,7 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
                     value = value / emPdf;
                     const float3 wo = its.sh.toLocal(dd);
                     float bpdf;
-                    const float3 bval = bsdf_eval<EXT>(S.bsdfs, bsdf, alb, wi, wo, bpdf);
+                    const float3 bval = bsdf_eval<EXT, MATS>(S.bsdfs, bsdf, alb, wi, wo, bpdf);
                     if (!isZero(bval) && (!I.strict_normals || dot(its.geoN, dd) * wo.z > 0)) {
                         const float weight = mis(pdf, bpdf);
                         const float3 c = T * value * bval * weight;
@@ -2874,7 +2921,7 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
             float sx, sy;
             next2D<SMP>(I, smp, sx, sy);
             BsdfSample bs;
-            if (!bsdf_sample<EXT>(S.bsdfs, bsdf, alb, wi, sx, sy, bs, [&]() { return next1D<SMP>(I, smp); })) {
+            if (!bsdf_sample<EXT, MATS>(S.bsdfs, bsdf, alb, wi, sx, sy, bs, [&]() { return next1D<SMP>(I, smp); })) {
                 done = true;
             } else {
                 flags |= F_SCATTERED;
@@ -3138,12 +3185,48 @@ DEV void shade_path_om(const DevScene &S, const DevIntegrator &I, const DevBatch
 }
 
 // k_shade's outgoing records: lane-private LDS rows until the block append
+// (ShadeStage: the .w words of d / shd / shc hold meta.x / .y / .w; o.w and
+// d.w are the constants kEpsilon / inf, shd.w kEpsilon, restored by stage_write)
 struct StageOut {
     ShadeStage &st;
-    DEV void shadow(float4 o, float4 d, float4 c) { st.sho[threadIdx.x] = o; st.shd[threadIdx.x] = d; st.shc[threadIdx.x] = c; }
-    DEV void next(float4 o, float4 d, float4 aux) { st.o[threadIdx.x] = o; st.d[threadIdx.x] = d; st.aux[threadIdx.x] = aux; }
-    DEV void state(float4 T, float4 L, uint4 meta) { st.T[threadIdx.x] = T; st.L[threadIdx.x] = L; st.meta[threadIdx.x] = meta; }
+    DEV void shadow(float4 o, float4 d, float4 c) {
+        const int t = threadIdx.x;
+        st.p[t] = o;
+        st.shd[t].x = d.x; st.shd[t].y = d.y; st.shd[t].z = d.z;
+        st.shc[t].x = c.x; st.shc[t].y = c.y; st.shc[t].z = c.z;
+    }
+    DEV void next(float4 o, float4 d, float4 aux) {
+        const int t = threadIdx.x;
+        st.p[t].x = o.x; st.p[t].y = o.y; st.p[t].z = o.z;
+        st.d[t].x = d.x; st.d[t].y = d.y; st.d[t].z = d.z;
+        st.aux[t] = aux;
+    }
+    DEV void state(float4 T, float4 L, uint4 meta) {
+        const int t = threadIdx.x;
+        st.T[t] = T;
+        st.L[t] = L;
+        st.d[t].w = __uint_as_float(meta.x);
+        st.shd[t].w = __uint_as_float(meta.y);
+        st.shc[t].w = __uint_as_float(meta.w);
+    }
 };
+// a survivor's records into the next bounce's arrays at position ic, and a
+// shadow ray into the shadow arrays at position is (sh_c.w: the target)
+DEV void stage_write_next(const ShadeStage &st, const DevPaths &P, int tid, uint32_t ic, uint32_t slot) {
+    const float4 p = st.p[tid], d = st.d[tid];
+    stS(&P.n_ray_o[ic], make_float4(p.x, p.y, p.z, kEpsilon));
+    stS(&P.n_ray_d[ic], make_float4(d.x, d.y, d.z, INFINITY));
+    stS(&P.n_T[ic], st.T[tid]);
+    stS(&P.n_aux[ic], st.aux[tid]);
+    stS(&P.n_Lp[ic], st.L[tid]);
+    stS(&P.n_meta[ic], make_uint4(__float_as_uint(d.w), __float_as_uint(st.shd[tid].w), slot, __float_as_uint(st.shc[tid].w)));
+}
+DEV void stage_write_shadow(const ShadeStage &st, const DevPaths &P, int tid, uint32_t is, uint32_t target) {
+    const float4 d = st.shd[tid], c = st.shc[tid];
+    stS(&P.sh_o[is], st.p[tid]);
+    stS(&P.sh_d[is], make_float4(d.x, d.y, d.z, kEpsilon));
+    stS(&P.sh_c[is], make_float4(c.x, c.y, c.z, __uint_as_float(target)));
+}
 
 // myPath2_OM's shading launch: one iteration of its Li per path (no shadow
 // rays: visibility comes from the occupancy maps inside the kernel)
@@ -3172,14 +3255,7 @@ __global__ void __launch_bounds__(SHADE_BLOCK) k_shade_om(DevScene S, DevIntegra
         const int tid = threadIdx.x;
         uint32_t is, ic;
         block_append2(ba, &P.cnt[cnt_s(bounce & 1)], &P.cnt[cnt_q(qout)], false, cont, is, ic);
-        if (cont) {
-            stS(&P.n_ray_o[ic], stage.o[tid]);
-            stS(&P.n_ray_d[ic], stage.d[tid]);
-            stS(&P.n_T[ic], stage.T[tid]);
-            stS(&P.n_aux[ic], stage.aux[tid]);
-            stS(&P.n_Lp[ic], stage.L[tid]);
-            stS(&P.n_meta[ic], stage.meta[tid]);
-        }
+        if (cont) stage_write_next(stage, P, tid, ic, meta.z);
     }
 }
 
@@ -3194,16 +3270,26 @@ constexpr int SHADE_LDS_BSDFS = 4, SHADE_LDS_EMITTERS = 16;
 #ifndef MTSG_SHADE_WAVES
 #define MTSG_SHADE_WAVES 4   // 127 VGPRs: 4 waves/SIMD (3 at 144; 5+ spill heavily)
 #endif
+// the material-specialised kernels (MATS != MATS_ALL) fit 96 VGPRs: with the
+// 28-KB stage (ShadeStage) 5 workgroups share a CU, 5 waves/SIMD
+#ifndef MTSG_SHADE_WAVES_MATS
+#define MTSG_SHADE_WAVES_MATS 5
+#endif
+#ifndef MTSG_SHADE_WAVES_MATS_ENV
+#define MTSG_SHADE_WAVES_MATS_ENV 5
+#endif
+#define SHADE_WAVES_OF(ENV, MATS) ((MATS) == MATS_ALL ? MTSG_SHADE_WAVES : (ENV) ? MTSG_SHADE_WAVES_MATS_ENV : MTSG_SHADE_WAVES_MATS)
 #if MTSG_SHADE_WAVES > 0
-#define SHADE_ATTR __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_SHADE_WAVES)))
+#define SHADE_ATTR(ENV, MATS) __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(SHADE_WAVES_OF(ENV, MATS))))
 #else
-#define SHADE_ATTR __launch_bounds__(SHADE_BLOCK)
+#define SHADE_ATTR(ENV, MATS) __launch_bounds__(SHADE_BLOCK)
 #endif
 // ENV: the scene has an environment emitter (the variant without it keeps
 // the environment code, and its registers, out of the common case)
 // SMP: the render's sampler (MTSG_SAMPLER_*)
-template <bool ENV, int SMP, bool EXT>
-__global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int bounce, int qin,
+// MATS: the material classes compiled in (MAT_*; the scene's set or a superset)
+template <bool ENV, int SMP, bool EXT, int MATS = MATS_ALL>
+__global__ void SHADE_ATTR(ENV, MATS) k_shade(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int bounce, int qin,
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
     __shared__ ShadeStage stage;
@@ -3260,7 +3346,7 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
             }
 #endif
             StageOut out{stage};
-            shade_path<ENV, SMP, EXT>(S, I, B, P, bounce == 0, i, meta, pl, hasAlpha, out, cont, shadow, tb);
+            shade_path<ENV, SMP, EXT, StageOut, MATS>(S, I, B, P, bounce == 0, i, meta, pl, hasAlpha, out, cont, shadow, tb);
         }
         const uint32_t slot = meta.z;
         // The output positions come from the workgroup-aggregated append; the
@@ -3275,22 +3361,9 @@ __global__ void SHADE_ATTR k_shade(DevScene S, DevIntegrator I, DevBatch B, DevP
 #else
         block_append2(ba, &P.cnt[cnt_s(bounce & 1)], &P.cnt[cnt_q(qout)], shadow, cont, is, ic);
 #endif
-        if (cont) {
-            // survivor: compacted into the next bounce's arrays
-            stS(&P.n_ray_o[ic], stage.o[tid]);
-            stS(&P.n_ray_d[ic], stage.d[tid]);
-            stS(&P.n_T[ic], stage.T[tid]);
-            stS(&P.n_aux[ic], stage.aux[tid]);
-            stS(&P.n_Lp[ic], stage.L[tid]);
-            stS(&P.n_meta[ic], stage.meta[tid]);
-        }
-        if (shadow) {
-            float4 c = stage.shc[tid];
-            c.w = __uint_as_float(cont ? ic : (0x80000000u | slot));
-            stS(&P.sh_o[is], stage.sho[tid]);
-            stS(&P.sh_d[is], stage.shd[tid]);
-            stS(&P.sh_c[is], c);
-        }
+        // survivor: compacted into the next bounce's arrays
+        if (cont) stage_write_next(stage, P, tid, ic, slot);
+        if (shadow) stage_write_shadow(stage, P, tid, is, cont ? ic : (0x80000000u | slot));
     }
 }
 

@@ -108,6 +108,8 @@ struct mtsg_scene {
     unsigned long long *waveTimes = nullptr;     // MTSG_FLAG_WAVETIME: [launch][wave][WT_WORDS]
     uint32_t wtLaunches = 0;
     bool extBsdfs = false;   // conductor / plastic / twosided records or textures present (k_shade<..., true>)
+    int mats = MATS_ALL;     // material classes of the scene's records (k_shade<..., MATS>)
+    bool shadeGeneric = false;   // MTSG_OPT_SHADE_GENERIC: the all-materials kernel (A/B tests)
     uint32_t nTextures = 0;
     const uint32_t *sobolM = nullptr;        // sobol sampler tables (device)
     const uint64_t *sobolVdc = nullptr, *sobolVdcInv = nullptr;
@@ -208,8 +210,9 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t
     else if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     // closest rays that met an exact tie: traced again with the mailbox
-    // (a grid a quarter of the trace grid's; two-level: the exact Havran)
-    if (MTSG_MAILBOX && cIn != -2) {
+    // (a grid a quarter of the trace grid's; two-level: the exact Havran).
+    // The flat traversal retraces them inside its own launch (TIE_INLINE).
+    if (MTSG_MAILBOX && cIn != -2 && (s->ds.inst || !TIE_INLINE)) {
         const dim3 tg(std::max<unsigned>(1u, (unsigned)s->traceGrid / 4u));
         if (s->ds.inst) hipLaunchKernelGGL(k_tie_i, tg, blk, 0, st, s->ds, P);
         else if (s->knobs) hipLaunchKernelGGL((k_tie<true>), tg, blk, 0, st, s->ds, P);
@@ -240,6 +243,7 @@ ShadeLaunch shade_args(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B,
     a.env = s->ds.has_env != 0;
     a.ext = s->extBsdfs;
     a.inst = s->ds.inst != nullptr;
+    a.mats = s->shadeGeneric ? (int)MATS_ALL : s->mats;
     return a;
 }
 void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {
@@ -1053,11 +1057,17 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     ds.instKeyStride = (uint64_t)d->n_prims * ((uint64_t)d->n_instances + 1) <= 0xFFFFFFFFull ? d->n_prims : 0x9E3779B1u;
     // environment emitter tables (envmap.h)
     ds.has_env = d->has_envmap ? 1 : 0;
+    s->mats = 0;
     for (uint32_t i = 0; i < d->n_bsdfs; ++i) {
         const mtsg_bsdf &b = d->bsdfs[i];
         if (b.type == MTSG_BSDF_CONDUCTOR || b.type == MTSG_BSDF_PLASTIC || b.type == MTSG_BSDF_ROUGHDIELECTRIC ||
             b.type == MTSG_BSDF_ROUGHPLASTIC || b.twosided)
             s->extBsdfs = true;
+        // the material classes the non-extended shading kernel must hold
+        if (b.type == MTSG_BSDF_DIFFUSE) s->mats |= MAT_DIFFUSE;
+        else if (b.type == MTSG_BSDF_ROUGHCONDUCTOR) s->mats |= b.distribution == MTSG_MF_GGX ? MAT_RC_GGX : MAT_RC_OTHER;
+        else if (b.type == MTSG_BSDF_DIELECTRIC) s->mats |= MAT_DIELECTRIC;
+        else s->mats |= MATS_ALL;
         if (b.twosided && (b.back < 0 || (uint32_t)b.back >= d->n_bsdfs)) {
             g_err = "bsdf " + std::to_string(i) + ": twosided back record out of range";
             return fail(MTSG_ERR_INVALID);
@@ -1203,7 +1213,6 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         s->sobolScramble = d->sobol_scramble;
     }
     // persistent grids from the occupancy query
-    if (const char *m = getenv("MTSG_TRACE_MODE")) s->traceMode = atoi(m);
     int perCU = 0;
     const void *occKernel = (const void *)k_trace_s<false, 16>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, occKernel, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
@@ -1235,10 +1244,6 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         s->ds.instSave = save;
     }
     s->finishPaths = MTSG_DEFAULT_FINISH_PATHS;
-    if (const char *f = getenv("MTSG_FINISH")) s->finishPaths = (uint32_t)strtoul(f, nullptr, 0);
-    if (const char *f = getenv("MTSG_FINISH_SHADE_MIN")) s->finishShadeMin = std::max(1, atoi(f));
-    if (const char *l = getenv("MTSG_LANES")) s->lanes = std::max(1, std::min(MTSG_MAX_LANES, atoi(l)));
-    if (const char *g = getenv("MTSG_STAGGER")) s->stagger = std::max(0, std::min(16, atoi(g)));
     s->lstream[0] = s->stream;
     for (int l = 1; l < MTSG_MAX_LANES; ++l)
         if (hipStreamCreateWithFlags(&s->lstream[l], hipStreamNonBlocking) != hipSuccess) { g_err = "stream"; return fail(MTSG_ERR_DEVICE); }
@@ -1283,6 +1288,34 @@ int mtsg_set_finish_paths(mtsg_scene *s, uint32_t paths) {
     if (!s) return MTSG_ERR_INVALID;
     s->finishPaths = paths;
     return MTSG_OK;
+}
+
+int mtsg_set_option(mtsg_scene *s, int32_t key, int64_t value) {
+    if (!s) { g_err = "null scene"; return MTSG_ERR_INVALID; }
+    switch (key) {
+        case MTSG_OPT_TRACE_REFILL:
+            if (value != 16 && value != 32) { g_err = "MTSG_OPT_TRACE_REFILL: 16 or 32 idle lanes"; return MTSG_ERR_INVALID; }
+            s->traceMode = value == 32 ? 1 : 0;
+            return MTSG_OK;
+        case MTSG_OPT_FINISH_SHADE_MIN:
+            if (value < 1 || value > 64) { g_err = "MTSG_OPT_FINISH_SHADE_MIN: 1..64 lanes"; return MTSG_ERR_INVALID; }
+            s->finishShadeMin = (uint32_t)value;
+            return MTSG_OK;
+        case MTSG_OPT_LANES:
+            if (value < 1 || value > MTSG_MAX_LANES) { g_err = "MTSG_OPT_LANES: 1..4 concurrent batches"; return MTSG_ERR_INVALID; }
+            s->lanes = (int)value;
+            return MTSG_OK;
+        case MTSG_OPT_STAGGER:
+            if (value < 0 || value > 16) { g_err = "MTSG_OPT_STAGGER: 0..16 bounces"; return MTSG_ERR_INVALID; }
+            s->stagger = (int)value;
+            return MTSG_OK;
+        case MTSG_OPT_SHADE_GENERIC:
+            s->shadeGeneric = value != 0;
+            return MTSG_OK;
+        default:
+            g_err = "unknown option key " + std::to_string(key);
+            return MTSG_ERR_INVALID;
+    }
 }
 
 int mtsg_set_flags(mtsg_scene *s, uint32_t flags) {

@@ -1,7 +1,8 @@
 // smp_kernels.hip -- the shading kernels (k_shade, k_finish) of one sampler.
 // Compiled once per sampler with -DMTSG_TU_SAMPLER=<MTSG_SAMPLER_* value>, so the
-// four ENV x EXT variants of both kernels of each sampler build in their own
-// translation unit, in parallel (see kernels.h and the Makefile).
+// ENV x EXT (x MATS for k_shade) variants of both kernels of each sampler
+// build in their own translation unit, in parallel (see kernels.h and the
+// Makefile).
 #include "kernels.h"
 
 #ifndef MTSG_TU_SAMPLER
@@ -9,6 +10,12 @@
 #endif
 
 namespace mtsg {
+
+template <int SMP, int MATS>
+void launch_shade_mats(const ShadeLaunch &a) {
+    if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, false, MATS>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+    else hipLaunchKernelGGL((k_shade<false, SMP, false, MATS>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+}
 
 template <>
 void launch_shade_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
@@ -23,9 +30,14 @@ void launch_shade_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
     if (a.ext) {
         if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
         else hipLaunchKernelGGL((k_shade<false, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
-    } else {
-        if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
-        else hipLaunchKernelGGL((k_shade<false, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+        return;
+    }
+    // the smallest compiled material set that holds the scene's (mats_kernel_set)
+    switch (mats_kernel_set(a.mats)) {
+        case MAT_DIFFUSE: launch_shade_mats<SMP, MAT_DIFFUSE>(a); break;
+        case MAT_DIFFUSE | MAT_RC_GGX: launch_shade_mats<SMP, MAT_DIFFUSE | MAT_RC_GGX>(a); break;
+        case MAT_DIFFUSE | MAT_RC_GGX | MAT_DIELECTRIC: launch_shade_mats<SMP, MAT_DIFFUSE | MAT_RC_GGX | MAT_DIELECTRIC>(a); break;
+        default: launch_shade_mats<SMP, MATS_ALL>(a);
     }
 }
 

@@ -27,6 +27,12 @@ MTSH_INSTANCING_TWO_LEVEL = 1
 MTSG_FLAG_TIMING = 1
 MTSG_FLAG_COUNT = 2
 MTSG_FLAG_WAVETIME = 4
+# mtsg_set_option keys (include/mtsg.h)
+MTSG_OPT_TRACE_REFILL = 1
+MTSG_OPT_FINISH_SHADE_MIN = 2
+MTSG_OPT_LANES = 3
+MTSG_OPT_STAGGER = 4
+MTSG_OPT_SHADE_GENERIC = 5
 
 
 class RenderParams(C.Structure):
@@ -220,7 +226,7 @@ DEVICE_SYMBOLS = [
     "mtsg_trace_closest", "mtsg_trace_shadow", "mtsg_render_samples", "mtsg_scene_destroy",
     "mtsg_last_error", "mtsg_env_eval", "mtsg_tex_eval", "mtsg_om_query", "mtsg_kd_build", "mtsg_kd_refit", "mtsg_kd_free",
     "mtsg_sampler_draws", "mtsg_debug_wavetimes", "mtsg_set_tile_callback",
-    "mtsg_debug_stragglers", "mtsg_set_test_knobs",
+    "mtsg_debug_stragglers", "mtsg_set_test_knobs", "mtsg_set_option",
 ]
 HOST_SYMBOLS = [
     "mtsh_scene_load", "mtsh_scene_load_overrides", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
@@ -360,6 +366,7 @@ def device_lib() -> C.CDLL:
         lib.mtsg_get_stats.argtypes = [C.c_void_p, C.POINTER(Stats)]
         lib.mtsg_set_batch_paths.argtypes = [C.c_void_p, C.c_uint32]
         lib.mtsg_set_finish_paths.argtypes = [C.c_void_p, C.c_uint32]
+        lib.mtsg_set_option.argtypes = [C.c_void_p, C.c_int32, C.c_int64]
         lib.mtsg_trace_closest.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p]
         lib.mtsg_trace_shadow.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
@@ -815,6 +822,10 @@ class GPUScene:
     def set_finish_paths(self, n: int) -> None:
         """Tail-mode threshold (paths; 0: off), see mtsg_set_finish_paths."""
         self._check(device_lib().mtsg_set_finish_paths(self._h, n), "mtsg_set_finish_paths")
+
+    def set_option(self, key: int, value: int) -> None:
+        """An execution option (MTSG_OPT_*, mtsg_set_option): scheduling only, never pixels."""
+        self._check(device_lib().mtsg_set_option(self._h, key, value), "mtsg_set_option")
 
     def stats(self) -> Stats:
         s = Stats()

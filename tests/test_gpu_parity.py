@@ -152,23 +152,44 @@ def test_tiling_is_additive(cbox_small, gpu_cbox):
 
 
 def test_staggered_lanes_are_bit_identical(cbox_small):
-    # the multi-lane render path (MTSG_LANES batches on their own streams,
-    # MTSG_STAGGER bounces apart) renders the same samples as one lane
-    import os as _os
+    # the multi-lane render path (MTSG_OPT_LANES batches on their own streams,
+    # MTSG_OPT_STAGGER bounces apart) renders the same samples as one lane
     p = cbox_small.params()
     b = cbox_small.border
     g1 = mtsg.GPUScene(cbox_small, 0)
     ref = g1.render(p, b)
     g1.close()
-    _os.environ["MTSG_LANES"], _os.environ["MTSG_STAGGER"] = "3", "2"
-    try:
-        g3 = mtsg.GPUScene(cbox_small, 0)
-        g3.set_batch_paths(16 * 16 * 4 * 4)
-        img = g3.render(p, b)
-        g3.close()
-    finally:
-        del _os.environ["MTSG_LANES"], _os.environ["MTSG_STAGGER"]
+    g3 = mtsg.GPUScene(cbox_small, 0)
+    g3.set_option(mtsg.MTSG_OPT_LANES, 3)
+    g3.set_option(mtsg.MTSG_OPT_STAGGER, 2)
+    g3.set_batch_paths(16 * 16 * 4 * 4)
+    img = g3.render(p, b)
+    g3.close()
     np.testing.assert_allclose(img, ref, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("name", ["cbox.xml", "bunny15.xml", "env_glass.xml", "cbox_glass.xml"])
+def test_material_kernels_match_the_generic_kernel(name):
+    # k_shade<.., MATS> holds only the scene's material classes (diffuse /
+    # GGX roughconductor / dielectric): the same arithmetic as the
+    # kernel with every class, so every sample's radiance is bit-identical (the
+    # film itself sums samples with float atomics in no fixed order)
+    scene = mtsg.Scene(os.path.join(SCENES, name), {"width": 64, "height": 48, "spp": 8})
+    p = scene.params()
+    g = mtsg.GPUScene(scene, 0)
+    spec = g.render_samples(p)
+    g.set_option(mtsg.MTSG_OPT_SHADE_GENERIC, 1)
+    gen = g.render_samples(p)
+    g.close()
+    assert np.array_equal(spec, gen, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(spec - gen))}"
+
+
+def test_set_option_rejects_unknown_keys_and_values(cbox_small):
+    g = mtsg.GPUScene(cbox_small, 0)
+    for key, value in ((99, 1), (mtsg.MTSG_OPT_LANES, 0), (mtsg.MTSG_OPT_TRACE_REFILL, 20)):
+        with pytest.raises(RuntimeError):
+            g.set_option(key, value)
+    g.close()
 
 
 def test_dielectric_scene_parity():

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-6 GPU call (one gpurun): the steps named on the command line, each under
+# its own time limit; a failing step ends the call (test failures, pytest rc 1,
+# excepted: the GPU is fine then and later steps still run).
+#   tools/gpu_r06.sh [tests] [bench] [cq-<var>] [q-<var>] [c5q-<var>] [e8q-<var>] [iq-<var>] ...
+# <var> = base (the in-tree libmtsg.so) or a Makefile VARIANTS name (my-mitsuba_amd/var/).
+O=gpurun_out/r6
+mkdir -p $O
+export TMPDIR=/tmp
+step() { local name=$1 lim=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; tail -n 3 "$O/$name.log" | cut -c1-2500; if [ $rc -ne 0 ] && ! { [ "${name%%-*}" = tests ] && [ $rc -eq 1 ]; }; then exit $rc; fi; }
+lib() { local v=${1%@*}; if [ "$v" = base ]; then echo ""; else echo "my-mitsuba_amd/var/libmtsg_$v.so"; fi; }
+PYT="python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread"
+Q="--no-cpu --no-parity"
+for w in ${*:-tests bench}; do
+  case $w in
+    tests) step tests 900 $PYT tests ;;
+    tests-parity) step tests-parity 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_c4.py ;;
+    tests-inst) step tests-inst 600 $PYT tests/test_gpu_instancing.py tests/test_gpu_edge_rays.py tests/test_gpu_finish.py ;;
+    vtests-*) v=${w#vtests-}; MTSG_LIB=$(lib $v) step $w 900 $PYT tests ;;
+    bench) step bench 600 python bench.py --steps 10 --warmup 3 ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    # C3 with the instrumented pass (SIMD efficiency, iterations) / without it
+    cq-*) v=${w#cq-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 10 --warmup 3 $Q ;;
+    q-*) v=${w#q-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 10 --warmup 3 $Q --no-count ;;
+    iq-*) v=${w#iq-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level $Q ;;
+    c5q-*) v=${w#c5q-}; MTSG_LIB=$(lib $v) step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count ;;
+    c5g) step c5g 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --shade-generic ;;
+    qg) step qg 300 python bench.py --steps 10 --warmup 3 $Q --no-count --shade-generic ;;
+    c2q-*) v=${w#c2q-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 5 --warmup 2 --workload cbox $Q --no-count ;;
+    e8q-*) v=${w#e8q-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 $Q --no-count ;;
+    c5) step c5 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 ;;
+    c2) step c2 600 python bench.py --steps 5 --warmup 2 --workload cbox ;;
+    inst) step inst 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity ;;
+    e8) step e8 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity ;;
+    stats-c3) step stats-c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-parity --no-count ;;
+    stats-c5) step stats-c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o c5 -- python3 bench.py --steps 2 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
+    pmc-c3) bash tools/gpu_pmc_config.sh r06 c3 || exit $? ;;
+    pmc-inst) bash tools/gpu_pmc_config.sh r06 c3_two_level --instancing two-level || exit $? ;;
+    pmc-c5) bash tools/gpu_pmc_config.sh r06 c5 --workload c5 --width 1920 --height 1080 --spp 1024 || exit $? ;;
+    pmc-e8) bash tools/gpu_pmc_config.sh r06 c4_share8 --emulate-ranks 8 || exit $? ;;
+    *) echo "unknown step $w"; exit 2 ;;
+  esac
+done
