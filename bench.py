@@ -116,6 +116,10 @@ def parse():
     ap.add_argument("--no-count", action="store_true",
                     help="skip the instrumented (untimed) pass of per-ray counts (profiler runs)")
     ap.add_argument("--print-pmc-key", action="store_true", help="print this configuration's PMC key and exit")
+    ap.add_argument("--pmc-pass", action="store_true",
+                    help="profiler pass (tools/gpu_pmc_config.sh): render only this configuration's frame -- share 0 "
+                         "of the stride deal when shares are emulated -- warmup + steps times, no balancing, no "
+                         "whole-frame timing, no instrumented pass; prints the frame count")
     ap.add_argument("--shade-generic", action="store_true",
                     help="shade with the all-materials kernel instead of the scene's material set (A/B measurement)")
     return ap.parse_args()
@@ -215,15 +219,9 @@ def mitsuba_tree_scene(scene):
     stopPrims 6; this build's GPU-tuned default is 4), so the CPU baseline
     traverses the tree Mitsuba would build."""
     import mtsg
-    old = os.environ.get("MTSH_KD_STOP_PRIMS")
-    os.environ["MTSH_KD_STOP_PRIMS"] = "6"
-    try:
-        return mtsg.Scene(scene.path, scene.defines, instancing=scene.instancing)
-    finally:
-        if old is None:
-            del os.environ["MTSH_KD_STOP_PRIMS"]
-        else:
-            os.environ["MTSH_KD_STOP_PRIMS"] = old
+    # the Scene's own kdStopPrims property (scene.cpp:64-65), as a Mitsuba
+    # scene file or plugin would set it
+    return mtsg.Scene(scene.path, scene.defines, instancing=scene.instancing, scene_props={"kdStopPrims": 6})
 
 
 def cpu_baseline(scene, params, border, target_s):
@@ -404,7 +402,7 @@ def main():
     scene = mtsg.Scene(path, defs, instancing=a.instancing)
     load_s = time.time() - t_load
     kd_info = {"kd_build": "host", "kd_build_ms": round(scene.info.kd_build_seconds * 1e3, 1), "kd_refs": scene.info.kd_indices,
-               "kd_stop_prims": int(os.environ.get("MTSH_KD_STOP_PRIMS", "4"))}   # Mitsuba: 6
+               "kd_stop_prims": 4}   # the build's GPU-tuned default; Mitsuba: 6
     if a.kd_build == "device":
         mtsg.kd_build(scene, device=dev)   # warm-up
         tree = mtsg.kd_build(scene, device=dev)
@@ -448,7 +446,9 @@ def main():
     emulated = a.emulate_ranks > 1 and world == 1
     n_shares = a.emulate_ranks if emulated else world
     n_tiles = ((params.tile_w + 15) // 16) * ((params.tile_h + 15) // 16)
-    balanced = n_shares > 1 and a.balance_rounds > 0
+    # balancing cuts runs of at least one tile per share: with fewer tiles
+    # than shares the stride deal is used (a share may then be empty)
+    balanced = n_shares > 1 and a.balance_rounds > 0 and n_tiles >= n_shares
     order = mtsg.balance_order(n_tiles)
     counts = np.array([len(range(r, n_tiles, n_shares)) for r in range(n_shares)], dtype=np.int64)
     cur = {"keys": None}
@@ -489,6 +489,21 @@ def main():
         gpu.render_device(params, film)
         mtsg.device_lib().mtsg_device_to_host(gpu._h, host_block.ctypes.data, film, nbytes)
 
+    if a.pmc_pass:
+        # rocprofv3 counts every launch of the process: render exactly the
+        # frames a PMC set is normalised by (tools/pmc_kernels.py), and nothing else
+        if n_shares > 1:
+            params.tile_stride, params.tile_offset = n_shares, 0
+        for _ in range(a.warmup + a.steps):
+            step()
+        gpu.free(film)
+        if wbuf is not None:
+            gpu.free(wbuf)
+        gpu.close()
+        if rank == 0:
+            print(json.dumps({"pmc_pass_frames": a.warmup + a.steps, "share": "0 of %d (stride deal)" % n_shares
+                              if n_shares > 1 else "whole frame"}))
+        return
     # --emulate-ranks N: every rank's tile share in turn on this one GPU, each
     # timed like a rank of an N-GPU run (max over the shares = the frame time)
     shares = list(range(a.emulate_ranks)) if emulated else [rank]
@@ -587,8 +602,13 @@ def main():
             pmc = {}
             for fam, ms in fam_ms.items():
                 ks = [v for n, v in pj["kernels"].items() if n == fam or n.startswith(fam + "<")]
-                b = sum(v.get("traffic_bytes_per_step", 0.0) for v in ks)
-                rp_ns = sum(v["rocprof_stats"]["avg_ns"] * v.get("launches_fetch_pass", 0) for v in ks
+                # per frame: the set's pass rendered frames_fetch_pass frames
+                # (bench.py --pmc-pass; sets of round 5 and before lack the
+                # count and are not quoted)
+                if "frames_fetch_pass" not in pj:
+                    continue
+                b = sum(v.get("traffic_bytes_per_frame", 0.0) for v in ks)
+                rp_ns = sum(v["rocprof_stats"]["avg_ns"] * v.get("launches_per_frame", 0) for v in ks
                             if "rocprof_stats" in v)
                 if b > 0 and rp_ns > 0:
                     hits = [v["tcc_hit_rate"] for v in ks if "tcc_hit_rate" in v]

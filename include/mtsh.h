@@ -57,6 +57,11 @@ typedef struct mtsh_scene_overrides {
 /* mtsh_scene_load, then the overrides (may be NULL) before finalisation. */
 mtsh_scene *mtsh_scene_load_overrides(const char *path, const char *const *defines, int n_defines,
                                       const mtsh_scene_overrides *overrides);
+/* ... and Scene properties (mtsh_scene_set_scene_props) applied after the
+ * file's own <scene>-level ones (n_scene_props may be 0). */
+mtsh_scene *mtsh_scene_load_props(const char *path, const char *const *defines, int n_defines,
+                                  const mtsh_scene_overrides *overrides, const struct mtsh_prop *scene_props,
+                                  int32_t n_scene_props);
 
 /* ---- building the scene Mitsuba holds in memory --------------------------
  *
@@ -102,14 +107,19 @@ typedef struct mtsh_prop {
     const char *s;
 } mtsh_prop;
 
-/* A TriMesh as Mitsuba holds it after TriMesh::configure (trimesh.cpp:362-386):
- * positions and (unless face_normals) vertex normals in world space, the
- * winding already flipped for flipped face normals.  Optional inputs make the
- * builder do configure's work instead: to_world (16 floats row-major, NULL =
- * identity; normals use its inverse transpose) is applied to positions and
- * normals, and NULL normals are
- * computed (TriMesh::computeNormals, trimesh.cpp:608-681), negated when
- * flip_normals is set. */
+/* A triangle mesh.  The builder runs the normal pass of TriMesh::configure
+ * (TriMesh::computeNormals, trimesh.cpp:608-681) on the arrays it is given,
+ * with flip_normals as that pass's m_flipNormals: NULL normals (and
+ * !face_normals) are computed, then given or computed normals are negated
+ * when flip_normals is set, and a face_normals mesh with flip_normals gets
+ * its winding swapped.  So:
+ *   - arrays read from a configured TriMesh (getVertexPositions / Normals /
+ *     Triangles after configure(), world space; the Mitsuba plugin's case,
+ *     INTEGRATION.md) already carry the flip: pass flip_normals = 0;
+ *   - a shape's own loader arrays (object space, before configure) pass the
+ *     shape's flipNormals and, optionally, to_world (16 floats row-major; NULL =
+ *     identity), applied to positions and to normals by its inverse
+ *     transpose, as the shape loaders do before configure. */
 typedef struct mtsh_mesh {
     const char *name;
     uint32_t n_vertices, n_triangles;
@@ -154,6 +164,15 @@ int32_t mtsh_scene_set_film(mtsh_builder *b, const char *plugin, const mtsh_prop
                             const char *rfilter, const mtsh_prop *rfilter_props, int32_t n_rfilter_props);
 int32_t mtsh_scene_set_sampler(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props);
 int32_t mtsh_scene_set_integrator(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n_props);
+/* The Scene's own Properties (Scene::Scene(props), scene.cpp:47-83; a
+ * plugin passes scene->getProperties()): the build parameters of the scene's
+ * kd-tree, kdIntersectionCost, kdTraversalCost, kdEmptySpaceBonus
+ * (float), kdStopPrims, kdMaxDepth, kdExactPrimitiveThreshold,
+ * kdMaxBadRefines (integer), kdClip, kdRetract, kdParallelBuild (boolean).
+ * Shape groups keep the defaults (ShapeGroup builds its own ShapeKDTree,
+ * shapegroup.cpp:74).  Hits do not depend on these, the tree's shape and
+ * speed do.  Returns 0, or -1 for another name or a value of another type. */
+int32_t mtsh_scene_set_scene_props(mtsh_builder *b, const mtsh_prop *props, int32_t n_props);
 /* Finalise (kd-tree, CDFs, environment tables; overrides may be NULL) and
  * free the builder.  Returns the scene, or NULL (see mtsh_last_error). */
 mtsh_scene *mtsh_scene_finish(mtsh_builder *b, const mtsh_scene_overrides *overrides);

@@ -824,7 +824,7 @@ DEV uint2 spec_take(SpecRay &r, const uint4 &pr, float tsplit, bool goLeft, bool
 // flat traversal: a tie's retrace runs in the lane that met it, inside the
 // trace launch (round 6), instead of in a k_tie launch after every trace launch
 #ifndef MTSG_TIE_INLINE
-#define MTSG_TIE_INLINE 1
+#define MTSG_TIE_INLINE 0   // measured r06: C3 trace +4.4 ms (64 VGPRs at the 8-wave limit), C2 +6.4 ms, C5 +40 ms: off
 #endif
 constexpr bool TIE_INLINE = MTSG_TIE_INLINE;
 __shared__ uint32_t s_mbPrev[TRACE_BLOCK];
@@ -1236,10 +1236,15 @@ DEV bool inst_enter(SpecRay &r, TopSave &ts, const DevScene &S, uint32_t ii, flo
 DEV bool inst_box(const SpecRay &r, float4 f0, float4 f1) {
     float t0 = r.mint, t1 = r.best;
     const float bmn[3] = {f0.y, f0.z, f0.w}, bmx[3] = {f1.x, f1.y, f1.z};
+    // the slab distances round with the ray's own magnitude (|o| ulps), which
+    // the box's margin (its size and position) does not bound for a small
+    // instance seen from far away: widen the box by 2^-20 |o|_max (8 ulps of
+    // the origin) as well, so the test stays conservative there
+    const float e = 0x1p-20f * fmaxf(fmaxf(fabsf(r.o.x), fabsf(r.o.y)), fabsf(r.o.z));
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float oa = comp(r.o, a), ia = comp(r.inv, a);
-        const float u = (bmn[a] - oa) * ia, v = (bmx[a] - oa) * ia;
+        const float u = (bmn[a] - e - oa) * ia, v = (bmx[a] + e - oa) * ia;
         t0 = fmaxf(t0, fminf(u, v));
         t1 = fminf(t1, fmaxf(u, v));
     }
@@ -3288,7 +3293,11 @@ constexpr int SHADE_LDS_BSDFS = 4, SHADE_LDS_EMITTERS = 16;
 // the environment code, and its registers, out of the common case)
 // SMP: the render's sampler (MTSG_SAMPLER_*)
 // MATS: the material classes compiled in (MAT_*; the scene's set or a superset)
-template <bool ENV, int SMP, bool EXT, int MATS = MATS_ALL>
+// FIRST: 1 = bounce 0 only (camera rays: differentials, the EWA environment
+// lookup of a primary miss, hideEmitters' camera case), 0 = later bounces only
+// (that code compiled out: C5's kernel then holds 96 VGPRs without spilling),
+// 2 = either (run-time)
+template <bool ENV, int SMP, bool EXT, int MATS = MATS_ALL, int FIRST = 2>
 __global__ void SHADE_ATTR(ENV, MATS) k_shade(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int bounce, int qin,
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
@@ -3320,6 +3329,7 @@ __global__ void SHADE_ATTR(ENV, MATS) k_shade(DevScene S, DevIntegrator I, DevBa
     if (qin >= 0) count = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
     const uint32_t nIter = (count + gridDim.x * blockDim.x - 1) / (gridDim.x * blockDim.x);
     const int qout = qin < 0 ? 1 : (qin ^ 1);
+    const bool first = FIRST == 2 ? bounce == 0 : FIRST == 1;
     for (uint32_t it = 0; it < nIter; ++it) {
         const uint32_t i = (it * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
         bool alive = i < count;
@@ -3329,7 +3339,7 @@ __global__ void SHADE_ATTR(ENV, MATS) k_shade(DevScene S, DevIntegrator I, DevBa
         if (alive) {
             meta = ldS(&P.meta[i]);
 #if MTSG_SHADE_PRELOAD == 1
-            pl = load_path(S, P, i, bounce == 0);
+            pl = load_path(S, P, i, first);
 #elif MTSG_SHADE_PRELOAD == 2
             pl.h = ldS(&P.hit[i]);
 #endif
@@ -3337,16 +3347,16 @@ __global__ void SHADE_ATTR(ENV, MATS) k_shade(DevScene S, DevIntegrator I, DevBa
         }
         if (alive) {
 #if MTSG_SHADE_PRELOAD == 0
-            pl = load_path(S, P, i, bounce == 0);
+            pl = load_path(S, P, i, first);
 #elif MTSG_SHADE_PRELOAD == 2
             {
                 const float4 h = pl.h;
-                pl = load_path_rest(S, P, i, bounce == 0);
+                pl = load_path_rest(S, P, i, first);
                 pl.h = h;
             }
 #endif
             StageOut out{stage};
-            shade_path<ENV, SMP, EXT, StageOut, MATS>(S, I, B, P, bounce == 0, i, meta, pl, hasAlpha, out, cont, shadow, tb);
+            shade_path<ENV, SMP, EXT, StageOut, MATS>(S, I, B, P, first, i, meta, pl, hasAlpha, out, cont, shadow, tb);
         }
         const uint32_t slot = meta.z;
         // The output positions come from the workgroup-aggregated append; the

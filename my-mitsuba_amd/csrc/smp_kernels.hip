@@ -11,10 +11,20 @@
 
 namespace mtsg {
 
+// the material-specialised kernels (MATS), one for bounce 0 and one for the
+// later bounces (FIRST); the generic kernel decides at run time
 template <int SMP, int MATS>
 void launch_shade_mats(const ShadeLaunch &a) {
-    if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, false, MATS>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
-    else hipLaunchKernelGGL((k_shade<false, SMP, false, MATS>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+    if (MATS == MATS_ALL) {
+        if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+        else hipLaunchKernelGGL((k_shade<false, SMP, false>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+    } else if (a.bounce == 0) {
+        if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, false, MATS, 1>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+        else hipLaunchKernelGGL((k_shade<false, SMP, false, MATS, 1>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+    } else {
+        if (a.env) hipLaunchKernelGGL((k_shade<true, SMP, false, MATS, 0>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+        else hipLaunchKernelGGL((k_shade<false, SMP, false, MATS, 0>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
+    }
 }
 
 template <>
@@ -32,13 +42,18 @@ void launch_shade_smp<MTSG_TU_SAMPLER>(const ShadeLaunch &a) {
         else hipLaunchKernelGGL((k_shade<false, SMP, true>), a.grid, a.block, 0, a.stream, *a.S, *a.I, *a.B, *a.P, a.bounce, a.qin, a.nIdentity, a.hasAlpha);
         return;
     }
-    // the smallest compiled material set that holds the scene's (mats_kernel_set)
-    switch (mats_kernel_set(a.mats)) {
-        case MAT_DIFFUSE: launch_shade_mats<SMP, MAT_DIFFUSE>(a); break;
-        case MAT_DIFFUSE | MAT_RC_GGX: launch_shade_mats<SMP, MAT_DIFFUSE | MAT_RC_GGX>(a); break;
-        case MAT_DIFFUSE | MAT_RC_GGX | MAT_DIELECTRIC: launch_shade_mats<SMP, MAT_DIFFUSE | MAT_RC_GGX | MAT_DIELECTRIC>(a); break;
-        default: launch_shade_mats<SMP, MATS_ALL>(a);
+    // the smallest compiled material set that holds the scene's (mats_kernel_set);
+    // compiled for the independent sampler (the other samplers' units keep
+    // their build time and shade with the generic kernel)
+    if constexpr (SMP == MTSG_SAMPLER_INDEPENDENT) {
+        switch (mats_kernel_set(a.mats)) {
+            case MAT_DIFFUSE: launch_shade_mats<SMP, MAT_DIFFUSE>(a); return;
+            case MAT_DIFFUSE | MAT_RC_GGX: launch_shade_mats<SMP, MAT_DIFFUSE | MAT_RC_GGX>(a); return;
+            case MAT_DIFFUSE | MAT_RC_GGX | MAT_DIELECTRIC: launch_shade_mats<SMP, MAT_DIFFUSE | MAT_RC_GGX | MAT_DIELECTRIC>(a); return;
+            default: break;
+        }
     }
+    launch_shade_mats<SMP, MATS_ALL>(a);
 }
 
 // SMP is a template parameter (not this unit's constant): every unit defines

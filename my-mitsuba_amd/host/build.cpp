@@ -372,7 +372,7 @@ void Scene::finalize() {
     for (size_t g = 0; g < groups.size(); ++g) {
         if (groupTris[g].empty()) throw std::runtime_error("shapegroup \"" + groups[g].id + "\" holds no triangles");
         GroupPrims gp(*this, groupTris[g]);
-        buildKDTree(gp, kd, groupTrees[g]);
+        buildKDTree(gp, groupKd, groupTrees[g]);
         const KDTree &T = groupTrees[g];
         mtsg_group gd{};
         gd.node_offset = (uint32_t)groupNodes.size();

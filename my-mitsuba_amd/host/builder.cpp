@@ -193,17 +193,60 @@ SceneBuilder::SceneBuilder(Scene &s) : scene(s) {}
 std::unique_ptr<Scene> SceneBuilder::newScene() {
     auto scene = std::make_unique<Scene>();
     scene->kd.threads = g_defaultKDThreads;
+    scene->groupKd = scene->kd;
     scene->twoLevel = g_instancing == 1;
-    // build-parameter overrides (tree-quality experiments; defaults follow
-    // gkdtree.h:734-744).  The tree changes, the hits do not.
-    if (const char *v = getenv("MTSH_KD_TRAVERSAL")) scene->kd.traversalCost = (float)atof(v);
-    if (const char *v = getenv("MTSH_KD_QUERY")) scene->kd.queryCost = (float)atof(v);
-    if (const char *v = getenv("MTSH_KD_EMPTY_BONUS")) scene->kd.emptySpaceBonus = (float)atof(v);
-    if (const char *v = getenv("MTSH_KD_STOP_PRIMS")) scene->kd.stopPrims = atoi(v);
-    if (const char *v = getenv("MTSH_KD_EXACT_LIMIT")) scene->kd.exactSweepLimit = atoi(v);
-    if (const char *v = getenv("MTSH_KD_MAX_DEPTH")) scene->kd.maxDepth = atoi(v);
-    if (const char *v = getenv("MTSH_KD_RETRACT")) scene->kd.retract = atoi(v) != 0;
     return scene;
+}
+
+// Scene::Scene(const Properties &) (scene.cpp:47-83): the scene's kd-tree
+// build parameters (the setters of gkdtree.h:760-925).  Unlike Mitsuba, which
+// logs unqueried properties, a name it would not read is an error here.
+void SceneBuilder::sceneProps(const Properties &props, int line) {
+    KDBuildParams &k = scene.kd;
+    static const std::map<std::string, const char *> kinds = {
+        {"kdIntersectionCost", "float"}, {"kdTraversalCost", "float"}, {"kdEmptySpaceBonus", "float"},
+        {"kdStopPrims", "integer"}, {"kdMaxDepth", "integer"}, {"kdExactPrimitiveThreshold", "integer"},
+        {"kdMaxBadRefines", "integer"}, {"kdClip", "boolean"}, {"kdRetract", "boolean"}, {"kdParallelBuild", "boolean"}};
+    // every property must be one Scene(props) reads, with its type
+    auto check = [&](const std::string &n, const char *type) {
+        auto it = kinds.find(n);
+        if (it == kinds.end()) throw err(at(line) + "unknown scene property '" + n + "'");
+        if (std::string(it->second) != type) throw err(at(line) + "scene property '" + n + "' must be of type " + it->second);
+    };
+    for (const auto &kv : props.strings) check(kv.first, "string");
+    for (const auto &kv : props.spectra) check(kv.first, "spectrum");
+    for (const auto &kv : props.points) check(kv.first, "point");
+    for (const auto &kv : props.transforms) check(kv.first, "transform");
+    for (const auto &kv : props.floats) {
+        check(kv.first, "float");
+        if (kv.first == "kdIntersectionCost") k.queryCost = kv.second;
+        else if (kv.first == "kdTraversalCost") k.traversalCost = kv.second;
+        else k.emptySpaceBonus = kv.second;
+    }
+    for (const auto &kv : props.ints) {
+        check(kv.first, "integer");
+        const std::string &n = kv.first;
+        const long long v = kv.second;
+        if (n == "kdStopPrims") {
+            if (v < 1) throw err(at(line) + "kdStopPrims must be >= 1");
+            k.stopPrims = (int)v;
+        } else if (n == "kdMaxDepth") {
+            if (v < 0 || v > 64) throw err(at(line) + "kdMaxDepth must lie in [0, 64]");
+            k.maxDepth = (int)v;
+        } else if (n == "kdExactPrimitiveThreshold") {
+            if (v < 0) throw err(at(line) + "kdExactPrimitiveThreshold must be >= 0");
+            k.exactPrimThreshold = k.exactSweepLimit = (int)std::min<long long>(v, 1 << 30);
+        } else {
+            if (v < 0) throw err(at(line) + "kdMaxBadRefines must be >= 0");
+            k.maxBadRefines = (int)v;
+        }
+    }
+    for (const auto &kv : props.bools) {
+        check(kv.first, "boolean");
+        if (kv.first == "kdClip") k.clip = kv.second;
+        else if (kv.first == "kdRetract") k.retract = kv.second;
+        // kdParallelBuild: accepted; the host build's threads are mtsh_set_kd_threads
+    }
 }
 
 std::string SceneBuilder::resolve(const std::string &f) const {

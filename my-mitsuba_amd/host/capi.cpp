@@ -36,6 +36,15 @@ mtsh_scene *mtsh_scene_load(const char *path, const char *const *defines, int n_
 
 mtsh_scene *mtsh_scene_load_overrides(const char *path, const char *const *defines, int n_defines,
                                       const mtsh_scene_overrides *overrides) {
+    return mtsh_scene_load_props(path, defines, n_defines, overrides, nullptr, 0);
+}
+}  // extern "C"
+namespace {
+mtsh::Properties toProps(const mtsh_prop *p, int32_t n, std::map<std::string, int> *textures = nullptr);
+}
+extern "C" {
+mtsh_scene *mtsh_scene_load_props(const char *path, const char *const *defines, int n_defines,
+                                  const mtsh_scene_overrides *overrides, const mtsh_prop *scene_props, int32_t n_scene_props) {
     try {
         std::map<std::string, std::string> defs;
         for (int i = 0; i < n_defines; ++i) {
@@ -45,7 +54,8 @@ mtsh_scene *mtsh_scene_load_overrides(const char *path, const char *const *defin
             defs[d.substr(0, eq)] = d.substr(eq + 1);
         }
         auto s = std::make_unique<mtsh_scene>();
-        s->scene = mtsh::loadScene(path, defs, overrides);
+        const mtsh::Properties sp = toProps(scene_props, n_scene_props);
+        s->scene = mtsh::loadScene(path, defs, overrides, n_scene_props > 0 ? &sp : nullptr);
         return s.release();
     } catch (const std::exception &e) {
         g_err = e.what();
@@ -65,7 +75,7 @@ struct mtsh_builder {
 
 namespace {
 // mtsh_prop list -> Properties (and a BSDF's textured parameters)
-mtsh::Properties toProps(const mtsh_prop *p, int32_t n, std::map<std::string, int> *textures = nullptr) {
+mtsh::Properties toProps(const mtsh_prop *p, int32_t n, std::map<std::string, int> *textures) {
     if (n < 0 || (n > 0 && !p)) throw std::runtime_error("invalid property list");
     mtsh::Properties props;
     for (int32_t k = 0; k < n; ++k) {
@@ -220,6 +230,13 @@ int32_t mtsh_scene_set_film(mtsh_builder *b, const char *plugin, const mtsh_prop
 int32_t mtsh_scene_set_sampler(mtsh_builder *b, const char *plugin, const mtsh_prop *props, int32_t n) {
     return guarded(b, [&] {
         b->b->sampler(plugin ? plugin : "", toProps(props, n));
+        return 0;
+    });
+}
+
+int32_t mtsh_scene_set_scene_props(mtsh_builder *b, const mtsh_prop *props, int32_t n) {
+    return guarded(b, [&] {
+        b->b->sceneProps(toProps(props, n));
         return 0;
     });
 }

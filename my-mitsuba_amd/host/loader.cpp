@@ -676,6 +676,14 @@ struct Loader {
         for (auto &cp : n.children) {
             XNode &c = *cp;
             substAll(c);
+            if (!parseValue(c, props)) nested.push_back(&c);
+        }
+    }
+
+    // one value element (<float>, <integer>, ... <transform>) into props;
+    // false for any other element
+    bool parseValue(XNode &c, Properties &props) {
+        {
             const std::string name = c.attr("name");
             const std::string &tag = c.tag;
             if (tag == "float") props.floats[name] = parseF(c.attr("value"), c.line);
@@ -705,9 +713,10 @@ struct Loader {
             } else if (tag == "transform") {
                 props.transforms[name] = parseTransform(c);
             } else {
-                nested.push_back(&c);
+                return false;
             }
         }
+        return true;
     }
 
     int parseTexture(XNode &n) {
@@ -840,6 +849,9 @@ struct Loader {
                 parseEmitter(c);
             } else if (tag == "ref") {
                 // scene-level refs are ignored
+            } else if (Properties p; parseValue(c, p)) {
+                // the Scene's own Properties (Scene::Scene(props), scene.cpp:47-83)
+                B.sceneProps(p, c.line);
             } else {
                 throw err("line " + std::to_string(c.line) + ": unsupported element <" + tag + ">");
             }
@@ -922,7 +934,7 @@ int g_defaultKDThreads = 0;
 int g_instancing = 0;
 
 std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::string, std::string> &defines,
-                                 const mtsh_scene_overrides *ov) {
+                                 const mtsh_scene_overrides *ov, const Properties *sceneProps) {
     auto scene = SceneBuilder::newScene();
     Loader L(*scene);
     L.defines = defines;
@@ -933,6 +945,7 @@ std::unique_ptr<Scene> loadScene(const std::string &path, const std::map<std::st
     auto root = p.element();
     if (root->tag != "scene") throw err("root element must be <scene>");
     L.parseScene(*root);
+    if (sceneProps) L.B.sceneProps(*sceneProps);
     L.B.finish(ov);
     return scene;
 }

@@ -56,7 +56,10 @@ struct mtsh_path_job {
     std::vector<int> lastCount;
     std::vector<double> lastSec;
     std::vector<int64_t> lastSig;
-    explicit mtsh_path_job(int n) : rendering(n, 0), sent(n, 0), gpuLock(n) {}
+    // the largest share each GPU has rendered: a render past it may have
+    // (re)allocated the handle's batch buffers, so its time is not a rate
+    std::vector<size_t> maxShare;
+    explicit mtsh_path_job(int n) : rendering(n, 0), sent(n, 0), gpuLock(n), maxShare(n, 0) {}
 };
 
 namespace {
@@ -221,12 +224,14 @@ int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, f
                 std::lock_guard<std::mutex> gl(job->gpuLock[g]);
                 job->rendering[g] = 1;
             }
-            const auto tg = std::chrono::steady_clock::now();
+            // the render call alone is timed (not the tile-list upload)
             if (job->cancel.load()) rcs[g] = MTSG_ERR_CANCELLED;
             else if (share[g].empty()) rcs[g] = MTSG_OK;   // fewer tiles than GPUs: this one idles
-            else if ((rcs[g] = mtsg_set_tile_list(job->handles[g], share[g].data(), (uint32_t)share[g].size())) == MTSG_OK)
+            else if ((rcs[g] = mtsg_set_tile_list(job->handles[g], share[g].data(), (uint32_t)share[g].size())) == MTSG_OK) {
+                const auto tg = std::chrono::steady_clock::now();
                 rcs[g] = mtsg_render(job->handles[g], &p, blocks[g].data());
-            sec[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - tg).count();
+                sec[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - tg).count();
+            }
             {
                 std::lock_guard<std::mutex> gl(job->gpuLock[g]);
                 job->rendering[g] = 0;
@@ -252,7 +257,14 @@ int mtsh_path_job_render(mtsh_path_job *job, const mtsg_render_params *params, f
     std::memset(rgbaw_out, 0, W * H * 5 * sizeof(float));
     for (int g = 0; g < n; ++g)
         for (size_t i = 0; i < W * H * 5; ++i) rgbaw_out[i] += blocks[g][i];
-    job->lastSig = sig;
+    // a GPU whose share grew past any it rendered before may have spent part
+    // of its time allocating: that render keeps the cut (no re-cut from it)
+    bool grew = false;
+    for (int g = 0; g < n; ++g) {
+        grew |= share[g].size() > job->maxShare[g];
+        job->maxShare[g] = std::max(job->maxShare[g], share[g].size());
+    }
+    job->lastSig = grew ? std::vector<int64_t>() : sig;
     job->lastCount = count;
     job->lastSec = sec;
     return MTSG_OK;
@@ -268,6 +280,8 @@ int mtsh_path_job_set_balance(mtsh_path_job *job, int on) {
 
 int mtsh_path_job_shares(const mtsh_path_job *job, int32_t *tiles, double *seconds) {
     if (!job) { g_perr = "null argument"; return MTSG_ERR_INVALID; }
+    // not while a render of the job rewrites them
+    std::lock_guard<std::mutex> lock(const_cast<mtsh_path_job *>(job)->renderLock);
     const size_t n = job->handles.size();
     for (size_t g = 0; g < n; ++g) {
         if (tiles) tiles[g] = g < job->lastCount.size() ? job->lastCount[g] : 0;

@@ -126,8 +126,9 @@ struct KDBuildParams {                // gkdtree.h:734-744 defaults, except stop
     // tests one primitive per iteration while it descends, so a primitive test
     // costs it more, relative to a node step, than Mitsuba's cost model
     // assumes: C3 1501 -> 1538 Msamples/s (5.99 instead of 7.24 tests per ray,
-    // DESIGN §3).  Hits do not depend on the tree; MTSH_KD_STOP_PRIMS=6 gives
-    // Mitsuba's tree (the CPU baseline in bench.py is timed on that one).
+    // DESIGN §3).  Hits do not depend on the tree; the scene's kdStopPrims
+    // property (scene.cpp:64) sets it, e.g. 6 for Mitsuba's own tree (the CPU
+    // baseline in bench.py is timed on that one).
     int stopPrims = 4, maxBadRefines = 3, minMaxBins = 128;
     int exactPrimThreshold = 65536;
     int exactSweepLimit = 65536;      // exact O(n log n) sweep below exactPrimThreshold (gkdtree.h:980, 1510), binned above
@@ -166,7 +167,8 @@ struct Scene {
     std::string samplerType = "independent";
     mtsg_sampler sampler{MTSG_SAMPLER_INDEPENDENT, -1, 4, 0};
     uint64_t sobolScrambleProp = 0;   // sobol 'scramble' (before TEA)
-    KDBuildParams kd;
+    KDBuildParams kd;                 // the scene's tree (its <scene> kd* properties)
+    KDBuildParams groupKd;            // shape groups' trees (defaults, shapegroup.cpp:74)
 
     // ---- flattened (filled by finalize()) ----
     std::vector<float> vtxPos, vtxNrm, triDpdu, emitterCdf, emitterTriCdf;
@@ -283,6 +285,7 @@ public:
     void sensor(const std::string &type, const Properties &props, int line = 0);
     void film(const std::string &type, const Properties &props);
     void rfilter(const std::string &type, const Properties &props);
+    void sceneProps(const Properties &props, int line = 0);   // Scene::Scene(props): kd build parameters
     void sampler(const std::string &type, const Properties &props);
     void finish(const mtsh_scene_overrides *overrides);   // validation, overrides, Scene::finalize
 
@@ -302,7 +305,8 @@ private:
 // XML loading (src/librender/scenehandler.cpp), `-D name=value` defines
 std::unique_ptr<Scene> loadScene(const std::string &path,
                                  const std::map<std::string, std::string> &defines,
-                                 const mtsh_scene_overrides *overrides = nullptr);
+                                 const mtsh_scene_overrides *overrides = nullptr,
+                                 const Properties *sceneProps = nullptr);
 
 // Mesh loaders
 void loadPLY(const std::string &path, Mesh &mesh);   // src/shapes/ply.cpp

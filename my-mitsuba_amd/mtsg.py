@@ -115,10 +115,10 @@ def kd_build(scene: "Scene", bounds: np.ndarray | None = None, device: int = 0, 
     """SAH kd-tree over the scene's primitives built on the GPU (mtsg_kd_build);
     bounds: their boxes (n, 6), by default scene.prim_bounds().  Costs are
     Mitsuba's (gkdtree.h:734-744); leaves stop at 4 primitives like the host
-    build's GPU-tuned default (MTSH_KD_STOP_PRIMS overrides both)."""
+    build's GPU-tuned default (params, e.g. stop_prims=6, override them)."""
     lib = device_lib()
     b = np.ascontiguousarray(scene.prim_bounds() if bounds is None else bounds, dtype=np.float32)
-    p = KDBuildParams(15.0, 20.0, 0.9, int(os.environ.get("MTSH_KD_STOP_PRIMS", "4")), 0, 0)
+    p = KDBuildParams(15.0, 20.0, 0.9, 4, 0, 0)
     for k, v in params.items():
         setattr(p, k, v)
     t = KDTree()
@@ -229,7 +229,7 @@ DEVICE_SYMBOLS = [
     "mtsg_debug_stragglers", "mtsg_set_test_knobs", "mtsg_set_option",
 ]
 HOST_SYMBOLS = [
-    "mtsh_scene_load", "mtsh_scene_load_overrides", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
+    "mtsh_scene_load", "mtsh_scene_load_overrides", "mtsh_scene_load_props", "mtsh_scene_set_scene_props", "mtsh_set_kd_threads", "mtsh_set_instancing", "mtsh_scene_desc", "mtsh_scene_render_params",
     "mtsh_scene_get_info", "mtsh_scene_free", "mtsh_develop", "mtsh_write_pfm", "mtsh_rough_transmittance",
     "mtsh_read_image", "mtsh_clip_triangle", "mtsh_texture_image", "mtsh_build_mipmap", "mtsh_scene_textures", "mtsh_scene_om", "mtsh_scene_prim_bounds", "mtsh_scene_set_kdtree",
     "mtsh_last_error",
@@ -284,6 +284,9 @@ def host_lib() -> C.CDLL:
         lib.mtsh_scene_load.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_int]
         lib.mtsh_scene_load_overrides.restype = C.c_void_p
         lib.mtsh_scene_load_overrides.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_int, C.POINTER(SceneOverrides)]
+        lib.mtsh_scene_load_props.restype = C.c_void_p
+        lib.mtsh_scene_load_props.argtypes = [C.c_char_p, C.POINTER(C.c_char_p), C.c_int, C.POINTER(SceneOverrides),
+                                              C.POINTER(Prop), C.c_int32]
         lib.mtsh_scene_desc.restype = C.c_void_p
         lib.mtsh_scene_desc.argtypes = [C.c_void_p]
         lib.mtsh_scene_render_params.argtypes = [C.c_void_p, C.POINTER(RenderParams)]
@@ -314,6 +317,8 @@ def host_lib() -> C.CDLL:
                    "mtsh_scene_set_integrator"):
             getattr(lib, fn).restype = C.c_int32
             getattr(lib, fn).argtypes = [C.c_void_p, C.c_char_p, PP, C.c_int32]
+        lib.mtsh_scene_set_scene_props.restype = C.c_int32
+        lib.mtsh_scene_set_scene_props.argtypes = [C.c_void_p, PP, C.c_int32]
         lib.mtsh_scene_add_bsdf.restype = C.c_int32
         lib.mtsh_scene_add_bsdf.argtypes = [C.c_void_p, C.c_char_p, PP, C.c_int32, C.POINTER(C.c_int32), C.c_int32]
         lib.mtsh_scene_add_group.restype = C.c_int32
@@ -410,10 +415,14 @@ class Scene:
     """A loaded Mitsuba XML scene (host side; owns the flat descriptor)."""
 
     def __init__(self, path: str, defines: dict | None = None, kd_threads: int = 0, instancing: str = "flatten",
-                 overrides: SceneOverrides | None = None):
+                 overrides: SceneOverrides | None = None, scene_props=None):
         """instancing: "flatten" (instances become world-space triangles of the
         one scene tree) or "two-level" (Mitsuba's instance / shapegroup
-        structure: per-group trees, rays transformed per instance visit)."""
+        structure: per-group trees, rays transformed per instance visit).
+        scene_props: the Scene's own Properties as [(name, kind, value)] or
+        {name: value} (ints -> integer, floats -> float, bools -> boolean),
+        applied after the file's <scene>-level ones (mtsh_scene_load_props:
+        the kd-tree build parameters of scene.cpp:47-83)."""
         lib = host_lib()
         lib.mtsh_set_kd_threads(kd_threads)
         if instancing not in ("flatten", "two-level"):
@@ -421,7 +430,11 @@ class Scene:
         lib.mtsh_set_instancing(MTSH_INSTANCING_TWO_LEVEL if instancing == "two-level" else MTSH_INSTANCING_FLATTEN)
         defs = [f"{k}={v}".encode() for k, v in (defines or {}).items()]
         arr = (C.c_char_p * max(1, len(defs)))(*defs)
-        if overrides is None:
+        if scene_props:
+            pa, pn, _keep = _props(_scene_prop_list(scene_props))
+            self._h = lib.mtsh_scene_load_props(path.encode(), arr, len(defs),
+                                                C.byref(overrides) if overrides is not None else None, pa, pn)
+        elif overrides is None:
             self._h = lib.mtsh_scene_load(path.encode(), arr, len(defs))
         else:
             self._h = lib.mtsh_scene_load_overrides(path.encode(), arr, len(defs), C.byref(overrides))
@@ -510,6 +523,14 @@ class Scene:
         if getattr(self, "_h", None):
             host_lib().mtsh_scene_free(self._h)
             self._h = None
+
+
+def _scene_prop_list(props):
+    """{name: value} -> [(name, kind, value)] (bool before int: bool is an int)."""
+    if isinstance(props, dict):
+        kind = lambda v: "boolean" if isinstance(v, bool) else "integer" if isinstance(v, int) else "float"  # noqa: E731
+        return [(k, kind(v), v) for k, v in props.items()]
+    return list(props)
 
 
 def _props(props) -> tuple:
@@ -627,6 +648,11 @@ class SceneBuilder:
         a, n, _k = _props(props)
         self._rc(host_lib().mtsh_scene_set_integrator(self._b, plugin.encode(), a, n), plugin)
 
+    def scene_props(self, props) -> None:
+        """The Scene's own Properties (mtsh_scene_set_scene_props): kd build parameters."""
+        a, n, _k = _props(_scene_prop_list(props))
+        self._rc(host_lib().mtsh_scene_set_scene_props(self._b, a, n), "scene")
+
     def finish(self, overrides: SceneOverrides | None = None, label: str = "<builder>") -> Scene:
         lib = host_lib()
         b, self._b = self._b, None
@@ -690,6 +716,8 @@ def balance_cuts(counts, times, damping: float = 0.5):
     counts = np.asarray(counts, dtype=np.float64)
     times = np.maximum(np.asarray(times, dtype=np.float64), 1e-9)
     total = int(round(counts.sum()))
+    if total < len(counts):
+        raise ValueError(f"balance_cuts: {total} tiles cannot give each of {len(counts)} shares one")
     target = counts / times
     target = target / target.sum() * total
     new = (1.0 - damping) * counts + damping * target

@@ -335,15 +335,27 @@ class Walker:
         if typ == "instance":
             self.call("instance", inst, [pp for pp in p if pp[0] == "toWorld"])
             return
-        if typ == "ply" and self.meshes in ("arrays", "world"):
+        if typ == "ply" and self.meshes in ("arrays", "world", "configured"):
             pos, nrm, uv, tris = read_ply(os.path.join(self.dir, pd["filename"]))
             m, inv = pd["toWorld"] if "toWorld" in pd else Xf().arrays()
+            face, flip = bool(pd.get("faceNormals", False)), bool(pd.get("flipNormals", False))
             if self.meshes == "world" and nrm is None:
                 # the positions as TriMesh holds them after the PLY loader
                 # applied toWorld (Transform::operator()(Point), transform.h)
                 pos, m, inv = transform_points(m, pos), None, None
+            if self.meshes == "configured" and flip and (face or nrm is not None):
+                # the flip as a configured TriMesh carries it (TriMesh::computeNormals,
+                # trimesh.cpp:608-681, already ran): normals negated, or the
+                # winding of a face-normal mesh swapped; the flag is not passed again
+                # (negation commutes with the linear normal transform and with
+                # normalisation, so the descriptor must not change)
+                if face:
+                    tris = tris[:, [1, 0, 2]].copy()
+                else:
+                    nrm = (-nrm).astype(np.float32)
+                flip = False
             self.call("mesh", pos, tris, normals=nrm, texcoords=uv, to_world=m, to_world_inv=inv,
-                      face_normals=bool(pd.get("faceNormals", False)), flip_normals=bool(pd.get("flipNormals", False)),
+                      face_normals=face, flip_normals=flip,
                       bsdf=bsdf, emitter=emitter, group=group, name=pd["filename"])
             return
         self.call("shape", typ, p, bsdf, emitter, group)
@@ -377,6 +389,10 @@ class Walker:
                 self.shape(e)
             elif e.tag == "emitter":
                 self.call("emitter", self.attr(e, "type"), self.props(e, e.get("id"))[0])
+        # the Scene's own Properties (scene->getProperties(): its kd* values)
+        sp, _ = self.props([e for e in root if e.tag in ("float", "integer", "boolean", "string")], "scene")
+        if sp:
+            self.call("scene_props", sp)
         return self.b.finish(overrides, label=f"builder:{os.path.basename(self.path)}")
 
 

@@ -56,3 +56,11 @@ def test_put_tile_windows_with_keys_matches_the_stride_form():
     k2 = mtsg.put_tile_windows(np.zeros((74, 104, 5), np.float32), win[:12][perm], tile_w, tile_h, b, 1, 0,
                                keys=keys[perm])
     np.testing.assert_allclose(k2, k, rtol=1e-6)
+
+
+def test_balance_cuts_needs_a_tile_per_share():
+    """fewer tiles than shares used to loop forever; bench.py then
+    keeps the stride deal instead of balancing."""
+    import pytest
+    with pytest.raises(ValueError):
+        mtsg.balance_cuts([1, 1, 0, 0], [0.1, 0.1, 0.1, 0.1])

@@ -149,3 +149,59 @@ def test_two_level_coplanar_tie_policy():
         check_render(c, gi)
     finally:
         g.close()
+
+
+SMALL_FAR_XML = """<?xml version="1.0"?>
+<scene version="0.5.0">
+  <sensor type="perspective"><transform name="toWorld"><lookat origin="0, 0, 3" target="0, 0, 0" up="0, 1, 0"/></transform>
+    <film type="hdrfilm"><integer name="width" value="8"/><integer name="height" value="8"/></film></sensor>
+  <shape type="shapegroup" id="g"><shape type="cube"><bsdf type="diffuse"/></shape></shape>
+  <shape type="instance"><ref id="g"/><transform name="toWorld"><rotate y="1" angle="{rot}"/><scale value="{s}"/></transform></shape>
+  <shape type="rectangle"><transform name="toWorld"><translate z="-5"/></transform>
+    <emitter type="area"><rgb name="radiance" value="1"/></emitter></shape>
+</scene>
+"""
+
+
+@pytest.mark.parametrize("size,dist", [(2e-3, 100.0), (1e-3, 1000.0)])
+def test_small_instance_seen_from_far_away(tmp_path, size, dist):
+    """the world-box prefilter (kernels.h inst_box) must never drop
+    an entry the exact group-space clip takes.  A small instance at the origin
+    (its box margin is ~1e-4 of its size) hit by rays from ~1e5 its size away,
+    aimed at points on and just outside its box faces and edges: hit/miss, the
+    primitive, t, u and v must equal the oracle's two-level traversal (which has
+    no prefilter) for every ray."""
+    p = tmp_path / "far.xml"
+    p.write_text(SMALL_FAR_XML.format(rot=27.0, s=size))
+    s = mtsg.Scene(str(p), instancing="two-level")
+    g = mtsg.GPUScene(s, 0)
+    rng = np.random.default_rng(int(dist))
+    n = 200000
+    # targets on the rotated cube's surface (uniform on faces, many on edges),
+    # pushed out by up to 1e-5 of its size, in world space
+    q = rng.uniform(-1, 1, (n, 3))
+    k = rng.integers(0, 3, n)
+    q[np.arange(n), k] = np.sign(q[np.arange(n), k])
+    edge = rng.random(n) < 0.5
+    k2 = (k + 1) % 3
+    q[edge, k2[edge]] = np.sign(q[edge, k2[edge]])
+    q *= 1 + rng.uniform(-1e-5, 1e-5, (n, 1))
+    c, sn = np.cos(np.radians(27.0)), np.sin(np.radians(27.0))
+    w = np.stack([c * q[:, 0] + sn * q[:, 2], q[:, 1], -sn * q[:, 0] + c * q[:, 2]], 1) * size
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = w - d * dist
+    rays[:, 3:6] = d
+    rays[:, 6] = 1e-4
+    rays[:, 7] = np.inf
+    t0, u0, v0, p0 = O.trace_closest(s.desc, rays)
+    t1, u1, v1, p1 = g.trace_closest(rays)
+    g.close()
+    hit0, hit1 = p0 != 0xFFFFFFFF, p1 != 0xFFFFFFFF
+    assert hit0.mean() > 0.2, hit0.mean()
+    assert np.array_equal(hit0, hit1), f"{(hit0 != hit1).sum()} rays disagree on hit/miss"
+    same = p0 == p1
+    assert same[hit0].mean() > 0.999
+    np.testing.assert_array_equal(t1[same & hit0], t0[same & hit0])
+    np.testing.assert_array_equal(u1[same & hit0], u0[same & hit0])

@@ -210,3 +210,74 @@ def test_builder_needs_a_sensor():
     b.shape("cube", [])
     with pytest.raises(RuntimeError, match="no <sensor>"):
         b.finish()
+
+
+def _ply_with_normals(path, n=6):
+    """A small binary PLY grid with per-vertex normals (a bumped sheet)."""
+    import numpy as np
+    xs = np.linspace(-0.5, 0.5, n, dtype=np.float32)
+    X, Y = np.meshgrid(xs, xs)
+    Z = (0.1 * np.sin(3 * X) * np.cos(2 * Y)).astype(np.float32)
+    pos = np.stack([X.ravel(), Y.ravel(), Z.ravel()], 1).astype(np.float32)
+    nrm = np.stack([-0.3 * np.cos(3 * X.ravel()), 0.2 * np.sin(2 * Y.ravel()), np.ones(n * n)], 1)
+    nrm = (nrm / np.linalg.norm(nrm, axis=1, keepdims=True)).astype(np.float32)
+    faces = []
+    for j in range(n - 1):
+        for i in range(n - 1):
+            a, b, c, d = j * n + i, j * n + i + 1, (j + 1) * n + i + 1, (j + 1) * n + i
+            faces += [(a, b, c), (a, c, d)]
+    head = ("ply\nformat binary_little_endian 1.0\nelement vertex %d\nproperty float x\nproperty float y\n"
+            "property float z\nproperty float nx\nproperty float ny\nproperty float nz\nelement face %d\n"
+            "property list uchar int vertex_indices\nend_header\n" % (n * n, len(faces))).encode()
+    body = np.concatenate([pos, nrm], 1).astype("<f4").tobytes()
+    for f in faces:
+        body += np.uint8(3).tobytes() + np.array(f, "<i4").tobytes()
+    open(path, "wb").write(head + body)
+
+
+FLIP_XML = """<?xml version="1.0"?>
+<scene version="0.5.0">
+  <integer name="kdStopPrims" value="2"/>
+  <float name="kdEmptySpaceBonus" value="0.8"/>
+  <integrator type="path"><integer name="maxDepth" value="3"/></integrator>
+  <sensor type="perspective">
+    <transform name="toWorld"><lookat origin="0, 0, 3" target="0, 0, 0" up="0, 1, 0"/></transform>
+    <sampler type="independent"><integer name="sampleCount" value="2"/></sampler>
+    <film type="hdrfilm"><integer name="width" value="16"/><integer name="height" value="16"/></film>
+  </sensor>
+  <shape type="ply"><string name="filename" value="sheet.ply"/><boolean name="flipNormals" value="true"/>
+    <transform name="toWorld"><rotate y="1" angle="20"/><translate x="0.3"/></transform>
+    <bsdf type="diffuse"/></shape>
+  <shape type="ply"><string name="filename" value="sheet.ply"/><boolean name="faceNormals" value="true"/>
+    <boolean name="flipNormals" value="true"/>
+    <transform name="toWorld"><translate x="-0.4" z="-0.5"/></transform><bsdf type="diffuse"/></shape>
+  <shape type="ply"><string name="filename" value="sheet.ply"/><transform name="toWorld"><translate y="0.6"/></transform>
+    <bsdf type="diffuse"/></shape>
+  <shape type="rectangle"><transform name="toWorld"><translate z="2"/></transform>
+    <emitter type="area"><rgb name="radiance" value="5"/></emitter></shape>
+</scene>
+"""
+
+
+@pytest.mark.parametrize("meshes", ["arrays", "configured"])
+def test_flipped_meshes_and_scene_kd_properties_through_the_builder(tmp_path, meshes):
+    """mtsh_mesh's flip contract (include/mtsh.h): flip_normals is the normal
+    pass's m_flipNormals, applied by the builder to the arrays it is given.
+    Loader arrays with the flag ("arrays") and arrays that already carry the
+    flip, negated normals / a swapped face-normal winding, without it
+    ("configured", a configured TriMesh) both give the XML route's descriptor
+    byte for byte; the <scene> kd properties travel as the Scene's Properties."""
+    import mtsg
+    _ply_with_normals(str(tmp_path / "sheet.ply"))
+    xml = tmp_path / "flip.xml"
+    xml.write_text(FLIP_XML)
+    by_xml = mtsg.Scene(str(xml)).digest()
+    walker = W.Walker(str(xml), {}, meshes=meshes)
+    by_builder = walker.walk().digest()
+    assert "mesh" in walker.log and "scene_props" in walker.log
+    assert differing(by_xml, by_builder) == []
+    # without the scene's kd properties the tree differs (they reached the build)
+    plain = tmp_path / "plain.xml"
+    plain.write_text(FLIP_XML.replace('<integer name="kdStopPrims" value="2"/>', "")
+                     .replace('<float name="kdEmptySpaceBonus" value="0.8"/>', ""))
+    assert differing(by_xml, mtsg.Scene(str(plain)).digest()) != []

@@ -173,16 +173,15 @@ def test_energy_conservation_scaling(tmp_path):
     np.testing.assert_allclose(r, [0.99, 0.495, 0.2475], rtol=1e-6)
 
 
-def test_leaf_size_default_and_mitsuba_tree(monkeypatch):
+def test_leaf_size_default_and_mitsuba_tree():
     """The build stops at 4 primitives per leaf (GPU-tuned, host/scene.h);
-    MTSH_KD_STOP_PRIMS=6 gives Mitsuba's tree (gkdtree.h:738), which bench.py's
-    CPU baseline traverses.  Both trees answer the same closest hits."""
+    the Scene's kdStopPrims property (scene.cpp:64-65) = 6 gives Mitsuba's tree
+    (gkdtree.h:738), which bench.py's CPU baseline traverses.  Both trees
+    answer the same closest hits."""
     path = os.path.join(SCENES, "bunny15.xml")
     defs = {"width": 16, "height": 16, "spp": 1}
     tuned = mtsg.Scene(path, defs)
-    monkeypatch.setenv("MTSH_KD_STOP_PRIMS", "6")
-    mitsuba = mtsg.Scene(path, defs)
-    monkeypatch.delenv("MTSH_KD_STOP_PRIMS")
+    mitsuba = mtsg.Scene(path, defs, scene_props={"kdStopPrims": 6})
     assert mitsuba.info.kd_leaves < tuned.info.kd_leaves
     assert mitsuba.info.kd_indices < tuned.info.kd_indices
     rays = chords(20000, np.array([0.0, 0.45, 0.0]), 3.2, 5)
@@ -195,10 +194,57 @@ def test_leaf_size_default_and_mitsuba_tree(monkeypatch):
 
 def test_bench_cpu_baseline_uses_mitsubas_tree(bunny_small):
     """bench.py times its CPU baseline on the tree Mitsuba would build
-    (stopPrims 6), not on the GPU-tuned one, and restores the environment."""
+    (kdStopPrims 6, through the Scene's properties), not on the GPU-tuned one."""
     import bench
-    before = os.environ.get("MTSH_KD_STOP_PRIMS")
     m = bench.mitsuba_tree_scene(bunny_small)
-    assert os.environ.get("MTSH_KD_STOP_PRIMS") == before
     assert m.info.n_triangles == bunny_small.info.n_triangles
     assert m.info.kd_indices < bunny_small.info.kd_indices
+
+
+def _with_scene_props(tmp_path, body):
+    """cbox.xml with `body` (value elements) as <scene>-level children."""
+    src = open(os.path.join(SCENES, "cbox.xml")).read()
+    i = src.index(">", src.index("<scene")) + 1
+    p = tmp_path / "cbox_kd.xml"
+    p.write_text(src[:i] + body + src[i:])
+    return str(p)
+
+
+def test_scene_kd_properties_on_the_xml_route(tmp_path):
+    """<scene>'s kd properties (Scene::Scene, scene.cpp:47-83) reach the build:
+    kdStopPrims 12 makes fewer, larger leaves; the hits stay identical."""
+    defs = {"width": 16, "height": 16, "spp": 1}
+    base = mtsg.Scene(os.path.join(SCENES, "cbox.xml"), defs)
+    big = mtsg.Scene(_with_scene_props(tmp_path, '<integer name="kdStopPrims" value="12"/>'
+                                                 '<float name="kdTraversalCost" value="10"/>'
+                                                 '<boolean name="kdRetract" value="false"/>'), defs)
+    assert big.info.kd_leaves < base.info.kd_leaves
+    rng = np.random.default_rng(11)
+    n = 20000
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = rng.uniform(-0.95, 0.95, (n, 3))
+    d = rng.normal(size=(n, 3))
+    rays[:, 3:6] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 6] = 1e-4
+    rays[:, 7] = np.inf
+    t0, _, _, p0 = O.trace_closest(base.desc, rays)
+    t1, _, _, p1 = O.trace_closest(big.desc, rays)
+    assert np.array_equal(p0 != 0xFFFFFFFF, p1 != 0xFFFFFFFF)
+    np.testing.assert_array_equal(t0, t1)
+    # the same through the Scene properties a plugin passes (mtsh_scene_load_props)
+    via = mtsg.Scene(os.path.join(SCENES, "cbox.xml"), defs,
+                     scene_props={"kdStopPrims": 12, "kdTraversalCost": 10.0, "kdRetract": False})
+    assert via.digest() == big.digest()
+
+
+def test_scene_kd_properties_are_checked(tmp_path):
+    defs = {"width": 16, "height": 16, "spp": 1}
+    for body, msg in (('<integer name="kdStopPrim" value="12"/>', "unknown scene property"),
+                      ('<float name="kdStopPrims" value="12"/>', "must be of type integer"),
+                      ('<integer name="kdMaxDepth" value="99"/>', "kdMaxDepth")):
+        try:
+            mtsg.Scene(_with_scene_props(tmp_path, body), defs)
+        except RuntimeError as e:
+            assert msg in str(e), str(e)
+        else:
+            raise AssertionError("expected an error for " + body)

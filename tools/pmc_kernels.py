@@ -53,7 +53,18 @@ def per_kernel(path, counters):
 
 
 def main():
-    d, key = sys.argv[1], json.loads(sys.argv[2])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("key")
+    ap.add_argument("--frames-stats", type=int, default=0, help="frames the stats pass rendered (bench.py --pmc-pass)")
+    ap.add_argument("--frames-pass", type=int, default=0, help="frames each counter pass rendered")
+    ap.add_argument("--fetch-factor", type=float, default=2.0,
+                    help="FETCH_SIZE correction of the streaming kernels (MI355X_MICROARCH.md: x2 on gfx950)")
+    ap.add_argument("--fetch-factor-trace", type=float, default=None,
+                    help="correction for the traversal kernels' gathers (profiles/r06_fetch_calibration.txt)")
+    a = ap.parse_args()
+    d, key = a.dir, json.loads(a.key)
     fetch = per_kernel(os.path.join(d, "fetch_counter_collection.csv"), {"FETCH_SIZE"})
     write = per_kernel(os.path.join(d, "write_counter_collection.csv"), {"WRITE_SIZE"})
     tcc = per_kernel(os.path.join(d, "tcc_counter_collection.csv"), {"TCC_HIT_sum", "TCC_MISS_sum"})
@@ -69,19 +80,33 @@ def main():
         w = write[name].get("WRITE_SIZE", [])
         h, m = sum(tcc[name].get("TCC_HIT_sum", [])), sum(tcc[name].get("TCC_MISS_sum", []))
         k = {"launches_fetch_pass": len(f), "launches_write_pass": len(w)}
+        trace = name.startswith("k_trace_s") or name.startswith("k_tie") or name.startswith("k_finish")
+        factor = a.fetch_factor_trace if (trace and a.fetch_factor_trace is not None) else a.fetch_factor
         if f and w:
-            fb = 2 * 1024 * sum(f) / len(f)
+            fb = factor * 1024 * sum(f) / len(f)
             wb = 1024 * sum(w) / len(w)
-            k.update(fetch_bytes_per_launch=fb, write_bytes_per_launch=wb, traffic_bytes_per_launch=fb + wb,
-                     traffic_bytes_per_step=fb * len(f) + wb * len(w))
+            k.update(fetch_factor=factor, fetch_bytes_per_launch=fb, write_bytes_per_launch=wb,
+                     traffic_bytes_per_launch=fb + wb, traffic_bytes_per_pass=fb * len(f) + wb * len(w))
+            if a.frames_pass > 0:
+                k.update(launches_per_frame=len(f) / a.frames_pass,
+                         traffic_bytes_per_frame=(fb * len(f) + wb * len(w)) / a.frames_pass)
         if h + m > 0:
             k.update(tcc_hit_rate=round(h / (h + m), 4), tcc_launches=len(tcc[name].get("TCC_HIT_sum", [])))
         if name in stats:
             k["rocprof_stats"] = stats[name]
         kernels[name] = k
-    print(json.dumps({"key": key, "kernels": kernels,
-                      "note": "traffic = FETCH_SIZE x2 (gfx950) + WRITE_SIZE per launch, memory-side requests "
-                              "(Infinity-Cache hits included); tcc_hit_rate = TCC_HIT_sum / (HIT + MISS)"}, indent=1))
+    out = {"key": key, "kernels": kernels}
+    if a.frames_pass > 0:
+        out.update(frames_fetch_pass=a.frames_pass, frames_stats_pass=a.frames_stats)
+        for k in kernels.values():
+            if "rocprof_stats" in k and "launches_per_frame" in k:
+                k["rocprof_ms_per_frame"] = k["rocprof_stats"]["avg_ns"] * k["launches_per_frame"] / 1e6
+    print(json.dumps({**out,
+                      "note": "traffic = FETCH_SIZE x fetch_factor (per kernel: x2 for gfx950's streaming reads, "
+                              "the calibrated gather factor for the traversal, profiles/r06_fetch_calibration.txt) "
+                              "+ WRITE_SIZE per launch, memory-side requests (Infinity-Cache hits included); "
+                              "tcc_hit_rate = TCC_HIT_sum / (HIT + MISS); *_per_frame: the pass rendered "
+                              "frames_fetch_pass frames (bench.py --pmc-pass)"}, indent=1))
 
 
 if __name__ == "__main__":
