@@ -120,6 +120,11 @@ def parse():
                     help="profiler pass (tools/gpu_pmc_config.sh): render only this configuration's frame -- share 0 "
                          "of the stride deal when shares are emulated -- warmup + steps times, no balancing, no "
                          "whole-frame timing, no instrumented pass; prints the frame count")
+    ap.add_argument("--share-layout", default="spread", choices=["spread", "bands"],
+                    help="balanced shares cut runs of: the golden-ratio key order (spread over the frame) or the "
+                         "row-major key order (each share a band of tile rows, its XCD ranges sub-bands)")
+    ap.add_argument("--ray-order", type=int, default=-1, choices=[-1, 0, 1],
+                    help="MTSG_OPT_RAY_ORDER: 1 = bounce rays in direction-sorted windows, 0 = append order (default)")
     ap.add_argument("--shade-generic", action="store_true",
                     help="shade with the all-materials kernel instead of the scene's material set (A/B measurement)")
     return ap.parse_args()
@@ -428,6 +433,8 @@ def main():
         gpu.set_finish_paths(a.finish_paths)
     if a.shade_generic:
         gpu.set_option(mtsg.MTSG_OPT_SHADE_GENERIC, 1)
+    if a.ray_order >= 0:
+        gpu.set_option(mtsg.MTSG_OPT_RAY_ORDER, a.ray_order)
     W, H = params.tile_w + 2 * border, params.tile_h + 2 * border
     nbytes = W * H * 5 * 4
     film = gpu.alloc(nbytes)
@@ -449,7 +456,7 @@ def main():
     # balancing cuts runs of at least one tile per share: with fewer tiles
     # than shares the stride deal is used (a share may then be empty)
     balanced = n_shares > 1 and a.balance_rounds > 0 and n_tiles >= n_shares
-    order = mtsg.balance_order(n_tiles)
+    order = mtsg.balance_order(n_tiles) if a.share_layout == "spread" else np.arange(n_tiles, dtype=np.int32)
     counts = np.array([len(range(r, n_tiles, n_shares)) for r in range(n_shares)], dtype=np.int64)
     cur = {"keys": None}
 
@@ -551,7 +558,7 @@ def main():
             step()
             st = gpu.stats()
             if off == shares[0]:
-                for f in ("ms_trace_closest", "ms_trace_shadow", "ms_shade", "ms_camera", "ms_splat", "ms_total",
+                for f in ("ms_trace_closest", "ms_trace_shadow", "ms_shade", "ms_camera", "ms_splat", "ms_total", "ms_sort",
                           "rays_closest", "rays_shadow", "launches_trace_closest", "launches_trace_shadow",
                           "ms_finish", "paths_finish", "launches_finish"):
                     acc[f] = acc.get(f, 0) + getattr(st, f)
@@ -581,7 +588,7 @@ def main():
     kernels = {}
     if rank == 0:
         k = a.steps
-        kernels = {"trace_ms": (acc["ms_trace_closest"] + acc["ms_trace_shadow"]) / k,
+        kernels = {"trace_ms": (acc["ms_trace_closest"] + acc["ms_trace_shadow"]) / k, "sort_ms": acc["ms_sort"] / k,
                    "shade_ms": acc["ms_shade"] / k, "camera_ms": acc["ms_camera"] / k, "splat_ms": acc["ms_splat"] / k,
                    "frame_ms": acc["ms_total"] / k, "closest_rays": acc["rays_closest"] // k,
                    "shadow_rays": acc["rays_shadow"] // k,
@@ -769,7 +776,9 @@ def main():
                         "share's time (the N-GPU frame time without launch and gather overheads); kernels = share 0"}
                if a.emulate_ranks > 1 and world == 1 else {}),
             **({"balance": {"rounds": balance_log, "tiles_per_share": counts.tolist(),
-                            "method": "shares are runs of the golden-ratio key order (mtsg.balance_order); each "
+                            "layout": a.share_layout,
+                            "method": "shares are runs of the golden-ratio key order (mtsg.balance_order; "
+                                      "--share-layout bands: the row-major key order); each "
                                       "warm-up round times every share (the faster of two steps) and gives share r "
                                       "tiles in proportion to its measured rate, damped 1/2 (mtsg.balance_cuts); "
                                       "the timed steps use the last cut"}}

@@ -489,6 +489,8 @@ typedef struct mtsg_stats {
     /* ... and instance primitives the world-box prefilter skipped before any
      * entry (not counted in instance_visits)                                */
     uint64_t instance_prefiltered;
+    /* ms of the ray-order sorts (k_sortwin, MTSG_OPT_RAY_ORDER; MTSG_FLAG_TIMING) */
+    double ms_sort;
 } mtsg_stats;
 
 enum {
@@ -629,13 +631,18 @@ int  mtsg_set_finish_paths(mtsg_scene *scene, uint32_t paths);
  *   MTSG_OPT_STAGGER          bounces between the lanes' starts (0..16)
  *   MTSG_OPT_SHADE_GENERIC    1: shade with the kernel that holds every material
  *                             class instead of the scene's own set (A/B tests)
+ *   MTSG_OPT_RAY_ORDER        the order the traversal takes a bounce's rays in:
+ *                             0 (default) = the order they were appended in,
+ *                             1 = windows of 4096 rays sorted by direction
+ *                             (measured slower)
  * Unknown keys and values out of range return MTSG_ERR_INVALID. */
 enum {
     MTSG_OPT_TRACE_REFILL = 1,
     MTSG_OPT_FINISH_SHADE_MIN = 2,
     MTSG_OPT_LANES = 3,
     MTSG_OPT_STAGGER = 4,
-    MTSG_OPT_SHADE_GENERIC = 5
+    MTSG_OPT_SHADE_GENERIC = 5,
+    MTSG_OPT_RAY_ORDER = 6
 };
 int  mtsg_set_option(mtsg_scene *scene, int32_t key, int64_t value);
 
@@ -646,11 +653,15 @@ int  mtsg_set_option(mtsg_scene *scene, int32_t key, int64_t value);
  * (default 8; a large value turns the guard off, which can change results);
  * restart_limit >= 0 is the restart number that ends a ray with
  * MTSG_ERR_TRAVERSAL (default 511), applied to shadow rays only when
- * limit_shadow_only.  Any change selects separate kernel instantiations;
+ * limit_shadow_only; no_instance_prefilter turns the two-level world-box
+ * prefilter off.  Any change selects separate kernel instantiations;
  * NULL restores the defaults.  Production renders never call this: no
  * environment variable or other setting changes these limits. */
 typedef struct mtsg_test_knobs {
     int32_t stack_cap, restart_guard, restart_limit, limit_shadow_only;
+    int32_t no_instance_prefilter;   /* 1: the two-level traversal enters every instance primitive it meets */
+                                     /* (no world-box prefilter; kernels.h inst_box), to check that the     */
+                                     /* prefilter drops only entries the exact clip rejects                 */
 } mtsg_test_knobs;
 int  mtsg_set_test_knobs(mtsg_scene *scene, const mtsg_test_knobs *knobs);
 

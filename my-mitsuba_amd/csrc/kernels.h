@@ -85,6 +85,7 @@ struct DevScene {
     // beyond its exit distance; restart rstMax (rstMaxC for closest-hit
     // rays) ends the ray with SB_ERR
     uint32_t capFlat, capGrp, capTop, rstGuard, rstMax, rstMaxC;
+    uint32_t instPrefilter;   // test knob: 0 = the two-level world-box prefilter off (KNOBS kernels only)
     // two-level exact-tie keys: key + (instance + 1) * instKeyStride, where
     // the stride is the number of TriAccel keys when keys x (instances + 1)
     // fit 32 bits (one key per (primitive, instance) pair, no collisions)
@@ -164,6 +165,10 @@ struct DevPaths {
     float4 *sh_c;     // NEE contribution, target (bits): next-bounce position, or 1 << 31 | slot
     uint32_t *cnt;    // counters, each on its own 256-B line (see CNT_*)
     unsigned long long *ctr;  // traversal counters (nodes, refs, tests)
+    // closest rays of a trace launch in ray order (k_sortwin): work-list entry
+    // i is the ray at position order[i]; nullptr: entry i is position i
+    uint32_t *order;
+    uint32_t *orderBuf;   // the buffer k_sortwin fills (one entry per path)
 };
 
 // arguments of the per-sampler shading launchers (smp_kernels.hip)
@@ -287,7 +292,7 @@ constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 29;   // 148 GB of path state; C5
 #ifndef MTSG_LANES
 #define MTSG_LANES 1
 #endif
-constexpr size_t PATH_STATE_BYTES = 276;    // bytes per path slot (DevPaths: 2 x 96 dense + hit, L, 3 x shadow, tie)
+constexpr size_t PATH_STATE_BYTES = 280;    // bytes per path slot (DevPaths: 2 x 96 dense + hit, L, 3 x shadow, tie, order)
 #ifndef MTSG_SHORT_STACK
 #define MTSG_SHORT_STACK 6   // 6 x 12 B x 64 lanes = 4.6 KB LDS/wave -> 8 waves/SIMD (8: 6.5, 12: 4.2)
 #endif
@@ -567,11 +572,11 @@ constexpr uint32_t RST_GUARD = 8, RST_MAX = SB_RST_MASK;
 // stack capacities and restart limits of a traversal: compile-time constants
 // in the production kernels (KNOBS = false), the scene's test overrides
 // (DevScene::capFlat ...) in the KNOBS instantiations
-struct TravLimits { uint32_t capFlat, capGrp, capTop, rstGuard, rstMax, rstMaxC; };
+struct TravLimits { uint32_t capFlat, capGrp, capTop, rstGuard, rstMax, rstMaxC; bool prefilter; };
 template <bool KNOBS>
 DEV TravLimits trav_limits(const DevScene &S) {
-    if (KNOBS) return TravLimits{S.capFlat, S.capGrp, S.capTop, S.rstGuard, S.rstMax, S.rstMaxC};
-    return TravLimits{(uint32_t)SHORT_STACK, (uint32_t)INNER_STACK, (uint32_t)OUTER_STACK, RST_GUARD, RST_MAX, RST_MAX};
+    if (KNOBS) return TravLimits{S.capFlat, S.capGrp, S.capTop, S.rstGuard, S.rstMax, S.rstMaxC, S.instPrefilter != 0};
+    return TravLimits{(uint32_t)SHORT_STACK, (uint32_t)INNER_STACK, (uint32_t)OUTER_STACK, RST_GUARD, RST_MAX, RST_MAX, true};
 }
 
 // kd-restart after the stack ran empty with entries dropped (Foley &
@@ -1343,7 +1348,7 @@ DEV bool spec_iter_i(const DevScene &S, SpecRay &r, TraceCounts &cnt, const DevP
         const bool isInst = enter;
 #if MTSG_INST_PREFILTER
         if (isInst) {
-            enter = inst_box(r, f0, f1);
+            enter = !L.prefilter || inst_box(r, f0, f1);
             if (COUNT && !enter) atomicAdd(P.ctr + 59, 1ull);   // stats.instance_prefiltered
         }
 #endif
@@ -1614,6 +1619,119 @@ __attribute__((noinline)) DEV void tie_retrace_i(const DevScene &S, const DevPat
 //   cIn: -1 = nIdentity closest rays (bounce 0), 0/1 = count in cnt_q(cIn), -2 = none
 //   sIn: 0/1 = count in CNT_S0/CNT_S1, -1 = none
 
+// ---------------------------------------------------------------------------
+// Ray order of a bounce (round 6).  The closest rays of bounce b >= 1 sit in
+// the order k_shade appended them: tile-major, so consecutive rays start from
+// neighbouring surface points of one 16x16 tile, at successive samples -- but
+// leave in directions spread over the BSDF lobes.  Rays taken in a random
+// order instead cost the C3 traversal 2.2x on the camera rays and +33% on
+// bounce 1 (profiles/r06_ray_order.txt: the order's locality is what keeps the
+// node and TriAccel fetches in L1/L2).  k_sortwin sorts each window of
+// SORT_WINDOW consecutive rays (16 samples of one tile) by an octahedral
+// direction bin, so a wave's refills take rays from one tile that also leave
+// in one direction cone; the traversal reads entry i from position order[i]
+// and writes its hit there, so shading keeps its dense order and the image
+// does not change (random numbers are keyed by pixel and sample).  Measured:
+// the sorted windows lose (C3 trace +6.7 ms): the production default is the
+// append order (MTSG_OPT_RAY_ORDER 0); the sort stays as that option.
+// ---------------------------------------------------------------------------
+#ifndef MTSG_SORT_WINDOW
+#define MTSG_SORT_WINDOW 4096
+#endif
+#ifndef MTSG_SORT_BINS_LOG
+#define MTSG_SORT_BINS_LOG 4   // 16 x 16 octahedral bins (~11 degrees)
+#endif
+constexpr uint32_t SORT_WINDOW = MTSG_SORT_WINDOW;
+constexpr int SORT_BLOCK = 1024;
+constexpr int SORT_BINS = 1 << (2 * MTSG_SORT_BINS_LOG);
+static_assert(SORT_BINS <= SORT_BLOCK && SORT_WINDOW % SORT_BLOCK == 0, "k_sortwin layout");
+// octahedral map of a direction (any length) to one of SORT_BINS cells
+DEV uint32_t dir_bin(float3 d) {
+    const float s = 1.0f / (fabsf(d.x) + fabsf(d.y) + fabsf(d.z));
+    float u = d.x * s, v = d.y * s;
+    if (d.z < 0.0f) {
+        const float uu = (1.0f - fabsf(v)) * (u < 0.0f ? -1.0f : 1.0f), vv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
+        u = uu;
+        v = vv;
+    }
+    constexpr int n = 1 << MTSG_SORT_BINS_LOG;
+    const int iu = min(n - 1, max(0, (int)((u * 0.5f + 0.5f) * (float)n)));
+    const int iv = min(n - 1, max(0, (int)((v * 0.5f + 0.5f) * (float)n)));
+    return (uint32_t)(iv * n + iu);
+}
+// one window per workgroup iteration: an LDS counting sort of its rays by
+// direction bin (rank within a bin from an LDS atomic: any order of a bin's
+// rays is as good), then order[window + slot] = the ray's position
+__global__ void __launch_bounds__(SORT_BLOCK) k_sortwin(DevPaths P, int qin) {
+    __shared__ uint32_t hist[SORT_BINS];
+    __shared__ uint32_t waveSum[SORT_BLOCK / 64];
+    constexpr int PER = (int)SORT_WINDOW / SORT_BLOCK;
+    const uint32_t n = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t w0 = blockIdx.x * SORT_WINDOW; w0 < n; w0 += gridDim.x * SORT_WINDOW) {
+        for (uint32_t k = tid; k < (uint32_t)SORT_BINS; k += SORT_BLOCK) hist[k] = 0u;
+        __syncthreads();
+        uint32_t key[PER], rank[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t pos = w0 + (uint32_t)j * SORT_BLOCK + tid;
+            key[j] = 0u;
+            rank[j] = 0u;
+            if (pos < n) {
+                key[j] = dir_bin(xyz(P.ray_d[pos]));
+                rank[j] = atomicAdd(&hist[key[j]], 1u);
+            }
+        }
+        __syncthreads();
+        // exclusive prefix sum of the bins: a wave scan per 64 bins, then the
+        // waves' totals
+        uint32_t v = 0u, incl = 0u;
+        if (tid < (uint32_t)SORT_BINS) {
+            v = hist[tid];
+            incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o);
+                if (__lane_id() >= (uint32_t)o) incl += t;
+            }
+            if (__lane_id() == 63u) waveSum[tid >> 6] = incl;
+        }
+        __syncthreads();
+        if (tid < (uint32_t)SORT_BINS) {
+            uint32_t before = 0u;
+            for (uint32_t w = 0; w < (tid >> 6); ++w) before += waveSum[w];
+            hist[tid] = before + incl - v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t pos = w0 + (uint32_t)j * SORT_BLOCK + tid;
+            if (pos < n) P.orderBuf[w0 + hist[key[j]] + rank[j]] = pos;
+        }
+        __syncthreads();
+    }
+}
+
+// MTSG_SHUFFLE (measurement variant, round 6): the traversal takes its rays in
+// a random order -- 1: closest rays, 2: shadow rays too -- to measure what the
+// work list's order (tile-major camera rays, append-ordered bounce rays) is
+// worth to the traversal: a bijection of [0, n) (cycle-walking over a
+// multiply / xor-shift bijection of the enclosing power of two)
+#ifndef MTSG_SHUFFLE
+#define MTSG_SHUFFLE 0
+#endif
+DEV uint32_t shuffle_index(uint32_t x, uint32_t n) {
+    if (n < 2) return x;
+    const uint32_t m = 32u - __clz(n - 1u), mask = m >= 32 ? 0xFFFFFFFFu : (1u << m) - 1u;
+    do {
+        x = (x * 0x9E3779B1u + 0x7F4A7C15u) & mask;
+        x ^= x >> ((m + 1) / 2);
+        x = (x * 0x85EBCA6Bu) & mask;
+        x ^= x >> ((m + 2) / 3);
+    } while (x >= n);
+    return x;
+}
+
 template <bool COUNT, int MIN_IDLE, bool INST = false, bool KNOBS = false>
 __global__ void __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(INST ? (COUNT ? 1 : MTSG_INST_WAVES) : MTSG_SPEC_WAVES)))
 k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned long long *wt) {
@@ -1651,7 +1769,11 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
             if (!active && rank < take) {
                 const uint32_t i = poolBase + rank;
                 const bool shadow = i >= nC;
-                idx = shadow ? i - nC : i;
+                idx = shadow ? i - nC : (P.order ? P.order[i] : i);
+#if MTSG_SHUFFLE
+                // measurement: the work list in a random order (coherence experiment)
+                if (!shadow || MTSG_SHUFFLE == 2) idx = shuffle_index(idx, shadow ? nS : nC);
+#endif
                 float4 ro = ldS((shadow ? P.sh_o : P.ray_o) + idx), rd = ldS((shadow ? P.sh_d : P.ray_d) + idx);
                 if (shadow) { const float mint = rd.w; rd.w = ro.w; ro.w = mint; }   // sh_o.w = maxt, sh_d.w = mint
                 if (spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, shadow, r)) {
@@ -1773,6 +1895,22 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
 // ---------------------------------------------------------------------------
 // camera rays (PerspectiveCamera::sampleRayDifferential, perspective.cpp:271-298)
 // ---------------------------------------------------------------------------
+// pixel of position `pix` (0..255) inside a 16x16 tile: in Z order, so that
+// 16 consecutive slots -- one refill of a traversal wave -- are a 4x4 pixel
+// block instead of a 16x1 row (measured r06: C3 +0.2%, the slowest 1/8 share
+// 22.04 -> 21.70 ms; MTSG_TILE_MORTON=0: row-major)
+#ifndef MTSG_TILE_MORTON
+#define MTSG_TILE_MORTON 1
+#endif
+__host__ __device__ inline void tile_pix(uint32_t pix, int &lx, int &ly) {
+#if MTSG_TILE_MORTON
+    lx = (int)((pix & 1u) | ((pix >> 1) & 2u) | ((pix >> 2) & 4u) | ((pix >> 3) & 8u));
+    ly = (int)(((pix >> 1) & 1u) | ((pix >> 2) & 2u) | ((pix >> 3) & 4u) | ((pix >> 4) & 8u));
+#else
+    lx = (int)(pix % TILE);
+    ly = (int)(pix / TILE);
+#endif
+}
 DEV void slot_pixel(const DevBatch &B, uint32_t slot, int &x, int &y, uint32_t &s) {
     const uint32_t pix = slot & (TILE * TILE - 1);
     const uint32_t rest = slot >> 8;
@@ -1780,8 +1918,10 @@ DEV void slot_pixel(const DevBatch &B, uint32_t slot, int &x, int &y, uint32_t &
     const uint32_t tl = rest / B.ns;
     int tx, ty;
     tile_of_key(batch_key(B, B.tile0 + (int)tl), B.tiles_x, tx, ty, B.skew);
-    x = B.rect_x + tx * TILE + (int)(pix % TILE);
-    y = B.rect_y + ty * TILE + (int)(pix / TILE);
+    int lx, ly;
+    tile_pix(pix, lx, ly);
+    x = B.rect_x + tx * TILE + lx;
+    y = B.rect_y + ty * TILE + ly;
     s = B.s0 + sl;
 }
 
@@ -3289,6 +3429,63 @@ constexpr int SHADE_LDS_BSDFS = 4, SHADE_LDS_EMITTERS = 16;
 #else
 #define SHADE_ATTR(ENV, MATS) __launch_bounds__(SHADE_BLOCK)
 #endif
+// Event order inside a workgroup (round 6): a wave runs the union of the code
+// paths its lanes take, so a wave that mixes an environment miss, a
+// dielectric hit and a smooth hit with next-event estimation pays all three.
+// Before shading, each workgroup classifies its 256 paths -- dead slot, miss,
+// or the BSDF class of the hit (dielectric / diffuse / roughconductor /
+// other: path.cpp:145-264 dispatches on these) -- and hands them to its
+// threads sorted by class, so most waves shade one kind of event: the
+// per-material queues of SURVEY §7 step 6, kept inside the workgroup so the
+// path state stays dense (the gathers stay within the workgroup's 256
+// positions).  Which thread shades a path changes nothing in its arithmetic.
+#ifndef MTSG_SHADE_SORT
+#define MTSG_SHADE_SORT 1
+#endif
+// measured r06 (profiles/r06_shade_sort.txt): C5 shade 424 -> 410 ms; where
+// the events barely diverge the classification only costs (C2, diffuse only:
+// +3.0 ms; C3, no environment: +1.2 ms shade, -1.2 ms trace), so the sort is
+// compiled into the kernels of scenes with an environment emitter (misses and
+// environment sampling are their expensive events) and several classes
+template <bool ENV, int MATS>
+constexpr bool shade_sorted() { return MTSG_SHADE_SORT && ENV && (MATS & (MATS - 1)) != 0; }
+constexpr int SHADE_CLASSES = 6;
+DEV uint32_t shade_class(const DevScene &S, const DevPaths &P, uint32_t i, bool first, const ShadeTables &tb) {
+    if (first && P.meta[i].x == 0u) return 0u;   // dead slot (bounce 0)
+    const uint32_t p = __float_as_uint(P.hit[i].w);
+    if (p == 0xFFFFFFFFu) return 1u;
+    const uint32_t bsdf = !(p & 0x80000000u) ? __float_as_uint(S.shrec[6 * (size_t)p + 5].z) & 0x7FFFFFFFu
+                                             : __float_as_uint(S.rectSh[2 * (size_t)(p & 0x7FFFFFFFu) + 1].w) & 0xFFFFu;
+    const int t = tb.bsdfs[bsdf].type;
+    return t == MTSG_BSDF_DIELECTRIC ? 2u : t == MTSG_BSDF_DIFFUSE ? 3u : t == MTSG_BSDF_ROUGHCONDUCTOR ? 4u : 5u;
+}
+// the workgroup's counting sort by class: returns the offset (within the
+// workgroup's 256 positions) of the path this thread shades
+DEV uint32_t shade_sort(uint32_t cls, uint32_t *cnt, uint16_t *perm) {
+    const uint32_t tid = threadIdx.x;
+    if (tid < (uint32_t)SHADE_CLASSES) cnt[tid] = 0u;
+    __syncthreads();
+    const unsigned long long below = (1ull << lane_id()) - 1ull;
+    uint32_t rank = 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)SHADE_CLASSES; ++k) {
+        const unsigned long long m = __ballot(cls == k);
+        uint32_t w = 0u;
+        if (m && lane_id() == 0) w = atomicAdd(&cnt[k], (uint32_t)__popcll(m));
+        w = __shfl(w, 0);
+        if (cls == k) rank = w + (uint32_t)__popcll(m & below);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0u;
+        for (int k = 0; k < SHADE_CLASSES; ++k) { const uint32_t c = cnt[k]; cnt[k] = run; run += c; }
+    }
+    __syncthreads();
+    perm[cnt[cls] + rank] = (uint16_t)tid;
+    __syncthreads();
+    return perm[tid];
+}
+
 // ENV: the scene has an environment emitter (the variant without it keeps
 // the environment code, and its registers, out of the common case)
 // SMP: the render's sampler (MTSG_SAMPLER_*)
@@ -3302,6 +3499,9 @@ __global__ void SHADE_ATTR(ENV, MATS) k_shade(DevScene S, DevIntegrator I, DevBa
                                                  uint32_t nIdentity, int hasAlpha) {
     __shared__ BlockAppend ba;
     __shared__ ShadeStage stage;
+    constexpr bool SORT = shade_sorted<ENV, MATS>();
+    __shared__ uint32_t s_classCnt[SHADE_CLASSES];
+    __shared__ uint16_t s_perm[SORT ? SHADE_BLOCK : 1];
 #if MTSG_SHADE_LDS_PAD
     // measurement: unused LDS that caps the workgroups per CU
     __shared__ uint32_t s_shadePad[MTSG_SHADE_LDS_PAD / 4];
@@ -3331,7 +3531,10 @@ __global__ void SHADE_ATTR(ENV, MATS) k_shade(DevScene S, DevIntegrator I, DevBa
     const int qout = qin < 0 ? 1 : (qin ^ 1);
     const bool first = FIRST == 2 ? bounce == 0 : FIRST == 1;
     for (uint32_t it = 0; it < nIter; ++it) {
-        const uint32_t i = (it * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+        const uint32_t i0 = (it * gridDim.x + blockIdx.x) * blockDim.x;
+        uint32_t i = i0 + threadIdx.x;
+        if constexpr (SORT)
+            i = i0 + shade_sort(i < count ? shade_class(S, P, i, first, tb) : 0u, s_classCnt, s_perm);
         bool alive = i < count;
         bool cont = false, shadow = false;
         uint4 meta = make_uint4(0u, 0u, 0u, 0u);
@@ -3557,7 +3760,8 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
     const int x0 = B.rect_x + tx * TILE, y0 = B.rect_y + ty * TILE;   // tile origin (film coords)
     const int bord = C.border;
     const int pix = threadIdx.x;
-    const int lx = pix % TILE, ly = pix / TILE;
+    int lx, ly;
+    tile_pix((uint32_t)pix, lx, ly);
     const int x = x0 + lx, y = y0 + ly;
     const bool inside = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
     // block (tile rect + border) bounds relative to the window origin (x - R, y - R)

@@ -97,6 +97,8 @@ struct mtsg_scene {
     int samplerType = MTSG_SAMPLER_INDEPENDENT, samplerDim = 4;
     int qmcInv[2][3] = {{0, 0, 0}, {0, 0, 0}};
     int traceMode = 0;            // 0: refill at 16 idle lanes (measured best), 1: at 32
+    int rayOrder = 0;             // MTSG_OPT_RAY_ORDER: 1 = bounce rays sorted per window by direction (k_sortwin;
+                                  // measured r06: C3 trace +6.7 ms, profiles/r06_ray_order.txt)
     float *dumpL = nullptr;
     std::atomic<int> cancel{0};
     bool knobs = false;   // traversal test overrides set (mtsg_set_test_knobs): KNOBS kernels, no tail mode
@@ -150,6 +152,8 @@ int ensure_batch(mtsg_scene *s, uint32_t paths, int lanes) {
     A(hit, float4); A(L, float4); A(sh_o, float4); A(sh_d, float4); A(sh_c, float4);
     if (s->ds.inst) { A(hitInst, uint32_t); } else P.hitInst = nullptr;
     A(tie, uint32_t);
+    A(orderBuf, uint32_t);
+    P.order = nullptr;
 #undef A
     if ((rc = alloc(CNT_WORDS * sizeof(uint32_t), (void **)&P.cnt)) != MTSG_OK) return rc;
     if ((rc = alloc(CTR_WORDS * sizeof(unsigned long long), (void **)&P.ctr)) != MTSG_OK) return rc;
@@ -160,7 +164,7 @@ int ensure_batch(mtsg_scene *s, uint32_t paths, int lanes) {
     return MTSG_OK;
 }
 
-enum { K_CAMERA = 0, K_CLOSEST, K_SHADOW, K_SHADE, K_SPLAT, K_FINISH };
+enum { K_CAMERA = 0, K_CLOSEST, K_SHADOW, K_SHADE, K_SPLAT, K_FINISH, K_SORT };
 
 // the survivors k_shade compacted into n_* are the next bounce's paths
 void swap_bounce(DevPaths &P) {
@@ -527,7 +531,16 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
                 const int qin = b == 0 ? -1 : (b & 1);
                 const int qout = (b & 1) ^ 1;
                 hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, st, P.cnt, qout, b & 1);
-                timed_launch(s, K_CLOSEST, st, [&]() { launch_trace(s, count, P, qin, b == 0 ? -1 : ((b - 1) & 1), L.B.nslots, st); });
+                // bounce rays in direction-sorted windows (k_sortwin); the
+                // camera rays keep their tile order
+                DevPaths PT = P;
+                if (b >= 1 && s->rayOrder == 1) {
+                    timed_launch(s, K_SORT, st, [&]() {
+                        hipLaunchKernelGGL(k_sortwin, dim3(s->cuCount * 2), dim3(SORT_BLOCK), 0, st, P, qin);
+                    });
+                    PT.order = P.orderBuf;
+                }
+                timed_launch(s, K_CLOSEST, st, [&]() { launch_trace(s, count, PT, qin, b == 0 ? -1 : ((b - 1) & 1), L.B.nslots, st); });
                 if (useFinish && b >= 1) {
                     // the count of this bounce's paths is known once bounce b-1 is
                     // done (the GPU meanwhile runs this bounce's trace): few left ->
@@ -639,7 +652,9 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
                 const uint32_t sl = rest % B.ns, tl = rest / B.ns;
                 int tx, ty;
                 tile_of_key(hostKey(B.tile0 + (int)tl), B.tiles_x, tx, ty, B.skew);
-                const int x = tx * TILE + (int)(pix % TILE), y = ty * TILE + (int)(pix / TILE);
+                int lx, ly;
+                tile_pix(pix, lx, ly);
+                const int x = tx * TILE + lx, y = ty * TILE + ly;
                 if (x >= p->tile_w || y >= p->tile_h) continue;
                 float *o = s->dumpL + (((size_t)y * p->tile_w + x) * p->spp + B.s0 + sl) * 4;
                 o[0] = L[slot].x; o[1] = L[slot].y; o[2] = L[slot].z; o[3] = L[slot].w;
@@ -677,6 +692,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
                 case K_SHADE: s->stats.ms_shade += ms; break;
                 case K_SPLAT: s->stats.ms_splat += ms; break;
                 case K_FINISH: s->stats.ms_finish += ms; break;
+                case K_SORT: s->stats.ms_sort += ms; break;
             }
         }
     }
@@ -1048,6 +1064,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     ds.rstGuard = RST_GUARD;
     ds.rstMax = RST_MAX;
     ds.rstMaxC = RST_MAX;
+    ds.instPrefilter = 1;
     s->knobs = false;
     // two-level tie keys (kernels.h spec_iter_i): the TriAccel key count as
     // the per-instance stride, so keys of different (primitive, instance)
@@ -1277,10 +1294,11 @@ int mtsg_set_test_knobs(mtsg_scene *s, const mtsg_test_knobs *k) {
         if (k->restart_limit >= 0) ds.rstMax = std::min<uint32_t>(RST_MAX, (uint32_t)k->restart_limit);
     }
     ds.rstMaxC = (k && k->limit_shadow_only) ? RST_MAX : ds.rstMax;
+    ds.instPrefilter = (k && k->no_instance_prefilter) ? 0u : 1u;
     // any change selects the KNOBS kernel instantiations (the production
     // kernels keep their compile-time constants) and turns the tail kernel off
     s->knobs = ds.capFlat != (uint32_t)SHORT_STACK || ds.capGrp != (uint32_t)INNER_STACK || ds.capTop != (uint32_t)OUTER_STACK ||
-               ds.rstGuard != RST_GUARD || ds.rstMax != RST_MAX || ds.rstMaxC != RST_MAX;
+               ds.rstGuard != RST_GUARD || ds.rstMax != RST_MAX || ds.rstMaxC != RST_MAX || !ds.instPrefilter;
     return MTSG_OK;
 }
 
@@ -1311,6 +1329,10 @@ int mtsg_set_option(mtsg_scene *s, int32_t key, int64_t value) {
             return MTSG_OK;
         case MTSG_OPT_SHADE_GENERIC:
             s->shadeGeneric = value != 0;
+            return MTSG_OK;
+        case MTSG_OPT_RAY_ORDER:
+            if (value < 0 || value > 1) { g_err = "MTSG_OPT_RAY_ORDER: 0 (append order) or 1 (direction-sorted windows)"; return MTSG_ERR_INVALID; }
+            s->rayOrder = (int)value;
             return MTSG_OK;
         default:
             g_err = "unknown option key " + std::to_string(key);

@@ -33,6 +33,7 @@ MTSG_OPT_FINISH_SHADE_MIN = 2
 MTSG_OPT_LANES = 3
 MTSG_OPT_STAGGER = 4
 MTSG_OPT_SHADE_GENERIC = 5
+MTSG_OPT_RAY_ORDER = 6
 
 
 class RenderParams(C.Structure):
@@ -56,7 +57,7 @@ class RenderParams(C.Structure):
 class TestKnobs(C.Structure):
     """mtsg_test_knobs (TEST ONLY: the traversal's stack sizes and restart guard)."""
     _fields_ = [("stack_cap", C.c_int32), ("restart_guard", C.c_int32), ("restart_limit", C.c_int32),
-                ("limit_shadow_only", C.c_int32)]
+                ("limit_shadow_only", C.c_int32), ("no_instance_prefilter", C.c_int32)]
 
 
 class Stats(C.Structure):
@@ -85,6 +86,7 @@ class Stats(C.Structure):
         ("guard_steps_closest", C.c_uint64), ("guard_steps_shadow", C.c_uint64),
         ("restarts_closest", C.c_uint64), ("restarts_shadow", C.c_uint64),
         ("instance_rejects", C.c_uint64), ("instance_prefiltered", C.c_uint64),
+        ("ms_sort", C.c_double),
     ]
 
 
@@ -841,10 +843,10 @@ class GPUScene:
         self._check(device_lib().mtsg_set_batch_paths(self._h, n), "mtsg_set_batch_paths")
 
     def set_test_knobs(self, stack_cap: int = 0, restart_guard: int = -1, restart_limit: int = -1,
-                       limit_shadow_only: bool = False) -> None:
+                       limit_shadow_only: bool = False, no_instance_prefilter: bool = False) -> None:
         """TEST ONLY (mtsg_set_test_knobs): shrink the traversal stacks / move
         the kd-restart guard; the defaults restore the production limits."""
-        k = TestKnobs(stack_cap, restart_guard, restart_limit, int(limit_shadow_only))
+        k = TestKnobs(stack_cap, restart_guard, restart_limit, int(limit_shadow_only), int(no_instance_prefilter))
         self._check(device_lib().mtsg_set_test_knobs(self._h, C.byref(k)), "mtsg_set_test_knobs")
 
     def set_finish_paths(self, n: int) -> None:

@@ -184,6 +184,22 @@ def test_material_kernels_match_the_generic_kernel(name):
     assert np.array_equal(spec, gen, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(spec - gen))}"
 
 
+@pytest.mark.parametrize("name", ["cbox.xml", "bunny15.xml", "env_glass.xml"])
+def test_ray_order_does_not_change_samples(name):
+    # the traversal takes bounce rays in direction-sorted windows
+    # (MTSG_OPT_RAY_ORDER 1, k_sortwin) or in append order (0): the hit of a
+    # ray does not depend on when it is traced, so every sample is bit-identical
+    scene = mtsg.Scene(os.path.join(SCENES, name), {"width": 80, "height": 64, "spp": 8})
+    p = scene.params()
+    g = mtsg.GPUScene(scene, 0)
+    g.set_option(mtsg.MTSG_OPT_RAY_ORDER, 1)
+    sorted_ = g.render_samples(p)
+    g.set_option(mtsg.MTSG_OPT_RAY_ORDER, 0)
+    plain = g.render_samples(p)
+    g.close()
+    assert np.array_equal(sorted_, plain, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(sorted_ - plain))}"
+
+
 def test_set_option_rejects_unknown_keys_and_values(cbox_small):
     g = mtsg.GPUScene(cbox_small, 0)
     for key, value in ((99, 1), (mtsg.MTSG_OPT_LANES, 0), (mtsg.MTSG_OPT_TRACE_REFILL, 20)):

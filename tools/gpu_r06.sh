@@ -14,6 +14,7 @@ Q="--no-cpu --no-parity"
 for w in ${*:-tests bench}; do
   case $w in
     tests) step tests 900 $PYT tests ;;
+    tfar-*) v=${w#tfar-}; MTSG_LIB=$(lib $v) step $w 300 $PYT tests/test_gpu_instancing.py -k far_away ;;
     tests-parity) step tests-parity 600 $PYT tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_c4.py ;;
     tests-inst) step tests-inst 600 $PYT tests/test_gpu_instancing.py tests/test_gpu_edge_rays.py tests/test_gpu_finish.py ;;
     vtests-*) v=${w#vtests-}; MTSG_LIB=$(lib $v) step $w 900 $PYT tests ;;
@@ -24,6 +25,16 @@ for w in ${*:-tests bench}; do
     q-*) v=${w#q-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 10 --warmup 3 $Q --no-count ;;
     iq-*) v=${w#iq-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level $Q ;;
     c5q-*) v=${w#c5q-}; MTSG_LIB=$(lib $v) step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count ;;
+    # the shading event sort A/B, both in append order
+    ssq-*) v=${w#ssq-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 10 --warmup 3 $Q --no-count --ray-order 0 ;;
+    ssc5-*) v=${w#ssc5-}; MTSG_LIB=$(lib $v) step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --ray-order 0 ;;
+    ssc2-*) v=${w#ssc2-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 5 --warmup 2 --workload cbox $Q --no-count --ray-order 0 ;;
+    qro0) step qro0 300 python bench.py --steps 10 --warmup 3 $Q --ray-order 0 ;;
+    c5ro0) step c5ro0 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --ray-order 0 ;;
+    e8bands*) step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 $Q --no-count --share-layout bands --balance-rounds 6 ;;
+    e8spread*) step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 $Q --no-count --balance-rounds 6 ;;
+    e8ro0) step e8ro0 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 $Q --no-count --ray-order 0 ;;
+    ktro0) step ktro0 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt_ro0 -o kt -- python3 bench.py --pmc-pass $Q --no-count --steps 1 --warmup 1 --ray-order 0 ;;
     c5g) step c5g 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --shade-generic ;;
     qg) step qg 300 python bench.py --steps 10 --warmup 3 $Q --no-count --shade-generic ;;
     c2q-*) v=${w#c2q-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 5 --warmup 2 --workload cbox $Q --no-count ;;
@@ -34,6 +45,12 @@ for w in ${*:-tests bench}; do
     e8) step e8 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 --no-cpu --no-parity ;;
     stats-c3) step stats-c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-parity --no-count ;;
     stats-c5) step stats-c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o c5 -- python3 bench.py --steps 2 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 --no-cpu --no-parity --no-count ;;
+    # per-launch kernel durations of one frame (tools/launch_times.py)
+    kt-*) v=${w#kt-}; MTSG_LIB=$(lib $v) step $w 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt_$v -o kt -- python3 bench.py --pmc-pass $Q --no-count --steps 1 --warmup 1 ;;
+    kte8-*) v=${w#kte8-}; MTSG_LIB=$(lib $v) step $w 300 rocprofv3 --kernel-trace --output-format csv -d $O/kte8_$v -o kt -- python3 bench.py --pmc-pass --emulate-ranks 8 $Q --no-count --steps 1 --warmup 1 ;;
+    kti-*) v=${w#kti-}; MTSG_LIB=$(lib $v) step $w 300 rocprofv3 --kernel-trace --output-format csv -d $O/kti_$v -o kt -- python3 bench.py --pmc-pass --instancing two-level $Q --no-count --steps 1 --warmup 1 ;;
+    # FETCH_SIZE against known bytes for streams and gathers (tools/fetch_calib.hip)
+    calib) step calib 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/calib -o calib -- tools/fetch_calib ;;
     pmc-c3) bash tools/gpu_pmc_config.sh r06 c3 || exit $? ;;
     pmc-inst) bash tools/gpu_pmc_config.sh r06 c3_two_level --instancing two-level || exit $? ;;
     pmc-c5) bash tools/gpu_pmc_config.sh r06 c5 --workload c5 --width 1920 --height 1080 --spp 1024 || exit $? ;;
