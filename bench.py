@@ -61,10 +61,13 @@ def pmc_key(a, world=1):
     the workload, its size and share, the batch and tail-kernel settings and
     the device library's build -- counters of another build or batch size
     describe other launches and are never quoted."""
-    return {"workload": a.workload, "instancing": a.instancing, "kd_build": a.kd_build, "width": a.width,
-            "height": a.height, "spp": a.spp, "share": max(world, a.emulate_ranks, 1),
-            "batch_paths": a.batch_paths or 0, "finish_paths": a.finish_paths,
-            "balance_rounds": a.balance_rounds if max(world, a.emulate_ranks, 1) > 1 else 0, "build": device_build_id()}
+    key = {"workload": a.workload, "instancing": a.instancing, "kd_build": a.kd_build, "width": a.width,
+           "height": a.height, "spp": a.spp, "share": max(world, a.emulate_ranks, 1),
+           "batch_paths": a.batch_paths or 0, "finish_paths": a.finish_paths,
+           "balance_rounds": a.balance_rounds if max(world, a.emulate_ranks, 1) > 1 else 0, "build": device_build_id()}
+    if getattr(a, "kd_props", ""):
+        key["kd_props"] = a.kd_props   # another tree: other launches
+    return key
 
 
 def pmc_lookup(key, directory=None):
@@ -125,6 +128,9 @@ def parse():
                          "row-major key order (each share a band of tile rows, its XCD ranges sub-bands)")
     ap.add_argument("--ray-order", type=int, default=-1, choices=[-1, 0, 1],
                     help="MTSG_OPT_RAY_ORDER: 1 = bounce rays in direction-sorted windows, 0 = append order (default)")
+    ap.add_argument("--kd-props", default="",
+                    help="scene kd-tree properties for the build, k=v[,k=v] (scene.cpp:47-83 names: "
+                         "kdIntersectionCost, kdTraversalCost, kdEmptySpaceBonus, kdStopPrims, ...; measurement)")
     ap.add_argument("--shade-generic", action="store_true",
                     help="shade with the all-materials kernel instead of the scene's material set (A/B measurement)")
     return ap.parse_args()
@@ -404,10 +410,16 @@ def main():
 
     path, defs = scene_args(a)
     t_load = time.time()
-    scene = mtsg.Scene(path, defs, instancing=a.instancing)
+    kd_props = {}
+    for kv in filter(None, a.kd_props.split(",")):
+        k, v = kv.split("=", 1)
+        kd_props[k.strip()] = float(v) if "Cost" in k or "Bonus" in k else int(v)
+    scene = mtsg.Scene(path, defs, instancing=a.instancing, scene_props=kd_props or None)
     load_s = time.time() - t_load
     kd_info = {"kd_build": "host", "kd_build_ms": round(scene.info.kd_build_seconds * 1e3, 1), "kd_refs": scene.info.kd_indices,
-               "kd_stop_prims": 4}   # the build's GPU-tuned default; Mitsuba: 6
+               "kd_stop_prims": kd_props.get("kdStopPrims", 4)}   # the build's GPU-tuned default; Mitsuba: 6
+    if kd_props:
+        kd_info["kd_props"] = kd_props
     if a.kd_build == "device":
         mtsg.kd_build(scene, device=dev)   # warm-up
         tree = mtsg.kd_build(scene, device=dev)

@@ -196,7 +196,7 @@ MTSG_DECLARE_LAUNCHERS(MTSG_SAMPLER_HALTON)
 MTSG_DECLARE_LAUNCHERS(MTSG_SAMPLER_HAMMERSLEY)
 MTSG_DECLARE_LAUNCHERS(MTSG_SAMPLER_LDSAMPLER)
 MTSG_DECLARE_LAUNCHERS(MTSG_SAMPLER_SOBOL)
-int finish_blocks_per_cu();   // k_finish workgroups per CU (occupancy query)
+int finish_blocks_per_cu(bool mats);   // k_finish workgroups per CU (occupancy query)
 
 }  // namespace mtsg
 
@@ -3607,10 +3607,24 @@ constexpr uint32_t FINISH_FETCH = 64;   // paths per wave draw (small pools: the
 #ifndef MTSG_FINISH_WAVES
 #define MTSG_FINISH_WAVES 3   // waves/SIMD asked of the compiler (r04: 3 at 168 VGPRs, 64 B of spills; C5 finish 52 -> 47 ms)
 #endif
+// the material-specialised tail kernels (MATS != MATS_ALL, round 6) fit 128
+// VGPRs: 4 waves/SIMD (the generic one holds 168 at 3)
+#ifndef MTSG_FINISH_WAVES_MATS
+#define MTSG_FINISH_WAVES_MATS 4
+#endif
+#ifndef MTSG_FINISH_MATS
+#define MTSG_FINISH_MATS 1   // 0: the tail always runs the all-materials kernel (A/B)
+#endif
+// whether launch_finish_inst runs a material-specialised k_finish (independent
+// sampler, flat scene, built-in BSDFs, a specialised material set)
+inline bool finish_uses_mats(int smp, bool ext, bool inst, int mats) {
+    return MTSG_FINISH_MATS && smp == MTSG_SAMPLER_INDEPENDENT && !ext && !inst && mats_kernel_set(mats) != MATS_ALL;
+}
 #if MTSG_FINISH_WAVES > 0
-#define FINISH_ATTR __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(MTSG_FINISH_WAVES)))
+#define FINISH_ATTR(MATS) __launch_bounds__(TRACE_BLOCK) \
+    __attribute__((amdgpu_waves_per_eu((MATS) == MATS_ALL ? MTSG_FINISH_WAVES : MTSG_FINISH_WAVES_MATS)))
 #else
-#define FINISH_ATTR __launch_bounds__(TRACE_BLOCK)
+#define FINISH_ATTR(MATS) __launch_bounds__(TRACE_BLOCK)
 #endif
 
 // qin: work list of the paths at their current bounce (their hits are ready:
@@ -3619,8 +3633,8 @@ constexpr uint32_t FINISH_FETCH = 64;   // paths per wave draw (small pools: the
 // INST: the two-level traversal (and its exact tie retrace) is compiled only
 // into the instantiations for instanced scenes, so the flat kernel carries
 // neither its registers nor the retrace's scratch stack
-template <bool ENV, int SMP, bool EXT, bool INST>
-__global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int qin, int hasAlpha, uint32_t shadeMin) {
+template <bool ENV, int SMP, bool EXT, bool INST, int MATS = MATS_ALL>
+__global__ void FINISH_ATTR(MATS) k_finish(DevScene S, DevIntegrator I, DevBatch B, DevPaths P, int qin, int hasAlpha, uint32_t shadeMin) {
     const SpecStack stk{};
     lds_top_init(S);
     const uint32_t n = __atomic_load_n(&P.cnt[cnt_q(qin)], __ATOMIC_RELAXED);
@@ -3675,7 +3689,7 @@ __global__ void FINISH_ATTR k_finish(DevScene S, DevIntegrator I, DevBatch B, De
                 const uint4 meta = ldS(&P.meta[idx]);
                 FinishOut out{P, idx, make_float4(0.f, 0.f, 0.f, 0.f)};
                 bool cont = false, shadow = false;
-                shade_path<ENV, SMP, EXT>(S, I, B, P, false, idx, meta, load_path(S, P, idx, false), hasAlpha, out, cont, shadow,
+                shade_path<ENV, SMP, EXT, FinishOut, MATS>(S, I, B, P, false, idx, meta, load_path(S, P, idx, false), hasAlpha, out, cont, shadow,
                                           global_tables(S));
                 state = FS_IDLE;
                 if (shadow) {
@@ -3866,9 +3880,12 @@ __global__ void k_reset(uint32_t *cnt, int qout, int sOut) {
 // traced again with the mailbox (tie_retrace); its grid strides over them
 template <bool KNOBS>
 __global__ void __launch_bounds__(TRACE_BLOCK) k_tie(DevScene S, DevPaths P) {
+    const uint32_t n = __atomic_load_n(&P.cnt[CNT_TIE], __ATOMIC_RELAXED);
+    // (most launches flag no tie: a workgroup with no entry leaves before it
+    // stages the tree's top in LDS; the exit is uniform over the workgroup)
+    if (blockIdx.x * TRACE_BLOCK >= n) return;
     const SpecStack stk{};
     lds_top_init(S);
-    const uint32_t n = __atomic_load_n(&P.cnt[CNT_TIE], __ATOMIC_RELAXED);
     const TravLimits L = trav_limits<KNOBS>(S);
     SpecRay r;
     for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
@@ -3881,6 +3898,7 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_tie(DevScene S, DevPaths P) {
 // the same for two-level scenes: the exact two-level Havran (tie_retrace_i)
 __global__ void __launch_bounds__(TRACE_BLOCK) k_tie_i(DevScene S, DevPaths P) {
     const uint32_t n = __atomic_load_n(&P.cnt[CNT_TIE], __ATOMIC_RELAXED);
+    if (blockIdx.x * TRACE_BLOCK >= n) return;
     for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
         bool err = false;
         tie_retrace_i(S, P, P.tie[i], err);

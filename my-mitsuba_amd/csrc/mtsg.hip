@@ -88,7 +88,7 @@ struct mtsg_scene {
     std::vector<void *> batchAllocs;
     uint32_t *hostCnt = nullptr;   // pinned copy of the queue counters (2 per lane)
     int cuCount = 0;
-    int traceGrid = 0, shadeGrid = 0, traceGridInst = 0, finishGrid = 0;
+    int traceGrid = 0, shadeGrid = 0, traceGridInst = 0, finishGrid = 0, finishGridMats = 0;
     // tail mode: once a bounce starts with fewer than finishPaths paths, k_finish
     // carries them through their remaining bounces in one launch (0: off)
     uint32_t finishPaths = 0;
@@ -261,7 +261,8 @@ void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, cons
     }
 }
 void launch_finish(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int qin, hipStream_t st) {
-    const ShadeLaunch a = shade_args(s, I, B, P, 1, qin, st, dim3(s->finishGrid), dim3(TRACE_BLOCK));
+    const bool mats = finish_uses_mats(I.smp.type, s->extBsdfs, s->ds.inst != nullptr, s->shadeGeneric ? (int)MATS_ALL : s->mats);
+    const ShadeLaunch a = shade_args(s, I, B, P, 1, qin, st, dim3(mats ? s->finishGridMats : s->finishGrid), dim3(TRACE_BLOCK));
     switch (I.smp.type) {
         case MTSG_SAMPLER_HALTON: launch_finish_smp<MTSG_SAMPLER_HALTON>(a); break;
         case MTSG_SAMPLER_HAMMERSLEY: launch_finish_smp<MTSG_SAMPLER_HAMMERSLEY>(a); break;
@@ -1245,8 +1246,10 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
 #endif
     s->shadeGrid = s->cuCount * MTSG_SHADE_WG_PER_CU * 256 / SHADE_BLOCK;
     perCU = 0;
-    if ((perCU = finish_blocks_per_cu()) <= 0) perCU = 4;
+    if ((perCU = finish_blocks_per_cu(false)) <= 0) perCU = 3;
     s->finishGrid = s->cuCount * perCU;
+    if ((perCU = finish_blocks_per_cu(true)) <= 0) perCU = 3;
+    s->finishGridMats = s->cuCount * perCU;
     // two-level traversal: the per-lane save slots of its grid (kernels.h save_vec)
     s->ds.instSave = nullptr;
     if (s->ds.inst && !MTSG_INST_REGSAVE) {

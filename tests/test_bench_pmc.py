@@ -51,3 +51,35 @@ def test_rocprof_names_normalise_to_the_instantiation():
     assert n("void (anonymous namespace)::k_trace_s<false, 16, true, false>(mtsg::DevScene)") == "k_trace_s<false, 16, true, false>"
     assert n("(anonymous namespace)::k_camera(mtsg::DevCamera, mtsg::DevIntegrator)") == "k_camera"
     assert n("void (anonymous namespace)::k_splat<5, 4>(mtsg::DevCamera, float*, int, int)") == "k_splat<5, 4>"
+
+
+def test_pmc_sets_are_per_frame():
+    """a PMC pass renders only the frames it is normalised by
+    (bench.py --pmc-pass), so a committed set's k_shade time per frame (rocprof
+    average x launches per frame) agrees with the HIP-event figure of the bench
+    line of the same configuration -- the multi-step 1/8-share set too."""
+    import glob
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pairs = {"c3": "bunny15", "c4_share8": "c4_e8", "c5": "c5", "c3_two_level": "bunny15_two_level"}
+    checked = 0
+    for tag, bench_tag in pairs.items():
+        sets = sorted(glob.glob(os.path.join(repo, "profiles", f"r*_pmc_{tag}.json")))
+        if not sets:
+            continue
+        pj = json.load(open(sets[-1]))
+        if "frames_fetch_pass" not in pj:
+            continue   # sets of round 5 and before: not normalised per frame, never quoted
+        rnd = os.path.basename(sets[-1]).split("_")[0]
+        line = os.path.join(repo, "profiles", f"{rnd}_bench_{bench_tag}.json")
+        if not os.path.exists(line):
+            continue
+        b = json.load(open(line))
+        ks = [v for n, v in pj["kernels"].items() if n.startswith("k_shade<") and "rocprof_ms_per_frame" in v]
+        pmc_ms = sum(v["rocprof_ms_per_frame"] for v in ks)
+        hip_ms = b["kernels"]["shade_ms"]
+        assert abs(pmc_ms - hip_ms) <= 0.10 * hip_ms, (tag, pmc_ms, hip_ms)
+        # and the bench line quotes the set's per-frame bytes for k_shade
+        assert abs(b["kernels"]["pmc"]["k_shade"]["rocprof_ms_per_frame"] - pmc_ms) < 2e-3
+        checked += 1
+    assert checked >= 1 or not glob.glob(os.path.join(repo, "profiles", "r06_pmc_*.json"))

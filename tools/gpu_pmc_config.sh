@@ -17,4 +17,7 @@ step fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d 
 step write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O -o write -- python bench.py $ARGS --pmc-pass --steps 1 --warmup 0
 step tcc 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O -o tcc -- python bench.py $ARGS --pmc-pass --steps 1 --warmup 0
 KEY=$(python bench.py $ARGS --print-pmc-key)
-python tools/pmc_kernels.py $O "$KEY" --frames-stats 4 --frames-pass 1 > $O/pmc.json && echo "pmc summary: $O/pmc.json"
+python tools/pmc_kernels.py $O "$KEY" --frames-stats 4 --frames-pass 1 > $O/pmc.json && echo "pmc summary: $O/pmc.json" || exit 1
+# into this (scratch) copy's profiles/, so the bench lines of the same call
+# quote the set (bench.py reads the newest committed rNN_pmc_*.json)
+cp $O/pmc.json profiles/${R}_pmc_${TAG}.json

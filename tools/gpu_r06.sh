@@ -36,9 +36,19 @@ for w in ${*:-tests bench}; do
     e8ro0) step e8ro0 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 $Q --no-count --ray-order 0 ;;
     ktro0) step ktro0 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt_ro0 -o kt -- python3 bench.py --pmc-pass $Q --no-count --steps 1 --warmup 1 --ray-order 0 ;;
     c5g) step c5g 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --shade-generic ;;
+    # kd-tree build properties (bench.py --kd-props), e.g. kdq:kdIntersectionCost=10,kdStopPrims=3
+    kdq:*) p=${w#kdq:}; step "kdq-${p//[=,]/_}" 300 python bench.py --steps 10 --warmup 3 $Q --no-count --kd-props "$p" ;;
+    kdi:*) p=${w#kdi:}; step "kdi-${p//[=,]/_}" 300 python bench.py --steps 5 --warmup 2 --instancing two-level $Q --no-count --kd-props "$p" ;;
+    kdc5:*) p=${w#kdc5:}; step "kdc5-${p//[=,]/_}" 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --kd-props "$p" ;;
     qg) step qg 300 python bench.py --steps 10 --warmup 3 $Q --no-count --shade-generic ;;
     c2q-*) v=${w#c2q-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 5 --warmup 2 --workload cbox $Q --no-count ;;
     e8q-*) v=${w#e8q-}; MTSG_LIB=$(lib $v) step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 $Q --no-count ;;
+    ranks)
+      # the launcher path (as the driver runs it) and the self-launching path,
+      # two ranks on this one GPU; then the refusal without --allow-shared
+      step ranks-torchrun 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu --allow-shared
+      step ranks-self 600 python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu --allow-shared
+      echo "== ranks-refuse"; timeout -k 10 300 python bench.py --gpus 2 --steps 1 --warmup 0 --no-cpu > $O/ranks-refuse.log 2>&1; echo "ranks-refuse rc=$? (non-zero expected)"; tail -n 2 $O/ranks-refuse.log ;;
     c5) step c5 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 ;;
     c2) step c2 600 python bench.py --steps 5 --warmup 2 --workload cbox ;;
     inst) step inst 300 python bench.py --steps 5 --warmup 2 --instancing two-level --no-cpu --no-parity ;;
