@@ -61,6 +61,10 @@ for w in ${*:-tests bench}; do
     kti-*) v=${w#kti-}; MTSG_LIB=$(lib $v) step $w 300 rocprofv3 --kernel-trace --output-format csv -d $O/kti_$v -o kt -- python3 bench.py --pmc-pass --instancing two-level $Q --no-count --steps 1 --warmup 1 ;;
     # FETCH_SIZE against known bytes for streams and gathers (tools/fetch_calib.hip)
     calib) step calib 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/calib -o calib -- tools/fetch_calib ;;
+    # TCC hit rate / traffic of the ray orders (profiles/r06_ray_order.txt; sets not quoted by bench)
+    pmcro-base) bash tools/gpu_pmc_config.sh r06ro append --ray-order 0 || exit $? ;;
+    pmcro-sorted) bash tools/gpu_pmc_config.sh r06ro sorted --ray-order 1 || exit $? ;;
+    pmcro-shuf1) MTSG_LIB=$(lib shuf1) bash tools/gpu_pmc_config.sh r06ro shuf1 || exit $? ;;
     pmc-c3) bash tools/gpu_pmc_config.sh r06 c3 || exit $? ;;
     pmc-inst) bash tools/gpu_pmc_config.sh r06 c3_two_level --instancing two-level || exit $? ;;
     pmc-c5) bash tools/gpu_pmc_config.sh r06 c5 --workload c5 --width 1920 --height 1080 --spp 1024 || exit $? ;;
