@@ -168,16 +168,25 @@ def test_staggered_lanes_are_bit_identical(cbox_small):
     np.testing.assert_allclose(img, ref, rtol=2e-5, atol=2e-5)
 
 
+@pytest.mark.parametrize("tail", ["default", "per-bounce", "late-tail"])
 @pytest.mark.parametrize("name", ["cbox.xml", "bunny15.xml", "env_glass.xml", "cbox_glass.xml"])
-def test_material_kernels_match_the_generic_kernel(name):
-    # k_shade<.., MATS> holds only the scene's material classes (diffuse /
-    # GGX roughconductor / dielectric): the same arithmetic as the
-    # kernel with every class, so every sample's radiance is bit-identical (the
-    # film itself sums samples with float atomics in no fixed order)
+def test_material_kernels_match_the_generic_kernel(name, tail):
+    # k_shade<.., MATS> and k_finish<.., MATS> hold only the scene's material
+    # classes (diffuse / GGX roughconductor / dielectric): the same
+    # arithmetic as the kernels with every class, so every sample's radiance is
+    # bit-identical (the film itself sums samples with float atomics in no fixed
+    # order).  tail: the small frame's paths go to the tail kernel after bounce 0
+    # (default threshold), never (per-bounce launches only), or once fewer than
+    # 4096 remain (per-bounce launches first, then the tail kernel)
     scene = mtsg.Scene(os.path.join(SCENES, name), {"width": 64, "height": 48, "spp": 8})
     p = scene.params()
     g = mtsg.GPUScene(scene, 0)
+    if tail != "default":
+        g.set_finish_paths(0 if tail == "per-bounce" else 4096)
     spec = g.render_samples(p)
+    st = g.stats()
+    if tail != "late-tail":
+        assert (st.launches_finish > 0) == (tail == "default"), st.launches_finish
     g.set_option(mtsg.MTSG_OPT_SHADE_GENERIC, 1)
     gen = g.render_samples(p)
     g.close()

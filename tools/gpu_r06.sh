@@ -58,6 +58,7 @@ for w in ${*:-tests bench}; do
     # per-launch kernel durations of one frame (tools/launch_times.py)
     kt-*) v=${w#kt-}; MTSG_LIB=$(lib $v) step $w 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt_$v -o kt -- python3 bench.py --pmc-pass $Q --no-count --steps 1 --warmup 1 ;;
     kte8-*) v=${w#kte8-}; MTSG_LIB=$(lib $v) step $w 300 rocprofv3 --kernel-trace --output-format csv -d $O/kte8_$v -o kt -- python3 bench.py --pmc-pass --emulate-ranks 8 $Q --no-count --steps 1 --warmup 1 ;;
+    ktc5-*) v=${w#ktc5-}; MTSG_LIB=$(lib $v) step $w 300 rocprofv3 --kernel-trace --output-format csv -d $O/ktc5_$v -o kt -- python3 bench.py --pmc-pass --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --steps 1 --warmup 0 ;;
     kti-*) v=${w#kti-}; MTSG_LIB=$(lib $v) step $w 300 rocprofv3 --kernel-trace --output-format csv -d $O/kti_$v -o kt -- python3 bench.py --pmc-pass --instancing two-level $Q --no-count --steps 1 --warmup 1 ;;
     # FETCH_SIZE against known bytes for streams and gathers (tools/fetch_calib.hip)
     calib) step calib 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/calib -o calib -- tools/fetch_calib ;;
