@@ -102,7 +102,7 @@ clean:
 
 # Measurement variants of the device library (my-mitsuba_amd/var/, loaded with
 # MTSG_LIB=...; objects in build/var/, which gpurun does not ship)
-VARIANTS := sg64:-DMTSG_SHADE_WG_PER_CU=64 sg128:-DMTSG_SHADE_WG_PER_CU=128 sg512:-DMTSG_SHADE_WG_PER_CU=512 sg32:-DMTSG_SHADE_WG_PER_CU=32 sb512:-DMTSG_SHADE_BLOCK=512 popsel:-DMTSG_POPSEL=1 eb0:-DMTSG_ENTER_BATCH=0 eb4:-DMTSG_ENTER_BATCH=4 eb16:-DMTSG_ENTER_BATCH=16 shocc3:-DMTSG_SHADE_LDS_PAD=2048 ii32:-DMTSG_INST_MIN_IDLE=32 ii24:-DMTSG_INST_MIN_IDLE=24 eb8x8:-DMTSG_EXIT_BATCH=8 iw7s5:-DMTSG_INST_WAVES=7@-DMTSG_INNER_STACK=5 ss7:-DMTSG_INST_REGSAVE=0@-DMTSG_INNER_STACK=5 ss8:-DMTSG_INST_REGSAVE=0@-DMTSG_INST_WAVES=8@-DMTSG_INNER_STACK=4@-DMTSG_SAVE_INV=0 occ7:-DMTSG_LDS_PAD=1024 occ6:-DMTSG_LDS_PAD=1792 powout:-DGMF_CALLS=45 fm16:-DMTSG_FETCH_MIN=16 fm64:-DMTSG_FETCH_MIN=64 gs1:-DMTSG_GUIDE_SPLIT=1 gs4:-DMTSG_GUIDE_SPLIT=4 noguide:-DMTSG_FETCH_MIN=256 wt:-DMTSG_WT_DRAIN=1 ss5:-DMTSG_SHORT_STACK=5 ldstop:-DMTSG_LDS_TOP=1 noguard:-DMTSG_RST_GUARD=0 iw7:-DMTSG_INST_WAVES=7 gs5:-DMTSG_INNER_STACK=5 noshlds:-DMTSG_SHADE_LDS=0 nosave:-DMTSG_SAVE_RAY=0 soct:-DMTSG_SORT_OCT=1 nomb:-DMTSG_MAILBOX=0 sinv:-DMTSG_SAVE_INV=1 silp:-mllvm@-amdgpu-sched-strategy=max-ilp smem:-mllvm@-amdgpu-sched-strategy=max-memory-clause ocmlmath:-DMTSG_GLIBC_MATH=0 call31:-DGMF_CALLS=31 call14:-DGMF_CALLS=14 call12:-DGMF_CALLS=12 call13:-DGMF_CALLS=13 slotsave:-DMTSG_INST_REGSAVE=0 pre0:-DMTSG_SHADE_PRELOAD=0 pre2:-DMTSG_SHADE_PRELOAD=2 rpend:-DMTSG_RECT_PEND=1 envfull:-DMTSG_ENV_GUIDE=0 fw3:-DMTSG_FINISH_WAVES=3 call0:-DGMF_CALLS=0 pre1:-DMTSG_SHADE_PRELOAD=1 pd:-DMTSG_PUSHDOWN=1 sc16:-DMTSG_SPLAT_CHUNK=16 shenv4:-DMTSG_SHADE_WAVES_MATS_ENV=4 tie1:-DMTSG_TIE_INLINE=1 shuf1:-DMTSG_SHUFFLE=1 shuf2:-DMTSG_SHUFFLE=2 sw16k:-DMTSG_SORT_WINDOW=16384 sw1k:-DMTSG_SORT_WINDOW=1024 sb3:-DMTSG_SORT_BINS_LOG=3 sb5:-DMTSG_SORT_BINS_LOG=5 ssort0:-DMTSG_SHADE_SORT=0 trow:-DMTSG_TILE_MORTON=0 nopf:-DMTSG_INST_PREFILTER=0 finm0:-DMTSG_FINISH_MATS=0 finm3:-DMTSG_FINISH_WAVES_MATS=3
+VARIANTS := sg64:-DMTSG_SHADE_WG_PER_CU=64 sg128:-DMTSG_SHADE_WG_PER_CU=128 sg512:-DMTSG_SHADE_WG_PER_CU=512 sg32:-DMTSG_SHADE_WG_PER_CU=32 sb512:-DMTSG_SHADE_BLOCK=512 popsel:-DMTSG_POPSEL=1 eb0:-DMTSG_ENTER_BATCH=0 eb4:-DMTSG_ENTER_BATCH=4 eb16:-DMTSG_ENTER_BATCH=16 shocc3:-DMTSG_SHADE_LDS_PAD=2048 ii32:-DMTSG_INST_MIN_IDLE=32 ii24:-DMTSG_INST_MIN_IDLE=24 eb8x8:-DMTSG_EXIT_BATCH=8 iw7s5:-DMTSG_INST_WAVES=7@-DMTSG_INNER_STACK=5 ss7:-DMTSG_INST_REGSAVE=0@-DMTSG_INNER_STACK=5 ss8:-DMTSG_INST_REGSAVE=0@-DMTSG_INST_WAVES=8@-DMTSG_INNER_STACK=4@-DMTSG_SAVE_INV=0 occ7:-DMTSG_LDS_PAD=1024 occ6:-DMTSG_LDS_PAD=1792 powout:-DGMF_CALLS=45 fm16:-DMTSG_FETCH_MIN=16 fm64:-DMTSG_FETCH_MIN=64 gs1:-DMTSG_GUIDE_SPLIT=1 gs4:-DMTSG_GUIDE_SPLIT=4 noguide:-DMTSG_FETCH_MIN=256 wt:-DMTSG_WT_DRAIN=1 ss5:-DMTSG_SHORT_STACK=5 ldstop:-DMTSG_LDS_TOP=1 noguard:-DMTSG_RST_GUARD=0 iw7:-DMTSG_INST_WAVES=7 gs5:-DMTSG_INNER_STACK=5 noshlds:-DMTSG_SHADE_LDS=0 nosave:-DMTSG_SAVE_RAY=0 soct:-DMTSG_SORT_OCT=1 nomb:-DMTSG_MAILBOX=0 sinv:-DMTSG_SAVE_INV=1 silp:-mllvm@-amdgpu-sched-strategy=max-ilp smem:-mllvm@-amdgpu-sched-strategy=max-memory-clause ocmlmath:-DMTSG_GLIBC_MATH=0 call31:-DGMF_CALLS=31 call14:-DGMF_CALLS=14 call12:-DGMF_CALLS=12 call13:-DGMF_CALLS=13 slotsave:-DMTSG_INST_REGSAVE=0 pre0:-DMTSG_SHADE_PRELOAD=0 pre2:-DMTSG_SHADE_PRELOAD=2 rpend:-DMTSG_RECT_PEND=1 envfull:-DMTSG_ENV_GUIDE=0 fw3:-DMTSG_FINISH_WAVES=3 call0:-DGMF_CALLS=0 pre1:-DMTSG_SHADE_PRELOAD=1 pd:-DMTSG_PUSHDOWN=1 sc16:-DMTSG_SPLAT_CHUNK=16 shenv4:-DMTSG_SHADE_WAVES_MATS_ENV=4 tie1:-DMTSG_TIE_INLINE=1 shuf1:-DMTSG_SHUFFLE=1 shuf2:-DMTSG_SHUFFLE=2 sw16k:-DMTSG_SORT_WINDOW=16384 sw1k:-DMTSG_SORT_WINDOW=1024 sb3:-DMTSG_SORT_BINS_LOG=3 sb5:-DMTSG_SORT_BINS_LOG=5 ssort0:-DMTSG_SHADE_SORT=0 trow:-DMTSG_TILE_MORTON=0 nopf:-DMTSG_INST_PREFILTER=0 sg256:-DMTSG_SHADE_WG_PER_CU=256 finm0:-DMTSG_FINISH_MATS=0 finm3:-DMTSG_FINISH_WAVES_MATS=3
 VAR_LIBS := $(foreach v,$(VARIANTS),$(PKG)/var/libmtsg_$(word 1,$(subst :, ,$(v))).so)
 .PHONY: variants
 variants: $(VAR_LIBS)

@@ -67,6 +67,8 @@ def pmc_key(a, world=1):
            "balance_rounds": a.balance_rounds if max(world, a.emulate_ranks, 1) > 1 else 0, "build": device_build_id()}
     if getattr(a, "kd_props", ""):
         key["kd_props"] = a.kd_props   # another tree: other launches
+    if getattr(a, "lanes", 0) > 0 or getattr(a, "stagger", -1) >= 0:
+        key["lanes"] = [a.lanes, a.stagger]   # other launch sequence
     return key
 
 
@@ -128,6 +130,9 @@ def parse():
                          "row-major key order (each share a band of tile rows, its XCD ranges sub-bands)")
     ap.add_argument("--ray-order", type=int, default=-1, choices=[-1, 0, 1],
                     help="MTSG_OPT_RAY_ORDER: 1 = bounce rays in direction-sorted windows, 0 = append order (default)")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="batches in flight on their own streams (MTSG_OPT_LANES; 0 = the library's default, 1)")
+    ap.add_argument("--stagger", type=int, default=-1, help="bounces between the lanes' starts (MTSG_OPT_STAGGER)")
     ap.add_argument("--kd-props", default="",
                     help="scene kd-tree properties for the build, k=v[,k=v] (scene.cpp:47-83 names: "
                          "kdIntersectionCost, kdTraversalCost, kdEmptySpaceBonus, kdStopPrims, ...; measurement)")
@@ -437,8 +442,8 @@ def main():
         gpu.set_batch_paths(a.batch_paths)
     elif devices and devices["shared"]:
         # ranks sharing a GPU size their batches from free-memory snapshots
-        # that can coincide: cap each rank at its share of the default batch
-        # (2^29 paths, 148 GB) so that together they fit the 288 GB HBM
+        # that can coincide: cap each rank at its share of 2^29 paths (148 GB)
+        # so that together they fit the 288 GB HBM
         sharing = devices["pci"].count(devices["pci"][rank])
         gpu.set_batch_paths(max(1 << 20, (1 << 29) // sharing))
     if a.finish_paths >= 0:
@@ -447,6 +452,10 @@ def main():
         gpu.set_option(mtsg.MTSG_OPT_SHADE_GENERIC, 1)
     if a.ray_order >= 0:
         gpu.set_option(mtsg.MTSG_OPT_RAY_ORDER, a.ray_order)
+    if a.lanes > 0:
+        gpu.set_option(mtsg.MTSG_OPT_LANES, a.lanes)
+    if a.stagger >= 0:
+        gpu.set_option(mtsg.MTSG_OPT_STAGGER, a.stagger)
     W, H = params.tile_w + 2 * border, params.tile_h + 2 * border
     nbytes = W * H * 5 * 4
     film = gpu.alloc(nbytes)

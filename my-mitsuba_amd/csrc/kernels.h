@@ -287,7 +287,11 @@ constexpr int TRACE_BLOCK = 64;             // one wave per workgroup for traver
 // rays finish, and late bounces hold few paths, so the batch should be as
 // large as the frame -- measured on the 1M-triangle scene (Msamples/s):
 // 4M paths 421, 16M 672, 32M 803, 64M 884, 128M 934, whole frame 960.
-constexpr uint32_t DEFAULT_BATCH_PATHS = 1u << 29;   // 148 GB of path state; C5 in 4 batches instead of 8: +2.5% (r04)
+// 3 * 2^28 paths = 225 GB of path state at most (r04: 2^29, C5 in 4 batches
+// instead of 8: +2.5%; r06: C5 in 3 batches of 713M paths, 200 GB, instead of
+// 4: +1.1%, profiles/r06_c5_batches.txt -- every batch pays its own tail of
+// small bounce launches); capped by the free HBM (render_impl)
+constexpr uint32_t DEFAULT_BATCH_PATHS = 3u << 28;
 #define MTSG_MAX_LANES 4
 #ifndef MTSG_LANES
 #define MTSG_LANES 1

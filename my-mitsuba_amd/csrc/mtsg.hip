@@ -384,7 +384,9 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
         size_t freeB = 0, totalB = 0;
         if (hipMemGetInfo(&freeB, &totalB) == hipSuccess) {
             const size_t held = (size_t)s->capacity * s->lanesAlloc * PATH_STATE_BYTES;
-            const size_t fit = (size_t)((freeB + held) * 0.6 / PATH_STATE_BYTES);
+            // 3/4 of the free HBM (288 GB on an MI355X: 768M paths, C5's three
+            // batches of 713M); the rest stays for the scene and other users
+            const size_t fit = (size_t)((freeB + held) * 0.75 / PATH_STATE_BYTES);
             maxPaths = (uint32_t)std::max<size_t>(TILE * TILE, std::min<size_t>(maxPaths, fit));
         }
     }

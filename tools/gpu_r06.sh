@@ -37,6 +37,14 @@ for w in ${*:-tests bench}; do
     ktro0) step ktro0 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt_ro0 -o kt -- python3 bench.py --pmc-pass $Q --no-count --steps 1 --warmup 1 --ray-order 0 ;;
     c5g) step c5g 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --shade-generic ;;
     # kd-tree build properties (bench.py --kd-props), e.g. kdq:kdIntersectionCost=10,kdStopPrims=3
+    # tail-kernel switch point (paths; bench.py --finish-paths): c5f-<N> / qf-<N> / e8f-<N>
+    c5f-*) n=${w#c5f-}; step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --finish-paths ${n%@*} ;;
+    qf-*) n=${w#qf-}; step $w 300 python bench.py --steps 10 --warmup 3 $Q --no-count --finish-paths ${n%@*} ;;
+    e8f-*) n=${w#e8f-}; step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 $Q --no-count --finish-paths ${n%@*} ;;
+    # batches in flight (C5): c5l:<lanes>:<stagger>:<batch paths>
+    c5l:*) IFS=: read -r _ ln sg bp <<< "$w"; step "c5l-$ln-$sg-$bp" 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --lanes $ln --stagger $sg --batch-paths $bp ;;
+    # batch size (paths; bench.py --batch-paths): c5b-<N>
+    c5b-*) n=${w#c5b-}; step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --batch-paths ${n%@*} ;;
     kdq:*) p=${w#kdq:}; step "kdq-${p//[=,]/_}" 300 python bench.py --steps 10 --warmup 3 $Q --no-count --kd-props "$p" ;;
     kdi:*) p=${w#kdi:}; step "kdi-${p//[=,]/_}" 300 python bench.py --steps 5 --warmup 2 --instancing two-level $Q --no-count --kd-props "$p" ;;
     kdc5:*) p=${w#kdc5:}; step "kdc5-${p//[=,]/_}" 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --kd-props "$p" ;;
@@ -66,6 +74,14 @@ for w in ${*:-tests bench}; do
     pmcro-base) bash tools/gpu_pmc_config.sh r06ro append --ray-order 0 || exit $? ;;
     pmcro-sorted) bash tools/gpu_pmc_config.sh r06ro sorted --ray-order 1 || exit $? ;;
     pmcro-shuf1) MTSG_LIB=$(lib shuf1) bash tools/gpu_pmc_config.sh r06ro shuf1 || exit $? ;;
+    # SQ counters per kernel (tools/sq_by_kernel.py): sq-c3 / sq-c5, one frame per pass (C5 at 256 spp)
+    sq-c3|sq-c5)
+      t=${w#sq-}; A="--pmc-pass $Q --no-count --steps 1 --warmup 0"
+      [ $t = c5 ] && A="$A --workload c5 --width 1920 --height 1080 --spp 256"
+      D=$O/sq_$t; mkdir -p $D
+      step sq-$t-p1 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D -o p1 -- python3 bench.py $A
+      step sq-$t-p2 200 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --kernel-trace --output-format csv -d $D -o p2 -- python3 bench.py $A
+      python3 tools/sq_by_kernel.py $D/p1_counter_collection.csv $D/p2_counter_collection.csv > $D/summary.txt; cat $D/summary.txt | cut -c1-300 ;;
     pmc-c3) bash tools/gpu_pmc_config.sh r06 c3 || exit $? ;;
     pmc-inst) bash tools/gpu_pmc_config.sh r06 c3_two_level --instancing two-level || exit $? ;;
     pmc-c5) bash tools/gpu_pmc_config.sh r06 c5 --workload c5 --width 1920 --height 1080 --spp 1024 || exit $? ;;
