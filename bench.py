@@ -67,6 +67,8 @@ def pmc_key(a, world=1):
            "balance_rounds": a.balance_rounds if max(world, a.emulate_ranks, 1) > 1 else 0, "build": device_build_id()}
     if getattr(a, "kd_props", ""):
         key["kd_props"] = a.kd_props   # another tree: other launches
+    if getattr(a, "finish_shade_min", 0) > 0:
+        key["finish_shade_min"] = a.finish_shade_min
     if getattr(a, "lanes", 0) > 0 or getattr(a, "stagger", -1) >= 0:
         key["lanes"] = [a.lanes, a.stagger]   # other launch sequence
     return key
@@ -130,6 +132,8 @@ def parse():
                          "row-major key order (each share a band of tile rows, its XCD ranges sub-bands)")
     ap.add_argument("--ray-order", type=int, default=-1, choices=[-1, 0, 1],
                     help="MTSG_OPT_RAY_ORDER: 1 = bounce rays in direction-sorted windows, 0 = append order (default)")
+    ap.add_argument("--finish-shade-min", type=int, default=0,
+                    help="tail kernel: a wave shades once this many of its busy lanes wait to (MTSG_OPT_FINISH_SHADE_MIN; 0 = the default, 16)")
     ap.add_argument("--lanes", type=int, default=0,
                     help="batches in flight on their own streams (MTSG_OPT_LANES; 0 = the library's default, 1)")
     ap.add_argument("--stagger", type=int, default=-1, help="bounces between the lanes' starts (MTSG_OPT_STAGGER)")
@@ -452,6 +456,8 @@ def main():
         gpu.set_option(mtsg.MTSG_OPT_SHADE_GENERIC, 1)
     if a.ray_order >= 0:
         gpu.set_option(mtsg.MTSG_OPT_RAY_ORDER, a.ray_order)
+    if a.finish_shade_min > 0:
+        gpu.set_option(mtsg.MTSG_OPT_FINISH_SHADE_MIN, a.finish_shade_min)
     if a.lanes > 0:
         gpu.set_option(mtsg.MTSG_OPT_LANES, a.lanes)
     if a.stagger >= 0:

@@ -608,7 +608,9 @@ int  mtsg_get_stats(mtsg_scene *scene, mtsg_stats *out);
 int  mtsg_debug_wavetimes(mtsg_scene *scene, uint64_t *out, uint32_t max_launches, uint32_t *waves);
 int  mtsg_debug_stragglers(mtsg_scene *scene, float *out, uint32_t max_rays);
 
-/* Wavefront batch size in paths (default chosen from device memory). */
+/* Wavefront batch size in paths.  Default: the whole rectangle, up to
+ * 3 * 2^28 paths (280 B of path state each) and at most 3/4 of the free
+ * device memory; larger renders run in equal batches. */
 int  mtsg_set_batch_paths(mtsg_scene *scene, uint32_t paths);
 
 /* Tail mode: once a bounce starts with fewer than `paths` paths, one
@@ -625,7 +627,7 @@ int  mtsg_set_finish_paths(mtsg_scene *scene, uint32_t paths);
  *   MTSG_OPT_TRACE_REFILL     idle lanes that make a traversal wave refill
  *                             from the work list: 16 (default) or 32
  *   MTSG_OPT_FINISH_SHADE_MIN tail kernel: a wave shades once that many of its
- *                             busy lanes wait for shading (1..64, default 1)
+ *                             busy lanes wait for shading (1..64, default 16)
  *   MTSG_OPT_LANES            concurrent batches on their own streams (1..4,
  *                             default 1; measured slower)
  *   MTSG_OPT_STAGGER          bounces between the lanes' starts (0..16)

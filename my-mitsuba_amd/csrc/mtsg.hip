@@ -92,7 +92,10 @@ struct mtsg_scene {
     // tail mode: once a bounce starts with fewer than finishPaths paths, k_finish
     // carries them through their remaining bounces in one launch (0: off)
     uint32_t finishPaths = 0;
-    uint32_t finishShadeMin = 1;
+    // a tail-kernel wave shades once 16 of its busy lanes wait to (or none traces):
+    // r06, with the 4-wave material kernels, C5 tail 18.3 -> 13.4 ms, C3 0.66 ->
+    // 0.58, two-level 1.16 -> 0.99 against 1 (profiles/r06_finish_threshold.txt)
+    uint32_t finishShadeMin = 16;
     uint32_t flags = 0;
     int samplerType = MTSG_SAMPLER_INDEPENDENT, samplerDim = 4;
     int qmcInv[2][3] = {{0, 0, 0}, {0, 0, 0}};

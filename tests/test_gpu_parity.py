@@ -193,6 +193,26 @@ def test_material_kernels_match_the_generic_kernel(name, tail):
     assert np.array_equal(spec, gen, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(spec - gen))}"
 
 
+@pytest.mark.parametrize("name", ["bunny15.xml", "env_glass.xml", "cbox_glass.xml"])
+def test_tail_shading_threshold_does_not_change_samples(name):
+    # the tail kernel shades a wave's waiting lanes once 16 of them wait (the
+    # default) or as soon as one does (MTSG_OPT_FINISH_SHADE_MIN 1, the default
+    # through round 5): which iteration shades a path changes nothing in its
+    # arithmetic, so every sample is bit-identical
+    scene = mtsg.Scene(os.path.join(SCENES, name), {"width": 64, "height": 48, "spp": 8})
+    p = scene.params()
+    g = mtsg.GPUScene(scene, 0)
+    a = g.render_samples(p)
+    assert g.stats().launches_finish > 0
+    g.set_option(mtsg.MTSG_OPT_FINISH_SHADE_MIN, 1)
+    b = g.render_samples(p)
+    g.set_option(mtsg.MTSG_OPT_FINISH_SHADE_MIN, 64)
+    c = g.render_samples(p)
+    g.close()
+    assert np.array_equal(a, b, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(a - b))}"
+    assert np.array_equal(a, c, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(a - c))}"
+
+
 @pytest.mark.parametrize("name", ["cbox.xml", "bunny15.xml", "env_glass.xml"])
 def test_ray_order_does_not_change_samples(name):
     # the traversal takes bounce rays in direction-sorted windows

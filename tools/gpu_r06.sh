@@ -45,6 +45,11 @@ for w in ${*:-tests bench}; do
     c5l:*) IFS=: read -r _ ln sg bp <<< "$w"; step "c5l-$ln-$sg-$bp" 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --lanes $ln --stagger $sg --batch-paths $bp ;;
     # batch size (paths; bench.py --batch-paths): c5b-<N>
     c5b-*) n=${w#c5b-}; step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --batch-paths ${n%@*} ;;
+    # tail kernel's shading threshold (bench.py --finish-shade-min): c5sm-<n> / e8sm-<n>
+    c5sm-*) n=${w#c5sm-}; step $w 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --finish-shade-min ${n%@*} ;;
+    qsm-*) n=${w#qsm-}; step $w 300 python bench.py --steps 10 --warmup 3 $Q --no-count --finish-shade-min ${n%@*} ;;
+    iqsm-*) n=${w#iqsm-}; step $w 300 python bench.py --steps 5 --warmup 2 --instancing two-level $Q --no-count --finish-shade-min ${n%@*} ;;
+    e8sm-*) n=${w#e8sm-}; step $w 300 python bench.py --steps 5 --warmup 2 --emulate-ranks 8 $Q --no-count --finish-shade-min ${n%@*} ;;
     kdq:*) p=${w#kdq:}; step "kdq-${p//[=,]/_}" 300 python bench.py --steps 10 --warmup 3 $Q --no-count --kd-props "$p" ;;
     kdi:*) p=${w#kdi:}; step "kdi-${p//[=,]/_}" 300 python bench.py --steps 5 --warmup 2 --instancing two-level $Q --no-count --kd-props "$p" ;;
     kdc5:*) p=${w#kdc5:}; step "kdc5-${p//[=,]/_}" 600 python bench.py --steps 3 --warmup 1 --workload c5 --width 1920 --height 1080 --spp 1024 $Q --no-count --kd-props "$p" ;;
