@@ -637,6 +637,11 @@ int  mtsg_set_finish_paths(mtsg_scene *scene, uint32_t paths);
  *                             0 (default) = the order they were appended in,
  *                             1 = windows of 4096 rays sorted by direction
  *                             (measured slower)
+ *   MTSG_OPT_CAMERA_DIFFS     environment scenes: 0 (default) = a camera ray
+ *                             that misses recomputes its ray differentials at
+ *                             bounce 0, 1 = the camera stores them in the path
+ *                             state (the layout through round 5; A/B tests).
+ *                             Scenes with filtered textures always store them.
  * Unknown keys and values out of range return MTSG_ERR_INVALID. */
 enum {
     MTSG_OPT_TRACE_REFILL = 1,
@@ -644,7 +649,8 @@ enum {
     MTSG_OPT_LANES = 3,
     MTSG_OPT_STAGGER = 4,
     MTSG_OPT_SHADE_GENERIC = 5,
-    MTSG_OPT_RAY_ORDER = 6
+    MTSG_OPT_RAY_ORDER = 6,
+    MTSG_OPT_CAMERA_DIFFS = 7
 };
 int  mtsg_set_option(mtsg_scene *scene, int32_t key, int64_t value);
 

@@ -23,6 +23,7 @@ namespace mtsg {
 // ---------------------------------------------------------------------------
 // device-side scene and path state
 // ---------------------------------------------------------------------------
+struct DevCamera;
 struct DevScene {
     // device kd-tree (built from Mitsuba's KDNode array at upload: same splits
     // and leaves, re-laid out as two-level blocks).  A block root's 64-B block
@@ -73,6 +74,12 @@ struct DevScene {
     const float *__restrict__ tex_texels;
     const float4 *__restrict__ ttex;
     int cam_diffs;        // bounce 0 carries the camera's ray differentials in T / aux
+                          // (filtered texture lookups; MTSG_OPT_CAMERA_DIFFS 1)
+    // environment scenes otherwise: a camera ray that misses recomputes its
+    // differentials at bounce 0 from the camera (camera_differentials), so
+    // k_camera writes and bounce 0 reads 32 B less per path (round 6)
+    int cam_env_diffs;
+    const DevCamera *__restrict__ camDev;
     // two-level traversal: per-lane save slots of the top-level state
     // (SAVE_VECS uint4 per lane of the traversal grid); nullptr: no instances
     uint4 *__restrict__ instSave;
@@ -237,6 +244,12 @@ DEV void camera_jitter(const DevIntegrator &I, int x, int y, uint32_t s, float &
         case MTSG_SAMPLER_SOBOL: next2D<MTSG_SAMPLER_SOBOL>(I, p, a, b); break;
         default: next2D<MTSG_SAMPLER_INDEPENDENT>(I, p, a, b); break;
     }
+}
+// (the same for a caller that knows the sampler: the shading kernels)
+template <int SMP>
+DEV void camera_jitter_smp(const DevIntegrator &I, int x, int y, uint32_t s, float &a, float &b) {
+    PathSampler p = path_sampler(I, x, y, s, 0, 0);
+    next2D<SMP>(I, p, a, b);
 }
 
 
@@ -1929,6 +1942,39 @@ DEV void slot_pixel(const DevBatch &B, uint32_t slot, int &x, int &y, uint32_t &
     s = B.s0 + sl;
 }
 
+// the camera-space point on the near plane of pixel (x, y)'s sample at
+// (x + a, y + b) (sampleToCamera, perspective.cpp:271-280)
+DEV float3 camera_near(const DevCamera &C, int x, int y, float a, float b) {
+    const float sx = ((float)x + a) * C.inv_res_x, sy = ((float)y + b) * C.inv_res_y;
+    const float *m = C.s2c;
+    float px = m[0] * sx + m[1] * sy + m[3], py = m[4] * sx + m[5] * sy + m[7];
+    float pz = m[8] * sx + m[9] * sy + m[11], pw = m[12] * sx + m[13] * sy + m[15];
+    return pw == 1.0f ? mk3(px, py, pz) : mk3(px, py, pz) / pw;
+}
+DEV float3 camera_to_world_dir(const DevCamera &C, float3 d) {
+    const float *t = C.c2w;
+    return mk3(t[0] * d.x + t[1] * d.y + t[2] * d.z, t[4] * d.x + t[5] * d.y + t[6] * d.z, t[8] * d.x + t[9] * d.y + t[10] * d.z);
+}
+// rx/ryDirection of the ray through nearP (world direction wd), scaled by
+// 1/sqrt(spp) (perspective.cpp:282-298, integrator.cpp:148-149, ray.h:163-168)
+DEV void camera_differentials(const DevCamera &C, const DevIntegrator &I, float3 nearP, float3 wd, float3 &rxs, float3 &rys) {
+    const float3 rxc = normalize(nearP + ld3(C.dx)), ryc = normalize(nearP + ld3(C.dy));
+    const float3 rx = camera_to_world_dir(C, rxc), ry = camera_to_world_dir(C, ryc);
+    const float scale = 1.0f / sqrtf((float)I.spp);
+    rxs = wd + (rx - wd) * scale;
+    rys = wd + (ry - wd) * scale;
+}
+// the scaled differentials of the camera ray of sample s of pixel (x, y), as
+// k_camera computes them (its jitter draw, its direction): the shading of a
+// bounce-0 environment miss recomputes them instead of reading them back
+template <int SMP>
+DEV void camera_ray_differentials(const DevCamera &C, const DevIntegrator &I, int x, int y, uint32_t s, float3 &rxs, float3 &rys) {
+    float a, b;
+    camera_jitter_smp<SMP>(I, x, y, s, a, b);   // (myPath2_OM, the one integrator without the jitter, has no differentials)
+    const float3 nearP = camera_near(C, x, y, a, b);
+    camera_differentials(C, I, nearP, camera_to_world_dir(C, normalize(nearP)), rxs, rys);
+}
+
 __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     bool alive = false;
@@ -1941,35 +1987,23 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
             float a = 0.5f, b = 0.5f;   // myPath2_OM without jitterSample: the pixel centre, no draw
             const bool jitter = !I.om || I.om_jitter;
             if (jitter) camera_jitter(I, x, y, s, a, b);
-            const float sx = ((float)x + a) * C.inv_res_x, sy = ((float)y + b) * C.inv_res_y;
-            const float *m = C.s2c;
-            float px = m[0] * sx + m[1] * sy + m[3], py = m[4] * sx + m[5] * sy + m[7];
-            float pz = m[8] * sx + m[9] * sy + m[11], pw = m[12] * sx + m[13] * sy + m[15];
-            float3 nearP = pw == 1.0f ? mk3(px, py, pz) : mk3(px, py, pz) / pw;
-            float3 d = normalize(nearP);
-            float invZ = 1.0f / d.z;
-            const float *t = C.c2w;
-            float3 wd = mk3(t[0] * d.x + t[1] * d.y + t[2] * d.z, t[4] * d.x + t[5] * d.y + t[6] * d.z,
-                            t[8] * d.x + t[9] * d.y + t[10] * d.z);
-            stS(&P.ray_o[slot], make_float4(t[3], t[7], t[11], C.near_clip * invZ));
+            const float3 nearP = camera_near(C, x, y, a, b);
+            const float3 d = normalize(nearP);
+            const float invZ = 1.0f / d.z;
+            const float3 wd = camera_to_world_dir(C, d);
+            stS(&P.ray_o[slot], make_float4(C.c2w[3], C.c2w[7], C.c2w[11], C.near_clip * invZ));
             stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
             if (C.diffs && !I.om) {   // myPath2_OM uses sensor->sampleRay: no differentials
-                // rx/ryDirection scaled by 1/sqrt(spp) (integrator.cpp:148-149, ray.h:163-168),
-                const float3 rxc = normalize(nearP + ld3(C.dx)), ryc = normalize(nearP + ld3(C.dy));
-                const float3 rx = mk3(t[0] * rxc.x + t[1] * rxc.y + t[2] * rxc.z, t[4] * rxc.x + t[5] * rxc.y + t[6] * rxc.z,
-                                      t[8] * rxc.x + t[9] * rxc.y + t[10] * rxc.z);
-                const float3 ry = mk3(t[0] * ryc.x + t[1] * ryc.y + t[2] * ryc.z, t[4] * ryc.x + t[5] * ryc.y + t[6] * ryc.z,
-                                      t[8] * ryc.x + t[9] * ryc.y + t[10] * ryc.z);
-                const float scale = 1.0f / sqrtf((float)I.spp);
-                const float3 rxs = wd + (rx - wd) * scale, rys = wd + (ry - wd) * scale;
+                float3 rxs, rys;
+                camera_differentials(C, I, nearP, wd, rxs, rys);
                 // parked in T and aux (throughput 1, no previous vertex) until
                 // bounce 0 is shaded
                 stS(&P.T[slot], make_float4(rxs.x, rxs.y, rxs.z, 1.f));
                 stS(&P.aux[slot], make_float4(rys.x, rys.y, rys.z, 0.f));
-                stS(&P.Lp[slot], make_float4(0.f, 0.f, 0.f, 1.0f));
             }
-            // otherwise T = 1 and Lp = (0, 0, 0, 1) are implied at bounce 0
-            // (shade_path `fresh`): 32 B per camera path neither written nor read
+            // Lp = (0, 0, 0, 1) is implied at bounce 0, and T = 1 without
+            // differentials (load_path): 16-32 B per camera path neither written
+            // nor read (r06: Lp with differentials too, C5 -16 B per path twice)
             // depth 1; the jitter used 2 dimensions in one 2D request
             stS(&P.meta[slot], jitter ? make_uint4(1u, 2u, slot, 1u) : make_uint4(1u, 0u, slot, 0u));
         } else {
@@ -2899,9 +2933,9 @@ DEV PathLoads load_path(const DevScene &S, const DevPaths &P, uint32_t i, bool f
     pl.ro4 = ldS(&P.ray_o[i]);
     pl.rd4 = ldS(&P.ray_d[i]);
     // a camera path starts with L = 0, alpha 1, T = 1, eta = 1: k_camera writes
-    // neither array then (T holds the ray differentials when cam_diffs)
+    // no L, and no T unless it holds the ray differentials (cam_diffs)
     const bool fresh = first && !S.cam_diffs;
-    pl.L4 = fresh ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
+    pl.L4 = first ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
     pl.T4 = fresh ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
     return pl;
 }
@@ -2910,7 +2944,7 @@ DEV PathLoads load_path_rest(const DevScene &S, const DevPaths &P, uint32_t i, b
     pl.ro4 = ldS(&P.ray_o[i]);
     pl.rd4 = ldS(&P.ray_d[i]);
     const bool fresh = first && !S.cam_diffs;
-    pl.L4 = fresh ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
+    pl.L4 = first ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
     pl.T4 = fresh ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
     return pl;
 }
@@ -2952,7 +2986,16 @@ DEV void shade_path(const DevScene &S, const DevIntegrator &I, const DevBatch &B
         if (!valid) {
             // Scene::evalEnvironment of the differential camera ray (path.cpp:136-143)
             if (ENV && !I.hide_emitters) {
-                const float3 rxd = T, ryd = xyz(ldS(&P.aux[i]));
+                float3 rxd, ryd;
+                if (S.cam_diffs) {
+                    rxd = T;
+                    ryd = xyz(ldS(&P.aux[i]));
+                } else {   // (cam_env_diffs) recomputed from the camera, bit for bit as k_camera's
+                    int x, y;
+                    uint32_t sIdx;
+                    slot_pixel(B, slot, x, y, sIdx);
+                    camera_ray_differentials<SMP>(*S.camDev, I, x, y, sIdx, rxd, ryd);
+                }
                 L += env_eval(S.env, rd, true, rxd, ryd);   // throughput 1
             }
             done = true;

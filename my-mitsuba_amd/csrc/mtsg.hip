@@ -100,6 +100,10 @@ struct mtsg_scene {
     int samplerType = MTSG_SAMPLER_INDEPENDENT, samplerDim = 4;
     int qmcInv[2][3] = {{0, 0, 0}, {0, 0, 0}};
     int traceMode = 0;            // 0: refill at 16 idle lanes (measured best), 1: at 32
+    // camera ray differentials (DevScene::cam_diffs / cam_env_diffs): stored
+    // in the path state for filtered textures (or MTSG_OPT_CAMERA_DIFFS 1),
+    // else recomputed at bounce 0 for environment misses
+    bool texDiffs = false, hasEnvmap = false, storeCamDiffs = false;
     int rayOrder = 0;             // MTSG_OPT_RAY_ORDER: 1 = bounce rays sorted per window by direction (k_sortwin;
                                   // measured r06: C3 trace +6.7 ms, profiles/r06_ray_order.txt)
     float *dumpL = nullptr;
@@ -252,6 +256,12 @@ ShadeLaunch shade_args(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B,
     a.inst = s->ds.inst != nullptr;
     a.mats = s->shadeGeneric ? (int)MATS_ALL : s->mats;
     return a;
+}
+// where bounce 0 finds the camera rays' differentials (mtsg_scene::storeCamDiffs)
+void camera_diff_mode(mtsg_scene *s) {
+    s->ds.cam_diffs = (s->texDiffs || (s->hasEnvmap && s->storeCamDiffs)) ? 1 : 0;
+    s->ds.cam_env_diffs = (s->hasEnvmap && !s->ds.cam_diffs) ? 1 : 0;
+    s->cam.diffs = s->ds.cam_diffs;
 }
 void launch_shade(mtsg_scene *s, const DevIntegrator &I, const DevBatch &B, const DevPaths &P, int b, int qin, hipStream_t st) {
     const ShadeLaunch a = shade_args(s, I, B, P, b, qin, st, dim3(s->shadeGrid), dim3(SHADE_BLOCK));
@@ -1166,7 +1176,8 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
         s->nTextures = d->n_textures;
         s->extBsdfs = true;   // texture lookups live in the extended shade kernel
     }
-    ds.cam_diffs = (d->has_envmap || texDiffs) ? 1 : 0;
+    s->texDiffs = texDiffs;
+    s->hasEnvmap = d->has_envmap != 0;
     // myPath2_OM occupancy maps (om.cpp)
     ds.om = nullptr; ds.om_bits = nullptr;
     if (d->om) {
@@ -1192,8 +1203,15 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     memcpy(c.filter_values, hc.filter_values, sizeof(c.filter_values));
     memcpy(c.dx, hc.dx, sizeof(c.dx));
     memcpy(c.dy, hc.dy, sizeof(c.dy));
-    c.diffs = ds.cam_diffs;
     c.crop_w = hc.crop_w; c.crop_h = hc.crop_h;
+    camera_diff_mode(s);
+    // the camera on the device too: bounce 0 recomputes a missing camera ray's
+    // differentials from it (DevScene::cam_env_diffs)
+    {
+        DevCamera *dc;
+        if ((rc = up(&s->cam, 1, &dc))) return fail(rc);
+        ds.camDev = dc;
+    }
     // sampler and its quasi-Monte Carlo tables
     s->samplerType = d->sampler.type;
     s->samplerDim = d->sampler.dimension;
@@ -1341,6 +1359,11 @@ int mtsg_set_option(mtsg_scene *s, int32_t key, int64_t value) {
         case MTSG_OPT_RAY_ORDER:
             if (value < 0 || value > 1) { g_err = "MTSG_OPT_RAY_ORDER: 0 (append order) or 1 (direction-sorted windows)"; return MTSG_ERR_INVALID; }
             s->rayOrder = (int)value;
+            return MTSG_OK;
+        case MTSG_OPT_CAMERA_DIFFS:
+            if (value < 0 || value > 1) { g_err = "MTSG_OPT_CAMERA_DIFFS: 0 (recomputed on a miss) or 1 (stored)"; return MTSG_ERR_INVALID; }
+            s->storeCamDiffs = value != 0;
+            camera_diff_mode(s);
             return MTSG_OK;
         default:
             g_err = "unknown option key " + std::to_string(key);

@@ -34,6 +34,7 @@ MTSG_OPT_LANES = 3
 MTSG_OPT_STAGGER = 4
 MTSG_OPT_SHADE_GENERIC = 5
 MTSG_OPT_RAY_ORDER = 6
+MTSG_OPT_CAMERA_DIFFS = 7
 
 
 class RenderParams(C.Structure):

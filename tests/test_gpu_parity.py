@@ -213,6 +213,25 @@ def test_tail_shading_threshold_does_not_change_samples(name):
     assert np.array_equal(a, c, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(a - c))}"
 
 
+@pytest.mark.parametrize("name", ["env_glass.xml", "cbox_textured.xml"])
+def test_recomputed_camera_differentials_match_stored_ones(name):
+    # an environment scene's camera ray that misses recomputes its ray
+    # differentials at bounce 0 from the camera (DevScene::cam_env_diffs)
+    # instead of reading them from the path state (MTSG_OPT_CAMERA_DIFFS 1, the
+    # layout through round 5): the same arithmetic, so every sample's radiance
+    # is bit-identical.  cbox_textured.xml (filtered textures: always stored)
+    # must not change either
+    scene = mtsg.Scene(os.path.join(SCENES, name), {"width": 80, "height": 64, "spp": 8})
+    p = scene.params()
+    g = mtsg.GPUScene(scene, 0)
+    rec = g.render_samples(p)
+    g.set_option(mtsg.MTSG_OPT_CAMERA_DIFFS, 1)
+    stored = g.render_samples(p)
+    g.close()
+    assert np.isfinite(rec).all()
+    assert np.array_equal(rec, stored, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(rec - stored))}"
+
+
 @pytest.mark.parametrize("name", ["cbox.xml", "bunny15.xml", "env_glass.xml"])
 def test_ray_order_does_not_change_samples(name):
     # the traversal takes bounce rays in direction-sorted windows
@@ -231,7 +250,7 @@ def test_ray_order_does_not_change_samples(name):
 
 def test_set_option_rejects_unknown_keys_and_values(cbox_small):
     g = mtsg.GPUScene(cbox_small, 0)
-    for key, value in ((99, 1), (mtsg.MTSG_OPT_LANES, 0), (mtsg.MTSG_OPT_TRACE_REFILL, 20)):
+    for key, value in ((99, 1), (mtsg.MTSG_OPT_LANES, 0), (mtsg.MTSG_OPT_TRACE_REFILL, 20), (mtsg.MTSG_OPT_CAMERA_DIFFS, 2)):
         with pytest.raises(RuntimeError):
             g.set_option(key, value)
     g.close()
