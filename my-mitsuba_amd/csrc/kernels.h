@@ -1975,6 +1975,18 @@ DEV void camera_ray_differentials(const DevCamera &C, const DevIntegrator &I, in
     camera_differentials(C, I, nearP, camera_to_world_dir(C, normalize(nearP)), rxs, rys);
 }
 
+// the meta word of camera path `slot` at bounce 0, as k_camera stored it
+// through round 6 (the `path` integrator: the jitter always draws): depth 1,
+// next dimension 2, the slot, one 2D request; a slot outside the render
+// rectangle is dead (0).  Bounce 0 computes it instead of reading 16 B per path.
+DEV uint4 camera_meta(const DevBatch &B, uint32_t slot) {
+    int x, y;
+    uint32_t s;
+    slot_pixel(B, slot, x, y, s);
+    const bool alive = x < B.rect_x + B.rect_w && y < B.rect_y + B.rect_h;
+    return alive ? make_uint4(1u, 2u, slot, 1u) : make_uint4(0u, 0u, slot, 0u);
+}
+
 __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, DevBatch B, DevPaths P) {
     const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     bool alive = false;
@@ -2003,13 +2015,15 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
             }
             // Lp = (0, 0, 0, 1) is implied at bounce 0, and T = 1 without
             // differentials (load_path): 16-32 B per camera path neither written
-            // nor read (r06: Lp with differentials too, C5 -16 B per path twice)
-            // depth 1; the jitter used 2 dimensions in one 2D request
-            stS(&P.meta[slot], jitter ? make_uint4(1u, 2u, slot, 1u) : make_uint4(1u, 0u, slot, 0u));
+            // nor read (r06: Lp with differentials too, C5 -16 B per path twice).
+            // The meta word too (camera_meta), except for myPath2_OM, whose
+            // shading kernel reads it: depth 1; the jitter used 2 dimensions in
+            // one 2D request
+            if (I.om) stS(&P.meta[slot], jitter ? make_uint4(1u, 2u, slot, 1u) : make_uint4(1u, 0u, slot, 0u));
         } else {
             // dead slot: bounce 0 runs over all slots and skips it
             stS(&P.ray_d[slot], make_float4(0.f, 0.f, 1.f, -1.0f));
-            stS(&P.meta[slot], make_uint4(0u, 0u, slot, 0u));
+            if (I.om) stS(&P.meta[slot], make_uint4(0u, 0u, slot, 0u));
             stS(&P.L[slot], make_float4(0.f, 0.f, 0.f, 0.f));
         }
     }
@@ -3497,8 +3511,8 @@ constexpr int SHADE_LDS_BSDFS = 4, SHADE_LDS_EMITTERS = 16;
 template <bool ENV, int MATS>
 constexpr bool shade_sorted() { return MTSG_SHADE_SORT && ENV && (MATS & (MATS - 1)) != 0; }
 constexpr int SHADE_CLASSES = 6;
-DEV uint32_t shade_class(const DevScene &S, const DevPaths &P, uint32_t i, bool first, const ShadeTables &tb) {
-    if (first && P.meta[i].x == 0u) return 0u;   // dead slot (bounce 0)
+DEV uint32_t shade_class(const DevScene &S, const DevBatch &B, const DevPaths &P, uint32_t i, bool first, const ShadeTables &tb) {
+    if (first && camera_meta(B, i).x == 0u) return 0u;   // dead slot (bounce 0)
     const uint32_t p = __float_as_uint(P.hit[i].w);
     if (p == 0xFFFFFFFFu) return 1u;
     const uint32_t bsdf = !(p & 0x80000000u) ? __float_as_uint(S.shrec[6 * (size_t)p + 5].z) & 0x7FFFFFFFu
@@ -3581,13 +3595,13 @@ __global__ void SHADE_ATTR(ENV, MATS) k_shade(DevScene S, DevIntegrator I, DevBa
         const uint32_t i0 = (it * gridDim.x + blockIdx.x) * blockDim.x;
         uint32_t i = i0 + threadIdx.x;
         if constexpr (SORT)
-            i = i0 + shade_sort(i < count ? shade_class(S, P, i, first, tb) : 0u, s_classCnt, s_perm);
+            i = i0 + shade_sort(i < count ? shade_class(S, B, P, i, first, tb) : 0u, s_classCnt, s_perm);
         bool alive = i < count;
         bool cont = false, shadow = false;
         uint4 meta = make_uint4(0u, 0u, 0u, 0u);
         PathLoads pl;
         if (alive) {
-            meta = ldS(&P.meta[i]);
+            meta = first ? camera_meta(B, i) : ldS(&P.meta[i]);
 #if MTSG_SHADE_PRELOAD == 1
             pl = load_path(S, P, i, first);
 #elif MTSG_SHADE_PRELOAD == 2
