@@ -80,6 +80,8 @@ struct DevScene {
     // k_camera writes and bounce 0 reads 32 B less per path (round 6)
     int cam_env_diffs;
     const DevCamera *__restrict__ camDev;
+    float camO[3], camNear, camFar;   // the camera's origin and clip distances (load_closest_ray)
+    int camCompact;   // k_camera stores ray_d = (direction, 1/z) only (flat scenes: load_closest_ray)
     // two-level traversal: per-lane save slots of the top-level state
     // (SAVE_VECS uint4 per lane of the traversal grid); nullptr: no instances
     uint4 *__restrict__ instSave;
@@ -109,6 +111,7 @@ struct DevCamera {
     float filter_values[32];
     float dx[3], dy[3];   // near-plane differentials (perspective.cpp:160-170)
     int diffs;            // store primary-ray differentials (environment / filtered texture lookups)
+    int compact;          // store ray_d = (direction, 1/z) only (DevScene::camCompact)
     int crop_w, crop_h;   // the sampler's space partition (setFilmResolution)
 };
 
@@ -176,6 +179,11 @@ struct DevPaths {
     // i is the ray at position order[i]; nullptr: entry i is position i
     uint32_t *order;
     uint32_t *orderBuf;   // the buffer k_sortwin fills (one entry per path)
+    // 1 while the closest rays are bounce 0's camera rays of a flat scene,
+    // which k_camera stores as ray_d = (direction, 1/z) only: their origin is
+    // the camera's and mint / maxt are near / far clip x 1/z (load_closest_ray,
+    // DevScene::camCompact; round 6)
+    uint32_t camEnc = 0;
 };
 
 // arguments of the per-sampler shading launchers (smp_kernels.hip)
@@ -1032,14 +1040,29 @@ DEV bool spec_iter(const DevScene &S, SpecRay &r, SpecStack stk, TraceCounts &cn
     return (r.bits & SB_TRAVDONE) && r.lfTmax < 0.0f;
 }
 
+// Closest ray idx of the work list: origin + mint, direction + maxt.  Bounce
+// 0's camera rays (P.camEnc) keep only ray_d = (direction, 1/z): the origin is
+// the camera's, and mint / maxt are the same products k_camera formed (near /
+// far clip x 1/z), so the ray is bit for bit the one it used to store; a dead
+// slot (1/z = -1) keeps a negative maxt
+DEV void load_closest_ray(const DevScene &S, const DevPaths &P, uint32_t idx, bool cam, float4 &ro, float4 &rd) {
+    rd = ldS(P.ray_d + idx);
+    if (cam) {
+        const float invZ = rd.w;
+        ro = make_float4(S.camO[0], S.camO[1], S.camO[2], S.camNear * invZ);
+        rd.w = S.camFar * invZ;
+    } else {
+        ro = ldS(P.ray_o + idx);
+    }
+}
+
 // A closest-hit ray whose traversal met an exact tie (SB_TIE: a hit at the
 // best distance so far) is traced again from its start with Mitsuba's mailbox
 // emulated (mailbox_step): that can only change which of the tied primitives
 // its hit record names.  Ties are rare (coplanar faces, shared edges), so the
 // traversal loop pays one compare per test for them instead of the mailbox.
-DEV void tie_retrace(const DevScene &S, SpecRay &r, SpecStack stk, const float4 *rayO, const float4 *rayD,
+DEV void tie_retrace(const DevScene &S, SpecRay &r, SpecStack stk, const float4 ro, const float4 rd,
                      float4 *hitOut, const TravLimits &L) {
-    const float4 ro = ldS(rayO), rd = ldS(rayD);
     TraceCounts tc{0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (!spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, false, r)) return;
     while (!spec_iter<false, true>(S, r, stk, tc, hitOut, L)) {}
@@ -1611,7 +1634,8 @@ DEV bool havran_level(const DevScene &S, float3 o, float3 d, float mint, float m
 // a closest ray of a two-level scene traced again exactly (ray from its work
 // list entry, as spec_init clips it): rewrites its hit record and instance
 __attribute__((noinline)) DEV void tie_retrace_i(const DevScene &S, const DevPaths &P, uint32_t idx, bool &err) {
-    const float4 ro = ldS(P.ray_o + idx), rd = ldS(P.ray_d + idx);
+    float4 ro, rd;
+    load_closest_ray(S, P, idx, P.camEnc != 0, ro, rd);
     SpecRay r;
     if (!spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, false, r)) return;
     HavranHit H;
@@ -1791,8 +1815,14 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
                 // measurement: the work list in a random order (coherence experiment)
                 if (!shadow || MTSG_SHUFFLE == 2) idx = shuffle_index(idx, shadow ? nS : nC);
 #endif
-                float4 ro = ldS((shadow ? P.sh_o : P.ray_o) + idx), rd = ldS((shadow ? P.sh_d : P.ray_d) + idx);
-                if (shadow) { const float mint = rd.w; rd.w = ro.w; ro.w = mint; }   // sh_o.w = maxt, sh_d.w = mint
+                float4 ro, rd;
+                if (shadow) {
+                    ro = ldS(P.sh_o + idx);
+                    rd = ldS(P.sh_d + idx);
+                    const float mint = rd.w; rd.w = ro.w; ro.w = mint;   // sh_o.w = maxt, sh_d.w = mint
+                } else {
+                    load_closest_ray(S, P, idx, !INST && P.camEnc != 0, ro, rd);   // (two-level scenes: never compact)
+                }
                 if (spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, shadow, r)) {
                     active = true;
                     if (COUNT) {
@@ -1847,7 +1877,8 @@ k_trace_s(DevScene S, DevPaths P, int cIn, int sIn, uint32_t nIdentity, unsigned
                 // a closest ray that met an exact tie is traced again from its
                 // start in this lane with the mailbox (tie_retrace), inside the
                 // launch: its drain absorbs the retrace, no k_tie launch follows
-                const float4 ro = ldS(P.ray_o + idx), rd = ldS(P.ray_d + idx);
+                float4 ro, rd;
+                load_closest_ray(S, P, idx, P.camEnc != 0, ro, rd);
                 spec_init(S, xyz(ro), xyz(rd), ro.w, rd.w, false, r);   // true: it passed before
                 r.bits |= SB_MBRUN;
                 done = false;
@@ -2003,8 +2034,15 @@ __global__ void __launch_bounds__(BLOCK) k_camera(DevCamera C, DevIntegrator I, 
             const float3 d = normalize(nearP);
             const float invZ = 1.0f / d.z;
             const float3 wd = camera_to_world_dir(C, d);
-            stS(&P.ray_o[slot], make_float4(C.c2w[3], C.c2w[7], C.c2w[11], C.near_clip * invZ));
-            stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
+            // flat scenes: the direction and 1/z only (load_closest_ray: C3 / C5
+            // k_camera 32 -> 16 B per path); two-level scenes keep the origin for
+            // their instance exits and tie retraces
+            if (C.compact) {
+                stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, invZ));
+            } else {
+                stS(&P.ray_o[slot], make_float4(C.c2w[3], C.c2w[7], C.c2w[11], C.near_clip * invZ));
+                stS(&P.ray_d[slot], make_float4(wd.x, wd.y, wd.z, C.far_clip * invZ));
+            }
             if (C.diffs && !I.om) {   // myPath2_OM uses sensor->sampleRay: no differentials
                 float3 rxs, rys;
                 camera_differentials(C, I, nearP, wd, rxs, rys);
@@ -2944,8 +2982,7 @@ struct PathLoads {
 DEV PathLoads load_path(const DevScene &S, const DevPaths &P, uint32_t i, bool first) {
     PathLoads pl;
     pl.h = ldS(&P.hit[i]);
-    pl.ro4 = ldS(&P.ray_o[i]);
-    pl.rd4 = ldS(&P.ray_d[i]);
+    load_closest_ray(S, P, i, first && S.camCompact, pl.ro4, pl.rd4);
     // a camera path starts with L = 0, alpha 1, T = 1, eta = 1: k_camera writes
     // no L, and no T unless it holds the ray differentials (cam_diffs)
     const bool fresh = first && !S.cam_diffs;
@@ -2955,8 +2992,7 @@ DEV PathLoads load_path(const DevScene &S, const DevPaths &P, uint32_t i, bool f
 }
 DEV PathLoads load_path_rest(const DevScene &S, const DevPaths &P, uint32_t i, bool first) {
     PathLoads pl;
-    pl.ro4 = ldS(&P.ray_o[i]);
-    pl.rd4 = ldS(&P.ray_d[i]);
+    load_closest_ray(S, P, i, first && S.camCompact, pl.ro4, pl.rd4);
     const bool fresh = first && !S.cam_diffs;
     pl.L4 = first ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);
     pl.T4 = fresh ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
@@ -3269,7 +3305,9 @@ DEV void shade_path_om(const DevScene &S, const DevIntegrator &I, const DevBatch
     constexpr int SMP = MTSG_SAMPLER_INDEPENDENT;
     const uint32_t slot = meta.z;
     const float4 h = ldS(&P.hit[i]);
-    const float3 ro = xyz(ldS(&P.ray_o[i])), rd = xyz(ldS(&P.ray_d[i]));
+    float4 ro4, rd4;
+    load_closest_ray(S, P, i, first && S.camCompact, ro4, rd4);
+    const float3 ro = xyz(ro4), rd = xyz(rd4);
     const float4 L4 = first ? make_float4(0.f, 0.f, 0.f, 1.f) : ldS(&P.Lp[i]);   // camera paths: see shade_path
     const float4 T4 = first ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&P.T[i]);
     PathSampler smp;
@@ -3779,7 +3817,7 @@ __global__ void FINISH_ATTR(MATS) k_finish(DevScene S, DevIntegrator I, DevBatch
         if (done) {
             if (MTSG_MAILBOX && (r.bits & (SB_TIE | SB_SHADOW)) == SB_TIE) {
                 if (!INST) {
-                    tie_retrace(S, r, stk, P.ray_o + idx, P.ray_d + idx, P.hit + idx, trav_limits<false>(S));
+                    tie_retrace(S, r, stk, ldS(P.ray_o + idx), ldS(P.ray_d + idx), P.hit + idx, trav_limits<false>(S));
                 } else {
                     bool herr = false;
                     tie_retrace_i(S, P, idx, herr);
@@ -3951,7 +3989,9 @@ __global__ void __launch_bounds__(TRACE_BLOCK) k_tie(DevScene S, DevPaths P) {
     SpecRay r;
     for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
         const uint32_t idx = P.tie[i];
-        tie_retrace(S, r, stk, P.ray_o + idx, P.ray_d + idx, P.hit + idx, L);
+        float4 ro, rd;
+        load_closest_ray(S, P, idx, P.camEnc != 0, ro, rd);
+        tie_retrace(S, r, stk, ro, rd, P.hit + idx, L);
         if (r.bits & SB_ERR) atomicOr(&P.cnt[CNT_ERR], CNT_ERR_TRAVERSAL);
     }
 }

@@ -550,6 +550,7 @@ int render_impl(mtsg_scene *s, const mtsg_render_params *p, float *film, int win
                 // bounce rays in direction-sorted windows (k_sortwin); the
                 // camera rays keep their tile order
                 DevPaths PT = P;
+                PT.camEnc = (b == 0 && s->ds.camCompact) ? 1u : 0u;   // bounce 0: camera rays as k_camera stores them
                 if (b >= 1 && s->rayOrder == 1) {
                     timed_launch(s, K_SORT, st, [&]() {
                         hipLaunchKernelGGL(k_sortwin, dim3(s->cuCount * 2), dim3(SORT_BLOCK), 0, st, P, qin);
@@ -1204,6 +1205,10 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     memcpy(c.dx, hc.dx, sizeof(c.dx));
     memcpy(c.dy, hc.dy, sizeof(c.dy));
     c.crop_w = hc.crop_w; c.crop_h = hc.crop_h;
+    ds.camO[0] = c.c2w[3]; ds.camO[1] = c.c2w[7]; ds.camO[2] = c.c2w[11];
+    ds.camNear = c.near_clip; ds.camFar = c.far_clip;
+    ds.camCompact = ds.inst ? 0 : 1;
+    c.compact = ds.camCompact;
     camera_diff_mode(s);
     // the camera on the device too: bounce 0 recomputes a missing camera ray's
     // differentials from it (DevScene::cam_env_diffs)
