@@ -232,6 +232,22 @@ def test_recomputed_camera_differentials_match_stored_ones(name):
     assert np.array_equal(rec, stored, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(rec - stored))}"
 
 
+@pytest.mark.parametrize("name", ["cbox.xml", "bunny15.xml"])
+def test_refill_width_does_not_change_samples(name):
+    # a traversal wave refills its idle lanes from the work list at 16 idle
+    # lanes (default) or 32 (MTSG_OPT_TRACE_REFILL): when a ray is started
+    # does not change its hit, so every sample is bit-identical
+    scene = mtsg.Scene(os.path.join(SCENES, name), {"width": 80, "height": 64, "spp": 8})
+    p = scene.params()
+    g = mtsg.GPUScene(scene, 0)
+    g.set_finish_paths(0)   # every bounce through the per-bounce traversal launches
+    a = g.render_samples(p)
+    g.set_option(mtsg.MTSG_OPT_TRACE_REFILL, 32)
+    b = g.render_samples(p)
+    g.close()
+    assert np.array_equal(a, b, equal_nan=True), f"{name}: max |diff| {np.nanmax(np.abs(a - b))}"
+
+
 @pytest.mark.parametrize("name", ["cbox.xml", "bunny15.xml", "env_glass.xml"])
 def test_ray_order_does_not_change_samples(name):
     # the traversal takes bounce rays in direction-sorted windows
