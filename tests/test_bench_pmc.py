@@ -83,3 +83,16 @@ def test_pmc_sets_are_per_frame():
         assert abs(b["kernels"]["pmc"]["k_shade"]["rocprof_ms_per_frame"] - pmc_ms) < 2e-3
         checked += 1
     assert checked >= 1 or not glob.glob(os.path.join(repo, "profiles", "r06_pmc_*.json"))
+
+
+def test_scheduling_and_tree_options_key_their_own_sets():
+    # options that change the launches (the tree, the tail kernel's shading
+    # group, lanes) key their own sets; their defaults keep the plain key, so
+    # the committed sets stay quotable by a default run
+    base = bench.pmc_key(args())
+    assert bench.pmc_key(args(kd_props="", finish_shade_min=0, lanes=0, stagger=-1)) == base
+    others = [bench.pmc_key(args(kd_props="kdStopPrims=5")), bench.pmc_key(args(finish_shade_min=1)),
+              bench.pmc_key(args(lanes=2)), bench.pmc_key(args(stagger=2))]
+    for k in others:
+        assert k != base
+        assert {n: v for n, v in k.items() if n in base} == base   # only the option's own entry differs
