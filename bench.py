@@ -70,7 +70,7 @@ def pmc_key(a, world=1):
     if getattr(a, "finish_shade_min", 0) > 0:
         key["finish_shade_min"] = a.finish_shade_min
     if getattr(a, "lanes", 0) > 0 or getattr(a, "stagger", -1) >= 0:
-        key["lanes"] = [a.lanes, a.stagger]   # other launch sequence
+        key["lanes"] = [getattr(a, "lanes", 0), getattr(a, "stagger", -1)]   # other launch sequence
     return key
 
 
