@@ -45,11 +45,18 @@ $(HOST_LIB): $(HOST_SRC) $(HOST_HDR) $(SOBOL_BIN)
 # register moves and VGPRs (63 -> 60 flat, 80 -> 76 two-level): C3 +1.8%,
 # two-level +1.2% (r03 variant noslp), results unchanged (same IEEE ops).
 DEV_FLAGS := -O3 -std=c++17 -fPIC -Wall -ffp-contract=off -fno-slp-vectorize -munsafe-fp-atomics -Wno-unused-value -Wno-unused-result
+# the flat traversal's own unit (trace_flat.hip): the memory-clause scheduler
+# groups each iteration's node-pair and TriAccel loads (C3 trace -1.0%, C5
+# -0.6%; the two-level kernel in mtsg.hip loses 3% under it: DESIGN §3)
+DEV_FLAT_FLAGS ?= -mllvm -amdgpu-sched-strategy=max-memory-clause
 DEV_OBJ   ?= build/dev
-DEV_OBJS  := $(DEV_OBJ)/mtsg.o $(DEV_OBJ)/kdbuild.o $(foreach k,0 1 2 3 4,$(DEV_OBJ)/smp_$(k).o)
+DEV_OBJS  := $(DEV_OBJ)/mtsg.o $(DEV_OBJ)/trace_flat.o $(DEV_OBJ)/kdbuild.o $(foreach k,0 1 2 3 4,$(DEV_OBJ)/smp_$(k).o)
 $(DEV_OBJ)/mtsg.o: $(PKG)/csrc/mtsg.hip $(DEV_HDR)
 	@mkdir -p $(DEV_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) $(DEV_EXTRA) -c -o $@ $<
+$(DEV_OBJ)/trace_flat.o: $(PKG)/csrc/trace_flat.hip $(DEV_HDR)
+	@mkdir -p $(DEV_OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) $(DEV_FLAT_FLAGS) $(DEV_EXTRA) -c -o $@ $<
 $(DEV_OBJ)/kdbuild.o: $(PKG)/csrc/kdbuild.hip include/mtsg.h
 	@mkdir -p $(DEV_OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) $(DEV_FLAGS) $(DEV_EXTRA) -c -o $@ $<

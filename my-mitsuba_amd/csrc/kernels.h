@@ -212,6 +212,20 @@ MTSG_DECLARE_LAUNCHERS(MTSG_SAMPLER_HAMMERSLEY)
 MTSG_DECLARE_LAUNCHERS(MTSG_SAMPLER_LDSAMPLER)
 MTSG_DECLARE_LAUNCHERS(MTSG_SAMPLER_SOBOL)
 int finish_blocks_per_cu(bool mats);   // k_finish workgroups per CU (occupancy query)
+// the flat traversal and its tie retrace (trace_flat.hip, its own translation
+// unit and scheduler flags): one launch over a work list, then k_tie if `tie`
+struct FlatTraceLaunch {
+    dim3 grid, tieGrid;
+    hipStream_t stream;
+    const DevScene *S;
+    const DevPaths *P;
+    int cIn, sIn;
+    uint32_t n;
+    unsigned long long *wt;
+    bool count, knobs, refill32, tie;
+};
+void launch_trace_flat(const FlatTraceLaunch &a);
+int trace_flat_blocks_per_cu();   // k_trace_s<false, 16> workgroups per CU (occupancy query)
 
 }  // namespace mtsg
 

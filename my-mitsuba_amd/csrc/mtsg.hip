@@ -214,21 +214,20 @@ void launch_trace_c(mtsg_scene *s, const DevPaths &P, int cIn, int sIn, uint32_t
         wt = s->waveTimes + (size_t)WT_WORDS * s->traceGrid * s->wtLaunches++;
     // the KNOBS instantiations read the stack caps and restart limits the
     // scene was created with (test overrides); the COUNT pass ignores them
-    if (s->ds.inst && s->knobs && !COUNT)
-        hipLaunchKernelGGL((k_trace_s<false, MTSG_INST_MIN_IDLE, true, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
-    else if (s->ds.inst) hipLaunchKernelGGL((k_trace_s<COUNT, MTSG_INST_MIN_IDLE, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
-    else if (s->knobs && !COUNT) hipLaunchKernelGGL((k_trace_s<false, 16, false, true>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
-    else if (s->traceMode == 1) hipLaunchKernelGGL((k_trace_s<COUNT, 32>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
-    else hipLaunchKernelGGL((k_trace_s<COUNT, 16>), g, blk, 0, st, s->ds, P, cIn, sIn, n, wt);
     // closest rays that met an exact tie: traced again with the mailbox
     // (a grid a quarter of the trace grid's; two-level: the exact Havran).
     // The flat traversal retraces them inside its own launch (TIE_INLINE).
-    if (MTSG_MAILBOX && cIn != -2 && (s->ds.inst || !TIE_INLINE)) {
-        const dim3 tg(std::max<unsigned>(1u, (unsigned)s->traceGrid / 4u));
-        if (s->ds.inst) hipLaunchKernelGGL(k_tie_i, tg, blk, 0, st, s->ds, P);
-        else if (s->knobs) hipLaunchKernelGGL((k_tie<true>), tg, blk, 0, st, s->ds, P);
-        else hipLaunchKernelGGL((k_tie<false>), tg, blk, 0, st, s->ds, P);
+    const dim3 tg(std::max<unsigned>(1u, (unsigned)s->traceGrid / 4u));
+    if (!s->ds.inst) {   // the flat kernels: trace_flat.hip
+        FlatTraceLaunch a{g, tg, st, &s->ds, &P, cIn, sIn, n, wt, COUNT, s->knobs, s->traceMode == 1,
+                          MTSG_MAILBOX && cIn != -2 && !TIE_INLINE};
+        launch_trace_flat(a);
+        return;
     }
+    if (s->knobs && !COUNT)
+        hipLaunchKernelGGL((k_trace_s<false, MTSG_INST_MIN_IDLE, true, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    else hipLaunchKernelGGL((k_trace_s<COUNT, MTSG_INST_MIN_IDLE, true>), dim3(s->traceGridInst), blk, 0, st, s->ds, P, cIn, sIn, n, wt);
+    if (MTSG_MAILBOX && cIn != -2) hipLaunchKernelGGL(k_tie_i, tg, blk, 0, st, s->ds, P);
 }
 void launch_trace(mtsg_scene *s, bool count, const DevPaths &P, int cIn, int sIn, uint32_t n, hipStream_t st) {
     if (count) launch_trace_c<true>(s, P, cIn, sIn, n, st);
@@ -1260,9 +1259,7 @@ int mtsg_scene_create(const mtsg_scene_desc *d, int device, mtsg_scene **out) {
     }
     // persistent grids from the occupancy query
     int perCU = 0;
-    const void *occKernel = (const void *)k_trace_s<false, 16>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, occKernel, TRACE_BLOCK, 0) != hipSuccess || perCU <= 0)
-        perCU = 8;
+    if ((perCU = trace_flat_blocks_per_cu()) <= 0) perCU = 8;
     s->traceGrid = s->cuCount * perCU;
     perCU = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, (const void *)k_trace_s<false, MTSG_INST_MIN_IDLE, true>, TRACE_BLOCK, 0) != hipSuccess ||
