@@ -3862,6 +3862,9 @@ constexpr int LT = TILE + 2 * MAX_BORDER;   // LDS tile edge
 #define MTSG_SPLAT_CHUNK 64   // r04: 16 -> 64 samples per workgroup, a quarter of the film atomics: C3 splat 2.86 -> 2.34 ms
 #endif
 constexpr int SPLAT_CHUNK = MTSG_SPLAT_CHUNK;   // samples per pixel per workgroup
+#ifndef MTSG_SPLAT_LDS_FILTER
+#define MTSG_SPLAT_LDS_FILTER 1   // 0: the filter table read from the kernel arguments (round-5 splat)
+#endif
 
 // One workgroup = one 16x16 tile x one chunk of SPLAT_CHUNK samples per pixel.
 // Each thread owns one pixel: all its samples fall in [x, x+1) x [y, y+1), so
@@ -3881,6 +3884,15 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
     __shared__ float acc[CH][LT * LT];
     constexpr int R = K / 2;
     for (int k = threadIdx.x; k < CH * LT * LT; k += BLOCK) (&acc[0][0])[k] = 0.0f;
+#if MTSG_SPLAT_LDS_FILTER
+    // the discretized filter's 32 values in LDS: the 2K per-sample lookups
+    // are lane-indexed, so from the kernel arguments each was a vector load
+    __shared__ float flt[32];
+    if (threadIdx.x < 32) flt[threadIdx.x] = C.filter_values[threadIdx.x];
+    __syncthreads();
+#else
+    const float *flt = C.filter_values;
+#endif
     const int tl = blockIdx.x;
     int tx, ty;
     tile_of_key(batch_key(B, B.tile0 + tl), B.tiles_x, tx, ty, B.skew);
@@ -3925,8 +3937,8 @@ __global__ void __launch_bounds__(BLOCK) k_splat(DevCamera C, DevIntegrator I, D
             for (int c = 0; c < K; ++c) {
                 const bool okx = c >= bx0 && c < bx0 + blockW;
                 const bool oky = c >= by0 && c < by0 + blockH;
-                wx[c] = okx ? C.filter_values[min((int)fabsf(((float)(wxo + c) - px) * C.filter_scale), 31)] : 0.0f;
-                wy[c] = oky ? C.filter_values[min((int)fabsf(((float)(wyo + c) - py) * C.filter_scale), 31)] : 0.0f;
+                wx[c] = okx ? flt[min((int)fabsf(((float)(wxo + c) - px) * C.filter_scale), 31)] : 0.0f;
+                wy[c] = oky ? flt[min((int)fabsf(((float)(wyo + c) - py) * C.filter_scale), 31)] : 0.0f;
             }
             const float v[5] = {L.x, L.y, L.z, L.w, 1.0f};
             {
