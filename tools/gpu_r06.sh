@@ -80,9 +80,10 @@ for w in ${*:-tests bench}; do
     pmcro-sorted) bash tools/gpu_pmc_config.sh r06ro sorted --ray-order 1 || exit $? ;;
     pmcro-shuf1) MTSG_LIB=$(lib shuf1) bash tools/gpu_pmc_config.sh r06ro shuf1 || exit $? ;;
     # SQ counters per kernel (tools/sq_by_kernel.py): sq-c3 / sq-c5, one frame per pass (C5 at 256 spp)
-    sq-c3|sq-c5)
+    sq-c3|sq-c5|sq-inst)
       t=${w#sq-}; A="--pmc-pass $Q --no-count --steps 1 --warmup 0"
       [ $t = c5 ] && A="$A --workload c5 --width 1920 --height 1080 --spp 256"
+      [ $t = inst ] && A="$A --instancing two-level"
       D=$O/sq_$t; mkdir -p $D
       step sq-$t-p1 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $D -o p1 -- python3 bench.py $A
       step sq-$t-p2 200 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --kernel-trace --output-format csv -d $D -o p2 -- python3 bench.py $A
