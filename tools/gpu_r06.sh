@@ -92,6 +92,7 @@ for w in ${*:-tests bench}; do
     pmc-inst) bash tools/gpu_pmc_config.sh r06 c3_two_level --instancing two-level || exit $? ;;
     pmc-c5) bash tools/gpu_pmc_config.sh r06 c5 --workload c5 --width 1920 --height 1080 --spp 1024 || exit $? ;;
     pmc-e8) bash tools/gpu_pmc_config.sh r06 c4_share8 --emulate-ranks 8 || exit $? ;;
+    pmc-c2) bash tools/gpu_pmc_config.sh r06 c2 --workload cbox || exit $? ;;
     *) echo "unknown step $w"; exit 2 ;;
   esac
 done

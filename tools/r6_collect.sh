@@ -5,7 +5,7 @@ set -u
 P=profiles
 copy() { if [ -f "$1" ]; then cp "$1" "$2"; echo "$2"; else echo "missing: $1" >&2; fi; }
 last_json() { if [ -f "$1" ]; then grep '^{' "$1" | tail -1 > "$2"; echo "$2"; else echo "missing: $1" >&2; fi; }
-for t in c3 c3_two_level c5 c4_share8; do
+for t in c3 c3_two_level c5 c4_share8 c2; do
   copy gpurun_out/pmc_r06_$t/pmc.json $P/r06_pmc_$t.json
   copy gpurun_out/pmc_r06_$t/stats_kernel_stats.csv $P/r06_${t}_kernel_stats.csv
 done
